@@ -1,0 +1,167 @@
+/*
+ * mtb_gpu.h — C-ABI drop-in boundary for the MI355X-native Metabuli `classify` hot path.
+ *
+ * The reference has no FFI layer: its seam is four C++ member calls made by one host thread in
+ * Classifier::startClassify (/root/reference/src/commons/Classifier.cpp:105-118):
+ *
+ *   KmerExtractor::extractQueryKmers  (KmerExtractor.h:77-83, KmerExtractor.cpp:52-81)
+ *   KmerMatcher::matchKmers           (KmerMatcher.h:228-230, KmerMatcher.cpp:123-481)
+ *   KmerMatcher::sortMatches          (KmerMatcher.h:244,     KmerMatcher.cpp:1071-1078)
+ *   Classifier::assignTaxonomy        (Classifier.h:77-80,    Classifier.cpp:166-208)
+ *
+ * plus the state those calls read, built in the Classifier/KmerMatcher constructors
+ * (Classifier.cpp:6-32, KmerMatcher.cpp:19-37,56-120, common.cpp:50-133).
+ *
+ * Every entry point here is plain C: pointers, sizes and POD structs, no C++ or torch types.
+ * Status codes: 0 = ok, 1 = capacity retry (caller enlarges its buffer and calls again),
+ * negative = fatal (the reference calls exit(1) in the same situations).
+ * One mtb_ctx per device; a context is not thread-safe.
+ */
+#ifndef MTB_GPU_H
+#define MTB_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTB_OK 0
+#define MTB_RETRY 1
+#define MTB_ERR_ARG (-1)
+#define MTB_ERR_IO (-2)
+#define MTB_ERR_HIP (-3)
+#define MTB_ERR_DB (-4)        /* DB inconsistent with taxonomy: KmerMatcher.cpp:292-300 exits */
+#define MTB_ERR_OOM (-5)
+#define MTB_ERR_UNSUPPORTED (-6)
+
+/* Flags for mtb_classify_batch. */
+#define MTB_INPUT_DEVICE 1u    /* seq/off pointers are device (HBM) pointers */
+#define MTB_KEEP_STAGES 2u     /* keep sorted query k-mers and sorted matches for mtb_get_* */
+
+/*
+ * Parameters of the path. Mirrors the LocalParameters fields the path reads
+ * (LocalParameters.h:165-190,222) with the classify workflow defaults (classify.cpp:10-37);
+ * DB-driven overrides are applied by mtb_load_db_parameters (common.cpp:88-133).
+ */
+typedef struct mtb_params {
+    int32_t seq_mode;         /* 1 single-end, 2 paired-end, 3 long reads       (--seq-mode)   */
+    int32_t kmer_format;      /* 1 = base-21 AA, right-to-left; 2 = 5-bit AA    (Kmer_format)  */
+    int32_t syncmer;          /* closed syncmer selection on/off                (Syncmer)      */
+    int32_t smer_len;         /* s-mer length (default 5; DB key "S-mer_len")                  */
+    int32_t reduced_aa;       /* must be 0: ReducedKmerMatcher is out of scope                 */
+    int32_t skip_redundancy;  /* DB "Skip_redundancy": 0 => info & 0x7FFFFFFF                  */
+    float min_score;          /* --min-score                                                   */
+    float min_sp_score;       /* --min-sp-score                                                */
+    int32_t min_cons_cnt;     /* --min-cons-cnt (4)                                            */
+    int32_t min_cons_cnt_euk; /* --min-cons-cnt-euk (9)                                        */
+    float tie_ratio;          /* --tie-ratio (0.95)                                            */
+    int32_t accession_level;  /* 0, 1, or 2 (2 = DB has accessions but not requested)          */
+    int32_t em;               /* must be 0: EM reassignment is out of scope                    */
+    int32_t threads;          /* host threads (oracle / host parsing only)                     */
+    int32_t mask_mode;        /* must be 0: tantan masking is out of scope                     */
+    int32_t reserved[3];
+} mtb_params;
+
+/* Query k-mer: 16 B, same layout as Kmer{uint64 value; QueryKmerInfo} (Kmer.h:11-31,45-46).
+ * info bits: [0,32) pos, [32,61) seqID (1-based within the batch), [61,64) frame (0-2 fwd, 3-5 rev). */
+typedef struct mtb_kmer {
+    uint64_t value;
+    uint64_t info;
+} mtb_kmer;
+
+/* Match: 24 B packed form of Match (Match.h:9-25; the reference's has a vptr and is 32 B). */
+typedef struct mtb_match {
+    uint64_t qinfo;             /* QueryKmerInfo bits, as mtb_kmer.info   */
+    uint32_t target_id;         /* info[] & mask (taxID, internal)        */
+    uint32_t species_id;        /* taxId2speciesId[target_id]             */
+    uint32_t dna_encoding;      /* target value & 0xFFFFFF                */
+    uint16_t right_end_hamming; /* 2 bits per codon                       */
+    uint8_t hamming;            /* Hamming-distance sum                   */
+    uint8_t pad;
+} mtb_match;
+
+/* Per-read classification result (the Query fields written by Taxonomer::chooseBestTaxon,
+ * Taxonomer.cpp:130-202, and printed by Reporter::writeReadClassification, Reporter.cpp:38-83). */
+typedef struct mtb_result {
+    int32_t classification;   /* internal taxID; 0 = unclassified                            */
+    float score;
+    int32_t hamming_dist;
+    uint32_t query_length;    /* queryLength + queryLength2 (getMaxCoveredLength of each mate) */
+    uint32_t taxcnt_offset;   /* into the pooled mtb_taxcnt array of the batch               */
+    uint32_t taxcnt_len;      /* entries, ascending taxID (std::map order)                   */
+    uint8_t is_classified;
+    uint8_t pad[7];
+} mtb_result;                 /* 32 B */
+
+typedef struct mtb_taxcnt {
+    int32_t tax_id;
+    uint32_t count;
+} mtb_taxcnt;
+
+typedef struct mtb_ctx mtb_ctx;
+
+/* DB arrays held in host memory (the on-disk files of Appendix B, already read). */
+typedef struct mtb_db_host {
+    const uint16_t* diff_idx;   uint64_t n_diff_idx;   /* diffIdx  */
+    const uint32_t* info;       uint64_t n_info;       /* info     */
+    const uint64_t* split;      uint64_t n_split;      /* split: n_split DiffIdxSplit {ADkmer, diffIdxOffset, infoIdxOffset} */
+    const int32_t* taxid_list;  uint64_t n_taxid_list; /* taxID_list */
+    /* Taxonomy as nodes.dmp rows in file order (node index = row). rank/name are NUL-separated
+     * string pools indexed by the offsets. merged.dmp pairs optional. */
+    const int32_t* node_taxid;  const int32_t* node_parent; uint64_t n_nodes;
+    const char* rank_pool;      const uint64_t* rank_off;
+    const char* name_pool;      const uint64_t* name_off;   /* scientific names; may be NULL */
+    const int32_t* merged_old;  const int32_t* merged_new;  uint64_t n_merged;
+} mtb_db_host;
+
+/* ---- parameters ---------------------------------------------------------------------------- */
+void mtb_default_params(mtb_params* par);                              /* classify.cpp:10-37   */
+int mtb_load_db_parameters(const char* db_dir, mtb_params* par);       /* common.cpp:88-133    */
+
+/* ---- context / DB residency ------------------------------------------------------------------ */
+/* Replaces Classifier::Classifier + KmerMatcher::KmerMatcher/loadTaxIdList + loadTaxonomy
+ * (Classifier.cpp:6-32, KmerMatcher.cpp:19-37,56-120, common.cpp:50-86): reads diffIdx, info,
+ * split, taxID_list and taxonomy/{nodes,names,merged}.dmp and makes them resident in HBM. */
+int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** out);
+int mtb_open_host(const mtb_db_host* db, const mtb_params* par, int device, mtb_ctx** out);
+void mtb_close(mtb_ctx* ctx);
+const char* mtb_last_error(void);
+int mtb_set_stream(mtb_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
+uint64_t mtb_db_kmers(const mtb_ctx* ctx);             /* number of reference k-mers          */
+
+/* ---- the hot path ------------------------------------------------------------------------- */
+/* One QuerySplit worth of reads (Classifier.cpp:81-133): extract (K1) + sort (K2) + match
+ * (K3/K4) + match sort (K5) + assign (K6). seq/off: concatenated bases of mate 1 and n_reads+1
+ * byte offsets; seq2/off2 the same for mate 2 (NULL unless seq_mode == 2). With
+ * MTB_INPUT_DEVICE the four pointers are device pointers. results: host array of n_reads, or
+ * NULL to leave them on the device (mtb_device_results). */
+int mtb_classify_batch(mtb_ctx* ctx, const char* seq, const uint64_t* off, const char* seq2,
+                       const uint64_t* off2, uint32_t n_reads, uint32_t flags, mtb_result* results);
+/* Pooled taxID:count lists of the last batch (ascending taxID per read). */
+int mtb_get_taxcnt(mtb_ctx* ctx, mtb_taxcnt* out, uint64_t capacity, uint64_t* n_out);
+/* Device pointers of the last batch's results (mtb_result[n_reads]) and pooled taxcnt. */
+int mtb_device_results(mtb_ctx* ctx, void** results, void** taxcnt, uint64_t* n_taxcnt);
+/* Counters the reference prints (Classifier.cpp:116, KmerMatcher.cpp:152). */
+int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches);
+/* Per-stage device time of the last batch in ms (HIP events on the launch stream):
+ * [0] extract, [1] k-mer sort, [2] match, [3] match sort + assign, [4] total. */
+int mtb_last_stage_ms(const mtb_ctx* ctx, float* ms, int n);
+
+/* ---- staged entry points (per-stage parity against the oracle) ----------------------------- */
+/* Sorted query k-mers of the last batch (blank slots dropped), compareQueryKmer order
+ * restricted to the AA part; requires MTB_KEEP_STAGES. */
+int mtb_get_query_kmers(mtb_ctx* ctx, mtb_kmer* out, uint64_t capacity, uint64_t* n_out);
+/* Matches of the last batch in compareMatches order (KmerMatcher.cpp:1149-1166); requires
+ * MTB_KEEP_STAGES. */
+int mtb_get_matches(mtb_ctx* ctx, mtb_match* out, uint64_t capacity, uint64_t* n_out);
+/* K5+K6 only, on caller-provided matches (any order): query_len[i] = queryLength+queryLength2
+ * of read i (seqID i+1). */
+int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches,
+                       const uint32_t* query_len, uint32_t n_reads, mtb_result* results);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTB_GPU_H */

@@ -1,0 +1,81 @@
+"""ctypes / numpy mirrors of the plain-data structs in include/mtb_gpu.h."""
+import ctypes
+
+import numpy as np
+
+
+class MtbParams(ctypes.Structure):
+    _fields_ = [
+        ("seq_mode", ctypes.c_int32),
+        ("kmer_format", ctypes.c_int32),
+        ("syncmer", ctypes.c_int32),
+        ("smer_len", ctypes.c_int32),
+        ("reduced_aa", ctypes.c_int32),
+        ("skip_redundancy", ctypes.c_int32),
+        ("min_score", ctypes.c_float),
+        ("min_sp_score", ctypes.c_float),
+        ("min_cons_cnt", ctypes.c_int32),
+        ("min_cons_cnt_euk", ctypes.c_int32),
+        ("tie_ratio", ctypes.c_float),
+        ("accession_level", ctypes.c_int32),
+        ("em", ctypes.c_int32),
+        ("threads", ctypes.c_int32),
+        ("mask_mode", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
+    ]
+
+
+class MtbDbHost(ctypes.Structure):
+    _fields_ = [
+        ("diff_idx", ctypes.c_void_p), ("n_diff_idx", ctypes.c_uint64),
+        ("info", ctypes.c_void_p), ("n_info", ctypes.c_uint64),
+        ("split", ctypes.c_void_p), ("n_split", ctypes.c_uint64),
+        ("taxid_list", ctypes.c_void_p), ("n_taxid_list", ctypes.c_uint64),
+        ("node_taxid", ctypes.c_void_p), ("node_parent", ctypes.c_void_p), ("n_nodes", ctypes.c_uint64),
+        ("rank_pool", ctypes.c_void_p), ("rank_off", ctypes.c_void_p),
+        ("name_pool", ctypes.c_void_p), ("name_off", ctypes.c_void_p),
+        ("merged_old", ctypes.c_void_p), ("merged_new", ctypes.c_void_p), ("n_merged", ctypes.c_uint64),
+    ]
+
+
+KMER_DTYPE = np.dtype([("value", "<u8"), ("info", "<u8")])
+MATCH_DTYPE = np.dtype([("qinfo", "<u8"), ("target_id", "<u4"), ("species_id", "<u4"), ("dna_encoding", "<u4"),
+                        ("right_end_hamming", "<u2"), ("hamming", "u1"), ("pad", "u1")])
+RESULT_DTYPE = np.dtype([("classification", "<i4"), ("score", "<f4"), ("hamming_dist", "<i4"),
+                         ("query_length", "<u4"), ("taxcnt_offset", "<u4"), ("taxcnt_len", "<u4"),
+                         ("is_classified", "u1"), ("pad", "u1", (7,))])
+TAXCNT_DTYPE = np.dtype([("tax_id", "<i4"), ("count", "<u4")])
+
+assert KMER_DTYPE.itemsize == 16 and MATCH_DTYPE.itemsize == 24
+assert RESULT_DTYPE.itemsize == 32 and TAXCNT_DTYPE.itemsize == 8
+
+MTB_OK, MTB_RETRY = 0, 1
+MTB_INPUT_DEVICE, MTB_KEEP_STAGES = 1, 2
+
+
+def default_params(**kw) -> MtbParams:
+    """setClassifyDefaults (classify.cpp:10-37)."""
+    p = MtbParams(seq_mode=2, kmer_format=1, syncmer=0, smer_len=5, reduced_aa=0, skip_redundancy=0,
+                  min_score=0.0, min_sp_score=0.0, min_cons_cnt=4, min_cons_cnt_euk=9, tie_ratio=0.95,
+                  accession_level=0, em=0, threads=1, mask_mode=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def ptr(a) -> ctypes.c_void_p:
+    if a is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def info_seq(info):
+    return (np.asarray(info, np.uint64) >> np.uint64(32)) & np.uint64(0x1FFFFFFF)
+
+
+def info_frame(info):
+    return np.asarray(info, np.uint64) >> np.uint64(61)
+
+
+def info_pos(info):
+    return np.asarray(info, np.uint64) & np.uint64(0xFFFFFFFF)

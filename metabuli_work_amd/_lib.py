@@ -1,0 +1,65 @@
+"""Loader for libmtbgpu.so — the C-ABI of include/mtb_gpu.h.
+
+The product path has no CPU fallback: if the HIP library is missing or fails to load, every
+entry point raises. Build it with `python -c "import __graft_entry__ as g; g.build()"` or
+`make -C metabuli_work_amd/csrc`.
+"""
+import ctypes
+import pathlib
+
+from ._abi import MtbDbHost, MtbParams
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libmtbgpu.so"
+_LIB = None
+
+# Every symbol include/mtb_gpu.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "mtb_default_params", "mtb_load_db_parameters", "mtb_open", "mtb_open_host", "mtb_close", "mtb_last_error",
+    "mtb_set_stream", "mtb_db_kmers", "mtb_classify_batch", "mtb_get_taxcnt", "mtb_device_results",
+    "mtb_last_counts", "mtb_last_stage_ms", "mtb_get_query_kmers", "mtb_get_matches", "mtb_assign_matches",
+]
+
+
+class MtbError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise MtbError(f"{LIB_PATH} not built: the HIP extension is required (no CPU fallback)")
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    P = ctypes.POINTER
+    L.mtb_default_params.argtypes = [P(MtbParams)]
+    L.mtb_default_params.restype = None
+    L.mtb_load_db_parameters.argtypes = [ctypes.c_char_p, P(MtbParams)]
+    L.mtb_open.argtypes = [ctypes.c_char_p, P(MtbParams), i32, P(vp)]
+    L.mtb_open_host.argtypes = [P(MtbDbHost), P(MtbParams), i32, P(vp)]
+    L.mtb_close.argtypes = [vp]
+    L.mtb_close.restype = None
+    L.mtb_last_error.restype = ctypes.c_char_p
+    L.mtb_set_stream.argtypes = [vp, vp]
+    L.mtb_db_kmers.argtypes = [vp]
+    L.mtb_db_kmers.restype = u64
+    L.mtb_classify_batch.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp]
+    L.mtb_get_taxcnt.argtypes = [vp, vp, u64, P(u64)]
+    L.mtb_device_results.argtypes = [vp, P(vp), P(vp), P(u64)]
+    L.mtb_last_counts.argtypes = [vp, P(u64), P(u64)]
+    L.mtb_last_stage_ms.argtypes = [vp, P(ctypes.c_float), i32]
+    L.mtb_get_query_kmers.argtypes = [vp, vp, u64, P(u64)]
+    L.mtb_get_matches.argtypes = [vp, vp, u64, P(u64)]
+    L.mtb_assign_matches.argtypes = [vp, vp, u64, vp, u32, vp]
+    L.mtb_debug_tables.argtypes = [vp, vp, vp]
+    L.mtb_debug_tables.restype = None
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise MtbError(f"{what} failed ({rc}): {lib().mtb_last_error().decode()}")
+    return rc

@@ -1,0 +1,260 @@
+"""Host-side mirror of the reference's Classifier for the `classify` path.
+
+Mirrors the reference interface (names, argument meaning, error behaviour):
+
+* ``LocalParameters`` — the fields of LocalParameters.h:165-190 the path reads, with
+  setClassifyDefaults (classify.cpp:10-37) and loadDbParameters (common.cpp:88-133);
+* ``Classifier(par)`` — Classifier::Classifier (Classifier.cpp:6-32): loads the DB and makes it
+  resident on the GPU through the C-ABI (mtb_open);
+* ``Classifier.classify_batch`` — one QuerySplit of Classifier::startClassify (Classifier.cpp:
+  81-133): extract, match, sort matches, assign, in one mtb_classify_batch call;
+* ``Classifier.startClassify`` — the batch loop over FASTA/FASTQ inputs, writing the per-read
+  TSV (Reporter::writeReadClassification, Reporter.cpp:38-83).
+
+All compute runs in libmtbgpu.so (HIP); there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import gzip
+import os
+from typing import Iterator, List, Optional, Tuple
+
+import numpy as np
+
+from . import _abi
+from ._abi import KMER_DTYPE, MATCH_DTYPE, RESULT_DTYPE, TAXCNT_DTYPE, MtbParams, ptr
+from ._lib import MtbError, check, lib
+
+
+@dataclasses.dataclass
+class LocalParameters:
+    seqMode: int = 2
+    kmerFormat: int = 1
+    syncmer: int = 0
+    smerLen: int = 5
+    reducedAA: int = 0
+    skipRedundancy: int = 0
+    minScore: float = 0.0
+    minSpScore: float = 0.0
+    minConsCnt: int = 4
+    minConsCntEuk: int = 9
+    tieRatio: float = 0.95
+    accessionLevel: int = 0
+    em: int = 0
+    threads: int = 1
+    maskMode: int = 0
+    filenames: List[str] = dataclasses.field(default_factory=list)
+
+    def to_c(self) -> MtbParams:
+        return MtbParams(seq_mode=self.seqMode, kmer_format=self.kmerFormat, syncmer=self.syncmer,
+                         smer_len=self.smerLen, reduced_aa=self.reducedAA, skip_redundancy=self.skipRedundancy,
+                         min_score=self.minScore, min_sp_score=self.minSpScore, min_cons_cnt=self.minConsCnt,
+                         min_cons_cnt_euk=self.minConsCntEuk, tie_ratio=self.tieRatio,
+                         accession_level=self.accessionLevel, em=self.em, threads=self.threads,
+                         mask_mode=self.maskMode)
+
+    def load_db_parameters(self, db_dir: str) -> "LocalParameters":
+        p = self.to_c()
+        lib().mtb_load_db_parameters(db_dir.encode(), ctypes.byref(p))
+        self.reducedAA, self.accessionLevel = p.reduced_aa, p.accession_level
+        self.skipRedundancy, self.syncmer, self.smerLen = p.skip_redundancy, p.syncmer, p.smer_len
+        self.kmerFormat = p.kmer_format
+        return self
+
+
+def setClassifyDefaults() -> LocalParameters:
+    return LocalParameters()
+
+
+@dataclasses.dataclass
+class BatchResult:
+    results: np.ndarray   # RESULT_DTYPE per read
+    taxcnt: np.ndarray    # TAXCNT_DTYPE pooled
+    query_kmers: int
+    matches: int
+    stage_ms: np.ndarray  # extract, k-mer sort, match, assign, total
+
+    def taxcnt_of(self, i: int) -> List[Tuple[int, int]]:
+        r = self.results[i]
+        s = int(r["taxcnt_offset"])
+        return [(int(t), int(c)) for t, c in self.taxcnt[s:s + int(r["taxcnt_len"])]]
+
+
+class Classifier:
+    """GPU-resident classifier; one instance per device (mirrors Classifier.cpp:6-32)."""
+
+    def __init__(self, par: LocalParameters, db_dir: Optional[str] = None, device: int = 0,
+                 db_host: Optional[_abi.MtbDbHost] = None):
+        self.par = par
+        self.device = device
+        self.handle = ctypes.c_void_p()
+        if db_host is not None:
+            check(lib().mtb_open_host(ctypes.byref(db_host), ctypes.byref(par.to_c()), device,
+                                      ctypes.byref(self.handle)), "mtb_open_host")
+        else:
+            if db_dir is None:
+                db_dir = par.filenames[1 + (par.seqMode == 2)]
+            par.load_db_parameters(db_dir)
+            check(lib().mtb_open(db_dir.encode(), ctypes.byref(par.to_c()), device, ctypes.byref(self.handle)),
+                  "mtb_open")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().mtb_close(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def db_kmers(self) -> int:
+        return int(lib().mtb_db_kmers(self.handle))
+
+    def set_stream(self, stream_ptr: int) -> None:
+        check(lib().mtb_set_stream(self.handle, ctypes.c_void_p(stream_ptr)), "mtb_set_stream")
+
+    # -- one QuerySplit --------------------------------------------------------------------------
+    def classify_batch(self, seq1: np.ndarray, off1: np.ndarray, seq2=None, off2=None, keep_stages: bool = False,
+                       device_input: bool = False, fetch: bool = True) -> Optional[BatchResult]:
+        n = (len(off1) - 1) if not device_input else int(off1.numel()) - 1
+        flags = (_abi.MTB_KEEP_STAGES if keep_stages else 0) | (_abi.MTB_INPUT_DEVICE if device_input else 0)
+        if device_input:
+            ptrs = [ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+                    for t in (seq1, off1, seq2, off2)]
+        else:
+            ptrs = [ptr(np.ascontiguousarray(a)) if a is not None else ctypes.c_void_p(0)
+                    for a in (seq1, off1, seq2, off2)]
+            self._keep = (seq1, off1, seq2, off2)
+        res = np.zeros(n, RESULT_DTYPE) if fetch else None
+        check(lib().mtb_classify_batch(self.handle, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, flags,
+                                       ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_classify_batch")
+        if not fetch:
+            return None
+        return BatchResult(res, self.taxcnt(), *self.last_counts(), self.stage_ms())
+
+    def taxcnt(self) -> np.ndarray:
+        nt = ctypes.c_uint64(0)
+        lib().mtb_get_taxcnt(self.handle, ctypes.c_void_p(0), 0, ctypes.byref(nt))
+        tc = np.zeros(int(nt.value), TAXCNT_DTYPE)
+        check(lib().mtb_get_taxcnt(self.handle, ptr(tc), len(tc), ctypes.byref(nt)), "mtb_get_taxcnt")
+        return tc
+
+    def last_counts(self) -> Tuple[int, int]:
+        q, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        lib().mtb_last_counts(self.handle, ctypes.byref(q), ctypes.byref(m))
+        return int(q.value), int(m.value)
+
+    def stage_ms(self) -> np.ndarray:
+        ms = (ctypes.c_float * 5)()
+        lib().mtb_last_stage_ms(self.handle, ms, 5)
+        return np.array(list(ms), np.float32)
+
+    def query_kmers(self) -> np.ndarray:
+        q, _ = self.last_counts()
+        out = np.zeros(q, KMER_DTYPE)
+        nq = ctypes.c_uint64(0)
+        check(lib().mtb_get_query_kmers(self.handle, ptr(out), q, ctypes.byref(nq)), "mtb_get_query_kmers")
+        return out
+
+    def matches(self) -> np.ndarray:
+        _, m = self.last_counts()
+        out = np.zeros(m, MATCH_DTYPE)
+        nm = ctypes.c_uint64(0)
+        check(lib().mtb_get_matches(self.handle, ptr(out), m, ctypes.byref(nm)), "mtb_get_matches")
+        return out
+
+    def assign_matches(self, matches: np.ndarray, query_len: np.ndarray) -> BatchResult:
+        matches = np.ascontiguousarray(matches, MATCH_DTYPE)
+        ql = np.ascontiguousarray(query_len, np.uint32)
+        res = np.zeros(len(ql), RESULT_DTYPE)
+        check(lib().mtb_assign_matches(self.handle, ptr(matches), len(matches), ptr(ql), len(ql), ptr(res)),
+              "mtb_assign_matches")
+        return BatchResult(res, self.taxcnt(), 0, len(matches), self.stage_ms())
+
+    # -- Classifier::startClassify over files ----------------------------------------------------
+    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000) -> int:
+        par = self.par
+        q1 = par.filenames[0]
+        q2 = par.filenames[1] if par.seqMode == 2 else None
+        total = 0
+        with open(out_tsv, "w") as out:
+            out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n")
+            for names, s1, o1, s2, o2 in read_batches(q1, q2, reads_per_batch):
+                br = self.classify_batch(s1, o1, s2, o2)
+                write_classifications(out, names, br, self._rank_of)
+                total += len(names)
+        return total
+
+    _rank_of = None
+
+
+# --------------------------------------------------------------------------------------------------
+# Host I/O: FASTA/FASTQ(.gz) reading (KSeqWrapper semantics: name = header up to first whitespace)
+# and the per-read TSV (Reporter.cpp:38-83).
+# --------------------------------------------------------------------------------------------------
+def _open(path: str):
+    return gzip.open(path, "rb") if path.endswith(".gz") else open(path, "rb")
+
+
+def read_records(path: str) -> Iterator[Tuple[bytes, bytes]]:
+    with _open(path) as f:
+        data = f.read()
+    if not data:
+        return
+    if data[:1] == b">":
+        for chunk in data[1:].split(b"\n>"):
+            lines = chunk.split(b"\n")
+            yield lines[0].split()[0] if lines[0].split() else b"", b"".join(l.strip() for l in lines[1:])
+    else:
+        lines = data.split(b"\n")
+        for i in range(0, len(lines) - 3, 4):
+            h = lines[i][1:].split()
+            yield (h[0] if h else b""), lines[i + 1].strip()
+
+
+def pack(seqs: List[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    return np.frombuffer(b"".join(seqs), np.uint8).copy(), off
+
+
+def read_batches(q1: str, q2: Optional[str], n: int):
+    it1 = read_records(q1)
+    it2 = read_records(q2) if q2 else None
+    while True:
+        names, a, b = [], [], []
+        for rec in it1:
+            names.append(rec[0].decode())
+            a.append(rec[1])
+            if it2 is not None:
+                r2 = next(it2, None)
+                if r2 is None:
+                    raise MtbError("paired-end inputs have different read counts (QueryIndexer.cpp:121-124)")
+                b.append(r2[1])
+            if len(names) == n:
+                break
+        if not names:
+            return
+        s1, o1 = pack(a)
+        s2, o2 = pack(b) if it2 is not None else (None, None)
+        yield names, s1, o1, s2, o2
+        if len(names) < n:
+            return
+
+
+def write_classifications(out, names: List[str], br: BatchResult, rank_of=None) -> None:
+    res = br.results
+    for i, nm in enumerate(names):
+        r = res[i]
+        score = "%g" % float(r["score"])
+        if r["is_classified"]:
+            rank = rank_of(int(r["classification"])) if rank_of else "-"
+            tc = "".join(f"{t}:{c} " for t, c in br.taxcnt_of(i))
+            out.write(f"1\t{nm}\t{int(r['classification'])}\t{int(r['query_length'])}\t{score}\t{rank}\t{tc}\n")
+        else:
+            out.write(f"0\t{nm}\t0\t{int(r['query_length'])}\t{score}\t-\t-\t\n")

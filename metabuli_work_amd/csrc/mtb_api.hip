@@ -1,0 +1,490 @@
+// C-ABI of the MI355X classify path (include/mtb_gpu.h): context, DB residency in HBM and the
+// per-batch pipeline K0 read metadata -> K1 extract -> K2 radix sort -> K4 match (count, scan,
+// emit) -> K5/K6 per-read sort + assignment -> taxcnt compaction.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mtb_host.h"
+#include "mtb_launch.h"
+
+using namespace mtb;
+
+#define HIP_TRY(x)                                                                                   \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x);                 \
+            return MTB_ERR_HIP;                                                                      \
+        }                                                                                            \
+    } while (0)
+
+namespace {
+
+struct DevBuf {  // grow-only device allocation
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t b = need + need / 8 + 256;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+};
+
+}  // namespace
+
+struct mtb_ctx {
+    int device = 0;
+    mtb_params par{};
+    hipStream_t stream = nullptr;
+    bool ownStream = false;
+    HostTables tables{};
+    // DB residency
+    uint64_t D = 0;
+    uint64_t* dbv = nullptr;
+    uint32_t* dbinfo = nullptr;
+    int32_t* spOf = nullptr;
+    int32_t maxTax = 0;
+    int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
+    uint8_t* tFlags = nullptr;
+    uint32_t cladePerMatch = 2;
+    // batch workspace
+    DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, qcapOff, scanTmp;
+    DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
+    DevBuf readCnt, mOff, matches, errFlag;
+    DevBuf local, paths, comb, conn, spScore, spId, quot, clade, tcPool, tcLen, tcOff, tcOut, results;
+    // last batch
+    uint32_t nReads = 0;
+    uint64_t Q = 0, M = 0, nTaxcnt = 0;
+    bool sortedInB = false;
+    bool keepStages = false;
+    float stageMs[5] = {0, 0, 0, 0, 0};
+    hipEvent_t ev[6]{};
+};
+
+static void free_db(mtb_ctx* c) {
+    void* ptrs[] = {c->dbv, c->dbinfo, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    c->dbv = nullptr;
+    c->dbinfo = nullptr;
+}
+
+template <typename T>
+static hipError_t upload(T** dst, const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = hipMalloc((void**)dst, std::max<size_t>(1, v.size()) * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+    return e;
+}
+
+static int validate_params(const mtb_params* p) {
+    if (p->reduced_aa) { set_error("reduced-AA DBs (ReducedKmerMatcher) are out of scope"); return MTB_ERR_UNSUPPORTED; }
+    if (p->em) { set_error("--em reassignment is out of scope"); return MTB_ERR_UNSUPPORTED; }
+    if (p->mask_mode) { set_error("low-complexity masking is out of scope"); return MTB_ERR_UNSUPPORTED; }
+    if (p->kmer_format != 1 && p->kmer_format != 2) { set_error("kmer_format must be 1 or 2"); return MTB_ERR_UNSUPPORTED; }
+    if (p->syncmer && p->kmer_format != 2) { set_error("syncmer requires kmer_format 2"); return MTB_ERR_UNSUPPORTED; }
+    if (p->syncmer && (p->smer_len < 1 || p->smer_len > 8)) { set_error("smer_len must be in [1, 8]"); return MTB_ERR_ARG; }
+    if (p->seq_mode < 1 || p->seq_mode > 3) { set_error("seq_mode must be 1, 2 or 3"); return MTB_ERR_ARG; }
+    return MTB_OK;
+}
+
+static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out) {
+    int rc = validate_params(par);
+    if (rc != MTB_OK) return rc;
+    if (!check_db(db)) return MTB_ERR_DB;
+    if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
+    mtb_ctx* c = new mtb_ctx();
+    c->device = device;
+    c->par = *par;
+    c->tables = make_tables();
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->ownStream = true;
+    for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+    hipStream_t s = c->stream;
+    c->D = db.info.size();
+    // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381)
+    uint16_t* dDiff = nullptr;
+    uint32_t* dFlag = nullptr;
+    uint64_t* dIdx = nullptr;
+    void* dTmp = nullptr;
+    const uint64_t nDiff = db.diffIdx.size();
+    HIP_TRY(hipMalloc(&c->dbv, c->D * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
+    HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+    decode_diff_idx(dDiff, nDiff, c->dbv, c->D, dFlag, dIdx, dTmp, s);
+    HIP_TRY(upload(&c->dbinfo, db.info, s));
+    const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
+    launch_mask_info(c->dbinfo, c->D, mask, s);
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(dDiff);
+    hipFree(dFlag);
+    hipFree(dIdx);
+    hipFree(dTmp);
+    // taxonomy + taxId2speciesId
+    const HostTaxonomy& T = db.tax;
+    c->maxTax = T.maxTax;
+    HIP_TRY(upload(&c->spOf, db.speciesOf, s));
+    HIP_TRY(upload(&c->tNodeOf, T.nodeOf, s));
+    HIP_TRY(upload(&c->tNodeTax, T.nodeTax, s));
+    HIP_TRY(upload(&c->tParent, T.parent, s));
+    HIP_TRY(upload(&c->tDepth, T.depth, s));
+    HIP_TRY(upload(&c->tSpParent, T.spParent, s));
+    HIP_TRY(upload(&c->tFlags, T.flags, s));
+    // clade scratch per match: 1 + deepest chain from a node up to its species
+    int maxSub = 0;
+    for (size_t i = 0; i < T.nodeTax.size(); i++) {
+        int32_t sp = T.taxIdAtRank(T.nodeTax[i], "species");
+        if (!T.exists(sp)) continue;
+        int spNode = T.nodeOf[sp];
+        if (T.lcaNode((int)i, spNode) != spNode) continue;
+        maxSub = std::max(maxSub, T.depth[i] - T.depth[spNode]);
+    }
+    c->cladePerMatch = (uint32_t)(maxSub + 1);
+    HIP_TRY(hipStreamSynchronize(s));
+    *out = c;
+    return MTB_OK;
+}
+
+extern "C" {
+
+int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** out) {
+    if (!db_dir || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
+    HostDb db;
+    if (!load_db_files(db_dir, db)) return MTB_ERR_IO;
+    return open_common(db, par, device, out);
+}
+
+int mtb_open_host(const mtb_db_host* h, const mtb_params* par, int device, mtb_ctx** out) {
+    if (!h || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
+    HostDb db;
+    db.diffIdx.assign(h->diff_idx, h->diff_idx + h->n_diff_idx);
+    db.info.assign(h->info, h->info + h->n_info);
+    if (h->split) db.split.assign(h->split, h->split + 3 * h->n_split);
+    db.taxIdList.assign(h->taxid_list, h->taxid_list + h->n_taxid_list);
+    std::vector<std::string> ranks(h->n_nodes), names(h->n_nodes);
+    for (uint64_t i = 0; i < h->n_nodes; i++) {
+        ranks[i] = h->rank_pool + h->rank_off[i];
+        if (h->name_pool) names[i] = h->name_pool + h->name_off[i];
+    }
+    if (!build_taxonomy(h->node_taxid, h->node_parent, h->n_nodes, ranks, names, h->merged_old, h->merged_new,
+                        h->n_merged, db.tax) ||
+        !build_species_map(db))
+        return MTB_ERR_DB;
+    return open_common(db, par, device, out);
+}
+
+void mtb_close(mtb_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_db(c);
+    DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
+                      &c->qcapOff, &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->errFlag, &c->local, &c->paths,
+                      &c->comb, &c->conn, &c->spScore, &c->spId, &c->quot, &c->clade, &c->tcPool, &c->tcLen,
+                      &c->tcOff, &c->tcOut, &c->results};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->ownStream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mtb_set_stream(mtb_ctx* c, void* stream) {
+    if (!c) return MTB_ERR_ARG;
+    if (c->ownStream && c->stream) hipStreamDestroy(c->stream);
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+        c->ownStream = false;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->ownStream = true;
+    }
+    return MTB_OK;
+}
+
+uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
+
+}  // extern "C"
+
+__global__ void k_qcap(const uint32_t* __restrict__ qlen, uint32_t n, int dnaShift, uint32_t* __restrict__ qcap) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) qcap[i] = (uint32_t)(((int)qlen[i] + 3) / dnaShift + 1);  // maxQuotient + 1 (Taxonomer.cpp:210)
+}
+
+static AssignArgs assign_args(const mtb_params& p) {
+    AssignArgs a;
+    a.kmerFormat = p.kmer_format;
+    if (p.syncmer) {  // Taxonomer.cpp:34-42
+        a.dnaShift = (8 - p.smer_len) * 3;
+        a.maxCodonShift = 8 - p.smer_len;
+    } else {
+        a.dnaShift = 3;
+        a.maxCodonShift = 1;
+    }
+    a.denominator = (p.seq_mode == 1 || p.seq_mode == 2) ? 100 : 1000;  // Taxonomer.cpp:44-48
+    a.minConsCnt = p.min_cons_cnt;
+    a.minConsCntEuk = p.min_cons_cnt_euk;
+    a.accessionLevel = p.accession_level;
+    a.minScore = p.min_score;
+    a.minSpScore = p.min_sp_score;
+    a.tieRatio = p.tie_ratio;
+    return a;
+}
+
+// K5 + K6 + taxcnt compaction on the matches already grouped by read in c->matches (mOff).
+static int assign_stage(mtb_ctx* c, uint32_t n) {
+    hipStream_t s = c->stream;
+    const uint64_t M = c->M;
+    AssignArgs a = assign_args(c->par);
+    if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
+    HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->qcapOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
+    k_qcap<<<(n + 255) / 256, 256, 0, s>>>(c->qlen.as<uint32_t>(), n, a.dnaShift, c->readCnt.as<uint32_t>());
+    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->qcapOff.as<uint64_t>(), c->scanTmp.p, s);
+    uint64_t QC = 0;
+    HIP_TRY(hipMemcpyAsync(&QC, c->qcapOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t Mc = std::max<uint64_t>(M, 1);
+    HIP_TRY(c->local.ensure(path_bytes() * Mc));
+    HIP_TRY(c->paths.ensure(path_bytes() * Mc));
+    HIP_TRY(c->comb.ensure(path_bytes() * Mc));
+    HIP_TRY(c->conn.ensure(Mc));
+    HIP_TRY(c->spScore.ensure(sizeof(float) * Mc));
+    HIP_TRY(c->spId.ensure(sizeof(int32_t) * Mc));
+    HIP_TRY(c->quot.ensure(quot_bytes() * std::max<uint64_t>(QC, 1)));
+    HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
+    HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Mc));
+    HIP_TRY(c->results.ensure(sizeof(mtb_result) * std::max<uint32_t>(n, 1)));
+    TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
+    AssignScratch sc{c->local.p, c->paths.p, c->comb.p, c->conn.as<uint8_t>(), c->spScore.as<float>(),
+                     c->spId.as<int32_t>(), c->quot.p, c->clade.p, c->cladePerMatch};
+    launch_assign(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
+                  n, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
+    HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
+    launch_taxcnt_len(c->results.as<mtb_result>(), n, c->tcLen.as<uint32_t>(), s);
+    exclusive_scan_u32(c->tcLen.as<uint32_t>(), n, c->tcOff.as<uint64_t>(), c->scanTmp.p, s);
+    uint64_t NT = 0;
+    HIP_TRY(hipMemcpyAsync(&NT, c->tcOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(c->tcOut.ensure(sizeof(mtb_taxcnt) * std::max<uint64_t>(NT, 1)));
+    launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), c->mOff.as<uint64_t>(), c->results.as<mtb_result>(),
+                          c->tcOff.as<uint64_t>(), n, c->tcOut.as<mtb_taxcnt>(), s);
+    c->nTaxcnt = NT;
+    return MTB_OK;
+}
+
+extern "C" {
+
+int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const char* seq2, const uint64_t* off2,
+                       uint32_t n, uint32_t flags, mtb_result* results) {
+    if (!c || !off || !seq) { set_error("null argument"); return MTB_ERR_ARG; }
+    const bool paired = c->par.seq_mode == 2;
+    if (paired && (!seq2 || !off2)) { set_error("seq_mode 2 needs both mates"); return MTB_ERR_ARG; }
+    if (n >= (1u << 29)) { set_error("batch exceeds the 29-bit seqID field (Kmer.h:14)"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->nReads = n;
+    c->keepStages = (flags & MTB_KEEP_STAGES) != 0;
+    const uint64_t *dOff1, *dOff2 = nullptr;
+    const uint8_t *dSeq1, *dSeq2 = nullptr;
+    HIP_TRY(hipEventRecord(c->ev[0], s));
+    if (flags & MTB_INPUT_DEVICE) {
+        dSeq1 = (const uint8_t*)seq;
+        dOff1 = off;
+        dSeq2 = (const uint8_t*)seq2;
+        dOff2 = off2;
+    } else {
+        uint64_t b1 = off[n], b2 = paired ? off2[n] : 0;
+        HIP_TRY(c->seq1.ensure(b1 + 1));
+        HIP_TRY(c->off1.ensure(sizeof(uint64_t) * (n + 1)));
+        HIP_TRY(hipMemcpyAsync(c->seq1.p, seq, b1, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(c->off1.p, off, sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, s));
+        dSeq1 = c->seq1.as<uint8_t>();
+        dOff1 = c->off1.as<uint64_t>();
+        if (paired) {
+            HIP_TRY(c->seq2.ensure(b2 + 1));
+            HIP_TRY(c->off2.ensure(sizeof(uint64_t) * (n + 1)));
+            HIP_TRY(hipMemcpyAsync(c->seq2.p, seq2, b2, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(c->off2.p, off2, sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, s));
+            dSeq2 = c->seq2.as<uint8_t>();
+            dOff2 = c->off2.as<uint64_t>();
+        }
+    }
+    // K0: read metadata and reserved slots (KmerExtractor.cpp:442-494, Buffer::reserveMemory)
+    HIP_TRY(c->meta.ensure(sizeof(ReadMeta) * (n + 1)));
+    HIP_TRY(c->reserve.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->slotOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
+    launch_read_meta(dOff1, dOff2, n, paired, c->meta.as<ReadMeta>(), c->reserve.as<uint64_t>(), c->qlen.as<uint32_t>(), s);
+    exclusive_scan_u64(c->reserve.as<uint64_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
+    uint64_t R = 0;
+    HIP_TRY(hipMemcpyAsync(&R, c->slotOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // K1 extract into reserved slots
+    const uint64_t Rc = std::max<uint64_t>(R, 1);
+    HIP_TRY(c->keysA.ensure(8 * Rc));
+    HIP_TRY(c->valsA.ensure(8 * Rc));
+    HIP_TRY(c->keysB.ensure(8 * Rc));
+    HIP_TRY(c->valsB.ensure(8 * Rc));
+    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(), n, paired, c->tables,
+                   c->par.kmer_format, c->par.syncmer, c->par.smer_len, c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(),
+                   s);
+    HIP_TRY(hipEventRecord(c->ev[1], s));
+    // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
+    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Rc)));
+    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
+    bool inB = false;
+    const int bitHi = c->par.kmer_format == 2 ? 64 : 64;
+    uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), c->keysB.as<uint64_t>(),
+                                  c->valsB.as<uint64_t>(), R, 24, bitHi, true, c->radixCounts.as<uint32_t>(),
+                                  c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+    c->Q = Q;
+    c->sortedInB = inB;
+    const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
+    const uint64_t* qi = inB ? c->valsB.as<uint64_t>() : c->valsA.as<uint64_t>();
+    HIP_TRY(hipEventRecord(c->ev[2], s));
+    // K4 match: count, scan per-read counts, emit into per-read segments
+    HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->errFlag.ensure(sizeof(int)));
+    HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+    HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
+    launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+                 c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), s);
+    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
+    uint64_t M = 0;
+    HIP_TRY(hipMemcpyAsync(&M, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->M = M;
+    HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
+    HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+    launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+                 c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
+    HIP_TRY(hipEventRecord(c->ev[3], s));
+    // K5 + K6
+    int rc = assign_stage(c, n);
+    if (rc != MTB_OK) return rc;
+    HIP_TRY(hipEventRecord(c->ev[4], s));
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
+    HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
+    if (err) {
+        set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
+        return MTB_ERR_DB;
+    }
+    return MTB_OK;
+}
+
+int mtb_get_taxcnt(mtb_ctx* c, mtb_taxcnt* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return MTB_ERR_ARG;
+    *n_out = c->nTaxcnt;
+    if (cap < c->nTaxcnt) return MTB_RETRY;
+    if (c->nTaxcnt) HIP_TRY(hipMemcpy(out, c->tcOut.p, sizeof(mtb_taxcnt) * c->nTaxcnt, hipMemcpyDeviceToHost));
+    return MTB_OK;
+}
+
+int mtb_device_results(mtb_ctx* c, void** results, void** taxcnt, uint64_t* n_taxcnt) {
+    if (!c) return MTB_ERR_ARG;
+    if (results) *results = c->results.p;
+    if (taxcnt) *taxcnt = c->tcOut.p;
+    if (n_taxcnt) *n_taxcnt = c->nTaxcnt;
+    return MTB_OK;
+}
+
+int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
+    if (!c) return MTB_ERR_ARG;
+    if (q) *q = c->Q;
+    if (m) *m = c->M;
+    return MTB_OK;
+}
+
+int mtb_last_stage_ms(const mtb_ctx* c, float* ms, int n) {
+    if (!c || !ms) return MTB_ERR_ARG;
+    for (int i = 0; i < n && i < 5; i++) ms[i] = c->stageMs[i];
+    return MTB_OK;
+}
+
+int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return MTB_ERR_ARG;
+    *n_out = c->Q;
+    if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
+    if (cap < c->Q) return MTB_RETRY;
+    std::vector<uint64_t> k(c->Q), v(c->Q);
+    const void* kp = c->sortedInB ? c->keysB.p : c->keysA.p;
+    const void* vp = c->sortedInB ? c->valsB.p : c->valsA.p;
+    if (c->Q) {
+        HIP_TRY(hipMemcpy(k.data(), kp, 8 * c->Q, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(v.data(), vp, 8 * c->Q, hipMemcpyDeviceToHost));
+    }
+    for (uint64_t i = 0; i < c->Q; i++) out[i] = mtb_kmer{k[i], v[i]};
+    return MTB_OK;
+}
+
+int mtb_get_matches(mtb_ctx* c, mtb_match* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return MTB_ERR_ARG;
+    *n_out = c->M;
+    if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
+    if (cap < c->M) return MTB_RETRY;
+    if (c->M) HIP_TRY(hipMemcpy(out, c->matches.p, sizeof(mtb_match) * c->M, hipMemcpyDeviceToHost));
+    return MTB_OK;
+}
+
+int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_t* qlen, uint32_t n,
+                       mtb_result* results) {
+    if (!c || (!m && nm) || !qlen) return MTB_ERR_ARG;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // group by read (counting sort by seqID) on the host, then K5 + K6 on the device
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint64_t i = 0; i < nm; i++) {
+        uint32_t sq = info_seq(m[i].qinfo);
+        if (sq == 0 || sq > n) { set_error("match seqID out of range"); return MTB_ERR_ARG; }
+        off[sq]++;
+    }
+    for (uint32_t i = 0; i < n; i++) off[i + 1] += off[i];
+    std::vector<mtb_match> grouped(std::max<uint64_t>(nm, 1));
+    std::vector<uint64_t> cur(off.begin(), off.end() - 1);
+    for (uint64_t i = 0; i < nm; i++) grouped[cur[info_seq(m[i].qinfo) - 1]++] = m[i];
+    c->M = nm;
+    c->nReads = n;
+    HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
+    HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(hipMemcpyAsync(c->matches.p, grouped.data(), sizeof(mtb_match) * nm, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->mOff.p, off.data(), sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->qlen.p, qlen, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+    int rc = assign_stage(c, n);
+    if (rc != MTB_OK) return rc;
+    if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->keepStages = true;
+    return MTB_OK;
+}
+
+}  // extern "C"

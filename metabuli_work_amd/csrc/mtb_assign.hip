@@ -1,0 +1,473 @@
+// K5 + K6: per-read match sort and taxonomic assignment (Classifier::assignTaxonomy,
+// Classifier.cpp:166-208; Taxonomer::chooseBestTaxon and helpers, Taxonomer.cpp:130-713).
+//
+// One thread per read in this version: the thread sorts its read's match segment in place
+// (compareMatches, KmerMatcher.cpp:1149-1166), then runs the reference's decision tree with
+// per-read scratch carved from batch-wide arrays by the read's match offset. Float arithmetic
+// follows the reference operation for operation (compiled with -ffp-contract=off).
+#include "mtb_launch.h"
+#include "mtb_stdsort.h"
+
+namespace mtb {
+
+struct Path {  // MatchPath (Taxonomer.h:35-59); start/end match as indices into the read segment
+    int start, end;
+    float score;
+    int hd, depth;
+    uint32_t sm, em;
+};
+
+__device__ __forceinline__ bool match_less(const mtb_match& a, const mtb_match& b) {
+    uint32_t sa = info_seq(a.qinfo), sb = info_seq(b.qinfo);
+    if (sa != sb) return sa < sb;
+    if (a.species_id != b.species_id) return (int)a.species_id < (int)b.species_id;
+    uint32_t fa = info_frame(a.qinfo), fb = info_frame(b.qinfo);
+    if (fa != fb) return fa < fb;
+    uint32_t pa = info_pos(a.qinfo), pb = info_pos(b.qinfo);
+    if (pa != pb) return pa < pb;
+    if (a.hamming != b.hamming) return a.hamming < b.hamming;
+    if (a.dna_encoding != b.dna_encoding) return a.dna_encoding < b.dna_encoding;
+    // compareMatches stops here; a valid DB has one entry per (value, species) so no two matches
+    // of one query k-mer tie. The extra keys only make the order total.
+    if (a.target_id != b.target_id) return a.target_id < b.target_id;
+    return a.right_end_hamming < b.right_end_hamming;
+}
+
+__device__ inline void heap_sift(mtb_match* a, long i, long n) {
+    while (true) {
+        long c = 2 * i + 1;
+        if (c >= n) return;
+        if (c + 1 < n && match_less(a[c], a[c + 1])) c++;
+        if (!match_less(a[i], a[c])) return;
+        mtb_match t = a[i]; a[i] = a[c]; a[c] = t;
+        i = c;
+    }
+}
+
+__device__ inline void sort_matches(mtb_match* a, long n) {
+    if (n < 2) return;
+    if (n <= 24) {
+        for (long i = 1; i < n; i++) {
+            mtb_match v = a[i];
+            long j = i;
+            while (j > 0 && match_less(v, a[j - 1])) { a[j] = a[j - 1]; j--; }
+            a[j] = v;
+        }
+        return;
+    }
+    for (long i = n / 2 - 1; i >= 0; i--) heap_sift(a, i, n);
+    for (long e = n - 1; e > 0; e--) {
+        mtb_match t = a[0]; a[0] = a[e]; a[e] = t;
+        heap_sift(a, 0, e);
+    }
+}
+
+struct TaxView {
+    const int32_t* nodeOf;    // taxID -> node index, -1 if absent (D array)
+    const int32_t* nodeTax;   // node -> taxID
+    const int32_t* parent;    // node -> parent node
+    const int32_t* depth;     // node -> depth below taxID 1
+    const uint8_t* flags;     // bit0: IsAncestor(Eukaryota, taxID); bit1: rank "" or "accession"
+    const int32_t* spParent;  // node -> parentTaxId of taxonNode(getTaxIdAtRank(taxID, "species"))
+    int32_t maxTax;
+    __device__ bool exists(int32_t t) const { return t >= 0 && t <= maxTax && nodeOf[t] >= 0; }
+    // NcbiTaxonomy::lcaHelper on node indices: node 0 short-circuits, otherwise the tree LCA.
+    __device__ int lca_node(int i, int j) const {
+        if (i == 0 || j == 0) return 0;
+        while (i != j) {
+            int di = depth[i], dj = depth[j];
+            if (di >= dj) i = parent[i];
+            if (dj >= di) j = parent[j];
+        }
+        return i;
+    }
+    __device__ int32_t lca(int32_t a, int32_t b) const {  // NcbiTaxonomy::LCA(TaxID, TaxID)
+        if (!exists(a)) return b;
+        if (!exists(b)) return a;
+        return nodeTax[lca_node(nodeOf[a], nodeOf[b])];
+    }
+};
+
+struct AssignCfg {
+    int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
+    float minScore, minSpScore, tieRatio;
+};
+
+struct Quot {
+    int32_t tax;
+    uint8_t minH, has, pad0, pad1;
+};
+
+struct Clade {
+    int32_t tax, parentTax;
+    uint32_t count;
+    int32_t removed;
+};
+
+__device__ __forceinline__ float score_fields(uint32_t reh, int range, bool left) {
+    float s = 0.0f;
+    for (int c = 0; c < range; c++) {
+        uint32_t h = left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u;
+        s += codon_score(h);
+    }
+    return s;
+}
+__device__ __forceinline__ int ham_fields(uint32_t reh, int range, bool left) {
+    int s = 0;
+    for (int c = 0; c < range; c++) s += (int)(left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u);
+    return s;
+}
+
+__global__ void __launch_bounds__(256) k_assign(mtb_match* __restrict__ matches, const uint64_t* __restrict__ mOff,
+                                                const uint32_t* __restrict__ qlen, const uint64_t* __restrict__ qOff,
+                                                uint32_t nReads, AssignCfg cfg, TaxView tax, Path* __restrict__ localP,
+                                                Path* __restrict__ pathsP, Path* __restrict__ combP,
+                                                uint8_t* __restrict__ connP, float* __restrict__ spScoreP,
+                                                int32_t* __restrict__ spIdP, Quot* __restrict__ quotP,
+                                                Clade* __restrict__ cladeP, uint32_t cladePerMatch,
+                                                mtb_taxcnt* __restrict__ tcP, mtb_result* __restrict__ results) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    const int readLength = (int)qlen[r];
+    mtb_result res;
+    res.classification = 0;
+    res.score = 0.0f;
+    res.hamming_dist = 0;
+    res.query_length = (uint32_t)readLength;
+    res.taxcnt_offset = (uint32_t)0;
+    res.taxcnt_len = 0;
+    res.is_classified = 0;
+    for (int k = 0; k < 7; k++) res.pad[k] = 0;
+    if (n == 0) { results[r] = res; return; }
+
+    mtb_match* M = matches + base;
+    sort_matches(M, n);
+    Path* L = localP + base;
+    Path* P = pathsP + base;
+    Path* C = combP + base;
+    uint8_t* conn = connP + base;
+    float* spScore = spScoreP + base;
+    int32_t* spId = spIdP + base;
+
+    // ---- getBestSpeciesMatches (Taxonomer.cpp:316-408) ----
+    long nP = 0, nC = 0, nS = 0, meaningful = 0;
+    float bestSpScore = 0.0f;
+    long bestFirst = 0, bestSecond = 0;
+    long i = 0;
+    while (i < n) {
+        const int32_t sp = (int32_t)M[i].species_id;
+        const long spStart = i;
+        const long prevP = nP;
+        while (i < n && (int32_t)M[i].species_id == sp) {
+            const uint32_t curFrame = info_frame(M[i].qinfo);
+            const long fs = i;
+            while (i < n && (int32_t)M[i].species_id == sp && info_frame(M[i].qinfo) == curFrame) i++;
+            if (i - fs <= 1) continue;
+            // ---- getMatchPaths(fs, i) (Taxonomer.cpp:487-648) ----
+            const long start = fs, end = i;
+            int minDepth = cfg.minConsCnt;
+            if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
+            const bool fwd = curFrame < 3;
+            for (long x = 0; x < end - start; x++) conn[x] = 0;
+            long k = start;
+            uint64_t currPos = info_pos(M[start].qinfo);
+            auto initPath = [&](long idx) {
+                Path p;
+                p.start = (int)info_pos(M[idx].qinfo);
+                p.end = p.start + 23;
+                p.score = score_fields(M[idx].right_end_hamming, 8, false);
+                p.hd = M[idx].hamming;
+                p.depth = 1;
+                p.sm = p.em = (uint32_t)idx;
+                L[idx - start] = p;
+            };
+            long curS = k;
+            while (k < end && info_pos(M[k].qinfo) == currPos) { initPath(k); ++k; }
+            long curE = k;
+            while (k < end) {
+                const uint32_t nextPos = info_pos(M[k].qinfo);
+                const long nxS = k;
+                while (k < end && info_pos(M[k].qinfo) == nextPos) { initPath(k); ++k; }
+                const long nxE = k;
+                const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
+                if (shift > 0 && shift <= cfg.maxCodonShift) {
+                    const uint32_t sh = 3u * (uint32_t)shift;
+                    const uint32_t lowMask = (1u << (24u - sh)) - 1u;
+                    for (long nx = nxS; nx < nxE; nx++) {
+                        const uint32_t nreh = M[nx].right_end_hamming;
+                        float inc = 0.0f;
+                        int hinc = 0;
+                        for (int c = 0; c < shift; c++) {
+                            uint32_t h = (nreh >> (2 * c)) & 3u;
+                            inc += codon_score(h);
+                            hinc += (int)h;
+                        }
+                        long best = -1;
+                        float bestScore = 0.0f;
+                        const uint32_t dn = M[nx].dna_encoding;
+                        for (long cu = curS; cu < curE; cu++) {
+                            const uint32_t dc = M[cu].dna_encoding;
+                            bool cons;
+                            if (cfg.kmerFormat == 2) {  // isConsecutive2 (Taxonomer.cpp:692-699)
+                                cons = fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
+                            } else {                    // isConsecutive (Taxonomer.cpp:677-683)
+                                cons = fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
+                            }
+                            if (cons) {
+                                conn[cu - start] = 1;
+                                if (L[cu - start].score > bestScore) { best = cu; bestScore = L[cu - start].score; }
+                            }
+                        }
+                        if (best >= 0) {
+                            const Path bp = L[best - start];
+                            Path& np = L[nx - start];
+                            np.start = bp.start;
+                            np.score = bp.score + inc;
+                            np.hd = bp.hd + hinc;
+                            np.depth = bp.depth + shift;
+                            np.sm = bp.sm;
+                        }
+                    }
+                }
+                for (long cu = curS; cu < curE; cu++)
+                    if (!conn[cu - start] && L[cu - start].depth >= minDepth) P[nP++] = L[cu - start];
+                if (k == end)
+                    for (long nx = nxS; nx < nxE; nx++)
+                        if (L[nx - start].depth >= minDepth) P[nP++] = L[nx - start];
+                curS = nxS;
+                curE = nxE;
+                currPos = nextPos;
+            }
+        }
+        if (nP > prevP) {
+            // ---- combineMatchPaths (Taxonomer.cpp:410-468) ----
+            stdsort::sort(P + prevP, P + nP, [](const Path& a, const Path& b) {
+                if (a.score != b.score) return a.score > b.score;
+                if (a.hd != b.hd) return a.hd < b.hd;
+                return a.start > b.start;
+            });
+            float score = 0.0f;
+            const long combStart = nC;
+            for (long pi = prevP; pi < nP; pi++) {
+                if (combStart == nC) {
+                    C[nC++] = P[pi];
+                    score += P[pi].score;
+                    continue;
+                }
+                bool overlapped = false;
+                for (long j = combStart; j < nC; j++) {
+                    Path& p = P[pi];
+                    const Path c = C[j];
+                    if ((p.end < c.start) || (c.end < p.start)) continue;
+                    const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
+                    if (ol == p.end - p.start + 1) { overlapped = true; break; }
+                    if (ol < 24) {  // trimMatchPath (Taxonomer.cpp:475-485)
+                        const int range = ol / 3;
+                        if (p.start < c.start) {
+                            const uint32_t reh = M[p.em].right_end_hamming;
+                            p.end = c.start - 1;
+                            p.hd = max(0, p.hd - ham_fields(reh, range, false));
+                            p.score = p.score - score_fields(reh, range, false) - (float)(ol % 3);
+                        } else {
+                            const uint32_t reh = M[p.sm].right_end_hamming;
+                            p.start = c.end + 1;
+                            p.hd = max(0, p.hd - ham_fields(reh, range, true));
+                            p.score = p.score - score_fields(reh, range, true) - (float)(ol % 3);
+                        }
+                        continue;
+                    }
+                    overlapped = true;
+                    break;
+                }
+                if (!overlapped) {
+                    C[nC++] = P[pi];
+                    score += P[pi].score;
+                }
+            }
+            score = score / (float)readLength;
+            score = (1.0f < score) ? 1.0f : score;  // std::min(score, 1.0f)
+            if (score < cfg.minScore) continue;
+            spId[nS] = sp;
+            spScore[nS] = score;
+            nS++;
+            if (score > 0.f) meaningful++;
+            if (score > bestSpScore) { bestSpScore = score; bestFirst = spStart; bestSecond = i; }
+        }
+    }
+
+    // ---- chooseBestTaxon (Taxonomer.cpp:130-202) ----
+    float spTotal = 0.0f;
+    int32_t bestTax = 0;
+    bool isLCA = false;
+    if (meaningful > 0) {
+        const float thr = bestSpScore * cfg.tieRatio;
+        long cnt = 0;
+        int lcaNode = -1;
+        for (long s = 0; s < nS; s++) {
+            if (spScore[s] >= thr) {
+                cnt++;
+                spTotal += spScore[s];
+                int32_t t = spId[s];
+                if (cnt == 1) bestTax = t;
+                if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
+            }
+        }
+        if (cnt > 1) {
+            isLCA = true;
+            bestTax = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
+            spTotal = spTotal / (float)cnt;
+        }
+    }
+    if (spTotal == 0 || spTotal < cfg.minScore) {
+        res.score = spTotal;
+        results[r] = res;
+        return;
+    }
+    if (isLCA) {
+        res.is_classified = 1;
+        res.classification = bestTax;
+        res.score = spTotal;
+        results[r] = res;
+        return;
+    }
+
+    // ---- filterRedundantMatches (Taxonomer.cpp:205-241) ----
+    Quot* Qs = quotP + qOff[r];
+    const long maxQ = (long)((readLength + 3) / cfg.dnaShift);
+    for (long q = 0; q <= maxQ; q++) { Qs[q].has = 0; Qs[q].minH = 255; Qs[q].tax = 0; }
+    for (long x = bestFirst; x < bestSecond; x++) {
+        const long q = (long)(info_pos(M[x].qinfo) / (uint32_t)cfg.dnaShift);
+        const uint8_t h = M[x].hamming;
+        const int32_t t = (int32_t)M[x].target_id;
+        if (!Qs[q].has) { Qs[q].has = 1; Qs[q].tax = t; Qs[q].minH = h; }
+        else if (h < Qs[q].minH) { Qs[q].tax = t; Qs[q].minH = h; }
+        else if (h == Qs[q].minH) Qs[q].tax = tax.lca(Qs[q].tax, t);
+    }
+    mtb_taxcnt* tc = tcP + base;  // capacity n (each quotient holds >= 1 match)
+    long nTc = 0;
+    for (long q = 0; q <= maxQ; q++) {
+        if (!Qs[q].has) continue;
+        const int32_t t = Qs[q].tax;
+        long f = 0;
+        while (f < nTc && tc[f].tax_id != t) f++;
+        if (f == nTc) { tc[nTc].tax_id = t; tc[nTc].count = 0; nTc++; }
+        tc[f].count++;
+    }
+    for (long a = 1; a < nTc; a++) {  // std::map order
+        mtb_taxcnt v = tc[a];
+        long b = a;
+        while (b > 0 && tc[b - 1].tax_id > v.tax_id) { tc[b] = tc[b - 1]; b--; }
+        tc[b] = v;
+    }
+    res.taxcnt_offset = (uint32_t)0;
+    res.taxcnt_len = (uint32_t)nTc;
+    res.is_classified = 1;
+    res.score = spTotal;
+    if (spTotal < cfg.minSpScore) {
+        res.classification = tax.exists(bestTax) ? tax.spParent[tax.nodeOf[bestTax]] : 0;
+        results[r] = res;
+        return;
+    }
+
+    // ---- lowerRankClassification / getSpeciesCladeCounts / BFS (Taxonomer.cpp:252-314) ----
+    const int32_t spT = bestTax;
+    Clade* cl = cladeP + base * cladePerMatch;
+    const long clCap = n * (long)cladePerMatch;
+    long nCl = 0;
+    auto findOrAdd = [&](int32_t t) -> long {
+        for (long z = 0; z < nCl; z++)
+            if (cl[z].tax == t) return z;
+        if (nCl >= clCap) return -1;
+        cl[nCl].tax = t;
+        cl[nCl].parentTax = 0;
+        cl[nCl].count = 0;
+        cl[nCl].removed = 0;
+        return nCl++;
+    };
+    for (long e = 0; e < nTc; e++) {
+        const uint32_t c = tc[e].count;
+        int node = tax.nodeOf[tc[e].tax_id];
+        int32_t t = tax.nodeTax[node];
+        long z = findOrAdd(t);
+        if (z < 0) break;
+        cl[z].count += c;
+        int guard = 0;
+        while (t != spT && guard++ < 64) {
+            const int pnode = tax.parent[node];
+            const int32_t pt = tax.nodeTax[pnode];
+            cl[z].parentTax = pt;  // t is a child of pt
+            long pz = findOrAdd(pt);
+            if (pz < 0) break;
+            cl[pz].count += c;
+            node = pnode;
+            t = pt;
+            z = pz;
+        }
+    }
+    if (cfg.accessionLevel == 2) {
+        for (long z = 0; z < nCl; z++)
+            if (cl[z].tax != spT && (tax.flags[tax.nodeOf[cl[z].tax]] & 2u)) cl[z].removed = 1;
+    }
+    const uint32_t thr = (uint32_t)((readLength - 1) / cfg.denominator);
+    int32_t cur = spT;
+    for (int step = 0; step < 64; step++) {
+        uint32_t maxCnt = thr;
+        long nBest = 0, best = -1, nChild = 0;
+        for (long z = 0; z < nCl; z++) {
+            if (cl[z].tax == spT || cl[z].removed || cl[z].parentTax != cur) continue;
+            nChild++;
+            const uint32_t cc = cl[z].count;
+            if (cc > maxCnt) { maxCnt = cc; best = z; nBest = 1; }
+            else if (cc == maxCnt) { if (nBest == 0) best = z; nBest++; }
+        }
+        if (nChild == 0 || nBest != 1) break;
+        cur = cl[best].tax;
+    }
+    res.classification = cur;
+    results[r] = res;
+}
+
+void launch_assign(mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
+                   uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
+    if (nReads == 0) return;
+    AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
+                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio};
+    TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
+    k_assign<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, qOff, nReads, cfg, tv, (Path*)s.local,
+                                                   (Path*)s.paths, (Path*)s.comb, s.conn, s.spScore, s.spId,
+                                                   (Quot*)s.quot, (Clade*)s.clade, s.cladePerMatch, tcPool, results);
+}
+
+uint64_t path_bytes() { return sizeof(Path); }
+uint64_t quot_bytes() { return sizeof(Quot); }
+uint64_t clade_bytes() { return sizeof(Clade); }
+
+// Compaction of the per-read taxcnt slices (capacity = match count) into one pooled array.
+__global__ void k_compact_taxcnt(const mtb_taxcnt* __restrict__ pool, const uint64_t* __restrict__ mOff,
+                                 mtb_result* __restrict__ results, const uint64_t* __restrict__ tcOff, uint32_t nReads,
+                                 mtb_taxcnt* __restrict__ out) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nReads) return;
+    uint32_t len = results[r].taxcnt_len;
+    uint64_t dst = tcOff[r];
+    results[r].taxcnt_offset = (uint32_t)dst;
+    for (uint32_t k = 0; k < len; k++) out[dst + k] = pool[mOff[r] + k];
+}
+
+__global__ void k_taxcnt_len(const mtb_result* __restrict__ results, uint32_t nReads, uint32_t* __restrict__ len) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < nReads) len[r] = results[r].taxcnt_len;
+}
+
+void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s) {
+    if (nReads) k_taxcnt_len<<<(nReads + 255) / 256, 256, 0, s>>>(results, nReads, len);
+}
+void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
+                           uint32_t nReads, mtb_taxcnt* out, hipStream_t s) {
+    if (nReads) k_compact_taxcnt<<<(nReads + 255) / 256, 256, 0, s>>>(pool, mOff, results, tcOff, nReads, out);
+}
+
+}  // namespace mtb

@@ -1,0 +1,90 @@
+// Device-side helpers of the MI355X classify path: record packing, codon tables, Hamming LUTs.
+// Every table here restates the reference's (cited per item); the oracle's copy is pinned
+// against the reference's GeneticCode.h (tests/golden/genetic_code.json).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtb_gpu.h"
+
+namespace mtb {
+
+constexpr uint64_t kSentinel = ~0ull;          // blank reserved slot (never a valid metamer)
+constexpr uint64_t kAAMask = ~0xFFFFFFull;     // AMINO_ACID_PART (KmerMatcher.h:22)
+
+__host__ __device__ inline uint64_t pack_info(uint32_t seq, uint32_t pos, uint32_t frame) {
+    return (uint64_t)pos | ((uint64_t)(seq & 0x1FFFFFFFu) << 32) | ((uint64_t)(frame & 7u) << 61);
+}
+__host__ __device__ inline uint32_t info_pos(uint64_t x) { return (uint32_t)x; }
+__host__ __device__ inline uint32_t info_seq(uint64_t x) { return (uint32_t)((x >> 32) & 0x1FFFFFFFu); }
+__host__ __device__ inline uint32_t info_frame(uint64_t x) { return (uint32_t)(x >> 61); }
+
+// getMaxCoveredLength / getQueryKmerNumber (LocalUtil.h:45-59)
+__host__ __device__ inline int max_covered_length(int len) {
+    int r = len % 3;
+    return r == 2 ? len - 2 : (r == 1 ? len - 4 : len - 3);
+}
+
+// Base byte -> 2-bit code {A:0, C:1, T:2, G:3} or 7 (N / anything else). This is
+// nuc2int(atcg[c]) (GeneticCode.h:6, common.cpp:13-17) folded into one 256-entry table; the
+// complement of a valid code is code ^ 2 (iRCT, common.cpp:19-23).
+struct BaseTable {
+    uint8_t code[256];
+};
+
+// Codon tables indexed by (b1 << 4 | b2 << 2 | b3) over valid 2-bit codes (GeneticCode.h:33-194):
+// aa in [0,20] (20 = stop) and the 3-bit synonymous-codon code. Invalid codons are handled by
+// the caller (any base code 7 => AA -1).
+struct CodonTable {
+    int8_t aa[64];
+    int8_t num[64];
+};
+
+// hammingLookup (KmerMatcher.h:66-70) packed as 3 bits per entry, one 24-bit row per query codon.
+__device__ __forceinline__ uint32_t hamming_lookup(uint32_t q, uint32_t t) {
+    // rows: {0,1,1,1,2,1,3,3} {1,0,1,1,2,2,3,2} {1,1,0,1,2,2,2,3} {1,1,1,0,1,2,3,3}
+    //       {2,2,2,1,0,1,4,4} {1,2,2,2,1,0,4,4} {3,3,2,3,4,4,0,1} {3,2,3,3,4,4,1,0}
+    constexpr uint32_t R0 = 0u | 1u << 3 | 1u << 6 | 1u << 9 | 2u << 12 | 1u << 15 | 3u << 18 | 3u << 21;
+    constexpr uint32_t R1 = 1u | 0u << 3 | 1u << 6 | 1u << 9 | 2u << 12 | 2u << 15 | 3u << 18 | 2u << 21;
+    constexpr uint32_t R2 = 1u | 1u << 3 | 0u << 6 | 1u << 9 | 2u << 12 | 2u << 15 | 2u << 18 | 3u << 21;
+    constexpr uint32_t R3 = 1u | 1u << 3 | 1u << 6 | 0u << 9 | 1u << 12 | 2u << 15 | 3u << 18 | 3u << 21;
+    constexpr uint32_t R4 = 2u | 2u << 3 | 2u << 6 | 1u << 9 | 0u << 12 | 1u << 15 | 4u << 18 | 4u << 21;
+    constexpr uint32_t R5 = 1u | 2u << 3 | 2u << 6 | 2u << 9 | 1u << 12 | 0u << 15 | 4u << 18 | 4u << 21;
+    constexpr uint32_t R6 = 3u | 3u << 3 | 2u << 6 | 3u << 9 | 4u << 12 | 4u << 15 | 0u << 18 | 1u << 21;
+    constexpr uint32_t R7 = 3u | 2u << 3 | 3u << 6 | 3u << 9 | 4u << 12 | 4u << 15 | 1u << 18 | 0u << 21;
+    uint32_t row = q == 0 ? R0 : q == 1 ? R1 : q == 2 ? R2 : q == 3 ? R3 : q == 4 ? R4 : q == 5 ? R5 : q == 6 ? R6 : R7;
+    return (row >> (3 * t)) & 7u;
+}
+
+// getHammingDistanceSum (KmerMatcher.h:348-360): sum over the 8 codons of the DNA part.
+__device__ __forceinline__ uint32_t hamming_sum(uint64_t a, uint64_t b) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s += hamming_lookup((uint32_t)(a >> (3 * i)) & 7u, (uint32_t)(b >> (3 * i)) & 7u);
+    return s;
+}
+
+// One 2-bit field of HAMMING_LUT0..7 (KmerMatcher.h:72-158): a distance of 4 is stored as 0,
+// except field 7 where query rows 4-5 against target columns 6-7 read 1.
+__device__ __forceinline__ uint32_t hamming_field(uint32_t q, uint32_t t, int field) {
+    uint32_t h = hamming_lookup(q, t);
+    if (field == 7 && (q == 4u || q == 5u) && (t == 6u || t == 7u)) return 1u;
+    return h == 4u ? 0u : h;
+}
+
+// getHammings (forward) / getHammings_reverse (KmerMatcher.h:386-416)
+__device__ __forceinline__ uint32_t hammings(uint64_t a, uint64_t b, bool reverse) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t q = (uint32_t)(a >> (3 * i)) & 7u, t = (uint32_t)(b >> (3 * i)) & 7u;
+        int field = reverse ? 7 - i : i;
+        h |= hamming_field(q, t, field) << (2 * field);
+    }
+    return h;
+}
+
+// Match::getScore and partial scores (Match.h:32-70): 3 for an exact codon, else 2 - 0.5h.
+__host__ __device__ inline float codon_score(uint32_t h) { return h == 0 ? 3.0f : 2.0f - 0.5f * (float)h; }
+
+}  // namespace mtb

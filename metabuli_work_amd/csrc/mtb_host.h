@@ -1,0 +1,52 @@
+// Host-side state of a context: DB files read into memory and the taxonomy flattened into the
+// arrays the device kernels read.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mtb_gpu.h"
+#include "mtb_launch.h"
+
+namespace mtb {
+
+struct HostTaxonomy {
+    int32_t maxTax = 0;
+    int32_t eukaryota = 0;
+    std::vector<int32_t> nodeOf;    // taxID -> node (D array of NcbiTaxonomy, merged IDs folded in)
+    std::vector<int32_t> nodeTax;   // node -> taxID
+    std::vector<int32_t> parent;    // node -> parent node
+    std::vector<int32_t> depth;     // node -> depth below taxID 1
+    std::vector<uint8_t> flags;     // bit0 under Eukaryota, bit1 rank "" or "accession"
+    std::vector<int32_t> spParent;  // node -> parentTaxId of its species node (minSpScore branch)
+    std::vector<std::string> rank;
+    std::vector<std::string> name;
+
+    bool exists(int32_t t) const { return t >= 0 && t <= maxTax && nodeOf[t] >= 0; }
+    int lcaNode(int i, int j) const;
+    int32_t taxIdAtRank(int32_t taxId, const std::string& rank) const;  // TaxonomyWrapper.cpp:479-498
+    static int rankIndex(const std::string& rank);
+};
+
+struct HostDb {
+    std::vector<uint16_t> diffIdx;
+    std::vector<uint32_t> info;
+    std::vector<uint64_t> split;  // 3 words per DiffIdxSplit
+    std::vector<int32_t> taxIdList;
+    HostTaxonomy tax;
+    std::vector<int32_t> speciesOf;  // dense taxId2speciesId (KmerMatcher::loadTaxIdList)
+};
+
+void set_error(const std::string& msg);
+HostTables make_tables();
+
+bool build_taxonomy(const int32_t* taxid, const int32_t* parent, uint64_t n, const std::vector<std::string>& ranks,
+                    const std::vector<std::string>& names, const int32_t* mergedOld, const int32_t* mergedNew,
+                    uint64_t nMerged, HostTaxonomy& out);
+bool load_dmp(const std::string& dir, HostTaxonomy& out);
+bool build_species_map(HostDb& db);
+bool load_db_files(const std::string& dir, HostDb& db);
+bool check_db(const HostDb& db);
+
+}  // namespace mtb

@@ -1,0 +1,572 @@
+// HIP kernels of the classify hot path for CDNA4 (gfx950): K1 extract, K2 radix sort,
+// K3 diffIdx decode, K4 merge-match. K5/K6 (per-read match sort + assignment) are in
+// mtb_assign.hip. All integer/byte work, HBM-bound: no MFMA.
+#include "mtb_launch.h"
+
+namespace mtb {
+
+// ------------------------------------------------------------------------------------------------
+// Block-wide scan helpers (256 threads = 4 wave64)
+// ------------------------------------------------------------------------------------------------
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ unsigned long long wave_inclusive_scan(unsigned long long x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// Exclusive scan over the block; returns the exclusive prefix of x, *total = block sum.
+__device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long long x, unsigned long long* total) {
+    __shared__ unsigned long long wsum[kWaves];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long inc = wave_inclusive_scan(x);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    unsigned long long off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; i++) {
+        if (i < w) off += wsum[i];
+        tot += wsum[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - x;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device-wide exclusive scan: out[i] = sum(in[0..i)), out[n] = total. Three launches:
+// per-tile sums, scan of tile sums (one block), per-tile scan + carry.
+// ------------------------------------------------------------------------------------------------
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kBlock * kScanItems;
+
+template <typename T>
+__global__ void k_scan_tiles(const T* __restrict__ in, uint64_t n, unsigned long long* __restrict__ tileSum) {
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        if (i < n) s += (unsigned long long)in[i];
+    }
+    unsigned long long tot;
+    block_exclusive_scan(s, &tot);
+    if (threadIdx.x == 0) tileSum[blockIdx.x] = tot;
+}
+
+__global__ void k_scan_tile_sums(unsigned long long* __restrict__ tileSum, uint64_t nTiles) {
+    unsigned long long carry = 0;
+    for (uint64_t b = 0; b < nTiles; b += kBlock) {
+        uint64_t i = b + threadIdx.x;
+        unsigned long long x = i < nTiles ? tileSum[i] : 0ull;
+        unsigned long long tot;
+        unsigned long long ex = block_exclusive_scan(x, &tot);
+        if (i < nTiles) tileSum[i] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tileSum[nTiles] = carry;
+}
+
+template <typename T>
+__global__ void k_scan_apply(const T* __restrict__ in, uint64_t n, const unsigned long long* __restrict__ tileSum,
+                             uint64_t* __restrict__ out) {
+    // Thread-contiguous items so each tile is scanned in element order.
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    unsigned long long v[kScanItems];
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        uint64_t i = base + k;
+        v[k] = i < n ? (unsigned long long)in[i] : 0ull;
+        s += v[k];
+    }
+    unsigned long long tot;
+    unsigned long long run = block_exclusive_scan(s, &tot) + tileSum[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        uint64_t i = base + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = tileSum[gridDim.x];
+}
+
+template <typename T>
+static void scan_impl(const T* in, uint64_t n, uint64_t* out, unsigned long long* tmp, hipStream_t s) {
+    uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles == 0) {
+        hipMemsetAsync(out, 0, sizeof(uint64_t), s);
+        return;
+    }
+    k_scan_tiles<T><<<(unsigned)tiles, kBlock, 0, s>>>(in, n, tmp);
+    k_scan_tile_sums<<<1, kBlock, 0, s>>>(tmp, tiles);
+    k_scan_apply<T><<<(unsigned)tiles, kBlock, 0, s>>>(in, n, tmp, out);
+}
+
+uint64_t scan_tmp_elems(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+void exclusive_scan_u32(const uint32_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s) {
+    scan_impl<uint32_t>(in, n, out, (unsigned long long*)tmp, s);
+}
+void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s) {
+    scan_impl<uint64_t>(in, n, out, (unsigned long long*)tmp, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K0 read metadata: loadChunkOfReads (KmerExtractor.cpp:442-494). Per read: covered lengths,
+// windows per frame of each mate (0 when the read is dropped by the shared empty rule), reserved
+// slots = getQueryKmerNumber of both mates (one slot per frame window).
+// ------------------------------------------------------------------------------------------------
+__global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* __restrict__ off2, uint32_t n,
+                            int paired, ReadMeta* __restrict__ meta, uint64_t* __restrict__ reserve,
+                            uint32_t* __restrict__ qlen) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int len1 = (int)(off1[i + 1] - off1[i]);
+    int ql1 = max_covered_length(len1);
+    int w1 = ql1 / 3 - 7;  // getQueryKmerNumber / 6
+    int len2 = 0, ql2 = 0, w2 = 0;
+    bool empty = w1 < 1;
+    if (paired) {
+        len2 = (int)(off2[i + 1] - off2[i]);
+        ql2 = max_covered_length(len2);
+        w2 = ql2 / 3 - 7;
+        if (w2 < 1) empty = true;
+    }
+    ReadMeta m;
+    m.len1 = len1; m.len2 = len2; m.ql1 = ql1; m.ql2 = ql2;
+    m.w1 = empty ? 0 : w1;
+    m.w2 = (empty || !paired) ? 0 : w2;
+    meta[i] = m;
+    reserve[i] = 6ull * (uint64_t)(m.w1 + m.w2);
+    qlen[i] = (uint32_t)(ql1 + ql2);
+}
+
+void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
+                      uint64_t* reserve, uint32_t* qlen, hipStream_t s) {
+    if (n == 0) return;
+    k_read_meta<<<(n + 255) / 256, 256, 0, s>>>(off1, off2, n, paired, meta, reserve, qlen);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1 extract: one thread per (read, mate, frame) runs the frame's scanner over its codons and
+// writes one reserved slot per window (fillQueryKmerBuffer, KmerExtractor.cpp:355-386). A window
+// is emitted iff its 8 codons translate (the N-restart of MetamerScanner::next,
+// KmerScanner.h:82-117) and, with syncmers, its earliest-minimum s-mer sits at either end
+// (SyncmerScanner::next, SyncmerScanner.h:36-102). Blank windows get the sentinel key, which
+// the first radix pass drops.
+//
+// Load order j of a frame's codons: format 2 reads left to right (forward) or from the right end
+// on the complement (reverse); format 1 (OldMetamerScanner, KmerScanner.h:137-181) reads the
+// forward frame from the right end and the reverse frame from the left end, both with the first
+// loaded codon most significant.
+// ------------------------------------------------------------------------------------------------
+struct ExtractTables {
+    uint8_t base[256];
+    int8_t aa[64];
+    int8_t num[64];
+};
+
+__global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
+                                                 const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
+                                                 const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ slotOff,
+                                                 uint32_t nReads, int paired, ExtractTables tabs, int kmerFormat,
+                                                 int syncmer, int smerLen, uint64_t* __restrict__ keys,
+                                                 uint64_t* __restrict__ vals) {
+    __shared__ uint8_t sBase[256];
+    __shared__ int8_t sAA[64], sNum[64];
+    sBase[threadIdx.x] = tabs.base[threadIdx.x];
+    if (threadIdx.x < 64) { sAA[threadIdx.x] = tabs.aa[threadIdx.x]; sNum[threadIdx.x] = tabs.num[threadIdx.x]; }
+    __syncthreads();
+
+    const int perRead = paired ? 12 : 6;
+    uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (uint64_t)nReads * perRead) return;
+    uint32_t r = (uint32_t)(tid / perRead);
+    int sub = (int)(tid % perRead);
+    int mate = sub / 6, frame = sub % 6;
+    ReadMeta m = meta[r];
+    int W = mate ? m.w2 : m.w1;
+    if (W <= 0) return;
+    const uint8_t* seq = mate ? seq2 + off2[r] : seq1 + off1[r];
+    int len = mate ? m.len2 : m.len1;
+    int used = mate ? m.ql2 : m.ql1;
+    uint32_t posOffset = mate ? (uint32_t)m.ql1 + 3u : 0u;  // KmerExtractor.cpp:341-345
+    uint64_t slot = slotOff[r] + (mate ? 6ull * (uint64_t)m.w1 : 0ull) + (uint64_t)frame * (uint64_t)W;
+    const bool fwd = frame < 3;
+    int begin;
+    if (fwd) begin = frame;
+    else { begin = (len % 3) - (frame % 3); if (begin < 0) begin += 3; }
+    const int s0 = begin, e0 = begin + used - 1;
+    const int aaLen = used / 3;
+    const uint32_t seqId = r + 1;
+    // which end the load order starts from, and whether codons are complemented
+    const bool fromLeft = (kmerFormat == 2) ? fwd : !fwd;
+    const bool comp = !fwd;
+    const int nSm = 8 - smerLen + 1;
+
+    uint64_t aaAcc = 0, dnaAcc = 0, smAcc = 0;
+    uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
+    const uint64_t smMask = (smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1);
+    int run = 0;
+    for (int j = 0; j < aaLen; j++) {
+        int c0 = fromLeft ? s0 + 3 * j : e0 - 3 * j;  // first base of the triplet in load order
+        uint32_t b1, b2, b3;
+        if (fromLeft) {
+            uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + 1]], z = sBase[seq[c0 + 2]];
+            if (comp) { b1 = z; b2 = y; b3 = x; } else { b1 = x; b2 = y; b3 = z; }
+        } else {
+            uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 - 1]], z = sBase[seq[c0 - 2]];
+            if (comp) { b1 = x; b2 = y; b3 = z; } else { b1 = z; b2 = y; b3 = x; }
+        }
+        int aa = -1, num = 0;
+        if ((b1 | b2 | b3) < 4u) {
+            if (comp) { b1 ^= 2u; b2 ^= 2u; b3 ^= 2u; }
+            int idx = (int)(b1 << 4 | b2 << 2 | b3);
+            aa = sAA[idx];
+            num = sNum[idx];
+        }
+        if (aa < 0) {
+            run = 0;
+        } else {
+            run++;
+            aaAcc = (aaAcc << 5) | (uint64_t)aa;
+            dnaAcc = (dnaAcc << 3) | (uint64_t)num;
+            smAcc = ((smAcc << 5) | (uint64_t)aa) & smMask;
+        }
+        if (syncmer) {
+            sm7 = sm6; sm6 = sm5; sm5 = sm4; sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = sm0; sm0 = smAcc;
+        }
+        if (j < 7) continue;
+        const int p = j - 7;
+        bool ok = run >= 8;
+        if (ok && syncmer) {
+            // s-mers of the window: positions p..p+nSm-1 end at codons j-nSm+1..j = sm[nSm-1]..sm0.
+            // Earliest minimum: scan from the oldest (k = nSm-1) to the newest with strict <.
+            const uint64_t sv[8] = {sm0, sm1, sm2, sm3, sm4, sm5, sm6, sm7};
+            int bestK = -1;
+            uint64_t best = ~0ull;
+#pragma unroll
+            for (int k = 7; k >= 0; k--) {
+                if (k <= nSm - 1 && sv[k] < best) { best = sv[k]; bestK = k; }
+            }
+            ok = (bestK == nSm - 1) || (bestK == 0);
+        }
+        uint64_t key = kSentinel, info = 0;
+        if (ok) {
+            uint64_t aaPart;
+            if (kmerFormat == 2) {
+                aaPart = aaAcc & ((1ull << 40) - 1);
+            } else {
+                aaPart = 0;
+#pragma unroll
+                for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
+            }
+            key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
+            uint32_t pos;
+            if (fromLeft) pos = (uint32_t)(s0 + 3 * p);
+            else pos = (uint32_t)(e0 - 3 * (p + 8) + 1);
+            info = pack_info(seqId, pos + posOffset, (uint32_t)frame);
+        }
+        keys[slot + p] = key;
+        vals[slot + p] = info;
+    }
+}
+
+void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
+                    const ReadMeta* meta, const uint64_t* slotOff, uint32_t nReads, int paired, const HostTables& t,
+                    int kmerFormat, int syncmer, int smerLen, uint64_t* keys, uint64_t* vals, hipStream_t s) {
+    ExtractTables tabs;
+    for (int i = 0; i < 256; i++) tabs.base[i] = t.base[i];
+    for (int i = 0; i < 64; i++) { tabs.aa[i] = t.aa[i]; tabs.num[i] = t.num[i]; }
+    uint64_t threads = (uint64_t)nReads * (paired ? 12 : 6);
+    if (threads == 0) return;
+    k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, slotOff, nReads, paired,
+                                                                tabs, kmerFormat, syncmer, smerLen, keys, vals);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2 LSD radix sort of (key, val) pairs on 8-bit digits of the key. Per pass: tile histograms
+// (digit-major so one device scan yields stable global offsets), scan, stable scatter through an
+// LDS-staged tile so each digit run leaves the block as one contiguous write. The first pass
+// (FILTER) drops sentinel keys: the compaction of blank reserved slots costs nothing extra.
+// ------------------------------------------------------------------------------------------------
+constexpr int kRadixItems = 16;
+constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
+
+template <bool FILTER>
+__global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
+                                                    uint32_t* __restrict__ counts, uint32_t nTiles) {
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+#pragma unroll
+    for (int k = 0; k < kRadixItems; k++) {
+        uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        if (i < n) {
+            uint64_t key = keys[i];
+            if (!FILTER || key != kSentinel) atomicAdd(&hist[(key >> shift) & 0xFF], 1u);
+        }
+    }
+    __syncthreads();
+    counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
+}
+
+template <bool FILTER>
+__global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn,
+                                                       const uint64_t* __restrict__ valsIn, uint64_t n, int shift,
+                                                       const uint64_t* __restrict__ offs, uint32_t nTiles,
+                                                       uint64_t* __restrict__ keysOut, uint64_t* __restrict__ valsOut) {
+    __shared__ uint64_t sKey[kRadixTile];
+    __shared__ uint64_t sVal[kRadixTile];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t tileStart[256];
+    __shared__ uint32_t running[256];
+    __shared__ uint32_t waveCnt[kWaves][256];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+
+    uint64_t k[kRadixItems], v[kRadixItems];
+    uint32_t vmask = 0;  // bit r: item r is a real (kept) element
+    hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRadixItems; r++) {
+        uint64_t i = base + (uint64_t)r * kBlock + tid;
+        k[r] = 0;
+        v[r] = 0;
+        if (i < n) {
+            k[r] = keysIn[i];
+            v[r] = valsIn[i];
+            if (!FILTER || k[r] != kSentinel) {
+                vmask |= 1u << r;
+                atomicAdd(&hist[(k[r] >> shift) & 0xFF], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    unsigned long long tot;
+    unsigned long long ex = block_exclusive_scan(hist[tid], &tot);
+    tileStart[tid] = (uint32_t)ex;
+    running[tid] = 0;
+    __syncthreads();
+
+    const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < kRadixItems; r++) {
+        const bool valid = (vmask >> r) & 1u;
+        const uint32_t d = (uint32_t)((k[r] >> shift) & 0xFF);
+        // lanes of this wave holding the same digit (match-any by 8 ballots)
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            unsigned long long m = __ballot(valid && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        for (int x = tid; x < kWaves * 256; x += kBlock) (&waveCnt[0][0])[x] = 0;
+        __syncthreads();
+        const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
+        if (valid && rankInWave == 0) waveCnt[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        {
+            uint32_t s = running[tid];
+#pragma unroll
+            for (int ww = 0; ww < kWaves; ww++) {
+                uint32_t c = waveCnt[ww][tid];
+                waveCnt[ww][tid] = s;
+                s += c;
+            }
+            running[tid] = s;
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = tileStart[d] + waveCnt[w][d] + rankInWave;
+            sKey[pos] = k[r];
+            sVal[pos] = v[r];
+        }
+        __syncthreads();
+    }
+    const uint32_t cnt = (uint32_t)tot;
+    for (uint32_t i = tid; i < cnt; i += kBlock) {
+        uint64_t key = sKey[i];
+        uint32_t d = (uint32_t)((key >> shift) & 0xFF);
+        uint64_t dst = offs[(uint64_t)d * nTiles + blockIdx.x] + (i - tileStart[d]);
+        keysOut[dst] = key;
+        valsOut[dst] = sVal[i];
+    }
+}
+
+uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) / kRadixTile) + 1; }
+
+// Sorts n pairs by key bits [bitLo, bitHi). Returns the kept count (sentinels dropped when
+// filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
+// *inB tells which.
+uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
+                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+                          hipStream_t s) {
+    uint64_t cur = n;
+    uint64_t *ki = keysA, *vi = valsA, *ko = keysB, *vo = valsB;
+    bool first = true;
+    *inB = false;
+    for (int shift = bitLo; shift < bitHi; shift += 8) {
+        uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
+        if (nTiles == 0) break;
+        if (first && filter) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
+        if (first && filter) {
+            k_radix_scatter<true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+            uint64_t kept = 0;
+            hipMemcpyAsync(&kept, offs + 256ull * nTiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+            hipStreamSynchronize(s);
+            cur = kept;
+        } else {
+            k_radix_scatter<false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        }
+        first = false;
+        std::swap(ki, ko);
+        std::swap(vi, vo);
+        *inB = !*inB;
+    }
+    return cur;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->
+// k-mer index by scan -> per-k-mer delta from its <= 5 15-bit groups -> values by 64-bit scan.
+// ------------------------------------------------------------------------------------------------
+__global__ void k_term_flags(const uint16_t* __restrict__ diff, uint64_t n, uint32_t* __restrict__ flag) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (diff[i] & 0x8000u) ? 1u : 0u;
+}
+
+__global__ void k_deltas(const uint16_t* __restrict__ diff, uint64_t n, const uint64_t* __restrict__ termIdx,
+                         uint64_t* __restrict__ delta) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !(diff[i] & 0x8000u)) return;
+    uint64_t d = diff[i] & 0x7FFFu;
+    int sh = 15;
+    for (uint64_t j = i; j > 0; j--) {
+        uint16_t w = diff[j - 1];
+        if (w & 0x8000u) break;
+        d |= (uint64_t)w << sh;
+        sh += 15;
+    }
+    delta[termIdx[i]] = d;
+}
+
+void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
+                     uint64_t* idxTmp, void* scanTmp, hipStream_t s) {
+    if (nDiff == 0) return;
+    k_term_flags<<<(unsigned)((nDiff + 255) / 256), 256, 0, s>>>(diff, nDiff, flagTmp);
+    exclusive_scan_u32(flagTmp, nDiff, idxTmp, scanTmp, s);
+    k_deltas<<<(unsigned)((nDiff + 255) / 256), 256, 0, s>>>(diff, nDiff, idxTmp, values);
+    // inclusive scan of deltas = exclusive scan shifted by one: scan into idxTmp then take [1..]
+    exclusive_scan_u64(values, nKmers, idxTmp, scanTmp, s);
+    hipMemcpyAsync(values, idxTmp + 1, nKmers * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K4 merge-match (KmerMatcher::matchKmers, KmerMatcher.cpp:275-450; compareDna :1117-1146).
+// Queries are sorted by their AA part. Each wave brackets the DB range of its 64 queries with two
+// binary searches, then each lane finds its own AA run inside that window. Candidates are the
+// whole run except the DB's last k-mer (the reference's reader stops at diffIdxPos ==
+// numOfDiffIdx before loading it, KmerMatcher.cpp:363,378). Selected = hamming sum <=
+// min(2*min, 7). COUNT pass: per-read match counts. EMIT pass: records into per-read segments.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* __restrict__ a, uint64_t lo, uint64_t hi,
+                                                    uint64_t key) {
+    while (lo < hi) {
+        uint64_t mid = lo + ((hi - lo) >> 1);
+        if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
+                                               uint64_t Q, const uint64_t* __restrict__ dbv,
+                                               const uint32_t* __restrict__ dbinfo, uint64_t D,
+                                               const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                               uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
+                                               mtb_match* __restrict__ out, int* __restrict__ err) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint64_t waveBase = gid - lane;
+    if (waveBase >= Q) return;
+    const uint64_t lastIdx = min(waveBase + 63, Q - 1);
+    // Wave window: [lower_bound(AA(first)), lower_bound(AA(last) + 2^24))
+    uint64_t winLo = 0, winHi = 0;
+    if (lane == 0) winLo = lower_bound_u64(dbv, 0, D, qkey[waveBase] & kAAMask);
+    if (lane == 1) winHi = lower_bound_u64(dbv, 0, D, (qkey[lastIdx] & kAAMask) + (1ull << 24));
+    winLo = __shfl(winLo, 0, 64);
+    winHi = __shfl(winHi, 1, 64);
+    if (gid >= Q) return;
+    const uint64_t key = qkey[gid];
+    const uint64_t aa = key & kAAMask;
+    uint64_t lo = lower_bound_u64(dbv, winLo, winHi, aa);
+    uint64_t hi = lower_bound_u64(dbv, lo, winHi, aa + (1ull << 24));
+    if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
+    if (lo >= hi) return;
+    uint32_t minSum = 255;
+    for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, dbv[t]));
+    const uint32_t thr = min(minSum * 2u, 7u);
+    const uint64_t info = qinfo[gid];
+    const uint32_t seq = info_seq(info);
+    if (!EMIT) {
+        uint32_t c = 0;
+        for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
+        if (c) atomicAdd(&readCnt[seq - 1], c);
+        return;
+    }
+    uint32_t c = 0;
+    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
+    uint64_t w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
+    const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
+    for (uint64_t t = lo; t < hi; t++) {
+        uint64_t tv = dbv[t];
+        uint32_t hs = hamming_sum(key, tv);
+        if (hs > thr) continue;
+        uint32_t tax = dbinfo[t];
+        int32_t sp = tax <= maxTax ? spOf[tax] : 0;
+        if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
+        mtb_match m;
+        m.qinfo = info;
+        m.target_id = tax;
+        m.species_id = (uint32_t)sp;
+        m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
+        m.right_end_hamming = (uint16_t)hammings(key, tv, rev);
+        m.hamming = (uint8_t)hs;
+        m.pad = 0;
+        out[w++] = m;
+    }
+}
+
+void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
+                  const uint32_t* dbinfo, uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
+                  uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err, hipStream_t s) {
+    if (Q == 0 || D < 2) return;
+    unsigned blocks = (unsigned)((Q + 255) / 256);
+    if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, spOf, maxTax, kmerFormat, readCnt,
+                                                   readOff, out, err);
+    else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, spOf, maxTax, kmerFormat, readCnt,
+                                               readOff, out, err);
+}
+
+__global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) info[i] &= mask;
+}
+
+void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s) {
+    if (n) k_mask_info<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(info, n, mask);
+}
+
+}  // namespace mtb

@@ -1,0 +1,83 @@
+// Internal interface between the C-ABI orchestration (mtb_api.hip) and the kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "mtb_device.h"
+
+namespace mtb {
+
+struct ReadMeta {  // per read: raw lengths, covered lengths, windows per frame of each mate
+    int32_t len1, len2, ql1, ql2, w1, w2;
+};
+
+struct HostTables {  // restated genetic code (mtb_host.cpp)
+    uint8_t base[256];
+    int8_t aa[64];
+    int8_t num[64];
+};
+
+struct TaxDevice {
+    const int32_t* nodeOf;
+    const int32_t* nodeTax;
+    const int32_t* parent;
+    const int32_t* depth;
+    const uint8_t* flags;
+    const int32_t* spParent;
+    int32_t maxTax;
+};
+
+struct AssignArgs {
+    int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
+    float minScore, minSpScore, tieRatio;
+};
+
+struct AssignScratch {
+    void* local;
+    void* paths;
+    void* comb;
+    uint8_t* conn;
+    float* spScore;
+    int32_t* spId;
+    void* quot;
+    void* clade;
+    uint32_t cladePerMatch;
+};
+
+// scans (out has n+1 entries; tmp needs scan_tmp_elems(n) u64)
+uint64_t scan_tmp_elems(uint64_t n);
+void exclusive_scan_u32(const uint32_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
+void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
+
+void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
+                      uint64_t* reserve, uint32_t* qlen, hipStream_t s);
+void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
+                    const ReadMeta* meta, const uint64_t* slotOff, uint32_t nReads, int paired, const HostTables& t,
+                    int kmerFormat, int syncmer, int smerLen, uint64_t* keys, uint64_t* vals, hipStream_t s);
+
+uint64_t radix_counts_elems(uint64_t n);
+uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
+                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+                          hipStream_t s);
+
+void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
+                     uint64_t* idxTmp, void* scanTmp, hipStream_t s);
+void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s);
+
+void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
+                  const uint32_t* dbinfo, uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
+                  uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err, hipStream_t s);
+
+uint64_t path_bytes();
+uint64_t quot_bytes();
+uint64_t clade_bytes();
+void launch_assign(mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
+                   uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st);
+void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
+void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
+                           uint32_t nReads, mtb_taxcnt* out, hipStream_t s);
+
+}  // namespace mtb

@@ -1,0 +1,253 @@
+"""Synthetic inputs for tests and the benchmark (SURVEY.md §8(d) "Synthetic inputs").
+
+There is no network, so the reference genomes, taxonomy and read sets are generated here from
+fixed seeds:
+
+* a taxonomy tree in NCBI dmp form (root 1 -> superkingdom -> ... -> genus -> species -> strain);
+* genomes: one random base genome per species, strains as substituted copies of it;
+* gene blocks: contiguous segments with a random strand, the analogue of the Prodigal ORFs the
+  reference's DB builder extracts target k-mers from (IndexCreator.cpp:1087-1240);
+* reads: fragments sampled from the genomes (paired 150 bp, or ONT-like long reads) with
+  substitutions, a share of random reads, and sprinkled N / IUPAC / lower-case characters.
+
+Everything is numpy and deterministic in its seed.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import List, Optional
+
+import numpy as np
+
+_BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+_COMP = np.zeros(256, dtype=np.uint8)
+for _a, _b in zip(b"ACGTNacgtn", b"TGCANtgcan"):
+    _COMP[_a] = _b
+
+
+@dataclasses.dataclass
+class Taxonomy:
+    taxid: np.ndarray      # int32, nodes.dmp row order (root first)
+    parent: np.ndarray     # int32
+    rank: List[str]
+    name: List[str]
+
+    def write_dmp(self, directory: str) -> None:
+        os.makedirs(directory, exist_ok=True)
+        with open(os.path.join(directory, "nodes.dmp"), "w") as f:
+            for t, p, r in zip(self.taxid.tolist(), self.parent.tolist(), self.rank):
+                f.write(f"{t}\t|\t{p}\t|\t{r}\t|\t\t|\n")
+        with open(os.path.join(directory, "names.dmp"), "w") as f:
+            for t, n in zip(self.taxid.tolist(), self.name):
+                f.write(f"{t}\t|\t{n}\t|\t\t|\tscientific name\t|\n")
+        with open(os.path.join(directory, "merged.dmp"), "w") as f:
+            pass
+
+
+@dataclasses.dataclass
+class Genomes:
+    seq: np.ndarray        # uint8, concatenated
+    off: np.ndarray        # uint64, n+1
+    taxid: np.ndarray      # int32 per genome (strain or species node)
+    species: np.ndarray    # int32 species taxID per genome
+    blk_genome: np.ndarray  # int32 gene blocks
+    blk_start: np.ndarray
+    blk_end: np.ndarray
+    blk_strand: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return len(self.off) - 1
+
+
+@dataclasses.dataclass
+class Reads:
+    seq1: np.ndarray
+    off1: np.ndarray
+    seq2: Optional[np.ndarray]
+    off2: Optional[np.ndarray]
+    origin: np.ndarray     # int32 genome index per read, -1 for random reads
+
+    @property
+    def n(self) -> int:
+        return len(self.off1) - 1
+
+    def names(self) -> List[str]:
+        return [f"read{i}" for i in range(self.n)]
+
+
+def make_taxonomy(n_species: int, strains_per_species: int, seed: int = 1, n_genera: Optional[int] = None,
+                  with_eukaryota: bool = True) -> Taxonomy:
+    """Root 1 -> {Bacteria, Eukaryota} -> phylum -> class -> order -> family -> genus -> species
+    -> strain ("no rank"). Species are spread over genera; the last 1/8 of the genera sit under
+    Eukaryota so that the minConsCntEuk branch (Taxonomer.cpp:497-500) is exercised."""
+    rng = np.random.default_rng(seed)
+    n_genera = n_genera or max(1, n_species // 3)
+    tax, par, rank, name = [1], [1], ["no rank"], ["root"]
+    nxt = [2]
+
+    def add(p: int, r: str, nm: Optional[str] = None) -> int:
+        t = nxt[0]
+        nxt[0] += 1
+        tax.append(t); par.append(p); rank.append(r); name.append(nm or f"{r}_{t}")
+        return t
+
+    bact = add(1, "superkingdom", "Bacteria")
+    euk = add(1, "superkingdom", "Eukaryota") if with_eukaryota else bact
+    genera = []
+    n_euk = n_genera // 8 if with_eukaryota else 0
+    for g in range(n_genera):
+        dom = euk if g >= n_genera - n_euk else bact
+        p = add(dom, "phylum")
+        c = add(p, "class")
+        o = add(c, "order")
+        fam = add(o, "family")
+        genera.append(add(fam, "genus"))
+    for s in range(n_species):
+        g = genera[int(rng.integers(0, n_genera))] if s >= n_genera else genera[s]
+        sp = add(g, "species")
+        for _ in range(strains_per_species):
+            add(sp, "no rank")
+    return Taxonomy(np.array(tax, np.int32), np.array(par, np.int32), rank, name)
+
+
+def _random_dna(rng, n: int, gc: float = 0.5) -> np.ndarray:
+    p = np.array([(1 - gc) / 2, gc / 2, gc / 2, (1 - gc) / 2])
+    return _BASES[rng.choice(4, size=n, p=p)]
+
+
+def _mutate(rng, s: np.ndarray, rate: float) -> np.ndarray:
+    out = s.copy()
+    m = rng.random(len(s)) < rate
+    k = int(m.sum())
+    if k:
+        shift = rng.integers(1, 4, size=k)
+        idx = np.searchsorted(_BASES, out[m])
+        idx = np.where(_BASES[np.clip(idx, 0, 3)] == out[m], idx, 0)
+        out[m] = _BASES[(idx + shift) % 4]
+    return out
+
+
+def make_genomes(taxo: Taxonomy, genome_len: int = 20000, strain_div: float = 0.02, seed: int = 1,
+                 len_jitter: float = 0.3, min_block: int = 300, max_block: int = 3000) -> Genomes:
+    """One genome per strain node (or per species when the species has no strain child)."""
+    rng = np.random.default_rng(seed)
+    rank = np.array(taxo.rank)
+    species_ids = taxo.taxid[rank == "species"]
+    children = {}
+    for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank):
+        if r == "no rank" and t != 1:
+            children.setdefault(p, []).append(t)
+    seqs, taxids, species = [], [], []
+    for sp in species_ids.tolist():
+        L = max(600, int(genome_len * (1 + len_jitter * (rng.random() * 2 - 1))))
+        base = _random_dna(rng, L, gc=float(rng.uniform(0.35, 0.65)))
+        kids = children.get(sp, [])
+        if not kids:
+            seqs.append(base); taxids.append(sp); species.append(sp)
+        for k in kids:
+            seqs.append(_mutate(rng, base, strain_div)); taxids.append(k); species.append(sp)
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    bg, bs, be, bst = [], [], [], []
+    for gi, s in enumerate(seqs):
+        pos = int(rng.integers(0, 50))
+        L = len(s)
+        while pos + min_block < L:
+            ln = int(rng.integers(min_block, max_block))
+            end = min(L - 1, pos + ln - 1)
+            bg.append(gi); bs.append(pos); be.append(end); bst.append(1 if rng.random() < 0.5 else -1)
+            pos = end + 1 + int(rng.integers(0, 60))
+    return Genomes(np.concatenate(seqs), off, np.array(taxids, np.int32), np.array(species, np.int32),
+                   np.array(bg, np.int32), np.array(bs, np.int32), np.array(be, np.int32), np.array(bst, np.int32))
+
+
+def _revcomp(s: np.ndarray) -> np.ndarray:
+    return _COMP[s[::-1]]
+
+
+def _sprinkle(rng, s: np.ndarray, rate_n: float, rate_iupac: float, rate_lower: float) -> np.ndarray:
+    if rate_n > 0:
+        s[rng.random(len(s)) < rate_n] = ord("N")
+    if rate_iupac > 0:
+        m = rng.random(len(s)) < rate_iupac
+        s[m] = np.frombuffer(b"RYKMSWBDHVU", np.uint8)[rng.integers(0, 11, int(m.sum()))]
+    if rate_lower > 0:
+        m = (rng.random(len(s)) < rate_lower) & (s >= 65) & (s <= 90)
+        s[m] = s[m] + 32
+    return s
+
+
+def _pack(reads: List[np.ndarray]):
+    off = np.zeros(len(reads) + 1, np.uint64)
+    off[1:] = np.cumsum([len(r) for r in reads])
+    seq = np.concatenate(reads) if reads else np.zeros(0, np.uint8)
+    return seq.astype(np.uint8), off
+
+
+def make_reads(gen: Genomes, n_reads: int, paired: bool = True, read_len: int = 150, insert: int = 300,
+               insert_sd: int = 30, sub_rate: float = 0.005, random_frac: float = 0.1, seed: int = 2,
+               rate_n: float = 0.0005, rate_iupac: float = 0.0002, rate_lower: float = 0.0005,
+               short_frac: float = 0.0) -> Reads:
+    """Illumina-style reads. short_frac of the reads get a mate shorter than one k-mer window so
+    the shared empty-read rule (KmerExtractor.cpp:451-494) is exercised."""
+    rng = np.random.default_rng(seed)
+    lens = np.diff(gen.off).astype(np.int64)
+    w = lens / lens.sum()
+    r1, r2, origin = [], [], np.full(n_reads, -1, np.int32)
+    for i in range(n_reads):
+        if rng.random() < random_frac:
+            a = _random_dna(rng, read_len)
+            b = _random_dna(rng, read_len)
+        else:
+            g = int(rng.choice(len(lens), p=w))
+            origin[i] = g
+            G = gen.seq[int(gen.off[g]):int(gen.off[g + 1])]
+            frag = int(max(read_len, min(len(G), rng.normal(insert, insert_sd))))
+            st = int(rng.integers(0, max(1, len(G) - frag + 1)))
+            f = G[st:st + frag]
+            if rng.random() < 0.5:
+                f = _revcomp(f)
+            a = _mutate(rng, f[:read_len], sub_rate)
+            b = _mutate(rng, _revcomp(f)[:read_len], sub_rate)
+        if short_frac > 0 and rng.random() < short_frac:
+            cut = int(rng.integers(5, 26))
+            if rng.random() < 0.5:
+                a = a[:cut]
+            else:
+                b = b[:cut]
+        r1.append(_sprinkle(rng, a.copy(), rate_n, rate_iupac, rate_lower))
+        r2.append(_sprinkle(rng, b.copy(), rate_n, rate_iupac, rate_lower))
+    s1, o1 = _pack(r1)
+    if paired:
+        s2, o2 = _pack(r2)
+        return Reads(s1, o1, s2, o2, origin)
+    return Reads(s1, o1, None, None, origin)
+
+
+def make_long_reads(gen: Genomes, n_reads: int, n50: int = 10000, min_len: int = 1000, sub_rate: float = 0.05,
+                    indel_rate: float = 0.01, seed: int = 7) -> Reads:
+    """ONT-like single-end reads: lognormal lengths, substitutions and indels."""
+    rng = np.random.default_rng(seed)
+    lens = np.diff(gen.off).astype(np.int64)
+    w = lens / lens.sum()
+    out, origin = [], np.zeros(n_reads, np.int32)
+    for i in range(n_reads):
+        g = int(rng.choice(len(lens), p=w))
+        origin[i] = g
+        G = gen.seq[int(gen.off[g]):int(gen.off[g + 1])]
+        L = int(min(len(G), max(min_len, rng.lognormal(np.log(n50 * 0.8), 0.5))))
+        st = int(rng.integers(0, max(1, len(G) - L + 1)))
+        f = G[st:st + L]
+        if rng.random() < 0.5:
+            f = _revcomp(f)
+        f = _mutate(rng, f, sub_rate)
+        if indel_rate > 0:
+            keep = rng.random(len(f)) >= indel_rate / 2
+            f = f[keep]
+            ins = rng.random(len(f)) < indel_rate / 2
+            f = np.insert(f, np.nonzero(ins)[0], _BASES[rng.integers(0, 4, int(ins.sum()))])
+        out.append(f.astype(np.uint8))
+    s, o = _pack(out)
+    return Reads(s, o, None, None, origin)

@@ -1,0 +1,73 @@
+// ORACLE — test infrastructure only (see orc_core.h header).
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "orc_core.h"
+#include "orc_taxonomy.h"
+
+namespace orc {
+
+struct DiffIdxSplit {  // Kmer.h:111-119
+    uint64_t ADkmer;
+    uint64_t diffIdxOffset;
+    uint64_t infoIdxOffset;
+};
+
+// A reference DB held in memory: the on-disk files of SURVEY Appendix B plus the loaded taxonomy
+// and the taxId2speciesId map built by KmerMatcher::loadTaxIdList (KmerMatcher.cpp:56-120).
+struct Db {
+    std::vector<uint16_t> diffIdx;
+    std::vector<uint32_t> info;
+    std::vector<DiffIdxSplit> split;
+    std::vector<TaxID> taxIdList;
+    Taxonomy tax;
+    std::unordered_map<TaxID, TaxID> taxId2speciesId;
+    bool buildSpeciesMap(std::string* err);
+};
+
+// Query (common.h:95-128), restricted to the fields the path writes.
+struct Query {
+    int queryLength = 0, queryLength2 = 0, kmerCnt = 0, kmerCnt2 = 0;
+    int classification = 0;
+    float score = 0;
+    int hammingDist = 0;
+    bool isClassified = false;
+    bool newSpecies = false;
+    std::map<TaxID, int> taxCnt;
+};
+
+struct Reads {
+    const char* seq1; const uint64_t* off1;
+    const char* seq2; const uint64_t* off2;
+    uint32_t n;
+};
+
+// KmerExtractor::extractQueryKmers (KmerExtractor.cpp:52-81): fills the reserved buffer exactly as
+// the reference does (unused reserved slots stay {0,0}) and sorts it by compareQueryKmer.
+void extractQueryKmers(const mtb_params& par, const Reads& reads, std::vector<mtb_kmer>& buf,
+                       std::vector<Query>& queries, bool sort);
+
+// KmerMatcher::matchKmers (KmerMatcher.cpp:123-481) over in-memory files.
+bool matchKmers(const Db& db, const mtb_params& par, const mtb_kmer* kmers, size_t nKmers,
+                std::vector<mtb_match>& matches, std::string* err);
+void sortMatches(std::vector<mtb_match>& matches);  // KmerMatcher.cpp:1071-1078
+bool compareMatches(const mtb_match& a, const mtb_match& b);
+
+// Classifier::assignTaxonomy (Classifier.cpp:166-208) with Taxonomer::chooseBestTaxon.
+void assignTaxonomy(const Db& db, const mtb_params& par, const mtb_match* matches, size_t n,
+                    std::vector<Query>& queries);
+
+// Synthetic reference DB writer (IndexCreator restatement, orc_dbwriter.cpp).
+struct BuildInput {
+    const char* seq; const uint64_t* off; uint32_t nGenomes; const int32_t* genomeTaxId;
+    const int32_t* blkGenome; const int32_t* blkStart; const int32_t* blkEnd; const int32_t* blkStrand; uint64_t nBlocks;
+    int splitNum;
+};
+bool buildDb(const mtb_params& par, const Taxonomy& tax, const BuildInput& in, Db& db, std::string* err);
+bool writeDbFiles(const Db& db, const mtb_params& par, const std::string& dir, std::string* err);
+
+}  // namespace orc

@@ -1,0 +1,411 @@
+// ORACLE — test infrastructure only (see orc_core.h header).
+// Classifier::assignTaxonomy (Classifier.cpp:166-208) and Taxonomer (Taxonomer.cpp:12-713,
+// Taxonomer.h:15-59), Match score helpers (Match.h:32-86).
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+#include "orc_internal.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace orc {
+
+static inline int get2(uint32_t x) { return (int)(x & 3u); }
+
+// Match::getScore / getRightPartScore / getLeftPartScore / *HammingDist (Match.h:32-86)
+static float matchScore(const mtb_match& m) {
+    float score = 0.0f;
+    for (int cnt = 0; cnt < 8; cnt++) {
+        int h = get2(m.right_end_hamming >> (cnt * 2));
+        score += (h == 0) ? 3.0f : 2.0f - 0.5f * h;
+    }
+    return score;
+}
+static float rightPartScore(const mtb_match& m, int range) {
+    float score = 0.0f;
+    for (int cnt = 0; cnt < range; cnt++) {
+        int h = get2(m.right_end_hamming >> (cnt * 2));
+        score += (h == 0) ? 3.0f : 2.0f - 0.5f * h;
+    }
+    return score;
+}
+static float leftPartScore(const mtb_match& m, int range) {
+    float score = 0.0f;
+    for (int cnt = 0; cnt < range; cnt++) {
+        int h = get2(m.right_end_hamming >> (14 - cnt * 2));
+        score += (h == 0) ? 3.0f : 2.0f - 0.5f * h;
+    }
+    return score;
+}
+static int rightPartHamming(const mtb_match& m, int range) {
+    int s = 0;
+    for (int i = 0; i < range; i++) s += get2(m.right_end_hamming >> (i * 2));
+    return s;
+}
+static int leftPartHamming(const mtb_match& m, int range) {
+    int s = 0;
+    for (int i = 0; i < range; i++) s += get2(m.right_end_hamming >> (14 - i * 2));
+    return s;
+}
+
+struct TaxonScore {
+    TaxID taxId = 0;
+    float score = 0.0f;
+    int hammingDist = 0;
+    bool LCA = false;
+};
+
+struct MatchPath {  // Taxonomer.h:35-59
+    int start = 0, end = 0;
+    float score = 0.f;
+    int hammingDist = 0, depth = 0;
+    const mtb_match* startMatch = nullptr;
+    const mtb_match* endMatch = nullptr;
+    MatchPath() {}
+    explicit MatchPath(const mtb_match* m)
+        : start((int)infoPos(m->qinfo)), end((int)infoPos(m->qinfo) + 23), score(matchScore(*m)),
+          hammingDist(m->hamming), depth(1), startMatch(m), endMatch(m) {}
+};
+
+class Taxonomer {
+public:
+    Taxonomer(const Db& db, const mtb_params& par) : db(db), par(par), tax(db.tax) {
+        minConsCnt = par.min_cons_cnt;
+        minConsCntEuk = par.min_cons_cnt_euk;
+        eukaryotaTaxId = tax.eukaryotaTaxID;
+        tieRatio = par.tie_ratio;
+        accessionLevel = par.accession_level;
+        kmerFormat = par.kmer_format;
+        if (par.syncmer) { dnaShift = (8 - par.smer_len) * 3; maxCodonShift = 8 - par.smer_len; }
+        else { dnaShift = 3; maxCodonShift = 1; }
+        denominator = (par.seq_mode == 1 || par.seq_mode == 2) ? 100 : 1000;
+        bitsPerCodon = 3; totalDnaBits = 24;
+    }
+
+    void chooseBestTaxon(uint32_t currentQuery, size_t offset, size_t end, const mtb_match* matchList,
+                         std::vector<Query>& queryList);
+
+private:
+    const Db& db;
+    const mtb_params& par;
+    const Taxonomy& tax;
+    int minConsCnt, minConsCntEuk, eukaryotaTaxId, accessionLevel, kmerFormat;
+    float tieRatio;
+    int dnaShift, maxCodonShift, denominator, bitsPerCodon, totalDnaBits;
+    std::vector<MatchPath> matchPaths, combinedMatchPaths, localMatchPaths;
+    std::vector<bool> connectedToNext;
+    std::vector<TaxID> maxSpecies;
+    std::unordered_map<TaxID, unsigned int> taxCnt;
+    std::unordered_map<TaxID, TaxonCounts> cladeCnt;
+    std::vector<const mtb_match*> bestMatchForQuotient;
+    std::vector<TaxID> bestMatchTaxIdForQuotient;
+    std::vector<uint8_t> minHammingForQuotient;
+
+    TaxonScore getBestSpeciesMatches(std::pair<size_t, size_t>& range, const mtb_match* ml, size_t end,
+                                     size_t offset, Query& q);
+    float combineMatchPaths(size_t pathStart, size_t combStart, int readLength);
+    void trimMatchPath(MatchPath& p1, const MatchPath& p2, int overlap);
+    void getMatchPaths(const mtb_match* ml, size_t start, size_t end, TaxID speciesId);
+    void filterRedundantMatches(const mtb_match* ml, const std::pair<size_t, size_t>& range, int queryLength);
+    TaxID lowerRankClassification(TaxID spTaxId, int queryLength);
+    void getSpeciesCladeCounts(TaxID speciesTaxID);
+    TaxID BFS(TaxID root, unsigned int maxCnt);
+
+    float calScoreIncrement(uint16_t h, int shift) const {
+        float inc = 0;
+        for (int i = 0; i < shift; i++) {
+            uint8_t x = (h >> (i * 2)) & 3;
+            inc += (x == 0) ? 3.0f : 2.0f - 0.5f * x;
+        }
+        return inc;
+    }
+    int calHammingDistIncrement(uint16_t h, int shift) const {
+        int inc = 0;
+        for (int i = 0; i < shift; i++) inc += (h >> (i * 2)) & 3;
+        return inc;
+    }
+    bool isConsecutive(const mtb_match* a, const mtb_match* b, int shift) const {  // Taxonomer.cpp:677-683
+        return (a->dna_encoding >> (bitsPerCodon * shift)) ==
+               (b->dna_encoding & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1));
+    }
+    bool isConsecutive2(const mtb_match* a, const mtb_match* b, int shift) const {  // :692-699
+        return (a->dna_encoding & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1)) ==
+               (b->dna_encoding >> (bitsPerCodon * shift));
+    }
+};
+
+void Taxonomer::chooseBestTaxon(uint32_t currentQuery, size_t offset, size_t end, const mtb_match* matchList,
+                                std::vector<Query>& queryList) {
+    Query& q = queryList[currentQuery];
+    std::pair<size_t, size_t> bestSpeciesRange(0, 0);
+    TaxonScore speciesScore = getBestSpeciesMatches(bestSpeciesRange, matchList, end, offset, q);
+    if (speciesScore.score == 0 || speciesScore.score < par.min_score) {
+        q.isClassified = false; q.classification = 0; q.score = speciesScore.score;
+        q.hammingDist = speciesScore.hammingDist; q.newSpecies = false;
+        return;
+    }
+    if (speciesScore.LCA) {
+        q.isClassified = true; q.classification = speciesScore.taxId; q.score = speciesScore.score;
+        q.hammingDist = speciesScore.hammingDist;
+        return;
+    }
+    taxCnt.clear();
+    filterRedundantMatches(matchList, bestSpeciesRange, q.queryLength + q.queryLength2);
+    for (auto& t : taxCnt) q.taxCnt[t.first] = (int)t.second;
+    if (speciesScore.score < par.min_sp_score) {
+        q.isClassified = true;
+        q.classification = tax.taxonNode(tax.getTaxIdAtRank(speciesScore.taxId, "species"))->parentTaxId;
+        q.score = speciesScore.score; q.hammingDist = speciesScore.hammingDist;
+        return;
+    }
+    q.isClassified = true; q.score = speciesScore.score; q.hammingDist = speciesScore.hammingDist;
+    q.newSpecies = false;
+    q.classification = lowerRankClassification(speciesScore.taxId, q.queryLength + q.queryLength2);
+}
+
+void Taxonomer::filterRedundantMatches(const mtb_match* ml, const std::pair<size_t, size_t>& range,
+                                       int queryLength) {  // Taxonomer.cpp:205-241
+    size_t maxQuotient = (size_t)((queryLength + 3) / dnaShift);
+    bestMatchForQuotient.assign(maxQuotient + 1, nullptr);
+    bestMatchTaxIdForQuotient.assign(maxQuotient + 1, 0);
+    minHammingForQuotient.assign(maxQuotient + 1, std::numeric_limits<uint8_t>::max());
+    for (size_t i = range.first; i < range.second; i++) {
+        size_t qt = infoPos(ml[i].qinfo) / (uint32_t)dnaShift;
+        uint8_t h = ml[i].hamming;
+        if (bestMatchForQuotient[qt] == nullptr) {
+            bestMatchForQuotient[qt] = ml + i; bestMatchTaxIdForQuotient[qt] = (TaxID)ml[i].target_id;
+            minHammingForQuotient[qt] = h;
+        } else if (h < minHammingForQuotient[qt]) {
+            bestMatchForQuotient[qt] = ml + i; bestMatchTaxIdForQuotient[qt] = (TaxID)ml[i].target_id;
+            minHammingForQuotient[qt] = h;
+        } else if (h == minHammingForQuotient[qt]) {
+            bestMatchTaxIdForQuotient[qt] = tax.LCA(bestMatchTaxIdForQuotient[qt], (TaxID)ml[i].target_id);
+        }
+    }
+    for (size_t i = 0; i <= maxQuotient; ++i)
+        if (bestMatchForQuotient[i] != nullptr) taxCnt[bestMatchTaxIdForQuotient[i]]++;
+}
+
+TaxID Taxonomer::lowerRankClassification(TaxID spTaxId, int queryLength) {  // :252-271
+    unsigned int minSubSpeciesMatch = (unsigned int)((queryLength - 1) / denominator);
+    cladeCnt.clear();
+    getSpeciesCladeCounts(spTaxId);
+    if (accessionLevel == 2) {
+        std::vector<TaxID> keys;
+        for (auto& kv : cladeCnt) keys.push_back(kv.first);
+        for (TaxID k : keys) {
+            const TaxonNode* taxon = tax.taxonNode(k);
+            if (taxon->rank == "" || taxon->rank == "accession") {
+                auto& ch = cladeCnt[taxon->parentTaxId].children;
+                ch.erase(std::find(ch.begin(), ch.end(), k));
+            }
+        }
+    }
+    return BFS(spTaxId, minSubSpeciesMatch);
+}
+
+void Taxonomer::getSpeciesCladeCounts(TaxID speciesTaxID) {  // :273-290
+    for (auto it = taxCnt.begin(); it != taxCnt.end(); ++it) {
+        const TaxonNode* taxon = tax.taxonNode(it->first);
+        cladeCnt[taxon->taxId].taxCount = it->second;
+        cladeCnt[taxon->taxId].cladeCount += it->second;
+        while (taxon->taxId != speciesTaxID) {
+            auto& ch = cladeCnt[taxon->parentTaxId].children;
+            if (std::find(ch.begin(), ch.end(), taxon->taxId) == ch.end()) ch.push_back(taxon->taxId);
+            cladeCnt[taxon->parentTaxId].cladeCount += it->second;
+            taxon = tax.taxonNode(taxon->parentTaxId);
+        }
+    }
+}
+
+TaxID Taxonomer::BFS(TaxID root, unsigned int maxCnt) {  // :292-314
+    unsigned int maxCnt2 = maxCnt;
+    if (cladeCnt.at(root).children.empty()) return root;
+    std::vector<TaxID> best;
+    for (TaxID c : cladeCnt.at(root).children) {
+        unsigned int cur = cladeCnt.at(c).cladeCount;
+        if (cur > maxCnt) { best.clear(); best.push_back(c); maxCnt = cur; }
+        else if (cur == maxCnt) best.push_back(c);
+    }
+    if (best.size() == 1) return BFS(best[0], maxCnt2);
+    return root;
+}
+
+TaxonScore Taxonomer::getBestSpeciesMatches(std::pair<size_t, size_t>& bestSpeciesRange, const mtb_match* ml,
+                                            size_t end, size_t offset, Query& query) {  // :316-408
+    matchPaths.clear();
+    combinedMatchPaths.clear();
+    std::vector<std::pair<TaxID, float>> sp2score;
+    int queryLength = query.queryLength + query.queryLength2;
+    TaxonScore bestScore;
+    float bestSpScore = 0;
+    size_t i = offset;
+    size_t meaningfulSpecies = 0;
+    while (i < end + 1) {
+        TaxID currentSpecies = (TaxID)ml[i].species_id;
+        size_t start = i;
+        size_t previousPathSize = matchPaths.size();
+        while ((i < end + 1) && currentSpecies == (TaxID)ml[i].species_id) {
+            uint32_t curFrame = infoFrame(ml[i].qinfo);
+            size_t fstart = i;
+            while ((i < end + 1) && currentSpecies == (TaxID)ml[i].species_id && curFrame == infoFrame(ml[i].qinfo)) i++;
+            if (i - fstart > 1) getMatchPaths(ml, fstart, i, currentSpecies);
+        }
+        size_t pathSize = matchPaths.size();
+        if (pathSize > previousPathSize) {
+            float score = combineMatchPaths(previousPathSize, combinedMatchPaths.size(), queryLength);
+            score = std::min(score, 1.0f);
+            if (score < par.min_score) continue;
+            sp2score.emplace_back(currentSpecies, score);
+            if (score > 0.f) meaningfulSpecies++;
+            if (score > bestSpScore) { bestSpScore = score; bestSpeciesRange = std::make_pair(start, i); }
+        }
+    }
+    if (meaningfulSpecies == 0) { bestScore.score = 0; return bestScore; }
+    maxSpecies.clear();
+    for (size_t k = 0; k < sp2score.size(); k++) {
+        if (sp2score[k].second >= bestSpScore * tieRatio) {
+            maxSpecies.push_back(sp2score[k].first);
+            bestScore.score += sp2score[k].second;
+        }
+    }
+    if (maxSpecies.size() > 1) {
+        bestScore.LCA = true;
+        bestScore.taxId = tax.LCA(maxSpecies)->taxId;
+        bestScore.score /= maxSpecies.size();
+        return bestScore;
+    }
+    bestScore.taxId = maxSpecies[0];
+    return bestScore;
+}
+
+float Taxonomer::combineMatchPaths(size_t matchPathStart, size_t combMatchPathStart, int readLength) {  // :410-468
+    std::sort(matchPaths.begin() + matchPathStart, matchPaths.end(), [](const MatchPath& a, const MatchPath& b) {
+        if (a.score != b.score) return a.score > b.score;
+        if (a.hammingDist != b.hammingDist) return a.hammingDist < b.hammingDist;
+        return a.start > b.start;
+    });
+    float score = 0;
+    for (size_t i = matchPathStart; i < matchPaths.size(); i++) {
+        if (combMatchPathStart == combinedMatchPaths.size()) {
+            combinedMatchPaths.push_back(matchPaths[i]);
+            score += matchPaths[i].score;
+        } else {
+            bool isOverlapped = false;
+            for (size_t j = combMatchPathStart; j < combinedMatchPaths.size(); j++) {
+                MatchPath& p = matchPaths[i];
+                const MatchPath& c = combinedMatchPaths[j];
+                if (!((p.end < c.start) || (c.end < p.start))) {
+                    int overlappedLength = std::min(p.end, c.end) - std::max(p.start, c.start) + 1;
+                    if (overlappedLength == p.end - p.start + 1) { isOverlapped = true; break; }
+                    if (overlappedLength < 24) { trimMatchPath(p, c, overlappedLength); continue; }
+                    isOverlapped = true;
+                    break;
+                }
+            }
+            if (!isOverlapped) {
+                combinedMatchPaths.push_back(matchPaths[i]);
+                score += matchPaths[i].score;
+            }
+        }
+    }
+    return score / readLength;
+}
+
+void Taxonomer::trimMatchPath(MatchPath& p1, const MatchPath& p2, int overlap) {  // :475-485
+    if (p1.start < p2.start) {
+        p1.end = p2.start - 1;
+        p1.hammingDist = std::max(0, p1.hammingDist - rightPartHamming(*p1.endMatch, overlap / 3));
+        p1.score = p1.score - rightPartScore(*p1.endMatch, overlap / 3) - (overlap % 3);
+    } else {
+        p1.start = p2.end + 1;
+        p1.hammingDist = std::max(0, p1.hammingDist - leftPartHamming(*p1.startMatch, overlap / 3));
+        p1.score = p1.score - leftPartScore(*p1.startMatch, overlap / 3) - (overlap % 3);
+    }
+}
+
+void Taxonomer::getMatchPaths(const mtb_match* ml, size_t start, size_t end, TaxID speciesId) {  // :487-648
+    size_t i = start;
+    size_t currPos = infoPos(ml[start].qinfo);
+    uint64_t frame = infoFrame(ml[start].qinfo);
+    int MIN_DEPTH = minConsCnt;
+    if (tax.IsAncestor(eukaryotaTaxId, speciesId)) MIN_DEPTH = minConsCntEuk;
+    connectedToNext.assign(end - start + 1, false);
+    localMatchPaths.clear();
+    localMatchPaths.resize(end - start + 1);
+    const bool fwd = frame < 3;
+
+    size_t curPosMatchStart = i;
+    while (i < end && infoPos(ml[i].qinfo) == currPos) { localMatchPaths[i - start] = MatchPath(ml + i); ++i; }
+    size_t curPosMatchEnd = i;
+    while (i < end) {
+        uint32_t nextPos = infoPos(ml[i].qinfo);
+        size_t nextPosMatchStart = i;
+        while (i < end && nextPos == infoPos(ml[i].qinfo)) { localMatchPaths[i - start] = MatchPath(ml + i); ++i; }
+        size_t nextPosMatchEnd = i;
+        int shift = (int)((nextPos - currPos) / 3);
+        if (shift > 0 && shift <= maxCodonShift) {
+            for (size_t nextIdx = nextPosMatchStart; nextIdx < nextPosMatchEnd; nextIdx++) {
+                float scoreIncrement = calScoreIncrement(ml[nextIdx].right_end_hamming, shift);
+                const MatchPath* bestPath = nullptr;
+                float bestScore = 0;
+                for (size_t curIdx = curPosMatchStart; curIdx < curPosMatchEnd; ++curIdx) {
+                    bool cons;
+                    if (kmerFormat == 2) cons = fwd ? isConsecutive2(ml + curIdx, ml + nextIdx, shift)
+                                                    : isConsecutive2(ml + nextIdx, ml + curIdx, shift);
+                    else cons = fwd ? isConsecutive(ml + curIdx, ml + nextIdx, shift)
+                                    : isConsecutive(ml + nextIdx, ml + curIdx, shift);
+                    if (cons) {
+                        connectedToNext[curIdx - start] = true;
+                        if (localMatchPaths[curIdx - start].score > bestScore) {
+                            bestPath = &localMatchPaths[curIdx - start];
+                            bestScore = localMatchPaths[curIdx - start].score;
+                        }
+                    }
+                }
+                if (bestPath != nullptr) {
+                    MatchPath& np = localMatchPaths[nextIdx - start];
+                    np.start = bestPath->start;
+                    np.score = bestPath->score + scoreIncrement;
+                    np.hammingDist = bestPath->hammingDist + calHammingDistIncrement(ml[nextIdx].right_end_hamming, shift);
+                    np.depth = bestPath->depth + shift;
+                    np.startMatch = bestPath->startMatch;
+                }
+            }
+        }
+        for (size_t curIdx = curPosMatchStart; curIdx < curPosMatchEnd; ++curIdx)
+            if (!connectedToNext[curIdx - start] && localMatchPaths[curIdx - start].depth >= MIN_DEPTH)
+                matchPaths.push_back(localMatchPaths[curIdx - start]);
+        if (i == end)
+            for (size_t nextIdx = nextPosMatchStart; nextIdx < nextPosMatchEnd; ++nextIdx)
+                if (localMatchPaths[nextIdx - start].depth >= MIN_DEPTH) matchPaths.push_back(localMatchPaths[nextIdx - start]);
+        curPosMatchStart = nextPosMatchStart;
+        curPosMatchEnd = nextPosMatchEnd;
+        currPos = nextPos;
+    }
+}
+
+void assignTaxonomy(const Db& db, const mtb_params& par, const mtb_match* matchList, size_t numOfMatches,
+                    std::vector<Query>& queryList) {
+    struct Block { size_t start, end; uint32_t id; };
+    std::vector<Block> blocks;
+    size_t matchIdx = 0;
+    while (matchIdx < numOfMatches) {  // Classifier.cpp:178-185
+        uint32_t cur = infoSeq(matchList[matchIdx].qinfo);
+        Block b{matchIdx, 0, cur};
+        while (matchIdx < numOfMatches && cur == infoSeq(matchList[matchIdx].qinfo)) ++matchIdx;
+        b.end = matchIdx - 1;
+        blocks.push_back(b);
+    }
+#pragma omp parallel
+    {
+        Taxonomer t(db, par);
+#pragma omp for schedule(dynamic, 1)
+        for (size_t i = 0; i < blocks.size(); ++i)
+            t.chooseBestTaxon(blocks[i].id - 1, blocks[i].start, blocks[i].end, matchList, queryList);
+    }
+}
+
+}  // namespace orc
