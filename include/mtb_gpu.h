@@ -161,6 +161,34 @@ int mtb_get_matches(mtb_ctx* ctx, mtb_match* out, uint64_t capacity, uint64_t* n
 int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches,
                        const uint32_t* query_len, uint32_t n_reads, mtb_result* results);
 
+/* ---- reference-DB builder (IndexCreator analogue) ----------------------------- */
+/* Genomes + gene blocks -> diffIdx / info / split / taxID_list in the reference's on-disk format
+ * (IndexCreator.cpp:316-376,811-886, IndexCreator.h:475-629), built on the GPU. */
+typedef struct mtb_build_input {
+    const uint8_t* seq;          /* concatenated genomes (device pointer with MTB_INPUT_DEVICE)  */
+    const uint64_t* off;         /* n_genomes+1 offsets (device pointer with MTB_INPUT_DEVICE)   */
+    uint32_t n_genomes;
+    const int32_t* genome_taxid; /* host */
+    const int32_t* blk_genome;   /* host: gene blocks {genome, start, end, strand (+1/-1)}        */
+    const int32_t* blk_start;
+    const int32_t* blk_end;
+    const int32_t* blk_strand;
+    uint64_t n_blocks;
+    int32_t split_num;           /* 4096 in the reference's build                               */
+    uint32_t flags;
+} mtb_build_input;
+
+typedef struct mtb_db_built {    /* malloc'd host arrays, release with mtb_free_built */
+    uint16_t* diff_idx; uint64_t n_diff_idx;
+    uint32_t* info;     uint64_t n_info;
+    uint64_t* split;    uint64_t n_split;
+    int32_t* taxid_list; uint64_t n_taxid_list;
+} mtb_db_built;
+
+int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxonomy, const mtb_params* par, int device,
+                 mtb_db_built* out);
+void mtb_free_built(mtb_db_built* b);
+
 #ifdef __cplusplus
 }
 #endif
