@@ -1,0 +1,290 @@
+#!/usr/bin/env python
+"""Benchmark of the MI355X classify hot path (BASELINE.json metric, configs[1]).
+
+Workload (config 2): 1M x 150 bp paired reads vs a RefSeq-viral-sized (~10 GB) reference DB, DB
+resident in HBM, reads resident in HBM when the timed region starts. Synthetic data (no network):
+species genomes + two 2%-diverged strains each, gene blocks shared by a species' strains, the DB
+built on the GPU in the reference's on-disk format (mtb_build_db), reads sampled from the genomes
+with 0.5% substitutions plus 10% random reads.
+
+One step = one pass of the whole path over the batch: K0 read metadata, K1 extract, K2 k-mer
+radix sort, K4 match (count + emit), K5/K6 per-read sort + assignment, taxcnt compaction; with
+N > 1 ranks, plus an RCCL all-gather of the per-read result records (weak scaling: every rank
+classifies its own batch against its own DB replica).
+
+Prints one JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from metabuli_work_amd import synth  # noqa: E402
+from metabuli_work_amd._abi import RESULT_DTYPE, default_params  # noqa: E402
+from metabuli_work_amd.classifier import Classifier, LocalParameters  # noqa: E402
+from metabuli_work_amd.dbbuild import build_db  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+KERNELS = ["extract", "kmer_sort", "match_count", "match_emit", "assign"]
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic data on the GPU
+# ---------------------------------------------------------------------------------------------
+def make_genomes_gpu(n_species, mean_len, strains, seed, dev):
+    rng = np.random.default_rng(seed)
+    taxo = synth.make_taxonomy(n_species, strains, seed=seed)
+    lens = rng.integers(int(mean_len * 0.3), int(mean_len * 1.7), size=n_species).astype(np.int64)
+    base_off = np.zeros(n_species + 1, np.int64)
+    base_off[1:] = np.cumsum(lens)
+    total = int(base_off[-1])
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    lut = torch.tensor([65, 67, 71, 84], dtype=torch.uint8, device=dev)
+    base = torch.randint(0, 4, (total,), dtype=torch.uint8, device=dev, generator=g)
+    seq = torch.empty(total * strains, dtype=torch.uint8, device=dev)
+    chunk = 1 << 28
+    for k in range(strains):
+        for a in range(0, total, chunk):
+            b = min(total, a + chunk)
+            x = base[a:b]
+            m = torch.rand(b - a, device=dev, generator=g) < 0.02
+            sh = torch.randint(1, 4, (b - a,), dtype=torch.uint8, device=dev, generator=g)
+            x = torch.where(m, (x + sh) % 4, x)
+            seq[k * total + a:k * total + b] = lut[x.long()]
+    del base
+    # genome k*n_species + s = strain k of species s; taxIDs: the strain nodes of each species
+    rank = np.array(taxo.rank)
+    sp_ids = taxo.taxid[rank == "species"]
+    strain_of = {}
+    for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank):
+        if r == "no rank" and t != 1:
+            strain_of.setdefault(p, []).append(t)
+    gtax = np.zeros(n_species * strains, np.int32)
+    for s, sp in enumerate(sp_ids.tolist()):
+        for k in range(strains):
+            gtax[k * n_species + s] = strain_of[sp][k]
+    off = np.zeros(n_species * strains + 1, np.int64)
+    off[1:] = np.concatenate([np.cumsum(np.tile(lens, strains))])
+    # gene blocks per species, shared by its strains (same coordinates)
+    bg, bs, be, bst = [], [], [], []
+    for s in range(n_species):
+        L = int(lens[s])
+        n_est = L // 300 + 2
+        ln = rng.integers(300, 3000, size=n_est)
+        gap = rng.integers(0, 60, size=n_est)
+        starts = np.concatenate([[int(rng.integers(0, 50))], np.cumsum(ln + gap)[:-1] + int(rng.integers(0, 50))])
+        ends = starts + ln - 1
+        keep = starts + 300 < L
+        starts, ends = starts[keep], np.minimum(ends[keep], L - 1)
+        strand = np.where(rng.random(len(starts)) < 0.5, 1, -1)
+        for k in range(strains):
+            bg.append(np.full(len(starts), k * n_species + s, np.int32))
+            bs.append(starts.astype(np.int32))
+            be.append(ends.astype(np.int32))
+            bst.append(strand.astype(np.int32))
+    gen = synth.Genomes(seq=None, off=off.astype(np.uint64), taxid=gtax,
+                        species=np.repeat(sp_ids, 1)[np.tile(np.arange(n_species), strains)],
+                        blk_genome=np.concatenate(bg), blk_start=np.concatenate(bs), blk_end=np.concatenate(be),
+                        blk_strand=np.concatenate(bst))
+    off_t = torch.from_numpy(off).to(dev)
+    return taxo, gen, seq, off_t, lens
+
+
+def make_reads_gpu(seq, off_t, n_pairs, seed, dev, read_len=150, sub_rate=0.005, random_frac=0.1):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    glen = (off_t[1:] - off_t[:-1]).to(torch.float32)
+    gsel = torch.multinomial(glen, n_pairs, replacement=True, generator=g)
+    gl = (off_t[1:] - off_t[:-1])[gsel]
+    ins = (torch.randn(n_pairs, device=dev, generator=g) * 30 + 300).round().long().clamp(min=read_len)
+    ins = torch.minimum(ins, gl)
+    start = (torch.rand(n_pairs, device=dev, generator=g) * (gl - ins + 1).float()).long()
+    start = torch.minimum(start, gl - ins)
+    p0 = off_t[gsel] + start
+    ar = torch.arange(read_len, device=dev)
+    A = seq[p0[:, None] + ar]
+    comp = torch.zeros(256, dtype=torch.uint8, device=dev)
+    comp[torch.tensor([65, 67, 71, 84], device=dev)] = torch.tensor([84, 71, 67, 65], dtype=torch.uint8, device=dev)
+    B = comp[seq[(p0 + ins - read_len)[:, None] + ar].long()].flip(1)
+    flip = (torch.rand(n_pairs, device=dev, generator=g) < 0.5)[:, None]
+    m1 = torch.where(flip, B, A)
+    m2 = torch.where(flip, A, B)
+    lut = torch.tensor([65, 67, 71, 84], dtype=torch.uint8, device=dev)
+    out = []
+    rnd = torch.rand(n_pairs, device=dev, generator=g) < random_frac
+    for m in (m1, m2):
+        sub = torch.rand(m.shape, device=dev, generator=g) < sub_rate
+        repl = lut[torch.randint(0, 4, m.shape, device=dev, generator=g)]
+        m = torch.where(sub, repl, m)
+        rr = lut[torch.randint(0, 4, m.shape, device=dev, generator=g)]
+        m = torch.where(rnd[:, None], rr, m)
+        out.append(m.contiguous().view(-1))
+    off = torch.arange(0, (n_pairs + 1) * read_len, read_len, dtype=torch.int64, device=dev)
+    return out[0], off, out[1], off.clone()
+
+
+# ---------------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=1_000_000, help="read pairs per rank per step")
+    ap.add_argument("--species", type=int, default=25000)
+    ap.add_argument("--mean-genome", type=int, default=75000)
+    ap.add_argument("--cpu-sample", type=int, default=50_000, help="read pairs timed on the CPU oracle (0 = off)")
+    ap.add_argument("--seed", type=int, default=5)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    t0 = time.time()
+    par = default_params(kmer_format=2, seq_mode=2)
+    taxo, gen, seq, off_t, lens = make_genomes_gpu(args.species, args.mean_genome, 2, args.seed, dev)
+    s1, o1, s2, o2 = make_reads_gpu(seq, off_t, args.pairs, args.seed * 1000 + 17 * rank + 1, dev)
+    torch.cuda.synchronize()
+    log(rank, f"[bench] genomes {seq.numel() / 1e9:.2f} Gbp in {len(lens) * 2} genomes, blocks "
+              f"{len(gen.blk_genome)}; reads {args.pairs} pairs ({time.time() - t0:.1f}s)")
+    hdb = build_db(gen, taxo, par, device=local, device_seq=(seq, off_t))
+    del seq
+    torch.cuda.empty_cache()
+    db_bytes = hdb.nbytes
+    log(rank, f"[bench] DB built: {hdb.n_kmers / 1e9:.3f}G k-mers, {db_bytes / 1e9:.2f} GB "
+              f"(diffIdx+info) ({time.time() - t0:.1f}s)")
+    lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    clf = Classifier(lp, db_host=hdb.c_struct(), device=local)
+    log(rank, f"[bench] DB resident in HBM ({time.time() - t0:.1f}s)")
+
+    n = args.pairs
+    gathered = None
+    res_dev = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    if world > 1:
+        gathered = torch.empty(world * res_dev.numel(), dtype=torch.uint8, device=dev)
+
+    def step():
+        clf.classify_batch(s1, o1, s2, o2, device_input=True, fetch=False)
+        if world > 1:
+            clf.copy_results(res_dev.data_ptr(), on_device=True)
+            dist.all_gather_into_tensor(gathered, res_dev)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern = np.zeros(5)
+    stage = np.zeros(5)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kern += clf.kernel_ms()
+        stage += clf.stage_ms()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern /= max(1, args.steps)
+    stage /= max(1, args.steps)
+    Q, M = clf.last_counts()
+    ms_per_step = elapsed / max(1, args.steps) * 1e3
+    value = world * n * args.steps / elapsed
+
+    # ---- roofline of the dominant kernel: algorithmic bytes per launch / event-timed duration ----
+    read_bytes = 2 * n * 150 + 2 * 8 * (n + 1)
+    R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
+    D = hdb.n_kmers
+    alg = {
+        "extract": read_bytes + 16 * R,                     # reads in, one 16-B slot per window out
+        "kmer_sort": 16 * R + 16 * Q,                       # the pairs read once, the kept pairs written once
+        "match_count": 16 * Q + 8 * min(D, Q),              # queries + the DB values their AA runs touch
+        "match_emit": 16 * Q + 12 * min(D, Q) + 24 * M,     # + info of candidates, matches written
+        "assign": 2 * 24 * M + 32 * n + 4 * n,              # matches read + written (sorted), results
+    }
+    dom = int(np.argmax(kern))
+    dname = KERNELS[dom]
+    achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": int(alg[dname]), "avg_launch_ms": round(float(kern[dom]), 3)}
+
+    # ---- CPU baseline: the oracle (restated reference algorithm, OpenMP) on a bounded sample ----
+    cpu = None
+    parity = None
+    if rank == 0 and args.cpu_sample > 0:
+        from tests import oracle_ctypes as oc  # checker / baseline only
+
+        S = min(args.cpu_sample, n)
+        h1 = s1[:S * 150].cpu().numpy()
+        h2 = s2[:S * 150].cpu().numpy()
+        ho = o1[:S + 1].cpu().numpy().astype(np.uint64)
+        reads = synth.Reads(h1, ho, h2, ho.copy(), np.zeros(S, np.int32))
+        cores = len(os.sched_getaffinity(0))
+        cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+        oc.lib().orc_set_threads(cores)
+        opar = lp.to_c()
+        opar.threads = cores
+        odb = oc.OracleDb.from_host(hdb.c_struct())
+        stage_s = np.zeros(4)
+        tc0 = time.perf_counter()
+        ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
+        cpu_t = time.perf_counter() - tc0
+        odb.close()
+        cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+               "sample": f"first {S} read pairs of the rank-0 batch, same DB; oracle/ (OpenMP C++ restatement "
+                         f"of the reference path), {cpu_t:.1f}s wall",
+               "stage_s": [round(x, 3) for x in stage_s]}
+        gb = clf.classify_batch(h1, ho, h2, ho.copy())
+        parity = bool(np.array_equal(gb.results["classification"], ores["classification"])
+                      and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
+                      and np.array_equal(gb.taxcnt, otc))
+
+    if rank == 0:
+        out = {
+            "metric": "reads/sec classified (150bp & 10kb) vs GTDB-scale DB at 1/2/4/8 MI355X",
+            "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "config 2: 1M x 150bp paired reads vs RefSeq-viral-sized DB (~10 GB), "
+                                   "format 2, DB + reads resident in HBM",
+                       "read_pairs_per_gpu": n, "read_len": 150, "db_kmers": D,
+                       "db_bytes": db_bytes, "query_kmers": Q, "matches": M,
+                       "parallelism": f"reads sharded, DB replicated x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms": {k: round(float(v), 3) for k, v in zip(KERNELS, kern)},
+            "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
+            "parity_sample": parity,
+        }
+        print(json.dumps(out), flush=True)
+    clf.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -154,6 +154,15 @@ class Classifier:
         lib().mtb_last_stage_ms(self.handle, ms, 5)
         return np.array(list(ms), np.float32)
 
+    def kernel_ms(self) -> np.ndarray:
+        """[extract, k-mer sort, match count, match emit, assign] of the last batch (HIP events)."""
+        ms = (ctypes.c_float * 5)()
+        lib().mtb_last_kernel_ms(self.handle, ms, 5)
+        return np.array(list(ms), np.float32)
+
+    def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:
+        check(lib().mtb_copy_results(self.handle, ctypes.c_void_p(dst_ptr), int(on_device)), "mtb_copy_results")
+
     def query_kmers(self) -> np.ndarray:
         q, _ = self.last_counts()
         out = np.zeros(q, KMER_DTYPE)

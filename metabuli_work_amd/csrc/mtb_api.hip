@@ -73,6 +73,9 @@ struct mtb_ctx {
     bool keepStages = false;
     float stageMs[5] = {0, 0, 0, 0, 0};
     hipEvent_t ev[6]{};
+    // tight event pairs around the main kernels: extract, k-mer sort, match count, match emit, assign
+    float kernMs[5] = {0, 0, 0, 0, 0};
+    hipEvent_t kev[10]{};
 };
 
 static void free_db(mtb_ctx* c) {
@@ -115,6 +118,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->ownStream = true;
     for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : c->kev) HIP_TRY(hipEventCreate(&e));
     hipStream_t s = c->stream;
     c->D = db.info.size();
     // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381)
@@ -204,6 +208,8 @@ void mtb_close(mtb_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
+    for (auto& e : c->kev)
+        if (e) hipEventDestroy(e);
     if (c->ownStream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -278,8 +284,10 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
     AssignScratch sc{c->local.p, c->paths.p, c->comb.p, c->conn.as<uint8_t>(), c->spScore.as<float>(),
                      c->spId.as<int32_t>(), c->quot.p, c->clade.p, c->cladePerMatch};
+    HIP_TRY(hipEventRecord(c->kev[8], s));
     launch_assign(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
                   n, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
+    HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
     launch_taxcnt_len(c->results.as<mtb_result>(), n, c->tcLen.as<uint32_t>(), s);
@@ -348,19 +356,23 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->valsA.ensure(8 * Rc));
     HIP_TRY(c->keysB.ensure(8 * Rc));
     HIP_TRY(c->valsB.ensure(8 * Rc));
+    HIP_TRY(hipEventRecord(c->kev[0], s));
     launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(), n, paired, c->tables,
                    c->par.kmer_format, c->par.syncmer, c->par.smer_len, c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(),
                    s);
+    HIP_TRY(hipEventRecord(c->kev[1], s));
     HIP_TRY(hipEventRecord(c->ev[1], s));
     // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
     HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Rc)));
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     bool inB = false;
-    const int bitHi = c->par.kmer_format == 2 ? 64 : 64;
+    const int bitHi = 64;
+    HIP_TRY(hipEventRecord(c->kev[2], s));
     uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), c->keysB.as<uint64_t>(),
                                   c->valsB.as<uint64_t>(), R, 24, bitHi, true, c->radixCounts.as<uint32_t>(),
                                   c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+    HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
     c->sortedInB = inB;
     const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
@@ -372,8 +384,10 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
+    HIP_TRY(hipEventRecord(c->kev[4], s));
     launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), s);
+    HIP_TRY(hipEventRecord(c->kev[5], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t M = 0;
     HIP_TRY(hipMemcpyAsync(&M, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -381,8 +395,10 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     c->M = M;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+    HIP_TRY(hipEventRecord(c->kev[6], s));
     launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
+    HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     // K5 + K6
     int rc = assign_stage(c, n);
@@ -394,6 +410,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipStreamSynchronize(s));
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
+    for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
     if (err) {
         set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
         return MTB_ERR_DB;
@@ -427,6 +444,20 @@ int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
 int mtb_last_stage_ms(const mtb_ctx* c, float* ms, int n) {
     if (!c || !ms) return MTB_ERR_ARG;
     for (int i = 0; i < n && i < 5; i++) ms[i] = c->stageMs[i];
+    return MTB_OK;
+}
+
+int mtb_last_kernel_ms(const mtb_ctx* c, float* ms, int n) {
+    if (!c || !ms) return MTB_ERR_ARG;
+    for (int i = 0; i < n && i < 5; i++) ms[i] = c->kernMs[i];
+    return MTB_OK;
+}
+
+int mtb_copy_results(mtb_ctx* c, void* dst, int dst_on_device) {
+    if (!c || !dst) return MTB_ERR_ARG;
+    HIP_TRY(hipMemcpyAsync(dst, c->results.p, sizeof(mtb_result) * c->nReads,
+                           dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return MTB_OK;
 }
 

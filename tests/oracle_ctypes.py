@@ -66,11 +66,18 @@ def build_db(out_dir: str, par: MtbParams, taxo, gen, split_num: int = 4096) -> 
 
 
 class OracleDb:
-    def __init__(self, db_dir: str):
+    def __init__(self, db_dir: str = None, host_struct=None):
         err = ctypes.create_string_buffer(512)
-        self.h = lib().orc_db_open(db_dir.encode(), err, 512)
+        if host_struct is not None:
+            self.h = lib().orc_db_open_host(ctypes.byref(host_struct), err, 512)
+        else:
+            self.h = lib().orc_db_open(db_dir.encode(), err, 512)
         if not self.h:
             raise RuntimeError(err.value.decode())
+
+    @classmethod
+    def from_host(cls, host_struct):
+        return cls(host_struct=host_struct)
 
     @property
     def n_kmers(self) -> int:
