@@ -61,16 +61,15 @@ def test_oracle_scanners_vs_closed_form(fmt, syncmer, smer, paired):
 
 
 def _decode(diff):
-    vals = []
-    cur = 0
-    acc = 0
-    for w in diff.tolist():
-        acc = (acc << 15) | (w & 0x7FFF)
-        if w & 0x8000:
-            cur += acc
-            vals.append(cur)
-            acc = 0
-    return np.array(vals, np.uint64)
+    """Vectorised getNextTargetKmer over a whole diffIdx: values and the word index after each."""
+    diff = diff.astype(np.uint64)
+    term = np.nonzero(diff & np.uint64(0x8000))[0]
+    starts = np.concatenate([[0], term[:-1] + 1])
+    kidx = np.repeat(np.arange(len(term)), term - starts + 1)
+    shift = (term[kidx] - np.arange(len(diff))) * 15
+    contrib = (diff & np.uint64(0x7FFF)) << shift.astype(np.uint64)
+    deltas = np.add.reduceat(contrib, starts)
+    return np.cumsum(deltas, dtype=np.uint64), term + 1
 
 
 @pytest.mark.parametrize("fmt,syncmer", [(2, 0), (2, 1), (1, 0)])
@@ -82,7 +81,7 @@ def test_db_writer_invariants(tmp_path, fmt, syncmer):
     diff = np.fromfile(os.path.join(d, "diffIdx"), np.uint16)
     info = np.fromfile(os.path.join(d, "info"), np.uint32)
     split = np.fromfile(os.path.join(d, "split"), np.uint64).reshape(-1, 3)
-    vals = _decode(diff)
+    vals, word_end = _decode(diff)
     assert len(vals) == len(info) > 4095                      # validateDatabase.cpp:78-131
     assert np.all(vals[1:] >= vals[:-1])                      # sorted by value
     assert len(split) == 4096 and not split[0].any()
@@ -90,7 +89,7 @@ def test_db_writer_invariants(tmp_path, fmt, syncmer):
     assert len(used) > 100
     for ad, doff, ioff in used:
         assert vals[ioff - 1] == ad                           # ADkmer = k-mer at infoIdxOffset-1
-        assert _decode(diff[:doff])[-1] == ad                 # diffIdxOffset counts words through it
+        assert word_end[ioff - 1] == doff                     # diffIdxOffset counts words through it
         assert ((vals[ioff - 2] ^ ad) >> np.uint64(24)) != 0  # starts a new AA group
     p = oc.load_db_parameters(d, default_params())
     assert (p.kmer_format, p.syncmer, p.skip_redundancy) == (fmt, syncmer, 1)
