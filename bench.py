@@ -34,7 +34,7 @@ from metabuli_work_amd.classifier import Classifier, LocalParameters  # noqa: E4
 from metabuli_work_amd.dbbuild import build_db  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-KERNELS = ["extract", "kmer_sort", "match_count", "match_emit", "assign"]
+KERNELS = ["extract", "kmer_sort", "match_count", "match_emit", "match_sort", "assign"]
 
 
 def log(rank, *a):
@@ -193,7 +193,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kern = np.zeros(5)
+    kern = np.zeros(len(KERNELS))
     stage = np.zeros(5)
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -223,7 +223,8 @@ def main():
         "kmer_sort": 16 * R + 16 * Q,                       # the pairs read once, the kept pairs written once
         "match_count": 16 * Q + 8 * min(D, Q),              # queries + the DB values their AA runs touch
         "match_emit": 16 * Q + 12 * min(D, Q) + 24 * M,     # + info of candidates, matches written
-        "assign": 2 * 24 * M + 32 * n + 4 * n,              # matches read + written (sorted), results
+        "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
+        "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
     }
     dom = int(np.argmax(kern))
     dname = KERNELS[dom]

@@ -155,9 +155,10 @@ class Classifier:
         return np.array(list(ms), np.float32)
 
     def kernel_ms(self) -> np.ndarray:
-        """[extract, k-mer sort, match count, match emit, assign] of the last batch (HIP events)."""
-        ms = (ctypes.c_float * 5)()
-        lib().mtb_last_kernel_ms(self.handle, ms, 5)
+        """[extract, k-mer sort, match count, match emit, match sort, assign] of the last batch
+        (HIP events)."""
+        ms = (ctypes.c_float * 6)()
+        lib().mtb_last_kernel_ms(self.handle, ms, 6)
         return np.array(list(ms), np.float32)
 
     def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:

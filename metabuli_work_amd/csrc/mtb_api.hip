@@ -64,7 +64,7 @@ struct mtb_ctx {
     // batch workspace
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, qcapOff, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
-    DevBuf readCnt, mOff, matches, errFlag;
+    DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
     DevBuf local, paths, comb, conn, spScore, spId, quot, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
     uint32_t nReads = 0;
@@ -73,9 +73,11 @@ struct mtb_ctx {
     bool keepStages = false;
     float stageMs[5] = {0, 0, 0, 0, 0};
     hipEvent_t ev[6]{};
-    // tight event pairs around the main kernels: extract, k-mer sort, match count, match emit, assign
-    float kernMs[5] = {0, 0, 0, 0, 0};
-    hipEvent_t kev[10]{};
+    // tight event pairs around the main kernels: extract, k-mer sort, match count, match emit,
+    // per-read match sort, assign
+    static constexpr int kNumKern = 6;
+    float kernMs[kNumKern] = {0, 0, 0, 0, 0, 0};
+    hipEvent_t kev[2 * kNumKern]{};
 };
 
 static void free_db(mtb_ctx* c) {
@@ -202,7 +204,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->qcapOff, &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->errFlag, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spId, &c->quot, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -281,13 +283,25 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
     HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Mc));
     HIP_TRY(c->results.ensure(sizeof(mtb_result) * std::max<uint32_t>(n, 1)));
+    // K5: per-read segmented sort into compareMatches order
+    HIP_TRY(c->matchesSorted.ensure(sizeof(mtb_match) * Mc));
+    HIP_TRY(c->maxSeg.ensure(sizeof(uint32_t)));
+    launch_max_seg(c->mOff.as<uint64_t>(), n, c->maxSeg.as<uint32_t>(), s);
+    uint32_t maxSeg = 0;
+    HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (maxSeg > kSegSortLds) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
+    HIP_TRY(hipEventRecord(c->kev[8], s));
+    launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
+                   c->segScratch.as<uint64_t>(), maxSeg > 512, s);
+    HIP_TRY(hipEventRecord(c->kev[9], s));
+    HIP_TRY(hipEventRecord(c->kev[10], s));
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
     AssignScratch sc{c->local.p, c->paths.p, c->comb.p, c->conn.as<uint8_t>(), c->spScore.as<float>(),
                      c->spId.as<int32_t>(), c->quot.p, c->clade.p, c->cladePerMatch};
-    HIP_TRY(hipEventRecord(c->kev[8], s));
-    launch_assign(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
+    launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
                   n, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
-    HIP_TRY(hipEventRecord(c->kev[9], s));
+    HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
     launch_taxcnt_len(c->results.as<mtb_result>(), n, c->tcLen.as<uint32_t>(), s);
@@ -410,7 +424,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipStreamSynchronize(s));
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
-    for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
+    for (int k = 0; k < mtb_ctx::kNumKern; k++)
+        HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
     if (err) {
         set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
         return MTB_ERR_DB;
@@ -449,7 +464,7 @@ int mtb_last_stage_ms(const mtb_ctx* c, float* ms, int n) {
 
 int mtb_last_kernel_ms(const mtb_ctx* c, float* ms, int n) {
     if (!c || !ms) return MTB_ERR_ARG;
-    for (int i = 0; i < n && i < 5; i++) ms[i] = c->kernMs[i];
+    for (int i = 0; i < n && i < mtb_ctx::kNumKern; i++) ms[i] = c->kernMs[i];
     return MTB_OK;
 }
 
@@ -482,7 +497,7 @@ int mtb_get_matches(mtb_ctx* c, mtb_match* out, uint64_t cap, uint64_t* n_out) {
     *n_out = c->M;
     if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
     if (cap < c->M) return MTB_RETRY;
-    if (c->M) HIP_TRY(hipMemcpy(out, c->matches.p, sizeof(mtb_match) * c->M, hipMemcpyDeviceToHost));
+    if (c->M) HIP_TRY(hipMemcpy(out, c->matchesSorted.p, sizeof(mtb_match) * c->M, hipMemcpyDeviceToHost));
     return MTB_OK;
 }
 

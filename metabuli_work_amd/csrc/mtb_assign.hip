@@ -1,9 +1,9 @@
 // K5 + K6: per-read match sort and taxonomic assignment (Classifier::assignTaxonomy,
 // Classifier.cpp:166-208; Taxonomer::chooseBestTaxon and helpers, Taxonomer.cpp:130-713).
 //
-// One thread per read in this version: the thread sorts its read's match segment in place
-// (compareMatches, KmerMatcher.cpp:1149-1166), then runs the reference's decision tree with
-// per-read scratch carved from batch-wide arrays by the read's match offset. Float arithmetic
+// K5 sorts each read's match segment (k_segsort_*); K6 then runs one thread per read over the
+// sorted segment, executing the reference's decision tree with per-read scratch carved from
+// batch-wide arrays by the read's match offset. Float arithmetic
 // follows the reference operation for operation (compiled with -ffp-contract=off).
 #include "mtb_launch.h"
 #include "mtb_stdsort.h"
@@ -17,49 +17,148 @@ struct Path {  // MatchPath (Taxonomer.h:35-59); start/end match as indices into
     uint32_t sm, em;
 };
 
-__device__ __forceinline__ bool match_less(const mtb_match& a, const mtb_match& b) {
-    uint32_t sa = info_seq(a.qinfo), sb = info_seq(b.qinfo);
-    if (sa != sb) return sa < sb;
-    if (a.species_id != b.species_id) return (int)a.species_id < (int)b.species_id;
-    uint32_t fa = info_frame(a.qinfo), fb = info_frame(b.qinfo);
-    if (fa != fb) return fa < fb;
-    uint32_t pa = info_pos(a.qinfo), pb = info_pos(b.qinfo);
-    if (pa != pb) return pa < pb;
-    if (a.hamming != b.hamming) return a.hamming < b.hamming;
-    if (a.dna_encoding != b.dna_encoding) return a.dna_encoding < b.dna_encoding;
-    // compareMatches stops here; a valid DB has one entry per (value, species) so no two matches
-    // of one query k-mer tie. The extra keys only make the order total.
-    if (a.target_id != b.target_id) return a.target_id < b.target_id;
-    return a.right_end_hamming < b.right_end_hamming;
+// ------------------------------------------------------------------------------------------------
+// K5 segmented sort of each read's matches into compareMatches order (KmerMatcher.cpp:1149-1166).
+// Key = (species:32 | frame:3 | pos:29, hamming:8 | dna:24 | target:32), compared as 128 bits;
+// the last field only makes the order total (a valid DB never ties before it).
+// Small segments (<= 512): one wave64 per read, bitonic sort of keys + 16-bit indices in LDS, then
+// a gather-permute of the 24-B records into the output segment (contiguous writes).
+// Larger segments: one 256-thread block per read, bitonic sort in LDS (<= 4096) or, beyond that,
+// in a global key scratch.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void match_key(const mtb_match& m, uint64_t& hi, uint64_t& lo) {
+    hi = ((uint64_t)m.species_id << 32) | ((uint64_t)info_frame(m.qinfo) << 29) | (info_pos(m.qinfo) & 0x1FFFFFFFu);
+    lo = ((uint64_t)m.hamming << 56) | ((uint64_t)(m.dna_encoding & 0xFFFFFFu) << 32) | m.target_id;
 }
 
-__device__ inline void heap_sift(mtb_match* a, long i, long n) {
-    while (true) {
-        long c = 2 * i + 1;
-        if (c >= n) return;
-        if (c + 1 < n && match_less(a[c], a[c + 1])) c++;
-        if (!match_less(a[i], a[c])) return;
-        mtb_match t = a[i]; a[i] = a[c]; a[c] = t;
-        i = c;
-    }
+__device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    return ah > bh || (ah == bh && al > bl);
 }
 
-__device__ inline void sort_matches(mtb_match* a, long n) {
-    if (n < 2) return;
-    if (n <= 24) {
-        for (long i = 1; i < n; i++) {
-            mtb_match v = a[i];
-            long j = i;
-            while (j > 0 && match_less(v, a[j - 1])) { a[j] = a[j - 1]; j--; }
-            a[j] = v;
-        }
+constexpr int kSmallSeg = 512;
+constexpr int kBlockSeg = 4096;
+
+__global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                      uint32_t nReads, mtb_match* __restrict__ out) {
+    __shared__ uint64_t sh[kSmallSeg], sl[kSmallSeg];
+    __shared__ uint16_t si[kSmallSeg];
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const int n = (int)(mOff[r + 1] - base);
+    if (n == 0 || n > kSmallSeg) return;
+    const int lane = threadIdx.x;
+    if (n == 1) {
+        if (lane == 0) out[base] = in[base];
         return;
     }
-    for (long i = n / 2 - 1; i >= 0; i--) heap_sift(a, i, n);
-    for (long e = n - 1; e > 0; e--) {
-        mtb_match t = a[0]; a[0] = a[e]; a[e] = t;
-        heap_sift(a, 0, e);
+    int p2 = 2;
+    while (p2 < n) p2 <<= 1;
+    for (int i = lane; i < p2; i += 64) {
+        uint64_t h = ~0ull, l = ~0ull;
+        if (i < n) match_key(in[base + i], h, l);
+        sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
     }
+    __syncthreads();
+    for (int k = 2; k <= p2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < p2; i += 64) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    uint64_t ah = sh[i], al = sl[i], bh = sh[ixj], bl = sl[ixj];
+                    if (key_gt(ah, al, bh, bl) == up) {
+                        sh[i] = bh; sl[i] = bl; sh[ixj] = ah; sl[ixj] = al;
+                        uint16_t t = si[i]; si[i] = si[ixj]; si[ixj] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = lane; i < n; i += 64) out[base + i] = in[base + si[i]];
+}
+
+// One block per large segment (the block loops over the reads of its 256-read slice). Segments with
+// p2 <= 4096 sort in LDS; larger ones in global scratch laid out as three arrays of 2*M words
+// (keys hi, keys lo, indices), the read's slice at offset 2*base (p2 <= 2n).
+__device__ void block_bitonic(uint64_t* H, uint64_t* Lo, uint32_t* I, long p2) {
+    for (long k = 2; k <= p2; k <<= 1)
+        for (long j = k >> 1; j > 0; j >>= 1) {
+            for (long i = threadIdx.x; i < p2; i += 256) {
+                const long ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    const uint64_t ah = H[i], al = Lo[i], bh = H[ixj], bl = Lo[ixj];
+                    if (key_gt(ah, al, bh, bl) == up) {
+                        H[i] = bh; Lo[i] = bl; H[ixj] = ah; Lo[ixj] = al;
+                        const uint32_t t = I[i]; I[i] = I[ixj]; I[ixj] = t;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+}
+
+__global__ void __launch_bounds__(256) k_segsort_large(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                       uint32_t nReads, uint64_t M, mtb_match* __restrict__ out,
+                                                       uint64_t* __restrict__ gScratch) {
+    __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
+    __shared__ uint32_t si[kBlockSeg];
+    const uint32_t r0 = blockIdx.x * 256;
+    const uint32_t r1 = min(r0 + 256u, nReads);
+    for (uint32_t r = r0; r < r1; r++) {
+        const uint64_t base = mOff[r];
+        const long n = (long)(mOff[r + 1] - base);
+        if (n <= kSmallSeg) continue;
+        long p2 = 2;
+        while (p2 < n) p2 <<= 1;
+        uint64_t *H = sh, *Lo = sl;
+        uint32_t* I = si;
+        if (p2 > kBlockSeg) {
+            H = gScratch + 2 * base;
+            Lo = gScratch + 2 * M + 2 * base;
+            I = (uint32_t*)(gScratch + 4 * M) + 2 * base;
+        }
+        for (long i = threadIdx.x; i < p2; i += 256) {
+            uint64_t h = ~0ull, l = ~0ull;
+            if (i < n) match_key(in[base + i], h, l);
+            H[i] = h; Lo[i] = l; I[i] = (uint32_t)i;
+        }
+        __threadfence_block();
+        __syncthreads();
+        block_bitonic(H, Lo, I, p2);
+        for (long i = threadIdx.x; i < n; i += 256) out[base + i] = in[base + I[i]];
+        __syncthreads();
+    }
+}
+
+__global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicMax(out, x[i]);
+}
+
+void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                    uint64_t* gScratch, bool anyLarge, hipStream_t s) {
+    if (nReads == 0) return;
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
+    if (anyLarge) k_segsort_large<<<(nReads + 255) / 256, 256, 0, s>>>(in, mOff, nReads, M, out, gScratch);
+}
+
+__global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicMax(out, (uint32_t)min<uint64_t>(off[i + 1] - off[i], 0xFFFFFFFFull));
+}
+
+void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s) {
+    hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+    if (n) k_max_seg<<<(n + 255) / 256, 256, 0, s>>>(off, n, out);
+}
+
+void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s) {
+    hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+    if (n) k_max_u32<<<(n + 255) / 256, 256, 0, s>>>(x, n, out);
 }
 
 struct TaxView {
@@ -118,7 +217,7 @@ __device__ __forceinline__ int ham_fields(uint32_t reh, int range, bool left) {
     return s;
 }
 
-__global__ void __launch_bounds__(256) k_assign(mtb_match* __restrict__ matches, const uint64_t* __restrict__ mOff,
+__global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ matches, const uint64_t* __restrict__ mOff,
                                                 const uint32_t* __restrict__ qlen, const uint64_t* __restrict__ qOff,
                                                 uint32_t nReads, AssignCfg cfg, TaxView tax, Path* __restrict__ localP,
                                                 Path* __restrict__ pathsP, Path* __restrict__ combP,
@@ -142,8 +241,7 @@ __global__ void __launch_bounds__(256) k_assign(mtb_match* __restrict__ matches,
     for (int k = 0; k < 7; k++) res.pad[k] = 0;
     if (n == 0) { results[r] = res; return; }
 
-    mtb_match* M = matches + base;
-    sort_matches(M, n);
+    const mtb_match* M = matches + base;  // sorted by K5
     Path* L = localP + base;
     Path* P = pathsP + base;
     Path* C = combP + base;
@@ -429,7 +527,7 @@ __global__ void __launch_bounds__(256) k_assign(mtb_match* __restrict__ matches,
     results[r] = res;
 }
 
-void launch_assign(mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
+void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
                    uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
                    mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
     if (nReads == 0) return;

@@ -73,7 +73,12 @@ void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64
 uint64_t path_bytes();
 uint64_t quot_bytes();
 uint64_t clade_bytes();
-void launch_assign(mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
+void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                    uint64_t* gScratch, bool anyLarge, hipStream_t s);
+void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
+void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
+constexpr uint32_t kSegSortLds = 4096;  // segments up to this many matches sort in LDS
+void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
                    uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
                    mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st);
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
