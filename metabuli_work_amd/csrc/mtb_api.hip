@@ -56,6 +56,8 @@ struct mtb_ctx {
     uint64_t D = 0;
     uint64_t* dbv = nullptr;
     uint32_t* dbinfo = nullptr;
+    uint64_t* dirMem = nullptr;
+    AADir dir{};
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -81,11 +83,12 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
-    void* ptrs[] = {c->dbv, c->dbinfo, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->dbv = nullptr;
     c->dbinfo = nullptr;
+    c->dirMem = nullptr;
 }
 
 template <typename T>
@@ -139,6 +142,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(upload(&c->dbinfo, db.info, s));
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
+    c->dir = make_aa_dir(c->D, par->kmer_format);
+    HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
+    c->dir.dir = c->dirMem;
+    build_aa_dir(c->dbv, c->D, c->dir, c->dirMem, s);
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(dDiff);
     hipFree(dFlag);
@@ -399,7 +406,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     HIP_TRY(hipEventRecord(c->kev[4], s));
-    launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+    launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), s);
     HIP_TRY(hipEventRecord(c->kev[5], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
@@ -410,7 +417,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipEventRecord(c->kev[6], s));
-    launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+    launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));

@@ -475,11 +475,13 @@ void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uin
 
 // ------------------------------------------------------------------------------------------------
 // K4 merge-match (KmerMatcher::matchKmers, KmerMatcher.cpp:275-450; compareDna :1117-1146).
-// Queries are sorted by their AA part. Each wave brackets the DB range of its 64 queries with two
-// binary searches, then each lane finds its own AA run inside that window. Candidates are the
-// whole run except the DB's last k-mer (the reference's reader stops at diffIdxPos ==
-// numOfDiffIdx before loading it, KmerMatcher.cpp:363,378). Selected = hamming sum <=
-// min(2*min, 7). COUNT pass: per-read match counts. EMIT pass: records into per-read segments.
+// The reference streams the whole diffIdx DB past each sorted query split. Here the decoded DB
+// stays resident and a prefix directory built at open (below) maps the first L amino acids of a
+// k-mer to its DB bucket, so each query finds its AA run with one directory read plus a short
+// binary search inside the bucket. Candidates are the whole run except the DB's last k-mer (the
+// reference's reader stops at diffIdxPos == numOfDiffIdx before loading it,
+// KmerMatcher.cpp:363,378). Selected = hamming sum <= min(2*min, 7). COUNT pass: per-read match
+// counts. EMIT pass: records into per-read segments.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* __restrict__ a, uint64_t lo, uint64_t hi,
                                                     uint64_t key) {
@@ -490,29 +492,65 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* __restrict__
     return lo;
 }
 
+// AA-prefix bucket of a k-mer value. Format 2 packs 8 five-bit AA codes (first AA most
+// significant); format 1 is a base-21 integer of the same 8 codes. Query codes are 0..20, so
+// ranking the first L codes in base 21 is monotone in the k-mer order for both formats.
+__device__ __forceinline__ uint64_t aa_bucket(uint64_t v, const AADir& d) {
+    const uint64_t aa = v >> 24;
+    if (d.fmt != 2) return aa / d.div;
+    uint64_t r = 0;
+    for (int i = 0; i < d.L; i++) r = r * 21 + ((aa >> (5 * (7 - i))) & 31u);
+    return r;
+}
+
+// Smallest k-mer value in bucket b (digits of b in the top L AA slots, the rest zero).
+__device__ __forceinline__ uint64_t aa_bucket_floor(uint64_t b, const AADir& d) {
+    if (d.fmt != 2) return (b * d.div) << 24;
+    uint64_t aa = 0;
+    for (int i = d.L - 1; i >= 0; i--) {
+        aa |= (b % 21) << (5 * (7 - i));
+        b /= 21;
+    }
+    return aa << 24;
+}
+
+__global__ void k_build_dir(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
+    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > d.R) return;
+    dir[b] = (b == d.R) ? D : lower_bound_u64(dbv, 0, D, aa_bucket_floor(b, d));
+}
+
+AADir make_aa_dir(uint64_t D, int kmerFormat) {
+    AADir d{};
+    d.fmt = kmerFormat;
+    d.L = 1;
+    uint64_t R = 21;
+    while (d.L < 7 && R * 21 * 8 <= D) { R *= 21; d.L++; }
+    d.R = R;
+    d.div = 1;
+    for (int i = d.L; i < 8; i++) d.div *= 21;
+    return d;
+}
+
+void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s) {
+    k_build_dir<<<(unsigned)((d.R + 1 + 255) / 256), 256, 0, s>>>(dbv, D, d, dir);
+}
+
 template <bool EMIT>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
                                                uint64_t Q, const uint64_t* __restrict__ dbv,
-                                               const uint32_t* __restrict__ dbinfo, uint64_t D,
+                                               const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                                uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
                                                mtb_match* __restrict__ out, int* __restrict__ err) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    const uint64_t waveBase = gid - lane;
-    if (waveBase >= Q) return;
-    const uint64_t lastIdx = min(waveBase + 63, Q - 1);
-    // Wave window: [lower_bound(AA(first)), lower_bound(AA(last) + 2^24))
-    uint64_t winLo = 0, winHi = 0;
-    if (lane == 0) winLo = lower_bound_u64(dbv, 0, D, qkey[waveBase] & kAAMask);
-    if (lane == 1) winHi = lower_bound_u64(dbv, 0, D, (qkey[lastIdx] & kAAMask) + (1ull << 24));
-    winLo = __shfl(winLo, 0, 64);
-    winHi = __shfl(winHi, 1, 64);
     if (gid >= Q) return;
     const uint64_t key = qkey[gid];
     const uint64_t aa = key & kAAMask;
-    uint64_t lo = lower_bound_u64(dbv, winLo, winHi, aa);
-    uint64_t hi = lower_bound_u64(dbv, lo, winHi, aa + (1ull << 24));
+    const uint64_t bkt = aa_bucket(key, d);
+    const uint64_t b0 = d.dir[bkt], b1 = d.dir[bkt + 1];
+    uint64_t lo = lower_bound_u64(dbv, b0, b1, aa);
+    uint64_t hi = lower_bound_u64(dbv, lo, b1, aa + (1ull << 24));
     if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
     if (lo >= hi) return;
     uint32_t minSum = 255;
@@ -520,14 +558,12 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint32_t thr = min(minSum * 2u, 7u);
     const uint64_t info = qinfo[gid];
     const uint32_t seq = info_seq(info);
+    uint32_t c = 0;
+    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
     if (!EMIT) {
-        uint32_t c = 0;
-        for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
         if (c) atomicAdd(&readCnt[seq - 1], c);
         return;
     }
-    uint32_t c = 0;
-    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
     uint64_t w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
@@ -550,14 +586,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 }
 
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
-                  const uint32_t* dbinfo, uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
-                  uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err, hipStream_t s) {
+                  const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
+                  int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
+                  hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + 255) / 256);
-    if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, spOf, maxTax, kmerFormat, readCnt,
-                                                   readOff, out, err);
-    else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, spOf, maxTax, kmerFormat, readCnt,
-                                               readOff, out, err);
+    if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
+                                                   readCnt, readOff, out, err);
+    else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
+                                               readCnt, readOff, out, err);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

@@ -66,9 +66,22 @@ void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uin
                      uint64_t* idxTmp, void* scanTmp, hipStream_t s);
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s);
 
+// AA-prefix directory over the decoded DB: dir[b] = first DB index whose value is >= the
+// smallest value of bucket b (first L AAs ranked in base 21), dir[R] = D.
+struct AADir {
+    const uint64_t* dir;
+    uint64_t R;    // 21^L buckets
+    uint64_t div;  // 21^(8-L) (format 1 bucket = AA part / div)
+    int L;
+    int fmt;
+};
+AADir make_aa_dir(uint64_t D, int kmerFormat);
+void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s);
+
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
-                  const uint32_t* dbinfo, uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
-                  uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err, hipStream_t s);
+                  const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
+                  int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
+                  hipStream_t s);
 
 uint64_t path_bytes();
 uint64_t quot_bytes();
