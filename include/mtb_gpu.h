@@ -156,8 +156,9 @@ int mtb_last_kernel_ms(const mtb_ctx* ctx, float* ms, int n);
 int mtb_copy_results(mtb_ctx* ctx, void* dst, int dst_on_device);
 
 /* ---- staged entry points (per-stage parity against the oracle) ----------------------------- */
-/* Sorted query k-mers of the last batch (blank slots dropped), compareQueryKmer order
- * restricted to the AA part; requires MTB_KEEP_STAGES. */
+/* Query k-mers of the last batch (blank slots dropped) in the order K4 consumed them: grouped by
+ * the top 24 bits of the base-21 rank of their 8 AA codes (the index join needs locality, not
+ * compareQueryKmer's total order); requires MTB_KEEP_STAGES. */
 int mtb_get_query_kmers(mtb_ctx* ctx, mtb_kmer* out, uint64_t capacity, uint64_t* n_out);
 /* Matches of the last batch in compareMatches order (KmerMatcher.cpp:1149-1166); requires
  * MTB_KEEP_STAGES. */

@@ -388,10 +388,14 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     bool inB = false;
-    const int bitHi = 64;
+    // The index join (K4) does not need a total order: matches are put in compareMatches order per
+    // read by K5, a total order for a valid DB. Sorting on the top 24 bits of the 36-bit base-21
+    // AA rank groups queries whose AA k-mers share ~6 leading amino acids, which is all the
+    // locality the directory lookups need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[2], s));
     uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), c->keysB.as<uint64_t>(),
-                                  c->valsB.as<uint64_t>(), R, 24, bitHi, true, c->radixCounts.as<uint32_t>(),
+                                  c->valsB.as<uint64_t>(), R, kQuerySortLo, kQuerySortHi, true,
+                                  c->par.kmer_format == 2, c->radixCounts.as<uint32_t>(),
                                   c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;

@@ -294,13 +294,32 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
 // ------------------------------------------------------------------------------------------------
 // K2 LSD radix sort of (key, val) pairs on 8-bit digits of the key. Per pass: tile histograms
 // (digit-major so one device scan yields stable global offsets), scan, stable scatter through an
-// LDS-staged tile so each digit run leaves the block as one contiguous write. The first pass
-// (FILTER) drops sentinel keys: the compaction of blank reserved slots costs nothing extra.
+// LDS-staged tile so each digit run leaves the block as one contiguous write. Each wave ranks its
+// own 1024-key slice with match-any ballots against a wave-private histogram, so the tile needs
+// two block barriers per pass rather than several per 256 keys. The first pass (FILTER) drops
+// sentinel keys: the compaction of blank reserved slots costs nothing extra. RANK21 takes the
+// digits from the base-21 rank of a format-2 k-mer's eight 5-bit AA codes (36 dense bits instead of
+// 40 sparse ones), which is monotone in the k-mer order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kRadixItems = 16;
 constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
+constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
-template <bool FILTER>
+__device__ __forceinline__ uint64_t rank21_key(uint64_t k) {
+    const uint64_t aa = k >> 24;
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) r = r * 21 + ((aa >> (5 * i)) & 31u);
+    return (r << 24) | (k & 0xFFFFFFull);
+}
+
+template <bool RANK21>
+__device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) {
+    if (RANK21) k = rank21_key(k);
+    return (uint32_t)((k >> shift) & 0xFF);
+}
+
+template <bool FILTER, bool RANK21>
 __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
                                                     uint32_t* __restrict__ counts, uint32_t nTiles) {
     __shared__ uint32_t hist[256];
@@ -312,93 +331,85 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
         uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
         if (i < n) {
             uint64_t key = keys[i];
-            if (!FILTER || key != kSentinel) atomicAdd(&hist[(key >> shift) & 0xFF], 1u);
+            if (!FILTER || key != kSentinel) atomicAdd(&hist[radix_digit<RANK21>(key, shift)], 1u);
         }
     }
     __syncthreads();
     counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
 }
 
-template <bool FILTER>
+template <bool FILTER, bool RANK21>
 __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn,
                                                        const uint64_t* __restrict__ valsIn, uint64_t n, int shift,
                                                        const uint64_t* __restrict__ offs, uint32_t nTiles,
                                                        uint64_t* __restrict__ keysOut, uint64_t* __restrict__ valsOut) {
     __shared__ uint64_t sKey[kRadixTile];
     __shared__ uint64_t sVal[kRadixTile];
-    __shared__ uint32_t hist[256];
+    __shared__ uint8_t sDig[kRadixTile];
+    __shared__ uint32_t waveHist[kWaves][256];
     __shared__ uint32_t tileStart[256];
-    __shared__ uint32_t running[256];
-    __shared__ uint32_t waveCnt[kWaves][256];
+    __shared__ uint32_t sKept;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-
-    uint64_t k[kRadixItems], v[kRadixItems];
-    uint32_t vmask = 0;  // bit r: item r is a real (kept) element
-    hist[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
-        uint64_t i = base + (uint64_t)r * kBlock + tid;
-        k[r] = 0;
-        v[r] = 0;
-        if (i < n) {
-            k[r] = keysIn[i];
-            v[r] = valsIn[i];
-            if (!FILTER || k[r] != kSentinel) {
-                vmask |= 1u << r;
-                atomicAdd(&hist[(k[r] >> shift) & 0xFF], 1u);
-            }
-        }
-    }
-    __syncthreads();
-    unsigned long long tot;
-    unsigned long long ex = block_exclusive_scan(hist[tid], &tot);
-    tileStart[tid] = (uint32_t)ex;
-    running[tid] = 0;
+    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile + (uint64_t)w * kRadixSlice;
+    for (int x = tid; x < kWaves * 256; x += kBlock) (&waveHist[0][0])[x] = 0;
     __syncthreads();
 
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t k[kRadixItems], v[kRadixItems];
+    uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
 #pragma unroll
     for (int r = 0; r < kRadixItems; r++) {
-        const bool valid = (vmask >> r) & 1u;
-        const uint32_t d = (uint32_t)((k[r] >> shift) & 0xFF);
-        // lanes of this wave holding the same digit (match-any by 8 ballots)
+        const uint64_t i = base + (uint64_t)r * 64 + lane;
+        k[r] = 0;
+        v[r] = 0;
+        bool valid = false;
+        if (i < n) {
+            k[r] = keysIn[i];
+            v[r] = valsIn[i];
+            valid = !FILTER || k[r] != kSentinel;
+        }
+        const uint32_t d = valid ? radix_digit<RANK21>(k[r], shift) : 0u;
         unsigned long long peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
             unsigned long long m = __ballot(valid && ((d >> b) & 1u));
             peers &= ((d >> b) & 1u) ? m : ~m;
         }
-        for (int x = tid; x < kWaves * 256; x += kBlock) (&waveCnt[0][0])[x] = 0;
-        __syncthreads();
+        // every peer reads the running count before the group's first lane advances it; LDS
+        // operations of one wave complete in program order
+        const uint32_t before = valid ? waveHist[w][d] : 0u;
         const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
-        if (valid && rankInWave == 0) waveCnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        {
-            uint32_t s = running[tid];
-#pragma unroll
-            for (int ww = 0; ww < kWaves; ww++) {
-                uint32_t c = waveCnt[ww][tid];
-                waveCnt[ww][tid] = s;
-                s += c;
-            }
-            running[tid] = s;
-        }
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = tileStart[d] + waveCnt[w][d] + rankInWave;
-            sKey[pos] = k[r];
-            sVal[pos] = v[r];
-        }
-        __syncthreads();
+        if (valid && rankInWave == 0) waveHist[w][d] = before + (uint32_t)__popcll(peers);
+        rk[r] = valid ? (d << 16 | (before + rankInWave)) : ~0u;
     }
-    const uint32_t cnt = (uint32_t)tot;
-    for (uint32_t i = tid; i < cnt; i += kBlock) {
-        uint64_t key = sKey[i];
-        uint32_t d = (uint32_t)((key >> shift) & 0xFF);
-        uint64_t dst = offs[(uint64_t)d * nTiles + blockIdx.x] + (i - tileStart[d]);
-        keysOut[dst] = key;
+    __syncthreads();
+    {
+        uint32_t c[kWaves], sum = 0;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ww++) { c[ww] = waveHist[ww][tid]; sum += c[ww]; }
+        unsigned long long tot;
+        const uint32_t start = (uint32_t)block_exclusive_scan(sum, &tot);
+        tileStart[tid] = start;
+        if (tid == 0) sKept = (uint32_t)tot;
+        uint32_t run = start;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ww++) { waveHist[ww][tid] = run; run += c[ww]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRadixItems; r++) {
+        if (rk[r] == ~0u) continue;
+        const uint32_t d = rk[r] >> 16;
+        const uint32_t pos = waveHist[w][d] + (rk[r] & 0xFFFFu);
+        sKey[pos] = k[r];
+        sVal[pos] = v[r];
+        sDig[pos] = (uint8_t)d;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < sKept; i += kBlock) {
+        const uint32_t d = sDig[i];
+        const uint64_t dst = offs[(uint64_t)d * nTiles + blockIdx.x] + (i - tileStart[d]);
+        keysOut[dst] = sKey[i];
         valsOut[dst] = sVal[i];
     }
 }
@@ -409,8 +420,8 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 // filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
 // *inB tells which.
 uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
-                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s) {
+                          int bitHi, bool filter, bool rank21, uint32_t* counts, uint64_t* offs, void* scanTmp,
+                          bool* inB, hipStream_t s) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *vi = valsA, *ko = keysB, *vo = valsB;
     bool first = true;
@@ -418,17 +429,23 @@ uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uin
     for (int shift = bitLo; shift < bitHi; shift += 8) {
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
-        if (first && filter) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
-        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        const bool f = first && filter;
+        if (f && rank21) k_radix_hist<true, true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else if (f) k_radix_hist<true, false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else if (rank21) k_radix_hist<false, true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else k_radix_hist<false, false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
-        if (first && filter) {
-            k_radix_scatter<true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        if (f) {
+            if (rank21) k_radix_scatter<true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+            else k_radix_scatter<true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
             uint64_t kept = 0;
             hipMemcpyAsync(&kept, offs + 256ull * nTiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
             hipStreamSynchronize(s);
             cur = kept;
+        } else if (rank21) {
+            k_radix_scatter<false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         } else {
-            k_radix_scatter<false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+            k_radix_scatter<false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         }
         first = false;
         std::swap(ki, ko);
