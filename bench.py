@@ -108,8 +108,10 @@ def make_genomes_gpu(n_species, mean_len, strains, seed, dev):
 def make_reads_gpu(seq, off_t, n_pairs, seed, dev, read_len=150, sub_rate=0.005, random_frac=0.1):
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    glen = (off_t[1:] - off_t[:-1]).to(torch.float32)
-    gsel = torch.multinomial(glen, n_pairs, replacement=True, generator=g)
+    # genome chosen proportionally to its length (searchsorted on the offsets: torch.multinomial is
+    # not run-to-run deterministic on this device)
+    u = (torch.rand(n_pairs, device=dev, generator=g, dtype=torch.float64) * float(off_t[-1].item())).long()
+    gsel = torch.searchsorted(off_t[1:], u, right=True).clamp(max=off_t.numel() - 2)
     gl = (off_t[1:] - off_t[:-1])[gsel]
     ins = (torch.randn(n_pairs, device=dev, generator=g) * 30 + 300).round().long().clamp(min=read_len)
     ins = torch.minimum(ins, gl)

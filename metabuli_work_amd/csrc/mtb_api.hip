@@ -8,6 +8,7 @@
 
 #include "mtb_host.h"
 #include "mtb_launch.h"
+#include <cstdlib>
 
 using namespace mtb;
 
@@ -58,6 +59,7 @@ struct mtb_ctx {
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
     AADir dir{};
+    uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -67,7 +69,9 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, qcapOff, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf local, paths, comb, conn, spScore, spId, quot, clade, tcPool, tcLen, tcOff, tcOut, results;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead;
+    DevBuf local, paths, comb, conn, spScore, spKeep, quot,
+        gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
     uint32_t nReads = 0;
     uint64_t Q = 0, M = 0, nTaxcnt = 0;
@@ -142,6 +146,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(upload(&c->dbinfo, db.info, s));
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
+    if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
@@ -211,8 +216,8 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->qcapOff, &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->local, &c->paths,
-                      &c->comb, &c->conn, &c->spScore, &c->spId, &c->quot, &c->clade, &c->tcPool, &c->tcLen,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->local, &c->paths,
+                      &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->quot, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : c->ev)
@@ -285,7 +290,9 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->comb.ensure(path_bytes() * Mc));
     HIP_TRY(c->conn.ensure(Mc));
     HIP_TRY(c->spScore.ensure(sizeof(float) * Mc));
-    HIP_TRY(c->spId.ensure(sizeof(int32_t) * Mc));
+    HIP_TRY(c->spKeep.ensure(Mc));
+    for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Mc + 1)));
+    for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
     HIP_TRY(c->quot.ensure(quot_bytes() * std::max<uint64_t>(QC, 1)));
     HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
     HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Mc));
@@ -303,11 +310,39 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                    c->segScratch.as<uint64_t>(), maxSeg > 512, s);
     HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(hipEventRecord(c->kev[10], s));
+    // launch order: reads by descending match count (2-3 radix passes over n keys)
+    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(n + 1)));
+    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(n + 1) + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(n + 1) + n + Mc + 2)));
+    launch_order_keys(c->mOff.as<uint64_t>(), n, maxSeg, c->ordKA.as<uint64_t>(), c->ordVA.as<uint64_t>(), s);
+    int segBits = 8;
+    while (segBits < 32 && (maxSeg >> segBits)) segBits += 8;
+    bool ordInB = false;
+    radix_sort_pairs(c->ordKA.as<uint64_t>(), c->ordVA.as<uint64_t>(), c->ordKB.as<uint64_t>(), c->ordVB.as<uint64_t>(),
+                     n, 32, 32 + segBits, false, false, c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(),
+                     c->scanTmp.p, &ordInB, s);
+    const uint64_t* order = ordInB ? c->ordKB.as<uint64_t>() : c->ordKA.as<uint64_t>();
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
-    AssignScratch sc{c->local.p, c->paths.p, c->comb.p, c->conn.as<uint8_t>(), c->spScore.as<float>(),
-                     c->spId.as<int32_t>(), c->quot.p, c->clade.p, c->cladePerMatch};
+    AssignScratch sc{c->local.p,
+                     c->paths.p,
+                     c->comb.p,
+                     c->conn.as<uint8_t>(),
+                     c->gFlag.as<uint32_t>(),
+                     c->sFlag.as<uint32_t>(),
+                     c->pathCnt.as<uint32_t>(),
+                     c->gScan.as<uint64_t>(),
+                     c->sScan.as<uint64_t>(),
+                     c->gStart.as<uint64_t>(),
+                     c->sStart.as<uint64_t>(),
+                     c->spScore.as<float>(),
+                     c->spKeep.as<uint8_t>(),
+                     c->scanTmp.p,
+                     c->quot.p,
+                     c->clade.p,
+                     c->cladePerMatch};
     launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
-                  n, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
+                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), order, s);
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -360,27 +395,38 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
             dOff2 = c->off2.as<uint64_t>();
         }
     }
-    // K0: read metadata and reserved slots (KmerExtractor.cpp:442-494, Buffer::reserveMemory)
+    // K0: read metadata (KmerExtractor.cpp:442-494) and K1 work units
     HIP_TRY(c->meta.ensure(sizeof(ReadMeta) * (n + 1)));
-    HIP_TRY(c->reserve.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->reserve.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->slotOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->maxSeg.ensure(sizeof(uint32_t)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
-    launch_read_meta(dOff1, dOff2, n, paired, c->meta.as<ReadMeta>(), c->reserve.as<uint64_t>(), c->qlen.as<uint32_t>(), s);
-    exclusive_scan_u64(c->reserve.as<uint64_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
-    uint64_t R = 0;
-    HIP_TRY(hipMemcpyAsync(&R, c->slotOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    launch_read_meta(dOff1, dOff2, n, paired, c->meta.as<ReadMeta>(), c->qlen.as<uint32_t>(), c->maxSeg.as<uint32_t>(),
+                     s);
+    uint32_t maxW = 0;
+    HIP_TRY(hipMemcpyAsync(&maxW, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    // K1 extract into reserved slots
+    // chunk = the longest frame when it is short (no padding for uniform short reads), else 64
+    const uint32_t C = std::min<uint32_t>(std::max<uint32_t>(maxW, 1), 64);
+    launch_read_units(c->meta.as<ReadMeta>(), n, C, c->reserve.as<uint32_t>(), s);
+    exclusive_scan_u32(c->reserve.as<uint32_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
+    uint64_t U = 0;
+    HIP_TRY(hipMemcpyAsync(&U, c->slotOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(c->unitRead.ensure(sizeof(uint32_t) * std::max<uint64_t>(U, 1)));
+    launch_unit_read(c->slotOff.as<uint64_t>(), n, c->unitRead.as<uint32_t>(), s);
+    const uint64_t R = extract_slots(U, C);
+    // K1 extract
     const uint64_t Rc = std::max<uint64_t>(R, 1);
     HIP_TRY(c->keysA.ensure(8 * Rc));
     HIP_TRY(c->valsA.ensure(8 * Rc));
     HIP_TRY(c->keysB.ensure(8 * Rc));
     HIP_TRY(c->valsB.ensure(8 * Rc));
     HIP_TRY(hipEventRecord(c->kev[0], s));
-    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(), n, paired, c->tables,
-                   c->par.kmer_format, c->par.syncmer, c->par.smer_len, c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(),
-                   s);
+    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                   c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
+                   c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[1], s));
     HIP_TRY(hipEventRecord(c->ev[1], s));
     // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
@@ -409,9 +455,12 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
+    HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
     HIP_TRY(hipEventRecord(c->kev[4], s));
+    launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
-                 c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), s);
+                 c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), c->matchWinCap,
+                 c->matchWin.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[5], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t M = 0;
@@ -422,7 +471,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipEventRecord(c->kev[6], s));
     launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
-                 c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
+                 c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(),
+                 c->matchWinCap, c->matchWin.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     // K5 + K6

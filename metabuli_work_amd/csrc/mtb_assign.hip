@@ -217,16 +217,225 @@ __device__ __forceinline__ int ham_fields(uint32_t reh, int range, bool left) {
     return s;
 }
 
-__global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ matches, const uint64_t* __restrict__ mOff,
-                                                const uint32_t* __restrict__ qlen, const uint64_t* __restrict__ qOff,
-                                                uint32_t nReads, AssignCfg cfg, TaxView tax, Path* __restrict__ localP,
-                                                Path* __restrict__ pathsP, Path* __restrict__ combP,
-                                                uint8_t* __restrict__ connP, float* __restrict__ spScoreP,
-                                                int32_t* __restrict__ spIdP, Quot* __restrict__ quotP,
-                                                Clade* __restrict__ cladeP, uint32_t cladePerMatch,
-                                                mtb_taxcnt* __restrict__ tcP, mtb_result* __restrict__ results) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nReads) return;
+// ------------------------------------------------------------------------------------------------
+// K6 as three kernels over the sorted match array. Work items are the runs the reference loops
+// over (Taxonomer.cpp:316-408): (read, species, frame) groups for getMatchPaths, (read, species)
+// runs for combineMatchPaths, reads for chooseBestTaxon onward. Neighbouring lanes take
+// neighbouring runs, so a wave's loads and scratch writes fall in one contiguous stretch of the
+// match array instead of 64 unrelated per-read segments.
+// ------------------------------------------------------------------------------------------------
+
+// Run boundaries: group starts where the read, species or frame changes; species runs where the
+// read or species changes.
+__global__ void k_run_flags(const mtb_match* __restrict__ M, uint64_t nM, uint32_t* __restrict__ gFlag,
+                            uint32_t* __restrict__ sFlag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nM) return;
+    uint32_t g = 1, sp = 1;
+    if (i > 0) {
+        const mtb_match a = M[i - 1], b = M[i];
+        const bool newSp = info_seq(a.qinfo) != info_seq(b.qinfo) || a.species_id != b.species_id;
+        sp = newSp;
+        g = newSp || info_frame(a.qinfo) != info_frame(b.qinfo);
+    }
+    gFlag[i] = g;
+    sFlag[i] = sp;
+}
+
+__global__ void k_run_starts(const uint32_t* __restrict__ gFlag, const uint32_t* __restrict__ sFlag,
+                             const uint64_t* __restrict__ gScan, const uint64_t* __restrict__ sScan, uint64_t nM,
+                             uint64_t* __restrict__ gStart, uint64_t* __restrict__ sStart) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nM) {
+        if (gFlag[i]) gStart[gScan[i]] = i;
+        if (sFlag[i]) sStart[sScan[i]] = i;
+    }
+    if (i == 0) {
+        gStart[gScan[nM]] = nM;
+        sStart[sScan[nM]] = nM;
+    }
+}
+
+// getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
+// P[gs + k] in emission order; L and conn are indexed by match.
+__global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
+                                                     uint64_t nG, AssignCfg cfg, TaxView tax, Path* __restrict__ L,
+                                                     Path* __restrict__ P, uint8_t* __restrict__ conn,
+                                                     uint32_t* __restrict__ pathCnt) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nG) return;
+    const uint64_t start = gStart[g], end = gStart[g + 1];
+    if (end - start <= 1) { pathCnt[g] = 0; return; }
+    const int32_t sp = (int32_t)M[start].species_id;
+    const uint32_t curFrame = info_frame(M[start].qinfo);
+    int minDepth = cfg.minConsCnt;
+    if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
+    const bool fwd = curFrame < 3;
+    for (uint64_t x = start; x < end; x++) conn[x] = 0;
+    uint64_t nP = start;
+    uint64_t k = start;
+    uint64_t currPos = info_pos(M[start].qinfo);
+    auto initPath = [&](uint64_t idx) {
+        Path p;
+        p.start = (int)info_pos(M[idx].qinfo);
+        p.end = p.start + 23;
+        p.score = score_fields(M[idx].right_end_hamming, 8, false);
+        p.hd = M[idx].hamming;
+        p.depth = 1;
+        p.sm = p.em = (uint32_t)idx;
+        L[idx] = p;
+    };
+    uint64_t curS = k;
+    while (k < end && info_pos(M[k].qinfo) == currPos) { initPath(k); ++k; }
+    uint64_t curE = k;
+    while (k < end) {
+        const uint32_t nextPos = info_pos(M[k].qinfo);
+        const uint64_t nxS = k;
+        while (k < end && info_pos(M[k].qinfo) == nextPos) { initPath(k); ++k; }
+        const uint64_t nxE = k;
+        const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
+        if (shift > 0 && shift <= cfg.maxCodonShift) {
+            const uint32_t sh = 3u * (uint32_t)shift;
+            const uint32_t lowMask = (1u << (24u - sh)) - 1u;
+            for (uint64_t nx = nxS; nx < nxE; nx++) {
+                const uint32_t nreh = M[nx].right_end_hamming;
+                float inc = 0.0f;
+                int hinc = 0;
+                for (int c = 0; c < shift; c++) {
+                    uint32_t h = (nreh >> (2 * c)) & 3u;
+                    inc += codon_score(h);
+                    hinc += (int)h;
+                }
+                int64_t best = -1;
+                float bestScore = 0.0f;
+                const uint32_t dn = M[nx].dna_encoding;
+                for (uint64_t cu = curS; cu < curE; cu++) {
+                    const uint32_t dc = M[cu].dna_encoding;
+                    bool cons;
+                    if (cfg.kmerFormat == 2) {  // isConsecutive2 (Taxonomer.cpp:692-699)
+                        cons = fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
+                    } else {                    // isConsecutive (Taxonomer.cpp:677-683)
+                        cons = fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
+                    }
+                    if (cons) {
+                        conn[cu] = 1;
+                        if (L[cu].score > bestScore) { best = (int64_t)cu; bestScore = L[cu].score; }
+                    }
+                }
+                if (best >= 0) {
+                    const Path bp = L[best];
+                    Path& np = L[nx];
+                    np.start = bp.start;
+                    np.score = bp.score + inc;
+                    np.hd = bp.hd + hinc;
+                    np.depth = bp.depth + shift;
+                    np.sm = bp.sm;
+                }
+            }
+        }
+        for (uint64_t cu = curS; cu < curE; cu++)
+            if (!conn[cu] && L[cu].depth >= minDepth) P[nP++] = L[cu];
+        if (k == end)
+            for (uint64_t nx = nxS; nx < nxE; nx++)
+                if (L[nx].depth >= minDepth) P[nP++] = L[nx];
+        curS = nxS;
+        curE = nxE;
+        currPos = nextPos;
+    }
+    pathCnt[g] = (uint32_t)(nP - start);
+}
+
+// combineMatchPaths (Taxonomer.cpp:410-468) and the species score (:380-395) for one (read,
+// species) run [ss, se): its groups' paths are packed in frame order (the order the reference
+// appends them), sorted with the libstdc++ introsort emulation and combined greedily.
+__global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ sStart,
+                                                       uint64_t nS, const uint64_t* __restrict__ gScan,
+                                                       const uint64_t* __restrict__ gStart,
+                                                       const uint32_t* __restrict__ pathCnt,
+                                                       const uint32_t* __restrict__ qlen, AssignCfg cfg,
+                                                       Path* __restrict__ P, Path* __restrict__ C,
+                                                       float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nS) return;
+    const uint64_t ss = sStart[s], se = sStart[s + 1];
+    uint64_t w = ss;
+    for (uint64_t g = gScan[ss]; gStart[g] < se; g++) {
+        const uint64_t src = gStart[g];
+        const uint32_t cnt = pathCnt[g];
+        if (src != w)
+            for (uint32_t k = 0; k < cnt; k++) P[w + k] = P[src + k];
+        w += cnt;
+    }
+    if (w == ss) { spKeep[s] = 0; return; }
+    Path* Ps = P + ss;
+    const long nP = (long)(w - ss);
+    const int readLength = (int)qlen[info_seq(M[ss].qinfo) - 1];
+    stdsort::sort(Ps, Ps + nP, [](const Path& a, const Path& b) {
+        if (a.score != b.score) return a.score > b.score;
+        if (a.hd != b.hd) return a.hd < b.hd;
+        return a.start > b.start;
+    });
+    Path* Cs = C + ss;
+    long nC = 0;
+    float score = 0.0f;
+    for (long pi = 0; pi < nP; pi++) {
+        if (nC == 0) {
+            Cs[nC++] = Ps[pi];
+            score += Ps[pi].score;
+            continue;
+        }
+        bool overlapped = false;
+        for (long j = 0; j < nC; j++) {
+            Path& p = Ps[pi];
+            const Path c = Cs[j];
+            if ((p.end < c.start) || (c.end < p.start)) continue;
+            const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
+            if (ol == p.end - p.start + 1) { overlapped = true; break; }
+            if (ol < 24) {  // trimMatchPath (Taxonomer.cpp:475-485)
+                const int range = ol / 3;
+                if (p.start < c.start) {
+                    const uint32_t reh = M[p.em].right_end_hamming;
+                    p.end = c.start - 1;
+                    p.hd = max(0, p.hd - ham_fields(reh, range, false));
+                    p.score = p.score - score_fields(reh, range, false) - (float)(ol % 3);
+                } else {
+                    const uint32_t reh = M[p.sm].right_end_hamming;
+                    p.start = c.end + 1;
+                    p.hd = max(0, p.hd - ham_fields(reh, range, true));
+                    p.score = p.score - score_fields(reh, range, true) - (float)(ol % 3);
+                }
+                continue;
+            }
+            overlapped = true;
+            break;
+        }
+        if (!overlapped) {
+            Cs[nC++] = Ps[pi];
+            score += Ps[pi].score;
+        }
+    }
+    score = score / (float)readLength;
+    score = (1.0f < score) ? 1.0f : score;  // std::min(score, 1.0f)
+    spScore[s] = score;
+    spKeep[s] = !(score < cfg.minScore);
+}
+
+// chooseBestTaxon (Taxonomer.cpp:130-202), filterRedundantMatches (:205-241), taxCnt and the
+// lower-rank BFS (:252-314) for one read.
+__global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff,
+                                                      const uint32_t* __restrict__ qlen,
+                                                      const uint64_t* __restrict__ qOff, uint32_t nReads,
+                                                      const uint64_t* __restrict__ order,
+                                                      const uint64_t* __restrict__ sScan,
+                                                      const uint64_t* __restrict__ sStart,
+                                                      const float* __restrict__ spScore,
+                                                      const uint8_t* __restrict__ spKeep, AssignCfg cfg, TaxView tax,
+                                                      Quot* __restrict__ quotP, Clade* __restrict__ cladeP,
+                                                      uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
+                                                      mtb_result* __restrict__ results) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= nReads) return;
+    const uint32_t r = order ? (uint32_t)order[gid] : gid;  // heaviest reads first (k_order_keys)
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
     const int readLength = (int)qlen[r];
@@ -241,158 +450,16 @@ __global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ ma
     for (int k = 0; k < 7; k++) res.pad[k] = 0;
     if (n == 0) { results[r] = res; return; }
 
-    const mtb_match* M = matches + base;  // sorted by K5
-    Path* L = localP + base;
-    Path* P = pathsP + base;
-    Path* C = combP + base;
-    uint8_t* conn = connP + base;
-    float* spScore = spScoreP + base;
-    int32_t* spId = spIdP + base;
-
-    // ---- getBestSpeciesMatches (Taxonomer.cpp:316-408) ----
-    long nP = 0, nC = 0, nS = 0, meaningful = 0;
+    // ---- getBestSpeciesMatches tail (Taxonomer.cpp:380-408) over the read's species runs ----
+    const uint64_t s0 = sScan[base], s1 = sScan[base + n];
+    long meaningful = 0;
     float bestSpScore = 0.0f;
-    long bestFirst = 0, bestSecond = 0;
-    long i = 0;
-    while (i < n) {
-        const int32_t sp = (int32_t)M[i].species_id;
-        const long spStart = i;
-        const long prevP = nP;
-        while (i < n && (int32_t)M[i].species_id == sp) {
-            const uint32_t curFrame = info_frame(M[i].qinfo);
-            const long fs = i;
-            while (i < n && (int32_t)M[i].species_id == sp && info_frame(M[i].qinfo) == curFrame) i++;
-            if (i - fs <= 1) continue;
-            // ---- getMatchPaths(fs, i) (Taxonomer.cpp:487-648) ----
-            const long start = fs, end = i;
-            int minDepth = cfg.minConsCnt;
-            if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
-            const bool fwd = curFrame < 3;
-            for (long x = 0; x < end - start; x++) conn[x] = 0;
-            long k = start;
-            uint64_t currPos = info_pos(M[start].qinfo);
-            auto initPath = [&](long idx) {
-                Path p;
-                p.start = (int)info_pos(M[idx].qinfo);
-                p.end = p.start + 23;
-                p.score = score_fields(M[idx].right_end_hamming, 8, false);
-                p.hd = M[idx].hamming;
-                p.depth = 1;
-                p.sm = p.em = (uint32_t)idx;
-                L[idx - start] = p;
-            };
-            long curS = k;
-            while (k < end && info_pos(M[k].qinfo) == currPos) { initPath(k); ++k; }
-            long curE = k;
-            while (k < end) {
-                const uint32_t nextPos = info_pos(M[k].qinfo);
-                const long nxS = k;
-                while (k < end && info_pos(M[k].qinfo) == nextPos) { initPath(k); ++k; }
-                const long nxE = k;
-                const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
-                if (shift > 0 && shift <= cfg.maxCodonShift) {
-                    const uint32_t sh = 3u * (uint32_t)shift;
-                    const uint32_t lowMask = (1u << (24u - sh)) - 1u;
-                    for (long nx = nxS; nx < nxE; nx++) {
-                        const uint32_t nreh = M[nx].right_end_hamming;
-                        float inc = 0.0f;
-                        int hinc = 0;
-                        for (int c = 0; c < shift; c++) {
-                            uint32_t h = (nreh >> (2 * c)) & 3u;
-                            inc += codon_score(h);
-                            hinc += (int)h;
-                        }
-                        long best = -1;
-                        float bestScore = 0.0f;
-                        const uint32_t dn = M[nx].dna_encoding;
-                        for (long cu = curS; cu < curE; cu++) {
-                            const uint32_t dc = M[cu].dna_encoding;
-                            bool cons;
-                            if (cfg.kmerFormat == 2) {  // isConsecutive2 (Taxonomer.cpp:692-699)
-                                cons = fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
-                            } else {                    // isConsecutive (Taxonomer.cpp:677-683)
-                                cons = fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
-                            }
-                            if (cons) {
-                                conn[cu - start] = 1;
-                                if (L[cu - start].score > bestScore) { best = cu; bestScore = L[cu - start].score; }
-                            }
-                        }
-                        if (best >= 0) {
-                            const Path bp = L[best - start];
-                            Path& np = L[nx - start];
-                            np.start = bp.start;
-                            np.score = bp.score + inc;
-                            np.hd = bp.hd + hinc;
-                            np.depth = bp.depth + shift;
-                            np.sm = bp.sm;
-                        }
-                    }
-                }
-                for (long cu = curS; cu < curE; cu++)
-                    if (!conn[cu - start] && L[cu - start].depth >= minDepth) P[nP++] = L[cu - start];
-                if (k == end)
-                    for (long nx = nxS; nx < nxE; nx++)
-                        if (L[nx - start].depth >= minDepth) P[nP++] = L[nx - start];
-                curS = nxS;
-                curE = nxE;
-                currPos = nextPos;
-            }
-        }
-        if (nP > prevP) {
-            // ---- combineMatchPaths (Taxonomer.cpp:410-468) ----
-            stdsort::sort(P + prevP, P + nP, [](const Path& a, const Path& b) {
-                if (a.score != b.score) return a.score > b.score;
-                if (a.hd != b.hd) return a.hd < b.hd;
-                return a.start > b.start;
-            });
-            float score = 0.0f;
-            const long combStart = nC;
-            for (long pi = prevP; pi < nP; pi++) {
-                if (combStart == nC) {
-                    C[nC++] = P[pi];
-                    score += P[pi].score;
-                    continue;
-                }
-                bool overlapped = false;
-                for (long j = combStart; j < nC; j++) {
-                    Path& p = P[pi];
-                    const Path c = C[j];
-                    if ((p.end < c.start) || (c.end < p.start)) continue;
-                    const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
-                    if (ol == p.end - p.start + 1) { overlapped = true; break; }
-                    if (ol < 24) {  // trimMatchPath (Taxonomer.cpp:475-485)
-                        const int range = ol / 3;
-                        if (p.start < c.start) {
-                            const uint32_t reh = M[p.em].right_end_hamming;
-                            p.end = c.start - 1;
-                            p.hd = max(0, p.hd - ham_fields(reh, range, false));
-                            p.score = p.score - score_fields(reh, range, false) - (float)(ol % 3);
-                        } else {
-                            const uint32_t reh = M[p.sm].right_end_hamming;
-                            p.start = c.end + 1;
-                            p.hd = max(0, p.hd - ham_fields(reh, range, true));
-                            p.score = p.score - score_fields(reh, range, true) - (float)(ol % 3);
-                        }
-                        continue;
-                    }
-                    overlapped = true;
-                    break;
-                }
-                if (!overlapped) {
-                    C[nC++] = P[pi];
-                    score += P[pi].score;
-                }
-            }
-            score = score / (float)readLength;
-            score = (1.0f < score) ? 1.0f : score;  // std::min(score, 1.0f)
-            if (score < cfg.minScore) continue;
-            spId[nS] = sp;
-            spScore[nS] = score;
-            nS++;
-            if (score > 0.f) meaningful++;
-            if (score > bestSpScore) { bestSpScore = score; bestFirst = spStart; bestSecond = i; }
-        }
+    uint64_t bestFirst = 0, bestSecond = 0;
+    for (uint64_t s = s0; s < s1; s++) {
+        if (!spKeep[s]) continue;
+        const float score = spScore[s];
+        if (score > 0.f) meaningful++;
+        if (score > bestSpScore) { bestSpScore = score; bestFirst = sStart[s]; bestSecond = sStart[s + 1]; }
     }
 
     // ---- chooseBestTaxon (Taxonomer.cpp:130-202) ----
@@ -403,11 +470,12 @@ __global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ ma
         const float thr = bestSpScore * cfg.tieRatio;
         long cnt = 0;
         int lcaNode = -1;
-        for (long s = 0; s < nS; s++) {
+        for (uint64_t s = s0; s < s1; s++) {
+            if (!spKeep[s]) continue;
             if (spScore[s] >= thr) {
                 cnt++;
                 spTotal += spScore[s];
-                int32_t t = spId[s];
+                const int32_t t = (int32_t)M[sStart[s]].species_id;
                 if (cnt == 1) bestTax = t;
                 if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
             }
@@ -435,7 +503,7 @@ __global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ ma
     Quot* Qs = quotP + qOff[r];
     const long maxQ = (long)((readLength + 3) / cfg.dnaShift);
     for (long q = 0; q <= maxQ; q++) { Qs[q].has = 0; Qs[q].minH = 255; Qs[q].tax = 0; }
-    for (long x = bestFirst; x < bestSecond; x++) {
+    for (uint64_t x = bestFirst; x < bestSecond; x++) {
         const long q = (long)(info_pos(M[x].qinfo) / (uint32_t)cfg.dnaShift);
         const uint8_t h = M[x].hamming;
         const int32_t t = (int32_t)M[x].target_id;
@@ -527,16 +595,56 @@ __global__ void __launch_bounds__(256) k_assign(const mtb_match* __restrict__ ma
     results[r] = res;
 }
 
+// Keys that order reads by descending match count (stable): one thread per read runs the whole
+// decision tree, so a wave costs as much as its heaviest read and the grid as much as its last
+// waves. Launching heavy reads first and grouping reads of similar weight in a wave keeps the
+// SIMDs busy (longest-processing-time-first).
+__global__ void k_order_keys(const uint64_t* __restrict__ mOff, uint32_t nReads, uint32_t maxSeg,
+                             uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nReads) return;
+    const uint32_t c = (uint32_t)(mOff[r + 1] - mOff[r]);
+    keys[r] = ((uint64_t)(maxSeg - c) << 32) | r;
+    vals[r] = r;
+}
+
+void launch_order_keys(const uint64_t* mOff, uint32_t nReads, uint32_t maxSeg, uint64_t* keys, uint64_t* vals,
+                       hipStream_t s) {
+    if (nReads) k_order_keys<<<(nReads + 255) / 256, 256, 0, s>>>(mOff, nReads, maxSeg, keys, vals);
+}
+
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
-                   uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
+                   uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, const uint64_t* order, hipStream_t st) {
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
                   a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio};
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
-    k_assign<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, qOff, nReads, cfg, tv, (Path*)s.local,
-                                                   (Path*)s.paths, (Path*)s.comb, s.conn, s.spScore, s.spId,
-                                                   (Quot*)s.quot, (Clade*)s.clade, s.cladePerMatch, tcPool, results);
+    if (nM) {
+        const unsigned bm = (unsigned)((nM + 255) / 256);
+        k_run_flags<<<bm, 256, 0, st>>>(matches, nM, s.gFlag, s.sFlag);
+        exclusive_scan_u32(s.gFlag, nM, s.gScan, s.scanTmp, st);
+        exclusive_scan_u32(s.sFlag, nM, s.sScan, s.scanTmp, st);
+        k_run_starts<<<bm, 256, 0, st>>>(s.gFlag, s.sFlag, s.gScan, s.sScan, nM, s.gStart, s.sStart);
+        // groups and runs never outnumber matches: size the grids by nM, threads past the count exit
+        uint64_t cnt[2] = {0, 0};
+        hipMemcpyAsync(&cnt[0], s.gScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&cnt[1], s.sScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        if (cnt[0])
+            k_match_paths<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(matches, s.gStart, cnt[0], cfg, tv,
+                                                                             (Path*)s.local, (Path*)s.paths, s.conn,
+                                                                             s.pathCnt);
+        if (cnt[1])
+            k_combine_paths<<<(unsigned)((cnt[1] + 255) / 256), 256, 0, st>>>(
+                matches, s.sStart, cnt[1], s.gScan, s.gStart, s.pathCnt, qlen, cfg, (Path*)s.paths, (Path*)s.comb,
+                s.spScore, s.spKeep);
+    } else {
+        hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
+    }
+    k_choose_taxon<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, qOff, nReads, order, s.sScan, s.sStart,
+                                                         s.spScore, s.spKeep, cfg, tv, (Quot*)s.quot,
+                                                         (Clade*)s.clade, s.cladePerMatch, tcPool, results);
 }
 
 uint64_t path_bytes() { return sizeof(Path); }

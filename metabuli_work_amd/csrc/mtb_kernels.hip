@@ -119,13 +119,13 @@ void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp
 }
 
 // ------------------------------------------------------------------------------------------------
-// K0 read metadata: loadChunkOfReads (KmerExtractor.cpp:442-494). Per read: covered lengths,
-// windows per frame of each mate (0 when the read is dropped by the shared empty rule), reserved
-// slots = getQueryKmerNumber of both mates (one slot per frame window).
+// K0 read metadata: loadChunkOfReads (KmerExtractor.cpp:442-494). Per read: covered lengths and
+// windows per frame of each mate (0 when the read is dropped by the shared empty rule); the batch
+// maximum sizes K1's chunks.
 // ------------------------------------------------------------------------------------------------
 __global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* __restrict__ off2, uint32_t n,
-                            int paired, ReadMeta* __restrict__ meta, uint64_t* __restrict__ reserve,
-                            uint32_t* __restrict__ qlen) {
+                            int paired, ReadMeta* __restrict__ meta, uint32_t* __restrict__ qlen,
+                            uint32_t* __restrict__ maxW) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int len1 = (int)(off1[i + 1] - off1[i]);
@@ -144,19 +144,48 @@ __global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* _
     m.w1 = empty ? 0 : w1;
     m.w2 = (empty || !paired) ? 0 : w2;
     meta[i] = m;
-    reserve[i] = 6ull * (uint64_t)(m.w1 + m.w2);
     qlen[i] = (uint32_t)(ql1 + ql2);
+    const uint32_t w = (uint32_t)max(m.w1, m.w2);
+    if (w) atomicMax(maxW, w);
+}
+
+// K1 work units per read: each (mate, frame) is cut into chunks of C windows.
+__global__ void k_read_units(const ReadMeta* __restrict__ meta, uint32_t n, uint32_t C, uint32_t* __restrict__ units) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ReadMeta m = meta[i];
+    units[i] = 6u * ((uint32_t)(m.w1 + C - 1) / C + (uint32_t)(m.w2 + C - 1) / C);
+}
+
+__global__ void k_unit_read(const uint64_t* __restrict__ uOff, uint32_t n, uint32_t* __restrict__ unitRead) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (uint64_t u = uOff[i]; u < uOff[i + 1]; u++) unitRead[u] = i;
 }
 
 void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
-                      uint64_t* reserve, uint32_t* qlen, hipStream_t s) {
+                      uint32_t* qlen, uint32_t* maxW, hipStream_t s) {
+    hipMemsetAsync(maxW, 0, sizeof(uint32_t), s);
     if (n == 0) return;
-    k_read_meta<<<(n + 255) / 256, 256, 0, s>>>(off1, off2, n, paired, meta, reserve, qlen);
+    k_read_meta<<<(n + 255) / 256, 256, 0, s>>>(off1, off2, n, paired, meta, qlen, maxW);
+}
+
+void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t* units, hipStream_t s) {
+    if (n) k_read_units<<<(n + 255) / 256, 256, 0, s>>>(meta, n, C, units);
+}
+
+void launch_unit_read(const uint64_t* uOff, uint32_t n, uint32_t* unitRead, hipStream_t s) {
+    if (n) k_unit_read<<<(n + 255) / 256, 256, 0, s>>>(uOff, n, unitRead);
 }
 
 // ------------------------------------------------------------------------------------------------
-// K1 extract: one thread per (read, mate, frame) runs the frame's scanner over its codons and
-// writes one reserved slot per window (fillQueryKmerBuffer, KmerExtractor.cpp:355-386). A window
+// K1 extract (fillQueryKmerBuffer, KmerExtractor.cpp:355-386): one thread per work unit = a chunk
+// of C consecutive windows of one (read, mate, frame). It loads the chunk's codons plus the 7
+// before its first window's last codon (a window depends on its own 8 codons only) and writes
+// window p of the chunk to slot (unit / 64) * 64C + 64p + unit % 64: the 64 lanes of a wave
+// store 64 consecutive slots per window step, so every store is one coalesced line. Pre-sort
+// slot order is free (K2 reorders everything) and slots past a chunk's windows get the sentinel.
+// A window
 // is emitted iff its 8 codons translate (the N-restart of MetamerScanner::next,
 // KmerScanner.h:82-117) and, with syncmers, its earliest-minimum s-mer sits at either end
 // (SyncmerScanner::next, SyncmerScanner.h:36-102). Blank windows get the sentinel key, which
@@ -175,30 +204,45 @@ struct ExtractTables {
 
 __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                  const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
-                                                 const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ slotOff,
-                                                 uint32_t nReads, int paired, ExtractTables tabs, int kmerFormat,
-                                                 int syncmer, int smerLen, uint64_t* __restrict__ keys,
-                                                 uint64_t* __restrict__ vals) {
+                                                 const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
+                                                 const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
+                                                 ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
+                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     sBase[threadIdx.x] = tabs.base[threadIdx.x];
     if (threadIdx.x < 64) { sAA[threadIdx.x] = tabs.aa[threadIdx.x]; sNum[threadIdx.x] = tabs.num[threadIdx.x]; }
     __syncthreads();
 
-    const int perRead = paired ? 12 : 6;
-    uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= (uint64_t)nReads * perRead) return;
-    uint32_t r = (uint32_t)(tid / perRead);
-    int sub = (int)(tid % perRead);
-    int mate = sub / 6, frame = sub % 6;
-    ReadMeta m = meta[r];
-    int W = mate ? m.w2 : m.w1;
-    if (W <= 0) return;
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
+    int W = 0, pFirst = 0, nWin = 0;
+    uint32_t r = 0;
+    int mate = 0, frame = 0;
+    if (u < nUnits) {
+        r = unitRead[u];
+        const ReadMeta m0 = meta[r];
+        uint32_t local = (uint32_t)(u - uOff[r]);
+        const uint32_t c1 = (uint32_t)(m0.w1 + C - 1) / C, c2 = (uint32_t)(m0.w2 + C - 1) / C;
+        uint32_t cpf = c1;
+        if (local >= 6 * c1) { local -= 6 * c1; mate = 1; cpf = c2; }
+        frame = (int)(local / cpf);
+        const int chunk = (int)(local % cpf);
+        W = mate ? m0.w2 : m0.w1;
+        pFirst = chunk * (int)C;
+        nWin = min((int)C, W - pFirst);
+    }
+    // slots of this unit past its windows (and of padding units) hold the sentinel
+    for (int p = max(nWin, 0); p < (int)C; p++) {
+        keys[slotBase + 64ull * p] = kSentinel;
+        vals[slotBase + 64ull * p] = 0;
+    }
+    if (nWin <= 0) return;
+    const ReadMeta m = meta[r];
     const uint8_t* seq = mate ? seq2 + off2[r] : seq1 + off1[r];
     int len = mate ? m.len2 : m.len1;
     int used = mate ? m.ql2 : m.ql1;
     uint32_t posOffset = mate ? (uint32_t)m.ql1 + 3u : 0u;  // KmerExtractor.cpp:341-345
-    uint64_t slot = slotOff[r] + (mate ? 6ull * (uint64_t)m.w1 : 0ull) + (uint64_t)frame * (uint64_t)W;
     const bool fwd = frame < 3;
     int begin;
     if (fwd) begin = frame;
@@ -215,7 +259,8 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
     uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
     const uint64_t smMask = (smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1);
     int run = 0;
-    for (int j = 0; j < aaLen; j++) {
+    (void)aaLen;
+    for (int j = pFirst; j < pFirst + nWin + 7; j++) {
         int c0 = fromLeft ? s0 + 3 * j : e0 - 3 * j;  // first base of the triplet in load order
         uint32_t b1, b2, b3;
         if (fromLeft) {
@@ -243,7 +288,7 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
         if (syncmer) {
             sm7 = sm6; sm6 = sm5; sm5 = sm4; sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = sm0; sm0 = smAcc;
         }
-        if (j < 7) continue;
+        if (j < pFirst + 7) continue;
         const int p = j - 7;
         bool ok = run >= 8;
         if (ok && syncmer) {
@@ -274,21 +319,24 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
             else pos = (uint32_t)(e0 - 3 * (p + 8) + 1);
             info = pack_info(seqId, pos + posOffset, (uint32_t)frame);
         }
-        keys[slot + p] = key;
-        vals[slot + p] = info;
+        keys[slotBase + 64ull * (p - pFirst)] = key;
+        vals[slotBase + 64ull * (p - pFirst)] = info;
     }
 }
 
+uint64_t extract_slots(uint64_t nUnits, uint32_t C) { return (nUnits + 63) / 64 * 64 * C; }
+
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
-                    const ReadMeta* meta, const uint64_t* slotOff, uint32_t nReads, int paired, const HostTables& t,
-                    int kmerFormat, int syncmer, int smerLen, uint64_t* keys, uint64_t* vals, hipStream_t s) {
+                    const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
+                    uint64_t* vals, hipStream_t s) {
     ExtractTables tabs;
     for (int i = 0; i < 256; i++) tabs.base[i] = t.base[i];
     for (int i = 0; i < 64; i++) { tabs.aa[i] = t.aa[i]; tabs.num[i] = t.num[i]; }
-    uint64_t threads = (uint64_t)nReads * (paired ? 12 : 6);
-    if (threads == 0) return;
-    k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, slotOff, nReads, paired,
-                                                                tabs, kmerFormat, syncmer, smerLen, keys, vals);
+    if (nUnits == 0) return;
+    const uint64_t threads = (nUnits + 63) / 64 * 64;  // whole waves: padding units write sentinels
+    k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits,
+                                                                C, tabs, kmerFormat, syncmer, smerLen, keys, vals);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -553,30 +601,60 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
     k_build_dir<<<(unsigned)((d.R + 1 + 255) / 256), 256, 0, s>>>(dbv, D, d, dir);
 }
 
+// Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
+// of that range (found with two directory lookups per block) are staged in LDS with coalesced
+// loads and every query of the block searches LDS. A block whose range holds more than kMatchWin
+// DB values (few queries against a large DB, or a very frequent AA k-mer) searches HBM through the
+// directory instead.
+constexpr int kMatchQ = 256;
+constexpr int kMatchWin = 1024;
+constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
+
+__device__ __forceinline__ uint64_t aa_rank36(uint64_t key, int fmt) {
+    const uint64_t aa = key >> 24;
+    if (fmt != 2) return aa;
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) r = r * 21 + ((aa >> (5 * i)) & 31u);
+    return r;
+}
+
+__device__ __forceinline__ uint64_t rank_floor_value(uint64_t r, int fmt) {  // smallest value of AA rank r
+    if (fmt != 2) return r << 24;
+    uint64_t aa = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        aa |= (r % 21) << (5 * i);
+        r /= 21;
+    }
+    return aa << 24;
+}
+
+__device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
+    const uint64_t b = aa_bucket(v, d);
+    return lower_bound_u64(dbv, d.dir[b], d.dir[b + 1], v);
+}
+
+// One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
 template <bool EMIT>
-__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
-                                               uint64_t Q, const uint64_t* __restrict__ dbv,
-                                               const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
-                                               const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                               uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                               mtb_match* __restrict__ out, int* __restrict__ err) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= Q) return;
-    const uint64_t key = qkey[gid];
+__device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64_t* __restrict__ qinfo,
+                                          const uint64_t* vals, uint64_t vOff, uint64_t sLo, uint64_t sHi,
+                                          uint64_t D, const uint32_t* __restrict__ dbinfo,
+                                          const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                          uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
+                                          mtb_match* __restrict__ out, int* __restrict__ err) {
     const uint64_t aa = key & kAAMask;
-    const uint64_t bkt = aa_bucket(key, d);
-    const uint64_t b0 = d.dir[bkt], b1 = d.dir[bkt + 1];
-    uint64_t lo = lower_bound_u64(dbv, b0, b1, aa);
-    uint64_t hi = lower_bound_u64(dbv, lo, b1, aa + (1ull << 24));
-    if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
+    const uint64_t lo = lower_bound_u64(vals, sLo, sHi, aa);
+    uint64_t hi = lower_bound_u64(vals, lo, sHi, aa + (1ull << 24));
+    if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
     if (lo >= hi) return;
     uint32_t minSum = 255;
-    for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, dbv[t]));
+    for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, vals[t]));
     const uint32_t thr = min(minSum * 2u, 7u);
-    const uint64_t info = qinfo[gid];
-    const uint32_t seq = info_seq(info);
     uint32_t c = 0;
-    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, dbv[t]) <= thr;
+    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
+    const uint64_t info = qinfo[q];
+    const uint32_t seq = info_seq(info);
     if (!EMIT) {
         if (c) atomicAdd(&readCnt[seq - 1], c);
         return;
@@ -584,11 +662,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     uint64_t w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
-        uint64_t tv = dbv[t];
-        uint32_t hs = hamming_sum(key, tv);
+        const uint64_t tv = vals[t];
+        const uint32_t hs = hamming_sum(key, tv);
         if (hs > thr) continue;
-        uint32_t tax = dbinfo[t];
-        int32_t sp = tax <= maxTax ? spOf[tax] : 0;
+        const uint32_t tax = dbinfo[vOff + t];
+        const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
         if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
         mtb_match m;
         m.qinfo = info;
@@ -602,16 +680,95 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     }
 }
 
+// Window of each query block = DB values whose AA rank lies in the block's sort-prefix range
+// (kQuerySortLo/Hi): [lower_bound(first prefix), lower_bound(last prefix + 1)). One thread per
+// block boundary; computed once per batch and shared by the count and emit passes.
+__global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, const uint64_t* __restrict__ dbv,
+                                uint64_t D, AADir d, int kmerFormat, uint64_t nBlocks, uint64_t* __restrict__ win) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * nBlocks) return;
+    const uint64_t b = i >> 1;
+    const uint32_t side = (uint32_t)(i & 1);
+    const uint64_t q = side ? min((b + 1) * kMatchQ, Q) - 1 : b * kMatchQ;
+    const int sh = kQuerySortLo - 24;
+    const uint64_t r = ((aa_rank36(qkey[q], kmerFormat) >> sh) + side) << sh;
+    win[i] = r >= kRankEnd ? D : db_lower_bound(dbv, d, rank_floor_value(r, kmerFormat));
+}
+
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
+                                               uint64_t Q, const uint64_t* __restrict__ dbv,
+                                               const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
+                                               const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                               uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
+                                               mtb_match* __restrict__ out, int* __restrict__ err, uint32_t winCap,
+                                               const uint64_t* __restrict__ win) {
+    __shared__ uint64_t sDb[kMatchWin];
+    constexpr int kPer = kMatchQ / 256;
+    const uint64_t q0 = (uint64_t)blockIdx.x * kMatchQ;
+    const uint64_t q1 = min(q0 + (uint64_t)kMatchQ, Q);
+    // issue every load of the block up front: the query keys, then the window (kMatchWin / 256
+    // values per thread), so their latencies overlap instead of adding up loop trip by loop trip
+    uint64_t key[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
+        key[j] = q < q1 ? qkey[q] : 0;
+    }
+    const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
+    if (winN <= (uint64_t)winCap) {
+        constexpr int kLoad = kMatchWin / 256;
+        uint64_t v[kLoad];
+#pragma unroll
+        for (int j = 0; j < kLoad; j++) {
+            const uint32_t i = threadIdx.x + j * 256;
+            v[j] = i < winN ? dbv[winLo + i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kLoad; j++) {
+            const uint32_t i = threadIdx.x + j * 256;
+            if (i < winN) sDb[i] = v[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
+            if (q < q1)
+                match_one<EMIT>(q, key[j], qinfo, sDb, winLo, 0, winN, D, dbinfo, spOf, maxTax, kmerFormat, readCnt,
+                                readOff, out, err);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
+            if (q >= q1) continue;
+            const uint64_t b = aa_bucket(key[j], d);
+            match_one<EMIT>(q, key[j], qinfo, dbv, 0, d.dir[b], d.dir[b + 1], D, dbinfo, spOf, maxTax, kmerFormat,
+                            readCnt, readOff, out, err);
+        }
+    }
+}
+
+uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
+
+void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
+                          int kmerFormat, uint64_t* win, hipStream_t s) {
+    if (Q == 0 || D < 2) return;
+    const uint64_t nb = (Q + kMatchQ - 1) / kMatchQ;
+    k_match_windows<<<(unsigned)((2 * nb + 255) / 256), 256, 0, s>>>(qkey, Q, dbv, D, dir, kmerFormat, nb, win);
+}
+
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
                   const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
                   int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  hipStream_t s) {
+                  uint32_t winCap, const uint64_t* win, hipStream_t s) {
     if (Q == 0 || D < 2) return;
-    unsigned blocks = (unsigned)((Q + 255) / 256);
+    unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
+    winCap = std::min<uint32_t>(winCap, kMatchWin);
     if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                                   readCnt, readOff, out, err);
+                                                   readCnt, readOff, out, err, winCap, win);
     else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                               readCnt, readOff, out, err);
+                                               readCnt, readOff, out, err, winCap, win);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

@@ -34,15 +34,18 @@ struct AssignArgs {
     float minScore, minSpScore, tieRatio;
 };
 
-struct AssignScratch {
-    void* local;
-    void* paths;
-    void* comb;
+struct AssignScratch {  // per match unless noted
+    void* local;           // Path
+    void* paths;           // Path
+    void* comb;            // Path
     uint8_t* conn;
-    float* spScore;
-    int32_t* spId;
-    void* quot;
-    void* clade;
+    uint32_t *gFlag, *sFlag, *pathCnt;
+    uint64_t *gScan, *sScan, *gStart, *sStart;  // M + 1 entries
+    float* spScore;        // per species run
+    uint8_t* spKeep;       // per species run
+    void* scanTmp;         // scan_tmp_elems(M) u64
+    void* quot;            // per read, qcapOff
+    void* clade;           // cladePerMatch per match
     uint32_t cladePerMatch;
 };
 
@@ -52,10 +55,15 @@ void exclusive_scan_u32(const uint32_t* in, uint64_t n, uint64_t* out, void* tmp
 void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
 
 void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
-                      uint64_t* reserve, uint32_t* qlen, hipStream_t s);
+                      uint32_t* qlen, uint32_t* maxW, hipStream_t s);
+void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t* units, hipStream_t s);
+void launch_unit_read(const uint64_t* uOff, uint32_t n, uint32_t* unitRead, hipStream_t s);
+uint64_t extract_slots(uint64_t nUnits, uint32_t C);
+// K1 over nUnits chunks of <= C windows; writes extract_slots(nUnits, C) slots
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
-                    const ReadMeta* meta, const uint64_t* slotOff, uint32_t nReads, int paired, const HostTables& t,
-                    int kmerFormat, int syncmer, int smerLen, uint64_t* keys, uint64_t* vals, hipStream_t s);
+                    const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
+                    uint64_t* vals, hipStream_t s);
 
 uint64_t radix_counts_elems(uint64_t n);
 // rank21: digits of the base-21 AA rank of a format-2 k-mer (see k_radix_scatter)
@@ -84,7 +92,10 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
                   const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
                   int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  hipStream_t s);
+                  uint32_t winCap, const uint64_t* win, hipStream_t s);  // winCap: max DB values staged per block
+uint64_t match_window_elems(uint64_t Q);
+void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
+                          int kmerFormat, uint64_t* win, hipStream_t s);
 
 uint64_t path_bytes();
 uint64_t quot_bytes();
@@ -94,9 +105,12 @@ void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, 
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 4096;  // segments up to this many matches sort in LDS
+void launch_order_keys(const uint64_t* mOff, uint32_t nReads, uint32_t maxSeg, uint64_t* keys, uint64_t* vals,
+                       hipStream_t s);
+// order: read indices in launch order (low 32 bits of each entry), or null for 0..nReads-1
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
-                   uint32_t nReads, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st);
+                   uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, const uint64_t* order, hipStream_t st);
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
 void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
                            uint32_t nReads, mtb_taxcnt* out, hipStream_t s);

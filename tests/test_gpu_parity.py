@@ -122,3 +122,24 @@ def test_end_to_end_batches(make_db, db_name):
             compare_results(br.results, br.taxcnt, ores, otc)
             assert br.results["is_classified"].mean() > 0.5
     odb.close()
+
+
+@pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
+@pytest.mark.parametrize("window", ["0", "64", "6144"])
+def test_match_window_paths(make_db, db_name, window, monkeypatch):
+    """K4's two search paths — DB window staged in LDS, or HBM search through the AA directory —
+    give the oracle's matches whatever the per-block window cap (0 forces the HBM path)."""
+    monkeypatch.setenv("MTB_MATCH_WINDOW", window)
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, 2)
+    reads = _reads(gen, "paired", 2000, seed=9)
+    opar = par.to_c()
+    odb = oc.OracleDb(db_dir)
+    okmers, ql1, ql2 = oc.extract(opar, reads)
+    omatches = oc.match(odb, opar, okmers)
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
+        gm = clf.matches()
+        assert len(gm) == len(omatches) == br.matches
+        assert np.array_equal(gm, omatches)
+    odb.close()
