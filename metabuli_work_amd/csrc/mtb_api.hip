@@ -59,18 +59,19 @@ struct mtb_ctx {
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
     AADir dir{};
-    uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
+    uint32_t matchWinCap = ~0u;
+    bool assignOrder = true;     // MTB_ASSIGN_ORDER=0 launches K6 reads in batch order  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
     uint8_t* tFlags = nullptr;
     uint32_t cladePerMatch = 2;
     // batch workspace
-    DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, qcapOff, scanTmp;
+    DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
     DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead;
-    DevBuf local, paths, comb, conn, spScore, spKeep, quot,
+    DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
     uint32_t nReads = 0;
@@ -215,9 +216,9 @@ void mtb_close(mtb_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
-                      &c->qcapOff, &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
+                      &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
                       &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->local, &c->paths,
-                      &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->quot, &c->clade, &c->tcPool, &c->tcLen,
+                      &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : c->ev)
@@ -244,11 +245,6 @@ int mtb_set_stream(mtb_ctx* c, void* stream) {
 uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
 
 }  // extern "C"
-
-__global__ void k_qcap(const uint32_t* __restrict__ qlen, uint32_t n, int dnaShift, uint32_t* __restrict__ qcap) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) qcap[i] = (uint32_t)(((int)qlen[i] + 3) / dnaShift + 1);  // maxQuotient + 1 (Taxonomer.cpp:210)
-}
 
 static AssignArgs assign_args(const mtb_params& p) {
     AssignArgs a;
@@ -277,13 +273,6 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     AssignArgs a = assign_args(c->par);
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
-    HIP_TRY(c->qcapOff.ensure(sizeof(uint64_t) * (n + 1)));
-    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
-    k_qcap<<<(n + 255) / 256, 256, 0, s>>>(c->qlen.as<uint32_t>(), n, a.dnaShift, c->readCnt.as<uint32_t>());
-    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->qcapOff.as<uint64_t>(), c->scanTmp.p, s);
-    uint64_t QC = 0;
-    HIP_TRY(hipMemcpyAsync(&QC, c->qcapOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
     const uint64_t Mc = std::max<uint64_t>(M, 1);
     HIP_TRY(c->local.ensure(path_bytes() * Mc));
     HIP_TRY(c->paths.ensure(path_bytes() * Mc));
@@ -293,7 +282,6 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->spKeep.ensure(Mc));
     for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Mc + 1)));
     for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
-    HIP_TRY(c->quot.ensure(quot_bytes() * std::max<uint64_t>(QC, 1)));
     HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
     HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Mc));
     HIP_TRY(c->results.ensure(sizeof(mtb_result) * std::max<uint32_t>(n, 1)));
@@ -310,19 +298,10 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                    c->segScratch.as<uint64_t>(), maxSeg > 512, s);
     HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(hipEventRecord(c->kev[10], s));
-    // launch order: reads by descending match count (2-3 radix passes over n keys)
-    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (n + 1)));
-    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(n + 1)));
-    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(n + 1) + 1)));
-    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(n + 1) + n + Mc + 2)));
-    launch_order_keys(c->mOff.as<uint64_t>(), n, maxSeg, c->ordKA.as<uint64_t>(), c->ordVA.as<uint64_t>(), s);
-    int segBits = 8;
-    while (segBits < 32 && (maxSeg >> segBits)) segBits += 8;
-    bool ordInB = false;
-    radix_sort_pairs(c->ordKA.as<uint64_t>(), c->ordVA.as<uint64_t>(), c->ordKB.as<uint64_t>(), c->ordVB.as<uint64_t>(),
-                     n, 32, 32 + segBits, false, false, c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(),
-                     c->scanTmp.p, &ordInB, s);
-    const uint64_t* order = ordInB ? c->ordKB.as<uint64_t>() : c->ordKA.as<uint64_t>();
+    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
+    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mc + 1)));
+    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mc + 1) + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Mc + 1) + n + Mc + 2)));
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
     AssignScratch sc{c->local.p,
                      c->paths.p,
@@ -338,11 +317,16 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                      c->spScore.as<float>(),
                      c->spKeep.as<uint8_t>(),
                      c->scanTmp.p,
-                     c->quot.p,
+                     c->ordKA.as<uint64_t>(),
+                     c->ordVA.as<uint64_t>(),
+                     c->ordKB.as<uint64_t>(),
+                     c->ordVB.as<uint64_t>(),
+                     c->radixCounts.as<uint32_t>(),
+                     c->radixOffs.as<uint64_t>(),
                      c->clade.p,
                      c->cladePerMatch};
-    launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(), c->qcapOff.as<uint64_t>(),
-                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), order, s);
+    launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(),
+                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -466,6 +450,10 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     uint64_t M = 0;
     HIP_TRY(hipMemcpyAsync(&M, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (M >= kMaxBatchMatches) {
+        set_error("batch produced >= 2^32 matches: split it into smaller batches");
+        return MTB_ERR_ARG;
+    }
     c->M = M;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
@@ -578,6 +566,7 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     std::vector<mtb_match> grouped(std::max<uint64_t>(nm, 1));
     std::vector<uint64_t> cur(off.begin(), off.end() - 1);
     for (uint64_t i = 0; i < nm; i++) grouped[cur[info_seq(m[i].qinfo) - 1]++] = m[i];
+    if (nm >= kMaxBatchMatches) { set_error("more than 2^32 - 1 matches in one call"); return MTB_ERR_ARG; }
     c->M = nm;
     c->nReads = n;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));

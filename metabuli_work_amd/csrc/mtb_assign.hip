@@ -192,11 +192,6 @@ struct AssignCfg {
     float minScore, minSpScore, tieRatio;
 };
 
-struct Quot {
-    int32_t tax;
-    uint8_t minH, has, pad0, pad1;
-};
-
 struct Clade {
     int32_t tax, parentTax;
     uint32_t count;
@@ -256,16 +251,34 @@ __global__ void k_run_starts(const uint32_t* __restrict__ gFlag, const uint32_t*
     }
 }
 
+// Work list for k_match_paths: the groups of >= 2 matches (a single match makes no path) in batch
+// order, so a wave's lanes still walk neighbouring groups (ordering them by size instead was
+// slower: the lost locality costs more than the divergence it removes). Single-match groups get
+// the sentinel key and zero paths; one stable radix pass on an all-zero digit compacts the rest.
+__global__ void k_group_keys(const uint64_t* __restrict__ gStart, uint64_t nG, uint64_t* __restrict__ keys,
+                             uint64_t* __restrict__ vals, uint32_t* __restrict__ pathCnt) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nG) return;
+    const uint64_t n = gStart[g + 1] - gStart[g];
+    if (n <= 1) {
+        pathCnt[g] = 0;
+        keys[g] = kSentinel;
+    } else {
+        keys[g] = g;
+    }
+    vals[g] = 0;
+}
+
 // getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
 // P[gs + k] in emission order; L and conn are indexed by match.
 __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
-                                                     uint64_t nG, AssignCfg cfg, TaxView tax, Path* __restrict__ L,
-                                                     Path* __restrict__ P, uint8_t* __restrict__ conn,
-                                                     uint32_t* __restrict__ pathCnt) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nG) return;
+                                                     const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
+                                                     TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
+                                                     uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nWork) return;
+    const uint64_t g = (uint32_t)order[i];
     const uint64_t start = gStart[g], end = gStart[g + 1];
-    if (end - start <= 1) { pathCnt[g] = 0; return; }
     const int32_t sp = (int32_t)M[start].species_id;
     const uint32_t curFrame = info_frame(M[start].qinfo);
     int minDepth = cfg.minConsCnt;
@@ -423,19 +436,18 @@ __global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restri
 // chooseBestTaxon (Taxonomer.cpp:130-202), filterRedundantMatches (:205-241), taxCnt and the
 // lower-rank BFS (:252-314) for one read.
 __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff,
-                                                      const uint32_t* __restrict__ qlen,
-                                                      const uint64_t* __restrict__ qOff, uint32_t nReads,
-                                                      const uint64_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ qlen, uint32_t nReads,
                                                       const uint64_t* __restrict__ sScan,
                                                       const uint64_t* __restrict__ sStart,
+                                                      const uint64_t* __restrict__ gScan,
+                                                      const uint64_t* __restrict__ gStart,
                                                       const float* __restrict__ spScore,
                                                       const uint8_t* __restrict__ spKeep, AssignCfg cfg, TaxView tax,
-                                                      Quot* __restrict__ quotP, Clade* __restrict__ cladeP,
+                                                      Clade* __restrict__ cladeP,
                                                       uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
                                                       mtb_result* __restrict__ results) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= nReads) return;
-    const uint32_t r = order ? (uint32_t)order[gid] : gid;  // heaviest reads first (k_order_keys)
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
     const int readLength = (int)qlen[r];
@@ -500,27 +512,70 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
     }
 
     // ---- filterRedundantMatches (Taxonomer.cpp:205-241) ----
-    Quot* Qs = quotP + qOff[r];
-    const long maxQ = (long)((readLength + 3) / cfg.dnaShift);
-    for (long q = 0; q <= maxQ; q++) { Qs[q].has = 0; Qs[q].minH = 255; Qs[q].tax = 0; }
-    for (uint64_t x = bestFirst; x < bestSecond; x++) {
-        const long q = (long)(info_pos(M[x].qinfo) / (uint32_t)cfg.dnaShift);
-        const uint8_t h = M[x].hamming;
-        const int32_t t = (int32_t)M[x].target_id;
-        if (!Qs[q].has) { Qs[q].has = 1; Qs[q].tax = t; Qs[q].minH = h; }
-        else if (h < Qs[q].minH) { Qs[q].tax = t; Qs[q].minH = h; }
-        else if (h == Qs[q].minH) Qs[q].tax = tax.lca(Qs[q].tax, t);
+    // Per quotient q = pos / dnaShift: the best (lowest hamming) match's taxon, ties folded with
+    // LCA — an order-free reduction. Within the best species the matches are sorted by frame, then
+    // position, so each frame's quotients ascend: a <= 6-way merge over the frame runs visits each
+    // quotient once, in order, with no per-read quotient table.
+    uint32_t fc[6], fin[6], head[6];
+    const mtb_match* B = M + bestFirst;
+    const uint32_t dnaShift = (uint32_t)cfg.dnaShift;
+    int nf = 0;
+    for (uint64_t g = gScan[bestFirst]; nf < 6 && gStart[g] < bestSecond; g++) {
+        fc[nf] = (uint32_t)(gStart[g] - bestFirst);
+        fin[nf] = (uint32_t)(gStart[g + 1] - bestFirst);
+        nf++;
     }
+#pragma unroll
+    for (int f = 0; f < 6; f++) head[f] = (f < nf) ? info_pos(B[fc[f]].qinfo) / dnaShift : 0xFFFFFFFFu;
+    // taxCnt: the first distinct taxa stay in registers, the rest (rare) in the read's pool slice
+    constexpr int kRegTc = 4;
+    int32_t rt[kRegTc];
+    uint32_t rc[kRegTc];
     mtb_taxcnt* tc = tcP + base;  // capacity n (each quotient holds >= 1 match)
     long nTc = 0;
-    for (long q = 0; q <= maxQ; q++) {
-        if (!Qs[q].has) continue;
-        const int32_t t = Qs[q].tax;
-        long f = 0;
-        while (f < nTc && tc[f].tax_id != t) f++;
-        if (f == nTc) { tc[nTc].tax_id = t; tc[nTc].count = 0; nTc++; }
-        tc[f].count++;
+    while (true) {
+        uint32_t qmin = 0xFFFFFFFFu;
+#pragma unroll
+        for (int f = 0; f < 6; f++) qmin = min(qmin, head[f]);
+        if (qmin == 0xFFFFFFFFu) break;
+        uint32_t minH = 256;
+        int32_t t = 0;
+#pragma unroll
+        for (int f = 0; f < 6; f++) {
+            while (head[f] == qmin) {
+                const mtb_match& x = B[fc[f]];
+                const uint32_t h = x.hamming;
+                if (h < minH) { minH = h; t = (int32_t)x.target_id; }
+                else if (h == minH) t = tax.lca(t, (int32_t)x.target_id);
+                fc[f]++;
+                head[f] = fc[f] < fin[f] ? info_pos(B[fc[f]].qinfo) / dnaShift : 0xFFFFFFFFu;
+            }
+        }
+        long e = -1;
+#pragma unroll
+        for (int k = 0; k < kRegTc; k++)
+            if (k < nTc && rt[k] == t) e = k;
+        if (e >= 0) {
+#pragma unroll
+            for (int k = 0; k < kRegTc; k++)
+                if (k == e) rc[k]++;
+            continue;
+        }
+        if (nTc < kRegTc) {
+#pragma unroll
+            for (int k = 0; k < kRegTc; k++)
+                if (k == nTc) { rt[k] = t; rc[k] = 1; }
+            nTc++;
+            continue;
+        }
+        e = kRegTc;
+        while (e < nTc && tc[e].tax_id != t) e++;
+        if (e == nTc) { tc[nTc].tax_id = t; tc[nTc].count = 0; nTc++; }
+        tc[e].count++;
     }
+#pragma unroll
+    for (int k = 0; k < kRegTc; k++)
+        if (k < nTc) { tc[k].tax_id = rt[k]; tc[k].count = rc[k]; }
     for (long a = 1; a < nTc; a++) {  // std::map order
         mtb_taxcnt v = tc[a];
         long b = a;
@@ -595,27 +650,8 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
     results[r] = res;
 }
 
-// Keys that order reads by descending match count (stable): one thread per read runs the whole
-// decision tree, so a wave costs as much as its heaviest read and the grid as much as its last
-// waves. Launching heavy reads first and grouping reads of similar weight in a wave keeps the
-// SIMDs busy (longest-processing-time-first).
-__global__ void k_order_keys(const uint64_t* __restrict__ mOff, uint32_t nReads, uint32_t maxSeg,
-                             uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nReads) return;
-    const uint32_t c = (uint32_t)(mOff[r + 1] - mOff[r]);
-    keys[r] = ((uint64_t)(maxSeg - c) << 32) | r;
-    vals[r] = r;
-}
-
-void launch_order_keys(const uint64_t* mOff, uint32_t nReads, uint32_t maxSeg, uint64_t* keys, uint64_t* vals,
-                       hipStream_t s) {
-    if (nReads) k_order_keys<<<(nReads + 255) / 256, 256, 0, s>>>(mOff, nReads, maxSeg, keys, vals);
-}
-
-void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
-                   uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, const uint64_t* order, hipStream_t st) {
+void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
                   a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio};
@@ -631,10 +667,17 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
         hipMemcpyAsync(&cnt[0], s.gScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(&cnt[1], s.sScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
         hipStreamSynchronize(st);
-        if (cnt[0])
-            k_match_paths<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(matches, s.gStart, cnt[0], cfg, tv,
-                                                                             (Path*)s.local, (Path*)s.paths, s.conn,
-                                                                             s.pathCnt);
+        if (cnt[0]) {
+            k_group_keys<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(s.gStart, cnt[0], s.ordKA, s.ordVA,
+                                                                            s.pathCnt);
+            bool inB = false;
+            const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true, false,
+                                                    s.radixCounts, s.radixOffs, s.scanTmp, &inB, st);
+            if (heavy)
+                k_match_paths<<<(unsigned)((heavy + 255) / 256), 256, 0, st>>>(
+                    matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
+                    s.conn, s.pathCnt);
+        }
         if (cnt[1])
             k_combine_paths<<<(unsigned)((cnt[1] + 255) / 256), 256, 0, st>>>(
                 matches, s.sStart, cnt[1], s.gScan, s.gStart, s.pathCnt, qlen, cfg, (Path*)s.paths, (Path*)s.comb,
@@ -642,13 +685,12 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
     }
-    k_choose_taxon<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, qOff, nReads, order, s.sScan, s.sStart,
-                                                         s.spScore, s.spKeep, cfg, tv, (Quot*)s.quot,
+    k_choose_taxon<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
+                                                         s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
                                                          (Clade*)s.clade, s.cladePerMatch, tcPool, results);
 }
 
 uint64_t path_bytes() { return sizeof(Path); }
-uint64_t quot_bytes() { return sizeof(Quot); }
 uint64_t clade_bytes() { return sizeof(Clade); }
 
 // Compaction of the per-read taxcnt slices (capacity = match count) into one pooled array.

@@ -43,8 +43,10 @@ struct AssignScratch {  // per match unless noted
     uint64_t *gScan, *sScan, *gStart, *sStart;  // M + 1 entries
     float* spScore;        // per species run
     uint8_t* spKeep;       // per species run
-    void* scanTmp;         // scan_tmp_elems(M) u64
-    void* quot;            // per read, qcapOff
+    void* scanTmp;         // scan_tmp_elems(radix_counts_elems(M + 1) + M + 2) u64
+    uint64_t *ordKA, *ordVA, *ordKB, *ordVB;  // M + 1 each: group work list (radix_sort_pairs)
+    uint32_t* radixCounts;                    // radix_counts_elems(M + 1)
+    uint64_t* radixOffs;                      // radix_counts_elems(M + 1) + 1
     void* clade;           // cladePerMatch per match
     uint32_t cladePerMatch;
 };
@@ -98,19 +100,16 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
                           int kmerFormat, uint64_t* win, hipStream_t s);
 
 uint64_t path_bytes();
-uint64_t quot_bytes();
 uint64_t clade_bytes();
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                     uint64_t* gScratch, bool anyLarge, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
-constexpr uint32_t kSegSortLds = 4096;  // segments up to this many matches sort in LDS
-void launch_order_keys(const uint64_t* mOff, uint32_t nReads, uint32_t maxSeg, uint64_t* keys, uint64_t* vals,
-                       hipStream_t s);
-// order: read indices in launch order (low 32 bits of each entry), or null for 0..nReads-1
-void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, const uint64_t* qOff,
-                   uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, const uint64_t* order, hipStream_t st);
+constexpr uint32_t kSegSortLds = 4096;
+// K6 indexes matches and groups with 32 bits
+constexpr uint64_t kMaxBatchMatches = 0xFFFFFFFFull;  // segments up to this many matches sort in LDS
+void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
+                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st);
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
 void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
                            uint32_t nReads, mtb_taxcnt* out, hipStream_t s);
