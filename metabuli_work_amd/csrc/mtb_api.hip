@@ -59,7 +59,8 @@ struct mtb_ctx {
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
     AADir dir{};
-    uint32_t matchWinCap = ~0u;
+    uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
+    bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool assignOrder = true;     // MTB_ASSIGN_ORDER=0 launches K6 reads in batch order  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
@@ -148,6 +149,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
+    if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
@@ -263,6 +266,7 @@ static AssignArgs assign_args(const mtb_params& p) {
     a.minScore = p.min_score;
     a.minSpScore = p.min_sp_score;
     a.tieRatio = p.tie_ratio;
+    a.generic = 0;
     return a;
 }
 
@@ -271,6 +275,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     hipStream_t s = c->stream;
     const uint64_t M = c->M;
     AssignArgs a = assign_args(c->par);
+    a.generic = c->forceGeneric ? 1 : 0;
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     const uint64_t Mc = std::max<uint64_t>(M, 1);

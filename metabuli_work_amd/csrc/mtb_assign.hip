@@ -190,6 +190,7 @@ struct TaxView {
 struct AssignCfg {
     int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
     float minScore, minSpScore, tieRatio;
+    int generic;  // 1: skip the register fast path (tests)
 };
 
 struct Clade {
@@ -269,6 +270,126 @@ __global__ void k_group_keys(const uint64_t* __restrict__ gStart, uint64_t nG, u
     vals[g] = 0;
 }
 
+// isConsecutive / isConsecutive2 (Taxonomer.cpp:677-699) of a current match (dc) and the next (dn)
+__device__ __forceinline__ bool consecutive(uint32_t dc, uint32_t dn, uint32_t sh, uint32_t lowMask, bool fwd,
+                                            int kmerFormat) {
+    if (kmerFormat == 2) return fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
+    return fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
+}
+
+// getMatchPaths with the DP state in registers: only the current and the next position group are
+// live, and both are almost always small (one DB k-mer per strain at a position). Returns false,
+// having written nothing that counts, if a position group holds more than kRegPos matches; the
+// caller then reruns the group through the general version.
+constexpr int kRegPos = 4;
+
+__device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M, uint64_t start, uint64_t end,
+                                                 const AssignCfg& cfg, int minDepth, bool fwd,
+                                                 Path* __restrict__ P, uint64_t& nPout) {
+    Path cp[kRegPos], np[kRegPos];
+    uint32_t cd[kRegPos], nd[kRegPos], nr[kRegPos];
+    bool cc[kRegPos];
+    int nc = 0, nn = 0;
+    uint64_t nP = start;
+    uint64_t k = start;
+    uint32_t currPos = info_pos(M[k].qinfo);
+    // first position group
+    while (k < end) {
+        const mtb_match m = M[k];
+        if (info_pos(m.qinfo) != currPos) break;
+        if (nc == kRegPos) return false;
+#pragma unroll
+        for (int x = 0; x < kRegPos; x++)
+            if (x == nc) {
+                cp[x].start = (int)currPos;
+                cp[x].end = (int)currPos + 23;
+                cp[x].score = score_fields(m.right_end_hamming, 8, false);
+                cp[x].hd = m.hamming;
+                cp[x].depth = 1;
+                cp[x].sm = cp[x].em = (uint32_t)k;
+                cd[x] = m.dna_encoding;
+                cc[x] = false;
+            }
+        nc++;
+        k++;
+    }
+    while (k < end) {
+        const uint32_t nextPos = info_pos(M[k].qinfo);
+        nn = 0;
+        while (k < end) {
+            const mtb_match m = M[k];
+            if (info_pos(m.qinfo) != nextPos) break;
+            if (nn == kRegPos) return false;
+#pragma unroll
+            for (int x = 0; x < kRegPos; x++)
+                if (x == nn) {
+                    np[x].start = (int)nextPos;
+                    np[x].end = (int)nextPos + 23;
+                    np[x].score = score_fields(m.right_end_hamming, 8, false);
+                    np[x].hd = m.hamming;
+                    np[x].depth = 1;
+                    np[x].sm = np[x].em = (uint32_t)k;
+                    nd[x] = m.dna_encoding;
+                    nr[x] = m.right_end_hamming;
+                }
+            nn++;
+            k++;
+        }
+        const int shift = (int)((nextPos - currPos) / 3);
+        if (shift > 0 && shift <= cfg.maxCodonShift) {
+            const uint32_t sh = 3u * (uint32_t)shift;
+            const uint32_t lowMask = (1u << (24u - sh)) - 1u;
+#pragma unroll
+            for (int x = 0; x < kRegPos; x++) {
+                if (x >= nn) continue;
+                float inc = 0.0f;
+                int hinc = 0;
+                for (int c = 0; c < shift; c++) {
+                    uint32_t h = (nr[x] >> (2 * c)) & 3u;
+                    inc += codon_score(h);
+                    hinc += (int)h;
+                }
+                bool found = false;
+                float bestScore = 0.0f;
+                Path bp{};
+#pragma unroll
+                for (int y = 0; y < kRegPos; y++) {
+                    if (y >= nc) continue;
+                    if (consecutive(cd[y], nd[x], sh, lowMask, fwd, cfg.kmerFormat)) {
+                        cc[y] = true;
+                        if (cp[y].score > bestScore) { found = true; bestScore = cp[y].score; bp = cp[y]; }
+                    }
+                }
+                if (found) {
+                    np[x].start = bp.start;
+                    np[x].score = bp.score + inc;
+                    np[x].hd = bp.hd + hinc;
+                    np[x].depth = bp.depth + shift;
+                    np[x].sm = bp.sm;
+                }
+            }
+        }
+#pragma unroll
+        for (int y = 0; y < kRegPos; y++)
+            if (y < nc && !cc[y] && cp[y].depth >= minDepth) P[nP++] = cp[y];
+        if (k == end) {
+#pragma unroll
+            for (int x = 0; x < kRegPos; x++)
+                if (x < nn && np[x].depth >= minDepth) P[nP++] = np[x];
+        }
+#pragma unroll
+        for (int x = 0; x < kRegPos; x++) {
+            cp[x] = np[x];
+            cd[x] = nd[x];
+            cc[x] = false;
+        }
+        nc = nn;
+        currPos = nextPos;
+    }
+    nPout = nP;
+    return true;
+}
+
 // getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
 // P[gs + k] in emission order; L and conn are indexed by match.
 __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
@@ -284,6 +405,13 @@ __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict
     int minDepth = cfg.minConsCnt;
     if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
     const bool fwd = curFrame < 3;
+    {
+        uint64_t nPr = start;
+        if (!cfg.generic && match_paths_regs(M, start, end, cfg, minDepth, fwd, P, nPr)) {
+            pathCnt[g] = (uint32_t)(nPr - start);
+            return;
+        }
+    }
     for (uint64_t x = start; x < end; x++) conn[x] = 0;
     uint64_t nP = start;
     uint64_t k = start;
@@ -654,7 +782,7 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                    mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
-                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio};
+                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic};
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
     if (nM) {
         const unsigned bm = (unsigned)((nM + 255) / 256);

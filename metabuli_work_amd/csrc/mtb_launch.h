@@ -32,6 +32,7 @@ struct TaxDevice {
 struct AssignArgs {
     int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
     float minScore, minSpScore, tieRatio;
+    int generic;  // MTB_FORCE_GENERIC: general code paths only (parity tests of the fallbacks)
 };
 
 struct AssignScratch {  // per match unless noted

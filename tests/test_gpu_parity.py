@@ -143,3 +143,19 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
         assert len(gm) == len(omatches) == br.matches
         assert np.array_equal(gm, omatches)
     odb.close()
+
+
+@pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
+def test_general_paths(make_db, db_name, monkeypatch):
+    """MTB_FORCE_GENERIC=1 turns off every fast path (LDS DB windows in K4, register DP in K6), so
+    the general code the fast paths fall back to is held to the oracle too."""
+    monkeypatch.setenv("MTB_FORCE_GENERIC", "1")
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, 2)
+    odb = oc.OracleDb(db_dir)
+    reads = _reads(gen, "paired", 1500, 31)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
