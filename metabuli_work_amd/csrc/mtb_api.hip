@@ -71,7 +71,7 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, qcnt;
     DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
@@ -220,7 +220,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->qcnt, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -445,11 +445,12 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
+    HIP_TRY(c->qcnt.ensure(std::max<uint64_t>(Q, 1)));
     HIP_TRY(hipEventRecord(c->kev[4], s));
     launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), c->matchWinCap,
-                 c->matchWin.as<uint64_t>(), s);
+                 c->matchWin.as<uint64_t>(), c->qcnt.as<uint8_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[5], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t M = 0;
@@ -465,7 +466,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipEventRecord(c->kev[6], s));
     launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
                  c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(),
-                 c->matchWinCap, c->matchWin.as<uint64_t>(), s);
+                 c->matchWinCap, c->matchWin.as<uint64_t>(), c->qcnt.as<uint8_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     // K5 + K6

@@ -395,10 +395,13 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __shared__ uint64_t sVal[kRadixTile];
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
-    __shared__ uint32_t tileStart[256];
+    __shared__ uint64_t sDst[256];  // global slot of this tile's first key of digit d, minus its tile offset
     __shared__ uint32_t sKept;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * kRadixTile + (uint64_t)w * kRadixSlice;
+    // the digit bases: one strided load per lane, issued first so its latency hides behind the
+    // key loads (a dependent load per key in the write-out loop was the old bottleneck)
+    const uint64_t digitBase = offs[(uint64_t)tid * nTiles + blockIdx.x];
     for (int x = tid; x < kWaves * 256; x += kBlock) (&waveHist[0][0])[x] = 0;
     __syncthreads();
 
@@ -437,7 +440,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         for (int ww = 0; ww < kWaves; ww++) { c[ww] = waveHist[ww][tid]; sum += c[ww]; }
         unsigned long long tot;
         const uint32_t start = (uint32_t)block_exclusive_scan(sum, &tot);
-        tileStart[tid] = start;
+        sDst[tid] = digitBase - start;
         if (tid == 0) sKept = (uint32_t)tot;
         uint32_t run = start;
 #pragma unroll
@@ -456,7 +459,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __syncthreads();
     for (uint32_t i = tid; i < sKept; i += kBlock) {
         const uint32_t d = sDig[i];
-        const uint64_t dst = offs[(uint64_t)d * nTiles + blockIdx.x] + (i - tileStart[d]);
+        const uint64_t dst = sDst[d] + i;
         keysOut[dst] = sKey[i];
         valsOut[dst] = sVal[i];
     }
@@ -636,30 +639,46 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
 }
 
 // One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
+// COUNT: writes the query's match count (saturated at 255) to qcnt and adds it to its read.
+// EMIT: called only for queries with qcnt != 0; a count below 255 is exact, so the read's slot is
+// claimed before the search and the atomic's latency hides behind it.
 template <bool EMIT>
 __device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64_t* __restrict__ qinfo,
                                           const uint64_t* vals, uint64_t vOff, uint64_t sLo, uint64_t sHi,
                                           uint64_t D, const uint32_t* __restrict__ dbinfo,
                                           const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                           uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                          mtb_match* __restrict__ out, int* __restrict__ err) {
+                                          uint8_t* __restrict__ qcnt, mtb_match* __restrict__ out,
+                                          int* __restrict__ err) {
+    uint64_t info = 0, w = 0;
+    uint32_t seq = 0, c8 = 0;
+    if (EMIT) {
+        c8 = qcnt[q];
+        info = qinfo[q];
+        seq = info_seq(info);
+        if (c8 < 255) w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c8);
+    }
     const uint64_t aa = key & kAAMask;
     const uint64_t lo = lower_bound_u64(vals, sLo, sHi, aa);
     uint64_t hi = lower_bound_u64(vals, lo, sHi, aa + (1ull << 24));
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
-    if (lo >= hi) return;
+    if (lo >= hi) {
+        if (!EMIT) qcnt[q] = 0;
+        return;
+    }
     uint32_t minSum = 255;
     for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, vals[t]));
     const uint32_t thr = min(minSum * 2u, 7u);
-    uint32_t c = 0;
-    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
-    const uint64_t info = qinfo[q];
-    const uint32_t seq = info_seq(info);
-    if (!EMIT) {
-        if (c) atomicAdd(&readCnt[seq - 1], c);
-        return;
+    if (!EMIT || c8 == 255) {
+        uint32_t c = 0;
+        for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
+        if (!EMIT) {
+            qcnt[q] = (uint8_t)min(c, 255u);
+            if (c) atomicAdd(&readCnt[info_seq(qinfo[q]) - 1], c);
+            return;
+        }
+        w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
     }
-    uint64_t w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
         const uint64_t tv = vals[t];
@@ -701,7 +720,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                                uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                               mtb_match* __restrict__ out, int* __restrict__ err, uint32_t winCap,
+                                               uint8_t* __restrict__ qcnt, mtb_match* __restrict__ out,
+                                               int* __restrict__ err, uint32_t winCap,
                                                const uint64_t* __restrict__ win) {
     __shared__ uint64_t sDb[kMatchWin];
     constexpr int kPer = kMatchQ / 256;
@@ -710,11 +730,16 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     // issue every load of the block up front: the query keys, then the window (kMatchWin / 256
     // values per thread), so their latencies overlap instead of adding up loop trip by loop trip
     uint64_t key[kPer];
+    bool live[kPer];
+    bool any = false;
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
-        key[j] = q < q1 ? qkey[q] : 0;
+        live[j] = q < q1 && (!EMIT || qcnt[q] != 0);  // EMIT: only queries the count pass matched
+        key[j] = live[j] ? qkey[q] : 0;
+        any |= live[j];
     }
+    if (EMIT && !__syncthreads_or(any)) return;
     const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
     if (winN <= (uint64_t)winCap) {
         constexpr int kLoad = kMatchWin / 256;
@@ -733,18 +758,18 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
-            if (q < q1)
+            if (live[j])
                 match_one<EMIT>(q, key[j], qinfo, sDb, winLo, 0, winN, D, dbinfo, spOf, maxTax, kmerFormat, readCnt,
-                                readOff, out, err);
+                                readOff, qcnt, out, err);
         }
     } else {
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
-            if (q >= q1) continue;
+            if (!live[j]) continue;
             const uint64_t b = aa_bucket(key[j], d);
             match_one<EMIT>(q, key[j], qinfo, dbv, 0, d.dir[b], d.dir[b + 1], D, dbinfo, spOf, maxTax, kmerFormat,
-                            readCnt, readOff, out, err);
+                            readCnt, readOff, qcnt, out, err);
         }
     }
 }
@@ -761,14 +786,14 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
                   const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
                   int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  uint32_t winCap, const uint64_t* win, hipStream_t s) {
+                  uint32_t winCap, const uint64_t* win, uint8_t* qcnt, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                                   readCnt, readOff, out, err, winCap, win);
+                                                   readCnt, readOff, qcnt, out, err, winCap, win);
     else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                               readCnt, readOff, out, err, winCap, win);
+                                               readCnt, readOff, qcnt, out, err, winCap, win);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

@@ -95,7 +95,8 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
                   const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
                   int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  uint32_t winCap, const uint64_t* win, hipStream_t s);  // winCap: max DB values staged per block
+                  uint32_t winCap, const uint64_t* win, uint8_t* qcnt, hipStream_t s);  // winCap: max DB values staged per block;
+// qcnt: Q bytes, written by the count pass and read by the emit pass
 uint64_t match_window_elems(uint64_t Q);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
