@@ -374,13 +374,16 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
     hist[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+    uint64_t key[kRadixItems];
 #pragma unroll
     for (int k = 0; k < kRadixItems; k++) {
-        uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
-        if (i < n) {
-            uint64_t key = keys[i];
-            if (!FILTER || key != kSentinel) atomicAdd(&hist[radix_digit<RANK21>(key, shift)], 1u);
-        }
+        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        key[k] = i < n ? keys[i] : kSentinel;
+    }
+#pragma unroll
+    for (int k = 0; k < kRadixItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
+        if (i < n && (!FILTER || key[k] != kSentinel)) atomicAdd(&hist[radix_digit<RANK21>(key[k], shift)], 1u);
     }
     __syncthreads();
     counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
@@ -408,17 +411,25 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t k[kRadixItems], v[kRadixItems];
     uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
+    // all loads first (unguarded for the full tiles) so the 32 loads of a lane are in flight
+    // together; interleaving them with the ranking serialised 16 memory round trips per tile
+    if ((uint64_t)(blockIdx.x + 1) * kRadixTile <= n) {
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) v[r] = valsIn[base + (uint64_t)r * 64 + lane];
+    } else {
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) {
+            const uint64_t i = base + (uint64_t)r * 64 + lane;
+            k[r] = i < n ? keysIn[i] : kSentinel;
+            v[r] = i < n ? valsIn[i] : 0;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < kRadixItems; r++) {
         const uint64_t i = base + (uint64_t)r * 64 + lane;
-        k[r] = 0;
-        v[r] = 0;
-        bool valid = false;
-        if (i < n) {
-            k[r] = keysIn[i];
-            v[r] = valsIn[i];
-            valid = !FILTER || k[r] != kSentinel;
-        }
+        const bool valid = i < n && (!FILTER || k[r] != kSentinel);
         const uint32_t d = valid ? radix_digit<RANK21>(k[r], shift) : 0u;
         unsigned long long peers = __ballot(valid);
 #pragma unroll
