@@ -620,8 +620,8 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 // loads and every query of the block searches LDS. A block whose range holds more than kMatchWin
 // DB values (few queries against a large DB, or a very frequent AA k-mer) searches HBM through the
 // directory instead.
-constexpr int kMatchQ = 256;
-constexpr int kMatchWin = 1024;
+constexpr int kMatchQ = 512;
+constexpr int kMatchWin = 2048;
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
 __device__ __forceinline__ uint64_t aa_rank36(uint64_t key, int fmt) {
@@ -650,28 +650,17 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
 }
 
 // One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
-// COUNT: writes the query's match count (saturated at 255) to qcnt and adds it to its read.
-// EMIT: called only for queries with qcnt != 0; a count below 255 is exact, so the read's slot is
-// claimed before the search and the atomic's latency hides behind it.
+// Second half of one query's match, given its AA run [lo, hi) in vals (LDS window or the whole
+// DB; vOff = DB index of vals[0], infos aligned with vals). COUNT: writes the query's match count
+// (saturated at 255) to qcnt and adds it to its read. EMIT (queries with qcnt != 0 only): a count
+// below 255 is exact, so the read's slots were claimed (w) before the search.
 template <bool EMIT>
-__device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64_t* __restrict__ qinfo,
-                                          const uint64_t* vals, uint64_t vOff, uint64_t sLo, uint64_t sHi,
-                                          uint64_t D, const uint32_t* __restrict__ dbinfo,
+__device__ __forceinline__ void match_run(uint64_t q, uint64_t key, uint64_t info, const uint64_t* vals,
+                                          const uint32_t* infos, uint64_t vOff, uint64_t lo, uint64_t hi, uint64_t D,
                                           const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                           uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                          uint8_t* __restrict__ qcnt, mtb_match* __restrict__ out,
-                                          int* __restrict__ err) {
-    uint64_t info = 0, w = 0;
-    uint32_t seq = 0, c8 = 0;
-    if (EMIT) {
-        c8 = qcnt[q];
-        info = qinfo[q];
-        seq = info_seq(info);
-        if (c8 < 255) w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c8);
-    }
-    const uint64_t aa = key & kAAMask;
-    const uint64_t lo = lower_bound_u64(vals, sLo, sHi, aa);
-    uint64_t hi = lower_bound_u64(vals, lo, sHi, aa + (1ull << 24));
+                                          uint8_t* __restrict__ qcnt, uint32_t c8, uint64_t w,
+                                          mtb_match* __restrict__ out, int* __restrict__ err) {
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
     if (lo >= hi) {
         if (!EMIT) qcnt[q] = 0;
@@ -680,12 +669,13 @@ __device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64
     uint32_t minSum = 255;
     for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, vals[t]));
     const uint32_t thr = min(minSum * 2u, 7u);
+    const uint32_t seq = info_seq(info);
     if (!EMIT || c8 == 255) {
         uint32_t c = 0;
         for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
         if (!EMIT) {
             qcnt[q] = (uint8_t)min(c, 255u);
-            if (c) atomicAdd(&readCnt[info_seq(qinfo[q]) - 1], c);
+            if (c) atomicAdd(&readCnt[seq - 1], c);
             return;
         }
         w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
@@ -695,7 +685,7 @@ __device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64
         const uint64_t tv = vals[t];
         const uint32_t hs = hamming_sum(key, tv);
         if (hs > thr) continue;
-        const uint32_t tax = dbinfo[vOff + t];
+        const uint32_t tax = infos[t];
         const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
         if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
         mtb_match m;
@@ -708,6 +698,22 @@ __device__ __forceinline__ void match_one(uint64_t q, uint64_t key, const uint64
         m.pad = 0;
         out[w++] = m;
     }
+}
+
+// Both ends of an AA run in an LDS window of n sorted values: lower bounds of aa and aa + 2^24 by
+// a fixed-trip binary search (the trip count depends only on n, so the two chains, and the
+// chains of a thread's other queries, interleave instead of waiting on each other).
+__device__ __forceinline__ void lds_run_bounds(const uint64_t* a, uint32_t n, uint32_t pow2, uint64_t aa,
+                                               uint32_t& lo, uint32_t& hi) {
+    const uint64_t aa2 = aa + (1ull << 24);
+    uint32_t p1 = 0, p2 = 0;
+    for (uint32_t step = pow2; step > 0; step >>= 1) {
+        const uint32_t i1 = p1 + step, i2 = p2 + step;
+        if (i1 <= n && a[i1 - 1] < aa) p1 = i1;
+        if (i2 <= n && a[i2 - 1] < aa2) p2 = i2;
+    }
+    lo = p1;
+    hi = p2;
 }
 
 // Window of each query block = DB values whose AA rank lies in the block's sort-prefix range
@@ -735,52 +741,77 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                int* __restrict__ err, uint32_t winCap,
                                                const uint64_t* __restrict__ win) {
     __shared__ uint64_t sDb[kMatchWin];
+    __shared__ uint32_t sInfo[EMIT ? kMatchWin : 1];  // EMIT: the window's taxIDs, loaded coalesced
     constexpr int kPer = kMatchQ / 256;
     const uint64_t q0 = (uint64_t)blockIdx.x * kMatchQ;
     const uint64_t q1 = min(q0 + (uint64_t)kMatchQ, Q);
-    // issue every load of the block up front: the query keys, then the window (kMatchWin / 256
-    // values per thread), so their latencies overlap instead of adding up loop trip by loop trip
-    uint64_t key[kPer];
+    // every independent load of the block is issued up front (query keys and infos, counts, the
+    // window bounds, then the window) so their latencies overlap instead of adding up
+    uint64_t key[kPer], info[kPer], w[kPer];
+    uint32_t c8[kPer];
     bool live[kPer];
     bool any = false;
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
-        live[j] = q < q1 && (!EMIT || qcnt[q] != 0);  // EMIT: only queries the count pass matched
+        c8[j] = (EMIT && q < q1) ? qcnt[q] : 0;
+        live[j] = q < q1 && (!EMIT || c8[j] != 0);  // EMIT: only queries the count pass matched
         key[j] = live[j] ? qkey[q] : 0;
+        info[j] = live[j] ? qinfo[q] : 0;
+        w[j] = 0;
         any |= live[j];
     }
-    if (EMIT && !__syncthreads_or(any)) return;
+    if (EMIT) {
+#pragma unroll
+        for (int j = 0; j < kPer; j++)  // claim the read's slots now; the search hides the latency
+            if (live[j] && c8[j] < 255) {
+                const uint32_t seq = info_seq(info[j]);
+                w[j] = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c8[j]);
+            }
+        if (!__syncthreads_or(any)) return;
+    }
     const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
     if (winN <= (uint64_t)winCap) {
         constexpr int kLoad = kMatchWin / 256;
         uint64_t v[kLoad];
+        uint32_t tv[EMIT ? kLoad : 1];
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + j * 256;
             v[j] = i < winN ? dbv[winLo + i] : 0;
+            if (EMIT) tv[j] = i < winN ? dbinfo[winLo + i] : 0;
         }
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + j * 256;
-            if (i < winN) sDb[i] = v[j];
+            if (i < winN) {
+                sDb[i] = v[j];
+                if (EMIT) sInfo[i] = tv[j];
+            }
         }
         __syncthreads();
+        const uint32_t n = (uint32_t)winN;
+        uint32_t pow2 = 1;
+        while (pow2 * 2 <= n) pow2 *= 2;
+        uint32_t lo[kPer], hi[kPer];
 #pragma unroll
-        for (int j = 0; j < kPer; j++) {
-            const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
+        for (int j = 0; j < kPer; j++) lds_run_bounds(sDb, n, pow2, key[j] & kAAMask, lo[j], hi[j]);
+#pragma unroll
+        for (int j = 0; j < kPer; j++)
             if (live[j])
-                match_one<EMIT>(q, key[j], qinfo, sDb, winLo, 0, winN, D, dbinfo, spOf, maxTax, kmerFormat, readCnt,
-                                readOff, qcnt, out, err);
-        }
+                match_run<EMIT>(q0 + threadIdx.x + (uint64_t)j * 256, key[j], info[j], sDb, sInfo, winLo, lo[j],
+                                hi[j], D, spOf, maxTax, kmerFormat, readCnt, readOff, qcnt, c8[j], w[j], out, err);
     } else {
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
-            const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
             if (!live[j]) continue;
+            const uint64_t aa = key[j] & kAAMask;
             const uint64_t b = aa_bucket(key[j], d);
-            match_one<EMIT>(q, key[j], qinfo, dbv, 0, d.dir[b], d.dir[b + 1], D, dbinfo, spOf, maxTax, kmerFormat,
-                            readCnt, readOff, qcnt, out, err);
+            const uint64_t b1 = d.dir[b + 1];
+            const uint64_t lo = lower_bound_u64(dbv, d.dir[b], b1, aa);
+            const uint64_t hi = lower_bound_u64(dbv, lo, b1, aa + (1ull << 24));
+            match_run<EMIT>(q0 + threadIdx.x + (uint64_t)j * 256, key[j], info[j], dbv, dbinfo, 0, lo, hi, D, spOf,
+                            maxTax, kmerFormat, readCnt, readOff, qcnt, c8[j], w[j], out, err);
         }
     }
 }
