@@ -148,6 +148,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(upload(&c->dbinfo, db.info, s));
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
+    if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
@@ -424,13 +425,12 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     bool inB = false;
     // The index join (K4) does not need a total order: matches are put in compareMatches order per
-    // read by K5, a total order for a valid DB. Sorting on the top 24 bits of the 36-bit base-21
-    // AA rank groups queries whose AA k-mers share ~6 leading amino acids, which is all the
-    // locality the directory lookups need: three passes instead of five.
+    // read by K5, a total order for a valid DB. Sorting on the top 24 bits of the 36-bit AA rank
+    // (resident rank form) groups queries whose AA k-mers share ~6 leading amino acids, which is
+    // all the locality the K4 windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[2], s));
     uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), c->keysB.as<uint64_t>(),
-                                  c->valsB.as<uint64_t>(), R, kQuerySortLo, kQuerySortHi, true,
-                                  c->par.kmer_format == 2, c->radixCounts.as<uint32_t>(),
+                                  c->valsB.as<uint64_t>(), R, kQuerySortLo, kQuerySortHi, true, c->radixCounts.as<uint32_t>(),
                                   c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
@@ -543,7 +543,8 @@ int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out
         HIP_TRY(hipMemcpy(k.data(), kp, 8 * c->Q, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(v.data(), vp, 8 * c->Q, hipMemcpyDeviceToHost));
     }
-    for (uint64_t i = 0; i < c->Q; i++) out[i] = mtb_kmer{k[i], v[i]};
+    const bool packed = c->par.kmer_format == 2;  // back from the resident rank form
+    for (uint64_t i = 0; i < c->Q; i++) out[i] = mtb_kmer{packed ? host_from_rank_form(k[i]) : k[i], v[i]};
     return MTB_OK;
 }
 

@@ -305,14 +305,10 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
         }
         uint64_t key = kSentinel, info = 0;
         if (ok) {
-            uint64_t aaPart;
-            if (kmerFormat == 2) {
-                aaPart = aaAcc & ((1ull << 40) - 1);
-            } else {
-                aaPart = 0;
+            // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
+            uint64_t aaPart = 0;
 #pragma unroll
-                for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
-            }
+            for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
             key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
             uint32_t pos;
             if (fromLeft) pos = (uint32_t)(s0 + 3 * p);
@@ -345,29 +341,15 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
 // LDS-staged tile so each digit run leaves the block as one contiguous write. Each wave ranks its
 // own 1024-key slice with match-any ballots against a wave-private histogram, so the tile needs
 // two block barriers per pass rather than several per 256 keys. The first pass (FILTER) drops
-// sentinel keys: the compaction of blank reserved slots costs nothing extra. RANK21 takes the
-// digits from the base-21 rank of a format-2 k-mer's eight 5-bit AA codes (36 dense bits instead of
-// 40 sparse ones), which is monotone in the k-mer order.
+// sentinel keys: the compaction of blank reserved slots costs nothing extra.
 // ------------------------------------------------------------------------------------------------
 constexpr int kRadixItems = 16;
 constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
 constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
-__device__ __forceinline__ uint64_t rank21_key(uint64_t k) {
-    const uint64_t aa = k >> 24;
-    uint64_t r = 0;
-#pragma unroll
-    for (int i = 7; i >= 0; i--) r = r * 21 + ((aa >> (5 * i)) & 31u);
-    return (r << 24) | (k & 0xFFFFFFull);
-}
+__device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) { return (uint32_t)((k >> shift) & 0xFF); }
 
-template <bool RANK21>
-__device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) {
-    if (RANK21) k = rank21_key(k);
-    return (uint32_t)((k >> shift) & 0xFF);
-}
-
-template <bool FILTER, bool RANK21>
+template <bool FILTER>
 __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
                                                     uint32_t* __restrict__ counts, uint32_t nTiles) {
     __shared__ uint32_t hist[256];
@@ -383,13 +365,13 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
 #pragma unroll
     for (int k = 0; k < kRadixItems; k++) {
         const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
-        if (i < n && (!FILTER || key[k] != kSentinel)) atomicAdd(&hist[radix_digit<RANK21>(key[k], shift)], 1u);
+        if (i < n && (!FILTER || key[k] != kSentinel)) atomicAdd(&hist[radix_digit(key[k], shift)], 1u);
     }
     __syncthreads();
     counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
 }
 
-template <bool FILTER, bool RANK21>
+template <bool FILTER>
 __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn,
                                                        const uint64_t* __restrict__ valsIn, uint64_t n, int shift,
                                                        const uint64_t* __restrict__ offs, uint32_t nTiles,
@@ -430,7 +412,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     for (int r = 0; r < kRadixItems; r++) {
         const uint64_t i = base + (uint64_t)r * 64 + lane;
         const bool valid = i < n && (!FILTER || k[r] != kSentinel);
-        const uint32_t d = valid ? radix_digit<RANK21>(k[r], shift) : 0u;
+        const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
         unsigned long long peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -482,8 +464,8 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 // filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
 // *inB tells which.
 uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
-                          int bitHi, bool filter, bool rank21, uint32_t* counts, uint64_t* offs, void* scanTmp,
-                          bool* inB, hipStream_t s) {
+                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+                          hipStream_t s) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *vi = valsA, *ko = keysB, *vo = valsB;
     bool first = true;
@@ -492,22 +474,17 @@ uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uin
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
         const bool f = first && filter;
-        if (f && rank21) k_radix_hist<true, true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
-        else if (f) k_radix_hist<true, false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
-        else if (rank21) k_radix_hist<false, true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
-        else k_radix_hist<false, false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
         if (f) {
-            if (rank21) k_radix_scatter<true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
-            else k_radix_scatter<true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+            k_radix_scatter<true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
             uint64_t kept = 0;
             hipMemcpyAsync(&kept, offs + 256ull * nTiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
             hipStreamSynchronize(s);
             cur = kept;
-        } else if (rank21) {
-            k_radix_scatter<false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         } else {
-            k_radix_scatter<false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+            k_radix_scatter<false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         }
         first = false;
         std::swap(ki, ko);
@@ -571,27 +548,43 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* __restrict__
     return lo;
 }
 
-// AA-prefix bucket of a k-mer value. Format 2 packs 8 five-bit AA codes (first AA most
-// significant); format 1 is a base-21 integer of the same 8 codes. Query codes are 0..20, so
-// ranking the first L codes in base 21 is monotone in the k-mer order for both formats.
-__device__ __forceinline__ uint64_t aa_bucket(uint64_t v, const AADir& d) {
+// AA-prefix bucket of a resident k-mer: keys and DB values are held in rank form (the AA part is
+// the base-21 rank of the 8 AA codes, see to_rank_form), so the first L AAs are rank / 21^(8-L).
+__device__ __forceinline__ uint64_t aa_bucket(uint64_t v, const AADir& d) { return (v >> 24) / d.div; }
+
+// Smallest k-mer value in bucket b.
+__device__ __forceinline__ uint64_t aa_bucket_floor(uint64_t b, const AADir& d) { return (b * d.div) << 24; }
+
+// Format 2 packs the 8 AA codes (0..20) as 5-bit fields; the resident form replaces that AA part
+// with its base-21 rank (what format 1 stores already). The map is monotone, so sorted stays
+// sorted, and the 24-bit DNA part, all the hamming and path code reads, is untouched; the AA part
+// becomes 36 dense bits (fewer radix passes, plain division for the directory).
+__host__ __device__ inline uint64_t to_rank_form(uint64_t v) {
     const uint64_t aa = v >> 24;
-    if (d.fmt != 2) return aa / d.div;
     uint64_t r = 0;
-    for (int i = 0; i < d.L; i++) r = r * 21 + ((aa >> (5 * (7 - i))) & 31u);
-    return r;
+    for (int i = 7; i >= 0; i--) r = r * 21 + ((aa >> (5 * i)) & 31u);
+    return (r << 24) | (v & 0xFFFFFFull);
 }
 
-// Smallest k-mer value in bucket b (digits of b in the top L AA slots, the rest zero).
-__device__ __forceinline__ uint64_t aa_bucket_floor(uint64_t b, const AADir& d) {
-    if (d.fmt != 2) return (b * d.div) << 24;
-    uint64_t aa = 0;
-    for (int i = d.L - 1; i >= 0; i--) {
-        aa |= (b % 21) << (5 * (7 - i));
-        b /= 21;
+__host__ __device__ inline uint64_t from_rank_form(uint64_t v) {
+    uint64_t r = v >> 24, aa = 0;
+    for (int i = 0; i < 8; i++) {
+        aa |= (r % 21) << (5 * i);
+        r /= 21;
     }
-    return aa << 24;
+    return (aa << 24) | (v & 0xFFFFFFull);
 }
+
+__global__ void k_to_rank_form(uint64_t* __restrict__ v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = to_rank_form(v[i]);
+}
+
+void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
+    if (n) k_to_rank_form<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(v, n);
+}
+
+uint64_t host_from_rank_form(uint64_t v) { return from_rank_form(v); }
 
 __global__ void k_build_dir(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
     uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -623,26 +616,6 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 constexpr int kMatchQ = 512;
 constexpr int kMatchWin = 2048;
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
-
-__device__ __forceinline__ uint64_t aa_rank36(uint64_t key, int fmt) {
-    const uint64_t aa = key >> 24;
-    if (fmt != 2) return aa;
-    uint64_t r = 0;
-#pragma unroll
-    for (int i = 7; i >= 0; i--) r = r * 21 + ((aa >> (5 * i)) & 31u);
-    return r;
-}
-
-__device__ __forceinline__ uint64_t rank_floor_value(uint64_t r, int fmt) {  // smallest value of AA rank r
-    if (fmt != 2) return r << 24;
-    uint64_t aa = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        aa |= (r % 21) << (5 * i);
-        r /= 21;
-    }
-    return aa << 24;
-}
 
 __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
     const uint64_t b = aa_bucket(v, d);
@@ -727,8 +700,8 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
     const uint32_t side = (uint32_t)(i & 1);
     const uint64_t q = side ? min((b + 1) * kMatchQ, Q) - 1 : b * kMatchQ;
     const int sh = kQuerySortLo - 24;
-    const uint64_t r = ((aa_rank36(qkey[q], kmerFormat) >> sh) + side) << sh;
-    win[i] = r >= kRankEnd ? D : db_lower_bound(dbv, d, rank_floor_value(r, kmerFormat));
+    const uint64_t r = (((qkey[q] >> 24) >> sh) + side) << sh;
+    win[i] = r >= kRankEnd ? D : db_lower_bound(dbv, d, r << 24);
 }
 
 template <bool EMIT>

@@ -69,11 +69,13 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
                     uint64_t* vals, hipStream_t s);
 
 uint64_t radix_counts_elems(uint64_t n);
-// rank21: digits of the base-21 AA rank of a format-2 k-mer (see k_radix_scatter)
 uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
-                          int bitHi, bool filter, bool rank21, uint32_t* counts, uint64_t* offs, void* scanTmp,
-                          bool* inB, hipStream_t s);
-// query k-mers are ordered by these bits of the base-21 AA rank key (rank << 24 | DNA part)
+                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+                          hipStream_t s);
+// format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
+void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
+uint64_t host_from_rank_form(uint64_t v);
+// query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
 
 void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,

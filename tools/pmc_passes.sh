@@ -1,8 +1,15 @@
+#!/bin/bash
+# Collect rocprofv3 PMC counters for one bench step in separate passes (no tracing domains are
+# combined with --pmc). Output under gpurun_out/pmc/<pass>/.
 set -e
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 B="python bench.py --steps 1 --warmup 0 --cpu-sample 0"
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -f csv -d gpurun_out/pmc/sq -o run -- $B > gpurun_out/pmc/sq.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -f csv -d gpurun_out/pmc/fetch -o run -- $B > gpurun_out/pmc/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d gpurun_out/pmc/write -o run -- $B > gpurun_out/pmc/write.log 2>&1
+pass() {
+    local name=$1; shift
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -f csv -d gpurun_out/pmc/$name -o run -- $B > gpurun_out/pmc/$name.log 2>&1
+}
+pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM
+pass mix SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
