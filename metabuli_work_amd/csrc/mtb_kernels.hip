@@ -376,8 +376,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
                                                        const uint64_t* __restrict__ valsIn, uint64_t n, int shift,
                                                        const uint64_t* __restrict__ offs, uint32_t nTiles,
                                                        uint64_t* __restrict__ keysOut, uint64_t* __restrict__ valsOut) {
-    __shared__ uint64_t sKey[kRadixTile];
-    __shared__ uint64_t sVal[kRadixTile];
+    __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
     __shared__ uint64_t sDst[256];  // global slot of this tile's first key of digit d, minus its tile offset
@@ -440,22 +439,24 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         for (int ww = 0; ww < kWaves; ww++) { waveHist[ww][tid] = run; run += c[ww]; }
     }
     __syncthreads();
+    // keys and values go through one LDS tile in two rounds (half the LDS of staging both, so
+    // twice the resident blocks per CU to hide the ranking's dependency chains)
 #pragma unroll
     for (int r = 0; r < kRadixItems; r++) {
         if (rk[r] == ~0u) continue;
         const uint32_t d = rk[r] >> 16;
-        const uint32_t pos = waveHist[w][d] + (rk[r] & 0xFFFFu);
-        sKey[pos] = k[r];
-        sVal[pos] = v[r];
-        sDig[pos] = (uint8_t)d;
+        rk[r] = waveHist[w][d] + (rk[r] & 0xFFFFu);  // now the tile position
+        sKV[rk[r]] = k[r];
+        sDig[rk[r]] = (uint8_t)d;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < sKept; i += kBlock) {
-        const uint32_t d = sDig[i];
-        const uint64_t dst = sDst[d] + i;
-        keysOut[dst] = sKey[i];
-        valsOut[dst] = sVal[i];
-    }
+    for (uint32_t i = tid; i < sKept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRadixItems; r++)
+        if (rk[r] != ~0u) sKV[rk[r]] = v[r];
+    __syncthreads();
+    for (uint32_t i = tid; i < sKept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sKV[i];
 }
 
 uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) / kRadixTile) + 1; }
