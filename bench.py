@@ -34,7 +34,7 @@ from metabuli_work_amd.classifier import Classifier, LocalParameters  # noqa: E4
 from metabuli_work_amd.dbbuild import build_db  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-KERNELS = ["extract", "kmer_sort", "match_count", "match_emit", "match_sort", "assign"]
+KERNELS = ["extract", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 
 
 def log(rank, *a):
@@ -223,8 +223,9 @@ def main():
     alg = {
         "extract": read_bytes + 16 * R,                     # reads in, one 16-B slot per window out
         "kmer_sort": 16 * R + 16 * Q,                       # the pairs read once, the kept pairs written once
-        "match_count": 16 * Q + 8 * min(D, Q),              # queries + the DB values their AA runs touch
-        "match_emit": 16 * Q + 12 * min(D, Q) + 24 * M,     # + info of candidates, matches written
+        "match_join": 16 * Q + 12 * D + 24 * M,             # queries, the DB (values + taxIDs) streamed through
+                                                            # the block windows once, staged matches written
+        "match_transpose": 2 * 24 * M + 8 * n,              # staged matches read, written to read segments
         "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
         "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
     }

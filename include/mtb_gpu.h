@@ -150,7 +150,8 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
 int mtb_last_stage_ms(const mtb_ctx* ctx, float* ms, int n);
 /* Device time of the main kernels of the last batch in ms, from event pairs recorded on the
  * launch stream tightly around each launch: [0] K1 extract, [1] K2 radix sort (all passes),
- * [2] K4 match count, [3] K4 match emit, [4] K5 per-read match sort, [5] K6 assign. */
+ * [2] K4 join (windows + select + stage), [3] K4 transpose into per-read segments, [4] K5 per-read
+ * match sort, [5] K6 assign. */
 int mtb_last_kernel_ms(const mtb_ctx* ctx, float* ms, int n);
 /* Copy the last batch's mtb_result[n_reads] to dst (device memory if dst_on_device). */
 int mtb_copy_results(mtb_ctx* ctx, void* dst, int dst_on_device);

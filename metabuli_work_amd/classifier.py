@@ -155,7 +155,7 @@ class Classifier:
         return np.array(list(ms), np.float32)
 
     def kernel_ms(self) -> np.ndarray:
-        """[extract, k-mer sort, match count, match emit, match sort, assign] of the last batch
+        """[extract, k-mer sort, match join, match transpose, match sort, assign] of the last batch
         (HIP events)."""
         ms = (ctypes.c_float * 6)()
         lib().mtb_last_kernel_ms(self.handle, ms, 6)

@@ -71,7 +71,8 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, qcnt;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, mStage, mTotal;
+    uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
@@ -221,7 +222,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->qcnt, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->mStage, &c->mTotal, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -438,35 +439,51 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
     const uint64_t* qi = inB ? c->valsB.as<uint64_t>() : c->valsA.as<uint64_t>();
     HIP_TRY(hipEventRecord(c->ev[2], s));
-    // K4 match: count, scan per-read counts, emit into per-read segments
+    // K4 join: one pass selects and stages the matches in AA order, counting them per read; a
+    // transpose pass then moves them into per-read segments (KmerMatcher::matchKmers)
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
-    HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
-    HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
+    HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
     HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
-    HIP_TRY(c->qcnt.ensure(std::max<uint64_t>(Q, 1)));
+    c->stageRegion = std::max<uint64_t>(c->stageRegion, std::max<uint64_t>(Q / 4 / kStageRegions, 64));
+    HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+    HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     HIP_TRY(hipEventRecord(c->kev[4], s));
     launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
-    launch_match(false, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
-                 c->readCnt.as<uint32_t>(), nullptr, nullptr, c->errFlag.as<int>(), c->matchWinCap,
-                 c->matchWin.as<uint64_t>(), c->qcnt.as<uint8_t>(), s);
-    HIP_TRY(hipEventRecord(c->kev[5], s));
-    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t M = 0;
-    HIP_TRY(hipMemcpyAsync(&M, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<unsigned long long> regTot(kStageRegions);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+        HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
+        launch_match(qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+                     c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
+                     c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(), s);
+        HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        M = 0;
+        uint64_t most = 0;
+        for (unsigned long long t : regTot) {
+            M += t;
+            most = std::max<uint64_t>(most, t);
+        }
+        if (most <= c->stageRegion || M >= kMaxBatchMatches) break;
+        c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
+        HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+    }
+    HIP_TRY(hipEventRecord(c->kev[5], s));
     if (M >= kMaxBatchMatches) {
         set_error("batch produced >= 2^32 matches: split it into smaller batches");
         return MTB_ERR_ARG;
     }
+    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     c->M = M;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipEventRecord(c->kev[6], s));
-    launch_match(true, qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
-                 c->readCnt.as<uint32_t>(), c->mOff.as<uint64_t>(), c->matches.as<mtb_match>(), c->errFlag.as<int>(),
-                 c->matchWinCap, c->matchWin.as<uint64_t>(), c->qcnt.as<uint8_t>(), s);
+    launch_match_transpose(c->mStage.as<mtb_match>(), c->stageRegion, c->mTotal.as<unsigned long long>(),
+                           c->mOff.as<uint64_t>(), c->readCnt.as<uint32_t>(), c->matches.as<mtb_match>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     // K5 + K6

@@ -624,36 +624,24 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
 }
 
 // One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
-// Second half of one query's match, given its AA run [lo, hi) in vals (LDS window or the whole
-// DB; vOff = DB index of vals[0], infos aligned with vals). COUNT: writes the query's match count
-// (saturated at 255) to qcnt and adds it to its read. EMIT (queries with qcnt != 0 only): a count
-// below 255 is exact, so the read's slots were claimed (w) before the search.
-template <bool EMIT>
-__device__ __forceinline__ void match_run(uint64_t q, uint64_t key, uint64_t info, const uint64_t* vals,
-                                          const uint32_t* infos, uint64_t vOff, uint64_t lo, uint64_t hi, uint64_t D,
-                                          const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                          uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                          uint8_t* __restrict__ qcnt, uint32_t c8, uint64_t w,
-                                          mtb_match* __restrict__ out, int* __restrict__ err) {
+// One query's AA run [lo, hi) in vals (LDS window or the whole DB; vOff = DB index of vals[0],
+// infos aligned with vals): the selection threshold and the number of selected candidates.
+__device__ __forceinline__ uint32_t run_select(uint64_t key, const uint64_t* vals, uint64_t vOff, uint64_t lo,
+                                               uint64_t& hi, uint64_t D, uint32_t& thr) {
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
-    if (lo >= hi) {
-        if (!EMIT) qcnt[q] = 0;
-        return;
-    }
+    if (lo >= hi) return 0;
     uint32_t minSum = 255;
     for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, vals[t]));
-    const uint32_t thr = min(minSum * 2u, 7u);
-    const uint32_t seq = info_seq(info);
-    if (!EMIT || c8 == 255) {
-        uint32_t c = 0;
-        for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
-        if (!EMIT) {
-            qcnt[q] = (uint8_t)min(c, 255u);
-            if (c) atomicAdd(&readCnt[seq - 1], c);
-            return;
-        }
-        w = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c);
-    }
+    thr = min(minSum * 2u, 7u);
+    uint32_t c = 0;
+    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
+    return c;
+}
+
+__device__ __forceinline__ void run_emit(uint64_t key, uint64_t info, const uint64_t* vals, const uint32_t* infos,
+                                         uint64_t lo, uint64_t hi, uint32_t thr, const int32_t* __restrict__ spOf,
+                                         uint32_t maxTax, int kmerFormat, mtb_match* __restrict__ out, uint64_t w,
+                                         int* __restrict__ err) {
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
         const uint64_t tv = vals[t];
@@ -705,89 +693,114 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
     win[i] = r >= kRankEnd ? D : db_lower_bound(dbv, d, r << 24);
 }
 
-template <bool EMIT>
+// The join in one pass. Each block selects its queries' candidates, counts them (per read with
+// atomics, per thread for the block), claims one contiguous stretch of the staging buffer with a
+// single atomic, and writes its matches there with the lanes' stretches adjacent. The buffer is
+// kStageRegions regions of `region` slots, each with its own counter (block b uses b mod
+// kStageRegions), so the claims do not all queue on one address. A later pass moves each match
+// into its read's segment (k_match_transpose). A region that would overflow is not written; the
+// caller grows the regions to the largest count and reruns.
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
                                                uint64_t Q, const uint64_t* __restrict__ dbv,
                                                const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                               uint32_t* __restrict__ readCnt, const uint64_t* __restrict__ readOff,
-                                               uint8_t* __restrict__ qcnt, mtb_match* __restrict__ out,
-                                               int* __restrict__ err, uint32_t winCap,
-                                               const uint64_t* __restrict__ win) {
+                                               uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
+                                               mtb_match* __restrict__ buf, uint64_t region, int* __restrict__ err,
+                                               uint32_t winCap, const uint64_t* __restrict__ win) {
     __shared__ uint64_t sDb[kMatchWin];
-    __shared__ uint32_t sInfo[EMIT ? kMatchWin : 1];  // EMIT: the window's taxIDs, loaded coalesced
+    __shared__ uint32_t sInfo[kMatchWin];
+    __shared__ unsigned long long sBase;
     constexpr int kPer = kMatchQ / 256;
     const uint64_t q0 = (uint64_t)blockIdx.x * kMatchQ;
     const uint64_t q1 = min(q0 + (uint64_t)kMatchQ, Q);
-    // every independent load of the block is issued up front (query keys and infos, counts, the
-    // window bounds, then the window) so their latencies overlap instead of adding up
-    uint64_t key[kPer], info[kPer], w[kPer];
-    uint32_t c8[kPer];
+    // every independent load of the block is issued up front (query keys and infos, the window
+    // bounds, then the window) so their latencies overlap instead of adding up
+    uint64_t key[kPer], info[kPer];
     bool live[kPer];
-    bool any = false;
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
-        c8[j] = (EMIT && q < q1) ? qcnt[q] : 0;
-        live[j] = q < q1 && (!EMIT || c8[j] != 0);  // EMIT: only queries the count pass matched
+        live[j] = q < q1;
         key[j] = live[j] ? qkey[q] : 0;
         info[j] = live[j] ? qinfo[q] : 0;
-        w[j] = 0;
-        any |= live[j];
-    }
-    if (EMIT) {
-#pragma unroll
-        for (int j = 0; j < kPer; j++)  // claim the read's slots now; the search hides the latency
-            if (live[j] && c8[j] < 255) {
-                const uint32_t seq = info_seq(info[j]);
-                w[j] = readOff[seq - 1] + atomicAdd(&readCnt[seq - 1], c8[j]);
-            }
-        if (!__syncthreads_or(any)) return;
     }
     const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
-    if (winN <= (uint64_t)winCap) {
+    const bool staged = winN <= (uint64_t)winCap;
+    uint64_t lo[kPer], hi[kPer];
+    if (staged) {
         constexpr int kLoad = kMatchWin / 256;
         uint64_t v[kLoad];
-        uint32_t tv[EMIT ? kLoad : 1];
+        uint32_t tv[kLoad];
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + j * 256;
             v[j] = i < winN ? dbv[winLo + i] : 0;
-            if (EMIT) tv[j] = i < winN ? dbinfo[winLo + i] : 0;
+            tv[j] = i < winN ? dbinfo[winLo + i] : 0;
         }
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + j * 256;
             if (i < winN) {
                 sDb[i] = v[j];
-                if (EMIT) sInfo[i] = tv[j];
+                sInfo[i] = tv[j];
             }
         }
         __syncthreads();
         const uint32_t n = (uint32_t)winN;
         uint32_t pow2 = 1;
         while (pow2 * 2 <= n) pow2 *= 2;
-        uint32_t lo[kPer], hi[kPer];
 #pragma unroll
-        for (int j = 0; j < kPer; j++) lds_run_bounds(sDb, n, pow2, key[j] & kAAMask, lo[j], hi[j]);
-#pragma unroll
-        for (int j = 0; j < kPer; j++)
-            if (live[j])
-                match_run<EMIT>(q0 + threadIdx.x + (uint64_t)j * 256, key[j], info[j], sDb, sInfo, winLo, lo[j],
-                                hi[j], D, spOf, maxTax, kmerFormat, readCnt, readOff, qcnt, c8[j], w[j], out, err);
+        for (int j = 0; j < kPer; j++) {
+            uint32_t l, h;
+            lds_run_bounds(sDb, n, pow2, key[j] & kAAMask, l, h);
+            lo[j] = l;
+            hi[j] = h;
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
-            if (!live[j]) continue;
             const uint64_t aa = key[j] & kAAMask;
             const uint64_t b = aa_bucket(key[j], d);
             const uint64_t b1 = d.dir[b + 1];
-            const uint64_t lo = lower_bound_u64(dbv, d.dir[b], b1, aa);
-            const uint64_t hi = lower_bound_u64(dbv, lo, b1, aa + (1ull << 24));
-            match_run<EMIT>(q0 + threadIdx.x + (uint64_t)j * 256, key[j], info[j], dbv, dbinfo, 0, lo, hi, D, spOf,
-                            maxTax, kmerFormat, readCnt, readOff, qcnt, c8[j], w[j], out, err);
+            lo[j] = lower_bound_u64(dbv, d.dir[b], b1, aa);
+            hi[j] = lower_bound_u64(dbv, lo[j], b1, aa + (1ull << 24));
         }
     }
+    const uint64_t* vals = staged ? sDb : dbv;
+    const uint32_t* infos = staged ? sInfo : dbinfo;
+    const uint64_t vOff = staged ? winLo : 0;
+    uint32_t c[kPer], thr[kPer], mine = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        c[j] = live[j] ? run_select(key[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+        if (c[j]) atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
+        mine += c[j];
+    }
+    unsigned long long blockTot;
+    uint64_t w = block_exclusive_scan(mine, &blockTot);
+    const uint32_t reg = blockIdx.x % kStageRegions;
+    if (threadIdx.x == 0) sBase = blockTot ? atomicAdd(&total[reg], blockTot) : 0;
+    __syncthreads();
+    const uint64_t base = sBase;
+    if (base + blockTot > region) return;  // region too small: the caller grows it and reruns
+    w += base + (uint64_t)reg * region;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        if (!c[j]) continue;
+        run_emit(key[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, w, err);
+        w += c[j];
+    }
+}
+
+// Each staged match into its read's segment; the order inside a segment is settled by K5.
+__global__ void k_match_transpose(const mtb_match* __restrict__ buf, uint64_t region,
+                                  const unsigned long long* __restrict__ total, const uint64_t* __restrict__ readOff,
+                                  uint32_t* __restrict__ cursor, mtb_match* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= region * kStageRegions || i % region >= total[i / region]) return;
+    const mtb_match m = buf[i];
+    const uint32_t r = info_seq(m.qinfo) - 1;
+    out[readOff[r] + atomicAdd(&cursor[r], 1u)] = m;
 }
 
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
@@ -799,17 +812,21 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
     k_match_windows<<<(unsigned)((2 * nb + 255) / 256), 256, 0, s>>>(qkey, Q, dbv, D, dir, kmerFormat, nb, win);
 }
 
-void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
-                  const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
-                  int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  uint32_t winCap, const uint64_t* win, uint8_t* qcnt, hipStream_t s) {
+void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv, const uint32_t* dbinfo,
+                  uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
+                  uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint64_t region, int* err,
+                  uint32_t winCap, const uint64_t* win, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
-    if (emit) k_match<true><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                                   readCnt, readOff, qcnt, out, err, winCap, win);
-    else k_match<false><<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                               readCnt, readOff, qcnt, out, err, winCap, win);
+    k_match<<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt, total, buf,
+                                   region, err, winCap, win);
+}
+
+void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
+                            const uint64_t* readOff, uint32_t* cursor, mtb_match* out, hipStream_t s) {
+    const uint64_t slots = region * kStageRegions;
+    if (slots) k_match_transpose<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(buf, region, total, readOff, cursor, out);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

@@ -94,11 +94,17 @@ struct AADir {
 AADir make_aa_dir(uint64_t D, int kmerFormat);
 void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s);
 
-void launch_match(bool emit, const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv,
-                  const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax,
-                  int kmerFormat, uint32_t* readCnt, const uint64_t* readOff, mtb_match* out, int* err,
-                  uint32_t winCap, const uint64_t* win, uint8_t* qcnt, hipStream_t s);  // winCap: max DB values staged per block;
-// qcnt: Q bytes, written by the count pass and read by the emit pass
+// K4 join: per-read counts into readCnt; matches staged in buf = kStageRegions regions of
+// `region` slots, total[k] = matches claimed in region k (all written iff every total[k] <= region).
+// winCap: max DB values staged in LDS per block.
+constexpr uint32_t kStageRegions = 256;
+void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv, const uint32_t* dbinfo,
+                  uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
+                  uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint64_t region, int* err,
+                  uint32_t winCap, const uint64_t* win, hipStream_t s);
+// staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
+void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
+                            const uint64_t* readOff, uint32_t* cursor, mtb_match* out, hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
