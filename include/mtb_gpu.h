@@ -35,6 +35,7 @@ extern "C" {
 #define MTB_ERR_DB (-4)        /* DB inconsistent with taxonomy: KmerMatcher.cpp:292-300 exits */
 #define MTB_ERR_OOM (-5)
 #define MTB_ERR_UNSUPPORTED (-6)
+#define MTB_ERR_INTERNAL (-7)  /* a device-side consistency check failed */
 
 /* Flags for mtb_classify_batch. */
 #define MTB_INPUT_DEVICE 1u    /* seq/off pointers are device (HBM) pointers */

@@ -483,7 +483,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
     HIP_TRY(hipEventRecord(c->kev[6], s));
     launch_match_transpose(c->mStage.as<mtb_match>(), c->stageRegion, c->mTotal.as<unsigned long long>(),
-                           c->mOff.as<uint64_t>(), c->readCnt.as<uint32_t>(), c->matches.as<mtb_match>(), s);
+                           c->mOff.as<uint64_t>(), n, c->readCnt.as<uint32_t>(), c->matches.as<mtb_match>(),
+                           c->errFlag.as<int>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     // K5 + K6
@@ -498,6 +499,10 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     for (int k = 0; k < mtb_ctx::kNumKern; k++)
         HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
+    if (err == 2) {
+        set_error("internal error: a staged match names a read outside the batch");
+        return MTB_ERR_INTERNAL;
+    }
     if (err) {
         set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
         return MTB_ERR_DB;

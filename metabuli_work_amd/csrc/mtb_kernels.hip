@@ -795,11 +795,16 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 // Each staged match into its read's segment; the order inside a segment is settled by K5.
 __global__ void k_match_transpose(const mtb_match* __restrict__ buf, uint64_t region,
                                   const unsigned long long* __restrict__ total, const uint64_t* __restrict__ readOff,
-                                  uint32_t* __restrict__ cursor, mtb_match* __restrict__ out) {
+                                  uint32_t nReads, uint32_t* __restrict__ cursor, mtb_match* __restrict__ out,
+                                  int* __restrict__ err) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= region * kStageRegions || i % region >= total[i / region]) return;
     const mtb_match m = buf[i];
     const uint32_t r = info_seq(m.qinfo) - 1;
+    if (r >= nReads) {  // cannot happen for staged matches; never write out of bounds
+        atomicExch(err, 2);
+        return;
+    }
     out[readOff[r] + atomicAdd(&cursor[r], 1u)] = m;
 }
 
@@ -824,9 +829,12 @@ void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const
 }
 
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
-                            const uint64_t* readOff, uint32_t* cursor, mtb_match* out, hipStream_t s) {
+                            const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
+                            hipStream_t s) {
     const uint64_t slots = region * kStageRegions;
-    if (slots) k_match_transpose<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(buf, region, total, readOff, cursor, out);
+    if (slots)
+        k_match_transpose<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(buf, region, total, readOff, nReads, cursor,
+                                                                          out, err);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

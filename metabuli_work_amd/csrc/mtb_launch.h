@@ -104,7 +104,8 @@ void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const
                   uint32_t winCap, const uint64_t* win, hipStream_t s);
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
-                            const uint64_t* readOff, uint32_t* cursor, mtb_match* out, hipStream_t s);
+                            const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
+                            hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
