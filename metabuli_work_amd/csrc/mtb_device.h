@@ -41,7 +41,7 @@ struct CodonTable {
 };
 
 // hammingLookup (KmerMatcher.h:66-70) packed as 3 bits per entry, one 24-bit row per query codon.
-__device__ __forceinline__ uint32_t hamming_lookup(uint32_t q, uint32_t t) {
+__device__ __forceinline__ uint32_t hamming_lookup_row(uint32_t q) {
     // rows: {0,1,1,1,2,1,3,3} {1,0,1,1,2,2,3,2} {1,1,0,1,2,2,2,3} {1,1,1,0,1,2,3,3}
     //       {2,2,2,1,0,1,4,4} {1,2,2,2,1,0,4,4} {3,3,2,3,4,4,0,1} {3,2,3,3,4,4,1,0}
     constexpr uint32_t R0 = 0u | 1u << 3 | 1u << 6 | 1u << 9 | 2u << 12 | 1u << 15 | 3u << 18 | 3u << 21;
@@ -52,8 +52,11 @@ __device__ __forceinline__ uint32_t hamming_lookup(uint32_t q, uint32_t t) {
     constexpr uint32_t R5 = 1u | 2u << 3 | 2u << 6 | 2u << 9 | 1u << 12 | 0u << 15 | 4u << 18 | 4u << 21;
     constexpr uint32_t R6 = 3u | 3u << 3 | 2u << 6 | 3u << 9 | 4u << 12 | 4u << 15 | 0u << 18 | 1u << 21;
     constexpr uint32_t R7 = 3u | 2u << 3 | 3u << 6 | 3u << 9 | 4u << 12 | 4u << 15 | 1u << 18 | 0u << 21;
-    uint32_t row = q == 0 ? R0 : q == 1 ? R1 : q == 2 ? R2 : q == 3 ? R3 : q == 4 ? R4 : q == 5 ? R5 : q == 6 ? R6 : R7;
-    return (row >> (3 * t)) & 7u;
+    return q == 0 ? R0 : q == 1 ? R1 : q == 2 ? R2 : q == 3 ? R3 : q == 4 ? R4 : q == 5 ? R5 : q == 6 ? R6 : R7;
+}
+
+__device__ __forceinline__ uint32_t hamming_lookup(uint32_t q, uint32_t t) {
+    return (hamming_lookup_row(q) >> (3 * t)) & 7u;
 }
 
 // getHammingDistanceSum (KmerMatcher.h:348-360): sum over the 8 codons of the DNA part.
@@ -61,6 +64,26 @@ __device__ __forceinline__ uint32_t hamming_sum(uint64_t a, uint64_t b) {
     uint32_t s = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) s += hamming_lookup((uint32_t)(a >> (3 * i)) & 7u, (uint32_t)(b >> (3 * i)) & 7u);
+    return s;
+}
+
+// The 8 lookup rows of a query k-mer's codons, selected once per query; a candidate's hamming
+// sum is then one 3-bit field extract per codon (hamming_sum_rows == hamming_sum).
+struct HamRows {
+    uint32_t r[8];
+};
+
+__device__ __forceinline__ HamRows hamming_rows(uint64_t key) {
+    HamRows h;
+#pragma unroll
+    for (int i = 0; i < 8; i++) h.r[i] = hamming_lookup_row((uint32_t)(key >> (3 * i)) & 7u);
+    return h;
+}
+
+__device__ __forceinline__ uint32_t hamming_sum_rows(const HamRows& h, uint64_t tv) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s += (h.r[i] >> (3 * ((uint32_t)(tv >> (3 * i)) & 7u))) & 7u;
     return s;
 }
 

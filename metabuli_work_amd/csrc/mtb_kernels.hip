@@ -625,27 +625,40 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
 
 // One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
 // One query's AA run [lo, hi) in vals (LDS window or the whole DB; vOff = DB index of vals[0],
-// infos aligned with vals): the selection threshold and the number of selected candidates.
-__device__ __forceinline__ uint32_t run_select(uint64_t key, const uint64_t* vals, uint64_t vOff, uint64_t lo,
+// infos aligned with vals): the selection threshold min(2 * min hamming sum, 7) and the number
+// of candidates within it, in one pass — sums <= 7 are tallied in the bytes of a 64-bit word
+// (runs of more than 255 candidates take a second pass).
+__device__ __forceinline__ uint32_t run_select(const HamRows& hr, const uint64_t* vals, uint64_t vOff, uint64_t lo,
                                                uint64_t& hi, uint64_t D, uint32_t& thr) {
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
     if (lo >= hi) return 0;
     uint32_t minSum = 255;
-    for (uint64_t t = lo; t < hi; t++) minSum = min(minSum, hamming_sum(key, vals[t]));
+    uint64_t tally = 0;
+    for (uint64_t t = lo; t < hi; t++) {
+        const uint32_t s = hamming_sum_rows(hr, vals[t]);
+        minSum = min(minSum, s);
+        if (s <= 7) tally += 1ull << (8 * s);
+    }
     thr = min(minSum * 2u, 7u);
     uint32_t c = 0;
-    for (uint64_t t = lo; t < hi; t++) c += hamming_sum(key, vals[t]) <= thr;
+    if (hi - lo <= 255) {
+#pragma unroll
+        for (uint32_t s = 0; s < 8; s++)
+            if (s <= thr) c += (uint32_t)(tally >> (8 * s)) & 0xFFu;
+    } else {
+        for (uint64_t t = lo; t < hi; t++) c += hamming_sum_rows(hr, vals[t]) <= thr;
+    }
     return c;
 }
 
-__device__ __forceinline__ void run_emit(uint64_t key, uint64_t info, const uint64_t* vals, const uint32_t* infos,
-                                         uint64_t lo, uint64_t hi, uint32_t thr, const int32_t* __restrict__ spOf,
-                                         uint32_t maxTax, int kmerFormat, mtb_match* __restrict__ out, uint64_t w,
-                                         int* __restrict__ err) {
+__device__ __forceinline__ void run_emit(uint64_t key, const HamRows& hr, uint64_t info, const uint64_t* vals,
+                                         const uint32_t* infos, uint64_t lo, uint64_t hi, uint32_t thr,
+                                         const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                         mtb_match* __restrict__ out, uint64_t w, int* __restrict__ err) {
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
         const uint64_t tv = vals[t];
-        const uint32_t hs = hamming_sum(key, tv);
+        const uint32_t hs = hamming_sum_rows(hr, tv);
         if (hs > thr) continue;
         const uint32_t tax = infos[t];
         const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
@@ -770,9 +783,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint32_t* infos = staged ? sInfo : dbinfo;
     const uint64_t vOff = staged ? winLo : 0;
     uint32_t c[kPer], thr[kPer], mine = 0;
+    HamRows hr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
-        c[j] = live[j] ? run_select(key[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+        hr[j] = hamming_rows(key[j]);
+        c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
         if (c[j]) atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
     }
@@ -787,7 +802,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         if (!c[j]) continue;
-        run_emit(key[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, w, err);
+        run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, w, err);
         w += c[j];
     }
 }
