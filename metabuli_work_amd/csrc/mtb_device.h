@@ -95,6 +95,21 @@ __device__ __forceinline__ uint32_t hamming_field(uint32_t q, uint32_t t, int fi
     return h == 4u ? 0u : h;
 }
 
+// hammings() from the query's rows: a distance of 4 occurs exactly at (q in 4-5, t in 6-7) and
+// (q in 6-7, t in 4-5); field 7 stores the first kind as 1, everything else stores 4 as 0.
+__device__ __forceinline__ uint32_t hammings_rows(const HamRows& hr, uint64_t a, uint64_t b, bool reverse) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t q = (uint32_t)(a >> (3 * i)) & 7u, t = (uint32_t)(b >> (3 * i)) & 7u;
+        const uint32_t d = (hr.r[i] >> (3 * t)) & 7u;
+        const int field = reverse ? 7 - i : i;
+        const uint32_t v = d == 4u ? ((field == 7 && q < 6u) ? 1u : 0u) : d;
+        h |= v << (2 * field);
+    }
+    return h;
+}
+
 // getHammings (forward) / getHammings_reverse (KmerMatcher.h:386-416)
 __device__ __forceinline__ uint32_t hammings(uint64_t a, uint64_t b, bool reverse) {
     uint32_t h = 0;

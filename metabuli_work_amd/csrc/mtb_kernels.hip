@@ -668,7 +668,7 @@ __device__ __forceinline__ void run_emit(uint64_t key, const HamRows& hr, uint64
         m.target_id = tax;
         m.species_id = (uint32_t)sp;
         m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
-        m.right_end_hamming = (uint16_t)hammings(key, tv, rev);
+        m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
         m.hamming = (uint8_t)hs;
         m.pad = 0;
         out[w++] = m;
