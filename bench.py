@@ -221,9 +221,9 @@ def main():
     R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
     D = hdb.n_kmers
     alg = {
-        "extract": read_bytes + 16 * R,                     # reads in, one 16-B slot per window out
-        "kmer_sort": 16 * R + 16 * Q,                       # the pairs read once, the kept pairs written once
-        "match_join": 16 * Q + 12 * D + 24 * M,             # queries, the DB (values + taxIDs) streamed through
+        "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
+        "kmer_sort": 8 * R + 12 * Q,                        # the keys read once, the kept (key, slot) written once
+        "match_join": 12 * Q + 12 * D + 24 * M,             # queries, the DB (values + taxIDs) streamed through
                                                             # the block windows once, staged matches written
         "match_transpose": 2 * 24 * M + 8 * n,              # staged matches read, written to read segments
         "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once

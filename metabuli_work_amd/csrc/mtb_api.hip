@@ -71,7 +71,8 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, mStage, mTotal;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal;
+    uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
@@ -222,7 +223,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->mStage, &c->mTotal, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->mStage, &c->mTotal, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -411,13 +412,16 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     // K1 extract
     const uint64_t Rc = std::max<uint64_t>(R, 1);
     HIP_TRY(c->keysA.ensure(8 * Rc));
-    HIP_TRY(c->valsA.ensure(8 * Rc));
+    HIP_TRY(c->valsA.ensure(4 * Rc));
     HIP_TRY(c->keysB.ensure(8 * Rc));
-    HIP_TRY(c->valsB.ensure(8 * Rc));
+    HIP_TRY(c->valsB.ensure(4 * Rc));
+    HIP_TRY(c->unitInfo.ensure(8 * std::max<uint64_t>(U, 1)));
+    if (R >= 0xFFFFFFFFull) { set_error("batch has >= 2^32 k-mer slots: split it"); return MTB_ERR_ARG; }
+    c->chunkC = C;
     HIP_TRY(hipEventRecord(c->kev[0], s));
     launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
                    c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
-                   c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), s);
+                   c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[1], s));
     HIP_TRY(hipEventRecord(c->ev[1], s));
     // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
@@ -430,14 +434,14 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     // (resident rank form) groups queries whose AA k-mers share ~6 leading amino acids, which is
     // all the locality the K4 windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[2], s));
-    uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint64_t>(), c->keysB.as<uint64_t>(),
-                                  c->valsB.as<uint64_t>(), R, kQuerySortLo, kQuerySortHi, true, c->radixCounts.as<uint32_t>(),
-                                  c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+    uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
+                                  c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
+                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
     c->sortedInB = inB;
     const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
-    const uint64_t* qi = inB ? c->valsB.as<uint64_t>() : c->valsA.as<uint64_t>();
+    const uint32_t* qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();  // K1 slots
     HIP_TRY(hipEventRecord(c->ev[2], s));
     // K4 join: one pass selects and stages the matches in AA order, counting them per read; a
     // transpose pass then moves them into per-read segments (KmerMatcher::matchKmers)
@@ -456,8 +460,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     for (int attempt = 0; attempt < 2; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
-        launch_match(qk, qi, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
-                     c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
+        launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf,
+                     (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
                      c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
@@ -558,15 +562,19 @@ int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out
     *n_out = c->Q;
     if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
     if (cap < c->Q) return MTB_RETRY;
-    std::vector<uint64_t> k(c->Q), v(c->Q);
+    std::vector<uint64_t> k(c->Q), ui(c->unitInfo.bytes / 8);
+    std::vector<uint32_t> v(c->Q);
     const void* kp = c->sortedInB ? c->keysB.p : c->keysA.p;
     const void* vp = c->sortedInB ? c->valsB.p : c->valsA.p;
     if (c->Q) {
         HIP_TRY(hipMemcpy(k.data(), kp, 8 * c->Q, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(v.data(), vp, 8 * c->Q, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(v.data(), vp, 4 * c->Q, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ui.data(), c->unitInfo.p, c->unitInfo.bytes, hipMemcpyDeviceToHost));
     }
     const bool packed = c->par.kmer_format == 2;  // back from the resident rank form
-    for (uint64_t i = 0; i < c->Q; i++) out[i] = mtb_kmer{packed ? host_from_rank_form(k[i]) : k[i], v[i]};
+    for (uint64_t i = 0; i < c->Q; i++)
+        out[i] = mtb_kmer{packed ? host_from_rank_form(k[i]) : k[i], slot_info(v[i], c->chunkC, ui.data(),
+                                                                               c->par.kmer_format)};
     return MTB_OK;
 }
 

@@ -799,7 +799,7 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
             k_group_keys<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(s.gStart, cnt[0], s.ordKA, s.ordVA,
                                                                             s.pathCnt);
             bool inB = false;
-            const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true,
+            const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true, false,
                                                     s.radixCounts, s.radixOffs, s.scanTmp, &inB, st);
             if (heavy)
                 k_match_paths<<<(unsigned)((heavy + 255) / 256), 256, 0, st>>>(

@@ -313,13 +313,13 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxo, const mtb_p
     HIP_B(hipMalloc(&counts, 4 * radix_counts_elems(R + 1)));
     HIP_B(hipMalloc(&offs, 8 * (radix_counts_elems(R + 1) + 1)));
     HIP_B(hipMalloc(&scanTmp, 8 * scan_tmp_elems(radix_counts_elems(R + 1) + R + 2)));
-    kept = radix_sort_pairs(pA, kA, pB, kB, R, 32, 32 + ((spBits + 7) / 8) * 8, true, counts, offs, scanTmp, &inB1, s);
+    kept = radix_sort_pairs(pA, kA, pB, kB, R, 32, 32 + ((spBits + 7) / 8) * 8, true, false, counts, offs, scanTmp, &inB1, s);
     {
         uint64_t* k1 = inB1 ? kB : kA;
         uint64_t* p1 = inB1 ? pB : pA;
         uint64_t* k2 = inB1 ? kA : kB;
         uint64_t* p2 = inB1 ? pA : pB;
-        radix_sort_pairs(k1, p1, k2, p2, kept, 0, 64, false, counts, offs, scanTmp, &inB2, s);
+        radix_sort_pairs(k1, p1, k2, p2, kept, 0, 64, false, false, counts, offs, scanTmp, &inB2, s);
         sk = inB2 ? k2 : k1;
         sp_ = inB2 ? p2 : p1;
     }

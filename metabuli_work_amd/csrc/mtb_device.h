@@ -19,6 +19,19 @@ __host__ __device__ inline uint32_t info_pos(uint64_t x) { return (uint32_t)x; }
 __host__ __device__ inline uint32_t info_seq(uint64_t x) { return (uint32_t)((x >> 32) & 0x1FFFFFFFu); }
 __host__ __device__ inline uint32_t info_frame(uint64_t x) { return (uint32_t)(x >> 61); }
 
+// K1 slot layout: work unit u owns window p of its chunk at slot (u / 64) * 64C + 64p + u % 64.
+// A unit's info (pack_info of its first window) plus the frame's direction gives every window's
+// info, so the sort carries 32-bit slots and K4 rebuilds the info of the queries that matched.
+__host__ __device__ inline uint64_t slot_info(uint32_t slot, uint32_t C, const uint64_t* unitInfo, int kmerFormat) {
+    const uint32_t wave = slot / (64u * C), rem = slot - wave * 64u * C;
+    const uint32_t p = rem >> 6, u = wave * 64u + (rem & 63u);
+    const uint64_t ui = unitInfo[u];
+    const uint32_t frame = (uint32_t)(ui >> 61);
+    const bool fromLeft = (kmerFormat == 2) ? frame < 3 : frame >= 3;
+    const uint32_t pos = fromLeft ? (uint32_t)ui + 3u * p : (uint32_t)ui - 3u * p;
+    return (ui & ~0xFFFFFFFFull) | pos;
+}
+
 // getMaxCoveredLength / getQueryKmerNumber (LocalUtil.h:45-59)
 __host__ __device__ inline int max_covered_length(int len) {
     int r = len % 3;

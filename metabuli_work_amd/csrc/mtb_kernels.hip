@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
                                                  const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
                                                  const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
                                                  ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
-                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ unitInfo) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     sBase[threadIdx.x] = tabs.base[threadIdx.x];
@@ -233,10 +233,7 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
         nWin = min((int)C, W - pFirst);
     }
     // slots of this unit past its windows (and of padding units) hold the sentinel
-    for (int p = max(nWin, 0); p < (int)C; p++) {
-        keys[slotBase + 64ull * p] = kSentinel;
-        vals[slotBase + 64ull * p] = 0;
-    }
+    for (int p = max(nWin, 0); p < (int)C; p++) keys[slotBase + 64ull * p] = kSentinel;
     if (nWin <= 0) return;
     const ReadMeta m = meta[r];
     const uint8_t* seq = mate ? seq2 + off2[r] : seq1 + off1[r];
@@ -254,6 +251,10 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
     const bool fromLeft = (kmerFormat == 2) ? fwd : !fwd;
     const bool comp = !fwd;
     const int nSm = 8 - smerLen + 1;
+    {
+        const uint32_t pos0 = fromLeft ? (uint32_t)(s0 + 3 * pFirst) : (uint32_t)(e0 - 3 * (pFirst + 8) + 1);
+        unitInfo[u] = pack_info(seqId, pos0 + posOffset, (uint32_t)frame);  // window p: pos0 +- 3p (slot_info)
+    }
 
     uint64_t aaAcc = 0, dnaAcc = 0, smAcc = 0;
     uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
@@ -303,20 +304,15 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
             }
             ok = (bestK == nSm - 1) || (bestK == 0);
         }
-        uint64_t key = kSentinel, info = 0;
+        uint64_t key = kSentinel;
         if (ok) {
             // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
             uint64_t aaPart = 0;
 #pragma unroll
             for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
             key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
-            uint32_t pos;
-            if (fromLeft) pos = (uint32_t)(s0 + 3 * p);
-            else pos = (uint32_t)(e0 - 3 * (p + 8) + 1);
-            info = pack_info(seqId, pos + posOffset, (uint32_t)frame);
         }
         keys[slotBase + 64ull * (p - pFirst)] = key;
-        vals[slotBase + 64ull * (p - pFirst)] = info;
     }
 }
 
@@ -325,14 +321,14 @@ uint64_t extract_slots(uint64_t nUnits, uint32_t C) { return (nUnits + 63) / 64 
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
                     uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* vals, hipStream_t s) {
+                    uint64_t* unitInfo, hipStream_t s) {
     ExtractTables tabs;
     for (int i = 0; i < 256; i++) tabs.base[i] = t.base[i];
     for (int i = 0; i < 64; i++) { tabs.aa[i] = t.aa[i]; tabs.num[i] = t.num[i]; }
     if (nUnits == 0) return;
     const uint64_t threads = (nUnits + 63) / 64 * 64;  // whole waves: padding units write sentinels
     k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits,
-                                                                C, tabs, kmerFormat, syncmer, smerLen, keys, vals);
+                                                                C, tabs, kmerFormat, syncmer, smerLen, keys, unitInfo);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -371,11 +367,13 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
     counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
 }
 
-template <bool FILTER>
-__global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn,
-                                                       const uint64_t* __restrict__ valsIn, uint64_t n, int shift,
-                                                       const uint64_t* __restrict__ offs, uint32_t nTiles,
-                                                       uint64_t* __restrict__ keysOut, uint64_t* __restrict__ valsOut) {
+// V: value type (64-bit payloads, or 32-bit slot indices). GEN: the values are the input positions
+// (the first pass of a sort of slots), so none are read.
+template <typename V, bool FILTER, bool GEN>
+__global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn, const V* __restrict__ valsIn,
+                                                       uint64_t n, int shift, const uint64_t* __restrict__ offs,
+                                                       uint32_t nTiles, uint64_t* __restrict__ keysOut,
+                                                       V* __restrict__ valsOut) {
     __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
@@ -390,7 +388,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __syncthreads();
 
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t k[kRadixItems], v[kRadixItems];
+    uint64_t k[kRadixItems];
+    V v[kRadixItems];
     uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
     // all loads first (unguarded for the full tiles) so the 32 loads of a lane are in flight
     // together; interleaving them with the ranking serialised 16 memory round trips per tile
@@ -398,13 +397,14 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) v[r] = valsIn[base + (uint64_t)r * 64 + lane];
+        for (int r = 0; r < kRadixItems; r++)
+            v[r] = GEN ? (V)(base + (uint64_t)r * 64 + lane) : valsIn[base + (uint64_t)r * 64 + lane];
     } else {
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
             k[r] = i < n ? keysIn[i] : kSentinel;
-            v[r] = i < n ? valsIn[i] : 0;
+            v[r] = GEN ? (V)i : (i < n ? valsIn[i] : (V)0);
         }
     }
 #pragma unroll
@@ -452,40 +452,44 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __syncthreads();
     for (uint32_t i = tid; i < sKept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
     __syncthreads();
+    V* sV = reinterpret_cast<V*>(sKV);
 #pragma unroll
     for (int r = 0; r < kRadixItems; r++)
-        if (rk[r] != ~0u) sKV[rk[r]] = v[r];
+        if (rk[r] != ~0u) sV[rk[r]] = v[r];
     __syncthreads();
-    for (uint32_t i = tid; i < sKept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sKV[i];
+    for (uint32_t i = tid; i < sKept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sV[i];
 }
 
 uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) / kRadixTile) + 1; }
 
 // Sorts n pairs by key bits [bitLo, bitHi). Returns the kept count (sentinels dropped when
 // filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
-// *inB tells which.
-uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
-                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+// *inB tells which. genVals: valsA is not read; the values are the input positions.
+template <typename V>
+uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
+                          bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
                           hipStream_t s) {
     uint64_t cur = n;
-    uint64_t *ki = keysA, *vi = valsA, *ko = keysB, *vo = valsB;
+    uint64_t *ki = keysA, *ko = keysB;
+    V *vi = valsA, *vo = valsB;
     bool first = true;
     *inB = false;
     for (int shift = bitLo; shift < bitHi; shift += 8) {
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
-        const bool f = first && filter;
+        const bool f = first && filter, g = first && genVals;
         if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
+        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         if (f) {
-            k_radix_scatter<true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
             uint64_t kept = 0;
             hipMemcpyAsync(&kept, offs + 256ull * nTiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
             hipStreamSynchronize(s);
             cur = kept;
-        } else {
-            k_radix_scatter<false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         }
         first = false;
         std::swap(ki, ko);
@@ -494,6 +498,11 @@ uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uin
     }
     return cur;
 }
+
+template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
+template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int, int, bool, bool,
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
 
 // ------------------------------------------------------------------------------------------------
 // K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->
@@ -623,7 +632,6 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
     return lower_bound_u64(dbv, d.dir[b], d.dir[b + 1], v);
 }
 
-// One query against DB values vals[sLo, sHi) (LDS window or the whole DB); vOff = DB index of vals[0].
 // One query's AA run [lo, hi) in vals (LDS window or the whole DB; vOff = DB index of vals[0],
 // infos aligned with vals): the selection threshold min(2 * min hamming sum, 7) and the number
 // of candidates within it, in one pass — sums <= 7 are tallied in the bytes of a 64-bit word
@@ -713,7 +721,8 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
 // kStageRegions), so the claims do not all queue on one address. A later pass moves each match
 // into its read's segment (k_match_transpose). A region that would overflow is not written; the
 // caller grows the regions to the largest count and reruns.
-__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qinfo,
+__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
+                                               const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const uint64_t* __restrict__ dbv,
                                                const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
@@ -729,13 +738,14 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     // every independent load of the block is issued up front (query keys and infos, the window
     // bounds, then the window) so their latencies overlap instead of adding up
     uint64_t key[kPer], info[kPer];
+    uint32_t slot[kPer];
     bool live[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const uint64_t q = q0 + threadIdx.x + (uint64_t)j * 256;
         live[j] = q < q1;
         key[j] = live[j] ? qkey[q] : 0;
-        info[j] = live[j] ? qinfo[q] : 0;
+        slot[j] = live[j] ? qslot[q] : 0;
     }
     const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
     const bool staged = winN <= (uint64_t)winCap;
@@ -788,6 +798,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     for (int j = 0; j < kPer; j++) {
         hr[j] = hamming_rows(key[j]);
         c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+        info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
         if (c[j]) atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
     }
@@ -832,15 +843,15 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
     k_match_windows<<<(unsigned)((2 * nb + 255) / 256), 256, 0, s>>>(qkey, Q, dbv, D, dir, kmerFormat, nb, win);
 }
 
-void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv, const uint32_t* dbinfo,
-                  uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
-                  uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint64_t region, int* err,
-                  uint32_t winCap, const uint64_t* win, hipStream_t s) {
+void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
+                  const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
+                  uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
+                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
-    k_match<<<blocks, 256, 0, s>>>(qkey, qinfo, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt, total, buf,
-                                   region, err, winCap, win);
+    k_match<<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt,
+                                   total, buf, region, err, winCap, win);
 }
 
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,

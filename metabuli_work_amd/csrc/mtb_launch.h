@@ -66,11 +66,13 @@ uint64_t extract_slots(uint64_t nUnits, uint32_t C);
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
                     uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* vals, hipStream_t s);
+                    uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
 
 uint64_t radix_counts_elems(uint64_t n);
-uint64_t radix_sort_pairs(uint64_t* keysA, uint64_t* valsA, uint64_t* keysB, uint64_t* valsB, uint64_t n, int bitLo,
-                          int bitHi, bool filter, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
+// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read)
+template <typename V>
+uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
+                          bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
                           hipStream_t s);
 // format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
@@ -98,10 +100,11 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 // `region` slots, total[k] = matches claimed in region k (all written iff every total[k] <= region).
 // winCap: max DB values staged in LDS per block.
 constexpr uint32_t kStageRegions = 256;
-void launch_match(const uint64_t* qkey, const uint64_t* qinfo, uint64_t Q, const uint64_t* dbv, const uint32_t* dbinfo,
-                  uint64_t D, const AADir& dir, const int32_t* spOf, uint32_t maxTax, int kmerFormat,
-                  uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint64_t region, int* err,
-                  uint32_t winCap, const uint64_t* win, hipStream_t s);
+// qslot: each query's K1 slot (its info is slot_info(slot, C, unitInfo))
+void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
+                  const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
+                  uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
+                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, hipStream_t s);
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
                             const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
