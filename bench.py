@@ -34,6 +34,7 @@ from metabuli_work_amd.classifier import Classifier, LocalParameters  # noqa: E4
 from metabuli_work_amd.dbbuild import build_db  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "stage_traffic.json")
 KERNELS = ["extract", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 
 
@@ -149,7 +150,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=1_000_000, help="read pairs per rank per step")
     ap.add_argument("--species", type=int, default=25000)
     ap.add_argument("--mean-genome", type=int, default=75000)
-    ap.add_argument("--cpu-sample", type=int, default=50_000, help="read pairs timed on the CPU oracle (0 = off)")
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="read pairs timed on the CPU oracle (0 = off)")
     ap.add_argument("--seed", type=int, default=5)
     args = ap.parse_args()
 
@@ -232,9 +233,21 @@ def main():
     dom = int(np.argmax(kern))
     dname = KERNELS[dom]
     achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
+    # HBM traffic of the same stage per step from rocprofv3 FETCH_SIZE/WRITE_SIZE passes over this
+    # workload (tools/pmc_passes.sh + tools/stage_profile.py, committed under profiles/)
+    traffic, traffic_src = None, None
+    try:
+        with open(TRAFFIC_FILE) as f:
+            tf = json.load(f)
+        if tf.get("pairs") == n and tf.get("species") == args.species and dname in tf["stages"]:
+            traffic = tf["stages"][dname]["hbm_bytes"]
+            traffic_src = os.path.relpath(TRAFFIC_FILE, ROOT)
+    except (OSError, ValueError, KeyError):
+        pass
     roofline = {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "alg_bytes_per_launch": int(alg[dname]), "avg_launch_ms": round(float(kern[dom]), 3)}
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": traffic_src, "alg_bytes_per_launch": int(alg[dname]),
+                "avg_launch_ms": round(float(kern[dom]), 3)}
 
     # ---- CPU baseline: the oracle (restated reference algorithm, OpenMP) on a bounded sample ----
     cpu = None

@@ -1,0 +1,99 @@
+"""Per-stage GPU time and HBM traffic of one classify step, from rocprofv3 output.
+
+Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by their order
+within a step: a step starts at k_read_meta; extract = k_extract; kmer_sort = everything from
+there to k_match_windows; match_join = k_match_windows + k_match (+ a rerun if the staging
+buffer grew); match_transpose = k_match_transpose; match_sort = k_segsort_*; assign = the rest
+of the step (K6 kernels, scans and taxcnt compaction). The last complete step is reported.
+
+Usage:
+  python tools/stage_profile.py time  <run_kernel_trace.csv>
+  python tools/stage_profile.py bytes <fetch run_counter_collection.csv> <write run_counter_collection.csv>
+FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE is doubled (MI355X_MICROARCH.md: on gfx950 it
+counts half the bytes of a wide coalesced read), WRITE_SIZE is taken as is.
+"""
+import collections
+import csv
+import json
+import sys
+
+STAGES = ["extract", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("mtb::", "").strip()
+
+
+def stage_of(seq):
+    """seq: kernel short names of one step in dispatch order -> stage name per dispatch."""
+    out = []
+    stage = "extract"
+    after_extract = False
+    for k in seq:
+        if k.startswith("k_read_meta"):
+            stage, after_extract = "extract", False
+        elif k.startswith("k_extract"):
+            stage, after_extract = "extract", True
+        elif k.startswith("k_match_windows") or k.startswith("k_match<") or k == "k_match":
+            stage = "match_join"
+        elif k.startswith("k_match_transpose"):
+            stage = "match_transpose"
+        elif k.startswith("k_segsort") or k.startswith("k_max_seg"):
+            stage = "match_sort"
+        elif stage == "match_sort":
+            stage = "assign"
+        elif stage == "extract" and after_extract:
+            stage = "kmer_sort"
+        out.append(stage)
+    return out
+
+
+def last_step(rows):
+    """rows: (dispatch_id, short_name, payload) sorted by dispatch; returns the last full step."""
+    starts = [i for i, r in enumerate(rows) if r[1].startswith("k_read_meta")]
+    if len(starts) < 2:
+        return rows[starts[-1]:] if starts else rows
+    return rows[starts[-2]:starts[-1]] if len(starts) >= 2 else rows
+
+
+def main():
+    mode = sys.argv[1]
+    if mode == "time":
+        rows = []
+        for r in csv.DictReader(open(sys.argv[2])):
+            if r.get("Kind", "KERNEL_DISPATCH") != "KERNEL_DISPATCH":
+                continue
+            rows.append((int(r["Dispatch_Id"]), short(r["Kernel_Name"]),
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+        rows.sort()
+        step = last_step(rows)
+        st = stage_of([r[1] for r in step])
+        tot = collections.OrderedDict((s, 0.0) for s in STAGES)
+        kern = collections.defaultdict(float)
+        for (d, k, ms), s in zip(step, st):
+            tot[s] += ms
+            kern[(s, k)] += ms
+        print(json.dumps({"stage_ms": {k: round(v, 3) for k, v in tot.items()},
+                          "kernels": {f"{s}/{k}": round(v, 3) for (s, k), v in sorted(kern.items())}}, indent=1))
+    else:
+        res = {}
+        for path, counter, scale in ((sys.argv[2], "FETCH_SIZE", 2.0), (sys.argv[3], "WRITE_SIZE", 1.0)):
+            rows = []
+            for r in csv.DictReader(open(path)):
+                if r["Counter_Name"] != counter:
+                    continue
+                rows.append((int(r["Dispatch_Id"]), short(r["Kernel_Name"]), float(r["Counter_Value"]) * 1024 * scale))
+            rows.sort()
+            step = last_step(rows)
+            st = stage_of([r[1] for r in step])
+            tot = collections.OrderedDict((s, 0.0) for s in STAGES)
+            for (d, k, b), s in zip(step, st):
+                tot[s] += b
+            res[counter] = tot
+        out = {s: {"fetch_bytes": int(res["FETCH_SIZE"][s]), "write_bytes": int(res["WRITE_SIZE"][s]),
+                   "hbm_bytes": int(res["FETCH_SIZE"][s] + res["WRITE_SIZE"][s])} for s in STAGES}
+        print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
