@@ -141,6 +141,51 @@ def make_reads_gpu(seq, off_t, n_pairs, seed, dev, read_len=150, sub_rate=0.005,
     return out[0], off, out[1], off.clone()
 
 
+def make_long_reads_gpu(seq, off_t, n_reads, seed, dev, n50=10000, min_len=1000, sub_rate=0.05, indel_rate=0.01):
+    """ONT-style single-end reads (SURVEY §8(d) config 4 shape): lognormal lengths (N50 ~10 kb,
+    >= 1 kb), random strand, 5% substitutions, 1% indels (half deletions, half insertions)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    glen = (off_t[1:] - off_t[:-1]).cpu().numpy()
+    cum = np.cumsum(glen)
+    gsel = np.searchsorted(cum, rng.random(n_reads) * cum[-1], side="right").clip(max=len(glen) - 1)
+    L = np.minimum(glen[gsel], np.maximum(min_len, rng.lognormal(np.log(n50 * 0.8), 0.5, n_reads))).astype(np.int64)
+    st = (rng.random(n_reads) * (glen[gsel] - L + 1)).astype(np.int64)
+    p0 = off_t.cpu().numpy()[gsel] + st
+    lens = torch.from_numpy(L).to(dev)
+    roff = torch.zeros(n_reads + 1, dtype=torch.int64, device=dev)
+    roff[1:] = torch.cumsum(lens, 0)
+    tot = int(roff[-1].item())
+    rid = torch.repeat_interleave(torch.arange(n_reads, device=dev), lens)
+    within = torch.arange(tot, device=dev) - roff[rid]
+    rev = torch.from_numpy(rng.random(n_reads) < 0.5).to(dev)
+    pos = torch.where(rev[rid], torch.from_numpy(p0).to(dev)[rid] + lens[rid] - 1 - within,
+                      torch.from_numpy(p0).to(dev)[rid] + within)
+    b = seq[pos]
+    comp = torch.zeros(256, dtype=torch.uint8, device=dev)
+    comp[torch.tensor([65, 67, 71, 84], device=dev)] = torch.tensor([84, 71, 67, 65], dtype=torch.uint8, device=dev)
+    b = torch.where(rev[rid], comp[b.long()], b)
+    lut = torch.tensor([65, 67, 71, 84], dtype=torch.uint8, device=dev)
+    sub = torch.rand(tot, device=dev, generator=g) < sub_rate
+    b = torch.where(sub, lut[torch.randint(0, 4, (tot,), device=dev, generator=g)], b)
+    # indels: each base is kept 0 (deleted), 1 or 2 times (a random base inserted after it)
+    u = torch.rand(tot, device=dev, generator=g)
+    copies = torch.ones(tot, dtype=torch.int64, device=dev)
+    copies[u < indel_rate / 2] = 0
+    copies[(u >= indel_rate / 2) & (u < indel_rate)] = 2
+    idx = torch.repeat_interleave(torch.arange(tot, device=dev), copies)
+    first = torch.ones(idx.numel(), dtype=torch.bool, device=dev)
+    first[1:] = idx[1:] != idx[:-1]
+    out = torch.where(first, b[idx], lut[torch.randint(0, 4, (idx.numel(),), device=dev, generator=g)])
+    new_len = torch.zeros(n_reads, dtype=torch.int64, device=dev).index_add_(0, rid, copies)
+    off = torch.zeros(n_reads + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(new_len, 0)
+    ls = np.sort(new_len.cpu().numpy())[::-1]
+    n50_obs = int(ls[np.searchsorted(np.cumsum(ls), ls.sum() / 2)])
+    return out.contiguous(), off, n50_obs
+
+
 # ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -152,6 +197,8 @@ def main():
     ap.add_argument("--mean-genome", type=int, default=75000)
     ap.add_argument("--cpu-sample", type=int, default=200_000, help="read pairs timed on the CPU oracle (0 = off)")
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--long-reads", type=int, default=50_000,
+                    help="ONT-style reads (N50 ~10 kb) per rank for the long-read line (0 = off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,6 +216,8 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"[bench] genomes {seq.numel() / 1e9:.2f} Gbp in {len(lens) * 2} genomes, blocks "
               f"{len(gen.blk_genome)}; reads {args.pairs} pairs ({time.time() - t0:.1f}s)")
+    if args.long_reads > 0:
+        ls1, lo1, long_n50 = make_long_reads_gpu(seq, off_t, args.long_reads, args.seed * 1000 + 17 * rank + 7, dev)
     hdb = build_db(gen, taxo, par, device=local, device_seq=(seq, off_t))
     del seq
     torch.cuda.empty_cache()
@@ -280,6 +329,41 @@ def main():
                       and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
                       and np.array_equal(gb.taxcnt, otc))
 
+    # ---- long reads (seq mode 3, same DB): reads/s of the same pipeline on ~10 kb reads ----
+    long_line = None
+    if args.long_reads > 0:
+        clf.close()
+        lpl = LocalParameters(seqMode=3, kmerFormat=2, skipRedundancy=1)
+        clfl = Classifier(lpl, db_host=hdb.c_struct(), device=local)
+        for _ in range(max(1, args.warmup)):
+            clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        lsteps = max(1, min(args.steps, 3))
+        kl = np.zeros(len(KERNELS))
+        tl0 = time.perf_counter()
+        for _ in range(lsteps):
+            clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
+            kl += clfl.kernel_ms()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tl = time.perf_counter() - tl0
+        if world > 1:
+            t = torch.tensor([tl], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tl = float(t.item())
+        lq, lm = clfl.last_counts()
+        long_line = {"value": round(world * args.long_reads * lsteps / tl, 1), "unit": "reads/s",
+                     "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
+                     "reads_per_gpu": args.long_reads, "bases_per_gpu": int(lo1[-1].item()), "n50": long_n50,
+                     "query_kmers": lq, "matches": lm,
+                     "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(KERNELS, kl)},
+                     "workload": "config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs the "
+                                 "same DB, seq mode 3"}
+        clfl.close()
+
     if rank == 0:
         out = {
             "metric": "reads/sec classified (150bp & 10kb) vs GTDB-scale DB at 1/2/4/8 MI355X",
@@ -296,6 +380,7 @@ def main():
             "kernel_ms": {k: round(float(v), 3) for k, v in zip(KERNELS, kern)},
             "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
             "parity_sample": parity,
+            "long_reads": long_line,
         }
         print(json.dumps(out), flush=True)
     clf.close()

@@ -300,10 +300,10 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     uint32_t maxSeg = 0;
     HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (maxSeg > kSegSortLds) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
+    if (maxSeg > kSegSortLds || c->forceGeneric) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
     HIP_TRY(hipEventRecord(c->kev[8], s));
     launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg > 512, s);
+                   c->segScratch.as<uint64_t>(), maxSeg > 128, maxSeg > 512, c->forceGeneric, s);
     HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(hipEventRecord(c->kev[10], s));
     for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));

@@ -36,12 +36,71 @@ __device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, ui
 }
 
 constexpr int kSmallSeg = 512;
-constexpr int kBlockSeg = 4096;
+constexpr int kRegSeg = 128;  // segments up to this many matches sort in registers
+constexpr int kBlockSeg = 8192;
+
+// Segments of up to 64E matches sort in registers: element e = 64*slot + lane. Exchanges at
+// distance j < 64 swap with lane ^ j through cross-lane shuffles, j >= 64 swap slots inside a lane;
+// the network is unrolled at compile time so the slots stay in VGPRs. No LDS, no barriers.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l)[E], uint32_t (&x)[E], int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int js = j >> 6;
+#pragma unroll
+                for (int sl = 0; sl < E; sl++) {
+                    if (sl & js) continue;
+                    const int s2 = sl | js;
+                    const bool up = ((64 * sl + lane) & k) == 0;
+                    if (key_gt(h[sl], l[sl], h[s2], l[s2]) == up) {
+                        const uint64_t th = h[sl], tl = l[sl];
+                        const uint32_t tx = x[sl];
+                        h[sl] = h[s2]; l[sl] = l[s2]; x[sl] = x[s2];
+                        h[s2] = th; l[s2] = tl; x[s2] = tx;
+                    }
+                }
+            } else {
+                const bool lower = (lane & j) == 0;
+#pragma unroll
+                for (int sl = 0; sl < E; sl++) {
+                    const bool up = ((64 * sl + lane) & k) == 0;
+                    const uint64_t ph = __shfl_xor(h[sl], j, 64), pl = __shfl_xor(l[sl], j, 64);
+                    const uint32_t px = (uint32_t)__shfl_xor((int)x[sl], j, 64);
+                    // the lower lane of the pair keeps the smaller key when ascending
+                    const bool takeP = (key_gt(h[sl], l[sl], ph, pl) == (lower == up));
+                    if (takeP) { h[sl] = ph; l[sl] = pl; x[sl] = px; }
+                }
+            }
+        }
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
+                                             uint64_t base, int n, int lane) {
+    uint64_t h[E], l[E];
+    uint32_t x[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        h[sl] = ~0ull;
+        l[sl] = ~0ull;
+        x[sl] = (uint32_t)e;
+        if (e < n) match_key(in[base + e], h[sl], l[sl]);
+    }
+    wave_bitonic_sort<E>(h, l, x, lane);
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        if (e < n) out[base + e] = in[base + x[sl]];
+    }
+}
 
 __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
                                                       uint32_t nReads, mtb_match* __restrict__ out) {
-    __shared__ uint64_t sh[kSmallSeg], sl[kSmallSeg];
-    __shared__ uint16_t si[kSmallSeg];
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
@@ -52,6 +111,21 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
         if (lane == 0) out[base] = in[base];
         return;
     }
+    if (n <= 64) segsort_regs<1>(in, out, base, n, lane);
+    else if (n <= kRegSeg) segsort_regs<2>(in, out, base, n, lane);
+}
+
+// 129..512 matches: one wave, bitonic network over LDS.
+__global__ void __launch_bounds__(64) k_segsort_mid(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                    uint32_t nReads, mtb_match* __restrict__ out) {
+    __shared__ uint64_t sh[kSmallSeg], sl[kSmallSeg];
+    __shared__ uint16_t si[kSmallSeg];
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const int n = (int)(mOff[r + 1] - base);
+    if (n <= kRegSeg || n > kSmallSeg) return;
+    const int lane = threadIdx.x;
     int p2 = 2;
     while (p2 < n) p2 <<= 1;
     for (int i = lane; i < p2; i += 64) {
@@ -62,15 +136,14 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
     __syncthreads();
     for (int k = 2; k <= p2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = lane; i < p2; i += 64) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & k) == 0;
-                    uint64_t ah = sh[i], al = sl[i], bh = sh[ixj], bl = sl[ixj];
-                    if (key_gt(ah, al, bh, bl) == up) {
-                        sh[i] = bh; sl[i] = bl; sh[ixj] = ah; sl[ixj] = al;
-                        uint16_t t = si[i]; si[i] = si[ixj]; si[ixj] = t;
-                    }
+            for (int t = lane; t < (p2 >> 1); t += 64) {
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const int ixj = i + j;
+                const bool up = (i & k) == 0;
+                uint64_t ah = sh[i], al = sl[i], bh = sh[ixj], bl = sl[ixj];
+                if (key_gt(ah, al, bh, bl) == up) {
+                    sh[i] = bh; sl[i] = bl; sh[ixj] = ah; sl[ixj] = al;
+                    uint16_t x = si[i]; si[i] = si[ixj]; si[ixj] = x;
                 }
             }
             __syncthreads();
@@ -82,18 +155,20 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
 // p2 <= 4096 sort in LDS; larger ones in global scratch laid out as three arrays of 2*M words
 // (keys hi, keys lo, indices), the read's slice at offset 2*base (p2 <= 2n).
-__device__ void block_bitonic(uint64_t* H, uint64_t* Lo, uint32_t* I, long p2) {
+// Bitonic sort of p2 (power of two) 128-bit keys with a permutation, one compare-exchange pair
+// per thread and step: pair t covers i = t with a zero bit inserted at log2(j), and i + j.
+template <int kThreads, typename Idx>
+__device__ void block_bitonic(uint64_t* H, uint64_t* Lo, Idx* I, long p2) {
     for (long k = 2; k <= p2; k <<= 1)
         for (long j = k >> 1; j > 0; j >>= 1) {
-            for (long i = threadIdx.x; i < p2; i += 256) {
-                const long ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & k) == 0;
-                    const uint64_t ah = H[i], al = Lo[i], bh = H[ixj], bl = Lo[ixj];
-                    if (key_gt(ah, al, bh, bl) == up) {
-                        H[i] = bh; Lo[i] = bl; H[ixj] = ah; Lo[ixj] = al;
-                        const uint32_t t = I[i]; I[i] = I[ixj]; I[ixj] = t;
-                    }
+            for (long t = threadIdx.x; t < (p2 >> 1); t += kThreads) {
+                const long i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const long ixj = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t ah = H[i], al = Lo[i], bh = H[ixj], bl = Lo[ixj];
+                if (key_gt(ah, al, bh, bl) == up) {
+                    H[i] = bh; Lo[i] = bl; H[ixj] = ah; Lo[ixj] = al;
+                    const Idx x = I[i]; I[i] = I[ixj]; I[ixj] = x;
                 }
             }
             __threadfence_block();
@@ -101,37 +176,46 @@ __device__ void block_bitonic(uint64_t* H, uint64_t* Lo, uint32_t* I, long p2) {
         }
 }
 
-__global__ void __launch_bounds__(256) k_segsort_large(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
-                                                       uint32_t nReads, uint64_t M, mtb_match* __restrict__ out,
-                                                       uint64_t* __restrict__ gScratch) {
+// Segments of 513..kBlockSeg matches sort in LDS with one 1024-thread block per read (long reads:
+// ~2.5k matches at N50 10 kb); larger ones run the same network over a global key scratch.
+constexpr int kLargeThreads = 1024;
+
+__global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match* __restrict__ in,
+                                                                 const uint64_t* __restrict__ mOff, uint32_t nReads,
+                                                                 uint64_t M, mtb_match* __restrict__ out,
+                                                                 uint64_t* __restrict__ gScratch, int global) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
-    __shared__ uint32_t si[kBlockSeg];
-    const uint32_t r0 = blockIdx.x * 256;
-    const uint32_t r1 = min(r0 + 256u, nReads);
-    for (uint32_t r = r0; r < r1; r++) {
-        const uint64_t base = mOff[r];
-        const long n = (long)(mOff[r + 1] - base);
-        if (n <= kSmallSeg) continue;
-        long p2 = 2;
-        while (p2 < n) p2 <<= 1;
-        uint64_t *H = sh, *Lo = sl;
-        uint32_t* I = si;
-        if (p2 > kBlockSeg) {
-            H = gScratch + 2 * base;
-            Lo = gScratch + 2 * M + 2 * base;
-            I = (uint32_t*)(gScratch + 4 * M) + 2 * base;
-        }
-        for (long i = threadIdx.x; i < p2; i += 256) {
+    __shared__ uint16_t si[kBlockSeg];
+    const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    if (global ? n == 0 : n <= kSmallSeg) return;  // global: every segment takes the scratch path (tests)
+    long p2 = 2;
+    while (p2 < n) p2 <<= 1;
+    if (!global && p2 <= kBlockSeg) {
+        for (long i = threadIdx.x; i < p2; i += kLargeThreads) {
             uint64_t h = ~0ull, l = ~0ull;
             if (i < n) match_key(in[base + i], h, l);
-            H[i] = h; Lo[i] = l; I[i] = (uint32_t)i;
+            sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
         }
-        __threadfence_block();
         __syncthreads();
-        block_bitonic(H, Lo, I, p2);
-        for (long i = threadIdx.x; i < n; i += 256) out[base + i] = in[base + I[i]];
-        __syncthreads();
+        block_bitonic<kLargeThreads, uint16_t>(sh, sl, si, p2);
+        for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + si[i]];
+        return;
     }
+    uint64_t* H = gScratch + 2 * base;
+    uint64_t* Lo = gScratch + 2 * M + 2 * base;
+    uint32_t* I = (uint32_t*)(gScratch + 4 * M) + 2 * base;
+    for (long i = threadIdx.x; i < p2; i += kLargeThreads) {
+        uint64_t h = ~0ull, l = ~0ull;
+        if (i < n) match_key(in[base + i], h, l);
+        H[i] = h; Lo[i] = l; I[i] = (uint32_t)i;
+    }
+    __threadfence_block();
+    __syncthreads();
+    block_bitonic<kLargeThreads, uint32_t>(H, Lo, I, p2);
+    for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + I[i]];
 }
 
 __global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* __restrict__ out) {
@@ -140,10 +224,15 @@ __global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* 
 }
 
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, bool anyLarge, hipStream_t s) {
+                    uint64_t* gScratch, bool anyMid, bool anyLarge, bool global, hipStream_t s) {
     if (nReads == 0) return;
+    if (global) {
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1);
+        return;
+    }
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (anyLarge) k_segsort_large<<<(nReads + 255) / 256, 256, 0, s>>>(in, mOff, nReads, M, out, gScratch);
+    if (anyMid) k_segsort_mid<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
+    if (anyLarge) k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0);
 }
 
 __global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {

@@ -115,11 +115,13 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 
 uint64_t path_bytes();
 uint64_t clade_bytes();
+// K5; anyMid / anyLarge: some read has more than 128 / 512 matches; global: every segment through
+// the global-scratch network (gScratch 6*M words; parity tests of the general path)
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, bool anyLarge, hipStream_t s);
+                    uint64_t* gScratch, bool anyMid, bool anyLarge, bool global, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
-constexpr uint32_t kSegSortLds = 4096;
+constexpr uint32_t kSegSortLds = 8192;
 // K6 indexes matches and groups with 32 bits
 constexpr uint64_t kMaxBatchMatches = 0xFFFFFFFFull;  // segments up to this many matches sort in LDS
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,

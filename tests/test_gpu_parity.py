@@ -147,8 +147,9 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
 def test_general_paths(make_db, db_name, monkeypatch):
-    """MTB_FORCE_GENERIC=1 turns off every fast path (LDS DB windows in K4, register DP in K6), so
-    the general code the fast paths fall back to is held to the oracle too."""
+    """MTB_FORCE_GENERIC=1 turns off every fast path (LDS DB windows in K4, register and LDS sorts in
+    K5, register DP in K6), so the general code the fast paths fall back to is held to the oracle
+    too."""
     monkeypatch.setenv("MTB_FORCE_GENERIC", "1")
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, 2)
