@@ -71,7 +71,7 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal, waveList, waveCount;
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
@@ -223,7 +223,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->mStage, &c->mTotal, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->mStage, &c->mTotal, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -288,6 +288,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->conn.ensure(Mc));
     HIP_TRY(c->spScore.ensure(sizeof(float) * Mc));
     HIP_TRY(c->spKeep.ensure(Mc));
+    HIP_TRY(c->waveList.ensure(sizeof(uint64_t) * Mc));
+    HIP_TRY(c->waveCount.ensure(sizeof(uint32_t)));
     for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Mc + 1)));
     for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
     HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
@@ -323,6 +325,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                      c->gStart.as<uint64_t>(),
                      c->sStart.as<uint64_t>(),
                      c->spScore.as<float>(),
+                     c->waveList.as<uint64_t>(),
+                     c->waveCount.as<uint32_t>(),
                      c->spKeep.as<uint8_t>(),
                      c->scanTmp.p,
                      c->ordKA.as<uint64_t>(),

@@ -575,37 +575,30 @@ __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict
     pathCnt[g] = (uint32_t)(nP - start);
 }
 
-// combineMatchPaths (Taxonomer.cpp:410-468) and the species score (:380-395) for one (read,
-// species) run [ss, se): its groups' paths are packed in frame order (the order the reference
-// appends them), sorted with the libstdc++ introsort emulation and combined greedily.
-__global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ sStart,
-                                                       uint64_t nS, const uint64_t* __restrict__ gScan,
-                                                       const uint64_t* __restrict__ gStart,
-                                                       const uint32_t* __restrict__ pathCnt,
-                                                       const uint32_t* __restrict__ qlen, AssignCfg cfg,
-                                                       Path* __restrict__ P, Path* __restrict__ C,
-                                                       float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nS) return;
-    const uint64_t ss = sStart[s], se = sStart[s + 1];
-    uint64_t w = ss;
-    for (uint64_t g = gScan[ss]; gStart[g] < se; g++) {
-        const uint64_t src = gStart[g];
-        const uint32_t cnt = pathCnt[g];
-        if (src != w)
-            for (uint32_t k = 0; k < cnt; k++) P[w + k] = P[src + k];
-        w += cnt;
+// trimMatchPath (Taxonomer.cpp:475-485): p overlaps c by ol < 24 bases at one end
+__device__ __forceinline__ void trim_path(const mtb_match* __restrict__ M, Path& p, const Path& c, int ol) {
+    const int range = ol / 3;
+    if (p.start < c.start) {
+        const uint32_t reh = M[p.em].right_end_hamming;
+        p.end = c.start - 1;
+        p.hd = max(0, p.hd - ham_fields(reh, range, false));
+        p.score = p.score - score_fields(reh, range, false) - (float)(ol % 3);
+    } else {
+        const uint32_t reh = M[p.sm].right_end_hamming;
+        p.start = c.end + 1;
+        p.hd = max(0, p.hd - ham_fields(reh, range, true));
+        p.score = p.score - score_fields(reh, range, true) - (float)(ol % 3);
     }
-    if (w == ss) { spKeep[s] = 0; return; }
-    Path* Ps = P + ss;
-    const long nP = (long)(w - ss);
-    const int readLength = (int)qlen[info_seq(M[ss].qinfo) - 1];
+}
+
+// combineMatchPaths (Taxonomer.cpp:410-468) on nP packed paths in global memory: the libstdc++
+// introsort emulation, then the greedy overlap pass. Returns the summed score.
+__device__ float combine_serial(const mtb_match* __restrict__ M, Path* Ps, long nP, Path* Cs) {
     stdsort::sort(Ps, Ps + nP, [](const Path& a, const Path& b) {
         if (a.score != b.score) return a.score > b.score;
         if (a.hd != b.hd) return a.hd < b.hd;
         return a.start > b.start;
     });
-    Path* Cs = C + ss;
     long nC = 0;
     float score = 0.0f;
     for (long pi = 0; pi < nP; pi++) {
@@ -621,19 +614,8 @@ __global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restri
             if ((p.end < c.start) || (c.end < p.start)) continue;
             const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
             if (ol == p.end - p.start + 1) { overlapped = true; break; }
-            if (ol < 24) {  // trimMatchPath (Taxonomer.cpp:475-485)
-                const int range = ol / 3;
-                if (p.start < c.start) {
-                    const uint32_t reh = M[p.em].right_end_hamming;
-                    p.end = c.start - 1;
-                    p.hd = max(0, p.hd - ham_fields(reh, range, false));
-                    p.score = p.score - score_fields(reh, range, false) - (float)(ol % 3);
-                } else {
-                    const uint32_t reh = M[p.sm].right_end_hamming;
-                    p.start = c.end + 1;
-                    p.hd = max(0, p.hd - ham_fields(reh, range, true));
-                    p.score = p.score - score_fields(reh, range, true) - (float)(ol % 3);
-                }
+            if (ol < 24) {
+                trim_path(M, p, c, ol);
                 continue;
             }
             overlapped = true;
@@ -644,10 +626,147 @@ __global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restri
             score += Ps[pi].score;
         }
     }
+    return score;
+}
+
+__device__ __forceinline__ void species_score(float score, int readLength, const AssignCfg& cfg, float* spScore,
+                                              uint8_t* spKeep, uint64_t s) {
     score = score / (float)readLength;
     score = (1.0f < score) ? 1.0f : score;  // std::min(score, 1.0f)
     spScore[s] = score;
     spKeep[s] = !(score < cfg.minScore);
+}
+
+// The species score (:380-395) for one (read, species) run [ss, se): its groups' paths are packed
+// in frame order (the order the reference appends them) and combined. Runs of more than
+// kWaveCombineMin paths (long reads) are queued for k_combine_wave instead.
+constexpr int kWaveCombineMin = 24;
+constexpr int kWaveCombineMax = 1024;
+
+__global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ sStart,
+                                                       uint64_t nS, const uint64_t* __restrict__ gScan,
+                                                       const uint64_t* __restrict__ gStart,
+                                                       const uint32_t* __restrict__ pathCnt,
+                                                       const uint32_t* __restrict__ qlen, AssignCfg cfg,
+                                                       Path* __restrict__ P, Path* __restrict__ C,
+                                                       float* __restrict__ spScore, uint8_t* __restrict__ spKeep,
+                                                       uint64_t* __restrict__ waveList, uint32_t* __restrict__ waveCount) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nS) return;
+    const uint64_t ss = sStart[s], se = sStart[s + 1];
+    uint64_t w = ss;
+    for (uint64_t g = gScan[ss]; gStart[g] < se; g++) {
+        const uint64_t src = gStart[g];
+        const uint32_t cnt = pathCnt[g];
+        if (src != w)
+            for (uint32_t k = 0; k < cnt; k++) P[w + k] = P[src + k];
+        w += cnt;
+    }
+    if (w == ss) { spKeep[s] = 0; return; }
+    const long nP = (long)(w - ss);
+    if (!cfg.generic && nP > kWaveCombineMin && nP <= kWaveCombineMax) {
+        waveList[atomicAdd(waveCount, 1u)] = ((uint64_t)nP << 32) | s;
+        return;
+    }
+    const int readLength = (int)qlen[info_seq(M[ss].qinfo) - 1];
+    species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
+}
+
+// One wave per queued run (list entry = nP << 32 | run; its nP paths are packed at P[ss..]). The
+// paths are sorted in LDS by (score desc, hd asc, start desc): when no two paths tie on all three,
+// that order is the unique one std::sort must produce; a tie sends the run through combine_serial
+// (the introsort emulation) on lane 0. The greedy pass finds the first combined path a candidate
+// overlaps with one ballot per 64 entries, and searches on from there after a trim.
+__global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict__ M, const uint64_t* __restrict__ sStart,
+                                                     const uint64_t* __restrict__ waveList,
+                                                     const uint32_t* __restrict__ qlen, AssignCfg cfg,
+                                                     Path* __restrict__ P, Path* __restrict__ C,
+                                                     float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
+    __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
+    __shared__ int cs[kWaveCombineMax], ce[kWaveCombineMax];
+    const uint64_t e = waveList[blockIdx.x];
+    const uint64_t s = (uint32_t)e;
+    const int nP = (int)(e >> 32);
+    const uint64_t ss = sStart[s];
+    const Path* Ps = P + ss;
+    const int lane = threadIdx.x;
+    const int readLength = (int)qlen[info_seq(M[ss].qinfo) - 1];
+    int p2 = 2;
+    while (p2 < nP) p2 <<= 1;
+    for (int i = lane; i < p2; i += 64) {
+        if (i < nP) {
+            const Path p = Ps[i];
+            kh[i] = ((uint64_t)(~__float_as_uint(p.score)) << 32) | (uint32_t)p.hd;
+            kl[i] = ((uint64_t)(~(uint32_t)p.start) << 32) | (uint32_t)i;
+        } else {
+            kh[i] = ~0ull;
+            kl[i] = ~0ull;
+        }
+    }
+    __syncthreads();
+    for (int k = 2; k <= p2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = lane; t < (p2 >> 1); t += 64) {
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const int ixj = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t ah = kh[i], al = kl[i], bh = kh[ixj], bl = kl[ixj];
+                if (key_gt(ah, al, bh, bl) == up) {
+                    kh[i] = bh; kl[i] = bl; kh[ixj] = ah; kl[ixj] = al;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    bool tie = false;
+    for (int i = lane; i + 1 < nP; i += 64)
+        tie |= kh[i] == kh[i + 1] && (kl[i] >> 32) == (kl[i + 1] >> 32);
+    if (__syncthreads_or(tie)) {  // the order of tied paths is whatever libstdc++'s introsort leaves
+        if (lane == 0) species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
+        return;
+    }
+    float score = 0.0f;
+    int nC = 0;
+    for (int pi = 0; pi < nP; pi++) {
+        Path p = Ps[(uint32_t)kl[pi]];  // wave-uniform
+        bool keep = true;
+        int j0 = 0;
+        while (true) {
+            int found = -1;
+            for (int jb = j0; jb < nC; jb += 64) {
+                const int j = jb + lane;
+                const bool ov = j < nC && !(p.end < cs[j] || ce[j] < p.start);
+                const unsigned long long m = __ballot(ov);
+                if (m) {
+                    found = jb + __ffsll((long long)m) - 1;
+                    break;
+                }
+            }
+            if (found < 0) break;
+            Path c;
+            c.start = cs[found];
+            c.end = ce[found];
+            const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
+            if (ol == p.end - p.start + 1) { keep = false; break; }
+            if (ol < 24) {
+                trim_path(M, p, c, ol);
+                j0 = found + 1;
+                continue;
+            }
+            keep = false;
+            break;
+        }
+        if (keep) {
+            if (lane == 0) {
+                cs[nC] = p.start;
+                ce[nC] = p.end;
+            }
+            __syncthreads();
+            nC++;
+            score += p.score;
+        }
+    }
+    if (lane == 0) species_score(score, readLength, cfg, spScore, spKeep, s);
 }
 
 // chooseBestTaxon (Taxonomer.cpp:130-202), filterRedundantMatches (:205-241), taxCnt and the
@@ -895,10 +1014,18 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                     matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
                     s.conn, s.pathCnt);
         }
-        if (cnt[1])
+        if (cnt[1]) {
+            hipMemsetAsync(s.waveCount, 0, sizeof(uint32_t), st);
             k_combine_paths<<<(unsigned)((cnt[1] + 255) / 256), 256, 0, st>>>(
                 matches, s.sStart, cnt[1], s.gScan, s.gStart, s.pathCnt, qlen, cfg, (Path*)s.paths, (Path*)s.comb,
-                s.spScore, s.spKeep);
+                s.spScore, s.spKeep, s.waveList, s.waveCount);
+            uint32_t nWave = 0;
+            hipMemcpyAsync(&nWave, s.waveCount, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+            hipStreamSynchronize(st);
+            if (nWave)
+                k_combine_wave<<<nWave, 64, 0, st>>>(matches, s.sStart, s.waveList, qlen, cfg, (Path*)s.paths,
+                                                     (Path*)s.comb, s.spScore, s.spKeep);
+        }
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
     }

@@ -43,6 +43,8 @@ struct AssignScratch {  // per match unless noted
     uint32_t *gFlag, *sFlag, *pathCnt;
     uint64_t *gScan, *sScan, *gStart, *sStart;  // M + 1 entries
     float* spScore;        // per species run
+    uint64_t* waveList;    // per species run: runs queued for k_combine_wave
+    uint32_t* waveCount;   // 1
     uint8_t* spKeep;       // per species run
     void* scanTmp;         // scan_tmp_elems(radix_counts_elems(M + 1) + M + 2) u64
     uint64_t *ordKA, *ordVA, *ordKB, *ordVB;  // M + 1 each: group work list (radix_sort_pairs)
