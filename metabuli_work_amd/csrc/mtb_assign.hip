@@ -684,6 +684,7 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                                                      float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
     __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
     __shared__ int cs[kWaveCombineMax], ce[kWaveCombineMax];
+    __shared__ uint32_t qsm[kWaveCombineMax], qem[kWaveCombineMax];
     const uint64_t e = waveList[blockIdx.x];
     const uint64_t s = (uint32_t)e;
     const int nP = (int)(e >> 32);
@@ -725,10 +726,35 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
         if (lane == 0) species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
         return;
     }
+    // the paths themselves, in sorted order, into LDS (over the dead key arrays, plus sm/em) so the
+    // sequential pass below reads no global memory but for the rare trims
+    constexpr int kPerLane = kWaveCombineMax / 64;
+    uint32_t src[kPerLane];
+#pragma unroll
+    for (int t = 0; t < kPerLane; t++) {
+        const int i = lane + 64 * t;
+        src[t] = i < nP ? (uint32_t)kl[i] : 0u;
+    }
+    __syncthreads();
+    int* qs = reinterpret_cast<int*>(kh);
+    int* qe = qs + kWaveCombineMax;
+    float* qsc = reinterpret_cast<float*>(kl);
+    int* qhd = reinterpret_cast<int*>(kl) + kWaveCombineMax;
+#pragma unroll
+    for (int t = 0; t < kPerLane; t++) {
+        const int i = lane + 64 * t;
+        if (i < nP) {
+            const Path q = Ps[src[t]];
+            qs[i] = q.start; qe[i] = q.end; qsc[i] = q.score; qhd[i] = q.hd; qsm[i] = q.sm; qem[i] = q.em;
+        }
+    }
+    __syncthreads();
     float score = 0.0f;
     int nC = 0;
     for (int pi = 0; pi < nP; pi++) {
-        Path p = Ps[(uint32_t)kl[pi]];  // wave-uniform
+        Path p;  // wave-uniform
+        p.start = qs[pi]; p.end = qe[pi]; p.score = qsc[pi]; p.hd = qhd[pi]; p.sm = qsm[pi]; p.em = qem[pi];
+        p.depth = 0;
         bool keep = true;
         int j0 = 0;
         while (true) {
