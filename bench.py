@@ -301,6 +301,8 @@ def main():
     # ---- CPU baseline: the oracle (restated reference algorithm, OpenMP) on a bounded sample ----
     cpu = None
     parity = None
+    odb = None
+    cores = 1
     if rank == 0 and args.cpu_sample > 0:
         from tests import oracle_ctypes as oc  # checker / baseline only
 
@@ -314,12 +316,11 @@ def main():
         oc.lib().orc_set_threads(cores)
         opar = lp.to_c()
         opar.threads = cores
-        odb = oc.OracleDb.from_host(hdb.c_struct())
+        odb = oc.OracleDb.from_host(hdb.c_struct())  # kept open for the long-read baseline below
         stage_s = np.zeros(4)
         tc0 = time.perf_counter()
         ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
         cpu_t = time.perf_counter() - tc0
-        odb.close()
         cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
                "sample": f"first {S} read pairs of the rank-0 batch, same DB; oracle/ (OpenMP C++ restatement "
                          f"of the reference path), {cpu_t:.1f}s wall",
@@ -355,14 +356,37 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tl = float(t.item())
         lq, lm = clfl.last_counts()
+        long_cpu = None
+        if rank == 0 and args.cpu_sample > 0:
+            # the oracle on the first reads of the long batch (~10 s of 16-core work), and the GPU's
+            # results for the same reads compared with it
+            LS = max(1, min(args.long_reads, args.cpu_sample // 100))
+            lo_h = lo1[:LS + 1].cpu().numpy().astype(np.uint64)
+            ls_h = ls1[:int(lo_h[-1])].cpu().numpy()
+            lreads = synth.Reads(ls_h, lo_h, None, None, np.zeros(LS, np.int32))
+            lopar = lpl.to_c()
+            lopar.threads = cores
+            tc0 = time.perf_counter()
+            lres, ltc = oc.classify(odb, lopar, lreads)
+            lcpu_t = time.perf_counter() - tc0
+            gl = clfl.classify_batch(ls_h, lo_h)
+            long_cpu = {"value": round(LS / lcpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+                        "sample": f"first {LS} long reads of the rank-0 batch, same DB, {lcpu_t:.1f}s wall",
+                        "parity_sample": bool(np.array_equal(gl.results["classification"], lres["classification"])
+                                              and np.array_equal(gl.results["score"].view(np.uint32),
+                                                                 lres["score"].view(np.uint32))
+                                              and np.array_equal(gl.taxcnt, ltc))}
         long_line = {"value": round(world * args.long_reads * lsteps / tl, 1), "unit": "reads/s",
                      "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
                      "reads_per_gpu": args.long_reads, "bases_per_gpu": int(lo1[-1].item()), "n50": long_n50,
                      "query_kmers": lq, "matches": lm,
                      "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(KERNELS, kl)},
+                     "cpu_baseline": long_cpu,
                      "workload": "config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs the "
                                  "same DB, seq mode 3"}
         clfl.close()
+    if odb is not None:
+        odb.close()
 
     if rank == 0:
         out = {

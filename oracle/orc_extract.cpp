@@ -7,6 +7,7 @@
 #include "orc_internal.h"
 #ifdef _OPENMP
 #include <omp.h>
+#include <parallel/algorithm>
 #endif
 
 namespace orc {
@@ -87,8 +88,9 @@ void extractQueryKmers(const mtb_params& par, const Reads& reads, std::vector<mt
         }
     }
     if (sort) {
-        // SORT_PARALLEL(..., Kmer::compareQueryKmer) (KmerExtractor.cpp:79, Kmer.h:89-94)
-        std::sort(buf.begin(), buf.end(), [](const mtb_kmer& a, const mtb_kmer& b) {
+        // SORT_PARALLEL(..., Kmer::compareQueryKmer) (KmerExtractor.cpp:79, Kmer.h:89-94); MMseqs2's
+        // SORT_PARALLEL is __gnu_parallel::sort under OpenMP
+        __gnu_parallel::sort(buf.begin(), buf.end(), [](const mtb_kmer& a, const mtb_kmer& b) {
             if (a.value != b.value) return a.value < b.value;
             return infoSeq(a.info) < infoSeq(b.info);
         });
