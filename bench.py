@@ -195,7 +195,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=1_000_000, help="read pairs per rank per step")
     ap.add_argument("--species", type=int, default=25000)
     ap.add_argument("--mean-genome", type=int, default=75000)
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="read pairs timed on the CPU oracle (0 = off)")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="read pairs timed on the CPU oracle (0 = off)")
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--long-reads", type=int, default=50_000,
                     help="ONT-style reads (N50 ~10 kb) per rank for the long-read line (0 = off)")
@@ -360,7 +360,7 @@ def main():
         if rank == 0 and args.cpu_sample > 0:
             # the oracle on the first reads of the long batch (~10 s of 16-core work), and the GPU's
             # results for the same reads compared with it
-            LS = max(1, min(args.long_reads, args.cpu_sample // 100))
+            LS = max(1, min(args.long_reads, args.cpu_sample // 50))
             lo_h = lo1[:LS + 1].cpu().numpy().astype(np.uint64)
             ls_h = ls1[:int(lo_h[-1])].cpu().numpy()
             lreads = synth.Reads(ls_h, lo_h, None, None, np.zeros(LS, np.int32))
