@@ -4,11 +4,12 @@ Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by
 within a step: a step starts at k_read_meta; extract = k_extract; kmer_sort = everything from
 there to k_match_windows; match_join = k_match_windows + k_match (+ a rerun if the staging
 buffer grew); match_transpose = k_match_transpose; match_sort = k_segsort_*; assign = the rest
-of the step (K6 kernels, scans and taxcnt compaction). The last complete step is reported.
+of the step (K6 kernels, scans and taxcnt compaction). 
 
 Usage:
-  python tools/stage_profile.py time  <run_kernel_trace.csv>
-  python tools/stage_profile.py bytes <fetch run_counter_collection.csv> <write run_counter_collection.csv>
+  python tools/stage_profile.py time  <run_kernel_trace.csv> <step index>
+  python tools/stage_profile.py bytes <fetch run_counter_collection.csv> <write run_counter_collection.csv> <step index>
+(bench.py default: steps 0-1 are warmup, 2-6 timed 150 bp steps; with --steps 1 --warmup 0 step 0)
 FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE is doubled (MI355X_MICROARCH.md: on gfx950 it
 counts half the bytes of a wide coalesced read), WRITE_SIZE is taken as is.
 """
@@ -30,6 +31,9 @@ def stage_of(seq):
     stage = "extract"
     after_extract = False
     for k in seq:
+        if stage == "post":
+            out.append(stage)
+            continue
         if k.startswith("k_read_meta"):
             stage, after_extract = "extract", False
         elif k.startswith("k_extract"):
@@ -45,15 +49,16 @@ def stage_of(seq):
         elif stage == "extract" and after_extract:
             stage = "kmer_sort"
         out.append(stage)
+        if k.startswith("k_compact_taxcnt"):
+            stage = "post"  # the step's last kernel; later dispatches (e.g. a DB open) are not the step's
     return out
 
 
-def last_step(rows):
-    """rows: (dispatch_id, short_name, payload) sorted by dispatch; returns the last full step."""
-    starts = [i for i, r in enumerate(rows) if r[1].startswith("k_read_meta")]
-    if len(starts) < 2:
-        return rows[starts[-1]:] if starts else rows
-    return rows[starts[-2]:starts[-1]] if len(starts) >= 2 else rows
+def pick_step(rows, nth):
+    """rows: (dispatch_id, short_name, payload) sorted by dispatch; returns the nth step (a step
+    starts at k_read_meta and runs to the next one)."""
+    starts = [i for i, r in enumerate(rows) if r[1].startswith("k_read_meta")] + [len(rows)]
+    return rows[starts[nth]:starts[nth + 1]]
 
 
 def main():
@@ -66,11 +71,13 @@ def main():
             rows.append((int(r["Dispatch_Id"]), short(r["Kernel_Name"]),
                          (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
         rows.sort()
-        step = last_step(rows)
+        step = pick_step(rows, int(sys.argv[3]))
         st = stage_of([r[1] for r in step])
         tot = collections.OrderedDict((s, 0.0) for s in STAGES)
         kern = collections.defaultdict(float)
         for (d, k, ms), s in zip(step, st):
+            if s == "post":
+                continue
             tot[s] += ms
             kern[(s, k)] += ms
         print(json.dumps({"stage_ms": {k: round(v, 3) for k, v in tot.items()},
@@ -84,11 +91,12 @@ def main():
                     continue
                 rows.append((int(r["Dispatch_Id"]), short(r["Kernel_Name"]), float(r["Counter_Value"]) * 1024 * scale))
             rows.sort()
-            step = last_step(rows)
+            step = pick_step(rows, int(sys.argv[4]))
             st = stage_of([r[1] for r in step])
             tot = collections.OrderedDict((s, 0.0) for s in STAGES)
             for (d, k, b), s in zip(step, st):
-                tot[s] += b
+                if s != "post":
+                    tot[s] += b
             res[counter] = tot
         out = {s: {"fetch_bytes": int(res["FETCH_SIZE"][s]), "write_bytes": int(res["WRITE_SIZE"][s]),
                    "hbm_bytes": int(res["FETCH_SIZE"][s] + res["WRITE_SIZE"][s])} for s in STAGES}
