@@ -673,9 +673,9 @@ __global__ void __launch_bounds__(256) k_combine_paths(const mtb_match* __restri
 }
 
 // One wave per queued run (list entry = nP << 32 | run; its nP paths are packed at P[ss..]). The
-// paths are sorted in LDS by (score desc, hd asc, start desc): when no two paths tie on all three,
-// that order is the unique one std::sort must produce; a tie sends the run through combine_serial
-// (the introsort emulation) on lane 0. The greedy pass finds the first combined path a candidate
+// paths are sorted in LDS by (score desc, hd asc, start desc): any correct sort places distinct
+// keys the same way, and tied paths only need std::sort's exact order (the introsort emulation,
+// combine_serial on lane 0) when they differ in a field the greedy pass reads. The greedy pass finds the first combined path a candidate
 // overlaps with one ballot per 64 entries, and searches on from there after a trim.
 __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict__ M, const uint64_t* __restrict__ sStart,
                                                      const uint64_t* __restrict__ waveList,
@@ -683,7 +683,6 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                                                      Path* __restrict__ P, Path* __restrict__ C,
                                                      float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
     __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
-    __shared__ int cs[kWaveCombineMax], ce[kWaveCombineMax];
     __shared__ uint32_t qsm[kWaveCombineMax], qem[kWaveCombineMax];
     const uint64_t e = waveList[blockIdx.x];
     const uint64_t s = (uint32_t)e;
@@ -719,9 +718,16 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
             __syncthreads();
         }
     }
+    // A tie on the comparator's key only matters if the tied paths can act differently in the
+    // greedy pass, which reads start, end, score and, when trimming, the end matches' hamming
+    // fields; tied paths equal in all of those are interchangeable in any order.
     bool tie = false;
-    for (int i = lane; i + 1 < nP; i += 64)
-        tie |= kh[i] == kh[i + 1] && (kl[i] >> 32) == (kl[i + 1] >> 32);
+    for (int i = lane; i + 1 < nP; i += 64) {
+        if (kh[i] != kh[i + 1] || (kl[i] >> 32) != (kl[i + 1] >> 32)) continue;
+        const Path a = Ps[(uint32_t)kl[i]], b = Ps[(uint32_t)kl[i + 1]];
+        tie |= a.end != b.end || M[a.sm].right_end_hamming != M[b.sm].right_end_hamming ||
+               M[a.em].right_end_hamming != M[b.em].right_end_hamming;
+    }
     if (__syncthreads_or(tie)) {  // the order of tied paths is whatever libstdc++'s introsort leaves
         if (lane == 0) species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
         return;
@@ -749,6 +755,14 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
         }
     }
     __syncthreads();
+    // Combined paths are pairwise disjoint (a kept path overlaps none of them), so the entries a
+    // candidate touches are found with one pass over the lane-distributed interval registers
+    // (entry j in slot j / 64 of lane j % 64) and then visited in insertion order, re-checked
+    // against the candidate as trims shrink it.
+    constexpr int kSlots = kWaveCombineMax / 64;
+    int rs[kSlots], re[kSlots];
+#pragma unroll
+    for (int t = 0; t < kSlots; t++) { rs[t] = 0; re[t] = -1; }
     float score = 0.0f;
     int nC = 0;
     for (int pi = 0; pi < nP; pi++) {
@@ -756,38 +770,27 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
         p.start = qs[pi]; p.end = qe[pi]; p.score = qsc[pi]; p.hd = qhd[pi]; p.sm = qsm[pi]; p.em = qem[pi];
         p.depth = 0;
         bool keep = true;
-        int j0 = 0;
-        while (true) {
-            int found = -1;
-            for (int jb = j0; jb < nC; jb += 64) {
-                const int j = jb + lane;
-                const bool ov = j < nC && !(p.end < cs[j] || ce[j] < p.start);
-                const unsigned long long m = __ballot(ov);
-                if (m) {
-                    found = jb + __ffsll((long long)m) - 1;
-                    break;
-                }
+#pragma unroll
+        for (int t = 0; t < kSlots; t++) {
+            if (!keep || 64 * t >= nC) break;
+            unsigned long long m = __ballot(64 * t + lane < nC && !(p.end < rs[t] || re[t] < p.start));
+            while (keep && m) {
+                const int l = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                Path c;
+                c.start = __shfl(rs[t], l, 64);
+                c.end = __shfl(re[t], l, 64);
+                if ((p.end < c.start) || (c.end < p.start)) continue;  // cleared by an earlier trim
+                const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
+                if (ol == p.end - p.start + 1) { keep = false; break; }
+                if (ol < 24) { trim_path(M, p, c, ol); continue; }
+                keep = false;
             }
-            if (found < 0) break;
-            Path c;
-            c.start = cs[found];
-            c.end = ce[found];
-            const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
-            if (ol == p.end - p.start + 1) { keep = false; break; }
-            if (ol < 24) {
-                trim_path(M, p, c, ol);
-                j0 = found + 1;
-                continue;
-            }
-            keep = false;
-            break;
         }
         if (keep) {
-            if (lane == 0) {
-                cs[nC] = p.start;
-                ce[nC] = p.end;
-            }
-            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < kSlots; t++)
+                if (t == (nC >> 6) && lane == (nC & 63)) { rs[t] = p.start; re[t] = p.end; }
             nC++;
             score += p.score;
         }
