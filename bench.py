@@ -263,6 +263,7 @@ def main():
     kern /= max(1, args.steps)
     stage /= max(1, args.steps)
     Q, M = clf.last_counts()
+    work = clf.stats()
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     value = world * n * args.steps / elapsed
 
@@ -356,6 +357,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tl = float(t.item())
         lq, lm = clfl.last_counts()
+        lwork = clfl.stats()
         long_cpu = None
         if rank == 0 and args.cpu_sample > 0:
             # the oracle on the first reads of the long batch (~10 s of 16-core work), and the GPU's
@@ -381,7 +383,7 @@ def main():
                      "reads_per_gpu": args.long_reads, "bases_per_gpu": int(lo1[-1].item()), "n50": long_n50,
                      "query_kmers": lq, "matches": lm,
                      "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(KERNELS, kl)},
-                     "cpu_baseline": long_cpu,
+                     "cpu_baseline": long_cpu, "work": lwork,
                      "workload": "config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs the "
                                  "same DB, seq mode 3"}
         clfl.close()
@@ -404,6 +406,7 @@ def main():
             "kernel_ms": {k: round(float(v), 3) for k, v in zip(KERNELS, kern)},
             "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
             "parity_sample": parity,
+            "work": work,
             "long_reads": long_line,
         }
         print(json.dumps(out), flush=True)

@@ -146,6 +146,11 @@ int mtb_get_taxcnt(mtb_ctx* ctx, mtb_taxcnt* out, uint64_t capacity, uint64_t* n
 int mtb_device_results(mtb_ctx* ctx, void** results, void** taxcnt, uint64_t* n_taxcnt);
 /* Counters the reference prints (Classifier.cpp:116, KmerMatcher.cpp:152). */
 int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches);
+/* Work counts of the last batch: [0] reserved k-mer slots, [1] query k-mers, [2] query k-mers
+ * with >= 1 match, [3] matches, [4] most matches of one read, [5] (read, species, frame) groups,
+ * [6] groups of >= 2 matches, [7] (read, species) runs, [8] runs combined one per wave, [9] of those,
+ * runs whose tied paths needed the std::sort emulation. */
+int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):
  * [0] extract, [1] k-mer sort, [2] match, [3] match sort + assign, [4] total. */
 int mtb_last_stage_ms(const mtb_ctx* ctx, float* ms, int n);

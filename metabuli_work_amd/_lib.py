@@ -17,7 +17,7 @@ _LIB = None
 EXPORTED = [
     "mtb_default_params", "mtb_load_db_parameters", "mtb_open", "mtb_open_host", "mtb_close", "mtb_last_error",
     "mtb_set_stream", "mtb_db_kmers", "mtb_classify_batch", "mtb_get_taxcnt", "mtb_device_results",
-    "mtb_last_counts", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
+    "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built",
 ]
 
@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_get_taxcnt.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_device_results.argtypes = [vp, P(vp), P(vp), P(u64)]
     L.mtb_last_counts.argtypes = [vp, P(u64), P(u64)]
+    L.mtb_last_stats.argtypes = [vp, P(u64), i32]
     L.mtb_last_stage_ms.argtypes = [vp, P(ctypes.c_float), i32]
     L.mtb_last_kernel_ms.argtypes = [vp, P(ctypes.c_float), i32]
     L.mtb_copy_results.argtypes = [vp, vp, i32]

@@ -149,6 +149,15 @@ class Classifier:
         lib().mtb_last_counts(self.handle, ctypes.byref(q), ctypes.byref(m))
         return int(q.value), int(m.value)
 
+    STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
+             "species_runs", "wave_runs", "wave_runs_emulated"]
+
+    def stats(self) -> dict:
+        """Work counts of the last batch (mtb_last_stats)."""
+        out = (ctypes.c_uint64 * len(self.STATS))()
+        lib().mtb_last_stats(self.handle, out, len(self.STATS))
+        return {k: int(v) for k, v in zip(self.STATS, out)}
+
     def stage_ms(self) -> np.ndarray:
         ms = (ctypes.c_float * 5)()
         lib().mtb_last_stage_ms(self.handle, ms, 5)

@@ -71,7 +71,8 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal, waveList, waveCount;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal, waveList, waveCount, devStats;
+    uint64_t stats[10] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
@@ -223,7 +224,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->mStage, &c->mTotal, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mTotal, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -337,8 +338,11 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                      c->radixOffs.as<uint64_t>(),
                      c->clade.p,
                      c->cladePerMatch};
+    c->stats[3] = M;
+    c->stats[4] = maxSeg;
     launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(),
-                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(), s);
+                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(),
+                  c->devStats.as<unsigned long long>(), c->stats + 5, s);
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -391,6 +395,9 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
             dOff2 = c->off2.as<uint64_t>();
         }
     }
+    for (uint64_t& x : c->stats) x = 0;
+    HIP_TRY(c->devStats.ensure(sizeof(unsigned long long) * 4));
+    HIP_TRY(hipMemsetAsync(c->devStats.p, 0, sizeof(unsigned long long) * 4, s));
     // K0: read metadata (KmerExtractor.cpp:442-494) and K1 work units
     HIP_TRY(c->meta.ensure(sizeof(ReadMeta) * (n + 1)));
     HIP_TRY(c->reserve.ensure(sizeof(uint32_t) * (n + 1)));
@@ -443,6 +450,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
                                   c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
+    c->stats[0] = R;
+    c->stats[1] = Q;
     c->sortedInB = inB;
     const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
     const uint32_t* qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();  // K1 slots
@@ -466,7 +475,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
         launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf,
                      (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
-                     c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(), s);
+                     c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
+                     c->devStats.as<unsigned long long>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -500,9 +510,13 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     if (rc != MTB_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev[4], s));
     int err = 0;
+    unsigned long long dstat[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(dstat, c->devStats.p, sizeof(dstat), hipMemcpyDeviceToHost, s));
     if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    c->stats[2] = dstat[0];
+    c->stats[9] = dstat[1];
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     for (int k = 0; k < mtb_ctx::kNumKern; k++)
@@ -538,6 +552,12 @@ int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
     if (!c) return MTB_ERR_ARG;
     if (q) *q = c->Q;
     if (m) *m = c->M;
+    return MTB_OK;
+}
+
+int mtb_last_stats(const mtb_ctx* c, uint64_t* out, int n) {
+    if (!c || !out) return MTB_ERR_ARG;
+    for (int i = 0; i < n && i < 10; i++) out[i] = c->stats[i];
     return MTB_OK;
 }
 
@@ -596,6 +616,9 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     if (!c || (!m && nm) || !qlen) return MTB_ERR_ARG;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
+    for (uint64_t& x : c->stats) x = 0;
+    HIP_TRY(c->devStats.ensure(sizeof(unsigned long long) * 4));
+    HIP_TRY(hipMemsetAsync(c->devStats.p, 0, sizeof(unsigned long long) * 4, s));
     // group by read (counting sort by seqID) on the host, then K5 + K6 on the device
     std::vector<uint64_t> off(n + 1, 0);
     for (uint64_t i = 0; i < nm; i++) {

@@ -681,7 +681,8 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                                                      const uint64_t* __restrict__ waveList,
                                                      const uint32_t* __restrict__ qlen, AssignCfg cfg,
                                                      Path* __restrict__ P, Path* __restrict__ C,
-                                                     float* __restrict__ spScore, uint8_t* __restrict__ spKeep) {
+                                                     float* __restrict__ spScore, uint8_t* __restrict__ spKeep,
+                                                     unsigned long long* __restrict__ stats) {
     __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
     __shared__ uint32_t qsm[kWaveCombineMax], qem[kWaveCombineMax];
     const uint64_t e = waveList[blockIdx.x];
@@ -729,6 +730,7 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                M[a.em].right_end_hamming != M[b.em].right_end_hamming;
     }
     if (__syncthreads_or(tie)) {  // the order of tied paths is whatever libstdc++'s introsort leaves
+        if (lane == 0) atomicAdd(&stats[1], 1ull);
         if (lane == 0) species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
         return;
     }
@@ -1016,7 +1018,9 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
 }
 
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st) {
+                   mtb_taxcnt* tcPool, mtb_result* results, unsigned long long* devStats, uint64_t* hostStats,
+                   hipStream_t st) {
+    for (int i = 0; i < 4; i++) hostStats[i] = 0;
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
                   a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic};
@@ -1032,12 +1036,15 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
         hipMemcpyAsync(&cnt[0], s.gScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(&cnt[1], s.sScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
         hipStreamSynchronize(st);
+        hostStats[0] = cnt[0];
+        hostStats[2] = cnt[1];
         if (cnt[0]) {
             k_group_keys<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(s.gStart, cnt[0], s.ordKA, s.ordVA,
                                                                             s.pathCnt);
             bool inB = false;
             const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true, false,
                                                     s.radixCounts, s.radixOffs, s.scanTmp, &inB, st);
+            hostStats[1] = heavy;
             if (heavy)
                 k_match_paths<<<(unsigned)((heavy + 255) / 256), 256, 0, st>>>(
                     matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
@@ -1053,7 +1060,8 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
             hipStreamSynchronize(st);
             if (nWave)
                 k_combine_wave<<<nWave, 64, 0, st>>>(matches, s.sStart, s.waveList, qlen, cfg, (Path*)s.paths,
-                                                     (Path*)s.comb, s.spScore, s.spKeep);
+                                                     (Path*)s.comb, s.spScore, s.spKeep, devStats);
+            hostStats[3] = nWave;
         }
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);

@@ -728,7 +728,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
                                                mtb_match* __restrict__ buf, uint64_t region, int* __restrict__ err,
-                                               uint32_t winCap, const uint64_t* __restrict__ win) {
+                                               uint32_t winCap, const uint64_t* __restrict__ win,
+                                               unsigned long long* __restrict__ stats) {
     __shared__ uint64_t sDb[kMatchWin];
     __shared__ uint32_t sInfo[kMatchWin];
     __shared__ unsigned long long sBase;
@@ -802,6 +803,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         if (c[j]) atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
     }
+    int hit = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) hit += c[j] != 0;
+    const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
+    if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
     unsigned long long blockTot;
     uint64_t w = block_exclusive_scan(mine, &blockTot);
     const uint32_t reg = blockIdx.x % kStageRegions;
@@ -846,12 +852,13 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
-                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, hipStream_t s) {
+                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, unsigned long long* stats,
+                  hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     k_match<<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt,
-                                   total, buf, region, err, winCap, win);
+                                   total, buf, region, err, winCap, win, stats);
 }
 
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,

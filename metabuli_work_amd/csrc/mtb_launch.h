@@ -106,7 +106,8 @@ constexpr uint32_t kStageRegions = 256;
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
-                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, hipStream_t s);
+                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, unsigned long long* stats,
+                  hipStream_t s);  // stats[0] += queries with >= 1 match
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
 void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
                             const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
@@ -127,7 +128,9 @@ constexpr uint32_t kSegSortLds = 8192;
 // K6 indexes matches and groups with 32 bits
 constexpr uint64_t kMaxBatchMatches = 0xFFFFFFFFull;  // segments up to this many matches sort in LDS
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
-                   mtb_taxcnt* tcPool, mtb_result* results, hipStream_t st);
+                   mtb_taxcnt* tcPool, mtb_result* results, unsigned long long* devStats, uint64_t* hostStats,
+                   hipStream_t st);  // devStats[1] += wave runs sent to the introsort emulation;
+                                     // hostStats = {groups, groups >= 2 matches, species runs, wave runs}
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
 void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
                            uint32_t nReads, mtb_taxcnt* out, hipStream_t s);
