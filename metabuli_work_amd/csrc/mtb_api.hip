@@ -58,6 +58,7 @@ struct mtb_ctx {
     uint64_t* dbv = nullptr;
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
+    uint32_t* aaSet = nullptr;  // AA 8-mer membership bitmap of the DB (4.7 GB)
     AADir dir{};
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
@@ -92,12 +93,13 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
-    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->aaSet, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->dbv = nullptr;
     c->dbinfo = nullptr;
     c->dirMem = nullptr;
+    c->aaSet = nullptr;
 }
 
 template <typename T>
@@ -159,6 +161,11 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
     build_aa_dir(c->dbv, c->D, c->dir, c->dirMem, s);
+    if (!c->forceGeneric) {
+        HIP_TRY(hipMalloc(&c->aaSet, kAASetWords * sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(c->aaSet, 0, kAASetWords * sizeof(uint32_t), s));
+        build_aa_set(c->dbv, c->D, c->aaSet, s);
+    }
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(dDiff);
     hipFree(dFlag);
@@ -447,7 +454,8 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipEventRecord(c->kev[2], s));
     uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
                                   c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
-                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s,
+                                  c->aaSet);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
     c->stats[0] = R;

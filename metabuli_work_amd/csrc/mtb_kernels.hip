@@ -345,9 +345,14 @@ constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
 __device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) { return (uint32_t)((k >> shift) & 0xFF); }
 
+// aaSet (first pass of the query sort, FILTER only): keys whose AA 8-mer is absent from the DB's
+// membership bitmap cannot match (matchKmers compares AA parts for equality first); they are
+// overwritten with the sentinel here, so the scatter drops them with the blank slots. The 16
+// lookups of a thread go out together, after its 16 key loads.
 template <bool FILTER>
-__global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
-                                                    uint32_t* __restrict__ counts, uint32_t nTiles) {
+__global__ void __launch_bounds__(256) k_radix_hist(uint64_t* __restrict__ keys, uint64_t n, int shift,
+                                                    uint32_t* __restrict__ counts, uint32_t nTiles,
+                                                    const uint32_t* __restrict__ aaSet) {
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
@@ -357,6 +362,20 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
     for (int k = 0; k < kRadixItems; k++) {
         const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
         key[k] = i < n ? keys[i] : kSentinel;
+    }
+    if (FILTER && aaSet) {
+        uint32_t word[kRadixItems];
+#pragma unroll
+        for (int k = 0; k < kRadixItems; k++) {
+            const uint64_t r = key[k] >> 24;
+            word[k] = key[k] != kSentinel ? aaSet[r >> 5] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kRadixItems; k++) {
+            if (key[k] == kSentinel || ((word[k] >> ((key[k] >> 24) & 31u)) & 1u)) continue;
+            key[k] = kSentinel;
+            keys[base + (uint64_t)k * kBlock + threadIdx.x] = kSentinel;
+        }
     }
 #pragma unroll
     for (int k = 0; k < kRadixItems; k++) {
@@ -468,7 +487,7 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s) {
+                          hipStream_t s, const uint32_t* aaSet) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *ko = keysB;
     V *vi = valsA, *vo = valsB;
@@ -478,8 +497,8 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
         const bool f = first && filter, g = first && genVals;
-        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
-        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles, aaSet);
+        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles, nullptr);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
         if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
@@ -500,9 +519,9 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
 }
 
 template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, const uint32_t*);
 template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, const uint32_t*);
 
 // ------------------------------------------------------------------------------------------------
 // K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->
@@ -595,6 +614,18 @@ void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
 }
 
 uint64_t host_from_rank_form(uint64_t v) { return from_rank_form(v); }
+
+__global__ void k_aa_set(const uint64_t* __restrict__ dbv, uint64_t D, uint32_t* __restrict__ bits) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= D) return;
+    const uint64_t r = dbv[i] >> 24;
+    if (i > 0 && (dbv[i - 1] >> 24) == r) return;  // first k-mer of each AA run sets the bit
+    atomicOr(&bits[r >> 5], 1u << (r & 31u));
+}
+
+void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s) {
+    if (D) k_aa_set<<<(unsigned)((D + 255) / 256), 256, 0, s>>>(dbv, D, bits);
+}
 
 __global__ void k_build_dir(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
     uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -71,14 +71,20 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
                     uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
 
 uint64_t radix_counts_elems(uint64_t n);
-// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read)
+// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read);
+// aaSet (with filter): keys whose AA rank is not in the bitmap are dropped too (keysA rewritten)
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s);
+                          hipStream_t s, const uint32_t* aaSet = nullptr);
 // format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
 uint64_t host_from_rank_form(uint64_t v);
+// AA 8-mers: base-21 ranks 0 .. 21^8 - 1
+constexpr uint64_t kAARankEnd = 37822859361ull;
+// AA membership bitmap of the DB: bit r of word r / 32 = some DB k-mer has AA rank r
+constexpr uint64_t kAASetWords = (kAARankEnd + 31) / 32;
+void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s);  // bits zeroed by caller
 // query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
 
