@@ -654,8 +654,8 @@ void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir
 // loads and every query of the block searches LDS. A block whose range holds more than kMatchWin
 // DB values (few queries against a large DB, or a very frequent AA k-mer) searches HBM through the
 // directory instead.
-constexpr int kMatchQ = 512;
-constexpr int kMatchWin = 2048;
+constexpr int kMatchQ = 256;
+constexpr int kMatchWin = 4096;
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
 __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
