@@ -439,7 +439,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipEventRecord(c->kev[0], s));
     launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
                    c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
-                   c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
+                   c->aaSet, c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[1], s));
     HIP_TRY(hipEventRecord(c->ev[1], s));
     // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
@@ -454,8 +454,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipEventRecord(c->kev[2], s));
     uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
                                   c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
-                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s,
-                                  c->aaSet);
+                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
     HIP_TRY(hipEventRecord(c->kev[3], s));
     c->Q = Q;
     c->stats[0] = R;

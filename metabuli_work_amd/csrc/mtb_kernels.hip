@@ -207,7 +207,8 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
                                                  const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
                                                  const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
                                                  ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
-                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ unitInfo) {
+                                                 const uint32_t* __restrict__ aaSet, uint64_t* __restrict__ keys,
+                                                 uint64_t* __restrict__ unitInfo) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     sBase[threadIdx.x] = tabs.base[threadIdx.x];
@@ -261,6 +262,9 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
     const uint64_t smMask = (smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1);
     int run = 0;
     (void)aaLen;
+    uint64_t pendKey = kSentinel;  // window awaiting its bitmap word
+    uint32_t pendWord = 0, pendBit = 0;
+    int pendP = -1;
     for (int j = pFirst; j < pFirst + nWin + 7; j++) {
         int c0 = fromLeft ? s0 + 3 * j : e0 - 3 * j;  // first base of the triplet in load order
         uint32_t b1, b2, b3;
@@ -305,30 +309,45 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
             ok = (bestK == nSm - 1) || (bestK == 0);
         }
         uint64_t key = kSentinel;
+        uint32_t word = 0xFFFFFFFFu, bit = 0;
         if (ok) {
             // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
             uint64_t aaPart = 0;
 #pragma unroll
             for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
             key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
+            // an AA 8-mer absent from the DB can match nothing (matchKmers compares AA parts for
+            // equality first): it is blanked so the sort and the join never see it. The bitmap
+            // word is only consumed one window later, so the random load overlaps a window's work.
+            if (aaSet) {
+                const uint64_t b = aaPart >> kAASetShift;
+                word = aaSet[b >> 5];
+                bit = (uint32_t)(b & 31u);
+            }
         }
-        keys[slotBase + 64ull * (p - pFirst)] = key;
+        if (pendP >= 0) keys[slotBase + 64ull * pendP] = ((pendWord >> pendBit) & 1u) ? pendKey : kSentinel;
+        pendKey = key;
+        pendWord = word;
+        pendBit = bit;
+        pendP = p - pFirst;
     }
+    if (pendP >= 0) keys[slotBase + 64ull * pendP] = ((pendWord >> pendBit) & 1u) ? pendKey : kSentinel;
 }
 
 uint64_t extract_slots(uint64_t nUnits, uint32_t C) { return (nUnits + 63) / 64 * 64 * C; }
 
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
-                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* unitInfo, hipStream_t s) {
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, const uint32_t* aaSet,
+                    uint64_t* keys, uint64_t* unitInfo, hipStream_t s) {
     ExtractTables tabs;
     for (int i = 0; i < 256; i++) tabs.base[i] = t.base[i];
     for (int i = 0; i < 64; i++) { tabs.aa[i] = t.aa[i]; tabs.num[i] = t.num[i]; }
     if (nUnits == 0) return;
     const uint64_t threads = (nUnits + 63) / 64 * 64;  // whole waves: padding units write sentinels
     k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits,
-                                                                C, tabs, kmerFormat, syncmer, smerLen, keys, unitInfo);
+                                                                C, tabs, kmerFormat, syncmer, smerLen, aaSet, keys,
+                                                                unitInfo);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -345,14 +364,9 @@ constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
 __device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) { return (uint32_t)((k >> shift) & 0xFF); }
 
-// aaSet (first pass of the query sort, FILTER only): keys whose AA 8-mer is absent from the DB's
-// membership bitmap cannot match (matchKmers compares AA parts for equality first); they are
-// overwritten with the sentinel here, so the scatter drops them with the blank slots. The 16
-// lookups of a thread go out together, after its 16 key loads.
 template <bool FILTER>
-__global__ void __launch_bounds__(256) k_radix_hist(uint64_t* __restrict__ keys, uint64_t n, int shift,
-                                                    uint32_t* __restrict__ counts, uint32_t nTiles,
-                                                    const uint32_t* __restrict__ aaSet) {
+__global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
+                                                    uint32_t* __restrict__ counts, uint32_t nTiles) {
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
@@ -362,20 +376,6 @@ __global__ void __launch_bounds__(256) k_radix_hist(uint64_t* __restrict__ keys,
     for (int k = 0; k < kRadixItems; k++) {
         const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
         key[k] = i < n ? keys[i] : kSentinel;
-    }
-    if (FILTER && aaSet) {
-        uint32_t word[kRadixItems];
-#pragma unroll
-        for (int k = 0; k < kRadixItems; k++) {
-            const uint64_t r = key[k] >> 24;
-            word[k] = key[k] != kSentinel ? aaSet[r >> 5] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kRadixItems; k++) {
-            if (key[k] == kSentinel || ((word[k] >> ((key[k] >> 24) & 31u)) & 1u)) continue;
-            key[k] = kSentinel;
-            keys[base + (uint64_t)k * kBlock + threadIdx.x] = kSentinel;
-        }
     }
 #pragma unroll
     for (int k = 0; k < kRadixItems; k++) {
@@ -487,7 +487,7 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s, const uint32_t* aaSet) {
+                          hipStream_t s) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *ko = keysB;
     V *vi = valsA, *vo = valsB;
@@ -497,8 +497,8 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
         const bool f = first && filter, g = first && genVals;
-        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles, aaSet);
-        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles, nullptr);
+        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
         if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
@@ -519,9 +519,9 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
 }
 
 template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, const uint32_t*);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
 template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, const uint32_t*);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
 
 // ------------------------------------------------------------------------------------------------
 // K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->
@@ -620,7 +620,8 @@ __global__ void k_aa_set(const uint64_t* __restrict__ dbv, uint64_t D, uint32_t*
     if (i >= D) return;
     const uint64_t r = dbv[i] >> 24;
     if (i > 0 && (dbv[i - 1] >> 24) == r) return;  // first k-mer of each AA run sets the bit
-    atomicOr(&bits[r >> 5], 1u << (r & 31u));
+    const uint64_t b = r >> kAASetShift;
+    atomicOr(&bits[b >> 5], 1u << (b & 31u));
 }
 
 void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s) {

@@ -67,23 +67,24 @@ uint64_t extract_slots(uint64_t nUnits, uint32_t C);
 // K1 over nUnits chunks of <= C windows; writes extract_slots(nUnits, C) slots
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
-                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, const uint32_t* aaSet,
+                    uint64_t* keys, uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit
+                    // (slot_info); aaSet (nullable): windows whose AA 8-mer the DB lacks are blanked
 
 uint64_t radix_counts_elems(uint64_t n);
-// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read);
-// aaSet (with filter): keys whose AA rank is not in the bitmap are dropped too (keysA rewritten)
+// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read)
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s, const uint32_t* aaSet = nullptr);
+                          hipStream_t s);
 // format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
 uint64_t host_from_rank_form(uint64_t v);
 // AA 8-mers: base-21 ranks 0 .. 21^8 - 1
 constexpr uint64_t kAARankEnd = 37822859361ull;
-// AA membership bitmap of the DB: bit r of word r / 32 = some DB k-mer has AA rank r
-constexpr uint64_t kAASetWords = (kAARankEnd + 31) / 32;
+// AA membership bitmap of the DB: bit b = r >> kAASetShift is set if some DB k-mer has AA rank r
+constexpr int kAASetShift = 0;
+constexpr uint64_t kAASetWords = ((kAARankEnd >> kAASetShift) + 32) / 32;
 void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s);  // bits zeroed by caller
 // query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
