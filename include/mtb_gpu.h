@@ -203,6 +203,35 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxonomy, const m
                  mtb_db_built* out);
 void mtb_free_built(mtb_db_built* b);
 
+/* ---- host I/O around the path ------------------------------------------ */
+/* One batch of reads in the flat layout mtb_classify_batch takes; names are the header's first
+ * token (kseq), concatenated, name i = names[name_off[i] .. name_off[i+1]). Buffers belong to the
+ * reader and stay valid until its next call. */
+typedef struct mtb_read_batch {
+    uint32_t n_reads;
+    const char* seq1;
+    const uint64_t* off1;
+    const char* seq2; /* NULL unless paired */
+    const uint64_t* off2;
+    const char* names;
+    const uint64_t* name_off;
+} mtb_read_batch;
+
+typedef struct mtb_reader mtb_reader;
+/* FASTA or FASTQ, plain or gzip; path2 NULL for single-end. Replaces QueryIndexer's indexing pass and
+ * KmerExtractor::loadChunkOfReads (QueryIndexer.cpp:30-147, KmerExtractor.cpp:442-494). */
+int mtb_reader_open(const char* path1, const char* path2, mtb_reader** out);
+/* Up to max_reads reads (and about max_bases bases); n_reads == 0 at end of input. MTB_ERR_IO on
+ * malformed input or mates with different read counts (QueryIndexer.cpp:121-124). */
+int mtb_reader_next(mtb_reader* r, uint32_t max_reads, uint64_t max_bases, mtb_read_batch* batch);
+void mtb_reader_close(mtb_reader* r);
+/* Rank name of a taxID in the context's taxonomy ("-" if absent). */
+const char* mtb_taxon_rank(const mtb_ctx* ctx, int32_t tax_id);
+/* Reporter::writeReadClassification (Reporter.cpp:38-83) for one batch: header line unless
+ * append, one line per read; taxcnt as returned by mtb_get_taxcnt. */
+int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
+                              const mtb_result* results, const mtb_taxcnt* taxcnt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,3 +79,16 @@ def info_frame(info):
 
 def info_pos(info):
     return np.asarray(info, np.uint64) & np.uint64(0xFFFFFFFF)
+
+
+class MtbReadBatch(ctypes.Structure):
+    """mtb_read_batch (include/mtb_gpu.h): one batch from mtb_reader_next."""
+    _fields_ = [
+        ("n_reads", ctypes.c_uint32),
+        ("seq1", ctypes.c_void_p),
+        ("off1", ctypes.POINTER(ctypes.c_uint64)),
+        ("seq2", ctypes.c_void_p),
+        ("off2", ctypes.POINTER(ctypes.c_uint64)),
+        ("names", ctypes.c_void_p),
+        ("name_off", ctypes.POINTER(ctypes.c_uint64)),
+    ]

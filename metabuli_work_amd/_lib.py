@@ -7,7 +7,7 @@ entry point raises. Build it with `python -c "import __graft_entry__ as g; g.bui
 import ctypes
 import pathlib
 
-from ._abi import MtbDbHost, MtbParams
+from ._abi import MtbDbHost, MtbParams, MtbReadBatch
 
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libmtbgpu.so"
@@ -18,7 +18,8 @@ EXPORTED = [
     "mtb_default_params", "mtb_load_db_parameters", "mtb_open", "mtb_open_host", "mtb_close", "mtb_last_error",
     "mtb_set_stream", "mtb_db_kmers", "mtb_classify_batch", "mtb_get_taxcnt", "mtb_device_results",
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
-    "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built",
+    "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
+    "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications",
 ]
 
 
@@ -57,6 +58,13 @@ def lib() -> ctypes.CDLL:
     L.mtb_get_query_kmers.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_get_matches.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_assign_matches.argtypes = [vp, vp, u64, vp, u32, vp]
+    L.mtb_reader_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(vp)]
+    L.mtb_reader_next.argtypes = [vp, u32, u64, P(MtbReadBatch)]
+    L.mtb_reader_close.argtypes = [vp]
+    L.mtb_reader_close.restype = None
+    L.mtb_taxon_rank.argtypes = [vp, ctypes.c_int32]
+    L.mtb_taxon_rank.restype = ctypes.c_char_p
+    L.mtb_write_classifications.argtypes = [vp, ctypes.c_char_p, i32, P(MtbReadBatch), vp, vp]
     L.mtb_debug_tables.argtypes = [vp, vp, vp]
     L.mtb_debug_tables.restype = None
     _LIB = L

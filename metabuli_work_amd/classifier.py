@@ -197,25 +197,81 @@ class Classifier:
 
     # -- Classifier::startClassify over files ----------------------------------------------------
     def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000) -> int:
+        """Classifier::startClassify (Classifier.cpp:44-164): batches from the native FASTA/FASTQ(.gz)
+        reader (mtb_reader_*), one mtb_classify_batch each, TSV lines by mtb_write_classifications."""
         par = self.par
         q1 = par.filenames[0]
         q2 = par.filenames[1] if par.seqMode == 2 else None
         total = 0
-        with open(out_tsv, "w") as out:
-            out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n")
-            for names, s1, o1, s2, o2 in read_batches(q1, q2, reads_per_batch):
-                br = self.classify_batch(s1, o1, s2, o2)
-                write_classifications(out, names, br, self._rank_of)
-                total += len(names)
+        first = True
+        with FastxReader(q1, q2) as rd:
+            while True:
+                b = rd.next(reads_per_batch)
+                if b.n_reads == 0:
+                    break
+                n = b.n_reads
+                res = np.zeros(n, RESULT_DTYPE)
+                check(lib().mtb_classify_batch(self.handle, b.seq1, b.off1, b.seq2, b.off2, n, 0, ptr(res)),
+                      "mtb_classify_batch")
+                tc = self.taxcnt()
+                check(lib().mtb_write_classifications(self.handle, out_tsv.encode(), 0 if first else 1,
+                                                      ctypes.byref(b), ptr(res), ptr(tc)),
+                      "mtb_write_classifications")
+                first = False
+                total += n
+        if first:  # no reads: header only
+            with open(out_tsv, "w") as out:
+                out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n")
         return total
 
     _rank_of = None
 
 
 # --------------------------------------------------------------------------------------------------
-# Host I/O: FASTA/FASTQ(.gz) reading (KSeqWrapper semantics: name = header up to first whitespace)
-# and the per-read TSV (Reporter.cpp:38-83).
+# Host I/O. FastxReader wraps the native reader (mtb_reader_*, mtb_io.cpp) the product path uses;
+# read_records / write_classifications below are an independent pure-Python restatement
+# (KSeqWrapper semantics: name = header up to first whitespace; Reporter.cpp:38-83) kept for tests.
 # --------------------------------------------------------------------------------------------------
+class FastxReader:
+    """Batches of reads from FASTA/FASTQ(.gz) (one file, or two mates in lock-step)."""
+
+    def __init__(self, path1: str, path2: Optional[str] = None):
+        self.h = ctypes.c_void_p()
+        check(lib().mtb_reader_open(path1.encode(), path2.encode() if path2 else None, ctypes.byref(self.h)),
+              "mtb_reader_open")
+
+    def next(self, max_reads: int, max_bases: int = 1 << 62) -> _abi.MtbReadBatch:
+        b = _abi.MtbReadBatch()
+        check(lib().mtb_reader_next(self.h, max_reads, max_bases, ctypes.byref(b)), "mtb_reader_next")
+        return b
+
+    @staticmethod
+    def arrays(b: _abi.MtbReadBatch):
+        """Copies of a batch as (names, seq1, off1, seq2, off2) numpy/py objects."""
+        n = b.n_reads
+        o1 = np.ctypeslib.as_array(b.off1, (n + 1,)).copy()
+        s1 = np.frombuffer(ctypes.string_at(b.seq1, int(o1[-1])), np.uint8).copy()
+        s2 = o2 = None
+        if b.seq2:
+            o2 = np.ctypeslib.as_array(b.off2, (n + 1,)).copy()
+            s2 = np.frombuffer(ctypes.string_at(b.seq2, int(o2[-1])), np.uint8).copy()
+        no = np.ctypeslib.as_array(b.name_off, (n + 1,)).copy()
+        raw = ctypes.string_at(b.names, int(no[-1]))
+        names = [raw[no[i]:no[i + 1]].decode() for i in range(n)]
+        return names, s1, o1, s2, o2
+
+    def close(self):
+        if self.h:
+            lib().mtb_reader_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 def _open(path: str):
     return gzip.open(path, "rb") if path.endswith(".gz") else open(path, "rb")
 

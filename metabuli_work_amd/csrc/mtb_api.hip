@@ -68,6 +68,8 @@ struct mtb_ctx {
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
     uint8_t* tFlags = nullptr;
     uint32_t cladePerMatch = 2;
+    std::vector<int32_t> hNodeOf;  // host copies for mtb_taxon_rank / the TSV writer
+    std::vector<std::string> hRank;
     // batch workspace
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
@@ -174,6 +176,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     // taxonomy + taxId2speciesId
     const HostTaxonomy& T = db.tax;
     c->maxTax = T.maxTax;
+    c->hNodeOf = T.nodeOf;
+    c->hRank = T.rank;
     HIP_TRY(upload(&c->spOf, db.speciesOf, s));
     HIP_TRY(upload(&c->tNodeOf, T.nodeOf, s));
     HIP_TRY(upload(&c->tNodeTax, T.nodeTax, s));
@@ -560,6 +564,11 @@ int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
     if (q) *q = c->Q;
     if (m) *m = c->M;
     return MTB_OK;
+}
+
+const char* mtb_taxon_rank(const mtb_ctx* c, int32_t t) {
+    if (!c || t < 0 || (size_t)t >= c->hNodeOf.size() || c->hNodeOf[t] < 0) return "-";
+    return c->hRank[c->hNodeOf[t]].c_str();
 }
 
 int mtb_last_stats(const mtb_ctx* c, uint64_t* out, int n) {

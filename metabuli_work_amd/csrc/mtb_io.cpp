@@ -1,0 +1,272 @@
+// Host I/O around the device path: a FASTA/FASTQ(.gz) batch reader that fills
+// the flat buffers mtb_classify_batch takes, and the per-read classification TSV writer.
+//
+// Reader: replaces QueryIndexer's counting pass plus KmerExtractor::loadChunkOfReads'
+// serial kseq loop (QueryIndexer.cpp:30-147, KmerExtractor.cpp:442-494): one streaming pass,
+// zlib's gzread (which also passes plain files through) into a large buffer, records split with
+// memchr, names cut at the first whitespace as kseq does. Mates are read in lock-step; unequal
+// read counts are an error, as in QueryIndexer.cpp:121-124.
+//
+// Writer: Reporter::writeReadClassification (Reporter.cpp:38-83), formatted by several threads
+// into per-thread strings and written in read order. Scores print as ostream << float (%g).
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mtb_host.h"
+
+namespace {
+
+struct FastxStream {
+    gzFile f = nullptr;
+    std::vector<char> buf;  // unread bytes live in [pos, end)
+    size_t pos = 0, end = 0;
+    bool eof = false;
+    char kind = 0;  // '>' FASTA, '@' FASTQ
+
+    bool open(const char* path) {
+        f = gzopen(path, "rb");
+        if (!f) return false;
+        gzbuffer(f, 1 << 20);
+        buf.resize(64u << 20);
+        return true;
+    }
+    void close() {
+        if (f) gzclose(f);
+        f = nullptr;
+    }
+    // Make at least `want` bytes available from pos (or everything left). Returns bytes available.
+    size_t fill(size_t want) {
+        if (end - pos >= want || eof) return end - pos;
+        if (pos > 0) {
+            memmove(buf.data(), buf.data() + pos, end - pos);
+            end -= pos;
+            pos = 0;
+        }
+        if (buf.size() < want + (1u << 20)) buf.resize(want + (1u << 20));
+        while (end < buf.size() && !eof) {
+            int got = gzread(f, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, 1u << 30));
+            if (got <= 0) {
+                eof = true;
+                break;
+            }
+            end += (size_t)got;
+            if (end - pos >= want) break;
+        }
+        return end - pos;
+    }
+    // Next line (without '\n' / '\r'); false at end of input.
+    bool line(const char*& p, size_t& n) {
+        for (size_t want = 1u << 16;; want *= 2) {
+            size_t avail = fill(want);
+            if (avail == 0) return false;
+            const char* s = buf.data() + pos;
+            const char* nl = (const char*)memchr(s, '\n', avail);
+            if (nl || eof) {
+                size_t len = nl ? (size_t)(nl - s) : avail;
+                pos += len + (nl ? 1 : 0);
+                if (len && s[len - 1] == '\r') len--;
+                p = s;
+                n = len;
+                return true;
+            }
+            if (avail < want) return false;
+        }
+    }
+    int peek() {
+        if (fill(1) == 0) return -1;
+        return (unsigned char)buf[pos];
+    }
+};
+
+// One record appended to (seq, names); false at end of input. Throws nothing: malformed input
+// sets err.
+bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, std::string& names,
+                 std::vector<uint64_t>& noff, std::string& err) {
+    const char* p;
+    size_t n;
+    // skip blank lines before a header
+    while (true) {
+        int c = s.peek();
+        if (c < 0) return false;
+        if (c == '\n' || c == '\r') {
+            s.line(p, n);
+            continue;
+        }
+        break;
+    }
+    if (!s.line(p, n)) return false;
+    if (n == 0 || (p[0] != '>' && p[0] != '@')) {
+        err = "not a FASTA/FASTQ record header";
+        return false;
+    }
+    if (!s.kind) s.kind = p[0];
+    size_t nameLen = 1;
+    while (nameLen < n && p[nameLen] != ' ' && p[nameLen] != '\t') nameLen++;
+    names.append(p + 1, nameLen - 1);
+    noff.push_back(names.size());
+    if (s.kind == '@') {
+        if (!s.line(p, n)) {
+            err = "truncated FASTQ record";
+            return false;
+        }
+        seq.append(p, n);
+        const char* q;
+        size_t qn;
+        if (!s.line(q, qn) || qn == 0 || q[0] != '+' || !s.line(q, qn)) {
+            err = "truncated FASTQ record";
+            return false;
+        }
+    } else {
+        while (true) {
+            int c = s.peek();
+            if (c < 0 || c == '>') break;
+            s.line(p, n);
+            seq.append(p, n);
+        }
+    }
+    off.push_back(seq.size());
+    return true;
+}
+
+}  // namespace
+
+struct mtb_reader {
+    FastxStream a, b;
+    bool paired = false;
+    std::string seq1, seq2, names, err;
+    std::vector<uint64_t> off1, off2, noff;
+};
+
+extern "C" {
+
+int mtb_reader_open(const char* path1, const char* path2, mtb_reader** out) {
+    if (!path1 || !out) return MTB_ERR_ARG;
+    mtb_reader* r = new mtb_reader();
+    if (!r->a.open(path1)) {
+        mtb::set_error(std::string("cannot open ") + path1);
+        delete r;
+        return MTB_ERR_IO;
+    }
+    if (path2) {
+        r->paired = true;
+        if (!r->b.open(path2)) {
+            mtb::set_error(std::string("cannot open ") + path2);
+            r->a.close();
+            delete r;
+            return MTB_ERR_IO;
+        }
+    }
+    *out = r;
+    return MTB_OK;
+}
+
+int mtb_reader_next(mtb_reader* r, uint32_t max_reads, uint64_t max_bases, mtb_read_batch* batch) {
+    if (!r || !batch || max_reads == 0) return MTB_ERR_ARG;
+    r->seq1.clear();
+    r->seq2.clear();
+    r->names.clear();
+    r->off1.assign(1, 0);
+    r->off2.assign(1, 0);
+    r->noff.assign(1, 0);
+    std::string dummyNames;
+    std::vector<uint64_t> dummyOff(1, 0);
+    uint32_t n = 0;
+    while (n < max_reads && r->seq1.size() + r->seq2.size() < max_bases) {
+        if (!next_record(r->a, r->seq1, r->off1, r->names, r->noff, r->err)) break;
+        if (r->paired) {
+            dummyNames.clear();
+            dummyOff.assign(1, 0);
+            if (!next_record(r->b, r->seq2, r->off2, dummyNames, dummyOff, r->err)) {
+                if (r->err.empty()) r->err = "paired-end inputs have different read counts (QueryIndexer.cpp:121-124)";
+                break;
+            }
+        }
+        n++;
+    }
+    if (!r->err.empty()) {
+        mtb::set_error(r->err);
+        return MTB_ERR_IO;
+    }
+    if (r->paired && n == 0 && r->b.peek() >= 0 && r->b.peek() != '\n') {
+        mtb::set_error("paired-end inputs have different read counts (QueryIndexer.cpp:121-124)");
+        return MTB_ERR_IO;
+    }
+    batch->n_reads = n;
+    batch->seq1 = r->seq1.data();
+    batch->off1 = r->off1.data();
+    batch->seq2 = r->paired ? r->seq2.data() : nullptr;
+    batch->off2 = r->paired ? r->off2.data() : nullptr;
+    batch->names = r->names.data();
+    batch->name_off = r->noff.data();
+    return MTB_OK;
+}
+
+void mtb_reader_close(mtb_reader* r) {
+    if (!r) return;
+    r->a.close();
+    r->b.close();
+    delete r;
+}
+
+int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
+                              const mtb_result* res, const mtb_taxcnt* taxcnt) {
+    if (!ctx || !path || !batch || (!res && batch->n_reads)) return MTB_ERR_ARG;
+    const uint32_t n = batch->n_reads;
+    const char* names = batch->names;
+    const uint64_t* name_off = batch->name_off;
+    const int header = !append;
+    FILE* f = fopen(path, append ? "ab" : "wb");
+    if (!f) {
+        mtb::set_error(std::string("cannot write ") + path);
+        return MTB_ERR_IO;
+    }
+    if (header) fputs("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n", f);
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint32_t per = (n + nt - 1) / nt;
+    std::vector<std::string> part(nt);
+    auto work = [&](unsigned t) {
+        std::string& o = part[t];
+        char tmp[64];
+        const uint32_t lo = t * per, hi = std::min<uint32_t>(n, lo + per);
+        o.reserve((size_t)(hi > lo ? hi - lo : 0) * 48);
+        for (uint32_t i = lo; i < hi; i++) {
+            const mtb_result& r = res[i];
+            o += r.is_classified ? "1\t" : "0\t";
+            o.append(names + name_off[i], names + name_off[i + 1]);
+            snprintf(tmp, sizeof tmp, "\t%d\t%u\t%g\t", r.is_classified ? r.classification : 0, r.query_length,
+                     (double)r.score);
+            o += tmp;
+            if (r.is_classified) {
+                o += mtb_taxon_rank(ctx, r.classification);
+                o += '\t';
+                for (uint32_t k = 0; k < r.taxcnt_len; k++) {
+                    const mtb_taxcnt& c = taxcnt[r.taxcnt_offset + k];
+                    snprintf(tmp, sizeof tmp, "%d:%u ", c.tax_id, c.count);
+                    o += tmp;
+                }
+                o += '\n';
+            } else {
+                o += "-\t-\t\n";
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (auto& s : part) fwrite(s.data(), 1, s.size(), f);
+    const bool ok = fclose(f) == 0;
+    if (!ok) {
+        mtb::set_error(std::string("write failed: ") + path);
+        return MTB_ERR_IO;
+    }
+    return MTB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+"""Native host I/O (mtb_io.cpp): the FASTA/FASTQ(.gz) batch reader against the
+independent Python reader and the synthesised reads, its error paths, and (GPU) the end-to-end
+startClassify TSV against the oracle's classifications."""
+import gzip
+
+import numpy as np
+import pytest
+
+from metabuli_work_amd import synth
+from metabuli_work_amd._lib import MtbError
+from metabuli_work_amd.classifier import Classifier, FastxReader, LocalParameters, read_records
+from tests import oracle_ctypes as oc
+
+
+def _mates(reads, which):
+    seq = reads.seq1 if which == 1 else reads.seq2
+    off = reads.off1 if which == 1 else reads.off2
+    return [bytes(seq[off[i]:off[i + 1]]) for i in range(reads.n)]
+
+
+def _write_fastq(path, names, seqs):
+    data = "".join(f"@{n} some comment\n{s.decode()}\n+\n{'I' * len(s)}\n" for n, s in zip(names, seqs)).encode()
+    if path.endswith(".gz"):
+        with gzip.open(path, "wb") as f:
+            f.write(data)
+    else:
+        with open(path, "wb") as f:
+            f.write(data)
+
+
+def _write_fasta(path, names, seqs, width=60):
+    with open(path, "w") as f:
+        for n, s in zip(names, seqs):
+            f.write(f">{n}\tdesc\n")
+            for i in range(0, len(s), width):
+                f.write(s[i:i + width].decode() + "\n")
+            if not s:
+                f.write("\n")
+
+
+def _read_all(p1, p2, batch):
+    names, m1, m2 = [], [], []
+    with FastxReader(p1, p2) as rd:
+        while True:
+            b = rd.next(batch)
+            if b.n_reads == 0:
+                break
+            nm, s1, o1, s2, o2 = FastxReader.arrays(b)
+            assert len(nm) <= batch
+            names += nm
+            m1 += [bytes(s1[o1[i]:o1[i + 1]]) for i in range(len(nm))]
+            if s2 is not None:
+                m2 += [bytes(s2[o2[i]:o2[i + 1]]) for i in range(len(nm))]
+    return names, m1, m2
+
+
+@pytest.fixture(scope="module")
+def reads():
+    taxo = synth.make_taxonomy(6, 2, seed=3)
+    gen = synth.make_genomes(taxo, genome_len=8000, seed=4)
+    return synth.make_reads(gen, 1000, paired=True, seed=9, short_frac=0.05, rate_n=0.01, rate_lower=0.01)
+
+
+@pytest.mark.parametrize("gz", [False, True])
+def test_fastq_pairs(tmp_path, reads, gz):
+    ext = ".fq.gz" if gz else ".fq"
+    names = [f"read{i}" for i in range(reads.n)]
+    p1, p2 = str(tmp_path / ("r1" + ext)), str(tmp_path / ("r2" + ext))
+    _write_fastq(p1, names, _mates(reads, 1))
+    _write_fastq(p2, names, _mates(reads, 2))
+    got_names, g1, g2 = _read_all(p1, p2, 333)
+    assert got_names == names
+    assert g1 == _mates(reads, 1) and g2 == _mates(reads, 2)
+    assert [s for _, s in read_records(p1)] == g1  # the independent Python reader agrees
+
+
+def test_fasta_multiline(tmp_path, reads):
+    names = [f"contig_{i}" for i in range(reads.n)]
+    seqs = _mates(reads, 1)
+    p = str(tmp_path / "r.fa")
+    _write_fasta(p, names, seqs, width=37)
+    got_names, g1, g2 = _read_all(p, None, 1000)
+    assert got_names == names and g1 == seqs and g2 == []
+
+
+def test_reader_errors(tmp_path, reads):
+    names = [f"r{i}" for i in range(10)]
+    seqs = _mates(reads, 1)[:10]
+    p1, p2 = str(tmp_path / "a.fq"), str(tmp_path / "b.fq")
+    _write_fastq(p1, names, seqs)
+    _write_fastq(p2, names[:7], seqs[:7])
+    with pytest.raises(MtbError, match="different read counts"):
+        _read_all(p1, p2, 4)
+    bad = str(tmp_path / "bad.fq")
+    with open(bad, "w") as f:
+        f.write("not a record\nACGT\n")
+    with pytest.raises(MtbError, match="header"):
+        _read_all(bad, None, 4)
+    with pytest.raises(MtbError, match="cannot open"):
+        FastxReader(str(tmp_path / "missing.fq"))
+
+
+@pytest.mark.gpu
+def test_start_classify_tsv(make_db, tmp_path):
+    """File in, TSV out (Classifier::startClassify + Reporter::writeReadClassification) against the
+    oracle's per-read results for the same reads."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 2500, paired=True, seed=41, short_frac=0.02)
+    names = [f"q{i}" for i in range(r.n)]
+    p1, p2 = str(tmp_path / "q1.fq.gz"), str(tmp_path / "q2.fq.gz")
+    _write_fastq(p1, names, _mates(r, 1))
+    _write_fastq(p2, names, _mates(r, 2))
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    out = str(tmp_path / "out.tsv")
+    with Classifier(par, db_dir=db_dir) as clf:
+        assert clf.startClassify(out, reads_per_batch=700) == r.n
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    rank_of = dict(zip(taxo.taxid.tolist(), taxo.rank))
+    lines = open(out).read().split("\n")
+    assert lines[0] == "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count"
+    body = [l for l in lines[1:] if l]
+    assert len(body) == r.n
+    for i, line in enumerate(body):
+        f = line.split("\t")
+        o = ores[i]
+        assert f[0] == ("1" if o["is_classified"] else "0") and f[1] == names[i]
+        assert int(f[2]) == (int(o["classification"]) if o["is_classified"] else 0)
+        assert int(f[3]) == int(o["query_length"])
+        assert f[4] == "%g" % float(o["score"])
+        if o["is_classified"]:
+            assert f[5] == rank_of.get(int(o["classification"]), "-")
+            s = int(o["taxcnt_offset"])
+            want = "".join(f"{int(t)}:{int(c)} " for t, c in otc[s:s + int(o["taxcnt_len"])])
+            assert f[6] == want
+        else:
+            assert f[5:] == ["-", "-", ""]
