@@ -35,7 +35,13 @@ from metabuli_work_amd.dbbuild import build_db  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "stage_traffic.json")
-KERNELS = ["extract", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
+# the six timed kernels of mtb_last_kernel_ms, by join path (mtb_last_stats[10])
+KERNELS_SORT = ["extract", "filter", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
+KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpose", "match_sort", "assign"]
+
+
+def kernel_names(work):
+    return KERNELS_PROBE if work.get("join_path", 1) == 0 else KERNELS_SORT
 
 
 def log(rank, *a):
@@ -245,7 +251,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kern = np.zeros(len(KERNELS))
+    kern = np.zeros(7)
     stage = np.zeros(5)
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -264,6 +270,7 @@ def main():
     stage /= max(1, args.steps)
     Q, M = clf.last_counts()
     work = clf.stats()
+    KERNELS = kernel_names(work)
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     value = world * n * args.steps / elapsed
 
@@ -272,11 +279,16 @@ def main():
     R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
     D = hdb.n_kmers
     alg = {
+        "filter": 8 * R + 4 * R + 20 * Q,                  # keys in, one 4-B membership word per window,
+                                                            # the present (key, slot, DB lower bound) out
+        # probe join: per query its (key, slot, lower bound), 8 DB values + taxIDs from there,
+        # its staged matches (+ rank) out
+        "probe_join": 20 * Q + 96 * Q + 28 * M,
         "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
-        "kmer_sort": 8 * R + 12 * Q,                        # the keys read once, the kept (key, slot) written once
-        "match_join": 12 * Q + 12 * D + 24 * M,             # queries, the DB (values + taxIDs) streamed through
+        "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
+        "match_join": 12 * Q + 12 * D + 28 * M,             # queries, the DB (values + taxIDs) streamed through
                                                             # the block windows once, staged matches written
-        "match_transpose": 2 * 24 * M + 8 * n,              # staged matches read, written to read segments
+        "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
         "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
     }
@@ -343,7 +355,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         lsteps = max(1, min(args.steps, 3))
-        kl = np.zeros(len(KERNELS))
+        kl = np.zeros(7)
         tl0 = time.perf_counter()
         for _ in range(lsteps):
             clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
@@ -382,7 +394,7 @@ def main():
                      "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
                      "reads_per_gpu": args.long_reads, "bases_per_gpu": int(lo1[-1].item()), "n50": long_n50,
                      "query_kmers": lq, "matches": lm,
-                     "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(KERNELS, kl)},
+                     "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(kernel_names(lwork), kl)},
                      "cpu_baseline": long_cpu, "work": lwork,
                      "workload": "config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs the "
                                  "same DB, seq mode 3"}

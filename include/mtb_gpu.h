@@ -149,15 +149,16 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
 /* Work counts of the last batch: [0] reserved k-mer slots, [1] query k-mers, [2] query k-mers
  * with >= 1 match, [3] matches, [4] most matches of one read, [5] (read, species, frame) groups,
  * [6] groups of >= 2 matches, [7] (read, species) runs, [8] runs combined one per wave, [9] of those,
- * runs whose tied paths needed the std::sort emulation. */
+ * runs whose tied paths needed the std::sort emulation, [10] join path (1 sort-merge join, the
+ * default; 0 probe join, MTB_JOIN=probe). Query k-mers = windows whose AA 8-mer the DB holds. */
 int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):
  * [0] extract, [1] k-mer sort, [2] match, [3] match sort + assign, [4] total. */
 int mtb_last_stage_ms(const mtb_ctx* ctx, float* ms, int n);
 /* Device time of the main kernels of the last batch in ms, from event pairs recorded on the
- * launch stream tightly around each launch: [0] K1 extract, [1] K2 radix sort (all passes),
- * [2] K4 join (windows + select + stage), [3] K4 transpose into per-read segments, [4] K5 per-read
- * match sort, [5] K6 assign. */
+ * launch stream tightly around each launch: [0] K1 extract, [1] K1F membership filter, [2] K2 radix
+ * sort (sort-merge join only), [3] K4 join (probe join, or windows + select + stage), [4] K4
+ * transpose into per-read segments, [5] K5 per-read match sort, [6] K6 assign. */
 int mtb_last_kernel_ms(const mtb_ctx* ctx, float* ms, int n);
 /* Copy the last batch's mtb_result[n_reads] to dst (device memory if dst_on_device). */
 int mtb_copy_results(mtb_ctx* ctx, void* dst, int dst_on_device);

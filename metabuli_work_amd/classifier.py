@@ -150,7 +150,7 @@ class Classifier:
         return int(q.value), int(m.value)
 
     STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
-             "species_runs", "wave_runs", "wave_runs_emulated"]
+             "species_runs", "wave_runs", "wave_runs_emulated", "join_path"]
 
     def stats(self) -> dict:
         """Work counts of the last batch (mtb_last_stats)."""
@@ -164,10 +164,10 @@ class Classifier:
         return np.array(list(ms), np.float32)
 
     def kernel_ms(self) -> np.ndarray:
-        """[extract, k-mer sort, match join, match transpose, match sort, assign] of the last batch
-        (HIP events)."""
-        ms = (ctypes.c_float * 6)()
-        lib().mtb_last_kernel_ms(self.handle, ms, 6)
+        """[extract, filter, k-mer sort, join, match transpose, match sort, assign] of the last batch
+        (HIP events; the sort is 0 on the probe join)."""
+        ms = (ctypes.c_float * 7)()
+        lib().mtb_last_kernel_ms(self.handle, ms, 7)
         return np.array(list(ms), np.float32)
 
     def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:

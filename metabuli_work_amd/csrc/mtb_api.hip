@@ -58,11 +58,11 @@ struct mtb_ctx {
     uint64_t* dbv = nullptr;
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
-    uint32_t* aaSet = nullptr;  // AA 8-mer membership bitmap of the DB (4.7 GB)
+    ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     AADir dir{};
+    int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
-    bool assignOrder = true;     // MTB_ASSIGN_ORDER=0 launches K6 reads in batch order  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -74,8 +74,10 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mTotal, waveList, waveCount, devStats;
-    uint64_t stats[10] = {};  // mtb_last_stats
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, waveList, waveCount, devStats;
+    DevBuf qFrom, probeStats;  // probe join: DB lower bounds of the filtered queries; striped counters
+    static constexpr int kNumStats = 11;
+    uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
@@ -83,25 +85,27 @@ struct mtb_ctx {
     // last batch
     uint32_t nReads = 0;
     uint64_t Q = 0, M = 0, nTaxcnt = 0;
-    bool sortedInB = false;
+    const uint64_t* qKeys = nullptr;   // the last batch's query k-mers (sorted on the sort-merge path)
+    const uint32_t* qSlots = nullptr;
     bool keepStages = false;
+    bool probed = false;  // the last batch took the probe join
     float stageMs[5] = {0, 0, 0, 0, 0};
     hipEvent_t ev[6]{};
     // tight event pairs around the main kernels: extract, k-mer sort, match count, match emit,
     // per-read match sort, assign
-    static constexpr int kNumKern = 6;
-    float kernMs[kNumKern] = {0, 0, 0, 0, 0, 0};
+    static constexpr int kNumKern = 7;
+    float kernMs[kNumKern] = {0, 0, 0, 0, 0, 0, 0};
     hipEvent_t kev[2 * kNumKern]{};
 };
 
 static void free_db(mtb_ctx* c) {
-    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->aaSet, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->lines, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->dbv = nullptr;
     c->dbinfo = nullptr;
     c->dirMem = nullptr;
-    c->aaSet = nullptr;
+    c->lines = nullptr;
 }
 
 template <typename T>
@@ -145,14 +149,17 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     uint64_t* dIdx = nullptr;
     void* dTmp = nullptr;
     const uint64_t nDiff = db.diffIdx.size();
-    HIP_TRY(hipMalloc(&c->dbv, c->D * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->dbv, (c->D + kDbPad) * sizeof(uint64_t)));  // + ~0 pad: the probe's 8 loads need no bound
+    HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
     HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
     HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
     HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
     HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
     decode_diff_idx(dDiff, nDiff, c->dbv, c->D, dFlag, dIdx, dTmp, s);
-    HIP_TRY(upload(&c->dbinfo, db.info, s));
+    HIP_TRY(hipMalloc(&c->dbinfo, (c->D + kDbPad) * sizeof(uint32_t)));  // + pad: the emit's 8 loads need no bound
+    HIP_TRY(hipMemcpyAsync(c->dbinfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
     if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
@@ -163,10 +170,11 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
     build_aa_dir(c->dbv, c->D, c->dir, c->dirMem, s);
+    if (const char* e = getenv("MTB_JOIN")) c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : 0;
     if (!c->forceGeneric) {
-        HIP_TRY(hipMalloc(&c->aaSet, kAASetWords * sizeof(uint32_t)));
-        HIP_TRY(hipMemsetAsync(c->aaSet, 0, kAASetWords * sizeof(uint32_t), s));
-        build_aa_set(c->dbv, c->D, c->aaSet, s);
+        HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
+        HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
+        build_probe_lines(c->dbv, c->D, c->dir, c->lines, s);
     }
     HIP_TRY(hipStreamSynchronize(s));
     hipFree(dDiff);
@@ -235,7 +243,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mTotal, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -315,11 +323,11 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (maxSeg > kSegSortLds || c->forceGeneric) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
-    HIP_TRY(hipEventRecord(c->kev[8], s));
+    HIP_TRY(hipEventRecord(c->kev[10], s));
     launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
                    c->segScratch.as<uint64_t>(), maxSeg > 128, maxSeg > 512, c->forceGeneric, s);
-    HIP_TRY(hipEventRecord(c->kev[9], s));
-    HIP_TRY(hipEventRecord(c->kev[10], s));
+    HIP_TRY(hipEventRecord(c->kev[11], s));
+    HIP_TRY(hipEventRecord(c->kev[12], s));
     for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
     HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mc + 1)));
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mc + 1) + 1)));
@@ -354,7 +362,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(),
                   n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(),
                   c->devStats.as<unsigned long long>(), c->stats + 5, s);
-    HIP_TRY(hipEventRecord(c->kev[11], s));
+    HIP_TRY(hipEventRecord(c->kev[13], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
     launch_taxcnt_len(c->results.as<mtb_result>(), n, c->tcLen.as<uint32_t>(), s);
@@ -366,6 +374,128 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), c->mOff.as<uint64_t>(), c->results.as<mtb_result>(),
                           c->tcOff.as<uint64_t>(), n, c->tcOut.as<mtb_taxcnt>(), s);
     c->nTaxcnt = NT;
+    return MTB_OK;
+}
+
+// K1 -> K1F filter -> K4 join (probe join, or radix sort + sort-merge join) -> transpose into
+// per-read segments. Kernel timers: 0 extract, 1 filter, 2 sort, 3 join, 4 transpose.
+static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, const uint8_t* dSeq2,
+                      const uint64_t* dOff2, uint32_t n, uint64_t U, uint32_t C, uint64_t R, uint64_t Rc) {
+    hipStream_t s = c->stream;
+    const bool probe = c->probed;
+    HIP_TRY(c->keysA.ensure(8 * Rc));
+    HIP_TRY(c->valsA.ensure(4 * Rc));
+    HIP_TRY(c->keysB.ensure(8 * Rc));
+    HIP_TRY(c->valsB.ensure(4 * Rc));
+    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Rc)));
+    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
+    HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
+    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * kStatStripes));
+    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+    // K1 extract: every window's key (the sentinel where no k-mer is emitted)
+    HIP_TRY(hipEventRecord(c->kev[0], s));
+    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                   c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
+                   c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
+    HIP_TRY(hipEventRecord(c->kev[1], s));
+    // K1F: the windows whose AA 8-mer the DB holds (MTB_FORCE_GENERIC: no filter, the sort's first
+    // pass drops the sentinels)
+    uint64_t Q = R;
+    const uint64_t* qk = c->keysA.as<uint64_t>();
+    const uint32_t* qi = nullptr;
+    const uint64_t* qf = nullptr;
+    HIP_TRY(hipEventRecord(c->kev[2], s));
+    if (c->lines) {
+        if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
+        Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
+                          probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), s);
+        qk = c->keysB.as<uint64_t>();
+        qi = c->valsB.as<uint32_t>();
+        qf = c->qFrom.as<uint64_t>();
+    }
+    HIP_TRY(hipEventRecord(c->kev[3], s));
+    HIP_TRY(hipEventRecord(c->ev[1], s));
+    // K2 (sort-merge join only): radix sort on the top 24 bits of the 36-bit AA rank. The join does
+    // not need a total order (K5 puts each read's matches in compareMatches order); a sort prefix
+    // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
+    HIP_TRY(hipEventRecord(c->kev[4], s));
+    if (!probe) {
+        bool inB = false;
+        if (c->lines) {
+            Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
+                                 c->valsA.as<uint32_t>(), Q, kQuerySortLo, kQuerySortHi, false, false,
+                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+            qk = inB ? c->keysA.as<uint64_t>() : c->keysB.as<uint64_t>();
+            qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
+        } else {
+            Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
+                                 c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
+                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+            qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
+            qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();
+        }
+    }
+    HIP_TRY(hipEventRecord(c->kev[5], s));
+    HIP_TRY(hipEventRecord(c->ev[2], s));
+    c->Q = Q;
+    c->stats[1] = Q;
+    c->qKeys = qk;
+    c->qSlots = qi;
+    // K4 join: per-read counts and ranks, matches staged in the join's order, then moved into
+    // per-read segments by the transpose (KmerMatcher::matchKmers)
+    HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
+    c->stageRegion = std::max<uint64_t>(c->stageRegion, std::max<uint64_t>(Q / kStageRegions, 64));
+    HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+    HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
+    HIP_TRY(hipEventRecord(c->kev[6], s));
+    if (!probe) launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
+    uint64_t M = 0;
+    std::vector<unsigned long long> regTot(kStageRegions);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+        HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
+        if (probe)
+            launch_probe(qk, qi, qf, Q, c->unitInfo.as<uint64_t>(), C, c->dbv, c->dbinfo, c->D, c->spOf,
+                         (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
+                         c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
+                         c->stageRegion, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(), s);
+        else
+            launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf,
+                         (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
+                         c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
+                         c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
+                         c->probeStats.as<unsigned long long>(), s);
+        HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        M = 0;
+        uint64_t most = 0;
+        for (unsigned long long t : regTot) {
+            M += t;
+            most = std::max<uint64_t>(most, t);
+        }
+        if (most <= c->stageRegion || M >= kMaxBatchMatches) break;
+        c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
+        HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+        HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
+        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+    }
+    HIP_TRY(hipEventRecord(c->kev[7], s));
+    if (M >= kMaxBatchMatches) {
+        set_error("batch produced >= 2^32 matches: split it into smaller batches");
+        return MTB_ERR_ARG;
+    }
+    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
+    c->M = M;
+    HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
+    HIP_TRY(hipEventRecord(c->kev[8], s));
+    launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
+                           c->mTotal.as<unsigned long long>(), c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(),
+                           c->errFlag.as<int>(), s);
+    HIP_TRY(hipEventRecord(c->kev[9], s));
+    HIP_TRY(hipEventRecord(c->ev[3], s));
     return MTB_OK;
 }
 
@@ -431,91 +561,18 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->unitRead.ensure(sizeof(uint32_t) * std::max<uint64_t>(U, 1)));
     launch_unit_read(c->slotOff.as<uint64_t>(), n, c->unitRead.as<uint32_t>(), s);
     const uint64_t R = extract_slots(U, C);
-    // K1 extract
     const uint64_t Rc = std::max<uint64_t>(R, 1);
-    HIP_TRY(c->keysA.ensure(8 * Rc));
-    HIP_TRY(c->valsA.ensure(4 * Rc));
-    HIP_TRY(c->keysB.ensure(8 * Rc));
-    HIP_TRY(c->valsB.ensure(4 * Rc));
-    HIP_TRY(c->unitInfo.ensure(8 * std::max<uint64_t>(U, 1)));
     if (R >= 0xFFFFFFFFull) { set_error("batch has >= 2^32 k-mer slots: split it"); return MTB_ERR_ARG; }
     c->chunkC = C;
-    HIP_TRY(hipEventRecord(c->kev[0], s));
-    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
-                   c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
-                   c->aaSet, c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
-    HIP_TRY(hipEventRecord(c->kev[1], s));
-    HIP_TRY(hipEventRecord(c->ev[1], s));
-    // K2 radix sort on the AA part (bits 24..63); the first pass drops blank slots.
-    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Rc)));
-    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
-    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
-    bool inB = false;
-    // The index join (K4) does not need a total order: matches are put in compareMatches order per
-    // read by K5, a total order for a valid DB. Sorting on the top 24 bits of the 36-bit AA rank
-    // (resident rank form) groups queries whose AA k-mers share ~6 leading amino acids, which is
-    // all the locality the K4 windows need: three passes instead of five.
-    HIP_TRY(hipEventRecord(c->kev[2], s));
-    uint64_t Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
-                                  c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
-                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
-    HIP_TRY(hipEventRecord(c->kev[3], s));
-    c->Q = Q;
     c->stats[0] = R;
-    c->stats[1] = Q;
-    c->sortedInB = inB;
-    const uint64_t* qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
-    const uint32_t* qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();  // K1 slots
-    HIP_TRY(hipEventRecord(c->ev[2], s));
-    // K4 join: one pass selects and stages the matches in AA order, counting them per read; a
-    // transpose pass then moves them into per-read segments (KmerMatcher::matchKmers)
-    HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
-    HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->unitInfo.ensure(8 * std::max<uint64_t>(U, 1)));
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
-    HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
-    HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
-    c->stageRegion = std::max<uint64_t>(c->stageRegion, std::max<uint64_t>(Q / 4 / kStageRegions, 64));
-    HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
-    HIP_TRY(hipEventRecord(c->kev[4], s));
-    launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
-    uint64_t M = 0;
-    std::vector<unsigned long long> regTot(kStageRegions);
-    for (int attempt = 0; attempt < 2; attempt++) {
-        HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
-        HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
-        launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf,
-                     (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
-                     c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
-                     c->devStats.as<unsigned long long>(), s);
-        HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
-                               hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        M = 0;
-        uint64_t most = 0;
-        for (unsigned long long t : regTot) {
-            M += t;
-            most = std::max<uint64_t>(most, t);
-        }
-        if (most <= c->stageRegion || M >= kMaxBatchMatches) break;
-        c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
-        HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
-    }
-    HIP_TRY(hipEventRecord(c->kev[5], s));
-    if (M >= kMaxBatchMatches) {
-        set_error("batch produced >= 2^32 matches: split it into smaller batches");
-        return MTB_ERR_ARG;
-    }
-    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
-    c->M = M;
-    HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
-    HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
-    HIP_TRY(hipEventRecord(c->kev[6], s));
-    launch_match_transpose(c->mStage.as<mtb_match>(), c->stageRegion, c->mTotal.as<unsigned long long>(),
-                           c->mOff.as<uint64_t>(), n, c->readCnt.as<uint32_t>(), c->matches.as<mtb_match>(),
-                           c->errFlag.as<int>(), s);
-    HIP_TRY(hipEventRecord(c->kev[7], s));
-    HIP_TRY(hipEventRecord(c->ev[3], s));
+    HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
+    c->probed = !c->forceGeneric && c->joinMode == 2;  // the sort-merge join is the default (faster here)
+    c->stats[10] = c->probed ? 0 : 1;
+    int jrc = join_stage(c, dSeq1, dOff1, dSeq2, dOff2, n, U, C, R, Rc);
+    if (jrc != MTB_OK) return jrc;
     // K5 + K6
     int rc = assign_stage(c, n);
     if (rc != MTB_OK) return rc;
@@ -526,15 +583,25 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipMemcpyAsync(dstat, c->devStats.p, sizeof(dstat), hipMemcpyDeviceToHost, s));
     if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    c->stats[2] = dstat[0];
     c->stats[9] = dstat[1];
+    {
+        std::vector<unsigned long long> ps(kStatStripes);
+        HIP_TRY(hipMemcpy(ps.data(), c->probeStats.p, sizeof(unsigned long long) * ps.size(), hipMemcpyDeviceToHost));
+        c->stats[2] = 0;
+        for (unsigned long long x : ps) c->stats[2] += x;  // queries with >= 1 match
+    }
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     for (int k = 0; k < mtb_ctx::kNumKern; k++)
         HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
-    if (err == 2) {
-        set_error("internal error: a staged match names a read outside the batch");
+    if (err == 2 || err == 4) {
+        set_error(err == 2 ? "internal error: a staged match names a read outside the batch"
+                           : "internal error: emitted matches disagree with the probe counts");
         return MTB_ERR_INTERNAL;
+    }
+    if (err == 3) {
+        set_error("a DB AA run holds >= 2^24 k-mers (probe join stash limit): use MTB_JOIN=sort");
+        return MTB_ERR_DB;
     }
     if (err) {
         set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
@@ -573,7 +640,7 @@ const char* mtb_taxon_rank(const mtb_ctx* c, int32_t t) {
 
 int mtb_last_stats(const mtb_ctx* c, uint64_t* out, int n) {
     if (!c || !out) return MTB_ERR_ARG;
-    for (int i = 0; i < n && i < 10; i++) out[i] = c->stats[i];
+    for (int i = 0; i < n && i < mtb_ctx::kNumStats; i++) out[i] = c->stats[i];
     return MTB_OK;
 }
 
@@ -601,11 +668,13 @@ int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out
     if (!c || !n_out) return MTB_ERR_ARG;
     *n_out = c->Q;
     if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
+    if (c->probed) { set_error("the probe join keeps no sorted query k-mers (MTB_JOIN=probe)"); return MTB_ERR_ARG; }
+    if (!c->qSlots) { set_error("no query k-mers kept"); return MTB_ERR_ARG; }
     if (cap < c->Q) return MTB_RETRY;
     std::vector<uint64_t> k(c->Q), ui(c->unitInfo.bytes / 8);
     std::vector<uint32_t> v(c->Q);
-    const void* kp = c->sortedInB ? c->keysB.p : c->keysA.p;
-    const void* vp = c->sortedInB ? c->valsB.p : c->valsA.p;
+    const void* kp = c->qKeys;
+    const void* vp = c->qSlots;
     if (c->Q) {
         HIP_TRY(hipMemcpy(k.data(), kp, 8 * c->Q, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(v.data(), vp, 4 * c->Q, hipMemcpyDeviceToHost));
@@ -648,6 +717,9 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     for (uint64_t i = 0; i < nm; i++) grouped[cur[info_seq(m[i].qinfo) - 1]++] = m[i];
     if (nm >= kMaxBatchMatches) { set_error("more than 2^32 - 1 matches in one call"); return MTB_ERR_ARG; }
     c->M = nm;
+    c->Q = 0;
+    c->qKeys = nullptr;
+    c->qSlots = nullptr;
     c->nReads = n;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));

@@ -202,83 +202,78 @@ struct ExtractTables {
     int8_t num[64];
 };
 
-__global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
-                                                 const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
-                                                 const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
-                                                 const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
-                                                 ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
-                                                 const uint32_t* __restrict__ aaSet, uint64_t* __restrict__ keys,
-                                                 uint64_t* __restrict__ unitInfo) {
-    __shared__ uint8_t sBase[256];
-    __shared__ int8_t sAA[64], sNum[64];
-    sBase[threadIdx.x] = tabs.base[threadIdx.x];
-    if (threadIdx.x < 64) { sAA[threadIdx.x] = tabs.aa[threadIdx.x]; sNum[threadIdx.x] = tabs.num[threadIdx.x]; }
-    __syncthreads();
+// One K1 work unit: a chunk of <= C consecutive windows of one (read, mate, frame).
+struct UnitWindows {
+    const uint8_t* seq;
+    int s0, e0;          // covered span of the frame (first / last base)
+    int pFirst, nWin;    // first window of the chunk, windows in the chunk (0: nothing to do)
+    bool fromLeft, comp;
+    uint64_t info0;      // pack_info of the chunk's first window (window p: pos0 +- 3p, slot_info)
+};
 
-    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
-    int W = 0, pFirst = 0, nWin = 0;
-    uint32_t r = 0;
-    int mate = 0, frame = 0;
-    if (u < nUnits) {
-        r = unitRead[u];
-        const ReadMeta m0 = meta[r];
-        uint32_t local = (uint32_t)(u - uOff[r]);
-        const uint32_t c1 = (uint32_t)(m0.w1 + C - 1) / C, c2 = (uint32_t)(m0.w2 + C - 1) / C;
-        uint32_t cpf = c1;
-        if (local >= 6 * c1) { local -= 6 * c1; mate = 1; cpf = c2; }
-        frame = (int)(local / cpf);
-        const int chunk = (int)(local % cpf);
-        W = mate ? m0.w2 : m0.w1;
-        pFirst = chunk * (int)C;
-        nWin = min((int)C, W - pFirst);
-    }
-    // slots of this unit past its windows (and of padding units) hold the sentinel
-    for (int p = max(nWin, 0); p < (int)C; p++) keys[slotBase + 64ull * p] = kSentinel;
-    if (nWin <= 0) return;
+__device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits, uint32_t C,
+                                                    const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
+                                                    const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
+                                                    const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
+                                                    const uint32_t* __restrict__ unitRead, int kmerFormat) {
+    UnitWindows w{};
+    if (u >= nUnits) return w;
+    const uint32_t r = unitRead[u];
     const ReadMeta m = meta[r];
-    const uint8_t* seq = mate ? seq2 + off2[r] : seq1 + off1[r];
-    int len = mate ? m.len2 : m.len1;
-    int used = mate ? m.ql2 : m.ql1;
-    uint32_t posOffset = mate ? (uint32_t)m.ql1 + 3u : 0u;  // KmerExtractor.cpp:341-345
+    uint32_t local = (uint32_t)(u - uOff[r]);
+    const uint32_t c1 = (uint32_t)(m.w1 + C - 1) / C, c2 = (uint32_t)(m.w2 + C - 1) / C;
+    uint32_t cpf = c1;
+    int mate = 0;
+    if (local >= 6 * c1) { local -= 6 * c1; mate = 1; cpf = c2; }
+    const int frame = (int)(local / cpf);
+    const int chunk = (int)(local % cpf);
+    const int W = mate ? m.w2 : m.w1;
+    w.pFirst = chunk * (int)C;
+    w.nWin = min((int)C, W - w.pFirst);
+    if (w.nWin <= 0) return w;
+    w.seq = mate ? seq2 + off2[r] : seq1 + off1[r];
+    const int len = mate ? m.len2 : m.len1;
+    const int used = mate ? m.ql2 : m.ql1;
+    const uint32_t posOffset = mate ? (uint32_t)m.ql1 + 3u : 0u;  // KmerExtractor.cpp:341-345
     const bool fwd = frame < 3;
     int begin;
     if (fwd) begin = frame;
     else { begin = (len % 3) - (frame % 3); if (begin < 0) begin += 3; }
-    const int s0 = begin, e0 = begin + used - 1;
-    const int aaLen = used / 3;
-    const uint32_t seqId = r + 1;
+    w.s0 = begin;
+    w.e0 = begin + used - 1;
     // which end the load order starts from, and whether codons are complemented
-    const bool fromLeft = (kmerFormat == 2) ? fwd : !fwd;
-    const bool comp = !fwd;
-    const int nSm = 8 - smerLen + 1;
-    {
-        const uint32_t pos0 = fromLeft ? (uint32_t)(s0 + 3 * pFirst) : (uint32_t)(e0 - 3 * (pFirst + 8) + 1);
-        unitInfo[u] = pack_info(seqId, pos0 + posOffset, (uint32_t)frame);  // window p: pos0 +- 3p (slot_info)
-    }
+    w.fromLeft = (kmerFormat == 2) ? fwd : !fwd;
+    w.comp = !fwd;
+    const uint32_t pos0 = w.fromLeft ? (uint32_t)(w.s0 + 3 * w.pFirst) : (uint32_t)(w.e0 - 3 * (w.pFirst + 8) + 1);
+    w.info0 = pack_info(r + 1, pos0 + posOffset, (uint32_t)frame);
+    return w;
+}
 
+// The unit's windows in order: f(p, ok, key) for p = 0 .. nWin-1 (p relative to the chunk); ok
+// when the window is emitted, key = its resident rank-form key (AA rank << 24 | DNA part).
+template <typename F>
+__device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* sBase, const int8_t* sAA,
+                                          const int8_t* sNum, int syncmer, int smerLen, F&& f) {
+    const int nSm = 8 - smerLen + 1;
     uint64_t aaAcc = 0, dnaAcc = 0, smAcc = 0;
     uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
     const uint64_t smMask = (smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1);
     int run = 0;
-    (void)aaLen;
-    uint64_t pendKey = kSentinel;  // window awaiting its bitmap word
-    uint32_t pendWord = 0, pendBit = 0;
-    int pendP = -1;
-    for (int j = pFirst; j < pFirst + nWin + 7; j++) {
-        int c0 = fromLeft ? s0 + 3 * j : e0 - 3 * j;  // first base of the triplet in load order
+    const uint8_t* seq = w.seq;
+    for (int j = w.pFirst; j < w.pFirst + w.nWin + 7; j++) {
+        const int c0 = w.fromLeft ? w.s0 + 3 * j : w.e0 - 3 * j;  // first base of the triplet in load order
         uint32_t b1, b2, b3;
-        if (fromLeft) {
-            uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + 1]], z = sBase[seq[c0 + 2]];
-            if (comp) { b1 = z; b2 = y; b3 = x; } else { b1 = x; b2 = y; b3 = z; }
+        if (w.fromLeft) {
+            const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + 1]], z = sBase[seq[c0 + 2]];
+            if (w.comp) { b1 = z; b2 = y; b3 = x; } else { b1 = x; b2 = y; b3 = z; }
         } else {
-            uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 - 1]], z = sBase[seq[c0 - 2]];
-            if (comp) { b1 = x; b2 = y; b3 = z; } else { b1 = z; b2 = y; b3 = x; }
+            const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 - 1]], z = sBase[seq[c0 - 2]];
+            if (w.comp) { b1 = x; b2 = y; b3 = z; } else { b1 = z; b2 = y; b3 = x; }
         }
         int aa = -1, num = 0;
         if ((b1 | b2 | b3) < 4u) {
-            if (comp) { b1 ^= 2u; b2 ^= 2u; b3 ^= 2u; }
-            int idx = (int)(b1 << 4 | b2 << 2 | b3);
+            if (w.comp) { b1 ^= 2u; b2 ^= 2u; b3 ^= 2u; }
+            const int idx = (int)(b1 << 4 | b2 << 2 | b3);
             aa = sAA[idx];
             num = sNum[idx];
         }
@@ -293,8 +288,7 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
         if (syncmer) {
             sm7 = sm6; sm6 = sm5; sm5 = sm4; sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = sm0; sm0 = smAcc;
         }
-        if (j < pFirst + 7) continue;
-        const int p = j - 7;
+        if (j < w.pFirst + 7) continue;
         bool ok = run >= 8;
         if (ok && syncmer) {
             // s-mers of the window: positions p..p+nSm-1 end at codons j-nSm+1..j = sm[nSm-1]..sm0.
@@ -309,45 +303,70 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
             ok = (bestK == nSm - 1) || (bestK == 0);
         }
         uint64_t key = kSentinel;
-        uint32_t word = 0xFFFFFFFFu, bit = 0;
         if (ok) {
             // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
             uint64_t aaPart = 0;
 #pragma unroll
             for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
             key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
-            // an AA 8-mer absent from the DB can match nothing (matchKmers compares AA parts for
-            // equality first): it is blanked so the sort and the join never see it. The bitmap
-            // word is only consumed one window later, so the random load overlaps a window's work.
-            if (aaSet) {
-                const uint64_t b = aaPart >> kAASetShift;
-                word = aaSet[b >> 5];
-                bit = (uint32_t)(b & 31u);
-            }
         }
-        if (pendP >= 0) keys[slotBase + 64ull * pendP] = ((pendWord >> pendBit) & 1u) ? pendKey : kSentinel;
-        pendKey = key;
-        pendWord = word;
-        pendBit = bit;
-        pendP = p - pFirst;
+        f(j - 7 - w.pFirst, ok, key);
     }
-    if (pendP >= 0) keys[slotBase + 64ull * pendP] = ((pendWord >> pendBit) & 1u) ? pendKey : kSentinel;
+}
+
+__device__ __forceinline__ void load_extract_tables(const ExtractTables& tabs, uint8_t* sBase, int8_t* sAA,
+                                                    int8_t* sNum) {
+    sBase[threadIdx.x] = tabs.base[threadIdx.x];
+    if (threadIdx.x < 64) { sAA[threadIdx.x] = tabs.aa[threadIdx.x]; sNum[threadIdx.x] = tabs.num[threadIdx.x]; }
+    __syncthreads();
+}
+
+// The AA-membership word and bit of a rank in the probe lines.
+__device__ __forceinline__ const uint32_t* line_word(const ProbeLine* lines, uint64_t rank, uint32_t& bit) {
+    const uint64_t L = rank / kLineRanks;
+    const uint32_t o = (uint32_t)(rank - L * kLineRanks);
+    bit = o & 31u;
+    return &lines[L].bits[o >> 5];
+}
+
+__global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
+                                                 const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
+                                                 const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
+                                                 const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
+                                                 ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
+                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ unitInfo) {
+    __shared__ uint8_t sBase[256];
+    __shared__ int8_t sAA[64], sNum[64];
+    load_extract_tables(tabs, sBase, sAA, sNum);
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
+    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
+    // slots of this unit past its windows (and of padding units) hold the sentinel
+    for (int p = max(w.nWin, 0); p < (int)C; p++) keys[slotBase + 64ull * p] = kSentinel;
+    if (w.nWin <= 0) return;
+    unitInfo[u] = w.info0;
+    unit_scan(w, sBase, sAA, sNum, syncmer, smerLen,
+              [&](int p, bool ok, uint64_t key) { keys[slotBase + 64ull * p] = ok ? key : kSentinel; });
 }
 
 uint64_t extract_slots(uint64_t nUnits, uint32_t C) { return (nUnits + 63) / 64 * 64 * C; }
 
-void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
-                    const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
-                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, const uint32_t* aaSet,
-                    uint64_t* keys, uint64_t* unitInfo, hipStream_t s) {
+static ExtractTables extract_tables(const HostTables& t) {
     ExtractTables tabs;
     for (int i = 0; i < 256; i++) tabs.base[i] = t.base[i];
     for (int i = 0; i < 64; i++) { tabs.aa[i] = t.aa[i]; tabs.num[i] = t.num[i]; }
+    return tabs;
+}
+
+void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
+                    const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
+                    uint64_t* unitInfo, hipStream_t s) {
     if (nUnits == 0) return;
     const uint64_t threads = (nUnits + 63) / 64 * 64;  // whole waves: padding units write sentinels
     k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits,
-                                                                C, tabs, kmerFormat, syncmer, smerLen, aaSet, keys,
-                                                                unitInfo);
+                                                                C, extract_tables(t), kmerFormat, syncmer, smerLen,
+                                                                keys, unitInfo);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -615,19 +634,6 @@ void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
 
 uint64_t host_from_rank_form(uint64_t v) { return from_rank_form(v); }
 
-__global__ void k_aa_set(const uint64_t* __restrict__ dbv, uint64_t D, uint32_t* __restrict__ bits) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= D) return;
-    const uint64_t r = dbv[i] >> 24;
-    if (i > 0 && (dbv[i - 1] >> 24) == r) return;  // first k-mer of each AA run sets the bit
-    const uint64_t b = r >> kAASetShift;
-    atomicOr(&bits[b >> 5], 1u << (b & 31u));
-}
-
-void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s) {
-    if (D) k_aa_set<<<(unsigned)((D + 255) / 256), 256, 0, s>>>(dbv, D, bits);
-}
-
 __global__ void k_build_dir(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
     uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b > d.R) return;
@@ -648,6 +654,47 @@ AADir make_aa_dir(uint64_t D, int kmerFormat) {
 
 void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s) {
     k_build_dir<<<(unsigned)((d.R + 1 + 255) / 256), 256, 0, s>>>(dbv, D, d, dir);
+}
+
+// Line heads: the DB index of the first k-mer of rank >= the line's first rank (lower bound inside
+// the directory bucket of that rank); the end line holds D.
+__global__ void k_line_base(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, ProbeLine* __restrict__ lines) {
+    const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= kProbeLines) return;
+    const uint64_t r = l * kLineRanks;
+    uint64_t base = D;
+    if (r < kAARankEnd) {
+        const uint64_t b = r / d.div;
+        base = lower_bound_u64(dbv, d.dir[b], d.dir[b + 1], r << 24);
+    }
+    lines[l].base = base;
+}
+
+// Line heads as base | min(k-mers of the line, 2^24 - 1) << 40 (the probe bounds its searches
+// with the count; a saturated count sends it to the next line's head).
+__global__ void k_line_count(ProbeLine* __restrict__ lines) {
+    const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l + 1 >= kProbeLines) return;
+    // the next head may already carry its count (another thread's write): its low 40 bits do not change
+    const uint64_t b = lines[l].base, n = (lines[l + 1].base & ((1ull << 40) - 1)) - b;
+    lines[l].base = b | (min(n, (uint64_t)0xFFFFFFu) << 40);
+}
+
+// Membership bits: the first k-mer of each AA run sets its rank's bit.
+__global__ void k_line_bits(const uint64_t* __restrict__ dbv, uint64_t D, ProbeLine* __restrict__ lines) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= D) return;
+    const uint64_t r = dbv[i] >> 24;
+    if (i > 0 && (dbv[i - 1] >> 24) == r) return;
+    uint32_t bit;
+    const uint32_t* w = line_word(lines, r, bit);
+    atomicOr(const_cast<uint32_t*>(w), 1u << bit);
+}
+
+void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines, hipStream_t s) {
+    k_line_base<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(dbv, D, dir, lines);
+    k_line_count<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines);
+    if (D) k_line_bits<<<(unsigned)((D + 255) / 256), 256, 0, s>>>(dbv, D, lines);
 }
 
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
@@ -691,15 +738,23 @@ __device__ __forceinline__ uint32_t run_select(const HamRows& hr, const uint64_t
     return c;
 }
 
-__device__ __forceinline__ void run_emit(uint64_t key, const HamRows& hr, uint64_t info, const uint64_t* vals,
-                                         const uint32_t* infos, uint64_t lo, uint64_t hi, uint32_t thr,
-                                         const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                         mtb_match* __restrict__ out, uint64_t w, int* __restrict__ err) {
+// Writes the run's selected candidates at out[w..wEnd); returns the next w (a selection that
+// would pass wEnd sets err 4 and stops). outRank (nullable) gets each match's rank inside its
+// read's segment, starting at `rank`.
+__device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, uint64_t info, const uint64_t* vals,
+                                             const uint32_t* infos, uint64_t lo, uint64_t hi, uint32_t thr,
+                                             const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                             mtb_match* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
+                                             uint64_t wEnd, uint32_t rank, int* __restrict__ err) {
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
         const uint64_t tv = vals[t];
         const uint32_t hs = hamming_sum_rows(hr, tv);
         if (hs > thr) continue;
+        if (w >= wEnd) {
+            atomicExch(err, 4);
+            return w;
+        }
         const uint32_t tax = infos[t];
         const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
         if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
@@ -711,8 +766,10 @@ __device__ __forceinline__ void run_emit(uint64_t key, const HamRows& hr, uint64
         m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
         m.hamming = (uint8_t)hs;
         m.pad = 0;
+        if (outRank) outRank[w] = rank++;
         out[w++] = m;
     }
+    return w;
 }
 
 // Both ends of an AA run in an LDS window of n sorted values: lower bounds of aa and aa + 2^24 by
@@ -759,8 +816,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
-                                               mtb_match* __restrict__ buf, uint64_t region, int* __restrict__ err,
-                                               uint32_t winCap, const uint64_t* __restrict__ win,
+                                               mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
+                                               uint64_t region, int* __restrict__ err, uint32_t winCap, const uint64_t* __restrict__ win,
                                                unsigned long long* __restrict__ stats) {
     __shared__ uint64_t sDb[kMatchWin];
     __shared__ uint32_t sInfo[kMatchWin];
@@ -825,14 +882,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint64_t* vals = staged ? sDb : dbv;
     const uint32_t* infos = staged ? sInfo : dbinfo;
     const uint64_t vOff = staged ? winLo : 0;
-    uint32_t c[kPer], thr[kPer], mine = 0;
+    uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
     HamRows hr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         hr[j] = hamming_rows(key[j]);
         c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
         info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
-        if (c[j]) atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
+        // the returned count is the query's first rank inside its read's segment
+        rk[j] = c[j] ? atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]) : 0;
         mine += c[j];
     }
     int hit = 0;
@@ -851,16 +909,18 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         if (!c[j]) continue;
-        run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, w, err);
+        run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank, w,
+                 w + c[j], rk[j], err);
         w += c[j];
     }
 }
 
-// Each staged match into its read's segment; the order inside a segment is settled by K5.
-__global__ void k_match_transpose(const mtb_match* __restrict__ buf, uint64_t region,
-                                  const unsigned long long* __restrict__ total, const uint64_t* __restrict__ readOff,
-                                  uint32_t nReads, uint32_t* __restrict__ cursor, mtb_match* __restrict__ out,
-                                  int* __restrict__ err) {
+// Each staged match into its read's segment at the rank the join reserved for it (no atomics);
+// the order inside a segment is settled by K5.
+__global__ void k_match_transpose(const mtb_match* __restrict__ buf, const uint32_t* __restrict__ bufRank,
+                                  uint64_t region, const unsigned long long* __restrict__ total,
+                                  const uint64_t* __restrict__ readOff, uint32_t nReads,
+                                  mtb_match* __restrict__ out, int* __restrict__ err) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= region * kStageRegions || i % region >= total[i / region]) return;
     const mtb_match m = buf[i];
@@ -869,7 +929,230 @@ __global__ void k_match_transpose(const mtb_match* __restrict__ buf, uint64_t re
         atomicExch(err, 2);
         return;
     }
-    out[readOff[r] + atomicAdd(&cursor[r], 1u)] = m;
+    const uint64_t o = readOff[r] + bufRank[i];
+    if (o >= readOff[r + 1]) {
+        atomicExch(err, 2);
+        return;
+    }
+    out[o] = m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1F membership filter: a query k-mer whose AA 8-mer is absent from the DB can match nothing
+// (matchKmers compares AA parts for equality first), so only the present ones go on. One thread
+// per 16 slots, all 16 keys and then all 16 probe-line words in flight at once (one random 4-B
+// read per window, the pass's whole cost); each block packs its present windows and claims their
+// output stretch with one atomic. For the probe join (FROM) a present window also gets its DB
+// lower bound: the line's base plus the present ranks before it in the line (each holds >= 1
+// DB k-mer), from the rest of the same line.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t line_base(uint64_t h) { return h & ((1ull << 40) - 1); }
+
+constexpr int kFilterPer = 16;
+
+template <bool FROM>
+__global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ keys, uint64_t R,
+                                                const ProbeLine* __restrict__ lines, uint64_t* __restrict__ qkey,
+                                                uint32_t* __restrict__ qslot, uint64_t* __restrict__ qfrom,
+                                                unsigned long long* __restrict__ counter) {
+    __shared__ unsigned long long sBase;
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * kFilterPer) + threadIdx.x;
+    uint64_t k[kFilterPer];
+    uint32_t word[kFilterPer];
+#pragma unroll
+    for (int j = 0; j < kFilterPer; j++) k[j] = base + 256ull * j < R ? keys[base + 256ull * j] : kSentinel;
+#pragma unroll
+    for (int j = 0; j < kFilterPer; j++) {
+        word[j] = 0;
+        if (k[j] != kSentinel) {
+            const uint64_t x = k[j] >> 24, L = x / kLineRanks;
+            const uint32_t o = (uint32_t)(x - L * kLineRanks);
+            word[j] = (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
+        }
+    }
+    uint32_t mask = 0;
+#pragma unroll
+    for (int j = 0; j < kFilterPer; j++) mask |= word[j] << j;
+    unsigned long long tot;
+    const unsigned long long off = block_exclusive_scan((unsigned long long)__popc(mask), &tot);
+    if (threadIdx.x == 0) sBase = tot ? atomicAdd(counter, tot) : 0;
+    __syncthreads();
+    uint64_t pos = sBase + off;
+#pragma unroll
+    for (int j = 0; j < kFilterPer; j++) {
+        if (!((mask >> j) & 1u)) continue;
+        qkey[pos] = k[j];
+        qslot[pos] = (uint32_t)(base + 256ull * j);
+        if (FROM) {
+            const uint64_t x = k[j] >> 24, L = x / kLineRanks;
+            const uint32_t o = (uint32_t)(x - L * kLineRanks);
+            const uint4* lp = reinterpret_cast<const uint4*>(lines + L);
+            const uint4 q0 = lp[0], q1 = lp[1], q2 = lp[2], q3 = lp[3];
+            const uint32_t w[14] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            uint32_t before = 0;
+#pragma unroll
+            for (int i = 0; i < 14; i++) {
+                const uint32_t wi = (uint32_t)i;
+                const uint32_t m = wi < (o >> 5) ? ~0u : (wi == (o >> 5) ? ((1u << (o & 31u)) - 1u) : 0u);
+                before += __popc(w[i] & m);
+            }
+            qfrom[pos] = line_base((uint64_t)q0.x | (uint64_t)q0.y << 32) + before;
+        }
+        pos++;
+    }
+}
+
+uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
+                       uint64_t* qfrom, unsigned long long* counter, hipStream_t s) {
+    hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
+    const uint64_t blocks = (R + 256 * kFilterPer - 1) / (256 * kFilterPer);
+    if (blocks) {
+        if (qfrom) k_filter<true><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter);
+        else k_filter<false><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter);
+    }
+    unsigned long long Q = 0;
+    hipMemcpyAsync(&Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    return Q;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K4P probe join (the default): instead of sorting the present query k-mers and streaming the DB
+// past them (sort + k_match), each one reads its run directly: 8 DB values and taxIDs from its
+// lower bound (K1F), which almost always hold the whole run (longer runs: exponential + binary
+// search). One thread per query, dense. Selection, per-read counting, staging and the transpose
+// that follows are k_match's, so the matches are identical.
+// ------------------------------------------------------------------------------------------------
+// First index >= lo with a[i] >= key (an answer exists below D + kDbPad: the pad is ~0).
+__device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key) {
+    uint64_t step = 8, hi = lo;
+    while (a[hi] < key) {
+        lo = hi + 1;
+        hi += step;
+        step *= 2;
+    }
+    return lower_bound_u64(a, lo, hi, key);
+}
+
+__global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
+                                               const uint64_t* __restrict__ qfrom, uint64_t Q,
+                                               const uint64_t* __restrict__ unitInfo, uint32_t C,
+                                               const uint64_t* __restrict__ dbv, const uint32_t* __restrict__ dbinfo,
+                                               uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
+                                               int kmerFormat, uint32_t* __restrict__ readCnt,
+                                               unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
+                                               uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
+                                               unsigned long long* __restrict__ stats) {
+    __shared__ unsigned long long sBase;
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = q < Q;
+    const uint64_t key = live ? qkey[q] : 0, from = live ? qfrom[q] : 0;
+    const uint32_t slot = live ? qslot[q] : 0;
+    uint64_t v[8];
+    uint32_t tax[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        v[k] = dbv[from + k];
+        tax[k] = dbinfo[from + k];
+    }
+    const uint64_t x = key >> 24;
+    uint32_t below = 0, in = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        below += (v[k] >> 24) < x;
+        in += (v[k] >> 24) == x;
+    }
+    const HamRows hr = hamming_rows(key);
+    const bool inReg = below + in < 8 || from + 8 >= D;
+    uint64_t lo, hi;
+    uint32_t thr = 0, c = 0;
+    uint32_t sums[8];
+    if (inReg) {
+        lo = from + below;
+        hi = min(lo + in, D - 1);  // the last DB k-mer is never a candidate (run_select)
+        uint32_t minSum = 255;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const bool in_run = from + k >= lo && from + k < hi;
+            sums[k] = in_run ? hamming_sum_rows(hr, v[k]) : 255u;
+            minSum = min(minSum, sums[k]);
+        }
+        thr = min(minSum * 2u, 7u);
+#pragma unroll
+        for (int k = 0; k < 8; k++) c += sums[k] <= thr;
+    } else {
+        lo = below < 8 ? from + below : gallop_lower(dbv, from + 8, x << 24);
+        hi = gallop_lower(dbv, max(lo, from + 8), (x + 1) << 24);
+        c = run_select(hr, dbv, 0, lo, hi, D, thr);
+    }
+    if (!live) c = 0;
+    const uint64_t info = c ? slot_info(slot, C, unitInfo, kmerFormat) : 0;
+    // The query's first rank inside its read's segment. Queries arrive in K1 slot order, so a
+    // wave's queries come from a few reads: one atomic per (wave, read) with the group's sum,
+    // the lanes' ranks from a scan inside the group (per-query atomics would queue on one address).
+    uint32_t rk = 0;
+    {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t r = c ? info_seq(info) - 1 : 0xFFFFFFFFu;
+        unsigned long long todo = __ballot(c != 0);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t r0 = __shfl(r, leader);
+            const unsigned long long grp = __ballot(r == r0);
+            const uint32_t mine = r == r0 ? c : 0u;
+            const uint32_t pre = (uint32_t)wave_inclusive_scan(mine) - mine;
+            const uint32_t sum = __shfl(pre + mine, 63);
+            uint32_t b = 0;
+            if (lane == leader) b = atomicAdd(&readCnt[r0], sum);
+            b = __shfl(b, leader);
+            if (r == r0) rk = b + pre;
+            todo &= ~grp;
+        }
+    }
+    const int blockHits = __syncthreads_count(c != 0);
+    if (threadIdx.x == 0 && blockHits)
+        atomicAdd(&stats[blockIdx.x % kStatStripes], (unsigned long long)blockHits);  // matched queries
+    unsigned long long blockTot;
+    uint64_t w = block_exclusive_scan(c, &blockTot);
+    const uint32_t reg = blockIdx.x % kStageRegions;
+    if (threadIdx.x == 0) sBase = blockTot ? atomicAdd(&total[reg], blockTot) : 0;
+    __syncthreads();
+    const uint64_t base = sBase;
+    if (base + blockTot > region || !c) return;  // region too small: the caller grows it and reruns
+    w += base + (uint64_t)reg * region;
+    if (!inReg) {
+        run_emit(key, hr, info, dbv, dbinfo, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
+        return;
+    }
+    const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
+    uint32_t rank = rk;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (sums[k] > thr) continue;
+        const uint32_t t = tax[k];
+        const int32_t sp = t <= maxTax ? spOf[t] : 0;
+        if (t == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
+        mtb_match m;
+        m.qinfo = info;
+        m.target_id = t;
+        m.species_id = (uint32_t)sp;
+        m.dna_encoding = (uint32_t)(v[k] & 0xFFFFFFull);
+        m.right_end_hamming = (uint16_t)hammings_rows(hr, key, v[k], rev);
+        m.hamming = (uint8_t)sums[k];
+        m.pad = 0;
+        bufRank[w] = rank++;
+        buf[w++] = m;
+    }
+}
+
+void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
+                  const uint64_t* unitInfo, uint32_t C, const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D,
+                  const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
+                  mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
+                  hipStream_t s) {
+    if (Q == 0 || D < 2) return;
+    k_probe<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, qslot, qfrom, Q, unitInfo, C, dbv, dbinfo, D, spOf, maxTax,
+                                                        kmerFormat, readCnt, total, buf, bufRank, region, err, stats);
 }
 
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
@@ -884,22 +1167,22 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
-                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, unsigned long long* stats,
-                  hipStream_t s) {
+                  uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
+                  unsigned long long* stats, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     k_match<<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt,
-                                   total, buf, region, err, winCap, win, stats);
+                                   total, buf, bufRank, region, err, winCap, win, stats);
 }
 
-void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
-                            const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
-                            hipStream_t s) {
+void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,
+                            const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
+                            int* err, hipStream_t s) {
     const uint64_t slots = region * kStageRegions;
     if (slots)
-        k_match_transpose<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(buf, region, total, readOff, nReads, cursor,
-                                                                          out, err);
+        k_match_transpose<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(buf, bufRank, region, total, readOff,
+                                                                          nReads, out, err);
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {

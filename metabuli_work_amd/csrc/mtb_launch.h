@@ -67,9 +67,8 @@ uint64_t extract_slots(uint64_t nUnits, uint32_t C);
 // K1 over nUnits chunks of <= C windows; writes extract_slots(nUnits, C) slots
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
-                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, const uint32_t* aaSet,
-                    uint64_t* keys, uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit
-                    // (slot_info); aaSet (nullable): windows whose AA 8-mer the DB lacks are blanked
+                    uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
+                    uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
 
 uint64_t radix_counts_elems(uint64_t n);
 // V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read)
@@ -82,10 +81,6 @@ void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
 uint64_t host_from_rank_form(uint64_t v);
 // AA 8-mers: base-21 ranks 0 .. 21^8 - 1
 constexpr uint64_t kAARankEnd = 37822859361ull;
-// AA membership bitmap of the DB: bit b = r >> kAASetShift is set if some DB k-mer has AA rank r
-constexpr int kAASetShift = 0;
-constexpr uint64_t kAASetWords = ((kAARankEnd >> kAASetShift) + 32) / 32;
-void build_aa_set(const uint64_t* dbv, uint64_t D, uint32_t* bits, hipStream_t s);  // bits zeroed by caller
 // query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
 
@@ -105,6 +100,34 @@ struct AADir {
 AADir make_aa_dir(uint64_t D, int kmerFormat);
 void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s);
 
+// DB probe lines: the AA membership bitmap of the DB (bit r set iff some DB k-mer has AA rank r)
+// cut into 64-B lines of kLineRanks ranks, each headed by the DB index of the first k-mer whose
+// rank is >= the line's first rank. One random 64-B read answers "does the DB hold this AA
+// 8-mer" and, when it does, names a DB index a few runs before the 8-mer's run.
+constexpr uint32_t kLineRanks = 448;
+struct alignas(64) ProbeLine {
+    uint64_t base;
+    uint32_t bits[kLineRanks / 32];
+};
+static_assert(sizeof(ProbeLine) == 64, "one probe line per 64-B segment");
+constexpr uint32_t kStatStripes = 256;
+constexpr uint64_t kDbPad = 8;  // ~0 values after the resident DB
+constexpr uint64_t kProbeLines = (kAARankEnd + kLineRanks - 1) / kLineRanks + 1;  // + an end line (base D)
+void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines,
+                       hipStream_t s);  // lines zeroed by the caller
+
+// K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
+// qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count.
+uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
+                       uint64_t* qfrom, unsigned long long* counter, hipStream_t s);
+// K4P probe join over the filtered queries: same outputs as launch_match (per-read counts and
+// ranks, staged matches); stats: kStatStripes counters of queries with >= 1 match.
+void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
+                  const uint64_t* unitInfo, uint32_t C, const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D,
+                  const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
+                  mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
+                  hipStream_t s);
+
 // K4 join: per-read counts into readCnt; matches staged in buf = kStageRegions regions of
 // `region` slots, total[k] = matches claimed in region k (all written iff every total[k] <= region).
 // winCap: max DB values staged in LDS per block.
@@ -113,12 +136,13 @@ constexpr uint32_t kStageRegions = 256;
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
-                  uint64_t region, int* err, uint32_t winCap, const uint64_t* win, unsigned long long* stats,
+                  uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
+                  unsigned long long* stats,
                   hipStream_t s);  // stats[0] += queries with >= 1 match
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
-void launch_match_transpose(const mtb_match* buf, uint64_t region, const unsigned long long* total,
-                            const uint64_t* readOff, uint32_t nReads, uint32_t* cursor, mtb_match* out, int* err,
-                            hipStream_t s);
+void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,
+                            const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
+                            int* err, hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);

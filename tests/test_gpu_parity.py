@@ -174,3 +174,34 @@ def test_general_paths(make_db, db_name, monkeypatch):
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
         compare_results(br.results, br.taxcnt, ores, otc)
     odb.close()
+
+
+@pytest.mark.parametrize("db_name,kind", [
+    ("fmt2", "paired"), ("fmt2", "long"), ("fmt2_syncmer", "paired"), ("fmt2_syncmer", "long"),
+    ("fmt1", "paired"), ("fmt1", "single"),
+])
+@pytest.mark.parametrize("join", ["probe", "sort"])
+def test_join_paths(make_db, db_name, kind, join, monkeypatch):
+    """Both joins — the probe join (read order, probe lines + DB runs, no query sort) and the
+    sort-merge join (radix-sorted queries against LDS windows of the DB) — give the oracle's
+    query k-mer count, matches (after K5, in compareMatches order) and classifications."""
+    monkeypatch.setenv("MTB_JOIN", join)
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    reads = _reads(gen, kind, 1200 if kind != "long" else 60, seed=77)
+    opar = par.to_c()
+    odb = oc.OracleDb(db_dir)
+    okmers, ql1, ql2 = oc.extract(opar, reads)
+    omatches = oc.match(odb, opar, okmers)
+    ores, otc = oc.assign(odb, opar, omatches, ql1, ql2)
+    ok = okmers[info_seq(okmers["info"]) != 0]
+    ok = ok[np.isin(_aa_rank(ok["value"], par.kmerFormat), _db_aa_ranks(db_dir, par.kmerFormat))]
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
+        assert clf.stats()["join_path"] == (0 if join == "probe" else 1)
+        assert br.query_kmers == len(ok)
+        gm = clf.matches()
+        assert len(gm) == len(omatches) == br.matches
+        assert np.array_equal(gm, omatches)
+        compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
