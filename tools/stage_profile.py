@@ -1,10 +1,11 @@
 """Per-stage GPU time and HBM traffic of one classify step, from rocprofv3 output.
 
 Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by their order
-within a step: a step starts at k_read_meta; extract = k_extract; kmer_sort = everything from
-there to k_match_windows; match_join = k_match_windows + k_match (+ a rerun if the staging
-buffer grew); match_transpose = k_match_transpose; match_sort = k_segsort_*; assign = the rest
-of the step (K6 kernels, scans and taxcnt compaction). 
+within a step: a step starts at k_read_meta; extract = up to and including k_extract; filter =
+k_filter; kmer_sort = everything from there to the join; match_join = k_match_windows + k_match
+(probe_join = k_probe on MTB_JOIN=probe), with the per-read count scan and a rerun if the staging
+buffer grew; match_transpose = k_match_transpose; match_sort = k_segsort_*; assign = the rest of
+the step (K6 kernels, scans and taxcnt compaction).
 
 Usage:
   python tools/stage_profile.py time  <run_kernel_trace.csv> <step index>
@@ -18,7 +19,7 @@ import csv
 import json
 import sys
 
-STAGES = ["extract", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
+STAGES = ["extract", "filter", "kmer_sort", "match_join", "probe_join", "match_transpose", "match_sort", "assign"]
 
 
 def short(name):
@@ -38,15 +39,19 @@ def stage_of(seq):
             stage, after_extract = "extract", False
         elif k.startswith("k_extract"):
             stage, after_extract = "extract", True
+        elif k.startswith("k_filter"):
+            stage = "filter"
         elif k.startswith("k_match_windows") or k.startswith("k_match<") or k == "k_match":
             stage = "match_join"
+        elif k == "k_probe" or k.startswith("k_probe<"):
+            stage = "probe_join"
         elif k.startswith("k_match_transpose"):
             stage = "match_transpose"
         elif k.startswith("k_segsort") or k.startswith("k_max_seg"):
             stage = "match_sort"
         elif stage == "match_sort":
             stage = "assign"
-        elif stage == "extract" and after_extract:
+        elif (stage == "extract" and after_extract) or stage == "filter":
             stage = "kmer_sort"
         out.append(stage)
         if k.startswith("k_compact_taxcnt"):
