@@ -703,7 +703,7 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
 // DB values (few queries against a large DB, or a very frequent AA k-mer) searches HBM through the
 // directory instead.
 constexpr int kMatchQ = 256;
-constexpr int kMatchWin = 4096;
+constexpr int kMatchWin = 3072;
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
 __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
