@@ -40,6 +40,8 @@ extern "C" {
 /* Flags for mtb_classify_batch. */
 #define MTB_INPUT_DEVICE 1u    /* seq/off pointers are device (HBM) pointers */
 #define MTB_KEEP_STAGES 2u     /* keep sorted query k-mers and sorted matches for mtb_get_* */
+#define MTB_MATCH_ONLY 4u      /* stop after the join: per-read match segments for mtb_copy_matches
+                                  (range-partitioned DB); no results of its own */
 
 /*
  * Parameters of the path. Mirrors the LocalParameters fields the path reads
@@ -62,7 +64,9 @@ typedef struct mtb_params {
     int32_t em;               /* must be 0: EM reassignment is out of scope                    */
     int32_t threads;          /* host threads (oracle / host parsing only)                     */
     int32_t mask_mode;        /* must be 0: tantan masking is out of scope                     */
-    int32_t reserved[3];
+    int32_t db_part;          /* range-partitioned DB: this context holds part db_part of      */
+    int32_t db_parts;         /* db_parts AA-aligned k-mer ranges (0 or 1 = the whole DB)      */
+    int32_t reserved[1];
 } mtb_params;
 
 /* Query k-mer: 16 B, same layout as Kmer{uint64 value; QueryKmerInfo} (Kmer.h:11-31,45-46).
@@ -175,6 +179,32 @@ int mtb_get_matches(mtb_ctx* ctx, mtb_match* out, uint64_t capacity, uint64_t* n
  * of read i (seqID i+1). */
 int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches,
                        const uint32_t* query_len, uint32_t n_reads, mtb_result* results);
+
+/* ---- range-partitioned DB across GPUs ---------------------------- */
+/* A DB larger than one GPU's HBM is cut at split entries (DiffIdxSplit, Kmer.h:111-119; written
+ * AA-group aligned by IndexCreator.cpp:843-851, read by KmerMatcher.cpp:180-192,255-271) into
+ * n_parts ranges of about equal k-mer count; a context opened with par->db_part/db_parts holds one
+ * range. Every rank extracts the whole batch, its membership filter keeps the k-mers of its range
+ * (an AA run never straddles two ranges), MTB_MATCH_ONLY stops after the join, the matches go
+ * all-to-all to the rank owning their read, and mtb_assign_chunks scores them there.
+ *
+ * kmer_start[p] = first global k-mer index of part p (p = 0..n_parts; kmer_start[n_parts] = n_kmers)
+ * and split_index[p] = the split entry it starts at. Host only (no device). MTB_ERR_DB when the
+ * split table has fewer usable entries than parts. */
+int mtb_partition_bounds(const uint64_t* split, uint64_t n_split, uint64_t n_kmers, int n_parts,
+                         uint64_t* kmer_start, uint64_t* split_index);
+/* After mtb_classify_batch(..., MTB_MATCH_ONLY): the batch's matches grouped by read (read order,
+ * unsorted within a read), the per-read match counts and query lengths (queryLength +
+ * queryLength2). Any pointer may be NULL; device pointers if dst_on_device. */
+int mtb_copy_matches(mtb_ctx* ctx, mtb_match* matches, uint32_t* read_counts, uint32_t* query_len,
+                     int dst_on_device);
+/* K5 + K6 on n_chunks concatenated chunks of matches, chunk c holding the matches of reads
+ * 0..n_reads-1 grouped by read with counts chunk_counts[c * n_reads + i] (the all-to-all receive
+ * layout). With MTB_INPUT_DEVICE, matches / chunk_counts / query_len are device pointers.
+ * results: host array or NULL (mtb_device_results / mtb_copy_results). */
+int mtb_assign_chunks(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches, const uint32_t* chunk_counts,
+                      uint32_t n_chunks, const uint32_t* query_len, uint32_t n_reads, uint32_t flags,
+                      mtb_result* results);
 
 /* ---- reference-DB builder (IndexCreator analogue) ----------------------------- */
 /* Genomes + gene blocks -> diffIdx / info / split / taxID_list in the reference's on-disk format

@@ -21,7 +21,9 @@ class MtbParams(ctypes.Structure):
         ("em", ctypes.c_int32),
         ("threads", ctypes.c_int32),
         ("mask_mode", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 3),
+        ("db_part", ctypes.c_int32),
+        ("db_parts", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 1),
     ]
 
 
@@ -50,7 +52,7 @@ assert KMER_DTYPE.itemsize == 16 and MATCH_DTYPE.itemsize == 24
 assert RESULT_DTYPE.itemsize == 32 and TAXCNT_DTYPE.itemsize == 8
 
 MTB_OK, MTB_RETRY = 0, 1
-MTB_INPUT_DEVICE, MTB_KEEP_STAGES = 1, 2
+MTB_INPUT_DEVICE, MTB_KEEP_STAGES, MTB_MATCH_ONLY = 1, 2, 4
 
 
 def default_params(**kw) -> MtbParams:

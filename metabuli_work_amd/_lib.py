@@ -19,7 +19,8 @@ EXPORTED = [
     "mtb_set_stream", "mtb_db_kmers", "mtb_classify_batch", "mtb_get_taxcnt", "mtb_device_results",
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
-    "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications",
+    "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
+    "mtb_assign_chunks",
 ]
 
 
@@ -58,6 +59,9 @@ def lib() -> ctypes.CDLL:
     L.mtb_get_query_kmers.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_get_matches.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_assign_matches.argtypes = [vp, vp, u64, vp, u32, vp]
+    L.mtb_partition_bounds.argtypes = [vp, u64, u64, i32, vp, vp]
+    L.mtb_copy_matches.argtypes = [vp, vp, vp, vp, i32]
+    L.mtb_assign_chunks.argtypes = [vp, vp, u64, vp, u32, vp, u32, u32, vp]
     L.mtb_reader_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(vp)]
     L.mtb_reader_next.argtypes = [vp, u32, u64, P(MtbReadBatch)]
     L.mtb_reader_close.argtypes = [vp]

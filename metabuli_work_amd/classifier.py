@@ -86,19 +86,24 @@ class Classifier:
     """GPU-resident classifier; one instance per device (mirrors Classifier.cpp:6-32)."""
 
     def __init__(self, par: LocalParameters, db_dir: Optional[str] = None, device: int = 0,
-                 db_host: Optional[_abi.MtbDbHost] = None):
+                 db_host: Optional[_abi.MtbDbHost] = None, db_part: Tuple[int, int] = (0, 1)):
+        """db_part = (part, parts): hold one AA-aligned k-mer range of a range-partitioned DB
+        (see dist.classify_partitioned)."""
         self.par = par
         self.device = device
+        self.db_part = db_part
         self.handle = ctypes.c_void_p()
-        if db_host is not None:
-            check(lib().mtb_open_host(ctypes.byref(db_host), ctypes.byref(par.to_c()), device,
-                                      ctypes.byref(self.handle)), "mtb_open_host")
-        else:
-            if db_dir is None:
-                db_dir = par.filenames[1 + (par.seqMode == 2)]
+        if db_host is None and db_dir is None:
+            db_dir = par.filenames[1 + (par.seqMode == 2)]
+        if db_dir is not None:
             par.load_db_parameters(db_dir)
-            check(lib().mtb_open(db_dir.encode(), ctypes.byref(par.to_c()), device, ctypes.byref(self.handle)),
-                  "mtb_open")
+        cp = par.to_c()
+        cp.db_part, cp.db_parts = int(db_part[0]), int(db_part[1])
+        if db_host is not None:
+            check(lib().mtb_open_host(ctypes.byref(db_host), ctypes.byref(cp), device, ctypes.byref(self.handle)),
+                  "mtb_open_host")
+        else:
+            check(lib().mtb_open(db_dir.encode(), ctypes.byref(cp), device, ctypes.byref(self.handle)), "mtb_open")
 
     def close(self) -> None:
         if self.handle:
@@ -120,9 +125,15 @@ class Classifier:
 
     # -- one QuerySplit --------------------------------------------------------------------------
     def classify_batch(self, seq1: np.ndarray, off1: np.ndarray, seq2=None, off2=None, keep_stages: bool = False,
-                       device_input: bool = False, fetch: bool = True) -> Optional[BatchResult]:
+                       device_input: bool = False, fetch: bool = True, match_only: bool = False
+                       ) -> Optional[BatchResult]:
+        """match_only: stop after the join (MTB_MATCH_ONLY); fetch the per-read match segments with
+        copy_matches and score them where the reads are owned (assign_chunks)."""
         n = (len(off1) - 1) if not device_input else int(off1.numel()) - 1
         flags = (_abi.MTB_KEEP_STAGES if keep_stages else 0) | (_abi.MTB_INPUT_DEVICE if device_input else 0)
+        if match_only:
+            flags |= _abi.MTB_MATCH_ONLY
+            fetch = False
         if device_input:
             ptrs = [ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
                     for t in (seq1, off1, seq2, off2)]
@@ -194,6 +205,38 @@ class Classifier:
         check(lib().mtb_assign_matches(self.handle, ptr(matches), len(matches), ptr(ql), len(ql), ptr(res)),
               "mtb_assign_matches")
         return BatchResult(res, self.taxcnt(), 0, len(matches), self.stage_ms())
+
+    # -- range-partitioned DB ------------------------------------------------------
+    def copy_matches(self, matches=None, read_counts=None, query_len=None) -> None:
+        """After classify_batch(match_only=True): per-read match segments, per-read counts and query
+        lengths into numpy arrays or device tensors (all of one kind)."""
+        arrs = [a for a in (matches, read_counts, query_len) if a is not None]
+        on_dev = bool(arrs) and not isinstance(arrs[0], np.ndarray)
+
+        def p(a):
+            if a is None:
+                return ctypes.c_void_p(0)
+            return ctypes.c_void_p(a.data_ptr()) if on_dev else ptr(a)
+        check(lib().mtb_copy_matches(self.handle, p(matches), p(read_counts), p(query_len), int(on_dev)),
+              "mtb_copy_matches")
+
+    def assign_chunks(self, matches, n_matches: int, chunk_counts, n_chunks: int, query_len, n_reads: int,
+                      fetch: bool = True) -> Optional[BatchResult]:
+        """K5 + K6 on the all-to-all receive layout: n_chunks chunks, each grouped by read, with
+        counts chunk_counts[c * n_reads + i]. numpy arrays (host) or device tensors."""
+        on_dev = not isinstance(matches, np.ndarray)
+        if on_dev:
+            ps = [ctypes.c_void_p(t.data_ptr()) for t in (matches, chunk_counts, query_len)]
+        else:
+            self._keep = tuple(np.ascontiguousarray(a) for a in (matches, chunk_counts, query_len))
+            ps = [ptr(a) for a in self._keep]
+        res = np.zeros(n_reads, RESULT_DTYPE) if fetch else None
+        check(lib().mtb_assign_chunks(self.handle, ps[0], n_matches, ps[1], n_chunks, ps[2], n_reads,
+                                      _abi.MTB_INPUT_DEVICE if on_dev else 0,
+                                      ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_assign_chunks")
+        if not fetch:
+            return None
+        return BatchResult(res, self.taxcnt(), 0, n_matches, self.stage_ms())
 
     # -- Classifier::startClassify over files ----------------------------------------------------
     def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000) -> int:

@@ -75,7 +75,8 @@ struct mtb_ctx {
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
     DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, waveList, waveCount, devStats;
-    DevBuf qFrom, probeStats;  // probe join: DB lower bounds of the filtered queries; striped counters
+    DevBuf qFrom, probeStats;
+    DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging  // probe join: DB lower bounds of the filtered queries; striped counters
     static constexpr int kNumStats = 11;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
@@ -89,6 +90,7 @@ struct mtb_ctx {
     const uint32_t* qSlots = nullptr;
     bool keepStages = false;
     bool probed = false;  // the last batch took the probe join
+    bool matchOnly = false;  // the last batch stopped after the join (MTB_MATCH_ONLY)
     float stageMs[5] = {0, 0, 0, 0, 0};
     hipEvent_t ev[6]{};
     // tight event pairs around the main kernels: extract, k-mer sort, match count, match emit,
@@ -132,6 +134,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (rc != MTB_OK) return rc;
     if (!check_db(db)) return MTB_ERR_DB;
     if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
+    if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
     mtb_ctx* c = new mtb_ctx();
     c->device = device;
     c->par = *par;
@@ -243,7 +246,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -573,15 +576,21 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     c->stats[10] = c->probed ? 0 : 1;
     int jrc = join_stage(c, dSeq1, dOff1, dSeq2, dOff2, n, U, C, R, Rc);
     if (jrc != MTB_OK) return jrc;
-    // K5 + K6
-    int rc = assign_stage(c, n);
-    if (rc != MTB_OK) return rc;
+    c->matchOnly = (flags & MTB_MATCH_ONLY) != 0;
+    if (c->matchOnly) {  // range-partitioned DB: the read owner sorts and scores (mtb_assign_chunks)
+        for (int k = 10; k < 14; k++) HIP_TRY(hipEventRecord(c->kev[k], s));
+        c->nTaxcnt = 0;
+    } else {  // K5 + K6
+        int rc = assign_stage(c, n);
+        if (rc != MTB_OK) return rc;
+    }
     HIP_TRY(hipEventRecord(c->ev[4], s));
     int err = 0;
     unsigned long long dstat[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(dstat, c->devStats.p, sizeof(dstat), hipMemcpyDeviceToHost, s));
-    if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
+    if (results && !c->matchOnly)
+        HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     c->stats[9] = dstat[1];
     {
@@ -684,6 +693,74 @@ int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out
     for (uint64_t i = 0; i < c->Q; i++)
         out[i] = mtb_kmer{packed ? host_from_rank_form(k[i]) : k[i], slot_info(v[i], c->chunkC, ui.data(),
                                                                                c->par.kmer_format)};
+    return MTB_OK;
+}
+
+int mtb_copy_matches(mtb_ctx* c, mtb_match* matches, uint32_t* read_counts, uint32_t* query_len, int dst_on_device) {
+    if (!c) return MTB_ERR_ARG;
+    if (!c->matchOnly) { set_error("batch was not run with MTB_MATCH_ONLY"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    const hipMemcpyKind k = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (matches && c->M) HIP_TRY(hipMemcpyAsync(matches, c->matches.p, sizeof(mtb_match) * c->M, k, c->stream));
+    if (read_counts && c->nReads)
+        HIP_TRY(hipMemcpyAsync(read_counts, c->readCnt.p, sizeof(uint32_t) * c->nReads, k, c->stream));
+    if (query_len && c->nReads)
+        HIP_TRY(hipMemcpyAsync(query_len, c->qlen.p, sizeof(uint32_t) * c->nReads, k, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MTB_OK;
+}
+
+int mtb_assign_chunks(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_t* cnt, uint32_t nChunks,
+                      const uint32_t* qlen, uint32_t n, uint32_t flags, mtb_result* results) {
+    if (!c || (!m && nm) || (!cnt && n && nChunks) || !qlen) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (nm >= kMaxBatchMatches) { set_error("more than 2^32 - 1 matches in one call"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const bool dev = (flags & MTB_INPUT_DEVICE) != 0;
+    const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const uint64_t nc = (uint64_t)nChunks * n;
+    for (uint64_t& x : c->stats) x = 0;
+    HIP_TRY(c->devStats.ensure(sizeof(unsigned long long) * 4));
+    HIP_TRY(hipMemsetAsync(c->devStats.p, 0, sizeof(unsigned long long) * 4, s));
+    HIP_TRY(hipEventRecord(c->ev[0], s));
+    for (int e = 1; e < 4; e++) HIP_TRY(hipEventRecord(c->ev[e], s));
+    const mtb_match* dm = m;
+    const uint32_t* dc = cnt;
+    if (!dev) {
+        HIP_TRY(c->chunkIn.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
+        HIP_TRY(c->chunkCnt.ensure(sizeof(uint32_t) * std::max<uint64_t>(nc, 1)));
+        if (nm) HIP_TRY(hipMemcpyAsync(c->chunkIn.p, m, sizeof(mtb_match) * nm, k, s));
+        if (nc) HIP_TRY(hipMemcpyAsync(c->chunkCnt.p, cnt, sizeof(uint32_t) * nc, k, s));
+        dm = c->chunkIn.as<mtb_match>();
+        dc = c->chunkCnt.as<uint32_t>();
+    }
+    HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
+    HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->chunkSrcOff.ensure(sizeof(uint64_t) * (nc + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(nc + n + 1)));
+    if (n) HIP_TRY(hipMemcpyAsync(c->qlen.p, qlen, sizeof(uint32_t) * n, k, s));
+    launch_regroup_chunks(dm, dc, nChunks, n, c->readCnt.as<uint32_t>(), c->chunkSrcOff.as<uint64_t>(),
+                          c->mOff.as<uint64_t>(), c->scanTmp.p, c->matches.as<mtb_match>(), s);
+    uint64_t total = 0;  // the chunks' counts must add up to the matches handed over
+    if (n) HIP_TRY(hipMemcpyAsync(&total, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (total != nm) { set_error("chunk counts do not add up to n_matches"); return MTB_ERR_ARG; }
+    c->M = nm;
+    c->Q = 0;
+    c->qKeys = nullptr;
+    c->qSlots = nullptr;
+    c->nReads = n;
+    c->matchOnly = false;
+    int rc = assign_stage(c, n);
+    if (rc != MTB_OK) return rc;
+    HIP_TRY(hipEventRecord(c->ev[4], s));
+    if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int e = 0; e < 4; e++) HIP_TRY(hipEventElapsedTime(&c->stageMs[e], c->ev[e], c->ev[e + 1]));
+    HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
+    c->keepStages = true;
     return MTB_OK;
 }
 

@@ -1099,4 +1099,41 @@ void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_res
     if (nReads) k_compact_taxcnt<<<(nReads + 255) / 256, 256, 0, s>>>(pool, mOff, results, tcOff, nReads, out);
 }
 
+// ---- all-to-all receive layout -> per-read segments (range-partitioned DB) ---------
+// The owner of reads [0, n) receives one chunk per DB part, each grouped by read. Per-read totals
+// (then scanned into mOff) and, per (chunk, read) piece, a wave copies it to its read's segment at
+// the running offset of the chunks before it. srcOff = exclusive scan of the chunk-major counts.
+__global__ void k_chunk_totals(const uint32_t* __restrict__ cnt, uint32_t nChunks, uint32_t n,
+                               uint32_t* __restrict__ tot) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    uint32_t t = 0;
+    for (uint32_t c = 0; c < nChunks; c++) t += cnt[(uint64_t)c * n + r];
+    tot[r] = t;
+}
+
+__global__ void __launch_bounds__(256) k_regroup_chunks(const uint64_t* __restrict__ src, const uint32_t* __restrict__ cnt,
+                                                        const uint64_t* __restrict__ srcOff, uint32_t nChunks, uint32_t n,
+                                                        const uint64_t* __restrict__ mOff, uint64_t* __restrict__ dst) {
+    const uint32_t r = blockIdx.x * 4 + threadIdx.x / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (r >= n) return;
+    uint64_t at = mOff[r] * 3;  // 24-B records as 3 words
+    for (uint32_t c = 0; c < nChunks; c++) {
+        const uint64_t k = (uint64_t)c * n + r;
+        const uint64_t words = (uint64_t)cnt[k] * 3, from = srcOff[k] * 3;
+        for (uint64_t w = lane; w < words; w += 64) dst[at + w] = src[from + w];
+        at += words;
+    }
+}
+
+void launch_regroup_chunks(const mtb_match* src, const uint32_t* cnt, uint32_t nChunks, uint32_t n, uint32_t* tot,
+                           uint64_t* srcOff, uint64_t* mOff, void* scanTmp, mtb_match* dst, hipStream_t s) {
+    if (!n) return;
+    k_chunk_totals<<<(n + 255) / 256, 256, 0, s>>>(cnt, nChunks, n, tot);
+    exclusive_scan_u32(tot, n, mOff, scanTmp, s);
+    exclusive_scan_u32(cnt, (uint64_t)nChunks * n, srcOff, scanTmp, s);
+    k_regroup_chunks<<<(n + 3) / 4, 256, 0, s>>>((const uint64_t*)src, cnt, srcOff, nChunks, n, mOff, (uint64_t*)dst);
+}
+
 }  // namespace mtb

@@ -5,6 +5,9 @@
 // MMseqs2 NcbiTaxonomy services those use (LCA / IsAncestor / findRankIndex / loadMerged).
 #include "mtb_host.h"
 
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -256,6 +259,90 @@ bool check_db(const HostDb& db) {
     return true;
 }
 
+// ---- range partition of the DB at split entries -------------------------
+// Split entry j (j >= 1) is written right after the first k-mer of a new AA group past each
+// (D / (splitNum-1)) mark: {value of that k-mer, diffIdx offset of the NEXT k-mer, its info index
+// + 1} (IndexCreator.cpp:843-851). The reader starts a thread at value ADkmer, info index
+// infoIdxOffset - 1 and diffIdx offset diffIdxOffset (KmerMatcher.cpp:255-271). Entry 0 is
+// {0, 0, 0} (decode from the start); unused entries stay 0 (KmerMatcher.cpp:134-141).
+bool partition_bounds(const uint64_t* split, uint64_t nSplit, uint64_t D, int parts, std::vector<uint64_t>& start,
+                      std::vector<uint64_t>& entry) {
+    if (parts < 1 || D == 0) { set_error("partition: need >= 1 part and a non-empty DB"); return false; }
+    std::vector<std::pair<uint64_t, uint64_t>> usable;  // (first k-mer index, split entry)
+    for (uint64_t j = 1; j < nSplit; j++) {
+        const uint64_t* e = split + 3 * j;
+        if (e[0] == 0 || e[0] == UINT64_MAX || e[2] == 0 || e[2] > D) continue;
+        if (!usable.empty() && e[2] - 1 <= usable.back().first) continue;
+        usable.emplace_back(e[2] - 1, j);
+    }
+    start.assign(1, 0);
+    entry.assign(1, 0);
+    size_t u = 0;
+    for (int p = 1; p < parts; p++) {
+        const double target = (double)D * p / parts;
+        size_t best = SIZE_MAX;
+        for (; u < usable.size(); u++) {  // first usable boundary at or past the target, or the one just before
+            if ((double)usable[u].first >= target) break;
+        }
+        for (size_t cand : {u ? u - 1 : SIZE_MAX, u}) {
+            if (cand >= usable.size() || usable[cand].first <= start.back()) continue;
+            if (usable.size() - cand < (size_t)(parts - p)) continue;  // leave one boundary per later part
+            if (best == SIZE_MAX ||
+                std::abs((double)usable[cand].first - target) < std::abs((double)usable[best].first - target))
+                best = cand;
+        }
+        if (best == SIZE_MAX) {
+            set_error("partition: the split table has too few AA-aligned entries for " + std::to_string(parts) +
+                      " parts");
+            return false;
+        }
+        start.push_back(usable[best].first);
+        entry.push_back(usable[best].second);
+        u = best + 1;
+    }
+    start.push_back(D);
+    return true;
+}
+
+// Keep part `part` of `parts`: k-mers [s_p, s_{p+1}) plus, for every part but the last, the first
+// k-mer of the next part, which is the part's last resident k-mer and so never a candidate (the
+// reference reader stops before the DB's last k-mer, KmerMatcher.cpp:363,378; the next part's AA
+// run holds it instead). diffIdx of the part = the varint of its first value (a delta from 0, as
+// IndexCreator's getDiffIdx writes it, IndexCreator.cpp:811-835) + the file's words from the split's
+// diffIdxOffset up to the next boundary's, so the device decode runs unchanged.
+bool slice_db_part(HostDb& db, int part, int parts) {
+    if (parts <= 1) return true;
+    if (part < 0 || part >= parts) { set_error("db_part out of range"); return false; }
+    if (db.split.size() < 6) { set_error("partitioned DB needs the split file"); return false; }
+    const uint64_t D = db.info.size(), nSplit = db.split.size() / 3;
+    std::vector<uint64_t> start, entry;
+    if (!partition_bounds(db.split.data(), nSplit, D, parts, start, entry)) return false;
+    const uint64_t s0 = start[part], s1 = start[part + 1];
+    const bool last = part == parts - 1;
+    const uint64_t* e0 = db.split.data() + 3 * entry[part];
+    const uint64_t dBeg = part == 0 ? 0 : e0[1];
+    const uint64_t dEnd = last ? db.diffIdx.size() : db.split[3 * entry[part + 1] + 1];
+    std::vector<uint16_t> diff;
+    if (part > 0) {  // getDiffIdx(lastKmer = 0, ADkmer)
+        uint64_t v = e0[0];
+        uint16_t buf[5];
+        int idx = 3;
+        buf[4] = (uint16_t)(0x8000u | (v & 0x7FFF));
+        v >>= 15;
+        while (v) {
+            buf[idx--] = (uint16_t)(v & 0x7FFF);
+            v >>= 15;
+        }
+        for (int i = idx + 1; i <= 4; i++) diff.push_back(buf[i]);
+    }
+    diff.insert(diff.end(), db.diffIdx.begin() + dBeg, db.diffIdx.begin() + dEnd);
+    const uint64_t iEnd = last ? D : s1 + 1;
+    std::vector<uint32_t> info(db.info.begin() + s0, db.info.begin() + iEnd);
+    db.diffIdx.swap(diff);
+    db.info.swap(info);
+    return check_db(db);  // terminal words == info entries
+}
+
 }  // namespace mtb
 
 using namespace mtb;
@@ -306,6 +393,17 @@ int mtb_load_db_parameters(const char* dir, mtb_params* par) {  // loadDbParamet
 }
 
 const char* mtb_last_error(void) { return g_error.c_str(); }
+
+int mtb_partition_bounds(const uint64_t* split, uint64_t n_split, uint64_t n_kmers, int n_parts, uint64_t* kmer_start,
+                         uint64_t* split_index) {
+    if (!split || !kmer_start) { set_error("null argument"); return MTB_ERR_ARG; }
+    std::vector<uint64_t> start, entry;
+    if (!partition_bounds(split, n_split, n_kmers, n_parts, start, entry)) return MTB_ERR_DB;
+    for (int p = 0; p <= n_parts; p++) kmer_start[p] = start[p];
+    if (split_index)
+        for (int p = 0; p < n_parts; p++) split_index[p] = entry[p];
+    return MTB_OK;
+}
 
 // Restated tables, for the CPU test that pins them against tests/golden/genetic_code.json.
 void mtb_debug_tables(uint8_t* base256, int8_t* aa64, int8_t* num64) {

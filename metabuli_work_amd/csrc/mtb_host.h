@@ -48,5 +48,8 @@ bool load_dmp(const std::string& dir, HostTaxonomy& out);
 bool build_species_map(HostDb& db);
 bool load_db_files(const std::string& dir, HostDb& db);
 bool check_db(const HostDb& db);
+bool partition_bounds(const uint64_t* split, uint64_t nSplit, uint64_t D, int parts, std::vector<uint64_t>& start,
+                      std::vector<uint64_t>& entry);
+bool slice_db_part(HostDb& db, int part, int parts);
 
 }  // namespace mtb

@@ -162,6 +162,9 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                    mtb_taxcnt* tcPool, mtb_result* results, unsigned long long* devStats, uint64_t* hostStats,
                    hipStream_t st);  // devStats[1] += wave runs sent to the introsort emulation;
                                      // hostStats = {groups, groups >= 2 matches, species runs, wave runs}
+// chunk-major per-(chunk, read) counts -> per-read totals, mOff (n + 1), segments in dst
+void launch_regroup_chunks(const mtb_match* src, const uint32_t* cnt, uint32_t nChunks, uint32_t n, uint32_t* tot,
+                           uint64_t* srcOff, uint64_t* mOff, void* scanTmp, mtb_match* dst, hipStream_t s);
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
 void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
                            uint32_t nReads, mtb_taxcnt* out, hipStream_t s);

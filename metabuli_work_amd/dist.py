@@ -44,3 +44,74 @@ def gather_records(local: torch.Tensor, counts: List[int], group=None) -> torch.
     dist.all_gather_into_tensor(out.view(-1), pad.view(-1), group=group)
     parts = [out[r * cap:r * cap + counts[r]] for r in range(world)]
     return torch.cat(parts, 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# Range-partitioned DB: rank r holds DB part r (AA-aligned k-mer range,
+# mtb_partition_bounds) and matches EVERY read of the batch against it; the matches then go
+# all-to-all to the rank that owns their read (C2), which sorts and scores them (mtb_assign_chunks);
+# the result records are gathered at the end (C1).
+# ---------------------------------------------------------------------------------------------
+MATCH_BYTES = 24
+
+
+def owner_bounds(n: int, world: int) -> List[Tuple[int, int]]:
+    """Reads [0, n) cut into `world` contiguous owner ranges of equal read count."""
+    cuts = [n * r // world for r in range(world + 1)]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def exchange_matches(matches: torch.Tensor, counts: torch.Tensor, bounds: List[Tuple[int, int]], group=None):
+    """All-to-all of per-read match segments to the owners of the reads.
+
+    matches: (M, 24) uint8, grouped by read in read order; counts: (n,) int32 matches per read.
+    Returns (recv_matches (R, 24) uint8, recv_counts (world * n_own,) int32): one chunk per source
+    rank, each grouped by the owner's reads — the layout mtb_assign_chunks takes."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_q = [hi - lo for lo, hi in bounds]
+    n_own = n_q[rank]
+    recv_cnt = torch.empty(world * n_own, dtype=torch.int32, device=counts.device)
+    dist.all_to_all_single(recv_cnt, counts, output_split_sizes=[n_own] * world, input_split_sizes=n_q, group=group)
+    csum = torch.zeros(len(counts) + 1, dtype=torch.int64, device=counts.device)
+    torch.cumsum(counts.to(torch.int64), 0, out=csum[1:])
+    cuts = csum[[lo for lo, _ in bounds] + [bounds[-1][1]]].cpu().tolist()
+    send = [cuts[q + 1] - cuts[q] for q in range(world)]
+    recv = recv_cnt.view(world, n_own).to(torch.int64).sum(1).cpu().tolist() if n_own else [0] * world
+    out = torch.empty((sum(recv), MATCH_BYTES), dtype=torch.uint8, device=matches.device)
+    dist.all_to_all_single(out, matches, output_split_sizes=recv, input_split_sizes=send, group=group)
+    return out, recv_cnt
+
+
+def classify_partitioned(clf, seq1, off1, seq2=None, off2=None, group=None, device_input: bool = False,
+                         on_device: bool = True):
+    """One batch through a range-partitioned DB. Every rank passes the SAME batch; `clf` holds this
+    rank's DB part (Classifier(..., db_part=(rank, world))). Returns (owner read range, BatchResult
+    of the owned reads, or None with on_device when results stay in HBM). on_device=False stages the
+    exchange through host memory (gloo)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = (int(off1.numel()) if device_input else len(off1)) - 1
+    clf.classify_batch(seq1, off1, seq2, off2, device_input=device_input, match_only=True)
+    _, M = clf.last_counts()
+    if on_device:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        matches = torch.empty((M, MATCH_BYTES), dtype=torch.uint8, device=dev)
+        counts = torch.empty(n, dtype=torch.int32, device=dev)
+        qlen = torch.empty(n, dtype=torch.int32, device=dev)
+        clf.copy_matches(matches, counts, qlen)
+    else:
+        m_np = np.zeros((M, MATCH_BYTES), np.uint8)
+        c_np = np.zeros(n, np.int32)
+        q_np = np.zeros(n, np.int32)
+        clf.copy_matches(m_np, c_np, q_np)
+        matches, counts, qlen = torch.from_numpy(m_np), torch.from_numpy(c_np), torch.from_numpy(q_np)
+    bounds = owner_bounds(n, world)
+    rm, rc = exchange_matches(matches, counts, bounds, group)
+    lo, hi = bounds[rank]
+    ql = qlen[lo:hi].contiguous()
+    if on_device:
+        br = clf.assign_chunks(rm, rm.shape[0], rc, world, ql, hi - lo, fetch=False)
+    else:
+        br = clf.assign_chunks(rm.numpy(), rm.shape[0], rc.numpy(), world, ql.numpy(), hi - lo)
+    return (lo, hi), br
