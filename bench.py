@@ -205,6 +205,9 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--long-reads", type=int, default=50_000,
                     help="ONT-style reads (N50 ~10 kb) per rank for the long-read line (0 = off)")
+    ap.add_argument("--db-parts", type=int, default=0,
+                    help="config-5 mode: the DB range-partitioned into this many parts (= the number of ranks; "
+                         "on one GPU every part is timed in turn)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -218,7 +221,8 @@ def main():
     t0 = time.time()
     par = default_params(kmer_format=2, seq_mode=2)
     taxo, gen, seq, off_t, lens = make_genomes_gpu(args.species, args.mean_genome, 2, args.seed, dev)
-    s1, o1, s2, o2 = make_reads_gpu(seq, off_t, args.pairs, args.seed * 1000 + 17 * rank + 1, dev)
+    rseed = args.seed * 1000 + 1 + (0 if args.db_parts > 1 else 17 * rank)  # config 5: one batch on all ranks
+    s1, o1, s2, o2 = make_reads_gpu(seq, off_t, args.pairs, rseed, dev)
     torch.cuda.synchronize()
     log(rank, f"[bench] genomes {seq.numel() / 1e9:.2f} Gbp in {len(lens) * 2} genomes, blocks "
               f"{len(gen.blk_genome)}; reads {args.pairs} pairs ({time.time() - t0:.1f}s)")
@@ -231,6 +235,8 @@ def main():
     log(rank, f"[bench] DB built: {hdb.n_kmers / 1e9:.3f}G k-mers, {db_bytes / 1e9:.2f} GB "
               f"(diffIdx+info) ({time.time() - t0:.1f}s)")
     lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    if args.db_parts > 1:
+        return run_partitioned(args, lp, hdb, (s1, o1, s2, o2), world, rank, local, dev)
     clf = Classifier(lp, db_host=hdb.c_struct(), device=local)
     log(rank, f"[bench] DB resident in HBM ({time.time() - t0:.1f}s)")
 
@@ -425,6 +431,110 @@ def main():
     clf.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_partitioned(args, lp, hdb, batch, world, rank, local, dev):
+    """Config-5 shape: the DB cut into P AA-aligned k-mer ranges, one per rank. Every
+    rank matches the WHOLE batch against its range (MTB_MATCH_ONLY), the matches go all-to-all to
+    the owners of their reads (RCCL), each owner sorts + scores its 1/P of the reads
+    (mtb_assign_chunks), and the result records are gathered. With world == P this runs for real;
+    on one GPU (world == 1) each part is timed in turn: a rank's step = its match-only pass over
+    the batch + the assignment of its owned reads (their matches from all parts); the all-to-all
+    is not timed there and its bytes are reported instead."""
+    from metabuli_work_amd.dist import classify_partitioned, gather_records, owner_bounds
+
+    P = args.db_parts
+    s1, o1, s2, o2 = batch
+    n = args.pairs
+    if world > 1 and world != P:
+        raise SystemExit("--db-parts must equal the number of ranks (or run on one GPU)")
+    out = {"metric": "reads/sec classified (150bp & 10kb) vs GTDB-scale DB at 1/2/4/8 MI355X", "unit": "reads/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic"}
+    if world > 1:
+        # same batch on every rank (rank-independent seed), each holding DB part `rank`
+        clf = Classifier(lp, db_host=hdb.c_struct(), device=local, db_part=(rank, P))
+        sizes = [b - a for a, b in owner_bounds(n, world)]
+        res = torch.empty((sizes[rank], RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+
+        def step():
+            _, br = classify_partitioned(clf, s1, o1, s2, o2, device_input=True, on_device=True)
+            clf.copy_results(res.data_ptr(), on_device=True)
+            gather_records(res, sizes)
+
+        for _ in range(args.warmup):
+            step()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        clf.close()
+        out.update(value=round(n * args.steps / el, 1), ms_per_step=round(el / args.steps * 1e3, 3),
+                   config={"workload": f"config-5 shape: {n} read pairs x 150 bp per step vs the bench DB "
+                                       f"range-partitioned over {P} GPUs (match all-to-all + result gather)",
+                           "db_kmers": hdb.n_kmers, "parallelism": f"DB range-partitioned x{P}"})
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        dist.destroy_process_group()
+        return
+    # one GPU: the owners' assignment inputs = the full DB's matches of their reads
+    full = Classifier(lp, db_host=hdb.c_struct(), device=local)
+    full.classify_batch(s1, o1, s2, o2, device_input=True, match_only=True)
+    _, Mf = full.last_counts()
+    mt = torch.empty((Mf, 24), dtype=torch.uint8, device=dev)
+    ct = torch.empty(n, dtype=torch.int32, device=dev)
+    qt = torch.empty(n, dtype=torch.int32, device=dev)
+    full.copy_matches(mt, ct, qt)
+    full.close()
+    cs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(ct.to(torch.int64), 0, out=cs[1:])
+    bounds = owner_bounds(n, P)
+    parts = []
+    for p in range(P):
+        clf = Classifier(lp, db_host=hdb.c_struct(), device=local, db_part=(p, P))
+        lo, hi = bounds[p]
+        a, b = int(cs[lo].item()), int(cs[hi].item())
+        om, oc_, oq = mt[a:b].contiguous(), ct[lo:hi].contiguous(), qt[lo:hi].contiguous()
+        for _ in range(args.warmup):
+            clf.classify_batch(s1, o1, s2, o2, device_input=True, match_only=True)
+            clf.assign_chunks(om, b - a, oc_, 1, oq, hi - lo, fetch=False)
+        torch.cuda.synchronize()
+        tm = ta = 0.0
+        kern = np.zeros(7)
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            clf.classify_batch(s1, o1, s2, o2, device_input=True, match_only=True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            kern += clf.kernel_ms()
+            clf.assign_chunks(om, b - a, oc_, 1, oq, hi - lo, fetch=False)
+            torch.cuda.synchronize()
+            tm += t1 - t0
+            ta += time.perf_counter() - t1
+        _, Mp = clf.last_counts()
+        clf.classify_batch(s1, o1, s2, o2, device_input=True, match_only=True)
+        _, Mp = clf.last_counts()
+        parts.append({"part": p, "db_kmers": clf.db_kmers, "match_only_ms": round(tm / args.steps * 1e3, 3),
+                      "assign_ms": round(ta / args.steps * 1e3, 3), "matches": Mp,
+                      "a2a_send_bytes": int(Mp * 24 * (P - 1) // P),
+                      "kernel_ms": {k: round(float(v) / args.steps, 3)
+                                    for k, v in zip(KERNELS_SORT[:5], kern[:5])}})
+        clf.close()
+        log(rank, f"[bench] part {p}/{P}: {parts[-1]}")
+    step_ms = max(q["match_only_ms"] + q["assign_ms"] for q in parts)
+    out.update(value=round(n / (step_ms * 1e-3), 1), ms_per_step=round(step_ms, 3),
+               config={"workload": f"config-5 shape on ONE GPU: {n} read pairs x 150 bp vs the bench DB range-"
+                                   f"partitioned into {P} parts, each part's rank step timed in turn (the "
+                                   "all-to-all over xGMI is not timed: a2a_send_bytes)",
+                       "db_kmers": hdb.n_kmers, "parallelism": f"DB range-partitioned x{P} (simulated)"},
+               parts=parts)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

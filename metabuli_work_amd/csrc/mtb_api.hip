@@ -60,6 +60,7 @@ struct mtb_ctx {
     uint64_t* dirMem = nullptr;
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     AADir dir{};
+    uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
@@ -166,6 +167,14 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
     launch_mask_info(c->dbinfo, c->D, mask, s);
     if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
+    if (par->db_parts > 1) {  // the part's AA-rank range: its first k-mer up to its guard k-mer's run
+        uint64_t ends[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(&ends[0], c->dbv, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&ends[1], c->dbv + c->D - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->rankLo = ends[0] >> 24;
+        c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ends[1] >> 24;
+    }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
@@ -412,7 +421,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     if (c->lines) {
         if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
         Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
-                          probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), s);
+                          probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), c->rankLo,
+                          c->rankHi, s);
         qk = c->keysB.as<uint64_t>();
         qi = c->valsB.as<uint32_t>();
         qf = c->qFrom.as<uint64_t>();

@@ -954,7 +954,8 @@ template <bool FROM>
 __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ keys, uint64_t R,
                                                 const ProbeLine* __restrict__ lines, uint64_t* __restrict__ qkey,
                                                 uint32_t* __restrict__ qslot, uint64_t* __restrict__ qfrom,
-                                                unsigned long long* __restrict__ counter) {
+                                                unsigned long long* __restrict__ counter, uint64_t rankLo,
+                                                uint64_t rankHi) {
     __shared__ unsigned long long sBase;
     const uint64_t base = (uint64_t)blockIdx.x * (256 * kFilterPer) + threadIdx.x;
     uint64_t k[kFilterPer];
@@ -964,8 +965,9 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 #pragma unroll
     for (int j = 0; j < kFilterPer; j++) {
         word[j] = 0;
-        if (k[j] != kSentinel) {
-            const uint64_t x = k[j] >> 24, L = x / kLineRanks;
+        const uint64_t xr = k[j] >> 24;
+        if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {  // outside a DB part's range: no probe
+            const uint64_t x = xr, L = x / kLineRanks;
             const uint32_t o = (uint32_t)(x - L * kLineRanks);
             word[j] = (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
         }
@@ -1003,12 +1005,12 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 }
 
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
-                       uint64_t* qfrom, unsigned long long* counter, hipStream_t s) {
+                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, hipStream_t s) {
     hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
     const uint64_t blocks = (R + 256 * kFilterPer - 1) / (256 * kFilterPer);
     if (blocks) {
-        if (qfrom) k_filter<true><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter);
-        else k_filter<false><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter);
+        if (qfrom) k_filter<true><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter, rankLo, rankHi);
+        else k_filter<false><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter, rankLo, rankHi);
     }
     unsigned long long Q = 0;
     hipMemcpyAsync(&Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);

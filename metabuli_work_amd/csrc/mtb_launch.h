@@ -118,8 +118,9 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count.
+// keys whose AA rank lies outside [rankLo, rankHi) (a DB part's range) are dropped without a probe
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
-                       uint64_t* qfrom, unsigned long long* counter, hipStream_t s);
+                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, hipStream_t s);
 // K4P probe join over the filtered queries: same outputs as launch_match (per-read counts and
 // ranks, staged matches); stats: kStatStripes counters of queries with >= 1 match.
 void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
