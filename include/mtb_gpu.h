@@ -121,6 +121,21 @@ typedef struct mtb_db_host {
     const int32_t* merged_old;  const int32_t* merged_new;  uint64_t n_merged;
 } mtb_db_host;
 
+/* A decoded reference DB already resident in HBM (a DB built in place on the device, e.g. the
+ * GTDB-scale synthetic DB of the bench, SURVEY §8(d) config 3, which is never written out).
+ * values: n_kmers sorted k-mer values (the diffIdx decoded: getNextTargetKmer, KmerMatcher.h:282-297);
+ * with rank_form = 1 and kmer_format 2 the AA part is already the base-21 rank of the 8 AA codes
+ * (the resident form). info: the matching taxIDs. Both are device arrays with room
+ * for n_kmers + 8 entries; the context uses them in place (pads written, info masked, format-2
+ * values converted to rank form) and does not free them: they must outlive the context. */
+typedef struct mtb_db_resident {
+    uint64_t* values;
+    uint32_t* info;
+    uint64_t n_kmers;
+    int32_t rank_form;
+    int32_t reserved;
+} mtb_db_resident;
+
 /* ---- parameters ---------------------------------------------------------------------------- */
 void mtb_default_params(mtb_params* par);                              /* classify.cpp:10-37   */
 int mtb_load_db_parameters(const char* db_dir, mtb_params* par);       /* common.cpp:88-133    */
@@ -131,6 +146,10 @@ int mtb_load_db_parameters(const char* db_dir, mtb_params* par);       /* common
  * split, taxID_list and taxonomy/{nodes,names,merged}.dmp and makes them resident in HBM. */
 int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** out);
 int mtb_open_host(const mtb_db_host* db, const mtb_params* par, int device, mtb_ctx** out);
+/* Context over a resident DB; `taxonomy` supplies the taxonomy and taxID_list only (its diffIdx,
+ * info and split pointers are not read). */
+int mtb_open_resident(const mtb_db_resident* db, const mtb_db_host* taxonomy, const mtb_params* par, int device,
+                      mtb_ctx** out);
 void mtb_close(mtb_ctx* ctx);
 const char* mtb_last_error(void);
 int mtb_set_stream(mtb_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
@@ -223,11 +242,18 @@ typedef struct mtb_build_input {
     uint32_t flags;
 } mtb_build_input;
 
+/* mtb_build_input.flags: MTB_INPUT_DEVICE (seq/off are device pointers) and */
+#define MTB_BUILD_DEVICE_OUT 8u  /* keep the deduplicated DB on the device as resident-form values + info
+                                    (dev_values / dev_info, n_info entries, capacity n_info + 8) instead
+                                    of encoding diffIdx / split to the host */
+
 typedef struct mtb_db_built {    /* malloc'd host arrays, release with mtb_free_built */
     uint16_t* diff_idx; uint64_t n_diff_idx;
     uint32_t* info;     uint64_t n_info;
     uint64_t* split;    uint64_t n_split;
     int32_t* taxid_list; uint64_t n_taxid_list;
+    uint64_t* dev_values;        /* MTB_BUILD_DEVICE_OUT: device arrays (hipFree'd by mtb_free_built) */
+    uint32_t* dev_info;
 } mtb_db_built;
 
 int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxonomy, const mtb_params* par, int device,

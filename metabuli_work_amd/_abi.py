@@ -40,6 +40,11 @@ class MtbDbHost(ctypes.Structure):
     ]
 
 
+class MtbDbResident(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("info", ctypes.c_void_p), ("n_kmers", ctypes.c_uint64),
+                ("rank_form", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 KMER_DTYPE = np.dtype([("value", "<u8"), ("info", "<u8")])
 MATCH_DTYPE = np.dtype([("qinfo", "<u8"), ("target_id", "<u4"), ("species_id", "<u4"), ("dna_encoding", "<u4"),
                         ("right_end_hamming", "<u2"), ("hamming", "u1"), ("pad", "u1")])

@@ -7,7 +7,7 @@ entry point raises. Build it with `python -c "import __graft_entry__ as g; g.bui
 import ctypes
 import pathlib
 
-from ._abi import MtbDbHost, MtbParams, MtbReadBatch
+from ._abi import MtbDbHost, MtbDbResident, MtbParams, MtbReadBatch
 
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libmtbgpu.so"
@@ -20,7 +20,7 @@ EXPORTED = [
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
-    "mtb_assign_chunks",
+    "mtb_assign_chunks", "mtb_open_resident",
 ]
 
 
@@ -42,6 +42,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_load_db_parameters.argtypes = [ctypes.c_char_p, P(MtbParams)]
     L.mtb_open.argtypes = [ctypes.c_char_p, P(MtbParams), i32, P(vp)]
     L.mtb_open_host.argtypes = [P(MtbDbHost), P(MtbParams), i32, P(vp)]
+    L.mtb_open_resident.argtypes = [P(MtbDbResident), P(MtbDbHost), P(MtbParams), i32, P(vp)]
     L.mtb_close.argtypes = [vp]
     L.mtb_close.restype = None
     L.mtb_last_error.restype = ctypes.c_char_p

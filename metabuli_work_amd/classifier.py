@@ -86,13 +86,21 @@ class Classifier:
     """GPU-resident classifier; one instance per device (mirrors Classifier.cpp:6-32)."""
 
     def __init__(self, par: LocalParameters, db_dir: Optional[str] = None, device: int = 0,
-                 db_host: Optional[_abi.MtbDbHost] = None, db_part: Tuple[int, int] = (0, 1)):
+                 db_host: Optional[_abi.MtbDbHost] = None, db_part: Tuple[int, int] = (0, 1), db_resident=None):
         """db_part = (part, parts): hold one AA-aligned k-mer range of a range-partitioned DB
-        (see dist.classify_partitioned)."""
+        (see dist.classify_partitioned). db_resident: a DB already in HBM
+        (gtdb_synth.ResidentDb), used in place (mtb_open_resident)."""
         self.par = par
         self.device = device
         self.db_part = db_part
         self.handle = ctypes.c_void_p()
+        if db_resident is not None:
+            self._resident = db_resident
+            cp = par.to_c()
+            check(lib().mtb_open_resident(ctypes.byref(db_resident.c_resident()),
+                                          ctypes.byref(db_resident.host.c_struct()), ctypes.byref(cp), device,
+                                          ctypes.byref(self.handle)), "mtb_open_resident")
+            return
         if db_host is None and db_dir is None:
             db_dir = par.filenames[1 + (par.seqMode == 2)]
         if db_dir is not None:

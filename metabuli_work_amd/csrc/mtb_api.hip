@@ -56,6 +56,7 @@ struct mtb_ctx {
     // DB residency
     uint64_t D = 0;
     uint64_t* dbv = nullptr;
+    bool borrowedDb = false;  // dbv/dbinfo belong to the caller (mtb_open_resident)
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
@@ -102,6 +103,7 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
+    if (c->borrowedDb) c->dbv = nullptr, c->dbinfo = nullptr;  // caller-owned (mtb_open_resident)
     void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->lines, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -130,12 +132,18 @@ static int validate_params(const mtb_params* p) {
     return MTB_OK;
 }
 
-static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out) {
+static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out,
+                       const mtb_db_resident* res = nullptr) {
     int rc = validate_params(par);
     if (rc != MTB_OK) return rc;
-    if (!check_db(db)) return MTB_ERR_DB;
-    if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
-    if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
+    if (res) {
+        if (par->db_parts > 1) { set_error("a resident DB cannot be range-partitioned: pass each part's arrays"); return MTB_ERR_ARG; }
+        if (!res->values || !res->info || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
+    } else {
+        if (!check_db(db)) return MTB_ERR_DB;
+        if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
+        if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
+    }
     mtb_ctx* c = new mtb_ctx();
     c->device = device;
     c->par = *par;
@@ -146,27 +154,43 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
     for (auto& e : c->kev) HIP_TRY(hipEventCreate(&e));
     hipStream_t s = c->stream;
-    c->D = db.info.size();
-    // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381)
-    uint16_t* dDiff = nullptr;
-    uint32_t* dFlag = nullptr;
-    uint64_t* dIdx = nullptr;
-    void* dTmp = nullptr;
-    const uint64_t nDiff = db.diffIdx.size();
-    HIP_TRY(hipMalloc(&c->dbv, (c->D + kDbPad) * sizeof(uint64_t)));  // + ~0 pad: the probe's 8 loads need no bound
-    HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
-    HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
-    HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
-    HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
-    HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-    decode_diff_idx(dDiff, nDiff, c->dbv, c->D, dFlag, dIdx, dTmp, s);
-    HIP_TRY(hipMalloc(&c->dbinfo, (c->D + kDbPad) * sizeof(uint32_t)));  // + pad: the emit's 8 loads need no bound
-    HIP_TRY(hipMemcpyAsync(c->dbinfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
-    launch_mask_info(c->dbinfo, c->D, mask, s);
-    if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
+    if (res) {  // caller-owned arrays, used in place (capacity n_kmers + kDbPad)
+        c->D = res->n_kmers;
+        c->dbv = res->values;
+        c->dbinfo = res->info;
+        c->borrowedDb = true;
+        HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
+        HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
+        launch_mask_info(c->dbinfo, c->D, mask, s);
+        if (par->kmer_format == 2 && !res->rank_form) launch_to_rank_form(c->dbv, c->D, s);
+    } else {
+        c->D = db.info.size();
+        // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381)
+        uint16_t* dDiff = nullptr;
+        uint32_t* dFlag = nullptr;
+        uint64_t* dIdx = nullptr;
+        void* dTmp = nullptr;
+        const uint64_t nDiff = db.diffIdx.size();
+        HIP_TRY(hipMalloc(&c->dbv, (c->D + kDbPad) * sizeof(uint64_t)));  // + ~0 pad: the probe's 8 loads need no bound
+        HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
+        HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
+        HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
+        HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
+        HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+        decode_diff_idx(dDiff, nDiff, c->dbv, c->D, dFlag, dIdx, dTmp, s);
+        HIP_TRY(hipMalloc(&c->dbinfo, (c->D + kDbPad) * sizeof(uint32_t)));  // + pad: the emit's 8 loads need no bound
+        HIP_TRY(hipMemcpyAsync(c->dbinfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
+        launch_mask_info(c->dbinfo, c->D, mask, s);
+        if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
+        HIP_TRY(hipStreamSynchronize(s));
+        hipFree(dDiff);
+        hipFree(dFlag);
+        hipFree(dIdx);
+        hipFree(dTmp);
+    }
     if (par->db_parts > 1) {  // the part's AA-rank range: its first k-mer up to its guard k-mer's run
         uint64_t ends[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(&ends[0], c->dbv, 8, hipMemcpyDeviceToHost, s));
@@ -189,10 +213,6 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         build_probe_lines(c->dbv, c->D, c->dir, c->lines, s);
     }
     HIP_TRY(hipStreamSynchronize(s));
-    hipFree(dDiff);
-    hipFree(dFlag);
-    hipFree(dIdx);
-    hipFree(dTmp);
     // taxonomy + taxId2speciesId
     const HostTaxonomy& T = db.tax;
     c->maxTax = T.maxTax;
@@ -246,6 +266,23 @@ int mtb_open_host(const mtb_db_host* h, const mtb_params* par, int device, mtb_c
         !build_species_map(db))
         return MTB_ERR_DB;
     return open_common(db, par, device, out);
+}
+
+int mtb_open_resident(const mtb_db_resident* r, const mtb_db_host* h, const mtb_params* par, int device,
+                      mtb_ctx** out) {
+    if (!r || !h || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
+    HostDb db;
+    db.taxIdList.assign(h->taxid_list, h->taxid_list + h->n_taxid_list);
+    std::vector<std::string> ranks(h->n_nodes), names(h->n_nodes);
+    for (uint64_t i = 0; i < h->n_nodes; i++) {
+        ranks[i] = h->rank_pool + h->rank_off[i];
+        if (h->name_pool) names[i] = h->name_pool + h->name_off[i];
+    }
+    if (!build_taxonomy(h->node_taxid, h->node_parent, h->n_nodes, ranks, names, h->merged_old, h->merged_new,
+                        h->n_merged, db.tax) ||
+        !build_species_map(db))
+        return MTB_ERR_DB;
+    return open_common(db, par, device, out, r);
 }
 
 void mtb_close(mtb_ctx* c) {

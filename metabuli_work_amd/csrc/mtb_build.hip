@@ -221,6 +221,8 @@ void mtb_free_built(mtb_db_built* b) {
     free(b->info);
     free(b->split);
     free(b->taxid_list);
+    if (b->dev_values) hipFree(b->dev_values);
+    if (b->dev_info) hipFree(b->dev_info);
     memset(b, 0, sizeof(*b));
 }
 
@@ -338,11 +340,21 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxo, const mtb_p
     exclusive_scan_u32(head, kept, uidx, scanTmp, s);
     HIP_B(hipMemcpyAsync(&U, uidx + kept, 8, hipMemcpyDeviceToHost, s));
     HIP_B(hipStreamSynchronize(s));
-    HIP_B(hipMalloc(&uval, 8 * (U + 1)));
-    HIP_B(hipMalloc(&uinfo, 4 * (U + 1)));
+    HIP_B(hipMalloc(&uval, 8 * (U + kDbPad)));
+    HIP_B(hipMalloc(&uinfo, 4 * (U + kDbPad)));
     if (kept)
         k_group_reduce<<<(unsigned)((kept + 255) / 256), 256, 0, s>>>(
             sk, sp_, kept, head, uidx, TaxLca{tNodeOf, tNodeTax, tParent, tDepth, T.maxTax}, uval, uinfo);
+    if (in->flags & MTB_BUILD_DEVICE_OUT) {  // resident form for mtb_open_resident; no diffIdx / split
+        if (par->kmer_format == 2) launch_to_rank_form(uval, U, s);
+        HIP_B(hipStreamSynchronize(s));
+        out->dev_values = uval;
+        out->dev_info = uinfo;
+        out->n_info = U;
+        uval = nullptr;
+        uinfo = nullptr;
+        goto taxids;
+    }
     // diffIdx words
     HIP_B(hipMalloc(&words, 4 * (U + 1)));
     HIP_B(hipMalloc(&woff, 8 * (U + 1)));
@@ -382,6 +394,7 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxo, const mtb_p
             idx++;
         }
     }
+taxids:
     {
         std::vector<int32_t> ids(in->genome_taxid, in->genome_taxid + in->n_genomes);
         std::sort(ids.begin(), ids.end());

@@ -29,7 +29,11 @@ class MtbDbBuilt(ctypes.Structure):
     _fields_ = [("diff_idx", ctypes.c_void_p), ("n_diff_idx", ctypes.c_uint64),
                 ("info", ctypes.c_void_p), ("n_info", ctypes.c_uint64),
                 ("split", ctypes.c_void_p), ("n_split", ctypes.c_uint64),
-                ("taxid_list", ctypes.c_void_p), ("n_taxid_list", ctypes.c_uint64)]
+                ("taxid_list", ctypes.c_void_p), ("n_taxid_list", ctypes.c_uint64),
+                ("dev_values", ctypes.c_void_p), ("dev_info", ctypes.c_void_p)]
+
+
+MTB_BUILD_DEVICE_OUT = 8
 
 
 def _pool(strings):
@@ -65,6 +69,7 @@ class HostDb:
             h.diff_idx, h.n_diff_idx = ptr(self.diff_idx), len(self.diff_idx)
             h.info, h.n_info = ptr(self.info), len(self.info)
             h.split, h.n_split = ptr(self.split), len(self.split) // 3
+        if self.taxid_list is not None:
             h.taxid_list, h.n_taxid_list = ptr(self.taxid_list), len(self.taxid_list)
         return h
 
@@ -95,28 +100,38 @@ class HostDb:
         self.taxo.write_dmp(os.path.join(directory, "taxonomy"))
 
 
-def build_db(gen, taxo, par: MtbParams, device: int = 0, split_num: int = 4096, device_seq=None) -> HostDb:
-    """Build the reference DB on the GPU. ``device_seq`` = (seq, off) torch tensors already in HBM
-    (bench path); otherwise ``gen.seq`` / ``gen.off`` are uploaded."""
-    hdb = HostDb(taxo)
+def _build_input(gen, device_seq, split_num, flags):
     inp = MtbBuildInput()
     if device_seq is not None:
         inp.seq, inp.off = device_seq[0].data_ptr(), device_seq[1].data_ptr()
-        inp.flags = MTB_INPUT_DEVICE
+        inp.flags = MTB_INPUT_DEVICE | flags
     else:
         inp.seq, inp.off = ptr(gen.seq).value, ptr(gen.off).value
-        inp.flags = 0
+        inp.flags = flags
     keep = [np.ascontiguousarray(a, np.int32) for a in (gen.taxid, gen.blk_genome, gen.blk_start, gen.blk_end,
                                                          gen.blk_strand)]
     inp.n_genomes = len(gen.taxid)
     inp.genome_taxid, inp.blk_genome, inp.blk_start, inp.blk_end, inp.blk_strand = [a.ctypes.data for a in keep]
     inp.n_blocks = len(keep[1])
     inp.split_num = split_num
-    out = MtbDbBuilt()
+    return inp, keep
+
+
+def _lib_build():
     L = lib()
     L.mtb_build_db.argtypes = [ctypes.POINTER(MtbBuildInput), ctypes.POINTER(MtbDbHost), ctypes.POINTER(MtbParams),
                                ctypes.c_int, ctypes.POINTER(MtbDbBuilt)]
     L.mtb_free_built.argtypes = [ctypes.POINTER(MtbDbBuilt)]
+    return L
+
+
+def build_db(gen, taxo, par: MtbParams, device: int = 0, split_num: int = 4096, device_seq=None) -> HostDb:
+    """Build the reference DB on the GPU. ``device_seq`` = (seq, off) torch tensors already in HBM
+    (bench path); otherwise ``gen.seq`` / ``gen.off`` are uploaded."""
+    hdb = HostDb(taxo)
+    inp, keep = _build_input(gen, device_seq, split_num, 0)
+    out = MtbDbBuilt()
+    L = _lib_build()
     tax_struct = hdb.c_struct()
     check(L.mtb_build_db(ctypes.byref(inp), ctypes.byref(tax_struct), ctypes.byref(par), device, ctypes.byref(out)),
           "mtb_build_db")
@@ -133,3 +148,41 @@ def build_db(gen, taxo, par: MtbParams, device: int = 0, split_num: int = 4096, 
     finally:
         L.mtb_free_built(ctypes.byref(out))
     return hdb
+
+
+_HIP = None
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch (and libmtbgpu) already use
+        _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _HIP
+
+
+def build_db_device(gen, taxo, par: MtbParams, device: int = 0, device_seq=None):
+    """Build the reference DB on the GPU and keep it there (MTB_BUILD_DEVICE_OUT): returns torch
+    tensors (values in resident rank form int64, taxIDs int32), deduplicated and sorted."""
+    import torch
+
+    inp, keep = _build_input(gen, device_seq, 4096, MTB_BUILD_DEVICE_OUT)
+    out = MtbDbBuilt()
+    L = _lib_build()
+    htax = HostDb(taxo)  # keeps the arrays the struct points into alive
+    tax_struct = htax.c_struct()
+    check(L.mtb_build_db(ctypes.byref(inp), ctypes.byref(tax_struct), ctypes.byref(par), device, ctypes.byref(out)),
+          "mtb_build_db")
+    try:
+        n = int(out.n_info)
+        dev = torch.device("cuda", device)
+        v = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        t = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        if n:
+            H = _hip()
+            if H.hipMemcpy(v.data_ptr(), out.dev_values, 8 * n, 3) or H.hipMemcpy(t.data_ptr(), out.dev_info, 4 * n, 3):
+                raise RuntimeError("hipMemcpy of the built DB failed")
+    finally:
+        L.mtb_free_built(ctypes.byref(out))
+    return v[:n], t[:n]

@@ -1,0 +1,232 @@
+"""GTDB-scale synthetic reference DB, built in place on the GPU.
+
+Shape: a true-signal part — genomes of `n_true_species` species x 2 strains with
+gene blocks, turned into DB k-mers by the GPU builder (mtb_build_db with MTB_BUILD_DEVICE_OUT:
+extractTargetKmers, (value, species) dedup with the LCA, IndexCreator.cpp:316-376,
+IndexCreator.h:475-629) — plus filler: uniformly random valid metamers (a random AA 8-mer, each
+codon a random synonymous one) with the strains of a ~130k-species skeleton taxonomy (GTDB r226 has
+129,671 species reps), up to `target_kmers` entries. The two sorted streams are merged by AA-rank
+chunk into one resident array (values in the resident rank form; taxIDs), which a
+context uses in place (mtb_open_resident). Nothing is written to disk: at 12G k-mers the diffIdx +
+info would be ~110 GB.
+
+`encode_into_oracle` writes the same DB in the reference's diffIdx / info / split format
+(getDiffIdx, IndexCreator.cpp:868-886; writeTargetFilesAndSplits, :811-861) straight into the
+oracle's buffers, for the CPU baseline and its parity sample (test / bench infrastructure).
+
+Bench/test data only: nothing here is on the classify path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+
+from . import synth
+from ._abi import MtbDbResident, MtbParams, default_params
+from ._lib import check, lib
+from .dbbuild import HostDb, build_db_device
+from .gpu_synth import make_genomes_gpu
+
+AA_RANKS = 21 ** 8
+INT64_MIN = -(1 << 63)
+
+
+def codon_counts() -> np.ndarray:
+    """Synonymous codons per AA code (GeneticCode.h, as the library's tables hold them)."""
+    base = np.zeros(256, np.uint8)
+    aa = np.zeros(64, np.int8)
+    num = np.zeros(64, np.int8)
+    lib().mtb_debug_tables(base.ctypes.data, aa.ctypes.data, num.ctypes.data)
+    cnt = np.ones(21, np.int64)
+    for i in range(64):
+        if 0 <= aa[i] < 21:
+            cnt[aa[i]] = max(cnt[aa[i]], int(num[i]) + 1)
+    return cnt
+
+
+class ResidentDb:
+    """A DB resident in HBM: values (int64, resident rank form) and taxIDs (int32), each with 8
+    spare entries the context pads; `host` carries the taxonomy and taxID_list."""
+
+    def __init__(self, values: torch.Tensor, info: torch.Tensor, n: int, host: HostDb, n_true: int):
+        self.values, self.info, self.n, self.host, self.n_true = values, info, n, host, n_true
+
+    def c_resident(self) -> MtbDbResident:
+        return MtbDbResident(values=self.values.data_ptr(), info=self.info.data_ptr(), n_kmers=self.n, rank_form=1)
+
+    @property
+    def n_kmers(self) -> int:
+        return self.n
+
+
+def _filler_chunk(lo: int, hi: int, count: int, g: torch.Generator, cnt_t: torch.Tensor, strain_t: torch.Tensor):
+    """`count` random valid metamers with AA ranks in [lo, hi), unique values, sorted; random strains."""
+    dev = cnt_t.device
+    r = torch.randint(lo, hi, (count,), generator=g, device=dev, dtype=torch.int64)
+    dna = torch.zeros_like(r)
+    rem = r.clone()
+    for k in range(8):  # least significant base-21 digit = the last codon = DNA bits 0..2
+        a = rem % 21
+        rem = rem // 21
+        c = (torch.rand(count, generator=g, device=dev) * cnt_t[a]).long().clamp_(max=7)
+        dna |= c << (3 * k)
+    del rem
+    v = torch.unique((r << 24) | dna)
+    del r, dna
+    tax = strain_t[torch.randint(0, strain_t.numel(), (v.numel(),), generator=g, device=dev)]
+    return v, tax
+
+
+def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: int = 3_000_000,
+                     total_species: int = 129_671, target_kmers: int = 12_000_000_000, strains: int = 2,
+                     seed: int = 6, n_chunks: int = 64,
+                     before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
+                     log: Callable[[str], None] = lambda s: None) -> ResidentDb:
+    """Build the DB on `dev`. before_free(seq, off) runs while the true-signal genomes are still in
+    HBM (the bench samples its reads there)."""
+    taxo = synth.make_taxonomy(total_species, strains, seed=seed)
+    taxo, gen, seq, off_t, _ = make_genomes_gpu(n_true_species, genome_len, strains, seed, dev, taxo=taxo)
+    if before_free is not None:
+        before_free(seq, off_t)
+    par = default_params(kmer_format=2, seq_mode=2)
+    tv, ti = build_db_device(gen, taxo, par, device=dev.index or 0, device_seq=(seq, off_t))
+    del seq, off_t
+    torch.cuda.empty_cache()
+    n_true = tv.numel()
+    log(f"true-signal DB part: {n_true / 1e9:.3f}G k-mers")
+    # filler strains: those of the skeleton species beyond the true-signal ones
+    rank = np.array(taxo.rank)
+    sp_all = taxo.taxid[rank == "species"]
+    filler_sp = set(sp_all[n_true_species:].tolist())
+    strains_f = np.array([t for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank)
+                          if r == "no rank" and p in filler_sp], np.int32)
+    strain_t = torch.from_numpy(strains_f).to(dev)
+    cnt_t = torch.from_numpy(codon_counts().astype(np.float32)).to(dev)
+    n_fill = max(0, int(target_kmers) - n_true)
+    per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
+    cap = n_true + n_fill + 8
+    values = torch.empty(cap, dtype=torch.int64, device=dev)
+    info = torch.empty(cap, dtype=torch.int32, device=dev)
+    edges = torch.tensor([c * AA_RANKS // n_chunks for c in range(n_chunks + 1)], dtype=torch.int64, device=dev)
+    cut = torch.searchsorted(tv, edges << 24).cpu().tolist()
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed * 7919 + 1)
+    pos = 0
+    for c in range(n_chunks):
+        lo, hi = int(edges[c].item()), int(edges[c + 1].item())
+        fv, ft = _filler_chunk(lo, hi, per[c], g, cnt_t, strain_t)
+        a, b = cut[c], cut[c + 1]
+        v = torch.cat([tv[a:b], fv])
+        t = torch.cat([ti[a:b], ft])
+        del fv, ft
+        # stable: a value held by a true-signal species and a filler species keeps species order
+        # (true-signal species have the smaller taxIDs), as the builder's (value, species) sort does
+        vs, order = torch.sort(v, stable=True)
+        m = vs.numel()
+        values[pos:pos + m] = vs
+        info[pos:pos + m] = t[order]
+        pos += m
+        del v, t, vs, order
+    del tv, ti
+    torch.cuda.empty_cache()
+    ids = np.unique(np.concatenate([gen.taxid.astype(np.int32), strains_f]))
+    host = HostDb(taxo, taxid_list=ids.astype(np.int32))
+    log(f"GTDB-scale DB: {pos / 1e9:.3f}G k-mers ({n_true / 1e9:.3f}G true signal), "
+        f"{len(sp_all)} species in the taxonomy")
+    return ResidentDb(values, info, pos, host, n_true)
+
+
+# ---------------------------------------------------------------------------------------------
+# The same DB in the reference's on-disk format, written into the oracle's buffers.
+# ---------------------------------------------------------------------------------------------
+def _lsr(x: torch.Tensor, s: int) -> torch.Tensor:
+    """Logical right shift of int64 bit patterns."""
+    return (x >> s) & ((1 << (64 - s)) - 1) if s else x
+
+
+def to_native_fmt2(v: torch.Tensor) -> torch.Tensor:
+    """Resident rank form -> format-2 value (8 x 5-bit AA codes above the 24-bit DNA part), as
+    int64 bit patterns."""
+    r = v >> 24
+    aa = torch.zeros_like(r)
+    for k in range(8):
+        aa |= (r % 21) << (5 * k)
+        r = r // 21
+    low = ((aa & ((1 << 39) - 1)) << 24) | (v & 0xFFFFFF)
+    return torch.where(aa >= (1 << 39), low | INT64_MIN, low)
+
+
+def _words(d: torch.Tensor) -> torch.Tensor:
+    nw = torch.ones_like(d)
+    for gi in range(1, 5):
+        nw += (_lsr(d, 15 * gi) != 0).long()
+    return nw
+
+
+def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk: int = 1 << 27):
+    """Oracle DB (diffIdx / info / split / taxID_list + taxonomy) of the resident DB. The values are
+    read from HBM chunk by chunk; diffIdx words are made on the device (getDiffIdx: big-endian
+    15-bit groups, the last with 0x8000)."""
+    n = rdb.n
+    vals = rdb.values
+    dev = vals.device
+
+    def chunk_deltas(a, b):
+        nat = to_native_fmt2(vals[a:b])
+        prev = to_native_fmt2(vals[a - 1:a]) if a > 0 else torch.zeros(1, dtype=torch.int64, device=dev)
+        return nat - torch.cat([prev, nat[:-1]]), nat
+
+    # pass 1: words per chunk
+    bases = [0]
+    for a in range(0, n, chunk):
+        d, _ = chunk_deltas(a, min(n, a + chunk))
+        bases.append(bases[-1] + int(_words(d).sum().item()))
+    W = bases[-1]
+    # split entries: after every n/(splitNum-1) k-mers, the first later k-mer of a new AA
+    size = n // (split_num - 1) if split_num > 1 else 0
+    gs = []
+    if size:
+        idx = torch.arange(1, split_num, dtype=torch.int64, device=dev) * size - 1
+        idx = idx[(idx >= 0) & (idx < n)]
+        key = ((vals[idx] >> 24) + 1) << 24
+        g_all = torch.searchsorted(vals[:n], key).cpu().numpy()
+        last = -1
+        for gv in g_all.tolist():
+            if gv < n and gv != last:
+                gs.append(gv)
+                last = gv
+    db, diff, info, split = oracle_cls.fillable(rdb.host.c_struct(), W, n, split_num)
+    split[:] = 0
+    gpos = {}  # k-mer index g+1 -> word offset of entry g+1 (start of the next k-mer)
+    want = sorted(set(g + 1 for g in gs))
+    for ci, a in enumerate(range(0, n, chunk)):
+        b = min(n, a + chunk)
+        d, _ = chunk_deltas(a, b)
+        nw = _words(d)
+        off = torch.cumsum(nw, 0) - nw
+        out = torch.empty(int(bases[ci + 1] - bases[ci]), dtype=torch.int32, device=dev)
+        for gi in range(5):
+            sel = nw > gi
+            wv = _lsr(d, 15 * gi) & 0x7FFF
+            if gi == 0:
+                wv = wv | 0x8000
+            out[(off + nw - 1 - gi)[sel]] = wv[sel].int()
+        out = torch.where(out >= 32768, out - 65536, out).to(torch.int16)
+        diff[bases[ci]:bases[ci + 1]] = out.cpu().numpy().view(np.uint16)
+        info[a:b] = rdb.info[a:b].cpu().numpy().view(np.uint32)
+        for w in want:
+            if a <= w < b:
+                gpos[w] = bases[ci] + int(off[w - a].item())
+            elif w == n and b == n:
+                gpos[w] = W
+        del d, nw, off, out
+    for k, gv in enumerate(gs, start=1):
+        if k >= split_num:
+            break
+        split[3 * k] = np.uint64(int(to_native_fmt2(vals[gv:gv + 1]).item()) & ((1 << 64) - 1))
+        split[3 * k + 1] = gpos[gv + 1]
+        split[3 * k + 2] = gv + 1
+    return db

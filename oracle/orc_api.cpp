@@ -92,6 +92,23 @@ void* orc_db_open_host(const mtb_db_host* h, char* err, int errlen) {
     return db;
 }
 
+// A DB whose diffIdx / info / split the caller fills in place (bench: the GTDB-scale DB lives on the
+// GPU and is encoded straight into these buffers, no second host copy). Taxonomy + taxID_list from h.
+void* orc_db_new(const mtb_db_host* h, uint64_t n_diff, uint64_t n_info, uint64_t n_split, void** diff, void** info,
+                 void** split, char* err, int errlen) {
+    mtb_db_host t = *h;
+    t.diff_idx = nullptr, t.n_diff_idx = 0, t.info = nullptr, t.n_info = 0, t.split = nullptr, t.n_split = 0;
+    Db* db = static_cast<Db*>(orc_db_open_host(&t, err, errlen));
+    if (!db) return nullptr;
+    db->diffIdx.resize(n_diff);
+    db->info.resize(n_info);
+    db->split.resize(n_split);
+    *diff = db->diffIdx.data();
+    *info = db->info.data();
+    *split = db->split.data();
+    return db;
+}
+
 void orc_db_close(void* db) { delete static_cast<Db*>(db); }
 
 uint64_t orc_db_kmers(void* db) { return static_cast<Db*>(db)->info.size(); }

@@ -25,6 +25,9 @@ def lib():
         L.orc_db_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i32]
         L.orc_db_open_host.restype = vp
         L.orc_db_open_host.argtypes = [vp, ctypes.c_char_p, i32]
+        L.orc_db_new.restype = vp
+        L.orc_db_new.argtypes = [vp, u64, u64, u64, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                 ctypes.c_char_p, i32]
         L.orc_db_close.argtypes = [vp]
         L.orc_db_kmers.restype = u64
         L.orc_db_kmers.argtypes = [vp]
@@ -78,6 +81,25 @@ class OracleDb:
     @classmethod
     def from_host(cls, host_struct):
         return cls(host_struct=host_struct)
+
+    @classmethod
+    def fillable(cls, host_struct, n_diff: int, n_info: int, n_split: int):
+        """A DB whose diffIdx / info / split the caller writes in place: returns (db, diff, info, split)
+        with numpy views of the oracle's own buffers (no second host copy of a large DB)."""
+        err = ctypes.create_string_buffer(512)
+        pd, pi, ps = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        h = lib().orc_db_new(ctypes.byref(host_struct), n_diff, n_info, n_split, ctypes.byref(pd), ctypes.byref(pi),
+                             ctypes.byref(ps), err, 512)
+        if not h:
+            raise RuntimeError(err.value.decode())
+        db = cls.__new__(cls)
+        db.h = h
+
+        def view(p, n, t):
+            if n == 0:
+                return np.zeros(0, t)
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(t))), shape=(n,))
+        return db, view(pd, n_diff, np.uint16), view(pi, n_info, np.uint32), view(ps, 3 * n_split, np.uint64)
 
     @property
     def n_kmers(self) -> int:

@@ -1,0 +1,80 @@
+"""GTDB-scale DB path at test scale: a DB built in place on the GPU
+(true-signal genomes through the device builder + random-metamer filler over a skeleton taxonomy),
+classified through mtb_open_resident, against the oracle on the same DB re-encoded in the
+reference's diffIdx / info / split format."""
+import numpy as np
+import pytest
+import torch
+
+from metabuli_work_amd import synth
+from tests import oracle_ctypes as oc
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_reads(s1, o1, s2, o2):
+    return synth.Reads(s1.cpu().numpy(), o1.cpu().numpy().astype(np.uint64), s2.cpu().numpy(),
+                       o2.cpu().numpy().astype(np.uint64), np.zeros(o1.numel() - 1, np.int32))
+
+
+def test_device_builder_and_encoder_match_the_file_format():
+    """MTB_BUILD_DEVICE_OUT + encode_into_oracle reproduce mtb_build_db's diffIdx / info / split."""
+    from metabuli_work_amd._abi import default_params
+    from metabuli_work_amd.dbbuild import HostDb, build_db, build_db_device
+    from metabuli_work_amd.gpu_synth import make_genomes_gpu
+    from metabuli_work_amd.gtdb_synth import ResidentDb, encode_into_oracle
+
+    dev = torch.device("cuda", 0)
+    taxo, gen, seq, off_t, _ = make_genomes_gpu(12, 40000, 2, 3, dev)
+    par = default_params(kmer_format=2, seq_mode=2)
+    hdb = build_db(gen, taxo, par, device=0, device_seq=(seq, off_t))
+    v, t = build_db_device(gen, taxo, par, device=0, device_seq=(seq, off_t))
+    n = v.numel()
+    assert n == hdb.n_kmers
+    vals = torch.empty(n + 8, dtype=torch.int64, device=dev)
+    info = torch.empty(n + 8, dtype=torch.int32, device=dev)
+    vals[:n], info[:n] = v, t
+    rdb = ResidentDb(vals, info, n, HostDb(taxo, taxid_list=hdb.taxid_list), n)
+    odb = encode_into_oracle(rdb, _Capture, split_num=4096, chunk=1 << 16)
+    assert np.array_equal(_Capture.diff, hdb.diff_idx)
+    assert np.array_equal(_Capture.info, hdb.info)
+    assert np.array_equal(_Capture.split, hdb.split)
+    odb.close()
+
+
+class _Capture(oc.OracleDb):
+    """OracleDb.fillable that also keeps the filled views for the comparison."""
+
+    @classmethod
+    def fillable(cls, host_struct, n_diff, n_info, n_split):
+        db, d, i, s = oc.OracleDb.fillable(host_struct, n_diff, n_info, n_split)
+        cls.diff, cls.info, cls.split = d, i, s
+        return db, d, i, s
+
+
+def test_gtdb_shaped_resident_db_parity():
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+    from metabuli_work_amd.gpu_synth import make_reads_gpu
+    from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle
+    from tests.test_gpu_parity import compare_results
+
+    dev = torch.device("cuda", 0)
+    got = {}
+
+    def grab(seq, off):
+        got["reads"] = make_reads_gpu(seq, off, 3000, 99, dev)
+
+    rdb = build_gtdb_scale(dev, n_true_species=10, genome_len=30000, total_species=300, target_kmers=3_000_000,
+                           n_chunks=4, before_free=grab)
+    assert rdb.n > 2_500_000 and rdb.n_true > 50_000
+    v = rdb.values[:rdb.n]
+    assert bool((v[1:] >= v[:-1]).all())
+    reads = _host_reads(*got["reads"])
+    par = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    with Classifier(par, db_resident=rdb) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+    odb = encode_into_oracle(rdb, oc.OracleDb, chunk=1 << 20)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    odb.close()
+    compare_results(br.results, br.taxcnt, ores, otc)
+    assert br.results["is_classified"].mean() > 0.5
