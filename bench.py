@@ -35,7 +35,7 @@ from metabuli_work_amd.dbbuild import build_db  # noqa: E402
 from metabuli_work_amd.gpu_synth import make_genomes_gpu, make_long_reads_gpu, make_reads_gpu  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "stage_traffic.json")
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r01", f) for f in ("stage_traffic.json", "stage_traffic_gtdb.json")]
 # the six timed kernels of mtb_last_kernel_ms, by join path (mtb_last_stats[10])
 KERNELS_SORT = ["extract", "filter", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpose", "match_sort", "assign"]
@@ -50,13 +50,64 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def alg_bytes(n, Q, M, D):
+    """Algorithmic bytes per launch of each timed kernel for a batch of n 150-bp pairs (R reserved
+    k-mer slots, Q kept query k-mers, M matches, D DB k-mers)."""
+    read_bytes = 2 * n * 150 + 2 * 8 * (n + 1)
+    R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
+    return {
+        "filter": 8 * R + 4 * R + 20 * Q,                  # keys in, one 4-B membership word per window,
+                                                            # the present (key, slot, DB lower bound) out
+        # probe join: per query its (key, slot, lower bound), 8 DB values + taxIDs from there,
+        # its staged matches (+ rank) out
+        "probe_join": 20 * Q + 96 * Q + 28 * M,
+        "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
+        "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
+        # queries, the DB (values + taxIDs) read once through the block windows, or, when the DB is
+        # much larger than the query stream, each query's run (8 entries), staged matches written
+        "match_join": 12 * Q + min(12 * D, 96 * Q) + 28 * M,
+        "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
+        "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
+        "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
+    }
+
+
+def load_traffic(match):
+    """Per-stage HBM bytes per batch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes over the same
+    workload (tools/pmc_passes.sh + tools/stage_profile.py, committed under profiles/): the first
+    committed file whose keys match `match`."""
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                tf = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if all(tf.get(k) == v for k, v in match.items()):
+            return tf, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def roofline_of(kern, names, n, Q, M, D, traffic):
+    """Roofline of the dominant kernel: algorithmic bytes per launch / its event-timed duration."""
+    alg = alg_bytes(n, Q, M, D)
+    dom = int(np.argmax(kern))
+    dname = names[dom]
+    achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
+    tf, src = traffic
+    hbm = tf["stages"][dname]["hbm_bytes"] if tf and dname in tf.get("stages", {}) else None
+    return {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": hbm,
+            "traffic_source": src if hbm is not None else None, "alg_bytes_per_launch": int(alg[dname]),
+            "avg_launch_ms": round(float(kern[dom]), 3)}
+
+
 # ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=1_000_000, help="read pairs per rank per step")
+    ap.add_argument("--pairs", type=int, default=1_000_000, help="config 2: read pairs per rank per step")
     ap.add_argument("--species", type=int, default=25000)
     ap.add_argument("--mean-genome", type=int, default=75000)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="read pairs timed on the CPU oracle (0 = off)")
@@ -66,6 +117,15 @@ def main():
     ap.add_argument("--db-parts", type=int, default=0,
                     help="config-5 mode: the DB range-partitioned into this many parts (= the number of ranks; "
                          "on one GPU every part is timed in turn)")
+    ap.add_argument("--skip-config2", action="store_true", help="config 3 only (experiments)")
+    ap.add_argument("--gtdb-kmers", type=float, default=12e9,
+                    help="config 3: k-mers of the GTDB-scale DB (0 = skip config 3; config 2 is then the headline)")
+    ap.add_argument("--gtdb-pairs", type=int, default=10_000_000, help="config 3: read pairs per rank per step")
+    ap.add_argument("--gtdb-batch", type=int, default=1_000_000, help="config 3: read pairs per mtb_classify_batch")
+    ap.add_argument("--gtdb-species", type=int, default=129_671)
+    ap.add_argument("--gtdb-true-species", type=int, default=1000)
+    ap.add_argument("--gtdb-genome", type=int, default=3_000_000)
+    ap.add_argument("--gtdb-cpu-sample", type=int, default=1_000_000, help="config 3: read pairs timed on the oracle")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,7 +135,35 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    c2 = run_config2(args, world, rank, local, dev) if not args.skip_config2 or args.db_parts > 1 else None
+    if args.db_parts > 1:
+        return
+    torch.cuda.empty_cache()
+    c3 = run_gtdb(args, world, rank, local, dev) if args.gtdb_kmers > 0 else None
+    if rank == 0:
+        head = c3 if c3 is not None else c2
+        if head is None:
+            return
+        out = {
+            "metric": "reads/sec classified (150bp & 10kb) vs GTDB-scale DB at 1/2/4/8 MI355X",
+            "value": head["value"], "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        }
+        for k, v in head.items():
+            if k not in ("value", "ms_per_step"):
+                out[k] = v
+        if c3 is not None and c2 is not None:
+            out["config2"] = {k: v for k, v in c2.items() if k != "long_reads"}
+        out["long_reads"] = c2.get("long_reads") if c2 is not None else None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def run_config2(args, world, rank, local, dev):
+    """Config 2 (1M x 150 bp pairs vs the RefSeq-viral-sized DB) + the long-read line; returns the
+    line's fields (rank 0)."""
     t0 = time.time()
     par = default_params(kmer_format=2, seq_mode=2)
     taxo, gen, seq, off_t, lens = make_genomes_gpu(args.species, args.mean_genome, 2, args.seed, dev)
@@ -138,42 +226,8 @@ def main():
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     value = world * n * args.steps / elapsed
 
-    # ---- roofline of the dominant kernel: algorithmic bytes per launch / event-timed duration ----
-    read_bytes = 2 * n * 150 + 2 * 8 * (n + 1)
-    R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
     D = hdb.n_kmers
-    alg = {
-        "filter": 8 * R + 4 * R + 20 * Q,                  # keys in, one 4-B membership word per window,
-                                                            # the present (key, slot, DB lower bound) out
-        # probe join: per query its (key, slot, lower bound), 8 DB values + taxIDs from there,
-        # its staged matches (+ rank) out
-        "probe_join": 20 * Q + 96 * Q + 28 * M,
-        "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
-        "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
-        "match_join": 12 * Q + 12 * D + 28 * M,             # queries, the DB (values + taxIDs) streamed through
-                                                            # the block windows once, staged matches written
-        "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
-        "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
-        "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
-    }
-    dom = int(np.argmax(kern))
-    dname = KERNELS[dom]
-    achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
-    # HBM traffic of the same stage per step from rocprofv3 FETCH_SIZE/WRITE_SIZE passes over this
-    # workload (tools/pmc_passes.sh + tools/stage_profile.py, committed under profiles/)
-    traffic, traffic_src = None, None
-    try:
-        with open(TRAFFIC_FILE) as f:
-            tf = json.load(f)
-        if tf.get("pairs") == n and tf.get("species") == args.species and dname in tf["stages"]:
-            traffic = tf["stages"][dname]["hbm_bytes"]
-            traffic_src = os.path.relpath(TRAFFIC_FILE, ROOT)
-    except (OSError, ValueError, KeyError):
-        pass
-    roofline = {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": traffic_src, "alg_bytes_per_launch": int(alg[dname]),
-                "avg_launch_ms": round(float(kern[dom]), 3)}
+    roofline = roofline_of(kern, KERNELS, n, Q, M, D, load_traffic({"pairs": n, "species": args.species}))
 
     # ---- CPU baseline: the oracle (restated reference algorithm, OpenMP) on a bounded sample ----
     cpu = None
@@ -266,29 +320,155 @@ def main():
     if odb is not None:
         odb.close()
 
-    if rank == 0:
-        out = {
-            "metric": "reads/sec classified (150bp & 10kb) vs GTDB-scale DB at 1/2/4/8 MI355X",
-            "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": "config 2: 1M x 150bp paired reads vs RefSeq-viral-sized DB (~10 GB), "
-                                   "format 2, DB + reads resident in HBM",
-                       "read_pairs_per_gpu": n, "read_len": 150, "db_kmers": D,
-                       "db_bytes": db_bytes, "query_kmers": Q, "matches": M,
-                       "parallelism": f"reads sharded, DB replicated x{world}"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "kernel_ms": {k: round(float(v), 3) for k, v in zip(KERNELS, kern)},
-            "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
-            "parity_sample": parity,
-            "work": work,
-            "long_reads": long_line,
-        }
-        print(json.dumps(out), flush=True)
+    out = {
+        "value": round(value, 1), "ms_per_step": round(ms_per_step, 3),
+        "config": {"workload": "config 2: 1M x 150bp paired reads vs RefSeq-viral-sized DB (~10 GB), "
+                               "format 2, DB + reads resident in HBM",
+                   "read_pairs_per_gpu": n, "read_len": 150, "db_kmers": D,
+                   "db_bytes": db_bytes, "query_kmers": Q, "matches": M,
+                   "parallelism": f"reads sharded, DB replicated x{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kernel_ms": {k: round(float(v), 3) for k, v in zip(KERNELS, kern)},
+        "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
+        "parity_sample": parity,
+        "work": work,
+        "long_reads": long_line,
+    }
     clf.close()
+    return out
+
+
+def run_gtdb(args, world, rank, local, dev):
+    """Config 3, the configuration BASELINE.json's metric names: 10M x 150 bp pairs per
+    GPU vs a GTDB-scale DB (~12G k-mers over a 129,671-species skeleton taxonomy: 1000 species x 2
+    strains x ~3 Mbp of true-signal genomes through the GPU builder, the rest random valid metamers),
+    built in place in HBM (gtdb_synth.build_gtdb_scale) and used there (mtb_open_resident). One step
+    = the rank's 10M pairs as 1M-pair QuerySplits (Classifier.cpp:81-133), plus, with N > 1, the
+    all-gather of the per-read result records."""
+    from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle
+
+    t0 = time.time()
+    N, B = args.gtdb_pairs, min(args.gtdb_batch, args.gtdb_pairs)
+    got = {}
+
+    def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
+        got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev)
+
+    rdb = build_gtdb_scale(dev, n_true_species=args.gtdb_true_species, genome_len=args.gtdb_genome,
+                           total_species=args.gtdb_species, target_kmers=int(args.gtdb_kmers), seed=args.seed + 1,
+                           before_free=grab, log=lambda m: log(rank, f"[bench] {m} ({time.time() - t0:.1f}s)"))
+    s1, o1, s2, o2 = got.pop("reads")
+    lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    clf = Classifier(lp, db_resident=rdb, device=local)
+    log(rank, f"[bench] GTDB-scale context open ({time.time() - t0:.1f}s)")
+    L = 150
+    spans = [(a, min(N, a + B)) for a in range(0, N, B)]
+    offs = {}
+    for a, b in spans:
+        if b - a not in offs:
+            offs[b - a] = o1[:b - a + 1].contiguous()
+    res_all = torch.empty((N, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world * N, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev) if world > 1 else None
+    kern = np.zeros(7)
+    stage = np.zeros(5)
+    tot_q = tot_m = 0
+
+    def step(timed):
+        nonlocal kern, stage, tot_q, tot_m
+        for a, b in spans:
+            ob = offs[b - a]
+            clf.classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
+            if timed:
+                kern += clf.kernel_ms()
+                stage += clf.stage_ms()
+                q, m = clf.last_counts()
+                tot_q += q
+                tot_m += m
+            if world > 1:
+                clf.copy_results(res_all[a:b].data_ptr(), on_device=True)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered.view(-1), res_all.view(-1))
+
+    for _ in range(args.warmup):
+        step(False)
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    launches = max(1, args.steps * len(spans))
+    kern /= launches
+    stage /= launches
+    Qb, Mb = tot_q / launches, tot_m / launches  # per 1M-pair batch
+    work = clf.stats()
+    names = kernel_names(work)
+    roofline = roofline_of(kern, names, B, Qb, Mb, rdb.n,
+                           load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}))
+    value = world * N * args.steps / elapsed
+    log(rank, f"[bench] config 3: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
+              f"kernels {dict(zip(names, np.round(kern, 2)))}")
+
+    cpu = parity = None
+    if rank == 0 and args.cpu_sample > 0 and args.gtdb_cpu_sample > 0:
+        from tests import oracle_ctypes as oc  # checker / baseline only
+
+        te = time.perf_counter()
+        odb = encode_into_oracle(rdb, oc.OracleDb)
+        log(rank, f"[bench] oracle DB encoded on the host ({time.perf_counter() - te:.1f}s)")
+        S = min(args.gtdb_cpu_sample, N)
+        h1 = s1[:S * L].cpu().numpy()
+        h2 = s2[:S * L].cpu().numpy()
+        ho = o1[:S + 1].cpu().numpy().astype(np.uint64)
+        reads = synth.Reads(h1, ho, h2, ho.copy(), np.zeros(S, np.int32))
+        cores = len(os.sched_getaffinity(0))
+        cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+        oc.lib().orc_set_threads(cores)
+        opar = lp.to_c()
+        opar.threads = cores
+        stage_s = np.zeros(4)
+        tc0 = time.perf_counter()
+        ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
+        cpu_t = time.perf_counter() - tc0
+        odb.close()
+        cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+               "sample": f"first {S} read pairs of the rank-0 batch, same GTDB-scale DB re-encoded as diffIdx/info/"
+                         f"split; oracle/ (OpenMP C++ restatement of the reference path), {cpu_t:.1f}s wall",
+               "stage_s": [round(x, 3) for x in stage_s]}
+        gb = clf.classify_batch(h1, ho, h2, ho.copy())
+        parity = bool(np.array_equal(gb.results["classification"], ores["classification"])
+                      and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
+                      and np.array_equal(gb.taxcnt, otc))
+        log(rank, f"[bench] config 3 CPU oracle: {cpu['value']} reads/s, parity {parity}")
+    clf.close()
+    out = {
+        "value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": "config 3: 10M x 150bp paired reads per GPU vs a GTDB-scale DB (~12G k-mers, "
+                               "129,671-species skeleton taxonomy), format 2, DB + reads resident in HBM, "
+                               f"{B}-pair batches",
+                   "read_pairs_per_gpu": N, "batch_pairs": B, "read_len": L, "db_kmers": rdb.n,
+                   "db_true_signal_kmers": rdb.n_true, "db_resident_bytes": rdb.n * 12,
+                   "query_kmers_per_batch": int(Qb), "matches_per_batch": int(Mb),
+                   "parallelism": f"reads sharded, DB replicated x{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kernel_ms": {k: round(float(v), 3) for k, v in zip(names, kern)},
+        "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
+        "parity_sample": parity,
+        "work": work,
+    }
+    del rdb
+    torch.cuda.empty_cache()
+    return out
 
 
 def run_partitioned(args, lp, hdb, batch, world, rank, local, dev):

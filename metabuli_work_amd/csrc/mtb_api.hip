@@ -212,6 +212,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
         build_probe_lines(c->dbv, c->D, c->dir, c->lines, s);
     }
+    HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
     HIP_TRY(hipStreamSynchronize(s));
     // taxonomy + taxId2speciesId
     const HostTaxonomy& T = db.tax;
@@ -632,6 +633,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
         if (rc != MTB_OK) return rc;
     }
     HIP_TRY(hipEventRecord(c->ev[4], s));
+    HIP_TRY(hipGetLastError());
     int err = 0;
     unsigned long long dstat[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));

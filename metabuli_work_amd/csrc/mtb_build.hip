@@ -134,27 +134,26 @@ struct TaxLca {
 // Group heads of equal (value, species) and the group's taxID = NcbiTaxonomy::LCA(vector).
 __global__ void k_group_heads(const uint64_t* __restrict__ v, const uint64_t* __restrict__ pay, uint64_t n,
                               uint32_t* __restrict__ head) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    head[i] = (i == 0 || v[i] != v[i - 1] || (pay[i] >> 32) != (pay[i - 1] >> 32)) ? 1u : 0u;
+    MTB_GRID_STRIDE(i, n) head[i] = (i == 0 || v[i] != v[i - 1] || (pay[i] >> 32) != (pay[i - 1] >> 32)) ? 1u : 0u;
 }
 
 __global__ void k_group_reduce(const uint64_t* __restrict__ v, const uint64_t* __restrict__ pay, uint64_t n,
                                const uint32_t* __restrict__ head, const uint64_t* __restrict__ uidx, TaxLca tax,
                                uint64_t* __restrict__ uval, uint32_t* __restrict__ uinfo) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !head[i]) return;
-    const uint32_t sp = (uint32_t)(pay[i] >> 32);
-    int red = -1;
-    for (uint64_t j = i; j < n && v[j] == v[i] && (uint32_t)(pay[j] >> 32) == sp; j++) {
-        int32_t t = (int32_t)(uint32_t)pay[j];
-        if (!tax.exists(t)) continue;
-        int nd = tax.nodeOf[t];
-        red = red < 0 ? nd : tax.lca_node(red, nd);
+    MTB_GRID_STRIDE(i, n) {
+        if (!head[i]) continue;
+        const uint32_t sp = (uint32_t)(pay[i] >> 32);
+        int red = -1;
+        for (uint64_t j = i; j < n && v[j] == v[i] && (uint32_t)(pay[j] >> 32) == sp; j++) {
+            int32_t t = (int32_t)(uint32_t)pay[j];
+            if (!tax.exists(t)) continue;
+            int nd = tax.nodeOf[t];
+            red = red < 0 ? nd : tax.lca_node(red, nd);
+        }
+        const uint64_t u = uidx[i];
+        uval[u] = v[i];
+        uinfo[u] = red >= 0 ? (uint32_t)tax.nodeTax[red] : (uint32_t)pay[i];
     }
-    const uint64_t u = uidx[i];
-    uval[u] = v[i];
-    uinfo[u] = red >= 0 ? (uint32_t)tax.nodeTax[red] : (uint32_t)pay[i];
 }
 
 __device__ __forceinline__ uint32_t diff_words(uint64_t d) {
@@ -165,22 +164,21 @@ __device__ __forceinline__ uint32_t diff_words(uint64_t d) {
 }
 
 __global__ void k_count_words(const uint64_t* __restrict__ uval, uint64_t U, uint32_t* __restrict__ words) {
-    uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < U) words[u] = diff_words(uval[u] - (u ? uval[u - 1] : 0ull));
+    MTB_GRID_STRIDE(u, U) words[u] = diff_words(uval[u] - (u ? uval[u - 1] : 0ull));
 }
 
 __global__ void k_write_words(const uint64_t* __restrict__ uval, uint64_t U, const uint64_t* __restrict__ woff,
                               uint16_t* __restrict__ diff) {
-    uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= U) return;
-    uint64_t d = uval[u] - (u ? uval[u - 1] : 0ull);
-    uint64_t o = woff[u], e = woff[u + 1];
-    // getDiffIdx: last group carries the 0x8000 end flag, groups big-endian
-    diff[e - 1] = (uint16_t)(0x8000u | (uint32_t)(d & 0x7FFFu));
-    d >>= 15;
-    for (uint64_t k = e - 1; k > o; k--) {
-        diff[k - 1] = (uint16_t)(d & 0x7FFFu);
+    MTB_GRID_STRIDE(u, U) {
+        uint64_t d = uval[u] - (u ? uval[u - 1] : 0ull);
+        uint64_t o = woff[u], e = woff[u + 1];
+        // getDiffIdx: last group carries the 0x8000 end flag, groups big-endian
+        diff[e - 1] = (uint16_t)(0x8000u | (uint32_t)(d & 0x7FFFu));
         d >>= 15;
+        for (uint64_t k = e - 1; k > o; k--) {
+            diff[k - 1] = (uint16_t)(d & 0x7FFFu);
+            d >>= 15;
+        }
     }
 }
 
@@ -336,14 +334,14 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxo, const mtb_p
     }
     HIP_B(hipMalloc(&head, 4 * (kept + 1)));
     HIP_B(hipMalloc(&uidx, 8 * (kept + 1)));
-    if (kept) k_group_heads<<<(unsigned)((kept + 255) / 256), 256, 0, s>>>(sk, sp_, kept, head);
+    if (kept) k_group_heads<<<stride_grid(kept), 256, 0, s>>>(sk, sp_, kept, head);
     exclusive_scan_u32(head, kept, uidx, scanTmp, s);
     HIP_B(hipMemcpyAsync(&U, uidx + kept, 8, hipMemcpyDeviceToHost, s));
     HIP_B(hipStreamSynchronize(s));
     HIP_B(hipMalloc(&uval, 8 * (U + kDbPad)));
     HIP_B(hipMalloc(&uinfo, 4 * (U + kDbPad)));
     if (kept)
-        k_group_reduce<<<(unsigned)((kept + 255) / 256), 256, 0, s>>>(
+        k_group_reduce<<<stride_grid(kept), 256, 0, s>>>(
             sk, sp_, kept, head, uidx, TaxLca{tNodeOf, tNodeTax, tParent, tDepth, T.maxTax}, uval, uinfo);
     if (in->flags & MTB_BUILD_DEVICE_OUT) {  // resident form for mtb_open_resident; no diffIdx / split
         if (par->kmer_format == 2) launch_to_rank_form(uval, U, s);
@@ -358,12 +356,12 @@ int mtb_build_db(const mtb_build_input* in, const mtb_db_host* taxo, const mtb_p
     // diffIdx words
     HIP_B(hipMalloc(&words, 4 * (U + 1)));
     HIP_B(hipMalloc(&woff, 8 * (U + 1)));
-    if (U) k_count_words<<<(unsigned)((U + 255) / 256), 256, 0, s>>>(uval, U, words);
+    if (U) k_count_words<<<stride_grid(U), 256, 0, s>>>(uval, U, words);
     exclusive_scan_u32(words, U, woff, scanTmp, s);
     HIP_B(hipMemcpyAsync(&NW, woff + U, 8, hipMemcpyDeviceToHost, s));
     HIP_B(hipStreamSynchronize(s));
     HIP_B(hipMalloc(&dDiff, 2 * (NW + 1)));
-    if (U) k_write_words<<<(unsigned)((U + 255) / 256), 256, 0, s>>>(uval, U, woff, dDiff);
+    if (U) k_write_words<<<stride_grid(U), 256, 0, s>>>(uval, U, woff, dDiff);
     // split table: the distinct first-AA-change indices after every uniqKmerCnt/(splitNum-1) k-mers
     sizeOfSplit = in->split_num > 1 ? U / (uint64_t)(in->split_num - 1) : 0;
     HIP_B(hipMalloc(&gend, 8 * (size_t)std::max(1, in->split_num)));

@@ -547,31 +547,31 @@ template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, ui
 // k-mer index by scan -> per-k-mer delta from its <= 5 15-bit groups -> values by 64-bit scan.
 // ------------------------------------------------------------------------------------------------
 __global__ void k_term_flags(const uint16_t* __restrict__ diff, uint64_t n, uint32_t* __restrict__ flag) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = (diff[i] & 0x8000u) ? 1u : 0u;
+    MTB_GRID_STRIDE(i, n) flag[i] = (diff[i] & 0x8000u) ? 1u : 0u;
 }
 
 __global__ void k_deltas(const uint16_t* __restrict__ diff, uint64_t n, const uint64_t* __restrict__ termIdx,
                          uint64_t* __restrict__ delta) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !(diff[i] & 0x8000u)) return;
-    uint64_t d = diff[i] & 0x7FFFu;
-    int sh = 15;
-    for (uint64_t j = i; j > 0; j--) {
-        uint16_t w = diff[j - 1];
-        if (w & 0x8000u) break;
-        d |= (uint64_t)w << sh;
-        sh += 15;
+    MTB_GRID_STRIDE(i, n) {
+        if (!(diff[i] & 0x8000u)) continue;
+        uint64_t d = diff[i] & 0x7FFFu;
+        int sh = 15;
+        for (uint64_t j = i; j > 0; j--) {
+            uint16_t w = diff[j - 1];
+            if (w & 0x8000u) break;
+            d |= (uint64_t)w << sh;
+            sh += 15;
+        }
+        delta[termIdx[i]] = d;
     }
-    delta[termIdx[i]] = d;
 }
 
 void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
                      uint64_t* idxTmp, void* scanTmp, hipStream_t s) {
     if (nDiff == 0) return;
-    k_term_flags<<<(unsigned)((nDiff + 255) / 256), 256, 0, s>>>(diff, nDiff, flagTmp);
+    k_term_flags<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, flagTmp);
     exclusive_scan_u32(flagTmp, nDiff, idxTmp, scanTmp, s);
-    k_deltas<<<(unsigned)((nDiff + 255) / 256), 256, 0, s>>>(diff, nDiff, idxTmp, values);
+    k_deltas<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, idxTmp, values);
     // inclusive scan of deltas = exclusive scan shifted by one: scan into idxTmp then take [1..]
     exclusive_scan_u64(values, nKmers, idxTmp, scanTmp, s);
     hipMemcpyAsync(values, idxTmp + 1, nKmers * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
@@ -624,12 +624,11 @@ __host__ __device__ inline uint64_t from_rank_form(uint64_t v) {
 }
 
 __global__ void k_to_rank_form(uint64_t* __restrict__ v, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) v[i] = to_rank_form(v[i]);
+    MTB_GRID_STRIDE(i, n) v[i] = to_rank_form(v[i]);
 }
 
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
-    if (n) k_to_rank_form<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(v, n);
+    if (n) k_to_rank_form<<<stride_grid(n), 256, 0, s>>>(v, n);
 }
 
 uint64_t host_from_rank_form(uint64_t v) { return from_rank_form(v); }
@@ -682,19 +681,19 @@ __global__ void k_line_count(ProbeLine* __restrict__ lines) {
 
 // Membership bits: the first k-mer of each AA run sets its rank's bit.
 __global__ void k_line_bits(const uint64_t* __restrict__ dbv, uint64_t D, ProbeLine* __restrict__ lines) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= D) return;
-    const uint64_t r = dbv[i] >> 24;
-    if (i > 0 && (dbv[i - 1] >> 24) == r) return;
-    uint32_t bit;
-    const uint32_t* w = line_word(lines, r, bit);
-    atomicOr(const_cast<uint32_t*>(w), 1u << bit);
+    MTB_GRID_STRIDE(i, D) {
+        const uint64_t r = dbv[i] >> 24;
+        if (i > 0 && (dbv[i - 1] >> 24) == r) continue;
+        uint32_t bit;
+        const uint32_t* w = line_word(lines, r, bit);
+        atomicOr(const_cast<uint32_t*>(w), 1u << bit);
+    }
 }
 
 void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines, hipStream_t s) {
     k_line_base<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(dbv, D, dir, lines);
     k_line_count<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines);
-    if (D) k_line_bits<<<(unsigned)((D + 255) / 256), 256, 0, s>>>(dbv, D, lines);
+    if (D) k_line_bits<<<stride_grid(D), 256, 0, s>>>(dbv, D, lines);
 }
 
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
@@ -1188,12 +1187,11 @@ void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint6
 }
 
 __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) info[i] &= mask;
+    MTB_GRID_STRIDE(i, n) info[i] &= mask;
 }
 
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s) {
-    if (n) k_mask_info<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(info, n, mask);
+    if (n) k_mask_info<<<stride_grid(n), 256, 0, s>>>(info, n, mask);
 }
 
 }  // namespace mtb

@@ -56,6 +56,14 @@ struct AssignScratch {  // per match unless noted
 
 // scans (out has n+1 entries; tmp needs scan_tmp_elems(n) u64)
 uint64_t scan_tmp_elems(uint64_t n);
+// Grid of a grid-stride launch over n items: one launch holds < 2^32 work-items in x, and DB-wide
+// arrays (12G k-mers at GTDB scale, ~30G diffIdx words) are larger.
+inline unsigned stride_grid(uint64_t n, unsigned block = 256) {
+    const uint64_t b = (n + block - 1) / block;
+    return (unsigned)(b < 1 ? 1 : (b > (1ull << 22) ? (1ull << 22) : b));
+}
+#define MTB_GRID_STRIDE(i, n) \
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (uint64_t)gridDim.x * blockDim.x)
 void exclusive_scan_u32(const uint32_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
 void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
 
