@@ -375,7 +375,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     if (maxSeg > kSegSortLds || c->forceGeneric) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
     HIP_TRY(hipEventRecord(c->kev[10], s));
     launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg > 128, maxSeg > 512, c->forceGeneric, s);
+                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric, s);
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(hipEventRecord(c->kev[12], s));
     for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
@@ -517,7 +517,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
-                         c->probeStats.as<unsigned long long>(), s);
+                         c->lines, c->probeStats.as<unsigned long long>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

@@ -21,10 +21,10 @@ struct Path {  // MatchPath (Taxonomer.h:35-59); start/end match as indices into
 // K5 segmented sort of each read's matches into compareMatches order (KmerMatcher.cpp:1149-1166).
 // Key = (species:32 | frame:3 | pos:29, hamming:8 | dna:24 | target:32), compared as 128 bits;
 // the last field only makes the order total (a valid DB never ties before it).
-// Small segments (<= 512): one wave64 per read, bitonic sort of keys + 16-bit indices in LDS, then
-// a gather-permute of the 24-B records into the output segment (contiguous writes).
-// Larger segments: one 256-thread block per read, bitonic sort in LDS (<= 4096) or, beyond that,
-// in a global key scratch.
+// Small segments (<= 512): one wave64 per read, register-resident bitonic sort of keys + indices
+// (up to 8 per lane, cross-lane shuffles), then a gather-permute of the 24-B records into the
+// output segment (contiguous writes). Larger segments: one 1024-thread block per read, bitonic
+// sort in LDS (<= 8192) or, beyond that, in a global key scratch.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void match_key(const mtb_match& m, uint64_t& hi, uint64_t& lo) {
     hi = ((uint64_t)m.species_id << 32) | ((uint64_t)info_frame(m.qinfo) << 29) | (info_pos(m.qinfo) & 0x1FFFFFFFu);
@@ -35,8 +35,7 @@ __device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, ui
     return ah > bh || (ah == bh && al > bl);
 }
 
-constexpr int kSmallSeg = 512;
-constexpr int kRegSeg = 128;  // segments up to this many matches sort in registers
+constexpr int kSmallSeg = 512;  // segments up to this many matches sort in registers (one wave, <= 8 per lane)
 constexpr int kBlockSeg = 8192;
 
 // Segments of up to 64E matches sort in registers: element e = 64*slot + lane. Exchanges at
@@ -105,51 +104,27 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
-    if (n == 0 || n > kSmallSeg) return;
+    if (n == 0 || n > 128) return;
     const int lane = threadIdx.x;
     if (n == 1) {
         if (lane == 0) out[base] = in[base];
         return;
     }
     if (n <= 64) segsort_regs<1>(in, out, base, n, lane);
-    else if (n <= kRegSeg) segsort_regs<2>(in, out, base, n, lane);
+    else if (n <= 128) segsort_regs<2>(in, out, base, n, lane);
 }
 
-// 129..512 matches: one wave, bitonic network over LDS.
-__global__ void __launch_bounds__(64) k_segsort_mid(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
-                                                    uint32_t nReads, mtb_match* __restrict__ out) {
-    __shared__ uint64_t sh[kSmallSeg], sl[kSmallSeg];
-    __shared__ uint16_t si[kSmallSeg];
+// 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
+// lane, in kernels of their own so the small kernel keeps its register budget (occupancy).
+template <int E>
+__global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                     uint32_t nReads, mtb_match* __restrict__ out) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
-    if (n <= kRegSeg || n > kSmallSeg) return;
-    const int lane = threadIdx.x;
-    int p2 = 2;
-    while (p2 < n) p2 <<= 1;
-    for (int i = lane; i < p2; i += 64) {
-        uint64_t h = ~0ull, l = ~0ull;
-        if (i < n) match_key(in[base + i], h, l);
-        sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
-    }
-    __syncthreads();
-    for (int k = 2; k <= p2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = lane; t < (p2 >> 1); t += 64) {
-                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                const int ixj = i + j;
-                const bool up = (i & k) == 0;
-                uint64_t ah = sh[i], al = sl[i], bh = sh[ixj], bl = sl[ixj];
-                if (key_gt(ah, al, bh, bl) == up) {
-                    sh[i] = bh; sl[i] = bl; sh[ixj] = ah; sl[ixj] = al;
-                    uint16_t x = si[i]; si[i] = si[ixj]; si[ixj] = x;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = lane; i < n; i += 64) out[base + i] = in[base + si[i]];
+    if (n <= 32 * E || n > 64 * E) return;
+    segsort_regs<E>(in, out, base, n, (int)threadIdx.x);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -224,15 +199,16 @@ __global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* 
 }
 
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, bool anyMid, bool anyLarge, bool global, hipStream_t s) {
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, hipStream_t s) {
     if (nReads == 0) return;
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1);
         return;
     }
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (anyMid) k_segsort_mid<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (anyLarge) k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0);
+    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
+    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
+    if (maxSeg > kSmallSeg) k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0);
 }
 
 __global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {

@@ -329,6 +329,31 @@ __device__ __forceinline__ const uint32_t* line_word(const ProbeLine* lines, uin
     return &lines[L].bits[o >> 5];
 }
 
+// DB index of the first k-mer of AA rank x, or below it: the line's base plus the present ranks
+// before x in the line (each holds >= 1 DB k-mer). One 64-B line read.
+__device__ __forceinline__ uint64_t line_lower_bound_at(const ProbeLine* line, uint32_t o) {
+    const uint4* lp = reinterpret_cast<const uint4*>(line);
+    const uint4 q0 = lp[0], q1 = lp[1], q2 = lp[2], q3 = lp[3];
+    const uint32_t w[14] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    uint32_t before = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        const uint32_t wi = (uint32_t)i;
+        const uint32_t m = wi < (o >> 5) ? ~0u : (wi == (o >> 5) ? ((1u << (o & 31u)) - 1u) : 0u);
+        before += __popc(w[i] & m);
+    }
+    return (((uint64_t)q0.x | (uint64_t)q0.y << 32) & ((1ull << 40) - 1)) + before;
+}
+
+__device__ __forceinline__ uint64_t line_lower_bound(const ProbeLine* __restrict__ lines, uint64_t x) {
+    const uint64_t L = x / kLineRanks;
+    return line_lower_bound_at(lines + L, (uint32_t)(x - L * kLineRanks));
+}
+
+// First index >= lo with a[i] >= key (an answer exists below D + kDbPad: the pad is ~0).
+__device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key);
+__device__ __forceinline__ uint64_t gallop_lower1(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key);
+
 __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                  const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                  const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -703,6 +728,8 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
 // directory instead.
 constexpr int kMatchQ = 256;
 constexpr int kMatchWin = 3072;
+constexpr uint32_t kStageFreeRatio = 24;  // D / Q above which K4 runs without LDS windows
+constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
 __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
@@ -809,6 +836,7 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
 // kStageRegions), so the claims do not all queue on one address. A later pass moves each match
 // into its read's segment (k_match_transpose). A region that would overflow is not written; the
 // caller grows the regions to the largest count and reruns.
+template <bool kStage>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const uint64_t* __restrict__ dbv,
@@ -817,9 +845,12 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
                                                mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
                                                uint64_t region, int* __restrict__ err, uint32_t winCap, const uint64_t* __restrict__ win,
-                                               unsigned long long* __restrict__ stats) {
-    __shared__ uint64_t sDb[kMatchWin];
-    __shared__ uint32_t sInfo[kMatchWin];
+                                               const ProbeLine* __restrict__ lines, unsigned long long* __restrict__ stats) {
+    // without staging (a DB much larger than the query stream: windows over the LDS cap) the
+    // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
+    __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
+    __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
+    __shared__ ProbeLine sLines[kStage ? 1 : kMatchLines];  // the block's probe lines (sorted queries)
     __shared__ unsigned long long sBase;
     constexpr int kPer = kMatchQ / 256;
     const uint64_t q0 = (uint64_t)blockIdx.x * kMatchQ;
@@ -837,9 +868,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         slot[j] = live[j] ? qslot[q] : 0;
     }
     const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
-    const bool staged = winN <= (uint64_t)winCap;
+    const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
-    if (staged) {
+    if (kStage && staged) {
         constexpr int kLoad = kMatchWin / 256;
         uint64_t v[kLoad];
         uint32_t tv[kLoad];
@@ -868,7 +899,30 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             lo[j] = l;
             hi[j] = h;
         }
-    } else {
+    } else if (lines) {  // HBM: the probe line names a lower bound of the run, a gallop finds its ends
+        // sorted queries: the block's probe lines are one contiguous stretch (its sort-prefix range),
+        // staged through LDS with coalesced loads unless it is long
+        const int sh = kQuerySortLo - 24;
+        const uint64_t L0 = ((qkey[q0] >> kQuerySortLo) << sh) / kLineRanks;
+        const uint64_t L1 = ((((qkey[q1 - 1] >> kQuerySortLo) + 1) << sh) - 1) / kLineRanks;
+        const bool inLds = !kStage && L1 - L0 < (uint64_t)kMatchLines;
+        if (!kStage && inLds) {
+            const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;  // 4 x 16 B per line
+            const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
+            uint4* dst = reinterpret_cast<uint4*>(sLines);
+            for (uint32_t i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+            __syncthreads();
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const uint64_t aa = key[j] & kAAMask, x = aa >> 24, L = x / kLineRanks;
+            const uint32_t o = (uint32_t)(x - L * kLineRanks);
+            const uint64_t from = !live[j] ? 0
+                                  : inLds ? line_lower_bound_at(sLines + (L - L0), o) : line_lower_bound_at(lines + L, o);
+            lo[j] = live[j] ? gallop_lower1(dbv, from, aa) : 0;
+            hi[j] = live[j] ? gallop_lower1(dbv, lo[j], aa + (1ull << 24)) : 0;
+        }
+    } else {  // HBM through the AA-prefix directory (no probe lines: MTB_FORCE_GENERIC)
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint64_t aa = key[j] & kAAMask;
@@ -984,21 +1038,7 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
         if (!((mask >> j) & 1u)) continue;
         qkey[pos] = k[j];
         qslot[pos] = (uint32_t)(base + 256ull * j);
-        if (FROM) {
-            const uint64_t x = k[j] >> 24, L = x / kLineRanks;
-            const uint32_t o = (uint32_t)(x - L * kLineRanks);
-            const uint4* lp = reinterpret_cast<const uint4*>(lines + L);
-            const uint4 q0 = lp[0], q1 = lp[1], q2 = lp[2], q3 = lp[3];
-            const uint32_t w[14] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-            uint32_t before = 0;
-#pragma unroll
-            for (int i = 0; i < 14; i++) {
-                const uint32_t wi = (uint32_t)i;
-                const uint32_t m = wi < (o >> 5) ? ~0u : (wi == (o >> 5) ? ((1u << (o & 31u)) - 1u) : 0u);
-                before += __popc(w[i] & m);
-            }
-            qfrom[pos] = line_base((uint64_t)q0.x | (uint64_t)q0.y << 32) + before;
-        }
+        if (FROM) qfrom[pos] = line_lower_bound(lines, k[j] >> 24);
         pos++;
     }
 }
@@ -1025,6 +1065,18 @@ uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines,
 // that follows are k_match's, so the matches are identical.
 // ------------------------------------------------------------------------------------------------
 // First index >= lo with a[i] >= key (an answer exists below D + kDbPad: the pad is ~0).
+// First index >= lo with a[i] >= key, by galloping from lo in steps 1, 2, 4, ... (runs at GTDB
+// scale are 1-2 k-mers: the first probes stay in lo's line).
+__device__ __forceinline__ uint64_t gallop_lower1(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key) {
+    uint64_t step = 1, hi = lo;
+    while (a[hi] < key) {
+        lo = hi + 1;
+        hi += step;
+        step *= 2;
+    }
+    return lower_bound_u64(a, lo, hi, key);
+}
+
 __device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key) {
     uint64_t step = 8, hi = lo;
     while (a[hi] < key) {
@@ -1169,12 +1221,18 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
-                  unsigned long long* stats, hipStream_t s) {
+                  const ProbeLine* lines, unsigned long long* stats, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
-    k_match<<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat, readCnt,
-                                   total, buf, bufRank, region, err, winCap, win, stats);
+    // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
+    // HBM path anyway
+    if (lines && (D > (uint64_t)kStageFreeRatio * Q || winCap == 0))
+        k_match<false><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
+                                              readCnt, total, buf, bufRank, region, err, winCap, win, lines, stats);
+    else
+        k_match<true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
+                                             readCnt, total, buf, bufRank, region, err, winCap, win, lines, stats);
 }
 
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,

@@ -146,8 +146,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
-                  unsigned long long* stats,
-                  hipStream_t s);  // stats[0] += queries with >= 1 match
+                  const ProbeLine* lines, unsigned long long* stats, hipStream_t s);  // stats[0] += queries with >= 1 match
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,
                             const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
@@ -158,10 +157,10 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 
 uint64_t path_bytes();
 uint64_t clade_bytes();
-// K5; anyMid / anyLarge: some read has more than 128 / 512 matches; global: every segment through
-// the global-scratch network (gScratch 6*M words; parity tests of the general path)
+// K5; maxSeg: the most matches of one read (picks the kernels to launch); global: every segment
+// through the global-scratch network (gScratch 6*M words; parity tests of the general path)
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, bool anyMid, bool anyLarge, bool global, hipStream_t s);
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 8192;
