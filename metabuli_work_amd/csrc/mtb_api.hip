@@ -78,8 +78,10 @@ struct mtb_ctx {
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
     DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, waveList, waveCount, devStats;
     DevBuf qFrom, probeStats;
-    DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging  // probe join: DB lower bounds of the filtered queries; striped counters
-    static constexpr int kNumStats = 11;
+    DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
+    DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
+    uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
+    static constexpr int kNumStats = 12;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -293,7 +295,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -373,9 +375,29 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (maxSeg > kSegSortLds || c->forceGeneric) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
+    // dead matches (no frame run of two in their species) are dropped in K5 unless the batch keeps
+    // its stages (mtb_get_matches returns every match) or runs the general paths
+    const bool prune = !c->keepStages && !c->forceGeneric;
+    HIP_TRY(c->liveCnt.ensure(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
     launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric, s);
+                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric, prune ? c->liveCnt.as<uint32_t>() : nullptr, s);
+    const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
+    const uint64_t* kOff = c->mOff.as<uint64_t>();
+    uint64_t kM = M;
+    if (prune) {
+        exclusive_scan_u32(c->liveCnt.as<uint32_t>(), n, c->liveOff.as<uint64_t>(), c->scanTmp.p, s);
+        HIP_TRY(hipMemcpyAsync(&kM, c->liveOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        launch_pack_live(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->liveOff.as<uint64_t>(), n,
+                         c->matches.as<mtb_match>(), s);  // K5's input buffer is free again
+        HIP_TRY(hipStreamSynchronize(s));
+        kIn = c->matches.as<mtb_match>();
+        kOff = c->liveOff.as<uint64_t>();
+    }
+    c->liveM = kM;
+    c->stats[11] = kM;
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(hipEventRecord(c->kev[12], s));
     for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
@@ -409,9 +431,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                      c->cladePerMatch};
     c->stats[3] = M;
     c->stats[4] = maxSeg;
-    launch_assign(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->qlen.as<uint32_t>(),
-                  n, M, a, t, sc, c->tcPool.as<mtb_taxcnt>(), c->results.as<mtb_result>(),
-                  c->devStats.as<unsigned long long>(), c->stats + 5, s);
+    launch_assign(kIn, kOff, c->qlen.as<uint32_t>(), n, kM, a, t, sc, c->tcPool.as<mtb_taxcnt>(),
+                  c->results.as<mtb_result>(), c->devStats.as<unsigned long long>(), c->stats + 5, s);
     HIP_TRY(hipEventRecord(c->kev[13], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->tcOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -421,8 +442,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(hipMemcpyAsync(&NT, c->tcOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(c->tcOut.ensure(sizeof(mtb_taxcnt) * std::max<uint64_t>(NT, 1)));
-    launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), c->mOff.as<uint64_t>(), c->results.as<mtb_result>(),
-                          c->tcOff.as<uint64_t>(), n, c->tcOut.as<mtb_taxcnt>(), s);
+    launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), kOff, c->results.as<mtb_result>(), c->tcOff.as<uint64_t>(), n,
+                          c->tcOut.as<mtb_taxcnt>(), s);
     c->nTaxcnt = NT;
     return MTB_OK;
 }

@@ -77,9 +77,16 @@ __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l
     }
 }
 
+// Dead matches: a (species, frame) run of one match is never given to getMatchPaths
+// (Taxonomer.cpp:334-344), so a species none of whose frame runs has two matches gets no path and
+// no score; it can be neither the best species nor in bestSpeciesRange, the only matches
+// filterRedundantMatches reads (Taxonomer.cpp:141-172,205-241). Its matches change nothing
+// downstream and are dropped here (prune): the sorted segment is written front-packed with only
+// the live matches, their count in liveCnt[r].
 template <int E>
 __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
-                                             uint64_t base, int n, int lane) {
+                                             uint64_t base, int n, int lane, uint32_t* __restrict__ liveCnt,
+                                             uint32_t r) {
     uint64_t h[E], l[E];
     uint32_t x[E];
 #pragma unroll
@@ -91,40 +98,82 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
         if (e < n) match_key(in[base + e], h[sl], l[sl]);
     }
     wave_bitonic_sort<E>(h, l, x, lane);
+    if (!liveCnt) {
+#pragma unroll
+        for (int sl = 0; sl < E; sl++) {
+            const int e = 64 * sl + lane;
+            if (e < n) out[base + e] = in[base + x[sl]];
+        }
+        return;
+    }
+    __shared__ uint8_t runLive[64 * E];
+    const uint64_t lt = (1ull << lane) - 1;
+    bool pair[E];
+    uint32_t rid[E];
+    uint32_t runs = 0;
 #pragma unroll
     for (int sl = 0; sl < E; sl++) {
         const int e = 64 * sl + lane;
-        if (e < n) out[base + e] = in[base + x[sl]];
+        const uint64_t sf = h[sl] >> 29;  // species << 3 | frame
+        uint64_t nx = __shfl_down(sf, 1, 64), pv = __shfl_up(sf, 1, 64);
+        const uint64_t nxSlot = sl + 1 < E ? __shfl(h[sl + 1 < E ? sl + 1 : sl] >> 29, 0, 64) : ~0ull;
+        const uint64_t pvSlot = sl > 0 ? __shfl(h[sl > 0 ? sl - 1 : 0] >> 29, 63, 64) : ~0ull;
+        if (lane == 63) nx = nxSlot;
+        if (lane == 0) pv = pvSlot;
+        pair[sl] = e + 1 < n && nx == sf;
+        const bool start = e < n && (e == 0 || (pv >> 3) != (sf >> 3));
+        const uint64_t m = __ballot(start);
+        rid[sl] = runs + (uint32_t)__popcll(m & lt) + (uint32_t)start - 1u;  // starts at or before e, - 1
+        runs += (uint32_t)__popcll(m);
+        runLive[64 * sl + lane] = 0;
     }
+    __syncthreads();
+#pragma unroll
+    for (int sl = 0; sl < E; sl++)
+        if (pair[sl]) runLive[rid[sl]] = 1;
+    __syncthreads();
+    uint32_t kept = 0;
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        const bool live = e < n && runLive[rid[sl]];
+        const uint64_t m = __ballot(live);
+        if (live) out[base + kept + (uint32_t)__popcll(m & lt)] = in[base + x[sl]];
+        kept += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) liveCnt[r] = kept;
 }
 
 __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
-                                                      uint32_t nReads, mtb_match* __restrict__ out) {
+                                                      uint32_t nReads, mtb_match* __restrict__ out,
+                                                      uint32_t* __restrict__ liveCnt) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
-    if (n == 0 || n > 128) return;
+    if (n > 128) return;
     const int lane = threadIdx.x;
-    if (n == 1) {
-        if (lane == 0) out[base] = in[base];
+    if (n <= 1) {  // a lone match is a dead species run
+        if (lane == 0 && n == 1 && !liveCnt) out[base] = in[base];
+        if (lane == 0 && liveCnt) liveCnt[r] = 0;
         return;
     }
-    if (n <= 64) segsort_regs<1>(in, out, base, n, lane);
-    else if (n <= 128) segsort_regs<2>(in, out, base, n, lane);
+    if (n <= 64) segsort_regs<1>(in, out, base, n, lane, liveCnt, r);
+    else segsort_regs<2>(in, out, base, n, lane, liveCnt, r);
 }
 
 // 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
 // lane, in kernels of their own so the small kernel keeps its register budget (occupancy).
 template <int E>
 __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
-                                                     uint32_t nReads, mtb_match* __restrict__ out) {
+                                                     uint32_t nReads, mtb_match* __restrict__ out,
+                                                     uint32_t* __restrict__ liveCnt) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n <= 32 * E || n > 64 * E) return;
-    segsort_regs<E>(in, out, base, n, (int)threadIdx.x);
+    segsort_regs<E>(in, out, base, n, (int)threadIdx.x, liveCnt, r);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -158,7 +207,8 @@ constexpr int kLargeThreads = 1024;
 __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match* __restrict__ in,
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
-                                                                 uint64_t* __restrict__ gScratch, int global) {
+                                                                 uint64_t* __restrict__ gScratch, int global,
+                                                                 uint32_t* __restrict__ liveCnt) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
@@ -166,6 +216,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
     if (global ? n == 0 : n <= kSmallSeg) return;  // global: every segment takes the scratch path (tests)
+    if (liveCnt && threadIdx.x == 0) liveCnt[r] = (uint32_t)n;  // large segments are kept whole
     long p2 = 2;
     while (p2 < n) p2 <<= 1;
     if (!global && p2 <= kBlockSeg) {
@@ -199,16 +250,35 @@ __global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* 
 }
 
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, hipStream_t s) {
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, hipStream_t s) {
     if (nReads == 0) return;
     if (global) {
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, nullptr);
         return;
     }
-    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out);
-    if (maxSeg > kSmallSeg) k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0);
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
+    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
+    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
+    if (maxSeg > kSmallSeg)
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt);
+}
+
+// Live matches (front-packed in each sorted segment) into one dense array: a wave per read.
+__global__ void __launch_bounds__(256) k_pack_live(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                   const uint64_t* __restrict__ liveOff, uint32_t nReads,
+                                                   mtb_match* __restrict__ out) {
+    const uint32_t r = blockIdx.x * 4 + threadIdx.x / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (r >= nReads) return;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(in + mOff[r]);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(out + liveOff[r]);
+    const uint64_t words = (liveOff[r + 1] - liveOff[r]) * 3;
+    for (uint64_t w = lane; w < words; w += 64) dst[w] = src[w];
+}
+
+void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
+                      mtb_match* out, hipStream_t s) {
+    if (nReads) k_pack_live<<<(nReads + 3) / 4, 256, 0, s>>>(in, mOff, liveOff, nReads, out);
 }
 
 __global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {

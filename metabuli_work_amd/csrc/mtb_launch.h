@@ -158,9 +158,14 @@ void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv,
 uint64_t path_bytes();
 uint64_t clade_bytes();
 // K5; maxSeg: the most matches of one read (picks the kernels to launch); global: every segment
-// through the global-scratch network (gScratch 6*M words; parity tests of the general path)
+// through the global-scratch network (gScratch 6*M words; parity tests of the general path).
+// liveCnt (nullable): drop dead matches (species without a frame run of two, which K6 never
+// reads) from segments of <= 512 matches, write each segment front-packed and its live count
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, hipStream_t s);
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, hipStream_t s);
+// the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
+void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
+                      mtb_match* out, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 8192;
