@@ -492,11 +492,13 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // not need a total order (K5 puts each read's matches in compareMatches order); a sort prefix
     // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[4], s));
+    const int sortLo = unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
+                           ? kQuerySortLoCoarse : kQuerySortLo;
     if (!probe) {
         bool inB = false;
         if (c->lines) {
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
-                                 c->valsA.as<uint32_t>(), Q, kQuerySortLo, kQuerySortHi, false, false,
+                                 c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
             qk = inB ? c->keysA.as<uint64_t>() : c->keysB.as<uint64_t>();
             qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
@@ -538,7 +540,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
-                         c->lines, c->probeStats.as<unsigned long long>(), s);
+                         c->lines, sortLo, c->probeStats.as<unsigned long long>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

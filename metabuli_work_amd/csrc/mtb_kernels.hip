@@ -729,6 +729,7 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
 constexpr int kMatchQ = 256;
 constexpr int kMatchWin = 3072;
 constexpr uint32_t kStageFreeRatio = 24;  // D / Q above which K4 runs without LDS windows
+constexpr int kFreePer = 1;               // queries per thread in the unstaged K4 (2 measured slower)
 constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
@@ -836,7 +837,7 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
 // kStageRegions), so the claims do not all queue on one address. A later pass moves each match
 // into its read's segment (k_match_transpose). A region that would overflow is not written; the
 // caller grows the regions to the largest count and reruns.
-template <bool kStage>
+template <bool kStage, int kPer>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const uint64_t* __restrict__ dbv,
@@ -845,16 +846,17 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
                                                mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
                                                uint64_t region, int* __restrict__ err, uint32_t winCap, const uint64_t* __restrict__ win,
-                                               const ProbeLine* __restrict__ lines, unsigned long long* __restrict__ stats) {
+                                               const ProbeLine* __restrict__ lines, int sortLo,
+                                               unsigned long long* __restrict__ stats) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
     __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
     __shared__ ProbeLine sLines[kStage ? 1 : kMatchLines];  // the block's probe lines (sorted queries)
     __shared__ unsigned long long sBase;
-    constexpr int kPer = kMatchQ / 256;
-    const uint64_t q0 = (uint64_t)blockIdx.x * kMatchQ;
-    const uint64_t q1 = min(q0 + (uint64_t)kMatchQ, Q);
+    static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
+    const uint64_t q0 = (uint64_t)blockIdx.x * (256 * kPer);
+    const uint64_t q1 = min(q0 + (uint64_t)(256 * kPer), Q);
     // every independent load of the block is issued up front (query keys and infos, the window
     // bounds, then the window) so their latencies overlap instead of adding up
     uint64_t key[kPer], info[kPer];
@@ -867,7 +869,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         key[j] = live[j] ? qkey[q] : 0;
         slot[j] = live[j] ? qslot[q] : 0;
     }
-    const uint64_t winLo = win[2 * blockIdx.x], winN = win[2 * blockIdx.x + 1] - winLo;
+    const uint64_t winLo = kStage ? win[2 * blockIdx.x] : 0, winN = kStage ? win[2 * blockIdx.x + 1] - winLo : 0;
     const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
     if (kStage && staged) {
@@ -902,9 +904,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     } else if (lines) {  // HBM: the probe line names a lower bound of the run, a gallop finds its ends
         // sorted queries: the block's probe lines are one contiguous stretch (its sort-prefix range),
         // staged through LDS with coalesced loads unless it is long
-        const int sh = kQuerySortLo - 24;
-        const uint64_t L0 = ((qkey[q0] >> kQuerySortLo) << sh) / kLineRanks;
-        const uint64_t L1 = ((((qkey[q1 - 1] >> kQuerySortLo) + 1) << sh) - 1) / kLineRanks;
+        const int sh = sortLo - 24;
+        const uint64_t L0 = ((qkey[q0] >> sortLo) << sh) / kLineRanks;
+        const uint64_t L1 = ((((qkey[q1 - 1] >> sortLo) + 1) << sh) - 1) / kLineRanks;
         const bool inLds = !kStage && L1 - L0 < (uint64_t)kMatchLines;
         if (!kStage && inLds) {
             const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;  // 4 x 16 B per line
@@ -1208,6 +1210,10 @@ void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* q
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, stats);
 }
 
+bool unstaged_join(bool lines, uint64_t D, uint64_t Q, uint32_t winCap) {
+    return lines && (D > (uint64_t)kStageFreeRatio * Q || winCap == 0);
+}
+
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
 
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
@@ -1221,18 +1227,22 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
-                  const ProbeLine* lines, unsigned long long* stats, hipStream_t s) {
+                  const ProbeLine* lines, int sortLo, unsigned long long* stats, hipStream_t s) {
     if (Q == 0 || D < 2) return;
-    unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
     // HBM path anyway
-    if (lines && (D > (uint64_t)kStageFreeRatio * Q || winCap == 0))
-        k_match<false><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                              readCnt, total, buf, bufRank, region, err, winCap, win, lines, stats);
-    else
-        k_match<true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax, kmerFormat,
-                                             readCnt, total, buf, bufRank, region, err, winCap, win, lines, stats);
+    if (unstaged_join(lines != nullptr, D, Q, winCap)) {
+        const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
+        k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax,
+                                                        kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
+                                                        win, lines, sortLo, stats);
+    } else {
+        const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
+        k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf,
+                                                            maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
+                                                            err, winCap, win, lines, kQuerySortLo, stats);
+    }
 }
 
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,
