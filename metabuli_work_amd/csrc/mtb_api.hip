@@ -493,7 +493,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[4], s));
     const int sortLo = unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
-                           ? kQuerySortLoCoarse : kQuerySortLo;
+                           ? kQuerySortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
         if (c->lines) {

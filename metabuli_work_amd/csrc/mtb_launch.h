@@ -91,7 +91,7 @@ uint64_t host_from_rank_form(uint64_t v);
 constexpr uint64_t kAARankEnd = 37822859361ull;
 // query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
-constexpr int kQuerySortLoCoarse = 28;  // four passes (16-rank prefixes): DRAM-page locality for the unstaged K4
+constexpr int kQuerySortLoFine = 28;  // four passes (16-rank prefixes): DRAM-page locality for the unstaged K4
 
 void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
                      uint64_t* idxTmp, void* scanTmp, hipStream_t s);
@@ -149,7 +149,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, int sortLo, unsigned long long* stats, hipStream_t s);
 // K4 runs without LDS DB windows (probe-line lower bounds, no window staging): a DB much larger
-// than the query stream; its queries are then sorted finer (kQuerySortLoCoarse: one more pass buys
+// than the query stream; its queries are then sorted finer (kQuerySortLoFine: one more pass buys
 // DRAM-page locality for the random DB reads, measured 28.8 -> 26.5 ms per 1M pairs at GTDB scale)
 bool unstaged_join(bool lines, uint64_t D, uint64_t Q, uint32_t winCap);  // stats[0] += queries with >= 1 match
 // staged matches -> per-read segments at readOff (cursor: zeroed per-read counters)
