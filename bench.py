@@ -155,7 +155,12 @@ def main():
                 out[k] = v
         if c3 is not None and c2 is not None:
             out["config2"] = {k: v for k, v in c2.items() if k != "long_reads"}
-        out["long_reads"] = c2.get("long_reads") if c2 is not None else None
+        if c3 is not None and c3.get("long_reads") is not None:
+            out["long_reads"] = c3["long_reads"]
+            if c2 is not None and c2.get("long_reads") is not None:
+                out["config2"]["long_reads"] = c2["long_reads"]
+        else:
+            out["long_reads"] = c2.get("long_reads") if c2 is not None else None
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -265,58 +270,8 @@ def run_config2(args, world, rank, local, dev):
     long_line = None
     if args.long_reads > 0:
         clf.close()
-        lpl = LocalParameters(seqMode=3, kmerFormat=2, skipRedundancy=1)
-        clfl = Classifier(lpl, db_host=hdb.c_struct(), device=local)
-        for _ in range(max(1, args.warmup)):
-            clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        lsteps = max(1, min(args.steps, 3))
-        kl = np.zeros(7)
-        tl0 = time.perf_counter()
-        for _ in range(lsteps):
-            clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
-            kl += clfl.kernel_ms()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        tl = time.perf_counter() - tl0
-        if world > 1:
-            t = torch.tensor([tl], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tl = float(t.item())
-        lq, lm = clfl.last_counts()
-        lwork = clfl.stats()
-        long_cpu = None
-        if rank == 0 and args.cpu_sample > 0:
-            # the oracle on the first reads of the long batch (~10 s of 16-core work), and the GPU's
-            # results for the same reads compared with it
-            LS = max(1, min(args.long_reads, args.cpu_sample // 50))
-            lo_h = lo1[:LS + 1].cpu().numpy().astype(np.uint64)
-            ls_h = ls1[:int(lo_h[-1])].cpu().numpy()
-            lreads = synth.Reads(ls_h, lo_h, None, None, np.zeros(LS, np.int32))
-            lopar = lpl.to_c()
-            lopar.threads = cores
-            tc0 = time.perf_counter()
-            lres, ltc = oc.classify(odb, lopar, lreads)
-            lcpu_t = time.perf_counter() - tc0
-            gl = clfl.classify_batch(ls_h, lo_h)
-            long_cpu = {"value": round(LS / lcpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
-                        "sample": f"first {LS} long reads of the rank-0 batch, same DB, {lcpu_t:.1f}s wall",
-                        "parity_sample": bool(np.array_equal(gl.results["classification"], lres["classification"])
-                                              and np.array_equal(gl.results["score"].view(np.uint32),
-                                                                 lres["score"].view(np.uint32))
-                                              and np.array_equal(gl.taxcnt, ltc))}
-        long_line = {"value": round(world * args.long_reads * lsteps / tl, 1), "unit": "reads/s",
-                     "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
-                     "reads_per_gpu": args.long_reads, "bases_per_gpu": int(lo1[-1].item()), "n50": long_n50,
-                     "query_kmers": lq, "matches": lm,
-                     "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(kernel_names(lwork), kl)},
-                     "cpu_baseline": long_cpu, "work": lwork,
-                     "workload": "config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs the "
-                                 "same DB, seq mode 3"}
-        clfl.close()
+        long_line = run_long_reads(args, lambda lpl: Classifier(lpl, db_host=hdb.c_struct(), device=local), ls1, lo1,
+                                   long_n50, world, rank, dev, odb, cores, "the config-2 DB")
     if odb is not None:
         odb.close()
 
@@ -339,6 +294,66 @@ def run_config2(args, world, rank, local, dev):
     return out
 
 
+def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, db_name):
+    """Long-read line (seq mode 3): reads/s of the same pipeline on ONT-style ~10 kb reads, and, on
+    rank 0 with an oracle DB, the oracle on the first reads of the batch (~10 s of 16-core work)
+    with the GPU's results for the same reads compared to it."""
+    lpl = LocalParameters(seqMode=3, kmerFormat=2, skipRedundancy=1)
+    clfl = open_clf(lpl)
+    for _ in range(max(1, args.warmup)):
+        clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lsteps = max(1, min(args.steps, 3))
+    kl = np.zeros(7)
+    tl0 = time.perf_counter()
+    for _ in range(lsteps):
+        clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
+        kl += clfl.kernel_ms()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    tl = time.perf_counter() - tl0
+    if world > 1:
+        t = torch.tensor([tl], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tl = float(t.item())
+    lq, lm = clfl.last_counts()
+    lwork = clfl.stats()
+    long_cpu = None
+    if rank == 0 and args.cpu_sample > 0 and odb is not None:
+        from tests import oracle_ctypes as oc  # checker / baseline only
+
+        nl = lo1.numel() - 1
+        LS = max(1, min(nl, args.cpu_sample // 50))
+        lo_h = lo1[:LS + 1].cpu().numpy().astype(np.uint64)
+        ls_h = ls1[:int(lo_h[-1])].cpu().numpy()
+        lreads = synth.Reads(ls_h, lo_h, None, None, np.zeros(LS, np.int32))
+        lopar = lpl.to_c()
+        lopar.threads = cores
+        tc0 = time.perf_counter()
+        lres, ltc = oc.classify(odb, lopar, lreads)
+        lcpu_t = time.perf_counter() - tc0
+        gl = clfl.classify_batch(ls_h, lo_h)
+        long_cpu = {"value": round(LS / lcpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+                    "sample": f"first {LS} long reads of the rank-0 batch, same DB, {lcpu_t:.1f}s wall",
+                    "parity_sample": bool(np.array_equal(gl.results["classification"], lres["classification"])
+                                          and np.array_equal(gl.results["score"].view(np.uint32),
+                                                             lres["score"].view(np.uint32))
+                                          and np.array_equal(gl.taxcnt, ltc))}
+    clfl.close()
+    n_long = lo1.numel() - 1
+    return {"value": round(world * n_long * lsteps / tl, 1), "unit": "reads/s",
+            "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
+            "reads_per_gpu": n_long, "bases_per_gpu": int(lo1[-1].item()), "n50": n50,
+            "query_kmers": lq, "matches": lm,
+            "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(kernel_names(lwork), kl)},
+            "cpu_baseline": long_cpu, "work": lwork,
+            "workload": f"config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs {db_name}, "
+                        "seq mode 3"}
+
+
 def run_gtdb(args, world, rank, local, dev):
     """Config 3, the configuration BASELINE.json's metric names: 10M x 150 bp pairs per
     GPU vs a GTDB-scale DB (~12G k-mers over a 129,671-species skeleton taxonomy: 1000 species x 2
@@ -354,6 +369,8 @@ def run_gtdb(args, world, rank, local, dev):
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
         got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev)
+        if args.long_reads > 0:
+            got["long"] = make_long_reads_gpu(seq, off, args.long_reads, args.seed * 1000 + 37 + 17 * rank, dev)
 
     rdb = build_gtdb_scale(dev, n_true_species=args.gtdb_true_species, genome_len=args.gtdb_genome,
                            total_species=args.gtdb_species, target_kmers=int(args.gtdb_kmers), seed=args.seed + 1,
@@ -418,7 +435,8 @@ def run_gtdb(args, world, rank, local, dev):
     log(rank, f"[bench] config 3: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
               f"kernels {dict(zip(names, np.round(kern, 2)))}")
 
-    cpu = parity = None
+    cpu = parity = odb = None
+    cores = 1
     if rank == 0 and args.cpu_sample > 0 and args.gtdb_cpu_sample > 0:
         from tests import oracle_ctypes as oc  # checker / baseline only
 
@@ -439,7 +457,6 @@ def run_gtdb(args, world, rank, local, dev):
         tc0 = time.perf_counter()
         ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
         cpu_t = time.perf_counter() - tc0
-        odb.close()
         cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
                "sample": f"first {S} read pairs of the rank-0 batch, same GTDB-scale DB re-encoded as diffIdx/info/"
                          f"split; oracle/ (OpenMP C++ restatement of the reference path), {cpu_t:.1f}s wall",
@@ -450,6 +467,14 @@ def run_gtdb(args, world, rank, local, dev):
                       and np.array_equal(gb.taxcnt, otc))
         log(rank, f"[bench] config 3 CPU oracle: {cpu['value']} reads/s, parity {parity}")
     clf.close()
+    long_line = None
+    if "long" in got:
+        ls1, lo1, n50 = got.pop("long")
+        long_line = run_long_reads(args, lambda lpl: Classifier(lpl, db_resident=rdb, device=local), ls1, lo1, n50,
+                                   world, rank, dev, odb, cores, "the GTDB-scale DB")
+        log(rank, f"[bench] config 3 long reads: {long_line['value']} reads/s")
+    if odb is not None:
+        odb.close()
     out = {
         "value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "config": {"workload": "config 3: 10M x 150bp paired reads per GPU vs a GTDB-scale DB (~12G k-mers, "
@@ -465,6 +490,7 @@ def run_gtdb(args, world, rank, local, dev):
         "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
         "parity_sample": parity,
         "work": work,
+        "long_reads": long_line,
     }
     del rdb
     torch.cuda.empty_cache()

@@ -4,7 +4,8 @@ Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by
 within a step: a step starts at k_read_meta; extract = up to and including k_extract; filter =
 k_filter; kmer_sort = everything from there to the join; match_join = k_match_windows + k_match
 (probe_join = k_probe on MTB_JOIN=probe), with the per-read count scan and a rerun if the staging
-buffer grew; match_transpose = k_match_transpose; match_sort = k_segsort_*; assign = the rest of
+buffer grew; match_transpose = k_match_transpose; match_sort = k_segsort_* (+ the live-match scan
+and k_pack_live); assign = the rest of
 the step (K6 kernels, scans and taxcnt compaction).
 
 Usage:
@@ -47,9 +48,9 @@ def stage_of(seq):
             stage = "probe_join"
         elif k.startswith("k_match_transpose"):
             stage = "match_transpose"
-        elif k.startswith("k_segsort") or k.startswith("k_max_seg"):
+        elif k.startswith("k_segsort") or k.startswith("k_max_seg") or k.startswith("k_pack_live"):
             stage = "match_sort"
-        elif stage == "match_sort":
+        elif stage == "match_sort" and not k.startswith("k_scan"):  # K5's live-count scan stays in K5
             stage = "assign"
         elif (stage == "extract" and after_extract) or stage == "filter":
             stage = "kmer_sort"
