@@ -65,6 +65,8 @@ struct mtb_ctx {
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
+    bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
+    uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -203,6 +205,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
+    if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
+    if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
@@ -348,6 +352,7 @@ static AssignArgs assign_args(const mtb_params& p) {
 // K5 + K6 + taxcnt compaction on the matches already grouped by read in c->matches (mOff).
 static int assign_stage(mtb_ctx* c, uint32_t n) {
     hipStream_t s = c->stream;
+    HIP_TRY(c->errFlag.ensure(sizeof(int)));  // mtb_assign_* may run before any batch
     const uint64_t M = c->M;
     AssignArgs a = assign_args(c->par);
     a.generic = c->forceGeneric ? 1 : 0;
@@ -374,7 +379,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     uint32_t maxSeg = 0;
     HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (maxSeg > kSegSortLds || c->forceGeneric) HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
+    if (maxSeg > kSegSortLds || c->forceGeneric || c->segsortGlobal || (c->mergeSeg && maxSeg > c->mergeSeg))
+        HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
     // dead matches (no frame run of two in their species) are dropped in K5 unless the batch keeps
     // its stages (mtb_get_matches returns every match) or runs the general paths
     const bool prune = !c->keepStages && !c->forceGeneric;
@@ -383,7 +389,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
     launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric, prune ? c->liveCnt.as<uint32_t>() : nullptr, s);
+                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
+                   prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s);
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();
     uint64_t kM = M;
@@ -391,8 +398,9 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
         exclusive_scan_u32(c->liveCnt.as<uint32_t>(), n, c->liveOff.as<uint64_t>(), c->scanTmp.p, s);
         HIP_TRY(hipMemcpyAsync(&kM, c->liveOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         launch_pack_live(c->matchesSorted.as<mtb_match>(), c->mOff.as<uint64_t>(), c->liveOff.as<uint64_t>(), n,
-                         c->matches.as<mtb_match>(), s);  // K5's input buffer is free again
+                         c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);  // K5's input buffer is free again
         HIP_TRY(hipStreamSynchronize(s));
+        if (kM > M) { set_error("internal error: K5 kept more matches than it sorted"); return MTB_ERR_INTERNAL; }
         kIn = c->matches.as<mtb_match>();
         kOff = c->liveOff.as<uint64_t>();
     }
@@ -570,6 +578,14 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                            c->errFlag.as<int>(), s);
     HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
+    return MTB_OK;
+}
+
+// After an mtb_assign_* call: a device-side consistency check (err 2) is reported.
+static int check_err_flag(mtb_ctx* c) {
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err == 2) { set_error("internal error: inconsistent per-read match counts in K5"); return MTB_ERR_INTERNAL; }
     return MTB_OK;
 }
 
@@ -825,6 +841,8 @@ int mtb_assign_chunks(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_
     c->qSlots = nullptr;
     c->nReads = n;
     c->matchOnly = false;
+    HIP_TRY(c->errFlag.ensure(sizeof(int)));
+    HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     int rc = assign_stage(c, n);
     if (rc != MTB_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev[4], s));
@@ -833,7 +851,7 @@ int mtb_assign_chunks(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_
     for (int e = 0; e < 4; e++) HIP_TRY(hipEventElapsedTime(&c->stageMs[e], c->ev[e], c->ev[e + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     c->keepStages = true;
-    return MTB_OK;
+    return check_err_flag(c);
 }
 
 int mtb_get_matches(mtb_ctx* c, mtb_match* out, uint64_t cap, uint64_t* n_out) {
@@ -876,12 +894,14 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     HIP_TRY(hipMemcpyAsync(c->matches.p, grouped.data(), sizeof(mtb_match) * nm, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->mOff.p, off.data(), sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->qlen.p, qlen, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(c->errFlag.ensure(sizeof(int)));
+    HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     int rc = assign_stage(c, n);
     if (rc != MTB_OK) return rc;
     if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     c->keepStages = true;
-    return MTB_OK;
+    return check_err_flag(c);
 }
 
 }  // extern "C"

@@ -5,6 +5,9 @@
 // sorted segment, executing the reference's decision tree with per-read scratch carved from
 // batch-wide arrays by the read's match offset. Float arithmetic
 // follows the reference operation for operation (compiled with -ffp-contract=off).
+#include <algorithm>
+#include <vector>
+
 #include "mtb_launch.h"
 #include "mtb_stdsort.h"
 
@@ -200,6 +203,70 @@ __device__ void block_bitonic(uint64_t* H, uint64_t* Lo, Idx* I, long p2) {
         }
 }
 
+// Exclusive block scan for kThreads-thread blocks (wave shuffles + one LDS word per wave).
+template <int kThreads>
+__device__ uint32_t block_scan_u32(uint32_t x, uint32_t* total, uint32_t* sWave) {
+    constexpr int kW = kThreads / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63) sWave[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int i = 0; i < kW; i++) {
+            const uint32_t t = sWave[i];
+            sWave[i] = run;
+            run += t;
+        }
+        sWave[kW] = run;
+    }
+    __syncthreads();
+    const uint32_t r = sWave[w] + inc - x;
+    *total = sWave[kW];
+    __syncthreads();
+    return r;
+}
+
+// Dead-match pruning for a segment sorted by a block (see segsort_regs): elements 0..n-1 in
+// sorted order, hi keys in H (species << 32 | frame << 29 | pos), the permutation in I. Each thread
+// takes a contiguous chunk: species-run ids by a block scan of run starts, a flag per run that has
+// a (species, frame) pair, then the live elements written in order. rid: n words, runLive: n bytes
+// of scratch. Returns the live count.
+template <int kThreads, typename Idx>
+__device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* rid, uint8_t* runLive, long n,
+                                     const mtb_match* __restrict__ in, mtb_match* __restrict__ out, uint64_t base,
+                                     uint32_t* sWave) {
+    const long per = (n + kThreads - 1) / kThreads;
+    const long b = (long)threadIdx.x * per, e = min(n, b + per);
+    uint32_t starts = 0;
+    for (long i = b; i < e; i++) starts += (i == 0 || (H[i] >> 32) != (H[i - 1] >> 32)) ? 1u : 0u;
+    uint32_t nRuns;
+    uint32_t run = block_scan_u32<kThreads>(starts, &nRuns, sWave);
+    for (long i = b; i < e; i++) {
+        if (i == 0 || (H[i] >> 32) != (H[i - 1] >> 32)) run++;
+        rid[i] = run - 1;
+    }
+    for (long i = threadIdx.x; i < (long)nRuns; i += kThreads) runLive[i] = 0;
+    __threadfence_block();  // the scratch may be global memory (segments over kBlockSeg)
+    __syncthreads();
+    for (long i = b; i < e; i++)
+        if (i + 1 < n && (H[i] >> 29) == (H[i + 1] >> 29)) runLive[rid[i]] = 1;
+    __threadfence_block();
+    __syncthreads();
+    uint32_t mine = 0;
+    for (long i = b; i < e; i++) mine += runLive[rid[i]];
+    uint32_t kept;
+    uint32_t at = block_scan_u32<kThreads>(mine, &kept, sWave);
+    for (long i = b; i < e; i++)
+        if (runLive[rid[i]]) out[base + at++] = in[base + I[i]];
+    return kept;
+}
+
 // Segments of 513..kBlockSeg matches sort in LDS with one 1024-thread block per read (long reads:
 // ~2.5k matches at N50 10 kb); larger ones run the same network over a global key scratch.
 constexpr int kLargeThreads = 1024;
@@ -208,18 +275,20 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
                                                                  uint64_t* __restrict__ gScratch, int global,
-                                                                 uint32_t* __restrict__ liveCnt) {
+                                                                 uint32_t* __restrict__ liveCnt, long mergeSeg) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
+    if (global && n == 0 && liveCnt && threadIdx.x == 0) liveCnt[r] = 0;  // k_segsort_small is not launched
     if (global ? n == 0 : n <= kSmallSeg) return;  // global: every segment takes the scratch path (tests)
-    if (liveCnt && threadIdx.x == 0) liveCnt[r] = (uint32_t)n;  // large segments are kept whole
+    __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
     long p2 = 2;
     while (p2 < n) p2 <<= 1;
-    if (!global && p2 <= kBlockSeg) {
+    if (!global && n > mergeSeg) return;  // chunked LDS sorts + merge path (launch_segsort)
+    if (!global) {
         for (long i = threadIdx.x; i < p2; i += kLargeThreads) {
             uint64_t h = ~0ull, l = ~0ull;
             if (i < n) match_key(in[base + i], h, l);
@@ -227,6 +296,13 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
         }
         __syncthreads();
         block_bitonic<kLargeThreads, uint16_t>(sh, sl, si, p2);
+        if (liveCnt) {  // the lo keys are no longer needed: their LDS holds the run ids and flags
+            uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
+            const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n),
+                                                                            n, in, out, base, sWave);
+            if (threadIdx.x == 0) liveCnt[r] = kept;
+            return;
+        }
         for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + si[i]];
         return;
     }
@@ -241,6 +317,13 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     __threadfence_block();
     __syncthreads();
     block_bitonic<kLargeThreads, uint32_t>(H, Lo, I, p2);
+    if (liveCnt) {  // run ids and flags in the lo-key scratch (2 * p2 words, p2 >= n)
+        uint32_t* rid = reinterpret_cast<uint32_t*>(Lo);
+        const uint32_t kept =
+            prune_pack_block<kLargeThreads, uint32_t>(H, I, rid, reinterpret_cast<uint8_t*>(rid + n), n, in, out, base, sWave);
+        if (threadIdx.x == 0) liveCnt[r] = kept;
+        return;
+    }
     for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + I[i]];
 }
 
@@ -249,36 +332,195 @@ __global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* 
     if (i < n) atomicMax(out, x[i]);
 }
 
+// ---- segments over kBlockSeg matches (long reads): each kBlockSeg chunk sorts in LDS, then the
+// sorted runs are merged pairwise (merge path: every thread finds its output diagonal's split by
+// binary search and merges 8 elements), then pruning / the gather-permute. Keys + segment-local
+// indices ping-pong between two scratch buffers indexed by the match's global position:
+// buffer b: hi keys at b*3M, lo keys at b*3M + M, indices (u32) at b*3M + 2M words.
+struct MergeBuf {
+    uint64_t* h;
+    uint64_t* l;
+    uint32_t* x;
+};
+__device__ __forceinline__ MergeBuf merge_buf(uint64_t* scratch, uint64_t M, int b) {
+    uint64_t* p = scratch + (uint64_t)b * 3 * M;
+    return MergeBuf{p, p + M, reinterpret_cast<uint32_t*>(p + 2 * M)};
+}
+
+__global__ void __launch_bounds__(kLargeThreads) k_chunk_sort(const mtb_match* __restrict__ in,
+                                                              const uint64_t* __restrict__ mOff,
+                                                              const uint2* __restrict__ chunks, uint64_t M,
+                                                              uint64_t* __restrict__ scratch, long chunk) {
+    __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
+    __shared__ uint16_t si[kBlockSeg];
+    const uint2 ck = chunks[blockIdx.x];  // (read, chunk start)
+    const uint64_t base = mOff[ck.x];
+    const long n = (long)(mOff[ck.x + 1] - base);
+    const long cs = ck.y, len = min(chunk, n - cs);
+    long p2 = 2;
+    while (p2 < len) p2 <<= 1;
+    for (long i = threadIdx.x; i < p2; i += kLargeThreads) {
+        uint64_t h = ~0ull, l = ~0ull;
+        if (i < len) match_key(in[base + cs + i], h, l);
+        sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    block_bitonic<kLargeThreads, uint16_t>(sh, sl, si, p2);
+    const MergeBuf o = merge_buf(scratch, M, 0);
+    for (long i = threadIdx.x; i < len; i += kLargeThreads) {
+        o.h[base + cs + i] = sh[i];
+        o.l[base + cs + i] = sl[i];
+        o.x[base + cs + i] = (uint32_t)(cs + si[i]);
+    }
+}
+
+constexpr int kMergePer = 8;                   // outputs per thread
+constexpr int kMergeTile = 256 * kMergePer;    // outputs per block
+
+// One tile of the merge of runs A = [ps, ps + w) and B = [ps + w, ps + 2w) (clipped to n) of a
+// segment, from buffer src into dst. tiles: (read, pair start, tile start).
+__global__ void __launch_bounds__(256) k_merge_tiles(const uint64_t* __restrict__ mOff, const uint4* __restrict__ tiles,
+                                                     uint64_t M, uint64_t* __restrict__ scratch, int src, long w) {
+    const uint4 t = tiles[blockIdx.x];
+    const uint64_t base = mOff[t.x];
+    const long n = (long)(mOff[t.x + 1] - base);
+    const long ps = t.y;
+    const long na = min(w, n - ps), nb = max(0l, min(w, n - ps - w));
+    const MergeBuf S = merge_buf(scratch, M, src), D = merge_buf(scratch, M, src ^ 1);
+    const uint64_t a0 = base + ps, b0 = a0 + na;
+    long d = (long)t.z + (long)threadIdx.x * kMergePer;
+    if (d >= na + nb) return;
+    // merge path: the first d outputs take i from A and d - i from B
+    long lo = max(0l, d - nb), hi = min(d, na);
+    while (lo < hi) {
+        const long i = (lo + hi) >> 1;
+        // A[i] goes before B[d - i - 1] ?  (ties cannot occur: the key is a total order)
+        if (key_gt(S.h[b0 + d - i - 1], S.l[b0 + d - i - 1], S.h[a0 + i], S.l[a0 + i])) lo = i + 1;
+        else hi = i;
+    }
+    long i = lo, j = d - lo;
+    const long end = min(na + nb, d + kMergePer);
+    for (; d < end; d++) {
+        const bool takeA = j >= nb || (i < na && !key_gt(S.h[a0 + i], S.l[a0 + i], S.h[b0 + j], S.l[b0 + j]));
+        const uint64_t from = takeA ? a0 + i : b0 + j;
+        D.h[a0 + d] = S.h[from];
+        D.l[a0 + d] = S.l[from];
+        D.x[a0 + d] = S.x[from];
+        if (takeA) i++; else j++;
+    }
+}
+
+// The merged segment in buffer b: pruning (run ids and flags in the other buffer's lo keys) or the
+// plain gather-permute.
+__global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match* __restrict__ in,
+                                                                const uint64_t* __restrict__ mOff,
+                                                                const uint32_t* __restrict__ reads, uint64_t M,
+                                                                uint64_t* __restrict__ scratch, int b,
+                                                                mtb_match* __restrict__ out,
+                                                                uint32_t* __restrict__ liveCnt) {
+    __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
+    const uint32_t r = reads[blockIdx.x];
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    const MergeBuf S = merge_buf(scratch, M, b), T = merge_buf(scratch, M, b ^ 1);
+    if (liveCnt) {
+        uint32_t* rid = reinterpret_cast<uint32_t*>(T.l + base);
+        const uint32_t kept = prune_pack_block<kLargeThreads, uint32_t>(S.h + base, S.x + base, rid,
+                                                                        reinterpret_cast<uint8_t*>(rid + n), n, in,
+                                                                        out, base, sWave);
+        if (threadIdx.x == 0) liveCnt[r] = kept;
+        return;
+    }
+    for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + S.x[base + i]];
+}
+
+static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                              uint64_t* scratch, uint32_t* liveCnt, long chunk, hipStream_t s) {
+    std::vector<uint64_t> off(nReads + 1);
+    hipMemcpyAsync(off.data(), mOff, sizeof(uint64_t) * (nReads + 1), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    std::vector<uint32_t> big;
+    std::vector<uint2> chunks;
+    long maxN = 0;
+    for (uint32_t r = 0; r < nReads; r++) {
+        const long n = (long)(off[r + 1] - off[r]);
+        if (n <= chunk) continue;
+        big.push_back(r);
+        maxN = std::max(maxN, n);
+        for (long c = 0; c < n; c += chunk) chunks.push_back(make_uint2(r, (uint32_t)c));
+    }
+    if (big.empty()) return;
+    uint2* dChunks = nullptr;
+    uint4* dTiles = nullptr;
+    uint32_t* dBig = nullptr;
+    hipMallocAsync((void**)&dChunks, sizeof(uint2) * chunks.size(), s);
+    hipMallocAsync((void**)&dBig, sizeof(uint32_t) * big.size(), s);
+    hipMemcpyAsync(dChunks, chunks.data(), sizeof(uint2) * chunks.size(), hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(dBig, big.data(), sizeof(uint32_t) * big.size(), hipMemcpyHostToDevice, s);
+    k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk);
+    int b = 0;
+    std::vector<uint4> tiles;
+    for (long w = chunk; w < maxN; w *= 2) {
+        tiles.clear();
+        for (uint32_t r : big) {
+            const long n = (long)(off[r + 1] - off[r]);
+            for (long ps = 0; ps < n; ps += 2 * w) {
+                const long len = std::min(2 * w, n - ps);
+                for (long t = 0; t < len; t += kMergeTile) tiles.push_back(make_uint4(r, (uint32_t)ps, (uint32_t)t, 0));
+            }
+        }
+        if (dTiles) hipFreeAsync(dTiles, s);
+        hipMallocAsync((void**)&dTiles, sizeof(uint4) * tiles.size(), s);
+        hipMemcpyAsync(dTiles, tiles.data(), sizeof(uint4) * tiles.size(), hipMemcpyHostToDevice, s);
+        k_merge_tiles<<<(unsigned)tiles.size(), 256, 0, s>>>(mOff, dTiles, M, scratch, b, w);
+        hipStreamSynchronize(s);  // the host tile vector is reused
+        b ^= 1;
+    }
+    k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt);
+    if (dTiles) hipFreeAsync(dTiles, s);
+    hipFreeAsync(dChunks, s);
+    hipFreeAsync(dBig, s);
+}
+
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, hipStream_t s) {
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
+                    hipStream_t s) {
     if (nReads == 0) return;
+    const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, nullptr);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk);
         return;
     }
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
     if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
     if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
     if (maxSeg > kSmallSeg)
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);
+    if (maxSeg > chunk) launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, s);
 }
 
 // Live matches (front-packed in each sorted segment) into one dense array: a wave per read.
 __global__ void __launch_bounds__(256) k_pack_live(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
                                                    const uint64_t* __restrict__ liveOff, uint32_t nReads,
-                                                   mtb_match* __restrict__ out) {
+                                                   mtb_match* __restrict__ out, int* __restrict__ err) {
     const uint32_t r = blockIdx.x * 4 + threadIdx.x / 64;
     const uint32_t lane = threadIdx.x & 63;
     if (r >= nReads) return;
+    const uint64_t live = liveOff[r + 1] - liveOff[r];
+    // a live count above the segment, or live offsets past the matches, would be a K5 bug: never
+    // copy out of bounds
+    if (live > mOff[r + 1] - mOff[r] || liveOff[r + 1] > mOff[nReads]) {
+        if (lane == 0) atomicExch(err, 2);
+        return;
+    }
     const uint64_t* src = reinterpret_cast<const uint64_t*>(in + mOff[r]);
     uint64_t* dst = reinterpret_cast<uint64_t*>(out + liveOff[r]);
-    const uint64_t words = (liveOff[r + 1] - liveOff[r]) * 3;
-    for (uint64_t w = lane; w < words; w += 64) dst[w] = src[w];
+    for (uint64_t w = lane; w < live * 3; w += 64) dst[w] = src[w];
 }
 
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
-                      mtb_match* out, hipStream_t s) {
-    if (nReads) k_pack_live<<<(nReads + 3) / 4, 256, 0, s>>>(in, mOff, liveOff, nReads, out);
+                      mtb_match* out, int* err, hipStream_t s) {
+    if (nReads) k_pack_live<<<(nReads + 3) / 4, 256, 0, s>>>(in, mOff, liveOff, nReads, out, err);
 }
 
 __global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {

@@ -166,11 +166,14 @@ uint64_t clade_bytes();
 // through the global-scratch network (gScratch 6*M words; parity tests of the general path).
 // liveCnt (nullable): drop dead matches (species without a frame run of two, which K6 never
 // reads) from segments of <= 512 matches, write each segment front-packed and its live count
+// mergeSeg: segments over this many matches (default, 0: 8192, the LDS capacity) sort as LDS chunks of
+// that size merged pairwise (tests lower it to exercise the merge path)
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, hipStream_t s);
+                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
+                    hipStream_t s);
 // the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
-                      mtb_match* out, hipStream_t s);
+                      mtb_match* out, int* err, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 8192;

@@ -159,6 +159,29 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     odb.close()
 
 
+@pytest.mark.parametrize("db_name,kind,glob,merge", [
+    ("fmt2", "paired", "1", "0"), ("fmt2", "long", "1", "0"), ("fmt1", "long", "1", "0"),
+    ("fmt2", "long", "0", "0"), ("fmt2_syncmer", "long", "0", "0"),
+    ("fmt2", "long", "0", "512"), ("fmt1", "long", "0", "600"), ("fmt2_syncmer", "long", "0", "512")])
+def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, monkeypatch):
+    """Dead-match pruning in every K5 variant, results against the oracle: long reads put segments
+    in the 1024-thread LDS sort; MTB_SEGSORT_GLOBAL=1 sends every segment through the global-scratch
+    sort; MTB_MERGE_SEG=n sends segments over n matches through the chunked LDS sorts + merge path
+    (long reads' path above 8192 matches)."""
+    monkeypatch.setenv("MTB_SEGSORT_GLOBAL", glob)
+    monkeypatch.setenv("MTB_MERGE_SEG", merge)
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    odb = oc.OracleDb(db_dir)
+    reads = _reads(gen, kind, 1500 if kind != "long" else 60, 35)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        assert clf.stats()["live_matches"] < br.matches
+        compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
+
+
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
 def test_general_paths(make_db, db_name, monkeypatch):
     """MTB_FORCE_GENERIC=1 turns off every fast path (LDS DB windows in K4, register and LDS sorts in
