@@ -271,6 +271,41 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
 // ~2.5k matches at N50 10 kb); larger ones run the same network over a global key scratch.
 constexpr int kLargeThreads = 1024;
 
+// Segments of 513..2048 matches: the same LDS sort with a 2048-entry tile and 256 threads, so four
+// blocks share a CU (the 8192-entry kernel holds 147 KB of LDS: one block per CU).
+constexpr int kMidSeg = 2048;
+constexpr int kMidThreads = 256;
+__global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
+                                                             const uint64_t* __restrict__ mOff, uint32_t nReads,
+                                                             mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
+                                                             long mergeSeg) {
+    __shared__ uint64_t sh[kMidSeg], sl[kMidSeg];
+    __shared__ uint16_t si[kMidSeg];
+    __shared__ uint32_t sWave[kMidThreads / 64 + 1];
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
+    long p2 = 2;
+    while (p2 < n) p2 <<= 1;
+    for (long i = threadIdx.x; i < p2; i += kMidThreads) {
+        uint64_t h = ~0ull, l = ~0ull;
+        if (i < n) match_key(in[base + i], h, l);
+        sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    block_bitonic<kMidThreads, uint16_t>(sh, sl, si, p2);
+    if (liveCnt) {
+        uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
+        const uint32_t kept = prune_pack_block<kMidThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n), n,
+                                                                      in, out, base, sWave);
+        if (threadIdx.x == 0) liveCnt[r] = kept;
+        return;
+    }
+    for (long i = threadIdx.x; i < n; i += kMidThreads) out[base + i] = in[base + si[i]];
+}
+
 __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match* __restrict__ in,
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
@@ -283,7 +318,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
     if (global && n == 0 && liveCnt && threadIdx.x == 0) liveCnt[r] = 0;  // k_segsort_small is not launched
-    if (global ? n == 0 : n <= kSmallSeg) return;  // global: every segment takes the scratch path (tests)
+    if (global ? n == 0 : n <= kMidSeg) return;  // global: every segment takes the scratch path (tests)
     __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
     long p2 = 2;
     while (p2 < n) p2 <<= 1;
@@ -494,7 +529,8 @@ void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, 
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
     if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
     if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
-    if (maxSeg > kSmallSeg)
+    if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk);
+    if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);
     if (maxSeg > chunk) launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, s);
 }
@@ -1354,7 +1390,10 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
     }
-    k_choose_taxon<<<(nReads + 255) / 256, 256, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
+    // one thread per read: with few, long reads (50k ONT reads) 256-thread blocks would leave CUs
+    // idle, so the blocks are one wave when the batch has fewer than 64 reads per CU
+    const unsigned ctT = nReads < 256u * 256u ? 64u : 256u;
+    k_choose_taxon<<<(nReads + ctT - 1) / ctT, ctT, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
                                                          s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
                                                          (Clade*)s.clade, s.cladePerMatch, tcPool, results);
 }
