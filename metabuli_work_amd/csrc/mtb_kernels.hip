@@ -402,7 +402,7 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
 // two block barriers per pass rather than several per 256 keys. The first pass (FILTER) drops
 // sentinel keys: the compaction of blank reserved slots costs nothing extra.
 // ------------------------------------------------------------------------------------------------
-constexpr int kRadixItems = 16;
+constexpr int kRadixItems = 32;
 constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
 constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
