@@ -60,6 +60,8 @@ struct mtb_ctx {
     uint32_t* dbinfo = nullptr;
     uint64_t* dirMem = nullptr;
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
+    uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
+    uint16_t* runOff = nullptr;  // ... and each present rank's run start in its line (2 B per present rank)
     AADir dir{};
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
@@ -108,13 +110,15 @@ struct mtb_ctx {
 
 static void free_db(mtb_ctx* c) {
     if (c->borrowedDb) c->dbv = nullptr, c->dbinfo = nullptr;  // caller-owned (mtb_open_resident)
-    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->lines, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->dbv = nullptr;
     c->dbinfo = nullptr;
     c->dirMem = nullptr;
     c->lines = nullptr;
+    c->lineP = nullptr;
+    c->runOff = nullptr;
 }
 
 template <typename T>
@@ -217,6 +221,22 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
         build_probe_lines(c->dbv, c->D, c->dir, c->lines, s);
+        const char* ri = getenv("MTB_RUN_INDEX");  // 0: no run index (the unstaged join gallops)
+        if (!ri || atoi(ri) != 0) {
+            uint32_t* pop = nullptr;
+            void* tmp = nullptr;
+            uint64_t P = 0;
+            HIP_TRY(hipMalloc(&c->lineP, (kProbeLines + 1) * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&pop, kProbeLines * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&tmp, scan_tmp_elems(kProbeLines) * sizeof(uint64_t)));
+            build_line_prefix(c->lines, c->lineP, pop, tmp, s);
+            HIP_TRY(hipMemcpyAsync(&P, c->lineP + kProbeLines, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            hipFree(pop);
+            hipFree(tmp);
+            HIP_TRY(hipMalloc(&c->runOff, (P + 1) * sizeof(uint16_t)));
+            build_run_offsets(c->dbv, c->D, c->lines, c->lineP, c->runOff, s);
+        }
     }
     HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
     HIP_TRY(hipStreamSynchronize(s));
@@ -548,7 +568,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
-                         c->lines, sortLo, c->probeStats.as<unsigned long long>(), s);
+                         c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

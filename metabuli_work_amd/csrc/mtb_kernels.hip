@@ -345,6 +345,28 @@ __device__ __forceinline__ uint64_t line_lower_bound_at(const ProbeLine* line, u
     return (((uint64_t)q0.x | (uint64_t)q0.y << 32) & ((1ull << 40) - 1)) + before;
 }
 
+// One line read for the run index: the head word; the present ranks before rank o of the line,
+// in the whole line, and whether o itself is present.
+__device__ __forceinline__ uint64_t line_scan(const ProbeLine* line, uint32_t o, uint32_t& before, uint32_t& total,
+                                              bool& present) {
+    const uint4* lp = reinterpret_cast<const uint4*>(line);
+    const uint4 q0 = lp[0], q1 = lp[1], q2 = lp[2], q3 = lp[3];
+    const uint32_t w[14] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    before = 0;
+    total = 0;
+    uint32_t at = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        const uint32_t wi = (uint32_t)i;
+        const uint32_t m = wi < (o >> 5) ? ~0u : (wi == (o >> 5) ? ((1u << (o & 31u)) - 1u) : 0u);
+        before += __popc(w[i] & m);
+        total += __popc(w[i]);
+        if (wi == (o >> 5)) at = w[i];
+    }
+    present = (at >> (o & 31u)) & 1u;
+    return (uint64_t)q0.x | (uint64_t)q0.y << 32;
+}
+
 __device__ __forceinline__ uint64_t line_lower_bound(const ProbeLine* __restrict__ lines, uint64_t x) {
     const uint64_t L = x / kLineRanks;
     return line_lower_bound_at(lines + L, (uint32_t)(x - L * kLineRanks));
@@ -721,6 +743,46 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
     if (D) k_line_bits<<<stride_grid(D), 256, 0, s>>>(dbv, D, lines);
 }
 
+// Run index: the exact DB run of every present AA rank, for the unstaged K4 (a DB much larger than
+// the query stream). lineP[L] = present ranks in the lines before L (exclusive scan of the lines'
+// popcounts); runOff[lineP[L] + k] = DB index of the first k-mer of line L's k-th present rank
+// minus the line's base. A query then finds its run [lo, hi) with one random 2-B read (two adjacent
+// entries) instead of galloping from the line's lower bound through the DB values, a chain of
+// dependent random reads. Lines of more than kRunIdxMax k-mers are not indexed: their queries
+// gallop as before.
+__global__ void k_line_pop(const ProbeLine* __restrict__ lines, uint32_t* __restrict__ pop) {
+    const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= kProbeLines) return;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < (int)(kLineRanks / 32); i++) c += __popc(lines[l].bits[i]);
+    pop[l] = c;
+}
+
+__global__ void k_run_offsets(const uint64_t* __restrict__ dbv, uint64_t D, const ProbeLine* __restrict__ lines,
+                              const uint64_t* __restrict__ lineP, uint16_t* __restrict__ runOff) {
+    MTB_GRID_STRIDE(i, D) {
+        const uint64_t r = dbv[i] >> 24;
+        if (i > 0 && (dbv[i - 1] >> 24) == r) continue;
+        const uint64_t L = r / kLineRanks;
+        const uint32_t o = (uint32_t)(r - L * kLineRanks);
+        const uint64_t head = lines[L].base;
+        if ((head >> 40) > kRunIdxMax) continue;
+        const uint64_t before = line_lower_bound_at(lines + L, o) - (head & ((1ull << 40) - 1));
+        runOff[lineP[L] + before] = (uint16_t)(i - (head & ((1ull << 40) - 1)));
+    }
+}
+
+void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s) {
+    k_line_pop<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines, popTmp);
+    exclusive_scan_u32(popTmp, kProbeLines, lineP, scanTmp, s);
+}
+
+void build_run_offsets(const uint64_t* dbv, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
+                       uint16_t* runOff, hipStream_t s) {
+    if (D) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(dbv, D, lines, lineP, runOff);
+}
+
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
 // of that range (found with two directory lookups per block) are staged in LDS with coalesced
 // loads and every query of the block searches LDS. A block whose range holds more than kMatchWin
@@ -765,6 +827,26 @@ __device__ __forceinline__ uint32_t run_select(const HamRows& hr, const uint64_t
     return c;
 }
 
+// One selected candidate (DB value tv, taxID tax, hamming sum hs) as a Match at out[w]
+// (KmerMatcher.cpp:431-448); outRank (nullable) gets its rank inside its read's segment.
+__device__ __forceinline__ void emit_match(uint64_t key, const HamRows& hr, uint64_t info, uint64_t tv, uint32_t tax,
+                                           uint32_t hs, bool rev, const int32_t* __restrict__ spOf, uint32_t maxTax,
+                                           mtb_match* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
+                                           uint32_t rank, int* __restrict__ err) {
+    const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
+    if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
+    mtb_match m;
+    m.qinfo = info;
+    m.target_id = tax;
+    m.species_id = (uint32_t)sp;
+    m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
+    m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
+    m.hamming = (uint8_t)hs;
+    m.pad = 0;
+    if (outRank) outRank[w] = rank;
+    out[w] = m;
+}
+
 // Writes the run's selected candidates at out[w..wEnd); returns the next w (a selection that
 // would pass wEnd sets err 4 and stops). outRank (nullable) gets each match's rank inside its
 // read's segment, starting at `rank`.
@@ -782,19 +864,7 @@ __device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, ui
             atomicExch(err, 4);
             return w;
         }
-        const uint32_t tax = infos[t];
-        const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
-        if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
-        mtb_match m;
-        m.qinfo = info;
-        m.target_id = tax;
-        m.species_id = (uint32_t)sp;
-        m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
-        m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
-        m.hamming = (uint8_t)hs;
-        m.pad = 0;
-        if (outRank) outRank[w] = rank++;
-        out[w++] = m;
+        emit_match(key, hr, info, tv, infos[t], hs, rev, spOf, maxTax, out, outRank, w++, rank++, err);
     }
     return w;
 }
@@ -846,13 +916,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
                                                mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
                                                uint64_t region, int* __restrict__ err, uint32_t winCap, const uint64_t* __restrict__ win,
-                                               const ProbeLine* __restrict__ lines, int sortLo,
-                                               unsigned long long* __restrict__ stats) {
+                                               const ProbeLine* __restrict__ lines,
+                                               const uint64_t* __restrict__ lineP, const uint16_t* __restrict__ runOff,
+                                               int sortLo, unsigned long long* __restrict__ stats) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
     __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
     __shared__ ProbeLine sLines[kStage ? 1 : kMatchLines];  // the block's probe lines (sorted queries)
+    __shared__ uint64_t sLineP[kStage ? 1 : kMatchLines];   // and their run-index bases
     __shared__ unsigned long long sBase;
     static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
     const uint64_t q0 = (uint64_t)blockIdx.x * (256 * kPer);
@@ -913,16 +985,36 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
             uint4* dst = reinterpret_cast<uint4*>(sLines);
             for (uint32_t i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+            if (runOff)
+                for (uint32_t i = threadIdx.x; i <= (uint32_t)(L1 - L0); i += 256) sLineP[i] = lineP[L0 + i];
             __syncthreads();
         }
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint64_t aa = key[j] & kAAMask, x = aa >> 24, L = x / kLineRanks;
             const uint32_t o = (uint32_t)(x - L * kLineRanks);
-            const uint64_t from = !live[j] ? 0
-                                  : inLds ? line_lower_bound_at(sLines + (L - L0), o) : line_lower_bound_at(lines + L, o);
-            lo[j] = live[j] ? gallop_lower1(dbv, from, aa) : 0;
-            hi[j] = live[j] ? gallop_lower1(dbv, lo[j], aa + (1ull << 24)) : 0;
+            if (!live[j]) {
+                lo[j] = hi[j] = 0;
+                continue;
+            }
+            const ProbeLine* pl = inLds ? sLines + (L - L0) : lines + L;
+            if (runOff) {  // exact run from the run index (indexed lines)
+                uint32_t before, pc;
+                bool present;
+                const uint64_t head = line_scan(pl, o, before, pc, present);
+                const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
+                if (cnt <= kRunIdxMax) {
+                    const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
+                    const uint32_t a = runOff[p];
+                    const uint32_t b = before + 1 < pc ? runOff[p + 1] : (uint32_t)cnt;
+                    lo[j] = base + a;
+                    hi[j] = present ? base + b : base + a;  // an absent rank (not filtered here) has no run
+                    continue;
+                }
+            }
+            const uint64_t from = line_lower_bound_at(pl, o);
+            lo[j] = gallop_lower1(dbv, from, aa);
+            hi[j] = gallop_lower1(dbv, lo[j], aa + (1ull << 24));
         }
     } else {  // HBM through the AA-prefix directory (no probe lines: MTB_FORCE_GENERIC)
 #pragma unroll
@@ -937,12 +1029,37 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint64_t* vals = staged ? sDb : dbv;
     const uint32_t* infos = staged ? sInfo : dbinfo;
     const uint64_t vOff = staged ? winLo : 0;
+    // unstaged: a run at GTDB scale is 1-2 k-mers, so the first two values of each run and their
+    // taxIDs are read at once (the pad makes lo + 1 readable) instead of value, then taxID
+    uint64_t rv[kPer][2];
+    uint32_t rt[kPer][2], rs[kPer][2];
+    bool small[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        if (hi[j] + vOff > D - 1) hi[j] = D - 1 - vOff;  // the last DB k-mer is never a candidate
+        if (lo[j] > hi[j]) hi[j] = lo[j];
+        small[j] = !staged && live[j] && hi[j] - lo[j] <= 2;
+        if (small[j]) {
+            rv[j][0] = dbv[lo[j]];
+            rv[j][1] = dbv[lo[j] + 1];
+            rt[j][0] = dbinfo[lo[j]];
+            rt[j][1] = dbinfo[lo[j] + 1];
+        }
+    }
     uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
     HamRows hr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         hr[j] = hamming_rows(key[j]);
-        c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+        if (small[j]) {  // run_select on the two registers
+            const uint32_t n = (uint32_t)(hi[j] - lo[j]);
+            rs[j][0] = n > 0 ? hamming_sum_rows(hr[j], rv[j][0]) : 255u;
+            rs[j][1] = n > 1 ? hamming_sum_rows(hr[j], rv[j][1]) : 255u;
+            thr[j] = min(min(rs[j][0], rs[j][1]) * 2u, 7u);
+            c[j] = (uint32_t)(rs[j][0] <= thr[j]) + (uint32_t)(rs[j][1] <= thr[j]);
+        } else {
+            c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+        }
         info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
         // the returned count is the query's first rank inside its read's segment
         rk[j] = c[j] ? atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]) : 0;
@@ -964,8 +1081,18 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         if (!c[j]) continue;
-        run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank, w,
-                 w + c[j], rk[j], err);
+        if (small[j]) {
+            const bool rev = ((info_frame(info[j]) < 3) != (kmerFormat == 2));
+            uint64_t wj = w;
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                if (rs[j][k] <= thr[j])
+                    emit_match(key[j], hr[j], info[j], rv[j][k], rt[j][k], rs[j][k], rev, spOf, maxTax, buf, bufRank,
+                               wj++, rk[j]++, err);
+        } else {
+            run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
+                     w, w + c[j], rk[j], err);
+        }
         w += c[j];
     }
 }
@@ -1227,7 +1354,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
-                  const ProbeLine* lines, int sortLo, unsigned long long* stats, hipStream_t s) {
+                  const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
+                  unsigned long long* stats, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -1236,12 +1364,13 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
         k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
-                                                        win, lines, sortLo, stats);
+                                                        win, lines, lineP, runOff, sortLo, stats);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
-                                                            err, winCap, win, lines, kQuerySortLo, stats);
+                                                            err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
+                                                            stats);
     }
 }
 

@@ -125,6 +125,15 @@ constexpr uint64_t kProbeLines = (kAARankEnd + kLineRanks - 1) / kLineRanks + 1;
 void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines,
                        hipStream_t s);  // lines zeroed by the caller
 
+// Run index (mtb_kernels.hip, k_run_offsets): lineP (kProbeLines + 1 u64: present ranks before
+// each line, the total at [kProbeLines]; popTmp kProbeLines u32, scanTmp scan_tmp_elems(kProbeLines)),
+// then runOff (lineP[kProbeLines] + 1 u16: each present rank's run start minus its line's base; lines
+// of more than kRunIdxMax k-mers are not indexed)
+constexpr uint64_t kRunIdxMax = 0xFFFF;
+void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s);
+void build_run_offsets(const uint64_t* dbv, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
+                       uint16_t* runOff, hipStream_t s);
+
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count.
 // keys whose AA rank lies outside [rankLo, rankHi) (a DB part's range) are dropped without a probe
@@ -147,7 +156,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
-                  const ProbeLine* lines, int sortLo, unsigned long long* stats, hipStream_t s);
+                  const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
+                  unsigned long long* stats, hipStream_t s);
 // K4 runs without LDS DB windows (probe-line lower bounds, no window staging): a DB much larger
 // than the query stream; its queries are then sorted finer (kQuerySortLoFine: one more pass buys
 // DRAM-page locality for the random DB reads, measured 28.8 -> 26.5 ms per 1M pairs at GTDB scale)
