@@ -66,6 +66,8 @@ struct mtb_ctx {
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
+    bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
+    bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
@@ -80,7 +82,7 @@ struct mtb_ctx {
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
-    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, waveList, waveCount, devStats;
+    DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, mDirect, ovFlag, waveList, waveCount, devStats;
     DevBuf qFrom, probeStats;
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
@@ -209,6 +211,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
+    if (const char* e = getenv("MTB_DIRECT")) {  // 0: staged join; 2: direct, then rerun staged (tests the fallback)
+        c->directJoin = atoi(e) != 0;
+        c->directRetry = atoi(e) == 2;
+    }
     if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (c->forceGeneric) c->matchWinCap = 0;
@@ -319,7 +325,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -549,15 +555,27 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->matchWin.ensure(sizeof(uint64_t) * std::max<uint64_t>(match_window_elems(Q), 1)));
     c->stageRegion = std::max<uint64_t>(c->stageRegion, std::max<uint64_t>(Q / kStageRegions, 64));
-    HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
-    HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
+    // direct join (sort-merge join): each read's matches go straight into its K1 slot stretch
+    // (a read has at most one query k-mer per slot, and in practice fewer matches than slots), no
+    // staging buffer and no transpose; a read with more matches than slots sends the batch through
+    // the staged join
+    bool direct = !probe && c->directJoin;
+    if (direct) {
+        HIP_TRY(c->mDirect.ensure(sizeof(mtb_match) * Rc));
+        HIP_TRY(c->ovFlag.ensure(sizeof(int)));
+    } else {
+        HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+        HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
+    }
     HIP_TRY(hipEventRecord(c->kev[6], s));
     if (!probe) launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     uint64_t M = 0;
     std::vector<unsigned long long> regTot(kStageRegions);
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0; attempt < 3; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
+        int overflow = 0;
+        if (direct) HIP_TRY(hipMemsetAsync(c->ovFlag.p, 0, sizeof(int), s));
         if (probe)
             launch_probe(qk, qi, qf, Q, c->unitInfo.as<uint64_t>(), C, c->dbv, c->dbinfo, c->D, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
@@ -568,10 +586,21 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
-                         c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(), s);
+                         c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
+                         direct ? c->mDirect.as<mtb_match>() : nullptr, c->slotOff.as<uint64_t>(),
+                         c->ovFlag.as<int>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
+        if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (direct) {
+            if (!overflow && !c->directRetry) break;
+            direct = false;  // a read outgrew its slot stretch: rerun staged
+            HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
+            HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+            continue;
+        }
         M = 0;
         uint64_t most = 0;
         for (unsigned long long t : regTot) {
@@ -585,17 +614,25 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
     }
     HIP_TRY(hipEventRecord(c->kev[7], s));
+    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
+    if (direct) {  // M = the per-read counts' total (the direct join claims no staging stretches)
+        HIP_TRY(hipMemcpyAsync(&M, c->mOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     if (M >= kMaxBatchMatches) {
         set_error("batch produced >= 2^32 matches: split it into smaller batches");
         return MTB_ERR_ARG;
     }
-    exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     c->M = M;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipEventRecord(c->kev[8], s));
-    launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
-                           c->mTotal.as<unsigned long long>(), c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(),
-                           c->errFlag.as<int>(), s);
+    if (direct)
+        launch_compact_segments(c->mDirect.as<mtb_match>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
+                                c->matches.as<mtb_match>(), s);
+    else
+        launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
+                               c->mTotal.as<unsigned long long>(), c->mOff.as<uint64_t>(), n,
+                               c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
     HIP_TRY(hipEventRecord(c->kev[9], s));
     HIP_TRY(hipEventRecord(c->ev[3], s));
     return MTB_OK;

@@ -918,7 +918,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                uint64_t region, int* __restrict__ err, uint32_t winCap, const uint64_t* __restrict__ win,
                                                const ProbeLine* __restrict__ lines,
                                                const uint64_t* __restrict__ lineP, const uint16_t* __restrict__ runOff,
-                                               int sortLo, unsigned long long* __restrict__ stats) {
+                                               int sortLo, unsigned long long* __restrict__ stats,
+                                               mtb_match* __restrict__ direct, const uint64_t* __restrict__ dirOff,
+                                               int* __restrict__ overflow) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -1070,6 +1072,35 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     for (int j = 0; j < kPer; j++) hit += c[j] != 0;
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
     if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
+    if (direct) {
+        // each query's matches straight into its read's segment, at the ranks just reserved: the
+        // read's stretch of C slots per K1 unit (slotOff) bounds it; a read with more matches than
+        // that sets the overflow flag and the caller reruns the batch through the staging buffer
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            if (!c[j]) continue;
+            const uint32_t r = info_seq(info[j]) - 1;
+            const uint64_t o = dirOff[r] * C, cap = dirOff[r + 1] * C - o;
+            if (rk[j] + c[j] > cap) {
+                atomicExch(overflow, 1);
+                continue;
+            }
+            mtb_match* out = direct + o;
+            if (small[j]) {
+                const bool rev = ((info_frame(info[j]) < 3) != (kmerFormat == 2));
+                uint64_t wj = rk[j];
+#pragma unroll
+                for (int k = 0; k < 2; k++)
+                    if (rs[j][k] <= thr[j])
+                        emit_match(key[j], hr[j], info[j], rv[j][k], rt[j][k], rs[j][k], rev, spOf, maxTax, out,
+                                   nullptr, wj++, 0, err);
+            } else {
+                run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
+                         nullptr, rk[j], rk[j] + c[j], 0, err);
+            }
+        }
+        return;
+    }
     unsigned long long blockTot;
     uint64_t w = block_exclusive_scan(mine, &blockTot);
     const uint32_t reg = blockIdx.x % kStageRegions;
@@ -1355,7 +1386,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
-                  unsigned long long* stats, hipStream_t s) {
+                  unsigned long long* stats, mtb_match* direct, const uint64_t* dirOff, int* overflow,
+                  hipStream_t s) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -1364,14 +1396,32 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
         k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
-                                                        win, lines, lineP, runOff, sortLo, stats);
+                                                        win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
+                                                        overflow);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
-                                                            stats);
+                                                            stats, direct, dirOff, overflow);
     }
+}
+
+// Direct join output -> compact per-read segments: read r's n = readOff[r + 1] - readOff[r]
+// matches from its reserved stretch (dirOff[r] * C) to readOff[r]. One wave per read, coalesced.
+__global__ void __launch_bounds__(256) k_compact_segments(const mtb_match* __restrict__ in,
+                                                          const uint64_t* __restrict__ dirOff, uint32_t C,
+                                                          const uint64_t* __restrict__ readOff, uint32_t nReads,
+                                                          mtb_match* __restrict__ out) {
+    const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= nReads) return;
+    const uint64_t src = dirOff[r] * C, dst = readOff[r], n = readOff[r + 1] - dst;
+    for (uint64_t i = lane; i < n; i += 64) out[dst + i] = in[src + i];
+}
+
+void launch_compact_segments(const mtb_match* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
+                             uint32_t nReads, mtb_match* out, hipStream_t s) {
+    if (nReads) k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out);
 }
 
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,

@@ -157,7 +157,13 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
-                  unsigned long long* stats, hipStream_t s);
+                  unsigned long long* stats, mtb_match* direct, const uint64_t* dirOff, int* overflow,
+                  hipStream_t s);
+// direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
+// slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A read whose matches do
+// not fit sets *overflow (nothing of it written): the caller reruns the batch staged.
+void launch_compact_segments(const mtb_match* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
+                             uint32_t nReads, mtb_match* out, hipStream_t s);
 // K4 runs without LDS DB windows (probe-line lower bounds, no window staging): a DB much larger
 // than the query stream; its queries are then sorted finer (kQuerySortLoFine: one more pass buys
 // DRAM-page locality for the random DB reads, measured 28.8 -> 26.5 ms per 1M pairs at GTDB scale)

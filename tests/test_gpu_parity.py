@@ -139,14 +139,17 @@ def test_end_to_end_batches(make_db, db_name):
 
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
-@pytest.mark.parametrize("window", ["0", "0:gallop", "64", "6144"])
+@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "64", "6144", "6144:staged"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
-    oracle's matches whatever the per-block window cap (0 forces the HBM path)."""
+    oracle's matches whatever the per-block window cap (0 forces the HBM path); and both outputs —
+    matches written straight into each read's slot stretch (default), or staged + transposed
+    (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback)."""
     window, _, mode = window.partition(":")
     monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
+    monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2"}.get(mode, "1"))
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, 2)
     reads = _reads(gen, "paired", 2000, seed=9)
