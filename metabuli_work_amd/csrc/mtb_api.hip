@@ -67,7 +67,8 @@ struct mtb_ctx {
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
-    bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
+    bool directRetry = false;
+    bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
@@ -414,9 +415,16 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
-    launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
-                   prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s);
+    if (c->sparse && (!prune || maxSeg > kSegSortRegs || c->segsortGlobal)) {  // K5 reads sparse segments only
+        launch_compact_segments(c->mDirect.as<mtb_match>(), c->slotOff.as<uint64_t>(), c->chunkC,
+                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), s);
+        c->sparse = false;
+    }
+    launch_segsort(c->sparse ? c->mDirect.as<mtb_match>() : c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n,
+                   Mc, c->matchesSorted.as<mtb_match>(), c->segScratch.as<uint64_t>(), maxSeg,
+                   c->forceGeneric || c->segsortGlobal, prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
+                   c->sparse ? c->slotOff.as<uint64_t>() : nullptr, c->chunkC);
+    c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();
     uint64_t kM = M;
@@ -626,10 +634,13 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     c->M = M;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipEventRecord(c->kev[8], s));
-    if (direct)
+    // a batch that goes on to K5 with pruning reads the direct join's segments in place (the
+    // register sorts, segments of <= kSegSortRegs matches); otherwise they are compacted here
+    c->sparse = direct && !c->keepStages && !c->forceGeneric && !c->matchOnly;
+    if (direct && !c->sparse)
         launch_compact_segments(c->mDirect.as<mtb_match>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
                                 c->matches.as<mtb_match>(), s);
-    else
+    else if (!direct)
         launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
                                c->mTotal.as<unsigned long long>(), c->mOff.as<uint64_t>(), n,
                                c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
@@ -718,9 +729,9 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
     c->probed = !c->forceGeneric && c->joinMode == 2;  // the sort-merge join is the default (faster here)
     c->stats[10] = c->probed ? 0 : 1;
+    c->matchOnly = (flags & MTB_MATCH_ONLY) != 0;
     int jrc = join_stage(c, dSeq1, dOff1, dSeq2, dOff2, n, U, C, R, Rc);
     if (jrc != MTB_OK) return jrc;
-    c->matchOnly = (flags & MTB_MATCH_ONLY) != 0;
     if (c->matchOnly) {  // range-partitioned DB: the read owner sorts and scores (mtb_assign_chunks)
         for (int k = 10; k < 14; k++) HIP_TRY(hipEventRecord(c->kev[k], s));
         c->nTaxcnt = 0;
@@ -879,6 +890,7 @@ int mtb_assign_chunks(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_
         dm = c->chunkIn.as<mtb_match>();
         dc = c->chunkCnt.as<uint32_t>();
     }
+    c->sparse = false;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -945,6 +957,7 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     c->qKeys = nullptr;
     c->qSlots = nullptr;
     c->nReads = n;
+    c->sparse = false;
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(nm, 1)));
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));

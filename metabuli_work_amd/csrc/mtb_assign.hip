@@ -39,6 +39,7 @@ __device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, ui
 }
 
 constexpr int kSmallSeg = 512;  // segments up to this many matches sort in registers (one wave, <= 8 per lane)
+static_assert(kSmallSeg == (int)kSegSortRegs, "one register-sort bound");
 constexpr int kBlockSeg = 8192;
 
 // Segments of up to 64E matches sort in registers: element e = 64*slot + lane. Exchanges at
@@ -88,8 +89,8 @@ __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l
 // the live matches, their count in liveCnt[r].
 template <int E>
 __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
-                                             uint64_t base, int n, int lane, uint32_t* __restrict__ liveCnt,
-                                             uint32_t r) {
+                                             uint64_t inBase, uint64_t base, int n, int lane,
+                                             uint32_t* __restrict__ liveCnt, uint32_t r) {
     uint64_t h[E], l[E];
     uint32_t x[E];
 #pragma unroll
@@ -98,14 +99,14 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
         h[sl] = ~0ull;
         l[sl] = ~0ull;
         x[sl] = (uint32_t)e;
-        if (e < n) match_key(in[base + e], h[sl], l[sl]);
+        if (e < n) match_key(in[inBase + e], h[sl], l[sl]);
     }
     wave_bitonic_sort<E>(h, l, x, lane);
     if (!liveCnt) {
 #pragma unroll
         for (int sl = 0; sl < E; sl++) {
             const int e = 64 * sl + lane;
-            if (e < n) out[base + e] = in[base + x[sl]];
+            if (e < n) out[base + e] = in[inBase + x[sl]];
         }
         return;
     }
@@ -141,13 +142,16 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
         const int e = 64 * sl + lane;
         const bool live = e < n && runLive[rid[sl]];
         const uint64_t m = __ballot(live);
-        if (live) out[base + kept + (uint32_t)__popcll(m & lt)] = in[base + x[sl]];
+        if (live) out[base + kept + (uint32_t)__popcll(m & lt)] = in[inBase + x[sl]];
         kept += (uint32_t)__popcll(m);
     }
     if (lane == 0) liveCnt[r] = kept;
 }
 
+// inOff (nullable): the segments are read from in + inOff[r] * inC (the direct join's per-read slot
+// stretches) instead of in + mOff[r]; the output is at out + mOff[r] either way.
 __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
                                                       uint32_t nReads, mtb_match* __restrict__ out,
                                                       uint32_t* __restrict__ liveCnt) {
     const uint32_t r = blockIdx.x;
@@ -155,20 +159,22 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n > 128) return;
+    const uint64_t inBase = inOff ? inOff[r] * inC : base;
     const int lane = threadIdx.x;
     if (n <= 1) {  // a lone match is a dead species run
-        if (lane == 0 && n == 1 && !liveCnt) out[base] = in[base];
+        if (lane == 0 && n == 1 && !liveCnt) out[base] = in[inBase];
         if (lane == 0 && liveCnt) liveCnt[r] = 0;
         return;
     }
-    if (n <= 64) segsort_regs<1>(in, out, base, n, lane, liveCnt, r);
-    else segsort_regs<2>(in, out, base, n, lane, liveCnt, r);
+    if (n <= 64) segsort_regs<1>(in, out, inBase, base, n, lane, liveCnt, r);
+    else segsort_regs<2>(in, out, inBase, base, n, lane, liveCnt, r);
 }
 
 // 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
 // lane, in kernels of their own so the small kernel keeps its register budget (occupancy).
 template <int E>
 __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                     const uint64_t* __restrict__ inOff, uint32_t inC,
                                                      uint32_t nReads, mtb_match* __restrict__ out,
                                                      uint32_t* __restrict__ liveCnt) {
     const uint32_t r = blockIdx.x;
@@ -176,7 +182,7 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n <= 32 * E || n > 64 * E) return;
-    segsort_regs<E>(in, out, base, n, (int)threadIdx.x, liveCnt, r);
+    segsort_regs<E>(in, out, inOff ? inOff[r] * inC : base, base, n, (int)threadIdx.x, liveCnt, r);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -519,16 +525,17 @@ static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_
 
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                     uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s) {
+                    hipStream_t s, const uint64_t* inOff, uint32_t inC) {
     if (nReads == 0) return;
+    if (inOff && (global || maxSeg > kSmallSeg)) return;  // sparse input: register sorts only (caller's contract)
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk);
         return;
     }
-    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
-    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
-    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, nReads, out, liveCnt);
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
+    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
+    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
     if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);

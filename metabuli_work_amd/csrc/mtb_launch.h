@@ -184,15 +184,18 @@ uint64_t clade_bytes();
 // reads) from segments of <= 512 matches, write each segment front-packed and its live count
 // mergeSeg: segments over this many matches (default, 0: 8192, the LDS capacity) sort as LDS chunks of
 // that size merged pairwise (tests lower it to exercise the merge path)
+// inOff (nullable, only with maxSeg <= 512 and !global): read segment r from in + inOff[r] * inC
+// (the direct join's layout) rather than in + mOff[r]
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                     uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s);
+                    hipStream_t s, const uint64_t* inOff = nullptr, uint32_t inC = 0);
 // the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
                       mtb_match* out, int* err, hipStream_t s);
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 8192;
+constexpr uint32_t kSegSortRegs = 512;  // segments up to this many matches sort in registers (sparse input allowed)
 // K6 indexes matches and groups with 32 bits
 constexpr uint64_t kMaxBatchMatches = 0xFFFFFFFFull;  // segments up to this many matches sort in LDS
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
