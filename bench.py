@@ -64,8 +64,10 @@ def alg_bytes(n, Q, M, D):
         "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
         "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
         # queries, the DB (values + taxIDs) read once through the block windows, or, when the DB is
-        # much larger than the query stream, each query's run (8 entries), staged matches written
-        "match_join": 12 * Q + min(12 * D, 96 * Q) + 28 * M,
+        # much larger than the query stream (D > 24 Q), each query's run: its two run-index entries
+        # (4 B) and the run's first two values + taxIDs (24 B); the matches written into the reads'
+        # segments (direct join)
+        "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 24 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
         "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
@@ -114,6 +116,7 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--long-reads", type=int, default=50_000,
                     help="ONT-style reads (N50 ~10 kb) per rank for the long-read line (0 = off)")
+    ap.add_argument("--long-batch", type=int, default=25_000, help="long reads per mtb_classify_batch")
     ap.add_argument("--db-parts", type=int, default=0,
                     help="config-5 mode: the DB range-partitioned into this many parts (= the number of ranks; "
                          "on one GPU every part is timed in turn)")
@@ -300,8 +303,25 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
     with the GPU's results for the same reads compared to it."""
     lpl = LocalParameters(seqMode=3, kmerFormat=2, skipRedundancy=1)
     clfl = open_clf(lpl)
+    # batches of at most args.long_batch reads (the reference's RAM-bounded QuerySplits), cut
+    # before the timed region
+    nl_all = lo1.numel() - 1
+    lb = max(1, args.long_batch)
+    cuts = []
+    for a in range(0, nl_all, lb):
+        b = min(nl_all, a + lb)
+        base = int(lo1[a].item())
+        cuts.append((ls1[base:int(lo1[b].item())], (lo1[a:b + 1] - base).contiguous()))
+
+    def long_step():
+        k = np.zeros(7)
+        for cs, co in cuts:
+            clfl.classify_batch(cs, co, device_input=True, fetch=False)
+            k += clfl.kernel_ms()
+        return k
+
     for _ in range(max(1, args.warmup)):
-        clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
+        long_step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -309,8 +329,7 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
     kl = np.zeros(7)
     tl0 = time.perf_counter()
     for _ in range(lsteps):
-        clfl.classify_batch(ls1, lo1, device_input=True, fetch=False)
-        kl += clfl.kernel_ms()
+        kl += long_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -347,7 +366,7 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
     return {"value": round(world * n_long * lsteps / tl, 1), "unit": "reads/s",
             "ms_per_step": round(tl / lsteps * 1e3, 3), "steps": lsteps,
             "reads_per_gpu": n_long, "bases_per_gpu": int(lo1[-1].item()), "n50": n50,
-            "query_kmers": lq, "matches": lm,
+            "batch_reads": lb, "query_kmers": lq, "matches": lm,  # counts and work: the step's last batch
             "kernel_ms": {k: round(float(v) / lsteps, 3) for k, v in zip(kernel_names(lwork), kl)},
             "cpu_baseline": long_cpu, "work": lwork,
             "workload": f"config-4-shaped ONT reads (lognormal N50 ~10 kb, 5% subs, 1% indels) vs {db_name}, "

@@ -568,8 +568,11 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // staging buffer and no transpose; a read with more matches than slots sends the batch through
     // the staged join
     bool direct = !probe && c->directJoin;
+    if (direct && c->mDirect.ensure(sizeof(mtb_match) * Rc) != hipSuccess) {
+        (void)hipGetLastError();  // no room for a slot-sized match buffer (e.g. a long-read batch): staged join
+        direct = false;
+    }
     if (direct) {
-        HIP_TRY(c->mDirect.ensure(sizeof(mtb_match) * Rc));
         HIP_TRY(c->ovFlag.ensure(sizeof(int)));
     } else {
         HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));

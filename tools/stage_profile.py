@@ -4,7 +4,7 @@ Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by
 within a step: a step starts at k_read_meta; extract = up to and including k_extract; filter =
 k_filter; kmer_sort = everything from there to the join; match_join = k_match_windows + k_match
 (probe_join = k_probe on MTB_JOIN=probe), with the per-read count scan and a rerun if the staging
-buffer grew; match_transpose = k_match_transpose; match_sort = k_segsort_* (+ the live-match scan
+buffer grew; match_transpose = k_match_transpose or k_compact_segments (direct join); match_sort = k_segsort_* (+ the live-match scan
 and k_pack_live); assign = the rest of
 the step (K6 kernels, scans and taxcnt compaction).
 
@@ -46,7 +46,7 @@ def stage_of(seq):
             stage = "match_join"
         elif k == "k_probe" or k.startswith("k_probe<"):
             stage = "probe_join"
-        elif k.startswith("k_match_transpose"):
+        elif k.startswith(("k_match_transpose", "k_compact_segments")):
             stage = "match_transpose"
         elif k.startswith(("k_segsort", "k_max_seg", "k_pack_live", "k_chunk_sort", "k_merge_tiles", "k_merge_finish")):
             stage = "match_sort"
