@@ -290,6 +290,14 @@ const char* mtb_taxon_rank(const mtb_ctx* ctx, int32_t tax_id);
  * append, one line per read; taxcnt as returned by mtb_get_taxcnt. */
 int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
                               const mtb_result* results, const mtb_taxcnt* taxcnt);
+/* Reporter::writeReportFile's per-taxon report (Reporter.cpp:175-190, writeReport :217-244; clade
+ * counts by NcbiTaxonomy::getCladeCounts / getParentToChildren semantics): tax_ids[i] / counts[i] =
+ * reads classified to each taxID over the run (++taxCounts[classification], Classifier.cpp:201-203;
+ * taxID 0 = unclassified), total_reads = all reads of the run. Writes the TSV
+ * "#clade_proportion\tclade_count\ttaxon_count\trank\ttaxID\tname"; the Krona chart is not
+ * written (its HTML prelude is MMseqs2 data absent from the reference). */
+int mtb_write_report(const mtb_ctx* ctx, const char* path, uint64_t total_reads, const int32_t* tax_ids,
+                     const uint32_t* counts, uint64_t n);
 
 #ifdef __cplusplus
 }

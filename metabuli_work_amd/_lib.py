@@ -20,7 +20,7 @@ EXPORTED = [
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
-    "mtb_assign_chunks", "mtb_open_resident",
+    "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report",
 ]
 
 
@@ -70,6 +70,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_taxon_rank.argtypes = [vp, ctypes.c_int32]
     L.mtb_taxon_rank.restype = ctypes.c_char_p
     L.mtb_write_classifications.argtypes = [vp, ctypes.c_char_p, i32, P(MtbReadBatch), vp, vp]
+    L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
     L.mtb_debug_tables.argtypes = [vp, vp, vp]
     L.mtb_debug_tables.restype = None
     _LIB = L

@@ -247,14 +247,24 @@ class Classifier:
         return BatchResult(res, self.taxcnt(), 0, n_matches, self.stage_ms())
 
     # -- Classifier::startClassify over files ----------------------------------------------------
-    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000) -> int:
+    def write_report(self, path: str, total_reads: int, tax_counts: dict) -> None:
+        """Reporter::writeReportFile (Reporter.cpp:175-190): the per-taxon report of a run from
+        tax_counts = {classification taxID: reads} (++taxCounts[classification], Classifier.cpp:201-203)."""
+        ids = np.fromiter(tax_counts.keys(), np.int32, len(tax_counts))
+        cnt = np.fromiter(tax_counts.values(), np.uint32, len(tax_counts))
+        check(lib().mtb_write_report(self.handle, path.encode(), total_reads, ptr(ids), ptr(cnt), len(ids)),
+              "mtb_write_report")
+
+    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164): batches from the native FASTA/FASTQ(.gz)
-        reader (mtb_reader_*), one mtb_classify_batch each, TSV lines by mtb_write_classifications."""
+        reader (mtb_reader_*), one mtb_classify_batch each, TSV lines by mtb_write_classifications;
+        with report_tsv, the per-taxon report of the run (mtb_write_report, Classifier.cpp:149)."""
         par = self.par
         q1 = par.filenames[0]
         q2 = par.filenames[1] if par.seqMode == 2 else None
         total = 0
         first = True
+        tax_counts: dict = {}
         with FastxReader(q1, q2) as rd:
             while True:
                 b = rd.next(reads_per_batch)
@@ -270,9 +280,15 @@ class Classifier:
                       "mtb_write_classifications")
                 first = False
                 total += n
+                cls, cnt = np.unique(np.where(res["is_classified"] != 0, res["classification"], 0),
+                                     return_counts=True)
+                for t, k in zip(cls.tolist(), cnt.tolist()):
+                    tax_counts[t] = tax_counts.get(t, 0) + k
         if first:  # no reads: header only
             with open(out_tsv, "w") as out:
                 out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n")
+        if report_tsv is not None:
+            self.write_report(report_tsv, total, tax_counts)
         return total
 
     _rank_of = None

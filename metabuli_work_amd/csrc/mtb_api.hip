@@ -5,6 +5,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <algorithm>
+#include <unordered_map>
 
 #include "mtb_host.h"
 #include "mtb_launch.h"
@@ -79,6 +81,7 @@ struct mtb_ctx {
     uint32_t cladePerMatch = 2;
     std::vector<int32_t> hNodeOf;  // host copies for mtb_taxon_rank / the TSV writer
     std::vector<std::string> hRank;
+    HostTaxonomy hTax;             // the report (mtb_write_report): names, parents, nodes.dmp order
     // batch workspace
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
@@ -252,6 +255,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     c->maxTax = T.maxTax;
     c->hNodeOf = T.nodeOf;
     c->hRank = T.rank;
+    c->hTax = T;
     HIP_TRY(upload(&c->spOf, db.speciesOf, s));
     HIP_TRY(upload(&c->tNodeOf, T.nodeOf, s));
     HIP_TRY(upload(&c->tNodeTax, T.nodeTax, s));
@@ -798,6 +802,92 @@ int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
     if (!c) return MTB_ERR_ARG;
     if (q) *q = c->Q;
     if (m) *m = c->M;
+    return MTB_OK;
+}
+
+// Kraken-style report. Clade counts: each taxID's reads added to itself and every ancestor below
+// the root's self-loop (getCladeCounts); children of a taxon in nodes.dmp order (getParentToChildren),
+// sorted by clade count, descending, with std::sort as SORT_SERIAL does (ties in libstdc++'s order);
+// a taxon is written only with a nonzero clade count, depth-first, two spaces of indent per level.
+namespace {
+struct CladeCounts {
+    uint32_t taxCount = 0, cladeCount = 0;
+};
+struct ReportWriter {
+    const HostTaxonomy& T;
+    const std::unordered_map<int32_t, CladeCounts>& cc;
+    const std::vector<std::vector<int32_t>>& children;  // by node
+    unsigned long total;
+    std::string out;
+    uint32_t cladeOf(int32_t t) const {
+        auto it = cc.find(t);
+        return it == cc.end() ? 0 : it->second.cladeCount;
+    }
+    void line(uint32_t clade, uint32_t taxc, const std::string& rank, int32_t t, int depth, const std::string& name) {
+        char buf[96];
+        // 100 * cladeCount is unsigned int arithmetic in the reference (Reporter.cpp:233)
+        snprintf(buf, sizeof buf, "%.4f\t%i\t%i\t", 100u * clade / double(total), (int)clade, (int)taxc);
+        out += buf;
+        out += rank;
+        snprintf(buf, sizeof buf, "\t%i\t", t);
+        out += buf;
+        out.append(2 * depth, ' ');
+        out += name;
+        out += '\n';
+    }
+    void walk(int32_t t, int depth) {  // Reporter::writeReport, Reporter.cpp:217-244
+        auto it = cc.find(t);
+        const uint32_t clade = it == cc.end() ? 0 : it->second.cladeCount;
+        if (t == 0) {
+            if (clade > 0) {
+                char buf[96];
+                snprintf(buf, sizeof buf, "%.4f\t%i\t%i\tno rank\t0\tunclassified\n", 100u * clade / double(total),
+                         (int)clade, (int)it->second.taxCount);
+                out += buf;
+            }
+            walk(1, 0);
+            return;
+        }
+        if (clade == 0) return;
+        const int node = T.nodeOf[t];
+        line(clade, it->second.taxCount, T.rank[node], t, depth, T.name[node]);
+        std::vector<int32_t> ch = children[node];
+        std::sort(ch.begin(), ch.end(), [&](int32_t a, int32_t b) { return cladeOf(a) > cladeOf(b); });
+        for (int32_t x : ch) {
+            if (!cc.count(x)) break;
+            walk(x, depth + 1);
+        }
+    }
+};
+}  // namespace
+
+int mtb_write_report(const mtb_ctx* c, const char* path, uint64_t total_reads, const int32_t* tax_ids,
+                     const uint32_t* counts, uint64_t n) {
+    if (!c || !path || (n && (!tax_ids || !counts))) { set_error("null argument"); return MTB_ERR_ARG; }
+    const HostTaxonomy& T = c->hTax;
+    if (!T.exists(1)) { set_error("context has no taxonomy"); return MTB_ERR_ARG; }
+    std::unordered_map<int32_t, CladeCounts> cc;
+    for (uint64_t i = 0; i < n; i++) {
+        const int32_t t = tax_ids[i];
+        cc[t].taxCount = counts[i];
+        cc[t].cladeCount += counts[i];
+        if (!T.exists(t)) continue;
+        int node = T.nodeOf[t];
+        while (T.parent[node] != node) {  // the root is its own parent
+            node = T.parent[node];
+            cc[T.nodeTax[node]].cladeCount += counts[i];
+        }
+    }
+    std::vector<std::vector<int32_t>> children(T.nodeTax.size());
+    for (size_t i = 0; i < T.nodeTax.size(); i++)
+        if ((int)i != T.parent[i]) children[T.parent[i]].push_back(T.nodeTax[i]);
+    ReportWriter w{T, cc, children, (unsigned long)(int)total_reads, {}};  // numOfQuery is an int
+    w.out = "#clade_proportion\tclade_count\ttaxon_count\trank\ttaxID\tname\n";
+    w.walk(0, 0);
+    FILE* f = fopen(path, "wb");
+    if (!f) { set_error(std::string("cannot write ") + path); return MTB_ERR_IO; }
+    fwrite(w.out.data(), 1, w.out.size(), f);
+    if (fclose(f) != 0) { set_error(std::string("write failed: ") + path); return MTB_ERR_IO; }
     return MTB_OK;
 }
 

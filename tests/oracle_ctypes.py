@@ -46,6 +46,8 @@ def lib():
         L.orc_set_threads.argtypes = [i32]
         L.orc_threads.restype = i32
         L.orc_genetic_tables.argtypes = [vp, vp, vp, vp]
+        L.orc_write_report.argtypes = [vp, ctypes.c_char_p, i32, vp, vp, u64]
+        L.orc_write_report.restype = i32
         _LIB = L
     return _LIB
 
@@ -186,3 +188,11 @@ def classify(db: OracleDb, par: MtbParams, reads, stage_s=None, counts=None):
     if counts is not None:
         counts[:] = cnt
     return out
+
+
+def write_report(db: OracleDb, path: str, total_reads: int, tax_counts: dict) -> None:
+    """Reporter::writeReportFile's per-taxon TSV (oracle/orc_reporter.cpp)."""
+    ids = np.fromiter(tax_counts.keys(), np.int32, len(tax_counts))
+    cnt = np.fromiter(tax_counts.values(), np.uint32, len(tax_counts))
+    if lib().orc_write_report(db.h, path.encode(), total_reads, ids.ctypes.data, cnt.ctypes.data, len(ids)) != 0:
+        raise RuntimeError("orc_write_report failed")

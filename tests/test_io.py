@@ -113,11 +113,20 @@ def test_start_classify_tsv(make_db, tmp_path):
     par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
     par.load_db_parameters(db_dir)
     out = str(tmp_path / "out.tsv")
+    rep = str(tmp_path / "report.tsv")
     with Classifier(par, db_dir=db_dir) as clf:
-        assert clf.startClassify(out, reads_per_batch=700) == r.n
+        assert clf.startClassify(out, reads_per_batch=700, report_tsv=rep) == r.n
     odb = oc.OracleDb(db_dir)
     ores, otc = oc.classify(odb, par.to_c(), r)
+    # the per-taxon report (Reporter::writeReportFile) of the oracle's classifications, byte for byte
+    cls, cnt = np.unique(np.where(ores["is_classified"] != 0, ores["classification"], 0), return_counts=True)
+    orep = str(tmp_path / "oracle_report.tsv")
+    oc.write_report(odb, orep, r.n, dict(zip(cls.tolist(), cnt.tolist())))
     odb.close()
+    got, want = open(rep).read(), open(orep).read()
+    assert got == want
+    assert want.startswith("#clade_proportion\tclade_count\ttaxon_count\trank\ttaxID\tname\n")
+    assert len(want.splitlines()) > 3
     rank_of = dict(zip(taxo.taxid.tolist(), taxo.rank))
     lines = open(out).read().split("\n")
     assert lines[0] == "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count"

@@ -124,3 +124,44 @@ def test_oracle_classifies_synthetic_reads(make_db):
     assert ok / tot > 0.95
     rnd = origin < 0
     assert res["is_classified"][rnd].mean() < 0.2
+
+
+def test_oracle_report_by_hand(make_db, tmp_path):
+    """The oracle's per-taxon report (Reporter::writeReportFile, Reporter.cpp:175-244) against a
+    report worked out here from the taxonomy: clade counts up the parent chain, unclassified first,
+    children by clade count (distinct counts: no ties), two spaces of indent per depth."""
+    d, taxo, gen = make_db("fmt2")
+    tid = taxo.taxid.tolist()
+    par = dict(zip(tid, taxo.parent.tolist()))
+    rank = dict(zip(tid, taxo.rank))
+    name = dict(zip(tid, taxo.name))
+    strains = [int(t) for t in gen.taxid[:3]]
+    counts = {0: 7, strains[0]: 5, strains[1]: 3, int(gen.species[2]): 2}
+    total = 20
+    clade = {}
+    for t, c in counts.items():
+        clade[t] = clade.get(t, 0) + c
+        x = t
+        while t and par[x] != x:
+            x = par[x]
+            clade[x] = clade.get(x, 0) + c
+    kids = {}
+    for t in tid:
+        if par[t] != t:
+            kids.setdefault(par[t], []).append(t)
+    want = ["#clade_proportion\tclade_count\ttaxon_count\trank\ttaxID\tname",
+            "%.4f\t%d\t%d\tno rank\t0\tunclassified" % (100 * 7 / total, 7, 7)]
+
+    def walk(t, depth):
+        want.append("%.4f\t%d\t%d\t%s\t%d\t%s%s" % (100 * clade[t] / total, clade[t], counts.get(t, 0), rank[t], t,
+                                                     "  " * depth, name[t]))
+        for c in sorted((k for k in kids.get(t, []) if k in clade), key=lambda k: -clade[k]):
+            walk(c, depth + 1)
+
+    walk(1, 0)
+    assert len(set(clade[k] for k in clade)) >= 3
+    db = oc.OracleDb(d)
+    out = str(tmp_path / "report.tsv")
+    oc.write_report(db, out, total, counts)
+    db.close()
+    assert open(out).read() == "\n".join(want) + "\n"
