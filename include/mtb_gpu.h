@@ -123,14 +123,14 @@ typedef struct mtb_db_host {
 
 /* A decoded reference DB already resident in HBM (a DB built in place on the device, e.g. the
  * GTDB-scale synthetic DB of the bench, SURVEY §8(d) config 3, which is never written out).
- * values: n_kmers sorted k-mer values (the diffIdx decoded: getNextTargetKmer, KmerMatcher.h:282-297);
- * with rank_form = 1 and kmer_format 2 the AA part is already the base-21 rank of the 8 AA codes
- * (the resident form). info: the matching taxIDs. Both are device arrays with room
- * for n_kmers + 8 entries; the context uses them in place (pads written, info masked, format-2
- * values converted to rank form) and does not free them: they must outlive the context. */
+ * records: a device array of n_kmers + 8 records of three uint32 {value low 32 bits, value high
+ * 32 bits, taxID}, sorted by value: the diffIdx decoded (getNextTargetKmer, KmerMatcher.h:282-297)
+ * next to its info entry. With rank_form = 1 and kmer_format 2 the AA part of each value is
+ * already the base-21 rank of the 8 AA codes (the resident form). The context uses
+ * the records in place (pads written, taxIDs masked, format-2 values converted to rank form) and
+ * does not free them: they must outlive the context. */
 typedef struct mtb_db_resident {
-    uint64_t* values;
-    uint32_t* info;
+    void* records;
     uint64_t n_kmers;
     int32_t rank_form;
     int32_t reserved;

@@ -41,7 +41,7 @@ class MtbDbHost(ctypes.Structure):
 
 
 class MtbDbResident(ctypes.Structure):
-    _fields_ = [("values", ctypes.c_void_p), ("info", ctypes.c_void_p), ("n_kmers", ctypes.c_uint64),
+    _fields_ = [("records", ctypes.c_void_p), ("n_kmers", ctypes.c_uint64),
                 ("rank_form", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 

@@ -57,9 +57,8 @@ struct mtb_ctx {
     HostTables tables{};
     // DB residency
     uint64_t D = 0;
-    uint64_t* dbv = nullptr;
-    bool borrowedDb = false;  // dbv/dbinfo belong to the caller (mtb_open_resident)
-    uint32_t* dbinfo = nullptr;
+    DbRec* db = nullptr;      // D + kDbPad records: value (rank form) + taxID & mask
+    bool borrowedDb = false;  // db belongs to the caller (mtb_open_resident)
     uint64_t* dirMem = nullptr;
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
@@ -115,12 +114,11 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
-    if (c->borrowedDb) c->dbv = nullptr, c->dbinfo = nullptr;  // caller-owned (mtb_open_resident)
-    void* ptrs[] = {c->dbv, c->dbinfo, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    if (c->borrowedDb) c->db = nullptr;  // caller-owned (mtb_open_resident)
+    void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    c->dbv = nullptr;
-    c->dbinfo = nullptr;
+    c->db = nullptr;
     c->dirMem = nullptr;
     c->lines = nullptr;
     c->lineP = nullptr;
@@ -152,7 +150,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (rc != MTB_OK) return rc;
     if (res) {
         if (par->db_parts > 1) { set_error("a resident DB cannot be range-partitioned: pass each part's arrays"); return MTB_ERR_ARG; }
-        if (!res->values || !res->info || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
+        if (!res->records || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
     } else {
         if (!check_db(db)) return MTB_ERR_DB;
         if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
@@ -169,49 +167,55 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     for (auto& e : c->kev) HIP_TRY(hipEventCreate(&e));
     hipStream_t s = c->stream;
     const uint32_t mask = ~((uint32_t)(par->skip_redundancy == 0) << 31);
-    if (res) {  // caller-owned arrays, used in place (capacity n_kmers + kDbPad)
+    const DbRec padRec[kDbPad] = {{~0u, ~0u, 0}, {~0u, ~0u, 0}, {~0u, ~0u, 0}, {~0u, ~0u, 0},
+                                  {~0u, ~0u, 0}, {~0u, ~0u, 0}, {~0u, ~0u, 0}, {~0u, ~0u, 0}};
+    if (res) {  // caller-owned records, used in place (capacity n_kmers + kDbPad)
         c->D = res->n_kmers;
-        c->dbv = res->values;
-        c->dbinfo = res->info;
+        c->db = reinterpret_cast<DbRec*>(res->records);
         c->borrowedDb = true;
-        HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
-        HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
-        launch_mask_info(c->dbinfo, c->D, mask, s);
-        if (par->kmer_format == 2 && !res->rank_form) launch_to_rank_form(c->dbv, c->D, s);
+        launch_rec_mask_info(c->db, c->D, mask, s);
+        if (par->kmer_format == 2 && !res->rank_form) launch_rec_rank_form(c->db, c->D, s);
     } else {
         c->D = db.info.size();
-        // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381)
+        // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381), then one record per k-mer
         uint16_t* dDiff = nullptr;
         uint32_t* dFlag = nullptr;
-        uint64_t* dIdx = nullptr;
+        uint64_t *dIdx = nullptr, *dVal = nullptr;
+        uint32_t* dInfo = nullptr;
         void* dTmp = nullptr;
         const uint64_t nDiff = db.diffIdx.size();
-        HIP_TRY(hipMalloc(&c->dbv, (c->D + kDbPad) * sizeof(uint64_t)));  // + ~0 pad: the probe's 8 loads need no bound
-        HIP_TRY(hipMemsetAsync(c->dbv + c->D, 0xFF, kDbPad * sizeof(uint64_t), s));
+        HIP_TRY(hipMalloc(&dVal, c->D * sizeof(uint64_t)));
         HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
         HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
         HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
         HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-        decode_diff_idx(dDiff, nDiff, c->dbv, c->D, dFlag, dIdx, dTmp, s);
-        HIP_TRY(hipMalloc(&c->dbinfo, (c->D + kDbPad) * sizeof(uint32_t)));  // + pad: the emit's 8 loads need no bound
-        HIP_TRY(hipMemcpyAsync(c->dbinfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(c->dbinfo + c->D, 0, kDbPad * sizeof(uint32_t), s));
-        launch_mask_info(c->dbinfo, c->D, mask, s);
-        if (par->kmer_format == 2) launch_to_rank_form(c->dbv, c->D, s);
+        decode_diff_idx(dDiff, nDiff, dVal, c->D, dFlag, dIdx, dTmp, s);
         HIP_TRY(hipStreamSynchronize(s));
         hipFree(dDiff);
         hipFree(dFlag);
         hipFree(dIdx);
         hipFree(dTmp);
-    }
-    if (par->db_parts > 1) {  // the part's AA-rank range: its first k-mer up to its guard k-mer's run
-        uint64_t ends[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(&ends[0], c->dbv, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(&ends[1], c->dbv + c->D - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMalloc(&dInfo, c->D * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpyAsync(dInfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        launch_mask_info(dInfo, c->D, mask, s);
+        if (par->kmer_format == 2) launch_to_rank_form(dVal, c->D, s);
+        HIP_TRY(hipMalloc(&c->db, (c->D + kDbPad) * sizeof(DbRec)));
+        launch_pack_db(dVal, dInfo, c->D, c->db, s);
         HIP_TRY(hipStreamSynchronize(s));
-        c->rankLo = ends[0] >> 24;
-        c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ends[1] >> 24;
+        hipFree(dVal);
+        hipFree(dInfo);
+    }
+    // + kDbPad records of value ~0 / taxID 0: the probe's 8-wide reads from any DB index need no bound
+    HIP_TRY(hipMemcpyAsync(c->db + c->D, padRec, sizeof(padRec), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (par->db_parts > 1) {  // the part's AA-rank range: its first k-mer up to its guard k-mer's run
+        DbRec ends[2];
+        HIP_TRY(hipMemcpyAsync(&ends[0], c->db, sizeof(DbRec), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&ends[1], c->db + c->D - 1, sizeof(DbRec), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->rankLo = ((uint64_t)ends[0].hi << 32 | ends[0].lo) >> 24;
+        c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
@@ -225,12 +229,12 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
-    build_aa_dir(c->dbv, c->D, c->dir, c->dirMem, s);
+    build_aa_dir(c->db, c->D, c->dir, c->dirMem, s);
     if (const char* e = getenv("MTB_JOIN")) c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : 0;
     if (!c->forceGeneric) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
-        build_probe_lines(c->dbv, c->D, c->dir, c->lines, s);
+        build_probe_lines(c->db, c->D, c->dir, c->lines, s);
         const char* ri = getenv("MTB_RUN_INDEX");  // 0: no run index (the unstaged join gallops)
         if (!ri || atoi(ri) != 0) {
             uint32_t* pop = nullptr;
@@ -245,7 +249,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
             hipFree(pop);
             hipFree(tmp);
             HIP_TRY(hipMalloc(&c->runOff, (P + 1) * sizeof(uint16_t)));
-            build_run_offsets(c->dbv, c->D, c->lines, c->lineP, c->runOff, s);
+            build_run_offsets(c->db, c->D, c->lines, c->lineP, c->runOff, s);
         }
     }
     HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
@@ -583,7 +587,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
     }
     HIP_TRY(hipEventRecord(c->kev[6], s));
-    if (!probe) launch_match_windows(qk, Q, c->dbv, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
+    if (!probe) launch_match_windows(qk, Q, c->db, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     uint64_t M = 0;
     std::vector<unsigned long long> regTot(kStageRegions);
     for (int attempt = 0; attempt < 3; attempt++) {
@@ -592,12 +596,12 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         int overflow = 0;
         if (direct) HIP_TRY(hipMemsetAsync(c->ovFlag.p, 0, sizeof(int), s));
         if (probe)
-            launch_probe(qk, qi, qf, Q, c->unitInfo.as<uint64_t>(), C, c->dbv, c->dbinfo, c->D, c->spOf,
+            launch_probe(qk, qi, qf, Q, c->unitInfo.as<uint64_t>(), C, c->db, c->D, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(), s);
         else
-            launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->dbv, c->dbinfo, c->D, c->dir, c->spOf,
+            launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->db, c->D, c->dir, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),

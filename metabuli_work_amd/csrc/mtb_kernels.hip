@@ -373,8 +373,20 @@ __device__ __forceinline__ uint64_t line_lower_bound(const ProbeLine* __restrict
 }
 
 // First index >= lo with a[i] >= key (an answer exists below D + kDbPad: the pad is ~0).
-__device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key);
-__device__ __forceinline__ uint64_t gallop_lower1(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key);
+// Read views of the resident DB records (value / taxID by index), so one search code serves LDS
+// windows (plain arrays) and the records in HBM.
+struct DbVal {
+    const DbRec* __restrict__ r;
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const { return (uint64_t)r[i].hi << 32 | r[i].lo; }
+};
+struct DbTax {
+    const DbRec* __restrict__ r;
+    __device__ __forceinline__ uint32_t operator[](uint64_t i) const { return r[i].tax; }
+};
+template <typename A>
+__device__ __forceinline__ uint64_t gallop_lower(const A& a, uint64_t lo, uint64_t key);
+template <typename A>
+__device__ __forceinline__ uint64_t gallop_lower1(const A& a, uint64_t lo, uint64_t key);
 
 __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                  const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
@@ -634,8 +646,8 @@ void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uin
 // KmerMatcher.cpp:363,378). Selected = hamming sum <= min(2*min, 7). COUNT pass: per-read match
 // counts. EMIT pass: records into per-read segments.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* __restrict__ a, uint64_t lo, uint64_t hi,
-                                                    uint64_t key) {
+template <typename A>
+__device__ __forceinline__ uint64_t lower_bound_u64(const A& a, uint64_t lo, uint64_t hi, uint64_t key) {
     while (lo < hi) {
         uint64_t mid = lo + ((hi - lo) >> 1);
         if (a[mid] < key) lo = mid + 1; else hi = mid;
@@ -674,13 +686,41 @@ __global__ void k_to_rank_form(uint64_t* __restrict__ v, uint64_t n) {
     MTB_GRID_STRIDE(i, n) v[i] = to_rank_form(v[i]);
 }
 
+__global__ void k_pack_db(const uint64_t* __restrict__ v, const uint32_t* __restrict__ tax, uint64_t n,
+                          DbRec* __restrict__ out) {
+    MTB_GRID_STRIDE(i, n) out[i] = DbRec{(uint32_t)v[i], (uint32_t)(v[i] >> 32), tax[i]};
+}
+
+__global__ void k_rec_rank_form(DbRec* __restrict__ db, uint64_t n) {
+    MTB_GRID_STRIDE(i, n) {
+        const uint64_t x = to_rank_form((uint64_t)db[i].hi << 32 | db[i].lo);
+        db[i].lo = (uint32_t)x;
+        db[i].hi = (uint32_t)(x >> 32);
+    }
+}
+
+__global__ void k_rec_mask_info(DbRec* __restrict__ db, uint64_t n, uint32_t mask) {
+    MTB_GRID_STRIDE(i, n) db[i].tax &= mask;
+}
+
+void launch_pack_db(const uint64_t* v, const uint32_t* tax, uint64_t n, DbRec* out, hipStream_t s) {
+    if (n) k_pack_db<<<stride_grid(n), 256, 0, s>>>(v, tax, n, out);
+}
+void launch_rec_rank_form(DbRec* db, uint64_t n, hipStream_t s) {
+    if (n) k_rec_rank_form<<<stride_grid(n), 256, 0, s>>>(db, n);
+}
+void launch_rec_mask_info(DbRec* db, uint64_t n, uint32_t mask, hipStream_t s) {
+    if (n) k_rec_mask_info<<<stride_grid(n), 256, 0, s>>>(db, n, mask);
+}
+
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
     if (n) k_to_rank_form<<<stride_grid(n), 256, 0, s>>>(v, n);
 }
 
 uint64_t host_from_rank_form(uint64_t v) { return from_rank_form(v); }
 
-__global__ void k_build_dir(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
+__global__ void k_build_dir(const DbRec* __restrict__ db, uint64_t D, AADir d, uint64_t* __restrict__ dir) {
+    const DbVal dbv{db};
     uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b > d.R) return;
     dir[b] = (b == d.R) ? D : lower_bound_u64(dbv, 0, D, aa_bucket_floor(b, d));
@@ -698,13 +738,14 @@ AADir make_aa_dir(uint64_t D, int kmerFormat) {
     return d;
 }
 
-void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s) {
-    k_build_dir<<<(unsigned)((d.R + 1 + 255) / 256), 256, 0, s>>>(dbv, D, d, dir);
+void build_aa_dir(const DbRec* db, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s) {
+    k_build_dir<<<(unsigned)((d.R + 1 + 255) / 256), 256, 0, s>>>(db, D, d, dir);
 }
 
 // Line heads: the DB index of the first k-mer of rank >= the line's first rank (lower bound inside
 // the directory bucket of that rank); the end line holds D.
-__global__ void k_line_base(const uint64_t* __restrict__ dbv, uint64_t D, AADir d, ProbeLine* __restrict__ lines) {
+__global__ void k_line_base(const DbRec* __restrict__ db, uint64_t D, AADir d, ProbeLine* __restrict__ lines) {
+    const DbVal dbv{db};
     const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= kProbeLines) return;
     const uint64_t r = l * kLineRanks;
@@ -727,7 +768,8 @@ __global__ void k_line_count(ProbeLine* __restrict__ lines) {
 }
 
 // Membership bits: the first k-mer of each AA run sets its rank's bit.
-__global__ void k_line_bits(const uint64_t* __restrict__ dbv, uint64_t D, ProbeLine* __restrict__ lines) {
+__global__ void k_line_bits(const DbRec* __restrict__ db, uint64_t D, ProbeLine* __restrict__ lines) {
+    const DbVal dbv{db};
     MTB_GRID_STRIDE(i, D) {
         const uint64_t r = dbv[i] >> 24;
         if (i > 0 && (dbv[i - 1] >> 24) == r) continue;
@@ -737,10 +779,10 @@ __global__ void k_line_bits(const uint64_t* __restrict__ dbv, uint64_t D, ProbeL
     }
 }
 
-void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines, hipStream_t s) {
-    k_line_base<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(dbv, D, dir, lines);
+void build_probe_lines(const DbRec* db, uint64_t D, const AADir& dir, ProbeLine* lines, hipStream_t s) {
+    k_line_base<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(db, D, dir, lines);
     k_line_count<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines);
-    if (D) k_line_bits<<<stride_grid(D), 256, 0, s>>>(dbv, D, lines);
+    if (D) k_line_bits<<<stride_grid(D), 256, 0, s>>>(db, D, lines);
 }
 
 // Run index: the exact DB run of every present AA rank, for the unstaged K4 (a DB much larger than
@@ -759,8 +801,9 @@ __global__ void k_line_pop(const ProbeLine* __restrict__ lines, uint32_t* __rest
     pop[l] = c;
 }
 
-__global__ void k_run_offsets(const uint64_t* __restrict__ dbv, uint64_t D, const ProbeLine* __restrict__ lines,
+__global__ void k_run_offsets(const DbRec* __restrict__ db, uint64_t D, const ProbeLine* __restrict__ lines,
                               const uint64_t* __restrict__ lineP, uint16_t* __restrict__ runOff) {
+    const DbVal dbv{db};
     MTB_GRID_STRIDE(i, D) {
         const uint64_t r = dbv[i] >> 24;
         if (i > 0 && (dbv[i - 1] >> 24) == r) continue;
@@ -778,9 +821,9 @@ void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp
     exclusive_scan_u32(popTmp, kProbeLines, lineP, scanTmp, s);
 }
 
-void build_run_offsets(const uint64_t* dbv, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
+void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s) {
-    if (D) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(dbv, D, lines, lineP, runOff);
+    if (D) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(db, D, lines, lineP, runOff);
 }
 
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
@@ -795,7 +838,7 @@ constexpr int kFreePer = 1;               // queries per thread in the unstaged 
 constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
-__device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ dbv, const AADir& d, uint64_t v) {
+__device__ __forceinline__ uint64_t db_lower_bound(const DbVal& dbv, const AADir& d, uint64_t v) {
     const uint64_t b = aa_bucket(v, d);
     return lower_bound_u64(dbv, d.dir[b], d.dir[b + 1], v);
 }
@@ -804,7 +847,8 @@ __device__ __forceinline__ uint64_t db_lower_bound(const uint64_t* __restrict__ 
 // infos aligned with vals): the selection threshold min(2 * min hamming sum, 7) and the number
 // of candidates within it, in one pass — sums <= 7 are tallied in the bytes of a 64-bit word
 // (runs of more than 255 candidates take a second pass).
-__device__ __forceinline__ uint32_t run_select(const HamRows& hr, const uint64_t* vals, uint64_t vOff, uint64_t lo,
+template <typename V>
+__device__ __forceinline__ uint32_t run_select(const HamRows& hr, const V& vals, uint64_t vOff, uint64_t lo,
                                                uint64_t& hi, uint64_t D, uint32_t& thr) {
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
     if (lo >= hi) return 0;
@@ -850,8 +894,9 @@ __device__ __forceinline__ void emit_match(uint64_t key, const HamRows& hr, uint
 // Writes the run's selected candidates at out[w..wEnd); returns the next w (a selection that
 // would pass wEnd sets err 4 and stops). outRank (nullable) gets each match's rank inside its
 // read's segment, starting at `rank`.
-__device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, uint64_t info, const uint64_t* vals,
-                                             const uint32_t* infos, uint64_t lo, uint64_t hi, uint32_t thr,
+template <typename V, typename T>
+__device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, uint64_t info, const V& vals,
+                                             const T& infos, uint64_t lo, uint64_t hi, uint32_t thr,
                                              const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                              mtb_match* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
                                              uint64_t wEnd, uint32_t rank, int* __restrict__ err) {
@@ -888,8 +933,9 @@ __device__ __forceinline__ void lds_run_bounds(const uint64_t* a, uint32_t n, ui
 // Window of each query block = DB values whose AA rank lies in the block's sort-prefix range
 // (kQuerySortLo/Hi): [lower_bound(first prefix), lower_bound(last prefix + 1)). One thread per
 // block boundary; computed once per batch and shared by the count and emit passes.
-__global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, const uint64_t* __restrict__ dbv,
+__global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, const DbRec* __restrict__ db,
                                 uint64_t D, AADir d, int kmerFormat, uint64_t nBlocks, uint64_t* __restrict__ win) {
+    const DbVal dbv{db};
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 2 * nBlocks) return;
     const uint64_t b = i >> 1;
@@ -910,8 +956,7 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
 template <bool kStage, int kPer>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
-                                               uint64_t Q, const uint64_t* __restrict__ dbv,
-                                               const uint32_t* __restrict__ dbinfo, uint64_t D, AADir d,
+                                               uint64_t Q, const DbRec* __restrict__ db, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
                                                uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
                                                mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
@@ -929,6 +974,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     __shared__ uint64_t sLineP[kStage ? 1 : kMatchLines];   // and their run-index bases
     __shared__ unsigned long long sBase;
     static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
+    const DbVal dbv{db};
+    const DbTax dbtax{db};
     const uint64_t q0 = (uint64_t)blockIdx.x * (256 * kPer);
     const uint64_t q1 = min(q0 + (uint64_t)(256 * kPer), Q);
     // every independent load of the block is issued up front (query keys and infos, the window
@@ -954,7 +1001,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + j * 256;
             v[j] = i < winN ? dbv[winLo + i] : 0;
-            tv[j] = i < winN ? dbinfo[winLo + i] : 0;
+            tv[j] = i < winN ? dbtax[winLo + i] : 0;
         }
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
@@ -1028,11 +1075,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             hi[j] = lower_bound_u64(dbv, lo[j], b1, aa + (1ull << 24));
         }
     }
-    const uint64_t* vals = staged ? sDb : dbv;
-    const uint32_t* infos = staged ? sInfo : dbinfo;
-    const uint64_t vOff = staged ? winLo : 0;
-    // unstaged: a run at GTDB scale is 1-2 k-mers, so the first two values of each run and their
-    // taxIDs are read at once (the pad makes lo + 1 readable) instead of value, then taxID
+    const uint64_t vOff = staged ? winLo : 0;  // DB index of the searched values' first entry
+    // unstaged: a run at GTDB scale is 1-2 k-mers, so the run's first two records (value + taxID,
+    // 24 contiguous bytes; the pad makes lo + 1 readable) are read at once
     uint64_t rv[kPer][2];
     uint32_t rt[kPer][2], rs[kPer][2];
     bool small[kPer];
@@ -1042,10 +1087,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         if (lo[j] > hi[j]) hi[j] = lo[j];
         small[j] = !staged && live[j] && hi[j] - lo[j] <= 2;
         if (small[j]) {
-            rv[j][0] = dbv[lo[j]];
-            rv[j][1] = dbv[lo[j] + 1];
-            rt[j][0] = dbinfo[lo[j]];
-            rt[j][1] = dbinfo[lo[j] + 1];
+            const DbRec r0 = db[lo[j]], r1 = db[lo[j] + 1];
+            rv[j][0] = (uint64_t)r0.hi << 32 | r0.lo;
+            rv[j][1] = (uint64_t)r1.hi << 32 | r1.lo;
+            rt[j][0] = r0.tax;
+            rt[j][1] = r1.tax;
         }
     }
     uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
@@ -1060,7 +1106,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             thr[j] = min(min(rs[j][0], rs[j][1]) * 2u, 7u);
             c[j] = (uint32_t)(rs[j][0] <= thr[j]) + (uint32_t)(rs[j][1] <= thr[j]);
         } else {
-            c[j] = live[j] ? run_select(hr[j], vals, vOff, lo[j], hi[j], D, thr[j]) : 0;
+            c[j] = !live[j] ? 0
+                   : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
+                            : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
         info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
         // the returned count is the query's first rank inside its read's segment
@@ -1094,8 +1142,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                     if (rs[j][k] <= thr[j])
                         emit_match(key[j], hr[j], info[j], rv[j][k], rt[j][k], rs[j][k], rev, spOf, maxTax, out,
                                    nullptr, wj++, 0, err);
+            } else if (staged) {
+                run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
+                         nullptr, rk[j], rk[j] + c[j], 0, err);
             } else {
-                run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
+                run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
                          nullptr, rk[j], rk[j] + c[j], 0, err);
             }
         }
@@ -1120,8 +1171,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 if (rs[j][k] <= thr[j])
                     emit_match(key[j], hr[j], info[j], rv[j][k], rt[j][k], rs[j][k], rev, spOf, maxTax, buf, bufRank,
                                wj++, rk[j]++, err);
+        } else if (staged) {
+            run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
+                     w, w + c[j], rk[j], err);
         } else {
-            run_emit(key[j], hr[j], info[j], vals, infos, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
+            run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
                      w, w + c[j], rk[j], err);
         }
         w += c[j];
@@ -1227,7 +1281,8 @@ uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines,
 // First index >= lo with a[i] >= key (an answer exists below D + kDbPad: the pad is ~0).
 // First index >= lo with a[i] >= key, by galloping from lo in steps 1, 2, 4, ... (runs at GTDB
 // scale are 1-2 k-mers: the first probes stay in lo's line).
-__device__ __forceinline__ uint64_t gallop_lower1(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key) {
+template <typename A>
+__device__ __forceinline__ uint64_t gallop_lower1(const A& a, uint64_t lo, uint64_t key) {
     uint64_t step = 1, hi = lo;
     while (a[hi] < key) {
         lo = hi + 1;
@@ -1237,7 +1292,8 @@ __device__ __forceinline__ uint64_t gallop_lower1(const uint64_t* __restrict__ a
     return lower_bound_u64(a, lo, hi, key);
 }
 
-__device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a, uint64_t lo, uint64_t key) {
+template <typename A>
+__device__ __forceinline__ uint64_t gallop_lower(const A& a, uint64_t lo, uint64_t key) {
     uint64_t step = 8, hi = lo;
     while (a[hi] < key) {
         lo = hi + 1;
@@ -1250,12 +1306,14 @@ __device__ __forceinline__ uint64_t gallop_lower(const uint64_t* __restrict__ a,
 __global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ qfrom, uint64_t Q,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
-                                               const uint64_t* __restrict__ dbv, const uint32_t* __restrict__ dbinfo,
+                                               const DbRec* __restrict__ db,
                                                uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
                                                int kmerFormat, uint32_t* __restrict__ readCnt,
                                                unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
                                                uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
                                                unsigned long long* __restrict__ stats) {
+    const DbVal dbv{db};
+    const DbTax dbtax{db};
     __shared__ unsigned long long sBase;
     const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool live = q < Q;
@@ -1266,7 +1324,7 @@ __global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         v[k] = dbv[from + k];
-        tax[k] = dbinfo[from + k];
+        tax[k] = dbtax[from + k];
     }
     const uint64_t x = key >> 24;
     uint32_t below = 0, in = 0;
@@ -1334,7 +1392,7 @@ __global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey
     if (base + blockTot > region || !c) return;  // region too small: the caller grows it and reruns
     w += base + (uint64_t)reg * region;
     if (!inReg) {
-        run_emit(key, hr, info, dbv, dbinfo, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
+        run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
         return;
     }
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
@@ -1359,12 +1417,12 @@ __global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey
 }
 
 void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
-                  const uint64_t* unitInfo, uint32_t C, const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D,
+                  const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D,
                   const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
                   mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
                   hipStream_t s) {
     if (Q == 0 || D < 2) return;
-    k_probe<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, qslot, qfrom, Q, unitInfo, C, dbv, dbinfo, D, spOf, maxTax,
+    k_probe<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, qslot, qfrom, Q, unitInfo, C, db, D, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, stats);
 }
 
@@ -1374,15 +1432,15 @@ bool unstaged_join(bool lines, uint64_t D, uint64_t Q, uint32_t winCap) {
 
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
 
-void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
+void launch_match_windows(const uint64_t* qkey, uint64_t Q, const DbRec* db, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     const uint64_t nb = (Q + kMatchQ - 1) / kMatchQ;
-    k_match_windows<<<(unsigned)((2 * nb + 255) / 256), 256, 0, s>>>(qkey, Q, dbv, D, dir, kmerFormat, nb, win);
+    k_match_windows<<<(unsigned)((2 * nb + 255) / 256), 256, 0, s>>>(qkey, Q, db, D, dir, kmerFormat, nb, win);
 }
 
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
-                  const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
+                  const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
@@ -1394,13 +1452,13 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
     // HBM path anyway
     if (unstaged_join(lines != nullptr, D, Q, winCap)) {
         const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
-        k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf, maxTax,
+        k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
                                                         overflow);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
-        k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, dbv, dbinfo, D, dir, spOf,
+        k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
                                                             stats, direct, dirOff, overflow);

@@ -97,6 +97,18 @@ void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uin
                      uint64_t* idxTmp, void* scanTmp, hipStream_t s);
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s);
 
+// A resident DB k-mer: its value in rank form (low / high 32 bits) and its taxID (info & mask) in
+// one 12-B record, so the join reads a candidate's value and taxID from one cache line.
+struct DbRec {
+    uint32_t lo, hi, tax;
+};
+static_assert(sizeof(DbRec) == 12, "12-B DB records");
+// values + taxIDs -> records (out may not alias the inputs)
+void launch_pack_db(const uint64_t* v, const uint32_t* tax, uint64_t n, DbRec* out, hipStream_t s);
+// in place on records: format-2 values to rank form; taxIDs & mask
+void launch_rec_rank_form(DbRec* db, uint64_t n, hipStream_t s);
+void launch_rec_mask_info(DbRec* db, uint64_t n, uint32_t mask, hipStream_t s);
+
 // AA-prefix directory over the decoded DB: dir[b] = first DB index whose value is >= the
 // smallest value of bucket b (first L AAs ranked in base 21), dir[R] = D.
 struct AADir {
@@ -107,7 +119,7 @@ struct AADir {
     int fmt;
 };
 AADir make_aa_dir(uint64_t D, int kmerFormat);
-void build_aa_dir(const uint64_t* dbv, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s);
+void build_aa_dir(const DbRec* db, uint64_t D, const AADir& d, uint64_t* dir, hipStream_t s);
 
 // DB probe lines: the AA membership bitmap of the DB (bit r set iff some DB k-mer has AA rank r)
 // cut into 64-B lines of kLineRanks ranks, each headed by the DB index of the first k-mer whose
@@ -122,7 +134,7 @@ static_assert(sizeof(ProbeLine) == 64, "one probe line per 64-B segment");
 constexpr uint32_t kStatStripes = 256;
 constexpr uint64_t kDbPad = 8;  // ~0 values after the resident DB
 constexpr uint64_t kProbeLines = (kAARankEnd + kLineRanks - 1) / kLineRanks + 1;  // + an end line (base D)
-void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeLine* lines,
+void build_probe_lines(const DbRec* db, uint64_t D, const AADir& dir, ProbeLine* lines,
                        hipStream_t s);  // lines zeroed by the caller
 
 // Run index (mtb_kernels.hip, k_run_offsets): lineP (kProbeLines + 1 u64: present ranks before
@@ -131,7 +143,7 @@ void build_probe_lines(const uint64_t* dbv, uint64_t D, const AADir& dir, ProbeL
 // of more than kRunIdxMax k-mers are not indexed)
 constexpr uint64_t kRunIdxMax = 0xFFFF;
 void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s);
-void build_run_offsets(const uint64_t* dbv, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
+void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s);
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
@@ -142,7 +154,7 @@ uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines,
 // K4P probe join over the filtered queries: same outputs as launch_match (per-read counts and
 // ranks, staged matches); stats: kStatStripes counters of queries with >= 1 match.
 void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
-                  const uint64_t* unitInfo, uint32_t C, const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D,
+                  const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D,
                   const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
                   mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
                   hipStream_t s);
@@ -153,7 +165,7 @@ void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* q
 constexpr uint32_t kStageRegions = 256;
 // qslot: each query's K1 slot (its info is slot_info(slot, C, unitInfo))
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
-                  const uint64_t* dbv, const uint32_t* dbinfo, uint64_t D, const AADir& dir, const int32_t* spOf,
+                  const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
@@ -173,7 +185,7 @@ void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint6
                             const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
                             int* err, hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
-void launch_match_windows(const uint64_t* qkey, uint64_t Q, const uint64_t* dbv, uint64_t D, const AADir& dir,
+void launch_match_windows(const uint64_t* qkey, uint64_t Q, const DbRec* db, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
 
 uint64_t path_bytes();

@@ -6,8 +6,8 @@ extractTargetKmers, (value, species) dedup with the LCA, IndexCreator.cpp:316-37
 IndexCreator.h:475-629) — plus filler: uniformly random valid metamers (a random AA 8-mer, each
 codon a random synonymous one) with the strains of a ~130k-species skeleton taxonomy (GTDB r226 has
 129,671 species reps), up to `target_kmers` entries. The two sorted streams are merged by AA-rank
-chunk into one resident array (values in the resident rank form; taxIDs), which a
-context uses in place (mtb_open_resident). Nothing is written to disk: at 12G k-mers the diffIdx +
+chunk into one resident array of 12-B records (value in the resident rank form, DESIGN.md §3, and
+taxID), which a context uses in place (mtb_open_resident). Nothing is written to disk: at 12G k-mers the diffIdx +
 info would be ~110 GB.
 
 `encode_into_oracle` writes the same DB in the reference's diffIdx / info / split format
@@ -48,18 +48,50 @@ def codon_counts() -> np.ndarray:
 
 
 class ResidentDb:
-    """A DB resident in HBM: values (int64, resident rank form) and taxIDs (int32), each with 8
-    spare entries the context pads; `host` carries the taxonomy and taxID_list."""
+    """A DB resident in HBM as 12-B records {value low 32 bits, value high 32 bits, taxID} (an
+    int32 tensor of shape (n + 8, 3), values in the resident rank form; the 8 spare records are the
+    context's pad), the layout mtb_open_resident uses in place; `host` carries the taxonomy and
+    taxID_list."""
 
-    def __init__(self, values: torch.Tensor, info: torch.Tensor, n: int, host: HostDb, n_true: int):
-        self.values, self.info, self.n, self.host, self.n_true = values, info, n, host, n_true
+    def __init__(self, records: torch.Tensor, n: int, host: HostDb, n_true: int):
+        assert records.dtype == torch.int32 and records.dim() == 2 and records.shape[1] == 3
+        assert records.shape[0] >= n + 8 and records.is_contiguous()
+        self.records, self.n, self.host, self.n_true = records, n, host, n_true
+
+    @classmethod
+    def from_arrays(cls, values: torch.Tensor, info: torch.Tensor, host: HostDb, n_true: Optional[int] = None):
+        """Records of sorted resident-form values (int64) and their taxIDs (int32)."""
+        n = values.numel()
+        rec = torch.empty(n + 8, 3, dtype=torch.int32, device=values.device)
+        put_records(rec, 0, values, info)
+        return cls(rec, n, host, n if n_true is None else n_true)
+
+    def values(self, a: int = 0, b: Optional[int] = None) -> torch.Tensor:
+        """Values [a, b) as int64 (b defaults to n)."""
+        b = self.n if b is None else b
+        return self.records[a:b, 0:2].clone(memory_format=torch.contiguous_format).view(torch.int64).view(-1)
+
+    def value_at(self, idx: torch.Tensor) -> torch.Tensor:
+        return self.records[idx][:, 0:2].clone(memory_format=torch.contiguous_format).view(torch.int64).view(-1)
+
+    def info(self, a: int = 0, b: Optional[int] = None) -> torch.Tensor:
+        b = self.n if b is None else b
+        return self.records[a:b, 2]
 
     def c_resident(self) -> MtbDbResident:
-        return MtbDbResident(values=self.values.data_ptr(), info=self.info.data_ptr(), n_kmers=self.n, rank_form=1)
+        return MtbDbResident(records=self.records.data_ptr(), n_kmers=self.n, rank_form=1)
 
     @property
     def n_kmers(self) -> int:
         return self.n
+
+
+def put_records(rec: torch.Tensor, pos: int, values: torch.Tensor, info: torch.Tensor) -> None:
+    """rec[pos:pos+m] = records of values (int64) and info (int32); little-endian: the int64 viewed
+    as two int32 is (low, high)."""
+    m = values.numel()
+    rec[pos:pos + m, 0:2] = values.contiguous().view(torch.int32).view(m, 2)
+    rec[pos:pos + m, 2] = info
 
 
 def _filler_chunk(lo: int, hi: int, count: int, g: torch.Generator, cnt_t: torch.Tensor, strain_t: torch.Tensor):
@@ -108,8 +140,7 @@ def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: 
     n_fill = max(0, int(target_kmers) - n_true)
     per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
     cap = n_true + n_fill + 8
-    values = torch.empty(cap, dtype=torch.int64, device=dev)
-    info = torch.empty(cap, dtype=torch.int32, device=dev)
+    rec = torch.empty(cap, 3, dtype=torch.int32, device=dev)
     edges = torch.tensor([c * AA_RANKS // n_chunks for c in range(n_chunks + 1)], dtype=torch.int64, device=dev)
     cut = torch.searchsorted(tv, edges << 24).cpu().tolist()
     g = torch.Generator(device=dev)
@@ -126,8 +157,7 @@ def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: 
         # (true-signal species have the smaller taxIDs), as the builder's (value, species) sort does
         vs, order = torch.sort(v, stable=True)
         m = vs.numel()
-        values[pos:pos + m] = vs
-        info[pos:pos + m] = t[order]
+        put_records(rec, pos, vs, t[order])
         pos += m
         del v, t, vs, order
     del tv, ti
@@ -136,7 +166,7 @@ def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: 
     host = HostDb(taxo, taxid_list=ids.astype(np.int32))
     log(f"GTDB-scale DB: {pos / 1e9:.3f}G k-mers ({n_true / 1e9:.3f}G true signal), "
         f"{len(sp_all)} species in the taxonomy")
-    return ResidentDb(values, info, pos, host, n_true)
+    return ResidentDb(rec, pos, host, n_true)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -171,12 +201,11 @@ def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk
     read from HBM chunk by chunk; diffIdx words are made on the device (getDiffIdx: big-endian
     15-bit groups, the last with 0x8000)."""
     n = rdb.n
-    vals = rdb.values
-    dev = vals.device
+    dev = rdb.records.device
 
     def chunk_deltas(a, b):
-        nat = to_native_fmt2(vals[a:b])
-        prev = to_native_fmt2(vals[a - 1:a]) if a > 0 else torch.zeros(1, dtype=torch.int64, device=dev)
+        nat = to_native_fmt2(rdb.values(a, b))
+        prev = to_native_fmt2(rdb.values(a - 1, a)) if a > 0 else torch.zeros(1, dtype=torch.int64, device=dev)
         return nat - torch.cat([prev, nat[:-1]]), nat
 
     # pass 1: words per chunk
@@ -191,8 +220,11 @@ def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk
     if size:
         idx = torch.arange(1, split_num, dtype=torch.int64, device=dev) * size - 1
         idx = idx[(idx >= 0) & (idx < n)]
-        key = ((vals[idx] >> 24) + 1) << 24
-        g_all = torch.searchsorted(vals[:n], key).cpu().numpy()
+        key = ((rdb.value_at(idx) >> 24) + 1) << 24
+        g_t = torch.zeros_like(key)  # lower bound over [0, n) = sum over chunks of the chunk's count below
+        for a in range(0, n, chunk):
+            g_t += torch.searchsorted(rdb.values(a, min(n, a + chunk)), key)
+        g_all = g_t.cpu().numpy()
         last = -1
         for gv in g_all.tolist():
             if gv < n and gv != last:
@@ -216,7 +248,7 @@ def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk
             out[(off + nw - 1 - gi)[sel]] = wv[sel].int()
         out = torch.where(out >= 32768, out - 65536, out).to(torch.int16)
         diff[bases[ci]:bases[ci + 1]] = out.cpu().numpy().view(np.uint16)
-        info[a:b] = rdb.info[a:b].cpu().numpy().view(np.uint32)
+        info[a:b] = rdb.info(a, b).cpu().numpy().view(np.uint32)
         for w in want:
             if a <= w < b:
                 gpos[w] = bases[ci] + int(off[w - a].item())
@@ -226,7 +258,7 @@ def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk
     for k, gv in enumerate(gs, start=1):
         if k >= split_num:
             break
-        split[3 * k] = np.uint64(int(to_native_fmt2(vals[gv:gv + 1]).item()) & ((1 << 64) - 1))
+        split[3 * k] = np.uint64(int(to_native_fmt2(rdb.values(gv, gv + 1)).item()) & ((1 << 64) - 1))
         split[3 * k + 1] = gpos[gv + 1]
         split[3 * k + 2] = gv + 1
     return db

@@ -31,10 +31,7 @@ def test_device_builder_and_encoder_match_the_file_format():
     v, t = build_db_device(gen, taxo, par, device=0, device_seq=(seq, off_t))
     n = v.numel()
     assert n == hdb.n_kmers
-    vals = torch.empty(n + 8, dtype=torch.int64, device=dev)
-    info = torch.empty(n + 8, dtype=torch.int32, device=dev)
-    vals[:n], info[:n] = v, t
-    rdb = ResidentDb(vals, info, n, HostDb(taxo, taxid_list=hdb.taxid_list), n)
+    rdb = ResidentDb.from_arrays(v, t, HostDb(taxo, taxid_list=hdb.taxid_list))
     odb = encode_into_oracle(rdb, _Capture, split_num=4096, chunk=1 << 16)
     assert np.array_equal(_Capture.diff, hdb.diff_idx)
     assert np.array_equal(_Capture.info, hdb.info)
@@ -67,7 +64,7 @@ def test_gtdb_shaped_resident_db_parity():
     rdb = build_gtdb_scale(dev, n_true_species=10, genome_len=30000, total_species=300, target_kmers=3_000_000,
                            n_chunks=4, before_free=grab)
     assert rdb.n > 2_500_000 and rdb.n_true > 50_000
-    v = rdb.values[:rdb.n]
+    v = rdb.values()
     assert bool((v[1:] >= v[:-1]).all())
     reads = _host_reads(*got["reads"])
     par = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
