@@ -87,10 +87,115 @@ __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l
 // filterRedundantMatches reads (Taxonomer.cpp:141-172,205-241). Its matches change nothing
 // downstream and are dropped here (prune): the sorted segment is written front-packed with only
 // the live matches, their count in liveCnt[r].
+// Open-addressing insert into a wave's LDS table of tn (power of two) slots, key 0 = empty; returns
+// the key's slot.
+template <typename K>
+__device__ __forceinline__ uint32_t lds_insert(K* tab, uint32_t tn, K key) {
+    uint32_t i = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 40) & (tn - 1);
+    while (true) {
+        const K prev = atomicCAS(&tab[i], (K)0, key);
+        if (prev == 0 || prev == key) return i;
+        i = (i + 1) & (tn - 1);
+    }
+}
+
+// The pruned sort with the dead matches dropped BEFORE sorting: (species, frame) pairs are counted
+// in an LDS hash table, a species with any pair counted twice is live (the run-of-two rule
+// above), and only the live matches (43% at GTDB scale) are compacted through LDS and sorted, in
+// the fewest register slots that hold them. The output is the live subset of the full sort's
+// order (a total order), as segsort_regs writes it.
+template <int E2>
+__device__ __forceinline__ void sort_live(const mtb_match* __restrict__ in, mtb_match* __restrict__ out, uint64_t inBase,
+                                          uint64_t base, int nLive, int lane, const uint64_t* cH,
+                                          const uint64_t* cL, const uint32_t* cX) {
+    uint64_t h[E2], l[E2];
+    uint32_t x[E2];
+#pragma unroll
+    for (int sl = 0; sl < E2; sl++) {
+        const int e = 64 * sl + lane;
+        const bool v = e < nLive;
+        h[sl] = v ? cH[e] : ~0ull;
+        l[sl] = v ? cL[e] : ~0ull;
+        x[sl] = v ? cX[e] : 0u;
+    }
+    wave_bitonic_sort<E2>(h, l, x, lane);
+#pragma unroll
+    for (int sl = 0; sl < E2; sl++) {
+        const int e = 64 * sl + lane;
+        if (e < nLive) out[base + e] = in[inBase + x[sl]];
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void prune_then_sort(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
+                                                uint64_t inBase, uint64_t base, int n, int lane,
+                                                uint32_t* __restrict__ liveCnt, uint32_t r) {
+    constexpr uint32_t T = 128 * E;  // load <= 1/2
+    __shared__ unsigned long long pairKey[T];  // (species << 3 | frame) + 1
+    __shared__ uint32_t pairCnt[T];
+    __shared__ uint32_t spKey[T];  // species (> 0 for a valid DB)
+    __shared__ uint32_t spLive[T];
+    __shared__ uint64_t cH[64 * E], cL[64 * E];
+    __shared__ uint32_t cX[64 * E];
+    for (uint32_t i = lane; i < T; i += 64) {
+        pairKey[i] = 0;
+        pairCnt[i] = 0;
+        spKey[i] = 0;
+        spLive[i] = 0;
+    }
+    __syncthreads();
+    uint64_t h[E], l[E];
+    uint32_t ps[E], ss[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        h[sl] = l[sl] = 0;
+        ps[sl] = ss[sl] = 0;
+        if (e < n) {
+            match_key(in[inBase + e], h[sl], l[sl]);
+            ps[sl] = lds_insert<unsigned long long>(pairKey, T, (h[sl] >> 29) + 1);
+            atomicAdd(&pairCnt[ps[sl]], 1u);
+            ss[sl] = lds_insert<uint32_t>(spKey, T, (uint32_t)(h[sl] >> 32));
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sl = 0; sl < E; sl++)
+        if (64 * sl + lane < n && pairCnt[ps[sl]] >= 2) spLive[ss[sl]] = 1;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    int nLive = 0;
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        const bool live = e < n && spLive[ss[sl]];
+        const uint64_t m = __ballot(live);
+        if (live) {
+            const int p = nLive + (int)__popcll(m & lt);
+            cH[p] = h[sl];
+            cL[p] = l[sl];
+            cX[p] = (uint32_t)e;
+        }
+        nLive += (int)__popcll(m);
+    }
+    __syncthreads();
+    if (nLive <= 64) sort_live<1>(in, out, inBase, base, nLive, lane, cH, cL, cX);
+    else if (E >= 2 && nLive <= 128) sort_live<(E >= 2 ? 2 : 1)>(in, out, inBase, base, nLive, lane, cH, cL, cX);
+    else if (E >= 4 && nLive <= 256) sort_live<(E >= 4 ? 4 : 1)>(in, out, inBase, base, nLive, lane, cH, cL, cX);
+    else sort_live<E>(in, out, inBase, base, nLive, lane, cH, cL, cX);
+    if (lane == 0) liveCnt[r] = (uint32_t)nLive;
+}
+
 template <int E>
 __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
                                              uint64_t inBase, uint64_t base, int n, int lane,
                                              uint32_t* __restrict__ liveCnt, uint32_t r) {
+    if constexpr (E >= 2) {
+        if (liveCnt) {
+            prune_then_sort<E>(in, out, inBase, base, n, lane, liveCnt, r);
+            return;
+        }
+    }
     uint64_t h[E], l[E];
     uint32_t x[E];
 #pragma unroll
