@@ -68,8 +68,9 @@ struct mtb_ctx {
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
-    bool directRetry = false;
-    bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
+    bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
+    bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
+    uint32_t maxW = 0;           // the batch's most windows in one frame of one read
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
@@ -424,14 +425,14 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
     if (c->sparse && (!prune || maxSeg > kSegSortRegs || c->segsortGlobal)) {  // K5 reads sparse segments only
-        launch_compact_segments(c->mDirect.as<mtb_match>(), c->slotOff.as<uint64_t>(), c->chunkC,
+        launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), c->chunkC,
                                 c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), s);
         c->sparse = false;
     }
-    launch_segsort(c->sparse ? c->mDirect.as<mtb_match>() : c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n,
-                   Mc, c->matchesSorted.as<mtb_match>(), c->segScratch.as<uint64_t>(), maxSeg,
-                   c->forceGeneric || c->segsortGlobal, prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
-                   c->sparse ? c->slotOff.as<uint64_t>() : nullptr, c->chunkC);
+    launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
+                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
+                   prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
+                   c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC);
     c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();
@@ -575,8 +576,10 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // (a read has at most one query k-mer per slot, and in practice fewer matches than slots), no
     // staging buffer and no transpose; a read with more matches than slots sends the batch through
     // the staged join
-    bool direct = !probe && c->directJoin;
-    if (direct && c->mDirect.ensure(sizeof(mtb_match) * Rc) != hipSuccess) {
+    // (16-B segment matches hold 24-bit taxIDs: a taxonomy with larger IDs runs staged; and 29-bit
+    // positions: reads of < 2^29 bases)
+    bool direct = !probe && c->directJoin && (uint64_t)c->maxTax <= kSegMaxTax && c->maxW < (1u << 26);
+    if (direct && c->mDirect.ensure(sizeof(SegMatch) * Rc) != hipSuccess) {
         (void)hipGetLastError();  // no room for a slot-sized match buffer (e.g. a long-read batch): staged join
         direct = false;
     }
@@ -606,7 +609,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
-                         direct ? c->mDirect.as<mtb_match>() : nullptr, c->slotOff.as<uint64_t>(),
+                         direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
                          c->ovFlag.as<int>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
@@ -649,7 +652,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // register sorts, segments of <= kSegSortRegs matches); otherwise they are compacted here
     c->sparse = direct && !c->keepStages && !c->forceGeneric && !c->matchOnly;
     if (direct && !c->sparse)
-        launch_compact_segments(c->mDirect.as<mtb_match>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
+        launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
                                 c->matches.as<mtb_match>(), s);
     else if (!direct)
         launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
@@ -722,6 +725,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipStreamSynchronize(s));
     // chunk = the longest frame when it is short (no padding for uniform short reads), else 64
     const uint32_t C = std::min<uint32_t>(std::max<uint32_t>(maxW, 1), 64);
+    c->maxW = maxW;
     launch_read_units(c->meta.as<ReadMeta>(), n, C, c->reserve.as<uint32_t>(), s);
     exclusive_scan_u32(c->reserve.as<uint32_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t U = 0;

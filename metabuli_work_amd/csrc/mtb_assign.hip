@@ -87,6 +87,20 @@ __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l
 // filterRedundantMatches reads (Taxonomer.cpp:141-172,205-241). Its matches change nothing
 // downstream and are dropped here (prune): the sorted segment is written front-packed with only
 // the live matches, their count in liveCnt[r].
+// K5 inputs: a segment of full matches, or of the direct join's 16-B SegMatch records of read r
+// (expanded on load: qinfo from r, species from spOf).
+struct MatchIn {
+    const mtb_match* __restrict__ p;
+    uint64_t base;
+    __device__ __forceinline__ mtb_match full(uint32_t e) const { return p[base + e]; }
+};
+struct SegIn {
+    const SegMatch* __restrict__ p;
+    uint64_t base;
+    uint64_t seqBits;
+    __device__ __forceinline__ mtb_match full(uint32_t e) const { return seg_expand(p[base + e], seqBits); }
+};
+
 // Open-addressing insert into a wave's LDS table of tn (power of two) slots, key 0 = empty; returns
 // the key's slot.
 template <typename K>
@@ -105,7 +119,7 @@ __device__ __forceinline__ uint32_t lds_insert(K* tab, uint32_t tn, K key) {
 // the fewest register slots that hold them. The output is the live subset of the full sort's
 // order (a total order), as segsort_regs writes it.
 template <int E2>
-__device__ __forceinline__ void sort_live(const mtb_match* __restrict__ in, mtb_match* __restrict__ out, uint64_t inBase,
+__device__ __forceinline__ void sort_live(mtb_match* __restrict__ out, uint64_t seqBits,
                                           uint64_t base, int nLive, int lane, const uint64_t* cH,
                                           const uint64_t* cL, const uint32_t* cX) {
     uint64_t h[E2], l[E2];
@@ -122,21 +136,48 @@ __device__ __forceinline__ void sort_live(const mtb_match* __restrict__ in, mtb_
 #pragma unroll
     for (int sl = 0; sl < E2; sl++) {
         const int e = 64 * sl + lane;
-        if (e < nLive) out[base + e] = in[inBase + x[sl]];
+        if (e < nLive) {  // the record rebuilt from its key (+ rightEndHamming riding in x): no gather
+            mtb_match m;
+            m.qinfo = ((h[sl] >> 29) & 7ull) << 61 | seqBits | (uint32_t)(h[sl] & 0x1FFFFFFFu);
+            m.target_id = (uint32_t)l[sl];
+            m.species_id = (uint32_t)(h[sl] >> 32);
+            m.dna_encoding = (uint32_t)(l[sl] >> 32) & 0xFFFFFFu;
+            m.right_end_hamming = (uint16_t)(x[sl] >> 16);
+            m.hamming = (uint8_t)(l[sl] >> 56);
+            m.pad = 0;
+            out[base + e] = m;
+        }
     }
 }
 
 template <int E>
-__device__ __forceinline__ void prune_then_sort(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
-                                                uint64_t inBase, uint64_t base, int n, int lane,
+struct PruneLds {
+    unsigned long long pairKey[128 * E];  // (species << 3 | frame) + 1
+    uint32_t pairCnt[128 * E];
+    uint32_t spKey[128 * E];  // species (> 0 for a valid DB)
+    uint32_t spLive[128 * E];
+    uint64_t cH[64 * E], cL[64 * E];
+    uint32_t cX[64 * E];
+};
+template <int E>
+__device__ __forceinline__ PruneLds<E>& prune_lds() {
+    __shared__ PruneLds<E> lds;
+    return lds;
+}
+template <int E>
+__device__ __forceinline__ uint8_t* run_live_lds() {
+    __shared__ uint8_t runLive[64 * E];
+    return runLive;
+}
+
+template <int E, typename In>
+__device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
                                                 uint32_t* __restrict__ liveCnt, uint32_t r) {
     constexpr uint32_t T = 128 * E;  // load <= 1/2
-    __shared__ unsigned long long pairKey[T];  // (species << 3 | frame) + 1
-    __shared__ uint32_t pairCnt[T];
-    __shared__ uint32_t spKey[T];  // species (> 0 for a valid DB)
-    __shared__ uint32_t spLive[T];
-    __shared__ uint64_t cH[64 * E], cL[64 * E];
-    __shared__ uint32_t cX[64 * E];
+    PruneLds<E>& L = prune_lds<E>();  // one LDS instance per E whatever the input type
+    unsigned long long* pairKey = L.pairKey;
+    uint32_t *pairCnt = L.pairCnt, *spKey = L.spKey, *spLive = L.spLive, *cX = L.cX;
+    uint64_t *cH = L.cH, *cL = L.cL;
     for (uint32_t i = lane; i < T; i += 64) {
         pairKey[i] = 0;
         pairCnt[i] = 0;
@@ -145,14 +186,16 @@ __device__ __forceinline__ void prune_then_sort(const mtb_match* __restrict__ in
     }
     __syncthreads();
     uint64_t h[E], l[E];
-    uint32_t ps[E], ss[E];
+    uint32_t ps[E], ss[E], rx[E];
 #pragma unroll
     for (int sl = 0; sl < E; sl++) {
         const int e = 64 * sl + lane;
         h[sl] = l[sl] = 0;
-        ps[sl] = ss[sl] = 0;
+        ps[sl] = ss[sl] = rx[sl] = 0;
         if (e < n) {
-            match_key(in[inBase + e], h[sl], l[sl]);
+            const mtb_match m = in.full((uint32_t)e);
+            match_key(m, h[sl], l[sl]);
+            rx[sl] = (uint32_t)m.right_end_hamming << 16;
             ps[sl] = lds_insert<unsigned long long>(pairKey, T, (h[sl] >> 29) + 1);
             atomicAdd(&pairCnt[ps[sl]], 1u);
             ss[sl] = lds_insert<uint32_t>(spKey, T, (uint32_t)(h[sl] >> 32));
@@ -174,25 +217,26 @@ __device__ __forceinline__ void prune_then_sort(const mtb_match* __restrict__ in
             const int p = nLive + (int)__popcll(m & lt);
             cH[p] = h[sl];
             cL[p] = l[sl];
-            cX[p] = (uint32_t)e;
+            cX[p] = rx[sl] | (uint32_t)e;
         }
         nLive += (int)__popcll(m);
     }
     __syncthreads();
-    if (nLive <= 64) sort_live<1>(in, out, inBase, base, nLive, lane, cH, cL, cX);
-    else if (E >= 2 && nLive <= 128) sort_live<(E >= 2 ? 2 : 1)>(in, out, inBase, base, nLive, lane, cH, cL, cX);
-    else if (E >= 4 && nLive <= 256) sort_live<(E >= 4 ? 4 : 1)>(in, out, inBase, base, nLive, lane, cH, cL, cX);
-    else sort_live<E>(in, out, inBase, base, nLive, lane, cH, cL, cX);
+    // the segment's read (every match of a segment carries it); keys hold the rest of the record
+    const uint64_t seqBits = nLive ? in.full(0).qinfo & (0x1FFFFFFFull << 32) : 0;
+    if (nLive <= 64) sort_live<1>(out, seqBits, base, nLive, lane, cH, cL, cX);
+    else if (E >= 2 && nLive <= 128) sort_live<(E >= 2 ? 2 : 1)>(out, seqBits, base, nLive, lane, cH, cL, cX);
+    else if (E >= 4 && nLive <= 256) sort_live<(E >= 4 ? 4 : 1)>(out, seqBits, base, nLive, lane, cH, cL, cX);
+    else sort_live<E>(out, seqBits, base, nLive, lane, cH, cL, cX);
     if (lane == 0) liveCnt[r] = (uint32_t)nLive;
 }
 
-template <int E>
-__device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, mtb_match* __restrict__ out,
-                                             uint64_t inBase, uint64_t base, int n, int lane,
+template <int E, typename In>
+__device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
                                              uint32_t* __restrict__ liveCnt, uint32_t r) {
     if constexpr (E >= 2) {
         if (liveCnt) {
-            prune_then_sort<E>(in, out, inBase, base, n, lane, liveCnt, r);
+            prune_then_sort<E>(in, out, base, n, lane, liveCnt, r);
             return;
         }
     }
@@ -204,18 +248,18 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
         h[sl] = ~0ull;
         l[sl] = ~0ull;
         x[sl] = (uint32_t)e;
-        if (e < n) match_key(in[inBase + e], h[sl], l[sl]);
+        if (e < n) match_key(in.full((uint32_t)e), h[sl], l[sl]);
     }
     wave_bitonic_sort<E>(h, l, x, lane);
     if (!liveCnt) {
 #pragma unroll
         for (int sl = 0; sl < E; sl++) {
             const int e = 64 * sl + lane;
-            if (e < n) out[base + e] = in[inBase + x[sl]];
+            if (e < n) out[base + e] = in.full(x[sl]);
         }
         return;
     }
-    __shared__ uint8_t runLive[64 * E];
+    uint8_t* runLive = run_live_lds<E>();
     const uint64_t lt = (1ull << lane) - 1;
     bool pair[E];
     uint32_t rid[E];
@@ -247,7 +291,7 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
         const int e = 64 * sl + lane;
         const bool live = e < n && runLive[rid[sl]];
         const uint64_t m = __ballot(live);
-        if (live) out[base + kept + (uint32_t)__popcll(m & lt)] = in[inBase + x[sl]];
+        if (live) out[base + kept + (uint32_t)__popcll(m & lt)] = in.full(x[sl]);
         kept += (uint32_t)__popcll(m);
     }
     if (lane == 0) liveCnt[r] = kept;
@@ -255,7 +299,20 @@ __device__ __forceinline__ void segsort_regs(const mtb_match* __restrict__ in, m
 
 // inOff (nullable): the segments are read from in + inOff[r] * inC (the direct join's per-read slot
 // stretches) instead of in + mOff[r]; the output is at out + mOff[r] either way.
+template <typename In>
+__device__ __forceinline__ void segsort_small_run(const In& in, mtb_match* __restrict__ out, uint64_t base, int n,
+                                                  int lane, uint32_t* __restrict__ liveCnt, uint32_t r) {
+    if (n <= 1) {  // a lone match is a dead species run
+        if (lane == 0 && n == 1 && !liveCnt) out[base] = in.full(0);
+        if (lane == 0 && liveCnt) liveCnt[r] = 0;
+        return;
+    }
+    if (n <= 64) segsort_regs<1>(in, out, base, n, lane, liveCnt, r);
+    else segsort_regs<2>(in, out, base, n, lane, liveCnt, r);
+}
+
 __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                      const SegMatch* __restrict__ seg,
                                                       const uint64_t* __restrict__ inOff, uint32_t inC,
                                                       uint32_t nReads, mtb_match* __restrict__ out,
                                                       uint32_t* __restrict__ liveCnt) {
@@ -264,21 +321,15 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n > 128) return;
-    const uint64_t inBase = inOff ? inOff[r] * inC : base;
-    const int lane = threadIdx.x;
-    if (n <= 1) {  // a lone match is a dead species run
-        if (lane == 0 && n == 1 && !liveCnt) out[base] = in[inBase];
-        if (lane == 0 && liveCnt) liveCnt[r] = 0;
-        return;
-    }
-    if (n <= 64) segsort_regs<1>(in, out, inBase, base, n, lane, liveCnt, r);
-    else segsort_regs<2>(in, out, inBase, base, n, lane, liveCnt, r);
+    if (seg) segsort_small_run(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, threadIdx.x, liveCnt, r);
+    else segsort_small_run(MatchIn{in, base}, out, base, n, threadIdx.x, liveCnt, r);
 }
 
 // 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
 // lane, in kernels of their own so the small kernel keeps its register budget (occupancy).
 template <int E>
 __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
+                                                     const SegMatch* __restrict__ seg,
                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
                                                      uint32_t nReads, mtb_match* __restrict__ out,
                                                      uint32_t* __restrict__ liveCnt) {
@@ -287,7 +338,8 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n <= 32 * E || n > 64 * E) return;
-    segsort_regs<E>(in, out, inOff ? inOff[r] * inC : base, base, n, (int)threadIdx.x, liveCnt, r);
+    if (seg) segsort_regs<E>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, (int)threadIdx.x, liveCnt, r);
+    else segsort_regs<E>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -630,17 +682,19 @@ static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_
 
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                     uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s, const uint64_t* inOff, uint32_t inC) {
+                    hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
     if (nReads == 0) return;
-    if (inOff && (global || maxSeg > kSmallSeg)) return;  // sparse input: register sorts only (caller's contract)
+    if (seg && (global || maxSeg > kSmallSeg)) return;  // sparse input: register sorts only (caller's contract)
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk);
         return;
     }
-    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
-    if (maxSeg > 128) k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
-    if (maxSeg > 256) k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, inOff, inC, nReads, out, liveCnt);
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
+    if (maxSeg > 128)
+        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
+    if (maxSeg > 256)
+        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
     if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);

@@ -873,9 +873,15 @@ __device__ __forceinline__ uint32_t run_select(const HamRows& hr, const V& vals,
 
 // One selected candidate (DB value tv, taxID tax, hamming sum hs) as a Match at out[w]
 // (KmerMatcher.cpp:431-448); outRank (nullable) gets its rank inside its read's segment.
+__device__ __forceinline__ void put_match(mtb_match* __restrict__ out, uint64_t w, const mtb_match& m) { out[w] = m; }
+__device__ __forceinline__ void put_match(SegMatch* __restrict__ out, uint64_t w, const mtb_match& m) {
+    out[w] = seg_pack(m);
+}
+
+template <typename O>
 __device__ __forceinline__ void emit_match(uint64_t key, const HamRows& hr, uint64_t info, uint64_t tv, uint32_t tax,
                                            uint32_t hs, bool rev, const int32_t* __restrict__ spOf, uint32_t maxTax,
-                                           mtb_match* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
+                                           O* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
                                            uint32_t rank, int* __restrict__ err) {
     const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
     if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
@@ -888,17 +894,17 @@ __device__ __forceinline__ void emit_match(uint64_t key, const HamRows& hr, uint
     m.hamming = (uint8_t)hs;
     m.pad = 0;
     if (outRank) outRank[w] = rank;
-    out[w] = m;
+    put_match(out, w, m);
 }
 
 // Writes the run's selected candidates at out[w..wEnd); returns the next w (a selection that
 // would pass wEnd sets err 4 and stops). outRank (nullable) gets each match's rank inside its
 // read's segment, starting at `rank`.
-template <typename V, typename T>
+template <typename V, typename T, typename O>
 __device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, uint64_t info, const V& vals,
                                              const T& infos, uint64_t lo, uint64_t hi, uint32_t thr,
                                              const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                             mtb_match* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
+                                             O* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
                                              uint64_t wEnd, uint32_t rank, int* __restrict__ err) {
     const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
     for (uint64_t t = lo; t < hi; t++) {
@@ -964,7 +970,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const ProbeLine* __restrict__ lines,
                                                const uint64_t* __restrict__ lineP, const uint16_t* __restrict__ runOff,
                                                int sortLo, unsigned long long* __restrict__ stats,
-                                               mtb_match* __restrict__ direct, const uint64_t* __restrict__ dirOff,
+                                               SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
                                                int* __restrict__ overflow) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
@@ -1133,7 +1139,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 atomicExch(overflow, 1);
                 continue;
             }
-            mtb_match* out = direct + o;
+            SegMatch* out = direct + o;
             if (small[j]) {
                 const bool rev = ((info_frame(info[j]) < 3) != (kmerFormat == 2));
                 uint64_t wj = rk[j];
@@ -1444,7 +1450,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
-                  unsigned long long* stats, mtb_match* direct, const uint64_t* dirOff, int* overflow,
+                  unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   hipStream_t s) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
@@ -1466,18 +1472,19 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 }
 
 // Direct join output -> compact per-read segments: read r's n = readOff[r + 1] - readOff[r]
-// matches from its reserved stretch (dirOff[r] * C) to readOff[r]. One wave per read, coalesced.
-__global__ void __launch_bounds__(256) k_compact_segments(const mtb_match* __restrict__ in,
+// matches from its reserved stretch (dirOff[r] * C), expanded to mtb_match, to readOff[r]. One wave
+// per read, coalesced.
+__global__ void __launch_bounds__(256) k_compact_segments(const SegMatch* __restrict__ in,
                                                           const uint64_t* __restrict__ dirOff, uint32_t C,
                                                           const uint64_t* __restrict__ readOff, uint32_t nReads,
                                                           mtb_match* __restrict__ out) {
     const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= nReads) return;
     const uint64_t src = dirOff[r] * C, dst = readOff[r], n = readOff[r + 1] - dst;
-    for (uint64_t i = lane; i < n; i += 64) out[dst + i] = in[src + i];
+    for (uint64_t i = lane; i < n; i += 64) out[dst + i] = seg_expand(in[src + i], (uint64_t)(r + 1) << 32);
 }
 
-void launch_compact_segments(const mtb_match* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
+void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
                              uint32_t nReads, mtb_match* out, hipStream_t s) {
     if (nReads) k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out);
 }

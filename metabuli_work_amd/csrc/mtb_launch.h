@@ -159,6 +159,34 @@ void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* q
                   mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
                   hipStream_t s);
 
+// A match inside a read's segment of the direct join, 16 B: the read is implicit (the segment's),
+// positions are < 2^29 (the sort key's width, K5) and taxIDs < 2^24 (kSegMaxTax; a taxonomy with
+// larger IDs runs the staged join): pos | frame << 29, target | hamming << 24, species |
+// rightEndHamming low byte << 24, dna (24 bits) | rightEndHamming high byte << 24. K5 and the
+// compaction expand it to mtb_match (seg_expand).
+constexpr uint32_t kSegMaxTax = (1u << 24) - 1;
+struct SegMatch {
+    uint32_t posFrame, targetHam, speciesReh, dnaReh;
+};
+static_assert(sizeof(SegMatch) == 16, "16-B segment matches");
+__host__ __device__ inline SegMatch seg_pack(const mtb_match& m) {
+    return SegMatch{(uint32_t)m.qinfo | (uint32_t)(m.qinfo >> 61) << 29, m.target_id | (uint32_t)m.hamming << 24,
+                    m.species_id | (uint32_t)(m.right_end_hamming & 0xFFu) << 24,
+                    (m.dna_encoding & 0xFFFFFFu) | (uint32_t)(m.right_end_hamming >> 8) << 24};
+}
+// the match of the segment whose qinfo carries seqBits (info_seq << 32)
+__host__ __device__ inline mtb_match seg_expand(const SegMatch& s, uint64_t seqBits) {
+    mtb_match m;
+    m.qinfo = (uint64_t)(s.posFrame >> 29) << 61 | seqBits | (s.posFrame & 0x1FFFFFFFu);
+    m.target_id = s.targetHam & 0xFFFFFFu;
+    m.species_id = s.speciesReh & 0xFFFFFFu;
+    m.dna_encoding = s.dnaReh & 0xFFFFFFu;
+    m.right_end_hamming = (uint16_t)((s.speciesReh >> 24) | (s.dnaReh >> 24) << 8);
+    m.hamming = (uint8_t)(s.targetHam >> 24);
+    m.pad = 0;
+    return m;
+}
+
 // K4 join: per-read counts into readCnt; matches staged in buf = kStageRegions regions of
 // `region` slots, total[k] = matches claimed in region k (all written iff every total[k] <= region).
 // winCap: max DB values staged in LDS per block.
@@ -169,12 +197,12 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
-                  unsigned long long* stats, mtb_match* direct, const uint64_t* dirOff, int* overflow,
+                  unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   hipStream_t s);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
 // slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A read whose matches do
 // not fit sets *overflow (nothing of it written): the caller reruns the batch staged.
-void launch_compact_segments(const mtb_match* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
+void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
                              uint32_t nReads, mtb_match* out, hipStream_t s);
 // K4 runs without LDS DB windows (probe-line lower bounds, no window staging): a DB much larger
 // than the query stream; its queries are then sorted finer (kQuerySortLoFine: one more pass buys
@@ -196,11 +224,11 @@ uint64_t clade_bytes();
 // reads) from segments of <= 512 matches, write each segment front-packed and its live count
 // mergeSeg: segments over this many matches (default, 0: 8192, the LDS capacity) sort as LDS chunks of
 // that size merged pairwise (tests lower it to exercise the merge path)
-// inOff (nullable, only with maxSeg <= 512 and !global): read segment r from in + inOff[r] * inC
-// (the direct join's layout) rather than in + mOff[r]
+// seg (nullable, only with maxSeg <= 512 and !global): read segment r from seg + inOff[r] * inC (the
+// direct join's layout, 16-B SegMatch) rather than in + mOff[r]
 void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                     uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s, const uint64_t* inOff = nullptr, uint32_t inC = 0);
+                    hipStream_t s, const SegMatch* seg = nullptr, const uint64_t* inOff = nullptr, uint32_t inC = 0);
 // the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
                       mtb_match* out, int* err, hipStream_t s);
