@@ -63,13 +63,13 @@ def alg_bytes(n, Q, M, D):
         "probe_join": 20 * Q + 96 * Q + 28 * M,
         "extract": read_bytes + 8 * R,                      # reads in, one 8-B key per window out
         "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
-        # queries, the DB (values + taxIDs) read once through the block windows, or, when the DB is
-        # much larger than the query stream (D > 24 Q), each query's run: its two run-index entries
-        # (4 B) and the run's first two values + taxIDs (24 B); the matches written into the reads'
-        # segments (direct join)
-        "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 24 * M,
+        # queries, the DB (12-B value + taxID records) read once through the block windows, or, when
+        # the DB is much larger than the query stream (D > 24 Q), each query's run: its two
+        # run-index entries (4 B) and the run's first two records (24 B); the 16-B segment matches
+        # written into the reads' segments (direct join)
+        "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 16 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
-        "match_sort": 2 * 24 * M + 8 * (n + 1),             # each read's matches read and written once
+        "match_sort": 16 * M + 24 * M + 8 * (n + 1),        # each read's segment matches read, live ones written
         "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
     }
 
