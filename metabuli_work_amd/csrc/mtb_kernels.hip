@@ -834,7 +834,7 @@ void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, cons
 constexpr int kMatchQ = 256;
 constexpr int kMatchWin = 3072;
 constexpr uint32_t kStageFreeRatio = 24;  // D / Q above which K4 runs without LDS windows
-constexpr int kFreePer = 1;               // queries per thread in the unstaged K4 (2 measured slower)
+constexpr int kFreePer = 1;               // queries per thread in the unstaged K4 (2: no gain with the run index; +1.6 ms before)
 constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
