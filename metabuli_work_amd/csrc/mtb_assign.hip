@@ -430,6 +430,60 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
     return kept;
 }
 
+// Lossy pre-prune for the block sorts (segments over 512 matches): (species, frame) pairs counted
+// in a hash indexed by the pair (collisions merge pairs), species flagged live in a hash indexed by
+// the species when one of their pairs counts twice. A collision can only keep a dead match (the
+// exact pruning after the sort still drops it), never drop a live one. The tables (T u32 each)
+// live in the LDS the sort uses afterwards; each thread keeps its <= 8 elements' keys in registers,
+// and the live ones are then written compacted into H / L / I. Returns the live count.
+template <int kThreads, int kPer, typename Idx>
+__device__ long preprune_load(const mtb_match* __restrict__ in, uint64_t base, long n, uint32_t* cnt, uint32_t* flag,
+                              uint32_t logT, uint64_t* H, uint64_t* L, Idx* I, uint32_t* sWave) {
+    const uint32_t T = 1u << logT;
+    for (uint32_t i = threadIdx.x; i < T; i += kThreads) {
+        cnt[i] = 0;
+        flag[i] = 0;
+    }
+    const long b = (long)threadIdx.x * kPer;
+    uint64_t h[kPer], l[kPer];
+    uint32_t hp[kPer], hs[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        h[k] = l[k] = 0;
+        hp[k] = hs[k] = 0;
+        if (b + k < n) {
+            match_key(in[base + b + k], h[k], l[k]);
+            hp[k] = (uint32_t)(((h[k] >> 29) * 0x9E3779B97F4A7C15ull) >> (64 - logT));
+            hs[k] = (uint32_t)(((h[k] >> 32) * 0xC2B2AE3D27D4EB4Full) >> (64 - logT));
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n) atomicAdd(&cnt[hp[k]], 1u);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n && cnt[hp[k]] >= 2) flag[hs[k]] = 1;
+    __syncthreads();
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n && flag[hs[k]]) mask |= 1u << k;
+    uint32_t nLive;
+    uint32_t at = block_scan_u32<kThreads>((uint32_t)__popc(mask), &nLive, sWave);  // syncs: the tables are free
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if ((mask >> k) & 1u) {
+            H[at] = h[k];
+            L[at] = l[k];
+            I[at] = (Idx)(b + k);
+            at++;
+        }
+    __syncthreads();
+    return (long)nLive;
+}
+
 // Segments of 513..kBlockSeg matches sort in LDS with one 1024-thread block per read (long reads:
 // ~2.5k matches at N50 10 kb); larger ones run the same network over a global key scratch.
 constexpr int kLargeThreads = 1024;
@@ -448,18 +502,30 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    const long n = (long)(mOff[r + 1] - base);
+    long n = (long)(mOff[r + 1] - base);
     if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
+    long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
+    if (liveCnt) {
+        static_assert(kMidSeg / kMidThreads == 8 && 2 * kMidSeg == 4096, "pre-prune geometry");
+        m = preprune_load<kMidThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
+                                                    reinterpret_cast<uint32_t*>(sl), 12, sh, sl, si, sWave);
+        if (m == 0) {
+            if (threadIdx.x == 0) liveCnt[r] = 0;
+            return;
+        }
+    }
     long p2 = 2;
-    while (p2 < n) p2 <<= 1;
+    while (p2 < m) p2 <<= 1;
     for (long i = threadIdx.x; i < p2; i += kMidThreads) {
+        if (liveCnt && i < m) continue;  // loaded by the pre-prune
         uint64_t h = ~0ull, l = ~0ull;
-        if (i < n) match_key(in[base + i], h, l);
+        if (i < m) match_key(in[base + i], h, l);
         sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
     }
     __syncthreads();
     block_bitonic<kMidThreads, uint16_t>(sh, sl, si, p2);
     if (liveCnt) {
+        n = m;
         uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
         const uint32_t kept = prune_pack_block<kMidThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n), n,
                                                                       in, out, base, sWave);
@@ -479,7 +545,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    const long n = (long)(mOff[r + 1] - base);
+    long n = (long)(mOff[r + 1] - base);
     if (global && n == 0 && liveCnt && threadIdx.x == 0) liveCnt[r] = 0;  // k_segsort_small is not launched
     if (global ? n == 0 : n <= kMidSeg) return;  // global: every segment takes the scratch path (tests)
     __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
@@ -487,13 +553,27 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     while (p2 < n) p2 <<= 1;
     if (!global && n > mergeSeg) return;  // chunked LDS sorts + merge path (launch_segsort)
     if (!global) {
+        long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
+        if (liveCnt) {
+            static_assert(kBlockSeg / kLargeThreads == 8 && 2 * kBlockSeg == 16384, "pre-prune geometry");
+            m = preprune_load<kLargeThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
+                                                          reinterpret_cast<uint32_t*>(sl), 14, sh, sl, si, sWave);
+            if (m == 0) {
+                if (threadIdx.x == 0) liveCnt[r] = 0;
+                return;
+            }
+            p2 = 2;
+            while (p2 < m) p2 <<= 1;
+        }
         for (long i = threadIdx.x; i < p2; i += kLargeThreads) {
+            if (liveCnt && i < m) continue;  // loaded by the pre-prune
             uint64_t h = ~0ull, l = ~0ull;
-            if (i < n) match_key(in[base + i], h, l);
+            if (i < m) match_key(in[base + i], h, l);
             sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
         }
         __syncthreads();
         block_bitonic<kLargeThreads, uint16_t>(sh, sl, si, p2);
+        n = m;
         if (liveCnt) {  // the lo keys are no longer needed: their LDS holds the run ids and flags
             uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
             const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n),
