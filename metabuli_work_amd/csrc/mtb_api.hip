@@ -71,6 +71,7 @@ struct mtb_ctx {
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
     bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
     uint32_t maxW = 0;           // the batch's most windows in one frame of one read
+    int sortLoFine = kQuerySortLoFine;  // MTB_SORT_LO_FINE (experiments)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
@@ -220,6 +221,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
+    if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix
+        const int v = atoi(e);
+        if (v >= 24 && v <= kQuerySortLo && (kQuerySortHi - v) % 8 == 0) c->sortLoFine = v;
+    }
     if (const char* e = getenv("MTB_DIRECT")) {  // 0: staged join; 2: direct, then rerun staged (tests the fallback)
         c->directJoin = atoi(e) != 0;
         c->directRetry = atoi(e) == 2;
@@ -544,7 +549,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[4], s));
     const int sortLo = unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
-                           ? kQuerySortLoFine : kQuerySortLo;
+                           ? c->sortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
         if (c->lines) {

@@ -91,7 +91,7 @@ uint64_t host_from_rank_form(uint64_t v);
 constexpr uint64_t kAARankEnd = 37822859361ull;
 // query k-mers are ordered by these bits of their rank-form key (AA rank << 24 | DNA part)
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
-constexpr int kQuerySortLoFine = 28;  // four passes (16-rank prefixes): DRAM-page locality for the unstaged K4
+constexpr int kQuerySortLoFine = 36;  // unstaged K4 sort prefix: 3 passes (4 passes, 28, measured 1.5 ms slower with the run index)
 
 void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
                      uint64_t* idxTmp, void* scanTmp, hipStream_t s);
