@@ -103,6 +103,39 @@ def roofline_of(kern, names, n, Q, M, D, traffic):
             "avg_launch_ms": round(float(kern[dom]), 3)}
 
 
+RANDOM_GATHER = os.path.join(ROOT, "profiles", "r01", "random_gather.json")
+
+
+def random_roofline(kern, names, work, Q, M, D):
+    """The random-access kernels against the chip's measured random-line ceiling
+    (tools/rand_gather.hip -> profiles/r01/random_gather.json: independent 4-B loads at random
+    64-B lines; the filter probes 5.4 GB of probe lines, the unstaged join 144 GB of records).
+    Requests per launch: K1F one probe line per window; the unstaged K4 one run-index line and one
+    record line per query, one rank atomic per matched query, one scattered 16-B write per match."""
+    try:
+        with open(RANDOM_GATHER) as f:
+            runs = json.load(f)["runs"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+    def ceiling(gb):
+        return min(runs, key=lambda r: abs(r["buffer_gb"] - gb))["glines_per_s"]
+
+    out = {}
+    req = {"filter": (float(work.get("slots", 0)), 5.4)}
+    if D > 24 * Q:
+        req["match_join"] = (2.0 * Q + float(work.get("matched_queries", 0)) + M, 144.0)
+    for k, (r, gb) in req.items():
+        if k not in names or r <= 0:
+            continue
+        ms = float(kern[names.index(k)])
+        got = r / (ms * 1e-3) / 1e9
+        out[k] = {"requests_per_launch": int(r), "achieved_greq_per_s": round(got, 2),
+                  "ceiling_greq_per_s": ceiling(gb), "frac": round(got / ceiling(gb), 3),
+                  "source": os.path.relpath(RANDOM_GATHER, ROOT)}
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -450,6 +483,7 @@ def run_gtdb(args, world, rank, local, dev):
     names = kernel_names(work)
     roofline = roofline_of(kern, names, B, Qb, Mb, rdb.n,
                            load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}))
+    rand_roof = random_roofline(kern, names, work, Qb, Mb, rdb.n)
     value = world * N * args.steps / elapsed
     log(rank, f"[bench] config 3: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
               f"kernels {dict(zip(names, np.round(kern, 2)))}")
@@ -504,6 +538,7 @@ def run_gtdb(args, world, rank, local, dev):
                    "query_kmers_per_batch": int(Qb), "matches_per_batch": int(Mb),
                    "parallelism": f"reads sharded, DB replicated x{world}"},
         "roofline": roofline,
+        "random_roofline": rand_roof,
         "cpu_baseline": cpu,
         "kernel_ms": {k: round(float(v), 3) for k, v in zip(names, kern)},
         "stage_ms": {k: round(float(v), 3) for k, v in zip(["extract", "sort", "match", "assign", "total"], stage)},
