@@ -1,10 +1,10 @@
-import os
 """Parity of the HIP path (through the C-ABI) against the oracle, per stage and end to end.
 
 Bar: bit-exact for k-mers, matches, taxIDs and taxID:count lists; per-read float score within
 1e-6 (the tolerance north_star states) — in practice the scores are compared bitwise too, since
 the device follows the reference's float operations one by one.
 """
+import os
 import numpy as np
 import pytest
 
