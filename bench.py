@@ -50,14 +50,17 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def alg_bytes(n, Q, M, D):
+def alg_bytes(n, Q, M, D, live=None, probe=False):
     """Algorithmic bytes per launch of each timed kernel for a batch of n 150-bp pairs (R reserved
-    k-mer slots, Q kept query k-mers, M matches, D DB k-mers)."""
+    k-mer slots, Q kept query k-mers, M matches, live = matches K6 reads after K5's pruning, D DB
+    k-mers)."""
     read_bytes = 2 * n * 150 + 2 * 8 * (n + 1)
     R = int(2 * 252 * n)  # reserved slots: getQueryKmerNumber(150) = (147/3 - 8 + 1) * 6 = 252 per mate
+    live = M if live is None else live
     return {
-        "filter": 8 * R + 4 * R + 20 * Q,                  # keys in, one 4-B membership word per window,
-                                                            # the present (key, slot, DB lower bound) out
+        # keys in, one 4-B membership word per window, the present (key, slot) out (+ the 8-B DB
+        # lower bound for the probe join)
+        "filter": 8 * R + 4 * R + (20 if probe else 12) * Q,
         # probe join: per query its (key, slot, lower bound), 8 DB values + taxIDs from there,
         # its staged matches (+ rank) out
         "probe_join": 20 * Q + 96 * Q + 28 * M,
@@ -70,7 +73,7 @@ def alg_bytes(n, Q, M, D):
         "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 16 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 16 * M + 24 * M + 8 * (n + 1),        # each read's segment matches read, live ones written
-        "assign": 24 * M + 32 * n + 4 * n + 8 * n,          # sorted matches read, results + lengths written
+        "assign": 24 * live + 32 * n + 4 * n + 8 * n,       # live sorted matches read, results + lengths
     }
 
 
@@ -89,9 +92,9 @@ def load_traffic(match):
     return None, None
 
 
-def roofline_of(kern, names, n, Q, M, D, traffic):
+def roofline_of(kern, names, n, Q, M, D, traffic, live=None):
     """Roofline of the dominant kernel: algorithmic bytes per launch / its event-timed duration."""
-    alg = alg_bytes(n, Q, M, D)
+    alg = alg_bytes(n, Q, M, D, live=live, probe=names is KERNELS_PROBE)
     dom = int(np.argmax(kern))
     dname = names[dom]
     achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
@@ -261,14 +264,16 @@ def run_config2(args, world, rank, local, dev):
         elapsed = float(t.item())
     kern /= max(1, args.steps)
     stage /= max(1, args.steps)
-    Q, M = clf.last_counts()
+    Qref, M = clf.last_counts()  # Qref: the reference's "Query k-mer number" (all non-blank windows)
     work = clf.stats()
+    Q = work["query_kmers"]      # the query k-mers K4 consumes (AA 8-mer in the DB)
     KERNELS = kernel_names(work)
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     value = world * n * args.steps / elapsed
 
     D = hdb.n_kmers
-    roofline = roofline_of(kern, KERNELS, n, Q, M, D, load_traffic({"pairs": n, "species": args.species}))
+    roofline = roofline_of(kern, KERNELS, n, Q, M, D, load_traffic({"pairs": n, "species": args.species}),
+                           live=work["live_matches"])
 
     # ---- CPU baseline: the oracle (restated reference algorithm, OpenMP) on a bounded sample ----
     cpu = None
@@ -371,8 +376,9 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
         t = torch.tensor([tl], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tl = float(t.item())
-    lq, lm = clfl.last_counts()
+    _, lm = clfl.last_counts()
     lwork = clfl.stats()
+    lq = lwork["query_kmers"]
     long_cpu = None
     if rank == 0 and args.cpu_sample > 0 and odb is not None:
         from tests import oracle_ctypes as oc  # checker / baseline only
@@ -441,18 +447,20 @@ def run_gtdb(args, world, rank, local, dev):
     gathered = torch.empty((world * N, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev) if world > 1 else None
     kern = np.zeros(7)
     stage = np.zeros(5)
-    tot_q = tot_m = 0
+    tot_q = tot_m = tot_live = 0
 
     def step(timed):
-        nonlocal kern, stage, tot_q, tot_m
+        nonlocal kern, stage, tot_q, tot_m, tot_live
         for a, b in spans:
             ob = offs[b - a]
             clf.classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
             if timed:
                 kern += clf.kernel_ms()
                 stage += clf.stage_ms()
-                q, m = clf.last_counts()
-                tot_q += q
+                _, m = clf.last_counts()
+                st = clf.stats()
+                tot_q += st["query_kmers"]
+                tot_live += st["live_matches"]
                 tot_m += m
             if world > 1:
                 clf.copy_results(res_all[a:b].data_ptr(), on_device=True)
@@ -482,7 +490,8 @@ def run_gtdb(args, world, rank, local, dev):
     work = clf.stats()
     names = kernel_names(work)
     roofline = roofline_of(kern, names, B, Qb, Mb, rdb.n,
-                           load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}))
+                           load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}),
+                           live=tot_live / launches)
     rand_roof = random_roofline(kern, names, work, Qb, Mb, rdb.n)
     value = world * N * args.steps / elapsed
     log(rank, f"[bench] config 3: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "

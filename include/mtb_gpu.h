@@ -167,7 +167,9 @@ int mtb_classify_batch(mtb_ctx* ctx, const char* seq, const uint64_t* off, const
 int mtb_get_taxcnt(mtb_ctx* ctx, mtb_taxcnt* out, uint64_t capacity, uint64_t* n_out);
 /* Device pointers of the last batch's results (mtb_result[n_reads]) and pooled taxcnt. */
 int mtb_device_results(mtb_ctx* ctx, void** results, void** taxcnt, uint64_t* n_taxcnt);
-/* Counters the reference prints (Classifier.cpp:116, KmerMatcher.cpp:152). */
+/* Counters the reference prints (Classifier.cpp:116, KmerMatcher.cpp:152): query_kmers = the
+ * batch's non-blank query k-mers ("Query k-mer number": every window the scanners emitted, before
+ * any test against the DB), matches = the matches found. */
 int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches);
 /* Work counts of the last batch: [0] reserved k-mer slots, [1] query k-mers, [2] query k-mers
  * with >= 1 match, [3] matches, [4] most matches of one read, [5] (read, species, frame) groups,
@@ -189,7 +191,8 @@ int mtb_last_kernel_ms(const mtb_ctx* ctx, float* ms, int n);
 int mtb_copy_results(mtb_ctx* ctx, void* dst, int dst_on_device);
 
 /* ---- staged entry points (per-stage parity against the oracle) ----------------------------- */
-/* Query k-mers of the last batch (blank slots dropped) in the order K4 consumed them: grouped by
+/* Query k-mers of the last batch (blank slots dropped, and those whose AA 8-mer the DB does not
+ * hold: they cannot match; mtb_last_stats[1] of them) in the order K4 consumed them: grouped by
  * the top 24 bits of the base-21 rank of their 8 AA codes (the index join needs locality, not
  * compareQueryKmer's total order); requires MTB_KEEP_STAGES. */
 int mtb_get_query_kmers(mtb_ctx* ctx, mtb_kmer* out, uint64_t capacity, uint64_t* n_out);
@@ -197,7 +200,7 @@ int mtb_get_query_kmers(mtb_ctx* ctx, mtb_kmer* out, uint64_t capacity, uint64_t
  * MTB_KEEP_STAGES. */
 int mtb_get_matches(mtb_ctx* ctx, mtb_match* out, uint64_t capacity, uint64_t* n_out);
 /* K5+K6 only, on caller-provided matches (any order): query_len[i] = queryLength+queryLength2
- * of read i (seqID i+1). */
+ * of read i (seqID i+1). Keeps every match (mtb_get_matches returns them in compareMatches order). */
 int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches,
                        const uint32_t* query_len, uint32_t n_reads, mtb_result* results);
 
@@ -221,7 +224,8 @@ int mtb_copy_matches(mtb_ctx* ctx, mtb_match* matches, uint32_t* read_counts, ui
                      int dst_on_device);
 /* K5 + K6 on n_chunks concatenated chunks of matches, chunk c holding the matches of reads
  * 0..n_reads-1 grouped by read with counts chunk_counts[c * n_reads + i] (the all-to-all receive
- * layout). With MTB_INPUT_DEVICE, matches / chunk_counts / query_len are device pointers.
+ * layout). With MTB_INPUT_DEVICE, matches / chunk_counts / query_len are device pointers; with
+ * MTB_KEEP_STAGES, K5 keeps every match (mtb_get_matches), else it drops the dead ones.
  * results: host array or NULL (mtb_device_results / mtb_copy_results). */
 int mtb_assign_chunks(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches, const uint32_t* chunk_counts,
                       uint32_t n_chunks, const uint32_t* query_len, uint32_t n_reads, uint32_t flags,

@@ -193,7 +193,8 @@ class Classifier:
         check(lib().mtb_copy_results(self.handle, ctypes.c_void_p(dst_ptr), int(on_device)), "mtb_copy_results")
 
     def query_kmers(self) -> np.ndarray:
-        q, _ = self.last_counts()
+        """The query k-mers K4 consumed (those whose AA 8-mer the DB holds), after MTB_KEEP_STAGES."""
+        q = self.stats()["query_kmers"]
         out = np.zeros(q, KMER_DTYPE)
         nq = ctypes.c_uint64(0)
         check(lib().mtb_get_query_kmers(self.handle, ptr(out), q, ctypes.byref(nq)), "mtb_get_query_kmers")
@@ -229,9 +230,10 @@ class Classifier:
               "mtb_copy_matches")
 
     def assign_chunks(self, matches, n_matches: int, chunk_counts, n_chunks: int, query_len, n_reads: int,
-                      fetch: bool = True) -> Optional[BatchResult]:
+                      fetch: bool = True, keep_stages: bool = False) -> Optional[BatchResult]:
         """K5 + K6 on the all-to-all receive layout: n_chunks chunks, each grouped by read, with
-        counts chunk_counts[c * n_reads + i]. numpy arrays (host) or device tensors."""
+        counts chunk_counts[c * n_reads + i]. numpy arrays (host) or device tensors. keep_stages:
+        no dead-match pruning, so matches() returns every match afterwards."""
         on_dev = not isinstance(matches, np.ndarray)
         if on_dev:
             ps = [ctypes.c_void_p(t.data_ptr()) for t in (matches, chunk_counts, query_len)]
@@ -240,7 +242,8 @@ class Classifier:
             ps = [ptr(a) for a in self._keep]
         res = np.zeros(n_reads, RESULT_DTYPE) if fetch else None
         check(lib().mtb_assign_chunks(self.handle, ps[0], n_matches, ps[1], n_chunks, ps[2], n_reads,
-                                      _abi.MTB_INPUT_DEVICE if on_dev else 0,
+                                      (_abi.MTB_INPUT_DEVICE if on_dev else 0) |
+                                      (_abi.MTB_KEEP_STAGES if keep_stages else 0),
                                       ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_assign_chunks")
         if not fetch:
             return None

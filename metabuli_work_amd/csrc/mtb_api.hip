@@ -101,6 +101,7 @@ struct mtb_ctx {
     // last batch
     uint32_t nReads = 0;
     uint64_t Q = 0, M = 0, nTaxcnt = 0;
+    uint64_t Qall = 0;  // non-blank query k-mers (KmerMatcher.cpp:143-152), before the AA filter
     const uint64_t* qKeys = nullptr;   // the last batch's query k-mers (sorted on the sort-merge path)
     const uint32_t* qSlots = nullptr;
     bool keepStages = false;
@@ -391,7 +392,9 @@ static AssignArgs assign_args(const mtb_params& p) {
 }
 
 // K5 + K6 + taxcnt compaction on the matches already grouped by read in c->matches (mOff).
-static int assign_stage(mtb_ctx* c, uint32_t n) {
+// keep: no dead-match pruning in K5, so matchesSorted holds every match in compareMatches order
+// afterwards (mtb_get_matches); the caller decides, nothing is inherited from an earlier call.
+static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     hipStream_t s = c->stream;
     HIP_TRY(c->errFlag.ensure(sizeof(int)));  // mtb_assign_* may run before any batch
     const uint64_t M = c->M;
@@ -424,7 +427,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
         HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
     // dead matches (no frame run of two in their species) are dropped in K5 unless the batch keeps
     // its stages (mtb_get_matches returns every match) or runs the general paths
-    const bool prune = !c->keepStages && !c->forceGeneric;
+    const bool prune = !keep && !c->forceGeneric;
+    c->keepStages = !prune;  // mtb_get_matches: matchesSorted is complete only without pruning
     HIP_TRY(c->liveCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
@@ -434,10 +438,10 @@ static int assign_stage(mtb_ctx* c, uint32_t n) {
                                 c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), s);
         c->sparse = false;
     }
-    launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
-                   c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
-                   prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
-                   c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC);
+    HIP_TRY(launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
+                           c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
+                           prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
+                           c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC));
     c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();
@@ -537,7 +541,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
         Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
                           probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), c->rankLo,
-                          c->rankHi, s);
+                          c->rankHi, &c->Qall, s);
         qk = c->keysB.as<uint64_t>();
         qi = c->valsB.as<uint32_t>();
         qf = c->qFrom.as<uint64_t>();
@@ -564,6 +568,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
             qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
             qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();
+            c->Qall = Q;  // no membership filter: every non-blank window was sorted
         }
     }
     HIP_TRY(hipEventRecord(c->kev[5], s));
@@ -756,7 +761,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
         for (int k = 10; k < 14; k++) HIP_TRY(hipEventRecord(c->kev[k], s));
         c->nTaxcnt = 0;
     } else {  // K5 + K6
-        int rc = assign_stage(c, n);
+        int rc = assign_stage(c, n, c->keepStages);
         if (rc != MTB_OK) return rc;
     }
     HIP_TRY(hipEventRecord(c->ev[4], s));
@@ -813,7 +818,7 @@ int mtb_device_results(mtb_ctx* c, void** results, void** taxcnt, uint64_t* n_ta
 
 int mtb_last_counts(const mtb_ctx* c, uint64_t* q, uint64_t* m) {
     if (!c) return MTB_ERR_ARG;
-    if (q) *q = c->Q;
+    if (q) *q = c->Qall;
     if (m) *m = c->M;
     return MTB_OK;
 }
@@ -1012,27 +1017,27 @@ int mtb_assign_chunks(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32_
     if (total != nm) { set_error("chunk counts do not add up to n_matches"); return MTB_ERR_ARG; }
     c->M = nm;
     c->Q = 0;
+    c->Qall = 0;
     c->qKeys = nullptr;
     c->qSlots = nullptr;
     c->nReads = n;
     c->matchOnly = false;
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
-    int rc = assign_stage(c, n);
+    int rc = assign_stage(c, n, (flags & MTB_KEEP_STAGES) != 0);
     if (rc != MTB_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev[4], s));
     if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     for (int e = 0; e < 4; e++) HIP_TRY(hipEventElapsedTime(&c->stageMs[e], c->ev[e], c->ev[e + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
-    c->keepStages = true;
     return check_err_flag(c);
 }
 
 int mtb_get_matches(mtb_ctx* c, mtb_match* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return MTB_ERR_ARG;
     *n_out = c->M;
-    if (!c->keepStages) { set_error("batch was not run with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
+    if (!c->keepStages) { set_error("the last K5 pruned dead matches: run the batch with MTB_KEEP_STAGES"); return MTB_ERR_ARG; }
     if (cap < c->M) return MTB_RETRY;
     if (c->M) HIP_TRY(hipMemcpy(out, c->matchesSorted.p, sizeof(mtb_match) * c->M, hipMemcpyDeviceToHost));
     return MTB_OK;
@@ -1060,6 +1065,7 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     if (nm >= kMaxBatchMatches) { set_error("more than 2^32 - 1 matches in one call"); return MTB_ERR_ARG; }
     c->M = nm;
     c->Q = 0;
+    c->Qall = 0;
     c->qKeys = nullptr;
     c->qSlots = nullptr;
     c->nReads = n;
@@ -1072,11 +1078,10 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
     HIP_TRY(hipMemcpyAsync(c->qlen.p, qlen, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
-    int rc = assign_stage(c, n);
+    int rc = assign_stage(c, n, true);  // staged entry point: every match stays readable
     if (rc != MTB_OK) return rc;
     if (results) HIP_TRY(hipMemcpyAsync(results, c->results.p, sizeof(mtb_result) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    c->keepStages = true;
     return check_err_flag(c);
 }
 

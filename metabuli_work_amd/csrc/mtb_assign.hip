@@ -712,11 +712,17 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
     for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + S.x[base + i]];
 }
 
-static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                              uint64_t* scratch, uint32_t* liveCnt, long chunk, hipStream_t s) {
+#define MTB_HIP_RET(x)                       \
+    do {                                     \
+        const hipError_t e_ = (x);           \
+        if (e_ != hipSuccess) return e_;     \
+    } while (0)
+
+static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M,
+                                    mtb_match* out, uint64_t* scratch, uint32_t* liveCnt, long chunk, hipStream_t s) {
     std::vector<uint64_t> off(nReads + 1);
-    hipMemcpyAsync(off.data(), mOff, sizeof(uint64_t) * (nReads + 1), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
+    MTB_HIP_RET(hipMemcpyAsync(off.data(), mOff, sizeof(uint64_t) * (nReads + 1), hipMemcpyDeviceToHost, s));
+    MTB_HIP_RET(hipStreamSynchronize(s));
     std::vector<uint32_t> big;
     std::vector<uint2> chunks;
     long maxN = 0;
@@ -727,18 +733,22 @@ static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_
         maxN = std::max(maxN, n);
         for (long c = 0; c < n; c += chunk) chunks.push_back(make_uint2(r, (uint32_t)c));
     }
-    if (big.empty()) return;
+    if (big.empty()) return hipSuccess;
     uint2* dChunks = nullptr;
     uint4* dTiles = nullptr;
     uint32_t* dBig = nullptr;
-    hipMallocAsync((void**)&dChunks, sizeof(uint2) * chunks.size(), s);
-    hipMallocAsync((void**)&dBig, sizeof(uint32_t) * big.size(), s);
-    hipMemcpyAsync(dChunks, chunks.data(), sizeof(uint2) * chunks.size(), hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(dBig, big.data(), sizeof(uint32_t) * big.size(), hipMemcpyHostToDevice, s);
-    k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk);
+    // every allocation and copy is checked: a kernel must never launch over a null buffer
+    hipError_t e = hipMallocAsync((void**)&dChunks, sizeof(uint2) * chunks.size(), s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&dBig, sizeof(uint32_t) * big.size(), s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dChunks, chunks.data(), sizeof(uint2) * chunks.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dBig, big.data(), sizeof(uint32_t) * big.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk);
+        e = hipGetLastError();
+    }
     int b = 0;
     std::vector<uint4> tiles;
-    for (long w = chunk; w < maxN; w *= 2) {
+    for (long w = chunk; e == hipSuccess && w < maxN; w *= 2) {
         tiles.clear();
         for (uint32_t r : big) {
             const long n = (long)(off[r + 1] - off[r]);
@@ -748,27 +758,34 @@ static void launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_
             }
         }
         if (dTiles) hipFreeAsync(dTiles, s);
-        hipMallocAsync((void**)&dTiles, sizeof(uint4) * tiles.size(), s);
-        hipMemcpyAsync(dTiles, tiles.data(), sizeof(uint4) * tiles.size(), hipMemcpyHostToDevice, s);
+        dTiles = nullptr;
+        e = hipMallocAsync((void**)&dTiles, sizeof(uint4) * tiles.size(), s);
+        if (e == hipSuccess) e = hipMemcpyAsync(dTiles, tiles.data(), sizeof(uint4) * tiles.size(), hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) break;
         k_merge_tiles<<<(unsigned)tiles.size(), 256, 0, s>>>(mOff, dTiles, M, scratch, b, w);
-        hipStreamSynchronize(s);  // the host tile vector is reused
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host tile vector is reused
         b ^= 1;
     }
-    k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt);
+    if (e == hipSuccess) {
+        k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt);
+        e = hipGetLastError();
+    }
     if (dTiles) hipFreeAsync(dTiles, s);
-    hipFreeAsync(dChunks, s);
-    hipFreeAsync(dBig, s);
+    if (dChunks) hipFreeAsync(dChunks, s);
+    if (dBig) hipFreeAsync(dBig, s);
+    return e;
 }
 
-void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
-    if (nReads == 0) return;
-    if (seg && (global || maxSeg > kSmallSeg)) return;  // sparse input: register sorts only (caller's contract)
+hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                          uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
+                          hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
+    if (nReads == 0) return hipSuccess;
+    if (seg && (global || maxSeg > kSmallSeg)) return hipErrorInvalidValue;  // sparse input: register sorts only
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk);
-        return;
+        return hipGetLastError();
     }
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
     if (maxSeg > 128)
@@ -778,7 +795,9 @@ void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, 
     if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);
-    if (maxSeg > chunk) launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, s);
+    MTB_HIP_RET(hipGetLastError());
+    if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, s);
+    return hipSuccess;
 }
 
 // Live matches (front-packed in each sorted segment) into one dense array: a wave per read.

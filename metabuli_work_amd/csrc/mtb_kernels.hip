@@ -1245,12 +1245,24 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
             word[j] = (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
         }
     }
-    uint32_t mask = 0;
+    uint32_t mask = 0, emitted = 0;
 #pragma unroll
-    for (int j = 0; j < kFilterPer; j++) mask |= word[j] << j;
+    for (int j = 0; j < kFilterPer; j++) {
+        mask |= word[j] << j;
+        emitted += k[j] != kSentinel;
+    }
+    // one scan carries both counts: present windows (the output offset) in the low 32 bits, emitted
+    // (non-blank) windows in the high 32 bits — the reference's "Query k-mer number"
+    // (KmerMatcher.cpp:143-152) counts every non-blank query k-mer, before any AA test
     unsigned long long tot;
-    const unsigned long long off = block_exclusive_scan((unsigned long long)__popc(mask), &tot);
-    if (threadIdx.x == 0) sBase = tot ? atomicAdd(counter, tot) : 0;
+    const unsigned long long off =
+        block_exclusive_scan((unsigned long long)__popc(mask) | ((unsigned long long)emitted << 32), &tot) &
+        0xFFFFFFFFull;
+    if (threadIdx.x == 0) {
+        const unsigned long long present = tot & 0xFFFFFFFFull;
+        sBase = present ? atomicAdd(counter, present) : 0;
+        if (tot >> 32) atomicAdd(counter + 1, tot >> 32);
+    }
     __syncthreads();
     uint64_t pos = sBase + off;
 #pragma unroll
@@ -1264,17 +1276,19 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 }
 
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
-                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, hipStream_t s) {
-    hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
+                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
+                       uint64_t* emitted, hipStream_t s) {
+    hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     const uint64_t blocks = (R + 256 * kFilterPer - 1) / (256 * kFilterPer);
     if (blocks) {
         if (qfrom) k_filter<true><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter, rankLo, rankHi);
         else k_filter<false><<<(unsigned)blocks, 256, 0, s>>>(keys, R, lines, qkey, qslot, qfrom, counter, rankLo, rankHi);
     }
-    unsigned long long Q = 0;
-    hipMemcpyAsync(&Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
+    unsigned long long Q[2] = {0, 0};
+    hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
-    return Q;
+    *emitted = Q[1];
+    return Q[0];
 }
 
 // ------------------------------------------------------------------------------------------------

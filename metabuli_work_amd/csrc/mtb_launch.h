@@ -147,10 +147,12 @@ void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, cons
                        uint16_t* runOff, hipStream_t s);
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
-// qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count.
+// qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count and sets
+// *emitted to the non-blank windows (the reference's query k-mer count). counter: 2 device words.
 // keys whose AA rank lies outside [rankLo, rankHi) (a DB part's range) are dropped without a probe
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
-                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, hipStream_t s);
+                       uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
+                       uint64_t* emitted, hipStream_t s);
 // K4P probe join over the filtered queries: same outputs as launch_match (per-read counts and
 // ranks, staged matches); stats: kStatStripes counters of queries with >= 1 match.
 void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* qfrom, uint64_t Q,
@@ -226,9 +228,12 @@ uint64_t clade_bytes();
 // that size merged pairwise (tests lower it to exercise the merge path)
 // seg (nullable, only with maxSeg <= 512 and !global): read segment r from seg + inOff[r] * inC (the
 // direct join's layout, 16-B SegMatch) rather than in + mOff[r]
-void launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
-                    uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                    hipStream_t s, const SegMatch* seg = nullptr, const uint64_t* inOff = nullptr, uint32_t inC = 0);
+// Returns the first HIP error of its allocations, copies and launches (hipErrorInvalidValue for a
+// sparse input outside the register sorts' range).
+hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                          uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
+                          hipStream_t s, const SegMatch* seg = nullptr, const uint64_t* inOff = nullptr,
+                          uint32_t inC = 0);
 // the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
                       mtb_match* out, int* err, hipStream_t s);

@@ -78,10 +78,14 @@ class Reads:
 
 
 def make_taxonomy(n_species: int, strains_per_species: int, seed: int = 1, n_genera: Optional[int] = None,
-                  with_eukaryota: bool = True) -> Taxonomy:
+                  with_eukaryota: bool = True, accessions: int = 0) -> Taxonomy:
     """Root 1 -> {Bacteria, Eukaryota} -> phylum -> class -> order -> family -> genus -> species
     -> strain ("no rank"). Species are spread over genera; the last 1/8 of the genera sit under
-    Eukaryota so that the minConsCntEuk branch (Taxonomer.cpp:497-500) is exercised."""
+    Eukaryota so that the minConsCntEuk branch (Taxonomer.cpp:497-500) is exercised.
+
+    accessions > 0: every strain (or strainless species) gets that many leaves of rank
+    "accession", as an accession-level DB build adds them (IndexCreator.cpp:640-660: one new taxon
+    per genome accession, child of the genome's taxID); genomes are then made per accession."""
     rng = np.random.default_rng(seed)
     n_genera = n_genera or max(1, n_species // 3)
     tax, par, rank, name = [1], [1], ["no rank"], ["root"]
@@ -107,8 +111,10 @@ def make_taxonomy(n_species: int, strains_per_species: int, seed: int = 1, n_gen
     for s in range(n_species):
         g = genera[int(rng.integers(0, n_genera))] if s >= n_genera else genera[s]
         sp = add(g, "species")
-        for _ in range(strains_per_species):
-            add(sp, "no rank")
+        leaves = [add(sp, "no rank") for _ in range(strains_per_species)] or [sp]
+        for lf in leaves:
+            for _ in range(accessions):
+                add(lf, "accession", f"GCF_{nxt[0]:09d}.1")
     return Taxonomy(np.array(tax, np.int32), np.array(par, np.int32), rank, name)
 
 
@@ -130,24 +136,47 @@ def _mutate(rng, s: np.ndarray, rate: float) -> np.ndarray:
 
 
 def make_genomes(taxo: Taxonomy, genome_len: int = 20000, strain_div: float = 0.02, seed: int = 1,
-                 len_jitter: float = 0.3, min_block: int = 300, max_block: int = 3000) -> Genomes:
-    """One genome per strain node (or per species when the species has no strain child)."""
+                 len_jitter: float = 0.3, min_block: int = 300, max_block: int = 3000,
+                 accession_div: float = 0.004, species_div: float = 0.0) -> Genomes:
+    """One genome per strain node (or per species when the species has no strain child); with
+    accession leaves, one genome per accession instead (accession_div from its strain's).
+    species_div > 0: the species of a genus are diverged copies of one genus genome (GTDB-like
+    sharing: related species hold the same AA 8-mers, so species ties and LCAs occur), instead of
+    independent random genomes."""
     rng = np.random.default_rng(seed)
     rank = np.array(taxo.rank)
     species_ids = taxo.taxid[rank == "species"]
-    children = {}
+    children, accs = {}, {}
     for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank):
         if r == "no rank" and t != 1:
             children.setdefault(p, []).append(t)
+        elif r == "accession":
+            accs.setdefault(p, []).append(t)
     seqs, taxids, species = [], [], []
+
+    def emit(g, t, sp):
+        if t in accs:
+            for a in accs[t]:
+                seqs.append(_mutate(rng, g, accession_div)); taxids.append(a); species.append(sp)
+        else:
+            seqs.append(g); taxids.append(t); species.append(sp)
+    parent_of = dict(zip(taxo.taxid.tolist(), taxo.parent.tolist()))
+    genus_base = {}
     for sp in species_ids.tolist():
-        L = max(600, int(genome_len * (1 + len_jitter * (rng.random() * 2 - 1))))
-        base = _random_dna(rng, L, gc=float(rng.uniform(0.35, 0.65)))
+        if species_div > 0:
+            gb = genus_base.get(parent_of[sp])
+            if gb is None:
+                L = max(600, int(genome_len * (1 + len_jitter * (rng.random() * 2 - 1))))
+                gb = genus_base[parent_of[sp]] = _random_dna(rng, L, gc=float(rng.uniform(0.35, 0.65)))
+            base = _mutate(rng, gb, species_div)
+        else:
+            L = max(600, int(genome_len * (1 + len_jitter * (rng.random() * 2 - 1))))
+            base = _random_dna(rng, L, gc=float(rng.uniform(0.35, 0.65)))
         kids = children.get(sp, [])
         if not kids:
-            seqs.append(base); taxids.append(sp); species.append(sp)
+            emit(base, sp, sp)
         for k in kids:
-            seqs.append(_mutate(rng, base, strain_div)); taxids.append(k); species.append(sp)
+            emit(_mutate(rng, base, strain_div), k, sp)
     off = np.zeros(len(seqs) + 1, np.uint64)
     off[1:] = np.cumsum([len(s) for s in seqs])
     bg, bs, be, bst = [], [], [], []
@@ -161,6 +190,21 @@ def make_genomes(taxo: Taxonomy, genome_len: int = 20000, strain_div: float = 0.
             pos = end + 1 + int(rng.integers(0, 60))
     return Genomes(np.concatenate(seqs), off, np.array(taxids, np.int32), np.array(species, np.int32),
                    np.array(bg, np.int32), np.array(bs, np.int32), np.array(be, np.int32), np.array(bst, np.int32))
+
+
+def concat_reads(parts: List["Reads"]) -> "Reads":
+    """One read set from several (e.g. drawn at different substitution rates)."""
+    def cat(seqs, offs):
+        out, base = [np.zeros(1, np.uint64)], 0
+        for o in offs:
+            out.append(o[1:] + np.uint64(base))
+            base += int(o[-1])
+        return np.concatenate(seqs).astype(np.uint8), np.concatenate(out)
+    s1, o1 = cat([p.seq1 for p in parts], [p.off1 for p in parts])
+    s2 = o2 = None
+    if parts[0].seq2 is not None:
+        s2, o2 = cat([p.seq2 for p in parts], [p.off2 for p in parts])
+    return Reads(s1, o1, s2, o2, np.concatenate([p.origin for p in parts]))
 
 
 def _revcomp(s: np.ndarray) -> np.ndarray:

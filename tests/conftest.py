@@ -26,11 +26,18 @@ def fixture_root(tmp_path_factory):
     return tmp_path_factory.mktemp("mtb_fixtures")
 
 
-# (name, kmer_format, syncmer, n_species, strains, genome_len)
+# (name, kmer_format, syncmer, n_species, strains, genome_len[, extras])
+# "*_acc": an accession-level DB (db.parameters "Accession_level 1"; genomes on rank-"accession"
+# leaves, IndexCreator.cpp:640-660), so classify runs with accessionLevel 1 or 2 (common.cpp:100-107);
+# its species are diverged copies of a genus genome (species_div), so species ties, LCAs and the
+# tie ratio matter
 DB_CONFIGS = {
     "fmt2": (2, 0, 14, 2, 24000),
     "fmt2_syncmer": (2, 1, 14, 2, 24000),
     "fmt1": (1, 0, 10, 2, 20000),
+    "fmt2_acc": (2, 0, 12, 2, 16000, {"accessions": 2, "species_div": 0.03}),
+    "fmt2_syncmer_acc": (2, 1, 12, 2, 16000, {"accessions": 2, "species_div": 0.03}),
+    "fmt1_acc": (1, 0, 12, 2, 14000, {"accessions": 2, "species_div": 0.03}),
 }
 
 
@@ -46,11 +53,13 @@ def make_db(fixture_root):
     def get(name):
         if name in cache:
             return cache[name]
-        fmt, syn, nsp, nst, glen = DB_CONFIGS[name]
-        taxo = synth.make_taxonomy(nsp, nst, seed=11)
-        gen = synth.make_genomes(taxo, genome_len=glen, seed=12)
+        fmt, syn, nsp, nst, glen, *ex = DB_CONFIGS[name]
+        ex = ex[0] if ex else {}
+        acc = ex.get("accessions", 0)
+        taxo = synth.make_taxonomy(nsp, nst, seed=11, accessions=acc)
+        gen = synth.make_genomes(taxo, genome_len=glen, seed=12, species_div=ex.get("species_div", 0.0))
         d = str(fixture_root / name)
-        par = default_params(kmer_format=fmt, syncmer=syn, smer_len=5)
+        par = default_params(kmer_format=fmt, syncmer=syn, smer_len=5, accession_level=1 if acc else 0)
         oc.build_db(d, par, taxo, gen)
         cache[name] = (d, taxo, gen)
         return cache[name]

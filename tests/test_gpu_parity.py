@@ -102,7 +102,10 @@ def test_stage_parity(make_db, db_name, kind):
         gk = clf.query_kmers()
         ok = okmers[info_seq(okmers["info"]) != 0]
         ok = ok[np.isin(_aa_rank(ok["value"], par.kmerFormat), _db_aa_ranks(db_dir, par.kmerFormat))]
-        assert len(gk) == len(ok) == br.query_kmers
+        assert len(gk) == len(ok) == clf.stats()["query_kmers"]
+        # mtb_last_counts: the reference's "Query k-mer number" (KmerMatcher.cpp:143-152), every
+        # non-blank query k-mer before any DB test
+        assert br.query_kmers == int((info_seq(okmers["info"]) != 0).sum())
         assert np.array_equal(_kmer_sorted(gk), _kmer_sorted(ok))
         # K2: ordered by the top 24 bits of the 36-bit base-21 AA rank (kQuerySortLo/Hi)
         pre = _aa_rank(gk["value"], par.kmerFormat) >> np.uint64(12)
@@ -139,14 +142,17 @@ def test_end_to_end_batches(make_db, db_name):
 
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
-@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "64", "6144", "6144:staged"])
+@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:fine28", "64", "6144", "6144:staged"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
     oracle's matches whatever the per-block window cap (0 forces the HBM path); and both outputs —
     matches written straight into each read's slot stretch (default), or staged + transposed
-    (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback)."""
+    (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback);
+    and the unstaged join over queries sorted on a 32-bit AA-rank prefix (MTB_SORT_LO_FINE=28, its
+    own block line ranges and LDS staging)."""
     window, _, mode = window.partition(":")
+    monkeypatch.setenv("MTB_SORT_LO_FINE", "28" if mode == "fine28" else "36")
     monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
     monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2"}.get(mode, "1"))
@@ -228,7 +234,8 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
     with Classifier(par, db_dir=db_dir) as clf:
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
         assert clf.stats()["join_path"] == (0 if join == "probe" else 1)
-        assert br.query_kmers == len(ok)
+        assert clf.stats()["query_kmers"] == len(ok)
+        assert br.query_kmers == int((info_seq(okmers["info"]) != 0).sum())
         gm = clf.matches()
         assert len(gm) == len(omatches) == br.matches
         assert np.array_equal(gm, omatches)

@@ -17,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from metabuli_work_amd._abi import MATCH_DTYPE, info_seq
-from metabuli_work_amd._lib import lib
+from metabuli_work_amd._lib import MtbError, lib
 from metabuli_work_amd.dist import MATCH_BYTES, exchange_matches, owner_bounds
 from tests import oracle_ctypes as oc
 
@@ -176,6 +176,11 @@ def test_partitioned_db_parity(make_db, db_name, parts):
         assert np.array_equal(qlen, ql1 + ql2)
         br = clfs[-1].assign_chunks(allm, len(allm), np.concatenate(counts), parts, qlen, n)
         compare_results(br.results, br.taxcnt, ores, otc)
+        with pytest.raises(MtbError, match="pruned"):  # K5 dropped dead matches: no full match array
+            clfs[-1].matches()
+        br = clfs[-1].assign_chunks(allm, len(allm), np.concatenate(counts), parts, qlen, n, keep_stages=True)
+        compare_results(br.results, br.taxcnt, ores, otc)
+        assert np.array_equal(clfs[-1].matches(), omatches)  # every match, compareMatches order
         # a match-only batch keeps no results of its own; an ordinary batch afterwards still works
         br2 = clfs[0].classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
         assert br2.matches == len(chunks[0])
