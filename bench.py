@@ -32,6 +32,7 @@ from metabuli_work_amd import synth  # noqa: E402
 from metabuli_work_amd._abi import RESULT_DTYPE, default_params  # noqa: E402
 from metabuli_work_amd.classifier import Classifier, LocalParameters  # noqa: E402
 from metabuli_work_amd.dbbuild import build_db  # noqa: E402
+from metabuli_work_amd.dist import gather_results  # noqa: E402
 from metabuli_work_amd.gpu_synth import make_genomes_gpu, make_long_reads_gpu, make_reads_gpu  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -43,6 +44,35 @@ KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpos
 
 def kernel_names(work):
     return KERNELS_PROBE if work.get("join_path", 1) == 0 else KERNELS_SORT
+
+
+class ResultGather:
+    """C1 of a multi-GPU step: each batch's result records and pooled taxID:count
+    lists are copied device-to-device into step buffers (the records' offsets rebased onto the step
+    pool), then gathered to every rank in one go (dist.gather_results: RCCL all-gathers)."""
+
+    def __init__(self, dev, n_reads):
+        self.dev = dev
+        self.pool = torch.empty((4 * n_reads + 1024, 8), dtype=torch.uint8, device=dev)
+        self.used = 0
+
+    def reset(self):
+        self.used = 0
+
+    def add(self, clf, rec):
+        clf.copy_results(rec.data_ptr(), on_device=True)
+        nt = clf.n_taxcnt()
+        if self.used + nt > self.pool.shape[0]:  # grow (rare: > 4 entries per read on average)
+            bigger = torch.empty((2 * (self.used + nt), 8), dtype=torch.uint8, device=self.dev)
+            bigger[:self.used] = self.pool[:self.used]
+            self.pool = bigger
+        clf.copy_taxcnt(self.pool[self.used:].data_ptr(), on_device=True)
+        if self.used:
+            rec.view(torch.int32).view(-1, 8)[:, 4] += self.used
+        self.used += nt
+
+    def gather(self, rec):
+        return gather_results(rec, self.pool[:self.used])
 
 
 def log(rank, *a):
@@ -231,16 +261,15 @@ def run_config2(args, world, rank, local, dev):
     log(rank, f"[bench] DB resident in HBM ({time.time() - t0:.1f}s)")
 
     n = args.pairs
-    gathered = None
-    res_dev = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    if world > 1:
-        gathered = torch.empty(world * res_dev.numel(), dtype=torch.uint8, device=dev)
+    res_dev = torch.empty((n, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    c1 = ResultGather(dev, n) if world > 1 else None
 
     def step():
         clf.classify_batch(s1, o1, s2, o2, device_input=True, fetch=False)
-        if world > 1:
-            clf.copy_results(res_dev.data_ptr(), on_device=True)
-            dist.all_gather_into_tensor(gathered, res_dev)
+        if world > 1:  # C1: result records + taxID:count lists to every rank (rank 0 writes the TSV)
+            c1.reset()
+            c1.add(clf, res_dev)
+            c1.gather(res_dev)
 
     for _ in range(args.warmup):
         step()
@@ -444,13 +473,15 @@ def run_gtdb(args, world, rank, local, dev):
         if b - a not in offs:
             offs[b - a] = o1[:b - a + 1].contiguous()
     res_all = torch.empty((N, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world * N, RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev) if world > 1 else None
+    c1 = ResultGather(dev, N) if world > 1 else None
     kern = np.zeros(7)
     stage = np.zeros(5)
     tot_q = tot_m = tot_live = 0
 
     def step(timed):
         nonlocal kern, stage, tot_q, tot_m, tot_live
+        if world > 1:
+            c1.reset()
         for a, b in spans:
             ob = offs[b - a]
             clf.classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
@@ -463,9 +494,9 @@ def run_gtdb(args, world, rank, local, dev):
                 tot_live += st["live_matches"]
                 tot_m += m
             if world > 1:
-                clf.copy_results(res_all[a:b].data_ptr(), on_device=True)
+                c1.add(clf, res_all[a:b])
         if world > 1:
-            dist.all_gather_into_tensor(gathered.view(-1), res_all.view(-1))
+            c1.gather(res_all)
 
     for _ in range(args.warmup):
         step(False)
@@ -568,7 +599,7 @@ def run_partitioned(args, lp, hdb, batch, world, rank, local, dev):
     on one GPU (world == 1) each part is timed in turn: a rank's step = its match-only pass over
     the batch + the assignment of its owned reads (their matches from all parts); the all-to-all
     is not timed there and its bytes are reported instead."""
-    from metabuli_work_amd.dist import classify_partitioned, gather_records, owner_bounds
+    from metabuli_work_amd.dist import classify_partitioned, owner_bounds
 
     P = args.db_parts
     s1, o1, s2, o2 = batch
@@ -583,11 +614,13 @@ def run_partitioned(args, lp, hdb, batch, world, rank, local, dev):
         clf = Classifier(lp, db_host=hdb.c_struct(), device=local, db_part=(rank, P))
         sizes = [b - a for a, b in owner_bounds(n, world)]
         res = torch.empty((sizes[rank], RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        c1 = ResultGather(dev, sizes[rank])
 
         def step():
-            _, br = classify_partitioned(clf, s1, o1, s2, o2, device_input=True, on_device=True)
-            clf.copy_results(res.data_ptr(), on_device=True)
-            gather_records(res, sizes)
+            classify_partitioned(clf, s1, o1, s2, o2, device_input=True, on_device=True)
+            c1.reset()
+            c1.add(clf, res)
+            c1.gather(res)  # C1: records + taxID:count lists
 
         for _ in range(args.warmup):
             step()

@@ -189,6 +189,10 @@ int mtb_last_stage_ms(const mtb_ctx* ctx, float* ms, int n);
 int mtb_last_kernel_ms(const mtb_ctx* ctx, float* ms, int n);
 /* Copy the last batch's mtb_result[n_reads] to dst (device memory if dst_on_device). */
 int mtb_copy_results(mtb_ctx* ctx, void* dst, int dst_on_device);
+/* Copy the last batch's pooled taxID:count entries (mtb_taxcnt[*n_out], the lists mtb_result
+ * offsets point into) to dst (device memory if dst_on_device); the multi-GPU gather (C1) moves them
+ * with the records. */
+int mtb_copy_taxcnt(mtb_ctx* ctx, void* dst, int dst_on_device, uint64_t* n_out);
 
 /* ---- staged entry points (per-stage parity against the oracle) ----------------------------- */
 /* Query k-mers of the last batch (blank slots dropped, and those whose AA 8-mer the DB does not

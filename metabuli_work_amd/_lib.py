@@ -20,7 +20,7 @@ EXPORTED = [
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
-    "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report",
+    "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt",
 ]
 
 
@@ -57,6 +57,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_last_stage_ms.argtypes = [vp, P(ctypes.c_float), i32]
     L.mtb_last_kernel_ms.argtypes = [vp, P(ctypes.c_float), i32]
     L.mtb_copy_results.argtypes = [vp, vp, i32]
+    L.mtb_copy_taxcnt.argtypes = [vp, vp, i32, P(u64)]
     L.mtb_get_query_kmers.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_get_matches.argtypes = [vp, vp, u64, P(u64)]
     L.mtb_assign_matches.argtypes = [vp, vp, u64, vp, u32, vp]

@@ -192,6 +192,19 @@ class Classifier:
     def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:
         check(lib().mtb_copy_results(self.handle, ctypes.c_void_p(dst_ptr), int(on_device)), "mtb_copy_results")
 
+    def n_taxcnt(self) -> int:
+        """Pooled taxID:count entries of the last batch."""
+        nt = ctypes.c_uint64(0)
+        lib().mtb_get_taxcnt(self.handle, ctypes.c_void_p(0), 0, ctypes.byref(nt))
+        return int(nt.value)
+
+    def copy_taxcnt(self, dst_ptr: int, on_device: bool = True) -> int:
+        """The last batch's pooled taxID:count entries to dst (8 B each); returns their number."""
+        nt = ctypes.c_uint64(0)
+        check(lib().mtb_copy_taxcnt(self.handle, ctypes.c_void_p(dst_ptr), int(on_device), ctypes.byref(nt)),
+              "mtb_copy_taxcnt")
+        return int(nt.value)
+
     def query_kmers(self) -> np.ndarray:
         """The query k-mers K4 consumed (those whose AA 8-mer the DB holds), after MTB_KEEP_STAGES."""
         q = self.stats()["query_kmers"]

@@ -940,6 +940,16 @@ int mtb_copy_results(mtb_ctx* c, void* dst, int dst_on_device) {
     return MTB_OK;
 }
 
+int mtb_copy_taxcnt(mtb_ctx* c, void* dst, int dst_on_device, uint64_t* n_out) {
+    if (!c || (!dst && c->nTaxcnt)) return MTB_ERR_ARG;
+    if (n_out) *n_out = c->nTaxcnt;
+    if (c->nTaxcnt)
+        HIP_TRY(hipMemcpyAsync(dst, c->tcOut.p, sizeof(mtb_taxcnt) * c->nTaxcnt,
+                               dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MTB_OK;
+}
+
 int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return MTB_ERR_ARG;
     *n_out = c->Q;

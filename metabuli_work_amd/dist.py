@@ -37,13 +37,75 @@ def gather_records(local: torch.Tensor, counts: List[int], group=None) -> torch.
     """All-gather variable-length rows (records of `local.shape[1]` bytes) in rank order."""
     world = dist.get_world_size(group)
     width = local.shape[1]
-    cap = max(counts)
+    cap = max(max(counts), 1)
     pad = torch.zeros((cap, width), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
     out = torch.empty((world * cap, width), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out.view(-1), pad.view(-1), group=group)
     parts = [out[r * cap:r * cap + counts[r]] for r in range(world)]
     return torch.cat(parts, 0)
+
+
+RESULT_BYTES = 32   # mtb_result
+TAXCNT_BYTES = 8    # mtb_taxcnt {tax_id, count}
+_TC_OFFSET_COL = 4  # mtb_result.taxcnt_offset, as the 5th int32 of the record
+
+
+def append_taxcnt(results: torch.Tensor, taxcnt: torch.Tensor, pool: torch.Tensor, used: int) -> int:
+    """Append one batch's pooled taxID:count entries (taxcnt (T, 8) uint8) to `pool` at `used` and
+    rebase the batch's result records (results (n, 32) uint8, in place) onto it. Returns the new fill."""
+    t = taxcnt.shape[0]
+    if t:
+        pool[used:used + t] = taxcnt
+        results.view(torch.int32).view(-1, RESULT_BYTES // 4)[:, _TC_OFFSET_COL] += used
+    return used + t
+
+
+def gather_results(results: torch.Tensor, taxcnt: torch.Tensor, group=None):
+    """C1: every rank's result records (n_r, 32) uint8 and pooled taxID:count lists
+    (T_r, 8) uint8 gathered in rank order, the records' taxcnt offsets rebased onto the gathered
+    pool — the same two arrays one GPU would have produced for all reads, so rank 0 can write the
+    reference's TSV (Reporter.cpp:38-83, taxID:count per read) and report. Returns
+    (results (Σn, 32), taxcnt (ΣT, 8)) on every rank."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = results.device
+    size = torch.tensor([results.shape[0], taxcnt.shape[0]], dtype=torch.int64, device=dev)
+    sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, size, group=group)
+    sizes = sizes.view(world, 2).cpu().tolist()
+    base = sum(sizes[r][1] for r in range(rank))
+    rec = results.clone()
+    if base and rec.shape[0]:
+        rec.view(torch.int32).view(-1, RESULT_BYTES // 4)[:, _TC_OFFSET_COL] += base
+    all_rec = gather_records(rec, [s[0] for s in sizes], group)
+    all_tc = gather_records(taxcnt, [s[1] for s in sizes], group)
+    return all_rec, all_tc
+
+
+def classify_sharded(clf, seq1, off1, seq2=None, off2=None, group=None):
+    """Replicated DB (configs 2-4): every rank passes the SAME host batch, classifies its shard of
+    it (contiguous, about equal bases, shard_bounds) against its own DB replica, and the results
+    are gathered (C1). Returns (results (n,) RESULT_DTYPE numpy, taxcnt TAXCNT_DTYPE numpy) for the
+    whole batch, in read order, on every rank."""
+    from ._abi import RESULT_DTYPE, TAXCNT_DTYPE
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_bounds(off1, world)[rank]
+    s1, o1 = shard_reads(seq1, off1, lo, hi)
+    s2 = o2 = None
+    if seq2 is not None:
+        s2, o2 = shard_reads(seq2, off2, lo, hi)
+    br = clf.classify_batch(s1, o1, s2, o2)
+    rec = torch.from_numpy(br.results.view(np.uint8).reshape(-1, RESULT_BYTES).copy())
+    tc = torch.from_numpy(br.taxcnt.view(np.uint8).reshape(-1, TAXCNT_BYTES).copy())
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rec, tc = rec.to(dev), tc.to(dev)
+    all_rec, all_tc = gather_results(rec, tc, group)
+    return (all_rec.cpu().numpy().reshape(-1).view(RESULT_DTYPE),
+            all_tc.cpu().numpy().reshape(-1).view(TAXCNT_DTYPE))
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1,4 +1,5 @@
 """N>1 path on CPU: world_size-2 gloo processes shard the reads and all-gather the result records."""
+import ctypes
 import os
 import socket
 
@@ -8,7 +9,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from metabuli_work_amd.dist import gather_records, shard_bounds, shard_reads
+from metabuli_work_amd._abi import RESULT_DTYPE, TAXCNT_DTYPE
+from metabuli_work_amd.dist import append_taxcnt, gather_records, gather_results, shard_bounds, shard_reads
 
 
 def _free_port():
@@ -70,3 +72,122 @@ def test_shard_bounds_balance():
     sizes = [e - s for s, e in b]
     assert max(sizes) - min(sizes) <= 1
     assert shard_bounds(np.zeros(1, np.uint64), 4) == [(0, 0)] * 4
+
+
+def _fake_batch(rng, n):
+    """Result records with per-read taxID:count lists pooled the way mtb_classify_batch pools them."""
+    res = np.zeros(n, RESULT_DTYPE)
+    lens = rng.integers(0, 4, n)
+    res["taxcnt_len"] = lens
+    res["taxcnt_offset"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    res["classification"] = rng.integers(1, 1000, n)
+    tc = np.zeros(int(lens.sum()), TAXCNT_DTYPE)
+    tc["tax_id"] = rng.integers(1, 1000, len(tc))
+    tc["count"] = rng.integers(1, 50, len(tc))
+    return res, tc
+
+
+def _lists(res, tc):
+    return [(int(r["classification"]), tc[r["taxcnt_offset"]:r["taxcnt_offset"] + r["taxcnt_len"]].tolist())
+            for r in res]
+
+
+def _results_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(100 + rank)
+    # two batches per rank, appended to one step pool as the bench's multi-GPU step does
+    pool = torch.zeros((64, 8), dtype=torch.uint8)
+    recs, used, want = [], 0, []
+    for n in (5 + rank, 0 if rank else 7):
+        res, tc = _fake_batch(rng, n)
+        want += _lists(res, tc)
+        r = torch.from_numpy(res.view(np.uint8).reshape(-1, 32).copy())
+        used = append_taxcnt(r, torch.from_numpy(tc.view(np.uint8).reshape(-1, 8).copy()), pool, used)
+        recs.append(r)
+    rec, tc = gather_results(torch.cat(recs), pool[:used])
+    if rank == 0:
+        q.put((rec.numpy().copy(), tc.numpy().copy()))
+    q.put(("want", rank, want))
+    dist.destroy_process_group()
+
+
+def test_gather_results_rebases_taxcnt_gloo():
+    """C1 with the taxID:count lists: rank 0 ends up with every rank's (classification, list) in
+    rank order, offsets pointing into one gathered pool."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_results_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    items = [q.get(timeout=120) for _ in range(world + 1)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {i[1]: i[2] for i in items if isinstance(i[0], str)}
+    rec, tc = next(i for i in items if not isinstance(i[0], str))
+    res = rec.reshape(-1).view(RESULT_DTYPE)
+    tcs = tc.reshape(-1).view(TAXCNT_DTYPE)
+    assert _lists(res, tcs) == want[0] + want[1]
+    assert int(res["taxcnt_len"].sum()) == len(tcs)
+
+
+class _FakeClf:
+    """Stands in for Classifier in bench.ResultGather: hands out one fake batch's records/taxcnt."""
+
+    def __init__(self, res, tc):
+        self.res, self.tc = res, tc
+
+    def copy_results(self, dst, on_device=True):
+        ctypes.memmove(dst, self.res.ctypes.data, self.res.nbytes)
+
+    def n_taxcnt(self):
+        return len(self.tc)
+
+    def copy_taxcnt(self, dst, on_device=True):
+        ctypes.memmove(dst, self.tc.ctypes.data, self.tc.nbytes)
+        return len(self.tc)
+
+
+def _bench_gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    rng = np.random.default_rng(7 + rank)
+    sizes = [6, 3 + rank, 5]
+    c1 = bench.ResultGather(torch.device("cpu"), 1)
+    c1.pool = c1.pool[:2]  # a tiny pool: the adds must grow it
+    rec = torch.empty((sum(sizes), 32), dtype=torch.uint8)
+    want, a = [], 0
+    c1.reset()
+    for n in sizes:
+        res, tc = _fake_batch(rng, n)
+        want += _lists(res, tc)
+        c1.add(_FakeClf(res, tc), rec[a:a + n])
+        a += n
+    r, t = c1.gather(rec)
+    q.put((rank, r.numpy().copy(), t.numpy().copy(), want))
+    dist.destroy_process_group()
+
+
+def test_bench_result_gather_gloo():
+    """bench.py's multi-GPU step (ResultGather: per-batch D2D copies + rebasing, one C1 gather)
+    gives every rank all reads' (classification, taxID:count list) in rank order."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    items = {i[0]: i[1:] for i in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = items[0][2] + items[1][2]
+    for r in range(world):
+        res = items[r][0].reshape(-1).view(RESULT_DTYPE)
+        assert _lists(res, items[r][1].reshape(-1).view(TAXCNT_DTYPE)) == want

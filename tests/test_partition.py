@@ -194,7 +194,7 @@ def _part_worker(rank, world, port, db_dir, seed, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from metabuli_work_amd import synth
     from metabuli_work_amd.classifier import Classifier, LocalParameters
-    from metabuli_work_amd.dist import classify_partitioned, gather_records
+    from metabuli_work_amd.dist import classify_partitioned, gather_results
 
     taxo = synth.make_taxonomy(14, 2, seed=11)
     gen = synth.make_genomes(taxo, genome_len=24000, seed=12)
@@ -203,38 +203,63 @@ def _part_worker(rank, world, port, db_dir, seed, q):
     with Classifier(par, db_dir=db_dir, device=0, db_part=(rank, world)) as clf:
         (lo, hi), br = classify_partitioned(clf, reads.seq1, reads.off1, reads.seq2, reads.off2, on_device=False)
         rec = torch.from_numpy(br.results.view(np.uint8).reshape(-1, 32).copy())
-        sizes = [b - a for a, b in owner_bounds(len(reads.off1) - 1, world)]
-        allres = gather_records(rec, sizes)
-    q.put((rank, allres.numpy().copy()))
+        tc = torch.from_numpy(br.taxcnt.view(np.uint8).reshape(-1, 8).copy())
+        allres, alltc = gather_results(rec, tc)  # C1 with the taxID:count lists, offsets rebased
+    q.put((rank, allres.numpy().copy(), alltc.numpy().copy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-def test_classify_partitioned_two_ranks(make_db):
-    """Two processes on cuda:0, each holding half of the DB, exchange matches over gloo."""
-    from metabuli_work_amd._abi import RESULT_DTYPE
+def _replica_worker(rank, world, port, db_dir, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from metabuli_work_amd import synth
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+    from metabuli_work_amd.dist import classify_sharded
 
-    db_dir, taxo, gen = make_db("fmt2")  # DB_CONFIGS["fmt2"]: 14 species x 2 strains, 24 kb, seeds 11/12
-    from metabuli_work_amd.classifier import LocalParameters
+    taxo = synth.make_taxonomy(14, 2, seed=11)
+    gen = synth.make_genomes(taxo, genome_len=24000, seed=12)
+    reads = _reads(gen, seed)
+    par = LocalParameters(seqMode=2).load_db_parameters(db_dir)
+    with Classifier(par, db_dir=db_dir, device=0) as clf:  # a full DB replica per rank
+        res, tc = classify_sharded(clf, reads.seq1, reads.off1, reads.seq2, reads.off2)
+    q.put((rank, res.view(np.uint8).copy(), tc.view(np.uint8).copy()))
+    dist.destroy_process_group()
 
-    reads = _reads(gen, 43)
-    par_c = LocalParameters(seqMode=2).load_db_parameters(db_dir).to_c()
-    odb = oc.OracleDb(db_dir)
-    ores, _ = oc.classify(odb, par_c, reads)
-    odb.close()
+
+def _run_two_ranks(target, db_dir, seed):
+    from metabuli_work_amd._abi import RESULT_DTYPE, TAXCNT_DTYPE
+
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_part_worker, args=(r, world, port, db_dir, 43, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, db_dir, seed, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=180) for _ in range(world))
+    got = {r: (a, b) for r, a, b in (q.get(timeout=180) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res = got[0].view(RESULT_DTYPE).reshape(-1)
+    return got[0][0].view(RESULT_DTYPE).reshape(-1), got[0][1].view(TAXCNT_DTYPE).reshape(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["partitioned", "replicated"])
+def test_classify_two_ranks(make_db, mode):
+    """Two processes on cuda:0 over gloo. partitioned: each holds half of the DB, matches go
+    all-to-all to the read owners (config 5); replicated: each holds the whole DB and classifies
+    half of the reads (configs 2-4). Either way rank 0's gathered results AND taxID:count lists
+    are the oracle's, element by element — what one GPU writes to the TSV."""
+    from tests.test_gpu_parity import compare_results
+    from metabuli_work_amd.classifier import LocalParameters
+
+    db_dir, taxo, gen = make_db("fmt2")  # DB_CONFIGS["fmt2"]: 14 species x 2 strains, 24 kb, seeds 11/12
+    reads = _reads(gen, 43)
+    par_c = LocalParameters(seqMode=2).load_db_parameters(db_dir).to_c()
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par_c, reads)
+    odb.close()
+    res, tc = _run_two_ranks(_part_worker if mode == "partitioned" else _replica_worker, db_dir, 43)
     assert len(res) == len(ores)
-    np.testing.assert_array_equal(res["classification"], ores["classification"])
-    assert np.array_equal(res["score"].view(np.uint32), ores["score"].view(np.uint32))
-    np.testing.assert_array_equal(res["taxcnt_len"] > 0, ores["taxcnt_len"] > 0)
+    assert int(res["taxcnt_len"].sum()) == len(tc)
+    compare_results(res, tc, ores, otc)
