@@ -294,10 +294,19 @@ int mtb_reader_next(mtb_reader* r, uint32_t max_reads, uint64_t max_bases, mtb_r
 void mtb_reader_close(mtb_reader* r);
 /* Rank name of a taxID in the context's taxonomy ("-" if absent). */
 const char* mtb_taxon_rank(const mtb_ctx* ctx, int32_t tax_id);
+/* TaxonomyWrapper::getOriginalTaxID (TaxonomyWrapper.h:70-79): the taxID the user's taxonomy
+ * names for an internal one (a taxonomyDB built with internal taxIDs); identity otherwise. Result
+ * records and taxcnt entries hold internal taxIDs; the writers print original ones. */
+int32_t mtb_original_taxid(const mtb_ctx* ctx, int32_t tax_id);
+/* TaxonomyWrapper::taxLineage2 (TaxonomyWrapper.cpp:431-454): "d_Bacteria;p_...;s_..." ("-" if
+ * the taxID is absent). The string lives as long as the context. */
+const char* mtb_taxon_lineage(const mtb_ctx* ctx, int32_t tax_id);
 /* Reporter::writeReadClassification (Reporter.cpp:38-83) for one batch: header line unless
- * append, one line per read; taxcnt as returned by mtb_get_taxcnt. */
+ * append, one line per read; taxcnt as returned by mtb_get_taxcnt. flags: MTB_WRITE_LINEAGE adds
+ * the lineage column (--lineage, par.printLineage). */
+#define MTB_WRITE_LINEAGE 1u
 int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
-                              const mtb_result* results, const mtb_taxcnt* taxcnt);
+                              const mtb_result* results, const mtb_taxcnt* taxcnt, uint32_t flags);
 /* Reporter::writeReportFile's per-taxon report (Reporter.cpp:175-190, writeReport :217-244; clade
  * counts by NcbiTaxonomy::getCladeCounts / getParentToChildren semantics): tax_ids[i] / counts[i] =
  * reads classified to each taxID over the run (++taxCounts[classification], Classifier.cpp:201-203;

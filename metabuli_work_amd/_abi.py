@@ -58,6 +58,7 @@ assert RESULT_DTYPE.itemsize == 32 and TAXCNT_DTYPE.itemsize == 8
 
 MTB_OK, MTB_RETRY = 0, 1
 MTB_INPUT_DEVICE, MTB_KEEP_STAGES, MTB_MATCH_ONLY = 1, 2, 4
+MTB_WRITE_LINEAGE = 1  # mtb_write_classifications flags
 
 
 def default_params(**kw) -> MtbParams:

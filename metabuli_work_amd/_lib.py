@@ -20,7 +20,8 @@ EXPORTED = [
     "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
-    "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt",
+    "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
+    "mtb_taxon_lineage",
 ]
 
 
@@ -70,7 +71,11 @@ def lib() -> ctypes.CDLL:
     L.mtb_reader_close.restype = None
     L.mtb_taxon_rank.argtypes = [vp, ctypes.c_int32]
     L.mtb_taxon_rank.restype = ctypes.c_char_p
-    L.mtb_write_classifications.argtypes = [vp, ctypes.c_char_p, i32, P(MtbReadBatch), vp, vp]
+    L.mtb_write_classifications.argtypes = [vp, ctypes.c_char_p, i32, P(MtbReadBatch), vp, vp, u32]
+    L.mtb_original_taxid.argtypes = [vp, ctypes.c_int32]
+    L.mtb_original_taxid.restype = ctypes.c_int32
+    L.mtb_taxon_lineage.argtypes = [vp, ctypes.c_int32]
+    L.mtb_taxon_lineage.restype = ctypes.c_char_p
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
     L.mtb_debug_tables.argtypes = [vp, vp, vp]
     L.mtb_debug_tables.restype = None

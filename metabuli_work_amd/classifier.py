@@ -45,6 +45,7 @@ class LocalParameters:
     em: int = 0
     threads: int = 1
     maskMode: int = 0
+    printLineage: int = 0   # --lineage: the TSV's lineage column (Reporter.cpp:41-43,59-61)
     filenames: List[str] = dataclasses.field(default_factory=list)
 
     def to_c(self) -> MtbParams:
@@ -263,6 +264,14 @@ class Classifier:
         return BatchResult(res, self.taxcnt(), 0, n_matches, self.stage_ms())
 
     # -- Classifier::startClassify over files ----------------------------------------------------
+    def original_taxid(self, tax_id: int) -> int:
+        """TaxonomyWrapper::getOriginalTaxID: results hold internal taxIDs (taxonomyDB)."""
+        return int(lib().mtb_original_taxid(self.handle, int(tax_id)))
+
+    def lineage(self, tax_id: int) -> str:
+        """TaxonomyWrapper::taxLineage2 of a taxID (the --lineage column)."""
+        return lib().mtb_taxon_lineage(self.handle, int(tax_id)).decode()
+
     def write_report(self, path: str, total_reads: int, tax_counts: dict) -> None:
         """Reporter::writeReportFile (Reporter.cpp:175-190): the per-taxon report of a run from
         tax_counts = {classification taxID: reads} (++taxCounts[classification], Classifier.cpp:201-203)."""
@@ -292,7 +301,8 @@ class Classifier:
                       "mtb_classify_batch")
                 tc = self.taxcnt()
                 check(lib().mtb_write_classifications(self.handle, out_tsv.encode(), 0 if first else 1,
-                                                      ctypes.byref(b), ptr(res), ptr(tc)),
+                                                      ctypes.byref(b), ptr(res), ptr(tc),
+                                                      _abi.MTB_WRITE_LINEAGE if par.printLineage else 0),
                       "mtb_write_classifications")
                 first = False
                 total += n
@@ -302,7 +312,8 @@ class Classifier:
                     tax_counts[t] = tax_counts.get(t, 0) + k
         if first:  # no reads: header only
             with open(out_tsv, "w") as out:
-                out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n")
+                out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank" +
+                          ("\tlineage" if par.printLineage else "") + "\ttaxID:match_count\n")
         if report_tsv is not None:
             self.write_report(report_tsv, total, tax_counts)
         return total

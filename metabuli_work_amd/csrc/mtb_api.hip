@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <mutex>
 #include <unordered_map>
 
 #include "mtb_host.h"
@@ -83,6 +84,8 @@ struct mtb_ctx {
     std::vector<int32_t> hNodeOf;  // host copies for mtb_taxon_rank / the TSV writer
     std::vector<std::string> hRank;
     HostTaxonomy hTax;             // the report (mtb_write_report): names, parents, nodes.dmp order
+    mutable std::vector<std::string> lineage;  // per node, built on first use (mtb_taxon_lineage)
+    mutable std::once_flag lineageOnce;
     // batch workspace
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
@@ -868,7 +871,7 @@ struct ReportWriter {
         }
         if (clade == 0) return;
         const int node = T.nodeOf[t];
-        line(clade, it->second.taxCount, T.rank[node], t, depth, T.name[node]);
+        line(clade, it->second.taxCount, T.rank[node], T.original(t), depth, T.name[node]);  // getOriginalTaxID
         std::vector<int32_t> ch = children[node];
         std::sort(ch.begin(), ch.end(), [&](int32_t a, int32_t b) { return cladeOf(a) > cladeOf(b); });
         for (int32_t x : ch) {
@@ -912,6 +915,42 @@ int mtb_write_report(const mtb_ctx* c, const char* path, uint64_t total_reads, c
 const char* mtb_taxon_rank(const mtb_ctx* c, int32_t t) {
     if (!c || t < 0 || (size_t)t >= c->hNodeOf.size() || c->hNodeOf[t] < 0) return "-";
     return c->hRank[c->hNodeOf[t]].c_str();
+}
+
+int32_t mtb_original_taxid(const mtb_ctx* c, int32_t t) { return c ? c->hTax.original(t) : t; }
+
+// TaxonomyWrapper::taxLineage2(node, infoAsName = true) (TaxonomyWrapper.cpp:431-454): the node and
+// its ancestors below the root, root-most first, each as findShortRank2(rank) + "_" + name (short
+// ranks of TaxonomyWrapper.h:8-24, "-" otherwise), joined by ';'. Built once per context.
+const char* mtb_taxon_lineage(const mtb_ctx* c, int32_t t) {
+    if (!c || !c->hTax.exists(t)) return "-";
+    const HostTaxonomy& T = c->hTax;
+    std::call_once(c->lineageOnce, [c, &T] {
+        static const std::unordered_map<std::string, std::string> shortRank = {
+            {"subspecies", "ss"}, {"species", "s"}, {"subgenus", "sg"}, {"genus", "g"}, {"subfamily", "sf"},
+            {"family", "f"}, {"suborder", "so"}, {"order", "o"}, {"subclass", "sc"}, {"class", "c"},
+            {"subphylum", "sp"}, {"phylum", "p"}, {"subkingdom", "sk"}, {"kingdom", "k"},
+            {"superkingdom", "d"}, {"domain", "d"}, {"realm", "r"}};
+        c->lineage.resize(T.nodeTax.size());
+        std::vector<int> chain;
+        for (size_t i = 0; i < T.nodeTax.size(); i++) {
+            chain.clear();
+            int node = (int)i;
+            do {
+                chain.push_back(node);
+                node = T.parent[node];
+            } while (T.parent[node] != node && chain.size() <= T.nodeTax.size());
+            std::string& out = c->lineage[i];
+            for (size_t k = chain.size(); k-- > 0;) {
+                auto it = shortRank.find(T.rank[chain[k]]);
+                out += it == shortRank.end() ? "-" : it->second;
+                out += '_';
+                out += T.name[chain[k]];
+                if (k > 0) out += ';';
+            }
+        }
+    });
+    return c->lineage[T.nodeOf[t]].c_str();
 }
 
 int mtb_last_stats(const mtb_ctx* c, uint64_t* out, int n) {

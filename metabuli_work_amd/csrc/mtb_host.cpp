@@ -198,6 +198,97 @@ bool load_dmp(const std::string& dir, HostTaxonomy& out) {
     return build_taxonomy(tax.data(), par.data(), tax.size(), ranks, names, mo.data(), mn.data(), mo.size(), out);
 }
 
+template <typename T>
+static bool read_file(const std::string& path, std::vector<T>& out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize((size_t)sz / sizeof(T));
+    size_t got = out.empty() ? 0 : fread(out.data(), sizeof(T), out.size(), f);
+    fclose(f);
+    return got == out.size();
+}
+
+// TaxonomyWrapper::unserialize (TaxonomyWrapper.cpp:363-421) over a taxonomyDB file: version,
+// [size_t 1 = internal taxIDs], size_t maxNodes, int maxTaxID, MMseqs2 TaxonNode[maxNodes]
+// {int id, taxId, parentTaxId; size_t rankIdx, nameIdx}, int D[maxTaxID + 1], [internal2orgTaxId],
+// E, L (2 maxNodes ints), H (maxNodes), the sparse table M, StringBlock<unsigned int>. The Euler
+// tour / sparse table are skipped: the device LCA is built from the parent links. The TaxonNode and
+// StringBlock layouts are MMseqs2's (submodule absent: unpinned). Returns 0 = loaded, 1 = other
+// serialization version (the reference falls back to the dmp files, common.cpp:71-85), -1 = error.
+int load_taxonomy_db(const std::string& path, HostTaxonomy& out) {
+    std::vector<char> mem;
+    if (!read_file(path, mem)) { set_error("cannot read " + path); return -1; }
+    const char* p = mem.data();
+    const char* end = p + mem.size();
+    auto take = [&](void* dst, size_t bytes) {
+        if ((size_t)(end - p) < bytes) return false;
+        if (dst) memcpy(dst, p, bytes);
+        p += bytes;
+        return true;
+    };
+    const std::string bad = path + ": truncated or malformed taxonomyDB";
+    int32_t version = 0;
+    if (!take(&version, 4)) { set_error(bad); return -1; }
+    if (version != kTaxonomyDbVersion) return 1;
+    uint64_t internalUsed = 0;
+    if ((size_t)(end - p) < 8) { set_error(bad); return -1; }
+    memcpy(&internalUsed, p, 8);  // read as size_t; only 1 means internal IDs (TaxonomyWrapper.cpp:372-381)
+    const bool internal = internalUsed == 1;
+    if (internal) p += 8;
+    uint64_t maxNodes = 0;
+    int32_t maxTax = 0;
+    if (!take(&maxNodes, 8) || !take(&maxTax, 4) || maxTax < 0 || maxNodes == 0 ||
+        maxNodes > (uint64_t)(end - p) / 32) { set_error(bad); return -1; }
+    struct RawNode { int32_t id, taxId, parentTaxId; uint64_t rankIdx, nameIdx; };
+    static_assert(sizeof(RawNode) == 32, "MMseqs2 TaxonNode layout");
+    std::vector<RawNode> raw(maxNodes);
+    std::vector<int32_t> D((size_t)maxTax + 1), i2o;
+    if (!take(raw.data(), maxNodes * 32) || !take(D.data(), D.size() * 4)) { set_error(bad); return -1; }
+    if (internal) {
+        i2o.resize((size_t)maxTax + 1);
+        if (!take(i2o.data(), i2o.size() * 4)) { set_error(bad); return -1; }
+    }
+    const uint64_t N = 2 * maxNodes;
+    uint64_t K = 0;  // (int)flog2(N) + 1 sparse-table columns
+    while ((2ull << K) <= N) K++;
+    K += 1;
+    if (!take(nullptr, (2 * N + maxNodes + N * K) * 4)) { set_error(bad); return -1; }  // E, L, H, M
+    uint32_t byteCap = 0, entryCap = 0, entryCount = 0;
+    if (!take(&byteCap, 4) || !take(&entryCap, 4) || !take(&entryCount, 4)) { set_error(bad); return -1; }
+    const char* bytes = p;
+    if (!take(nullptr, byteCap)) { set_error(bad); return -1; }
+    std::vector<uint32_t> offs(entryCap);
+    if (!take(offs.data(), (size_t)entryCap * 4)) { set_error(bad); return -1; }
+    auto str = [&](uint64_t idx) -> std::string {  // StringBlock::getString (NULL past entryCount)
+        if (idx >= entryCount || offs[idx] >= byteCap) return std::string();
+        return std::string(bytes + offs[idx], strnlen(bytes + offs[idx], byteCap - offs[idx]));
+    };
+    std::vector<int32_t> tax(maxNodes), par(maxNodes), mo, mn;
+    std::vector<std::string> ranks(maxNodes), names(maxNodes);
+    for (uint64_t i = 0; i < maxNodes; i++) {
+        tax[i] = raw[i].taxId;
+        par[i] = raw[i].parentTaxId;
+        ranks[i] = str(raw[i].rankIdx);
+        names[i] = raw[i].nameIdx == 0 ? std::string() : str(raw[i].nameIdx);  // setEukaryoteTaxID skips index 0
+        if (tax[i] < 0 || tax[i] > maxTax) { set_error(bad); return -1; }
+    }
+    for (int32_t t = 0; t <= maxTax; t++) {  // D entries of IDs that are not a node's own: merged IDs
+        const int32_t d = D[t];
+        if (d < 0) continue;
+        if ((uint64_t)d >= maxNodes) { set_error(bad); return -1; }
+        if (tax[d] != t) { mo.push_back(t); mn.push_back(tax[d]); }
+    }
+    if (!build_taxonomy(tax.data(), par.data(), maxNodes, ranks, names, mo.data(), mn.data(), mo.size(), out))
+        return -1;
+    // internal IDs unused by any node still map (getOriginalTaxID indexes the full table)
+    if (out.maxTax < maxTax) out.nodeOf.resize((size_t)maxTax + 1, -1), out.maxTax = maxTax;
+    out.internal2org = i2o;
+    return 0;
+}
+
 bool build_species_map(HostDb& db) {
     // KmerMatcher::loadTaxIdList, non-contamination branch (KmerMatcher.cpp:92-117).
     const HostTaxonomy& T = db.tax;
@@ -218,19 +309,6 @@ bool build_species_map(HostDb& db) {
     return true;
 }
 
-template <typename T>
-static bool read_file(const std::string& path, std::vector<T>& out) {
-    FILE* f = fopen(path.c_str(), "rb");
-    if (!f) return false;
-    fseek(f, 0, SEEK_END);
-    long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    out.resize((size_t)sz / sizeof(T));
-    size_t got = out.empty() ? 0 : fread(out.data(), sizeof(T), out.size(), f);
-    fclose(f);
-    return got == out.size();
-}
-
 bool load_db_files(const std::string& dir, HostDb& db) {
     if (!read_file(dir + "/diffIdx", db.diffIdx) || !read_file(dir + "/info", db.info)) {
         set_error("cannot read " + dir + "/diffIdx or /info");
@@ -242,8 +320,12 @@ bool load_db_files(const std::string& dir, HostDb& db) {
     std::string line;
     while (std::getline(tl, line))
         if (!line.empty()) db.taxIdList.push_back((int32_t)std::stoul(line));
-    // taxonomyDB (MMseqs2 serialization) is not supported: loadTaxonomy's dmp fallback only.
-    if (!load_dmp(dir + "/taxonomy", db.tax)) return false;
+    // loadTaxonomy (common.cpp:50-86): the taxonomyDB binary when present and of the current
+    // serialization version, else taxonomy/{nodes,names,merged}.dmp (original taxIDs)
+    int rc = 1;
+    if (std::ifstream(dir + "/taxonomyDB").good()) rc = load_taxonomy_db(dir + "/taxonomyDB", db.tax);
+    if (rc < 0) return false;
+    if (rc == 1 && !load_dmp(dir + "/taxonomy", db.tax)) return false;
     return build_species_map(db);
 }
 

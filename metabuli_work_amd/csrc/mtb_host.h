@@ -22,8 +22,13 @@ struct HostTaxonomy {
     std::vector<int32_t> spParent;  // node -> parentTaxId of its species node (minSpScore branch)
     std::vector<std::string> rank;
     std::vector<std::string> name;
+    std::vector<int32_t> internal2org;  // taxonomyDB with internal taxIDs; empty = IDs are original
 
     bool exists(int32_t t) const { return t >= 0 && t <= maxTax && nodeOf[t] >= 0; }
+    // TaxonomyWrapper::getOriginalTaxID (TaxonomyWrapper.h:70-79)
+    int32_t original(int32_t t) const {
+        return internal2org.empty() || t < 0 || (size_t)t >= internal2org.size() ? t : internal2org[t];
+    }
     int lcaNode(int i, int j) const;
     int32_t taxIdAtRank(int32_t taxId, const std::string& rank) const;  // TaxonomyWrapper.cpp:479-498
     static int rankIndex(const std::string& rank);
@@ -45,6 +50,8 @@ bool build_taxonomy(const int32_t* taxid, const int32_t* parent, uint64_t n, con
                     const std::vector<std::string>& names, const int32_t* mergedOld, const int32_t* mergedNew,
                     uint64_t nMerged, HostTaxonomy& out);
 bool load_dmp(const std::string& dir, HostTaxonomy& out);
+constexpr int32_t kTaxonomyDbVersion = 2;  // NcbiTaxonomy::SERIALIZATION_VERSION (MMseqs2, unpinned)
+int load_taxonomy_db(const std::string& path, HostTaxonomy& out);
 bool build_species_map(HostDb& db);
 bool load_db_files(const std::string& dir, HostDb& db);
 bool check_db(const HostDb& db);

@@ -215,7 +215,7 @@ void mtb_reader_close(mtb_reader* r) {
 }
 
 int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
-                              const mtb_result* res, const mtb_taxcnt* taxcnt) {
+                              const mtb_result* res, const mtb_taxcnt* taxcnt, uint32_t flags) {
     if (!ctx || !path || !batch || (!res && batch->n_reads)) return MTB_ERR_ARG;
     const uint32_t n = batch->n_reads;
     const char* names = batch->names;
@@ -226,7 +226,11 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
         mtb::set_error(std::string("cannot write ") + path);
         return MTB_ERR_IO;
     }
-    if (header) fputs("#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n", f);
+    const bool lineage = (flags & MTB_WRITE_LINEAGE) != 0;
+    if (header)
+        fputs(lineage ? "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage\ttaxID:match_count\n"
+                      : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n", f);
+    if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const uint32_t per = (n + nt - 1) / nt;
     std::vector<std::string> part(nt);
@@ -239,20 +243,26 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
             const mtb_result& r = res[i];
             o += r.is_classified ? "1\t" : "0\t";
             o.append(names + name_off[i], names + name_off[i + 1]);
-            snprintf(tmp, sizeof tmp, "\t%d\t%u\t%g\t", r.is_classified ? r.classification : 0, r.query_length,
-                     (double)r.score);
+            // taxIDs print through getOriginalTaxID (Reporter.cpp:55,65,72); the std::map order of
+            // the taxID:count list is the internal one, as the reference's
+            snprintf(tmp, sizeof tmp, "\t%d\t%u\t%g\t", mtb_original_taxid(ctx, r.is_classified ? r.classification : 0),
+                     r.query_length, (double)r.score);
             o += tmp;
             if (r.is_classified) {
                 o += mtb_taxon_rank(ctx, r.classification);
                 o += '\t';
+                if (lineage) {
+                    o += mtb_taxon_lineage(ctx, r.classification);
+                    o += '\t';
+                }
                 for (uint32_t k = 0; k < r.taxcnt_len; k++) {
                     const mtb_taxcnt& c = taxcnt[r.taxcnt_offset + k];
-                    snprintf(tmp, sizeof tmp, "%d:%u ", c.tax_id, c.count);
+                    snprintf(tmp, sizeof tmp, "%d:%u ", mtb_original_taxid(ctx, c.tax_id), c.count);
                     o += tmp;
                 }
                 o += '\n';
             } else {
-                o += "-\t-\t\n";
+                o += lineage ? "-\t-\t-\t\n" : "-\t-\t\n";
             }
         }
     };

@@ -295,3 +295,103 @@ def make_long_reads(gen: Genomes, n_reads: int, n50: int = 10000, min_len: int =
         out.append(f.astype(np.uint8))
     s, o = _pack(out)
     return Reads(s, o, None, None, origin)
+
+
+def to_internal_ids(taxo: Taxonomy):
+    """Internal taxIDs as TaxonomyWrapper's dmp loader assigns them with useInternalTaxID
+    (TaxonomyWrapper.cpp:147-185: 1, 2, ... in order of first appearance scanning nodes.dmp rows,
+    each row's taxID then its parent; internal 0 stays unused). Returns (the taxonomy in internal
+    IDs, internal2org as an int32 array with internal2org[0] = 0)."""
+    o2i, i2o = {}, [0]
+    for t, p in zip(taxo.taxid.tolist(), taxo.parent.tolist()):
+        for x in (t, p):
+            if x not in o2i:
+                o2i[x] = len(i2o)
+                i2o.append(x)
+    tax = np.array([o2i[t] for t in taxo.taxid.tolist()], np.int32)
+    par = np.array([o2i[p] for p in taxo.parent.tolist()], np.int32)
+    return Taxonomy(tax, par, list(taxo.rank), list(taxo.name)), np.array(i2o, np.int32)
+
+
+TAXONOMY_DB_VERSION = 2  # NcbiTaxonomy::SERIALIZATION_VERSION (MMseqs2; the submodule is absent: unpinned)
+
+
+def write_taxonomy_db(taxo: Taxonomy, path: str, internal2org: Optional[np.ndarray] = None) -> None:
+    """A taxonomyDB file as TaxonomyWrapper::serialize writes it (TaxonomyWrapper.cpp:289-361):
+    version int, [size_t 1 when internal taxIDs are used], size_t maxNodes, int maxTaxID,
+    TaxonNode[maxNodes] (MMseqs2 layout: int id, taxId, parentTaxId, 4 pad bytes, size_t rankIdx,
+    nameIdx), int D[maxTaxID + 1], [int internal2orgTaxId[maxTaxID + 1]], int E[2 maxNodes],
+    L[2 maxNodes], H[maxNodes], the sparse table M[2 maxNodes][flog2(2 maxNodes) + 1] (initTaxonomy,
+    :115-146), then StringBlock<unsigned int> {byteCapacity, entryCapacity, entryCount, bytes,
+    offsets}. `taxo` is in the IDs the DB uses (internal ones when internal2org is given)."""
+    n = len(taxo.taxid)
+    max_tax = int(max(taxo.taxid.max(), taxo.parent.max()))
+    if internal2org is not None:
+        max_tax = max(max_tax, len(internal2org) - 1)
+    D = np.full(max_tax + 1, -1, np.int32)
+    D[taxo.taxid] = np.arange(n, dtype=np.int32)
+    # string block: each node's rank appended in node order (loadNodes), then the names (loadNames)
+    strings, rank_idx, name_idx = [], [], []
+    for r in taxo.rank:
+        rank_idx.append(len(strings)); strings.append(r)
+    for nm in taxo.name:
+        name_idx.append(len(strings)); strings.append(nm)
+    enc = [s.encode() + b"\0" for s in strings]
+    offs = np.zeros(len(enc), np.uint32)
+    offs[1:] = np.cumsum([len(e) for e in enc])[:-1]
+    blob = b"".join(enc)
+    # Euler tour from taxID 1 (NcbiTaxonomy::elh), iterative
+    children = [[] for _ in range(n)]
+    for i in range(n):
+        if taxo.parent[i] != taxo.taxid[i]:
+            children[D[taxo.parent[i]]].append(int(taxo.taxid[i]))
+    E, L, H = [], [], np.zeros(n, np.int32)
+    stack = [(1, 0, 0)]  # (taxID, level, next child)
+    while stack:
+        t, lvl, k = stack.pop()
+        i = int(D[t])
+        if k == 0:
+            if H[i] == 0:
+                H[i] = len(E)
+            E.append(i); L.append(lvl)
+        if k < len(children[i]):
+            stack.append((t, lvl, k + 1))
+            stack.append((children[i][k], lvl + 1, 0))
+        else:
+            E.append(int(D[taxo.parent[i]])); L.append(lvl - 1)
+    N = 2 * n
+    E = np.array((E + [0] * N)[:N], np.int32)
+    L = np.array((L + [0] * N)[:N], np.int32)
+    K = int(np.floor(np.log2(N))) + 1
+    M = np.zeros((N, K), np.int32)
+    M[:, 0] = np.arange(N)
+    j = 1
+    while (1 << j) <= N:  # NcbiTaxonomy::computeSparseTable
+        h = 1 << (j - 1)
+        m = N - (1 << j) + 1
+        a, b = M[:m, j - 1], M[h:h + m, j - 1]
+        M[:m, j] = np.where(L[a] < L[b], a, b)
+        j += 1
+    node = np.zeros(n, np.dtype([("id", "<i4"), ("taxId", "<i4"), ("parentTaxId", "<i4"), ("pad", "<i4"),
+                                 ("rankIdx", "<u8"), ("nameIdx", "<u8")]))
+    node["id"] = np.arange(n)
+    node["taxId"] = taxo.taxid
+    node["parentTaxId"] = taxo.parent
+    node["rankIdx"] = rank_idx
+    node["nameIdx"] = name_idx
+    with open(path, "wb") as f:
+        f.write(np.int32(TAXONOMY_DB_VERSION).tobytes())
+        if internal2org is not None:
+            f.write(np.uint64(1).tobytes())
+        f.write(np.uint64(n).tobytes())
+        f.write(np.int32(max_tax).tobytes())
+        f.write(node.tobytes())
+        f.write(D.tobytes())
+        if internal2org is not None:
+            i2o = np.zeros(max_tax + 1, np.int32)
+            i2o[:len(internal2org)] = internal2org
+            f.write(i2o.tobytes())
+        f.write(E.tobytes()); f.write(L.tobytes()); f.write(H.tobytes()); f.write(M.tobytes())
+        f.write(np.array([len(blob), len(enc), len(enc)], np.uint32).tobytes())
+        f.write(blob)
+        f.write(offs.tobytes())

@@ -62,7 +62,18 @@ void* orc_db_open(const char* dir, char* err, int errlen) {
     std::ifstream tl(d + "/taxID_list");
     std::string line;
     while (std::getline(tl, line)) if (!line.empty()) db->taxIdList.push_back((TaxID)std::stoul(line));
-    if (!db->tax.loadDmp(d + "/taxonomy", &e) || !db->buildSpeciesMap(&e)) {
+    // loadTaxonomy (common.cpp:50-86): the taxonomyDB binary when present and current, else the dmp
+    // files under taxonomy/
+    bool haveTax = false;
+    if (std::ifstream(d + "/taxonomyDB").good()) {
+        haveTax = db->tax.loadTaxonomyDb(d + "/taxonomyDB", &e);
+        if (!haveTax && !e.empty()) {
+            setErr(err, errlen, e);
+            delete db;
+            return nullptr;
+        }
+    }
+    if ((!haveTax && !db->tax.loadDmp(d + "/taxonomy", &e)) || !db->buildSpeciesMap(&e)) {
         setErr(err, errlen, e);
         delete db;
         return nullptr;

@@ -66,7 +66,8 @@ static void writeReport(FILE* fp, const Taxonomy& t, const std::unordered_map<Ta
     }
     if (clade == 0) return;
     const TaxonNode& n = t.nodes[t.D[taxId]];
-    fprintf(fp, "%.4f\t%i\t%i\t%s\t%i\t%s%s\n", 100 * clade / double(total), clade, taxc, n.rank.c_str(), taxId,
+    fprintf(fp, "%.4f\t%i\t%i\t%s\t%i\t%s%s\n", 100 * clade / double(total), clade, taxc, n.rank.c_str(),
+            t.getOriginalTaxID(taxId),
             std::string(2 * depth, ' ').c_str(), n.name.c_str());
     std::vector<TaxID> ch = it->second.children;
     std::sort(ch.begin(), ch.end(), [&](TaxID a, TaxID b) { return cladeOf(cc, a) > cladeOf(cc, b); });

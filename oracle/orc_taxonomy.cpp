@@ -2,6 +2,8 @@
 #include "orc_taxonomy.h"
 
 #include <cassert>
+#include <cstring>
+#include <iterator>
 #include <fstream>
 #include <functional>
 
@@ -112,6 +114,78 @@ void Taxonomy::finish() {
             int a = M[i][j - 1], b = M[i + (1ul << (j - 1))][j - 1];
             M[i][j] = (L[a] < L[b]) ? a : b;
         }
+}
+
+bool Taxonomy::loadTaxonomyDb(const std::string& path, std::string* err) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) { *err = "cannot open " + path; return false; }
+    std::vector<char> mem((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    const char* p = mem.data();
+    const char* end = p + mem.size();
+    auto take = [&](void* dst, size_t bytes) {
+        if ((size_t)(end - p) < bytes) return false;
+        memcpy(dst, p, bytes);
+        p += bytes;
+        return true;
+    };
+    err->clear();
+    int version = 0;
+    if (!take(&version, sizeof(int))) { *err = "taxonomyDB truncated"; return false; }
+    if (version != kSerializationVersion) return false;  // outdated: dmp fallback
+    size_t internalUsed = 0;  // read as size_t; only the value 1 means "internal IDs" (:372-381)
+    if ((size_t)(end - p) < sizeof(size_t)) { *err = "taxonomyDB truncated"; return false; }
+    memcpy(&internalUsed, p, sizeof(size_t));
+    useInternalTaxID = internalUsed == 1;
+    if (useInternalTaxID) p += sizeof(size_t);
+    size_t maxNodes = 0;
+    int maxTax = 0;
+    if (!take(&maxNodes, sizeof(size_t)) || !take(&maxTax, sizeof(int)) || maxTax < 0) {
+        *err = "taxonomyDB truncated"; return false;
+    }
+    struct RawNode { int id; int taxId; int parentTaxId; size_t rankIdx; size_t nameIdx; };  // MMseqs2 TaxonNode
+    static_assert(sizeof(RawNode) == 32, "TaxonNode layout");
+    std::vector<RawNode> raw(maxNodes);
+    std::vector<int> d((size_t)maxTax + 1);
+    if (!take(raw.data(), maxNodes * sizeof(RawNode)) || !take(d.data(), d.size() * sizeof(int))) {
+        *err = "taxonomyDB truncated"; return false;
+    }
+    internal2orgTaxId.clear();
+    if (useInternalTaxID) {
+        internal2orgTaxId.resize((size_t)maxTax + 1);
+        if (!take(internal2orgTaxId.data(), internal2orgTaxId.size() * sizeof(int))) { *err = "taxonomyDB truncated"; return false; }
+    }
+    const size_t N = maxNodes * 2;
+    size_t K = 0;  // (int)flog2(N) + 1 columns
+    while ((2ul << K) <= N) K++;
+    K += 1;
+    E.assign(N, 0); L.assign(N, 0); H.assign(maxNodes, 0);
+    std::vector<int> flatM(N * K);
+    if (!take(E.data(), N * sizeof(int)) || !take(L.data(), N * sizeof(int)) || !take(H.data(), maxNodes * sizeof(int)) ||
+        !take(flatM.data(), flatM.size() * sizeof(int))) {
+        *err = "taxonomyDB truncated"; return false;
+    }
+    M.assign(N, std::vector<int>(K));
+    for (size_t i = 0; i < N; i++)
+        for (size_t k = 0; k < K; k++) M[i][k] = flatM[i * K + k];
+    // StringBlock<unsigned int>: byteCapacity, entryCapacity, entryCount, bytes, offsets
+    unsigned int byteCap = 0, entryCap = 0, entryCount = 0;
+    if (!take(&byteCap, 4) || !take(&entryCap, 4) || !take(&entryCount, 4)) { *err = "taxonomyDB truncated"; return false; }
+    std::vector<char> bytes(byteCap);
+    std::vector<unsigned int> offs(entryCap);
+    if (!take(bytes.data(), byteCap) || !take(offs.data(), (size_t)entryCap * 4)) { *err = "taxonomyDB truncated"; return false; }
+    auto str = [&](size_t idx) -> std::string {  // StringBlock::getString: NULL past entryCount
+        if (idx >= entryCount || offs[idx] >= byteCap) return "";
+        return std::string(bytes.data() + offs[idx], strnlen(bytes.data() + offs[idx], byteCap - offs[idx]));
+    };
+    nodes.clear();
+    for (size_t i = 0; i < maxNodes; i++)
+        nodes.push_back({raw[i].id, raw[i].taxId, raw[i].parentTaxId, str(raw[i].rankIdx), str(raw[i].nameIdx)});
+    maxTaxID = maxTax;
+    D = d;
+    eukaryotaTaxID = 0;  // setEukaryoteTaxID (TaxonomyWrapper.h:89-100): nodes with nameIdx 0 skipped
+    for (size_t i = 0; i < maxNodes; i++)
+        if (raw[i].nameIdx != 0 && nodes[i].name == "Eukaryota") { eukaryotaTaxID = nodes[i].taxId; break; }
+    return true;
 }
 
 int Taxonomy::rmq(int i, int j) const {  // NcbiTaxonomy::RangeMinimumQuery

@@ -42,6 +42,18 @@ public:
 
     // NcbiTaxonomy(names, nodes, merged) non-internal path (TaxonomyWrapper.cpp:67-118).
     bool loadDmp(const std::string& dir, std::string* err);
+    // TaxonomyWrapper::unserialize (TaxonomyWrapper.cpp:363-421) of a taxonomyDB file, with the
+    // MMseqs2 TaxonNode / StringBlock<unsigned int> layouts (unpinned). Returns false with *err
+    // empty when the serialization version differs (the reference then falls back to the dmp
+    // files, common.cpp:71-85), with *err set on a malformed file.
+    bool loadTaxonomyDb(const std::string& path, std::string* err);
+    static const int kSerializationVersion = 2;  // NcbiTaxonomy::SERIALIZATION_VERSION (MMseqs2)
+    bool useInternalTaxID = false;
+    std::vector<int> internal2orgTaxId;  // TaxonomyWrapper::internal2orgTaxId
+    TaxID getOriginalTaxID(TaxID t) const {  // TaxonomyWrapper.h:70-79
+        if (!useInternalTaxID) return t;
+        return (t >= 0 && t <= maxTaxID) ? internal2orgTaxId[t] : t;
+    }
     bool fromArrays(const int32_t* taxid, const int32_t* parent, size_t n, const std::vector<std::string>& ranks,
                     const std::vector<std::string>& names, const int32_t* mergedOld, const int32_t* mergedNew,
                     size_t nMerged, std::string* err);
