@@ -443,7 +443,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     }
     HIP_TRY(launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
                            c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
-                           prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg, s,
+                           prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg,
+                           prune_min_matches(a.minConsCnt, a.minConsCntEuk, a.maxCodonShift), s,
                            c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC));
     c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();

@@ -172,7 +172,7 @@ __device__ __forceinline__ uint8_t* run_live_lds() {
 
 template <int E, typename In>
 __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
-                                                uint32_t* __restrict__ liveCnt, uint32_t r) {
+                                                uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
     constexpr uint32_t T = 128 * E;  // load <= 1/2
     PruneLds<E>& L = prune_lds<E>();  // one LDS instance per E whatever the input type
     unsigned long long* pairKey = L.pairKey;
@@ -204,7 +204,7 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
     __syncthreads();
 #pragma unroll
     for (int sl = 0; sl < E; sl++)
-        if (64 * sl + lane < n && pairCnt[ps[sl]] >= 2) spLive[ss[sl]] = 1;
+        if (64 * sl + lane < n && pairCnt[ps[sl]] >= pm) spLive[ss[sl]] = 1;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
     int nLive = 0;
@@ -233,10 +233,10 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
 
 template <int E, typename In>
 __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
-                                             uint32_t* __restrict__ liveCnt, uint32_t r) {
+                                             uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
     if constexpr (E >= 2) {
         if (liveCnt) {
-            prune_then_sort<E>(in, out, base, n, lane, liveCnt, r);
+            prune_then_sort<E>(in, out, base, n, lane, liveCnt, r, pm);
             return;
         }
     }
@@ -259,6 +259,7 @@ __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict
         }
         return;
     }
+    if constexpr (E == 1) {  // E >= 2 prunes before sorting (prune_then_sort)
     uint8_t* runLive = run_live_lds<E>();
     const uint64_t lt = (1ull << lane) - 1;
     bool pair[E];
@@ -268,12 +269,11 @@ __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict
     for (int sl = 0; sl < E; sl++) {
         const int e = 64 * sl + lane;
         const uint64_t sf = h[sl] >> 29;  // species << 3 | frame
-        uint64_t nx = __shfl_down(sf, 1, 64), pv = __shfl_up(sf, 1, 64);
-        const uint64_t nxSlot = sl + 1 < E ? __shfl(h[sl + 1 < E ? sl + 1 : sl] >> 29, 0, 64) : ~0ull;
-        const uint64_t pvSlot = sl > 0 ? __shfl(h[sl > 0 ? sl - 1 : 0] >> 29, 63, 64) : ~0ull;
-        if (lane == 63) nx = nxSlot;
-        if (lane == 0) pv = pvSlot;
-        pair[sl] = e + 1 < n && nx == sf;
+        // sorted: a (species, frame) group of >= pm matches starts at e when e + pm - 1 has its pair
+        const uint64_t far = __shfl(sf, min(lane + (int)pm - 1, 63), 64);
+        uint64_t pv = __shfl_up(sf, 1, 64);  // every lane takes part in the shuffles
+        if (lane == 0) pv = ~0ull;
+        pair[sl] = e + (int)pm - 1 < n && far == sf;
         const bool start = e < n && (e == 0 || (pv >> 3) != (sf >> 3));
         const uint64_t m = __ballot(start);
         rid[sl] = runs + (uint32_t)__popcll(m & lt) + (uint32_t)start - 1u;  // starts at or before e, - 1
@@ -295,34 +295,35 @@ __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict
         kept += (uint32_t)__popcll(m);
     }
     if (lane == 0) liveCnt[r] = kept;
+    }
 }
 
 // inOff (nullable): the segments are read from in + inOff[r] * inC (the direct join's per-read slot
 // stretches) instead of in + mOff[r]; the output is at out + mOff[r] either way.
 template <typename In>
 __device__ __forceinline__ void segsort_small_run(const In& in, mtb_match* __restrict__ out, uint64_t base, int n,
-                                                  int lane, uint32_t* __restrict__ liveCnt, uint32_t r) {
-    if (n <= 1) {  // a lone match is a dead species run
+                                                  int lane, uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
+    if (n <= 1 || (liveCnt && n < (int)pm)) {  // too few matches for one live (species, frame) group
         if (lane == 0 && n == 1 && !liveCnt) out[base] = in.full(0);
         if (lane == 0 && liveCnt) liveCnt[r] = 0;
         return;
     }
-    if (n <= 64) segsort_regs<1>(in, out, base, n, lane, liveCnt, r);
-    else segsort_regs<2>(in, out, base, n, lane, liveCnt, r);
+    if (n <= 64) segsort_regs<1>(in, out, base, n, lane, liveCnt, r, pm);
+    else segsort_regs<2>(in, out, base, n, lane, liveCnt, r, pm);
 }
 
 __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
                                                       const SegMatch* __restrict__ seg,
                                                       const uint64_t* __restrict__ inOff, uint32_t inC,
                                                       uint32_t nReads, mtb_match* __restrict__ out,
-                                                      uint32_t* __restrict__ liveCnt) {
+                                                      uint32_t* __restrict__ liveCnt, uint32_t pm) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n > 128) return;
-    if (seg) segsort_small_run(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, threadIdx.x, liveCnt, r);
-    else segsort_small_run(MatchIn{in, base}, out, base, n, threadIdx.x, liveCnt, r);
+    if (seg) segsort_small_run(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, threadIdx.x, liveCnt, r, pm);
+    else segsort_small_run(MatchIn{in, base}, out, base, n, threadIdx.x, liveCnt, r, pm);
 }
 
 // 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
@@ -332,14 +333,14 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
                                                      const SegMatch* __restrict__ seg,
                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
                                                      uint32_t nReads, mtb_match* __restrict__ out,
-                                                     uint32_t* __restrict__ liveCnt) {
+                                                     uint32_t* __restrict__ liveCnt, uint32_t pm) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const int n = (int)(mOff[r + 1] - base);
     if (n <= 32 * E || n > 64 * E) return;
-    if (seg) segsort_regs<E>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, (int)threadIdx.x, liveCnt, r);
-    else segsort_regs<E>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r);
+    if (seg) segsort_regs<E>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
+    else segsort_regs<E>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -403,7 +404,7 @@ __device__ uint32_t block_scan_u32(uint32_t x, uint32_t* total, uint32_t* sWave)
 template <int kThreads, typename Idx>
 __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* rid, uint8_t* runLive, long n,
                                      const mtb_match* __restrict__ in, mtb_match* __restrict__ out, uint64_t base,
-                                     uint32_t* sWave) {
+                                     uint32_t* sWave, uint32_t pm) {
     const long per = (n + kThreads - 1) / kThreads;
     const long b = (long)threadIdx.x * per, e = min(n, b + per);
     uint32_t starts = 0;
@@ -418,7 +419,7 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
     __threadfence_block();  // the scratch may be global memory (segments over kBlockSeg)
     __syncthreads();
     for (long i = b; i < e; i++)
-        if (i + 1 < n && (H[i] >> 29) == (H[i + 1] >> 29)) runLive[rid[i]] = 1;
+        if (i + (long)pm - 1 < n && (H[i] >> 29) == (H[i + pm - 1] >> 29)) runLive[rid[i]] = 1;  // a group of >= pm
     __threadfence_block();
     __syncthreads();
     uint32_t mine = 0;
@@ -438,7 +439,7 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
 // and the live ones are then written compacted into H / L / I. Returns the live count.
 template <int kThreads, int kPer, typename Idx>
 __device__ long preprune_load(const mtb_match* __restrict__ in, uint64_t base, long n, uint32_t* cnt, uint32_t* flag,
-                              uint32_t logT, uint64_t* H, uint64_t* L, Idx* I, uint32_t* sWave) {
+                              uint32_t logT, uint64_t* H, uint64_t* L, Idx* I, uint32_t* sWave, uint32_t pm) {
     const uint32_t T = 1u << logT;
     for (uint32_t i = threadIdx.x; i < T; i += kThreads) {
         cnt[i] = 0;
@@ -464,7 +465,7 @@ __device__ long preprune_load(const mtb_match* __restrict__ in, uint64_t base, l
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kPer; k++)
-        if (b + k < n && cnt[hp[k]] >= 2) flag[hs[k]] = 1;
+        if (b + k < n && cnt[hp[k]] >= pm) flag[hs[k]] = 1;
     __syncthreads();
     uint32_t mask = 0;
 #pragma unroll
@@ -495,7 +496,7 @@ constexpr int kMidThreads = 256;
 __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
                                                              const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                              mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
-                                                             long mergeSeg) {
+                                                             long mergeSeg, uint32_t pm) {
     __shared__ uint64_t sh[kMidSeg], sl[kMidSeg];
     __shared__ uint16_t si[kMidSeg];
     __shared__ uint32_t sWave[kMidThreads / 64 + 1];
@@ -508,7 +509,7 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
     if (liveCnt) {
         static_assert(kMidSeg / kMidThreads == 8 && 2 * kMidSeg == 4096, "pre-prune geometry");
         m = preprune_load<kMidThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
-                                                    reinterpret_cast<uint32_t*>(sl), 12, sh, sl, si, sWave);
+                                                    reinterpret_cast<uint32_t*>(sl), 12, sh, sl, si, sWave, pm);
         if (m == 0) {
             if (threadIdx.x == 0) liveCnt[r] = 0;
             return;
@@ -528,7 +529,7 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
         n = m;
         uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
         const uint32_t kept = prune_pack_block<kMidThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n), n,
-                                                                      in, out, base, sWave);
+                                                                      in, out, base, sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
@@ -539,7 +540,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
                                                                  uint64_t* __restrict__ gScratch, int global,
-                                                                 uint32_t* __restrict__ liveCnt, long mergeSeg) {
+                                                                 uint32_t* __restrict__ liveCnt, long mergeSeg, uint32_t pm) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
@@ -557,7 +558,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
         if (liveCnt) {
             static_assert(kBlockSeg / kLargeThreads == 8 && 2 * kBlockSeg == 16384, "pre-prune geometry");
             m = preprune_load<kLargeThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
-                                                          reinterpret_cast<uint32_t*>(sl), 14, sh, sl, si, sWave);
+                                                          reinterpret_cast<uint32_t*>(sl), 14, sh, sl, si, sWave, pm);
             if (m == 0) {
                 if (threadIdx.x == 0) liveCnt[r] = 0;
                 return;
@@ -577,7 +578,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
         if (liveCnt) {  // the lo keys are no longer needed: their LDS holds the run ids and flags
             uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
             const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n),
-                                                                            n, in, out, base, sWave);
+                                                                            n, in, out, base, sWave, pm);
             if (threadIdx.x == 0) liveCnt[r] = kept;
             return;
         }
@@ -598,7 +599,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     if (liveCnt) {  // run ids and flags in the lo-key scratch (2 * p2 words, p2 >= n)
         uint32_t* rid = reinterpret_cast<uint32_t*>(Lo);
         const uint32_t kept =
-            prune_pack_block<kLargeThreads, uint32_t>(H, I, rid, reinterpret_cast<uint8_t*>(rid + n), n, in, out, base, sWave);
+            prune_pack_block<kLargeThreads, uint32_t>(H, I, rid, reinterpret_cast<uint8_t*>(rid + n), n, in, out, base, sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
@@ -695,7 +696,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
                                                                 const uint32_t* __restrict__ reads, uint64_t M,
                                                                 uint64_t* __restrict__ scratch, int b,
                                                                 mtb_match* __restrict__ out,
-                                                                uint32_t* __restrict__ liveCnt) {
+                                                                uint32_t* __restrict__ liveCnt, uint32_t pm) {
     __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
     const uint32_t r = reads[blockIdx.x];
     const uint64_t base = mOff[r];
@@ -705,7 +706,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
         uint32_t* rid = reinterpret_cast<uint32_t*>(T.l + base);
         const uint32_t kept = prune_pack_block<kLargeThreads, uint32_t>(S.h + base, S.x + base, rid,
                                                                         reinterpret_cast<uint8_t*>(rid + n), n, in,
-                                                                        out, base, sWave);
+                                                                        out, base, sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
@@ -719,7 +720,8 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
     } while (0)
 
 static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M,
-                                    mtb_match* out, uint64_t* scratch, uint32_t* liveCnt, long chunk, hipStream_t s) {
+                                    mtb_match* out, uint64_t* scratch, uint32_t* liveCnt, long chunk, uint32_t pm,
+                                    hipStream_t s) {
     std::vector<uint64_t> off(nReads + 1);
     MTB_HIP_RET(hipMemcpyAsync(off.data(), mOff, sizeof(uint64_t) * (nReads + 1), hipMemcpyDeviceToHost, s));
     MTB_HIP_RET(hipStreamSynchronize(s));
@@ -768,7 +770,7 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
         b ^= 1;
     }
     if (e == hipSuccess) {
-        k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt);
+        k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt, pm);
         e = hipGetLastError();
     }
     if (dTiles) hipFreeAsync(dTiles, s);
@@ -779,24 +781,25 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
 
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                          hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
+                          uint32_t pm, hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
+    pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
     if (seg && (global || maxSeg > kSmallSeg)) return hipErrorInvalidValue;  // sparse input: register sorts only
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm);
         return hipGetLastError();
     }
-    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
     if (maxSeg > 128)
-        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
+        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
     if (maxSeg > 256)
-        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt);
-    if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk);
+        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
+    if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm);
     if (maxSeg > kMidSeg)
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm);
     MTB_HIP_RET(hipGetLastError());
-    if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, s);
+    if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, s);
     return hipSuccess;
 }
 
@@ -930,16 +933,17 @@ __global__ void k_run_starts(const uint32_t* __restrict__ gFlag, const uint32_t*
     }
 }
 
-// Work list for k_match_paths: the groups of >= 2 matches (a single match makes no path) in batch
-// order, so a wave's lanes still walk neighbouring groups (ordering them by size instead was
-// slower: the lost locality costs more than the divergence it removes). Single-match groups get
-// the sentinel key and zero paths; one stable radix pass on an all-zero digit compacts the rest.
+// Work list for k_match_paths: the groups that can emit a path (>= prune_min_matches matches: a
+// single match is never searched, and fewer matches cannot chain MIN_DEPTH codons) in batch order,
+// so a wave's lanes still walk neighbouring groups (ordering them by size instead was slower: the
+// lost locality costs more than the divergence it removes). The others get the sentinel key and
+// zero paths; one stable radix pass on an all-zero digit compacts the rest.
 __global__ void k_group_keys(const uint64_t* __restrict__ gStart, uint64_t nG, uint64_t* __restrict__ keys,
-                             uint64_t* __restrict__ vals, uint32_t* __restrict__ pathCnt) {
+                             uint64_t* __restrict__ vals, uint32_t* __restrict__ pathCnt, uint32_t minGroup) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nG) return;
     const uint64_t n = gStart[g + 1] - gStart[g];
-    if (n <= 1) {
+    if (n < minGroup) {  // too few matches to chain a path of MIN_DEPTH (prune_min_matches): no paths
         pathCnt[g] = 0;
         keys[g] = kSentinel;
     } else {
@@ -1628,8 +1632,9 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
         hostStats[0] = cnt[0];
         hostStats[2] = cnt[1];
         if (cnt[0]) {
-            k_group_keys<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(s.gStart, cnt[0], s.ordKA, s.ordVA,
-                                                                            s.pathCnt);
+            k_group_keys<<<(unsigned)((cnt[0] + 255) / 256), 256, 0, st>>>(
+                s.gStart, cnt[0], s.ordKA, s.ordVA, s.pathCnt,
+                prune_min_matches(a.minConsCnt, a.minConsCntEuk, a.maxCodonShift));
             bool inB = false;
             const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true, false,
                                                     s.radixCounts, s.radixOffs, s.scanTmp, &inB, st);

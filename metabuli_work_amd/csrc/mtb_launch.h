@@ -230,10 +230,24 @@ uint64_t clade_bytes();
 // direct join's layout, 16-B SegMatch) rather than in + mOff[r]
 // Returns the first HIP error of its allocations, copies and launches (hipErrorInvalidValue for a
 // sparse input outside the register sorts' range).
+// pruneMin: a species is live when one of its (species, frame) groups holds >= pruneMin matches
+// (prune_min_matches); >= 2 always.
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                          hipStream_t s, const SegMatch* seg = nullptr, const uint64_t* inOff = nullptr,
-                          uint32_t inC = 0);
+                          uint32_t pruneMin, hipStream_t s, const SegMatch* seg = nullptr,
+                          const uint64_t* inOff = nullptr, uint32_t inC = 0);
+// The fewest matches a (species, frame) group needs for getMatchPaths to emit a path: a path of
+// depth d chains >= 1 + ceil((d - 1) / maxCodonShift) matches (each link adds a shift of at most
+// maxCodonShift codons, Taxonomer.cpp:487-648), paths are emitted at depth >= MIN_DEPTH
+// (minConsCnt, or minConsCntEuk under Eukaryota: the smaller bounds both), and a group of one match
+// is never searched (Taxonomer.cpp:334-344). A species with no path gets no score and is read by
+// nothing downstream (Taxonomer.cpp:347-408), so its matches are dead.
+inline uint32_t prune_min_matches(int minConsCnt, int minConsCntEuk, int maxCodonShift) {
+    const int d = minConsCnt < minConsCntEuk ? minConsCnt : minConsCntEuk;
+    const int sh = maxCodonShift > 0 ? maxCodonShift : 1;
+    const int need = d <= 1 ? 1 : 1 + (d - 1 + sh - 1) / sh;
+    return (uint32_t)(need < 2 ? 2 : need);
+}
 // the live prefix of each segment (mOff) to out at liveOff (exclusive scan of liveCnt)
 void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t* liveOff, uint32_t nReads,
                       mtb_match* out, int* err, hipStream_t s);
