@@ -76,6 +76,7 @@ struct mtb_ctx {
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
+    int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1: K6 chooseBestTaxon thread / wave per read (tests; default auto)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -235,6 +236,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
@@ -403,6 +405,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     const uint64_t M = c->M;
     AssignArgs a = assign_args(c->par);
     a.generic = c->forceGeneric ? 1 : 0;
+    a.waveTaxon = c->waveTaxon;
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     const uint64_t Mc = std::max<uint64_t>(M, 1);

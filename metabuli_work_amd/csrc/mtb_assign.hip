@@ -1393,92 +1393,17 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
     if (lane == 0) species_score(score, readLength, cfg, spScore, spKeep, s);
 }
 
-// chooseBestTaxon (Taxonomer.cpp:130-202), filterRedundantMatches (:205-241), taxCnt and the
-// lower-rank BFS (:252-314) for one read.
-__global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff,
-                                                      const uint32_t* __restrict__ qlen, uint32_t nReads,
-                                                      const uint64_t* __restrict__ sScan,
-                                                      const uint64_t* __restrict__ sStart,
-                                                      const uint64_t* __restrict__ gScan,
-                                                      const uint64_t* __restrict__ gStart,
-                                                      const float* __restrict__ spScore,
-                                                      const uint8_t* __restrict__ spKeep, AssignCfg cfg, TaxView tax,
-                                                      Clade* __restrict__ cladeP,
-                                                      uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
-                                                      mtb_result* __restrict__ results) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nReads) return;
-    const uint64_t base = mOff[r];
-    const long n = (long)(mOff[r + 1] - base);
-    const int readLength = (int)qlen[r];
-    mtb_result res;
-    res.classification = 0;
-    res.score = 0.0f;
-    res.hamming_dist = 0;
-    res.query_length = (uint32_t)readLength;
-    res.taxcnt_offset = (uint32_t)0;
-    res.taxcnt_len = 0;
-    res.is_classified = 0;
-    for (int k = 0; k < 7; k++) res.pad[k] = 0;
-    if (n == 0) { results[r] = res; return; }
-
-    // ---- getBestSpeciesMatches tail (Taxonomer.cpp:380-408) over the read's species runs ----
-    const uint64_t s0 = sScan[base], s1 = sScan[base + n];
-    long meaningful = 0;
-    float bestSpScore = 0.0f;
-    uint64_t bestFirst = 0, bestSecond = 0;
-    for (uint64_t s = s0; s < s1; s++) {
-        if (!spKeep[s]) continue;
-        const float score = spScore[s];
-        if (score > 0.f) meaningful++;
-        if (score > bestSpScore) { bestSpScore = score; bestFirst = sStart[s]; bestSecond = sStart[s + 1]; }
-    }
-
-    // ---- chooseBestTaxon (Taxonomer.cpp:130-202) ----
-    float spTotal = 0.0f;
-    int32_t bestTax = 0;
-    bool isLCA = false;
-    if (meaningful > 0) {
-        const float thr = bestSpScore * cfg.tieRatio;
-        long cnt = 0;
-        int lcaNode = -1;
-        for (uint64_t s = s0; s < s1; s++) {
-            if (!spKeep[s]) continue;
-            if (spScore[s] >= thr) {
-                cnt++;
-                spTotal += spScore[s];
-                const int32_t t = (int32_t)M[sStart[s]].species_id;
-                if (cnt == 1) bestTax = t;
-                if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
-            }
-        }
-        if (cnt > 1) {
-            isLCA = true;
-            bestTax = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
-            spTotal = spTotal / (float)cnt;
-        }
-    }
-    if (spTotal == 0 || spTotal < cfg.minScore) {
-        res.score = spTotal;
-        results[r] = res;
-        return;
-    }
-    if (isLCA) {
-        res.is_classified = 1;
-        res.classification = bestTax;
-        res.score = spTotal;
-        results[r] = res;
-        return;
-    }
-
-    // ---- filterRedundantMatches (Taxonomer.cpp:205-241) ----
-    // Per quotient q = pos / dnaShift: the best (lowest hamming) match's taxon, ties folded with
-    // LCA — an order-free reduction. Within the best species the matches are sorted by frame, then
-    // position, so each frame's quotients ascend: a <= 6-way merge over the frame runs visits each
-    // quotient once, in order, with no per-read quotient table.
+// filterRedundantMatches (Taxonomer.cpp:205-241) for the best species' matches B[0, nb), serially.
+// Per quotient q = pos / dnaShift: the best (lowest hamming) match's taxon, ties folded with LCA —
+// an order-free reduction. Within the best species the matches are sorted by frame, then position,
+// so each frame's quotients ascend: a <= 6-way merge over the frame runs visits each quotient once,
+// in order, with no per-read quotient table. taxCnt goes to tc (capacity >= nb) in std::map order
+// (ascending taxID); returns its length.
+__device__ long filter_redundant_serial(const mtb_match* __restrict__ M, uint64_t bestFirst, uint64_t bestSecond,
+                                        const uint64_t* __restrict__ gScan, const uint64_t* __restrict__ gStart,
+                                        uint32_t dnaShift, const TaxView& tax, mtb_taxcnt* __restrict__ tc) {
     uint32_t fc[6], fin[6], head[6];
     const mtb_match* B = M + bestFirst;
-    const uint32_t dnaShift = (uint32_t)cfg.dnaShift;
     int nf = 0;
     for (uint64_t g = gScan[bestFirst]; nf < 6 && gStart[g] < bestSecond; g++) {
         fc[nf] = (uint32_t)(gStart[g] - bestFirst);
@@ -1491,7 +1416,6 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
     constexpr int kRegTc = 4;
     int32_t rt[kRegTc];
     uint32_t rc[kRegTc];
-    mtb_taxcnt* tc = tcP + base;  // capacity n (each quotient holds >= 1 match)
     long nTc = 0;
     while (true) {
         uint32_t qmin = 0xFFFFFFFFu;
@@ -1542,20 +1466,24 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
         while (b > 0 && tc[b - 1].tax_id > v.tax_id) { tc[b] = tc[b - 1]; b--; }
         tc[b] = v;
     }
+    return nTc;
+}
+
+// chooseBestTaxon after filterRedundantMatches (Taxonomer.cpp:175-201): the parent of the species
+// below minSpScore, else lowerRankClassification / getSpeciesCladeCounts / BFS (:252-314) over the
+// taxCnt list tc[0, nTc). cl: the read's clade scratch (clCap entries).
+__device__ void classify_tail(mtb_result& res, const mtb_taxcnt* __restrict__ tc, long nTc, float spTotal,
+                              int32_t bestTax, int readLength, const AssignCfg& cfg, const TaxView& tax,
+                              Clade* __restrict__ cl, long clCap) {
     res.taxcnt_offset = (uint32_t)0;
     res.taxcnt_len = (uint32_t)nTc;
     res.is_classified = 1;
     res.score = spTotal;
     if (spTotal < cfg.minSpScore) {
         res.classification = tax.exists(bestTax) ? tax.spParent[tax.nodeOf[bestTax]] : 0;
-        results[r] = res;
         return;
     }
-
-    // ---- lowerRankClassification / getSpeciesCladeCounts / BFS (Taxonomer.cpp:252-314) ----
     const int32_t spT = bestTax;
-    Clade* cl = cladeP + base * cladePerMatch;
-    const long clCap = n * (long)cladePerMatch;
     long nCl = 0;
     auto findOrAdd = [&](int32_t t) -> long {
         for (long z = 0; z < nCl; z++)
@@ -1607,6 +1535,288 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
         cur = cl[best].tax;
     }
     res.classification = cur;
+}
+
+__device__ __forceinline__ mtb_result empty_result(int readLength) {
+    mtb_result res;
+    res.classification = 0;
+    res.score = 0.0f;
+    res.hamming_dist = 0;
+    res.query_length = (uint32_t)readLength;
+    res.taxcnt_offset = (uint32_t)0;
+    res.taxcnt_len = 0;
+    res.is_classified = 0;
+    for (int k = 0; k < 7; k++) res.pad[k] = 0;
+    return res;
+}
+
+// chooseBestTaxon (Taxonomer.cpp:130-202), filterRedundantMatches (:205-241), taxCnt and the
+// lower-rank BFS (:252-314): one thread per read (short reads).
+__global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff,
+                                                      const uint32_t* __restrict__ qlen, uint32_t nReads,
+                                                      const uint64_t* __restrict__ sScan,
+                                                      const uint64_t* __restrict__ sStart,
+                                                      const uint64_t* __restrict__ gScan,
+                                                      const uint64_t* __restrict__ gStart,
+                                                      const float* __restrict__ spScore,
+                                                      const uint8_t* __restrict__ spKeep, AssignCfg cfg, TaxView tax,
+                                                      Clade* __restrict__ cladeP,
+                                                      uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
+                                                      mtb_result* __restrict__ results) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    const int readLength = (int)qlen[r];
+    mtb_result res = empty_result(readLength);
+    if (n == 0) { results[r] = res; return; }
+
+    // ---- getBestSpeciesMatches tail (Taxonomer.cpp:380-408) over the read's species runs ----
+    const uint64_t s0 = sScan[base], s1 = sScan[base + n];
+    long meaningful = 0;
+    float bestSpScore = 0.0f;
+    uint64_t bestFirst = 0, bestSecond = 0;
+    for (uint64_t s = s0; s < s1; s++) {
+        if (!spKeep[s]) continue;
+        const float score = spScore[s];
+        if (score > 0.f) meaningful++;
+        if (score > bestSpScore) { bestSpScore = score; bestFirst = sStart[s]; bestSecond = sStart[s + 1]; }
+    }
+
+    // ---- chooseBestTaxon (Taxonomer.cpp:130-202) ----
+    float spTotal = 0.0f;
+    int32_t bestTax = 0;
+    bool isLCA = false;
+    if (meaningful > 0) {
+        const float thr = bestSpScore * cfg.tieRatio;
+        long cnt = 0;
+        int lcaNode = -1;
+        for (uint64_t s = s0; s < s1; s++) {
+            if (!spKeep[s]) continue;
+            if (spScore[s] >= thr) {
+                cnt++;
+                spTotal += spScore[s];
+                const int32_t t = (int32_t)M[sStart[s]].species_id;
+                if (cnt == 1) bestTax = t;
+                if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
+            }
+        }
+        if (cnt > 1) {
+            isLCA = true;
+            bestTax = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
+            spTotal = spTotal / (float)cnt;
+        }
+    }
+    if (spTotal == 0 || spTotal < cfg.minScore) {
+        res.score = spTotal;
+        results[r] = res;
+        return;
+    }
+    if (isLCA) {
+        res.is_classified = 1;
+        res.classification = bestTax;
+        res.score = spTotal;
+        results[r] = res;
+        return;
+    }
+    mtb_taxcnt* tc = tcP + base;  // capacity n (each quotient holds >= 1 match)
+    const long nTc = filter_redundant_serial(M, bestFirst, bestSecond, gScan, gStart, (uint32_t)cfg.dnaShift, tax, tc);
+    classify_tail(res, tc, nTc, spTotal, bestTax, readLength, cfg, tax, cladeP + base * cladePerMatch,
+                  n * (long)cladePerMatch);
+    results[r] = res;
+}
+
+// The same for reads with many matches (long reads): one wave per read. The species-run scan is
+// spread over the lanes (sum / max reductions, the first maximum by ballot; the tie set summed in
+// species order, as the reference's float additions run); filterRedundantMatches is a parallel
+// reduction over a per-quotient table in LDS (atomicMin of the hamming, then LCA folds of the
+// minimal matches' taxa by compare-and-swap: an order-free reduction, as the serial fold is), and
+// taxCnt a small LDS hash of (taxon, count). Reads whose quotients or distinct taxa do not fit take
+// the serial code on lane 0.
+constexpr int kWavePerReadMatches = 256;  // live matches per read above which K6 goes wave per read
+constexpr int kQuotLds = 8192;   // quotients per read in LDS: reads of up to ~24.5 kb at dnaShift 3
+constexpr int kTcHash = 256;     // distinct taxa of one read's taxCnt in LDS
+
+__device__ __forceinline__ float wave_max_f(float x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x = fmaxf(x, __shfl_xor(x, d, 64));
+    return x;
+}
+__device__ __forceinline__ long wave_sum_l(long x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+__global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff,
+                                                          const uint32_t* __restrict__ qlen, uint32_t nReads,
+                                                          const uint64_t* __restrict__ sScan,
+                                                          const uint64_t* __restrict__ sStart,
+                                                          const uint64_t* __restrict__ gScan,
+                                                          const uint64_t* __restrict__ gStart,
+                                                          const float* __restrict__ spScore,
+                                                          const uint8_t* __restrict__ spKeep, AssignCfg cfg,
+                                                          TaxView tax, Clade* __restrict__ cladeP,
+                                                          uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
+                                                          mtb_result* __restrict__ results) {
+    __shared__ uint32_t qmin[kQuotLds];
+    __shared__ int32_t qtax[kQuotLds];
+    __shared__ int32_t hk[kTcHash];
+    __shared__ uint32_t hc[kTcHash];
+    __shared__ int sFlag;
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const int lane = threadIdx.x;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    const int readLength = (int)qlen[r];
+    mtb_result res = empty_result(readLength);
+    if (n == 0) {
+        if (lane == 0) results[r] = res;
+        return;
+    }
+    const uint64_t s0 = sScan[base], s1 = sScan[base + n];
+    long meaningful = 0;
+    float bestSpScore = 0.0f;
+    for (uint64_t s = s0 + lane; s < s1; s += 64) {
+        if (!spKeep[s]) continue;
+        const float score = spScore[s];
+        meaningful += score > 0.f;
+        bestSpScore = fmaxf(bestSpScore, score);
+    }
+    meaningful = wave_sum_l(meaningful);
+    bestSpScore = wave_max_f(bestSpScore);  // every lane: the maximum (> 0 when meaningful)
+    float spTotal = 0.0f;
+    int32_t bestTax = 0;
+    bool isLCA = false;
+    uint64_t bestFirst = 0, bestSecond = 0;
+    if (meaningful > 0) {
+        // the first species run reaching the maximum (the serial scan keeps the first strict max)
+        for (uint64_t c = s0; c < s1; c += 64) {
+            const uint64_t s = c + lane;
+            const bool hit = s < s1 && spKeep[s] && spScore[s] == bestSpScore;
+            const unsigned long long m = __ballot(hit);
+            if (m) {
+                const uint64_t sb = c + (uint64_t)(__ffsll((long long)m) - 1);
+                bestFirst = sStart[sb];
+                bestSecond = sStart[sb + 1];
+                break;
+            }
+        }
+        // the tie set in species order: scores summed one by one (wave-uniform), LCA folded
+        const float thr = bestSpScore * cfg.tieRatio;
+        long cnt = 0;
+        int lcaNode = -1;
+        for (uint64_t c = s0; c < s1; c += 64) {
+            const uint64_t s = c + lane;
+            const bool in = s < s1 && spKeep[s] && spScore[s] >= thr;
+            const float sc = in ? spScore[s] : 0.0f;
+            const int32_t sp = in ? (int32_t)M[sStart[s]].species_id : 0;
+            unsigned long long m = __ballot(in);
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const float v = __shfl(sc, b, 64);
+                const int32_t t = __shfl(sp, b, 64);
+                cnt++;
+                spTotal += v;
+                if (cnt == 1) bestTax = t;
+                if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
+            }
+        }
+        if (cnt > 1) {
+            isLCA = true;
+            bestTax = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
+            spTotal = spTotal / (float)cnt;
+        }
+    }
+    if (spTotal == 0 || spTotal < cfg.minScore || isLCA) {
+        if (lane == 0) {
+            res.score = spTotal;
+            if (isLCA && !(spTotal == 0 || spTotal < cfg.minScore)) {
+                res.is_classified = 1;
+                res.classification = bestTax;
+            }
+            results[r] = res;
+        }
+        return;
+    }
+    // ---- filterRedundantMatches over the best species' matches ----
+    mtb_taxcnt* tc = tcP + base;  // capacity n
+    const uint32_t dnaShift = (uint32_t)cfg.dnaShift;
+    const long maxQ = (readLength + 3) / (long)dnaShift;
+    const long nb = (long)(bestSecond - bestFirst);
+    const mtb_match* B = M + bestFirst;
+    long nTc = -1;  // -1: take the serial path
+    if (maxQ < kQuotLds) {
+        for (long q = lane; q <= maxQ; q += 64) { qmin[q] = 0xFFFFFFFFu; qtax[q] = 0; }
+        for (int k = lane; k < kTcHash; k += 64) { hk[k] = 0; hc[k] = 0; }
+        if (lane == 0) sFlag = 0;
+        __syncthreads();
+        for (long i = lane; i < nb; i += 64) {
+            const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
+            if (q > (uint32_t)maxQ) { sFlag = 1; continue; }
+            atomicMin(&qmin[q], (uint32_t)B[i].hamming);
+        }
+        __syncthreads();
+        if (!sFlag) {
+            for (long i = lane; i < nb; i += 64) {
+                const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
+                if ((uint32_t)B[i].hamming != qmin[q]) continue;
+                const int32_t t = (int32_t)B[i].target_id;
+                int32_t old = qtax[q];
+                while (true) {  // qtax[q] = LCA(qtax[q], t), 0 = empty
+                    const int32_t nv = old == 0 ? t : tax.lca(old, t);
+                    if (nv == old) break;
+                    const int32_t prev = atomicCAS(&qtax[q], old, nv);
+                    if (prev == old) break;
+                    old = prev;
+                }
+            }
+            __syncthreads();
+            for (long q = lane; q <= maxQ; q += 64) {
+                const int32_t t = qtax[q];
+                if (t == 0) continue;
+                uint32_t h = ((uint32_t)t * 2654435761u) & (kTcHash - 1);
+                int probes = 0;
+                while (true) {
+                    const int32_t prev = atomicCAS(&hk[h], 0, t);
+                    if (prev == 0 || prev == t) { atomicAdd(&hc[h], 1u); break; }
+                    h = (h + 1) & (kTcHash - 1);
+                    if (++probes == kTcHash) { sFlag = 1; break; }
+                }
+            }
+            __syncthreads();
+        }
+        if (!sFlag) {  // entries out in slot order, then std::map order (ascending taxID) on lane 0
+            long at = 0;
+            for (int k0 = 0; k0 < kTcHash; k0 += 64) {
+                const int k = k0 + lane;
+                const bool v = hk[k] != 0;
+                const unsigned long long m = __ballot(v);
+                if (v) {
+                    const long p = at + (long)__popcll(m & ((1ull << lane) - 1));
+                    tc[p].tax_id = hk[k];
+                    tc[p].count = hc[k];
+                }
+                at += (long)__popcll(m);
+            }
+            nTc = at;
+        }
+    }
+    if (lane != 0) return;
+    if (nTc < 0) {
+        nTc = filter_redundant_serial(M, bestFirst, bestSecond, gScan, gStart, dnaShift, tax, tc);
+    } else {
+        for (long a = 1; a < nTc; a++) {
+            mtb_taxcnt v = tc[a];
+            long b = a;
+            while (b > 0 && tc[b - 1].tax_id > v.tax_id) { tc[b] = tc[b - 1]; b--; }
+            tc[b] = v;
+        }
+    }
+    classify_tail(res, tc, nTc, spTotal, bestTax, readLength, cfg, tax, cladeP + base * cladePerMatch,
+                  n * (long)cladePerMatch);
     results[r] = res;
 }
 
@@ -1660,12 +1870,19 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
     }
-    // one thread per read: with few, long reads (50k ONT reads) 256-thread blocks would leave CUs
-    // idle, so the blocks are one wave when the batch has fewer than 64 reads per CU
-    const unsigned ctT = nReads < 256u * 256u ? 64u : 256u;
-    k_choose_taxon<<<(nReads + ctT - 1) / ctT, ctT, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
-                                                         s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
-                                                         (Clade*)s.clade, s.cladePerMatch, tcPool, results);
+    // one thread per read, or one wave per read when reads carry many matches (long reads: a
+    // thread per read would leave most SIMDs idle and serialise each read's best-species scan)
+    const bool wave = a.waveTaxon >= 0 ? a.waveTaxon == 1 : (!a.generic && nM > (uint64_t)kWavePerReadMatches * nReads);
+    if (wave) {
+        k_choose_taxon_wave<<<nReads, 64, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart, s.gScan, s.gStart,
+                                                   s.spScore, s.spKeep, cfg, tv, (Clade*)s.clade, s.cladePerMatch,
+                                                   tcPool, results);
+    } else {
+        const unsigned ctT = nReads < 256u * 256u ? 64u : 256u;
+        k_choose_taxon<<<(nReads + ctT - 1) / ctT, ctT, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
+                                                             s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
+                                                             (Clade*)s.clade, s.cladePerMatch, tcPool, results);
+    }
 }
 
 uint64_t path_bytes() { return sizeof(Path); }

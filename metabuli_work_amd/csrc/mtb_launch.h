@@ -33,6 +33,7 @@ struct AssignArgs {
     int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
     float minScore, minSpScore, tieRatio;
     int generic;  // MTB_FORCE_GENERIC: general code paths only (parity tests of the fallbacks)
+    int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread per read, 1 wave per read (K6 chooseBestTaxon)
 };
 
 struct AssignScratch {  // per match unless noted

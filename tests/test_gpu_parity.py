@@ -241,3 +241,22 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
         assert np.array_equal(gm, omatches)
         compare_results(br.results, br.taxcnt, ores, otc)
     odb.close()
+
+
+@pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt1", "long"),
+                                          ("fmt2_syncmer", "long"), ("fmt2_syncmer", "paired")])
+@pytest.mark.parametrize("wave", ["0", "1"])
+def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
+    """K6's chooseBestTaxon both ways — a thread per read (short reads) and a wave per read (long
+    reads: parallel species scan, per-quotient LDS reduction for filterRedundantMatches) — forced
+    on every read kind with MTB_WAVE_TAXON, against the oracle."""
+    monkeypatch.setenv("MTB_WAVE_TAXON", wave)
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    odb = oc.OracleDb(db_dir)
+    reads = _reads(gen, kind, 1500 if kind != "long" else 80, 55)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
