@@ -77,6 +77,7 @@ struct mtb_ctx {
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
     int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1: K6 chooseBestTaxon thread / wave per read (tests; default auto)
+    bool pruneCompact = true;    // MTB_PRUNE_COMPACT=0: big K5 segments are not thinned before their sort (tests)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -95,6 +96,7 @@ struct mtb_ctx {
     DevBuf qFrom, probeStats;
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
+    DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
     static constexpr int kNumStats = 12;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
@@ -237,6 +239,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
@@ -346,7 +349,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results};
     for (DevBuf* b : bufs) b->release();
@@ -429,11 +432,13 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     uint32_t maxSeg = 0;
     HIP_TRY(hipMemcpyAsync(&maxSeg, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    // dead matches (species with no path-capable (species, frame) group) are dropped in K5 unless
+    // the batch keeps its stages (mtb_get_matches returns every match) or runs the general paths
+    const bool prune = !keep && !c->forceGeneric;
     if (maxSeg > kSegSortLds || c->forceGeneric || c->segsortGlobal || (c->mergeSeg && maxSeg > c->mergeSeg))
         HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
-    // dead matches (no frame run of two in their species) are dropped in K5 unless the batch keeps
-    // its stages (mtb_get_matches returns every match) or runs the general paths
-    const bool prune = !keep && !c->forceGeneric;
+    const bool compact = prune && maxSeg > kSegSortRegs && !c->segsortGlobal && c->pruneCompact;
+    if (compact) HIP_TRY(c->segLen.ensure(sizeof(uint32_t) * (n + 1)));  // big segments thinned before sorting
     c->keepStages = !prune;  // mtb_get_matches: matchesSorted is complete only without pruning
     HIP_TRY(c->liveCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -448,7 +453,9 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
                            c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
                            prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg,
                            prune_min_matches(a.minConsCnt, a.minConsCntEuk, a.maxCodonShift), s,
-                           c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC));
+                           c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC,
+                           compact ? c->segLen.as<uint32_t>() : nullptr,
+                           c->maxSeg.as<uint32_t>()));
     c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();

@@ -41,6 +41,16 @@ __device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, ui
 constexpr int kSmallSeg = 512;  // segments up to this many matches sort in registers (one wave, <= 8 per lane)
 static_assert(kSmallSeg == (int)kSegSortRegs, "one register-sort bound");
 constexpr int kBlockSeg = 8192;
+constexpr uint32_t kSegSkip = 0xFFFFFFFFu;  // segLen entry of a read another pass sorts
+
+// The length of read r's segment: its mOff stretch, or segLen[r] when given (segments compacted in
+// place by k_prune_compact); -1 = not this pass's read (kSegSkip).
+__device__ __forceinline__ long seg_len(const uint64_t* __restrict__ mOff, const uint32_t* __restrict__ segLen,
+                                        uint32_t r) {
+    if (!segLen) return (long)(mOff[r + 1] - mOff[r]);
+    const uint32_t v = segLen[r];
+    return v == kSegSkip ? -1 : (long)v;
+}
 
 // Segments of up to 64E matches sort in registers: element e = 64*slot + lane. Exchanges at
 // distance j < 64 swap with lane ^ j through cross-lane shuffles, j >= 64 swap slots inside a lane;
@@ -316,12 +326,14 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
                                                       const SegMatch* __restrict__ seg,
                                                       const uint64_t* __restrict__ inOff, uint32_t inC,
                                                       uint32_t nReads, mtb_match* __restrict__ out,
-                                                      uint32_t* __restrict__ liveCnt, uint32_t pm) {
+                                                      uint32_t* __restrict__ liveCnt, uint32_t pm,
+                                                      const uint32_t* __restrict__ segLen) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    const int n = (int)(mOff[r + 1] - base);
-    if (n > 128) return;
+    const long nl = seg_len(mOff, segLen, r);
+    if (nl < 0 || nl > 128) return;
+    const int n = (int)nl;
     if (seg) segsort_small_run(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, threadIdx.x, liveCnt, r, pm);
     else segsort_small_run(MatchIn{in, base}, out, base, n, threadIdx.x, liveCnt, r, pm);
 }
@@ -333,12 +345,14 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
                                                      const SegMatch* __restrict__ seg,
                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
                                                      uint32_t nReads, mtb_match* __restrict__ out,
-                                                     uint32_t* __restrict__ liveCnt, uint32_t pm) {
+                                                     uint32_t* __restrict__ liveCnt, uint32_t pm,
+                                                     const uint32_t* __restrict__ segLen) {
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    const int n = (int)(mOff[r + 1] - base);
-    if (n <= 32 * E || n > 64 * E) return;
+    const long nl = seg_len(mOff, segLen, r);
+    if (nl <= 32 * E || nl > 64 * E) return;
+    const int n = (int)nl;
     if (seg) segsort_regs<E>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
     else segsort_regs<E>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
 }
@@ -496,14 +510,15 @@ constexpr int kMidThreads = 256;
 __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
                                                              const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                              mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
-                                                             long mergeSeg, uint32_t pm) {
+                                                             long mergeSeg, uint32_t pm,
+                                                             const uint32_t* __restrict__ segLen) {
     __shared__ uint64_t sh[kMidSeg], sl[kMidSeg];
     __shared__ uint16_t si[kMidSeg];
     __shared__ uint32_t sWave[kMidThreads / 64 + 1];
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    long n = (long)(mOff[r + 1] - base);
+    long n = seg_len(mOff, segLen, r);
     if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
     long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
     if (liveCnt) {
@@ -540,13 +555,15 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
                                                                  uint64_t* __restrict__ gScratch, int global,
-                                                                 uint32_t* __restrict__ liveCnt, long mergeSeg, uint32_t pm) {
+                                                                 uint32_t* __restrict__ liveCnt, long mergeSeg, uint32_t pm,
+                                                                 const uint32_t* __restrict__ segLen) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
-    long n = (long)(mOff[r + 1] - base);
+    long n = seg_len(mOff, segLen, r);
+    if (n < 0) return;
     if (global && n == 0 && liveCnt && threadIdx.x == 0) liveCnt[r] = 0;  // k_segsort_small is not launched
     if (global ? n == 0 : n <= kMidSeg) return;  // global: every segment takes the scratch path (tests)
     __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
@@ -629,12 +646,13 @@ __device__ __forceinline__ MergeBuf merge_buf(uint64_t* scratch, uint64_t M, int
 __global__ void __launch_bounds__(kLargeThreads) k_chunk_sort(const mtb_match* __restrict__ in,
                                                               const uint64_t* __restrict__ mOff,
                                                               const uint2* __restrict__ chunks, uint64_t M,
-                                                              uint64_t* __restrict__ scratch, long chunk) {
+                                                              uint64_t* __restrict__ scratch, long chunk,
+                                                              const uint32_t* __restrict__ segLen) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint2 ck = chunks[blockIdx.x];  // (read, chunk start)
     const uint64_t base = mOff[ck.x];
-    const long n = (long)(mOff[ck.x + 1] - base);
+    const long n = seg_len(mOff, segLen, ck.x);
     const long cs = ck.y, len = min(chunk, n - cs);
     long p2 = 2;
     while (p2 < len) p2 <<= 1;
@@ -659,10 +677,11 @@ constexpr int kMergeTile = 256 * kMergePer;    // outputs per block
 // One tile of the merge of runs A = [ps, ps + w) and B = [ps + w, ps + 2w) (clipped to n) of a
 // segment, from buffer src into dst. tiles: (read, pair start, tile start).
 __global__ void __launch_bounds__(256) k_merge_tiles(const uint64_t* __restrict__ mOff, const uint4* __restrict__ tiles,
-                                                     uint64_t M, uint64_t* __restrict__ scratch, int src, long w) {
+                                                     uint64_t M, uint64_t* __restrict__ scratch, int src, long w,
+                                                     const uint32_t* __restrict__ segLen) {
     const uint4 t = tiles[blockIdx.x];
     const uint64_t base = mOff[t.x];
-    const long n = (long)(mOff[t.x + 1] - base);
+    const long n = seg_len(mOff, segLen, t.x);
     const long ps = t.y;
     const long na = min(w, n - ps), nb = max(0l, min(w, n - ps - w));
     const MergeBuf S = merge_buf(scratch, M, src), D = merge_buf(scratch, M, src ^ 1);
@@ -696,11 +715,12 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
                                                                 const uint32_t* __restrict__ reads, uint64_t M,
                                                                 uint64_t* __restrict__ scratch, int b,
                                                                 mtb_match* __restrict__ out,
-                                                                uint32_t* __restrict__ liveCnt, uint32_t pm) {
+                                                                uint32_t* __restrict__ liveCnt, uint32_t pm,
+                                                                const uint32_t* __restrict__ segLen) {
     __shared__ uint32_t sWave[kLargeThreads / 64 + 1];
     const uint32_t r = reads[blockIdx.x];
     const uint64_t base = mOff[r];
-    const long n = (long)(mOff[r + 1] - base);
+    const long n = seg_len(mOff, segLen, r);
     const MergeBuf S = merge_buf(scratch, M, b), T = merge_buf(scratch, M, b ^ 1);
     if (liveCnt) {
         uint32_t* rid = reinterpret_cast<uint32_t*>(T.l + base);
@@ -721,15 +741,24 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
 
 static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M,
                                     mtb_match* out, uint64_t* scratch, uint32_t* liveCnt, long chunk, uint32_t pm,
-                                    hipStream_t s) {
+                                    const uint32_t* segLen, hipStream_t s) {
     std::vector<uint64_t> off(nReads + 1);
+    std::vector<uint32_t> len;
     MTB_HIP_RET(hipMemcpyAsync(off.data(), mOff, sizeof(uint64_t) * (nReads + 1), hipMemcpyDeviceToHost, s));
+    if (segLen) {
+        len.resize(nReads);
+        MTB_HIP_RET(hipMemcpyAsync(len.data(), segLen, sizeof(uint32_t) * nReads, hipMemcpyDeviceToHost, s));
+    }
     MTB_HIP_RET(hipStreamSynchronize(s));
+    auto nOf = [&](uint32_t r) -> long {
+        if (!segLen) return (long)(off[r + 1] - off[r]);
+        return len[r] == kSegSkip ? -1 : (long)len[r];
+    };
     std::vector<uint32_t> big;
     std::vector<uint2> chunks;
     long maxN = 0;
     for (uint32_t r = 0; r < nReads; r++) {
-        const long n = (long)(off[r + 1] - off[r]);
+        const long n = nOf(r);
         if (n <= chunk) continue;
         big.push_back(r);
         maxN = std::max(maxN, n);
@@ -745,7 +774,7 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
     if (e == hipSuccess) e = hipMemcpyAsync(dChunks, chunks.data(), sizeof(uint2) * chunks.size(), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dBig, big.data(), sizeof(uint32_t) * big.size(), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk);
+        k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk, segLen);
         e = hipGetLastError();
     }
     int b = 0;
@@ -753,10 +782,10 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
     for (long w = chunk; e == hipSuccess && w < maxN; w *= 2) {
         tiles.clear();
         for (uint32_t r : big) {
-            const long n = (long)(off[r + 1] - off[r]);
+            const long n = nOf(r);
             for (long ps = 0; ps < n; ps += 2 * w) {
-                const long len = std::min(2 * w, n - ps);
-                for (long t = 0; t < len; t += kMergeTile) tiles.push_back(make_uint4(r, (uint32_t)ps, (uint32_t)t, 0));
+                const long len2 = std::min(2 * w, n - ps);
+                for (long t = 0; t < len2; t += kMergeTile) tiles.push_back(make_uint4(r, (uint32_t)ps, (uint32_t)t, 0));
             }
         }
         if (dTiles) hipFreeAsync(dTiles, s);
@@ -764,13 +793,14 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
         e = hipMallocAsync((void**)&dTiles, sizeof(uint4) * tiles.size(), s);
         if (e == hipSuccess) e = hipMemcpyAsync(dTiles, tiles.data(), sizeof(uint4) * tiles.size(), hipMemcpyHostToDevice, s);
         if (e != hipSuccess) break;
-        k_merge_tiles<<<(unsigned)tiles.size(), 256, 0, s>>>(mOff, dTiles, M, scratch, b, w);
+        k_merge_tiles<<<(unsigned)tiles.size(), 256, 0, s>>>(mOff, dTiles, M, scratch, b, w, segLen);
         e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host tile vector is reused
         b ^= 1;
     }
     if (e == hipSuccess) {
-        k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt, pm);
+        k_merge_finish<<<(unsigned)big.size(), kLargeThreads, 0, s>>>(in, mOff, dBig, M, scratch, b, out, liveCnt, pm,
+                                                                       segLen);
         e = hipGetLastError();
     }
     if (dTiles) hipFreeAsync(dTiles, s);
@@ -779,28 +809,121 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
     return e;
 }
 
+// Segments too big for one LDS sort (> chunk matches, long reads; ~75% of their matches are dead)
+// are thinned before they are sorted: one block per read counts the read's (species, frame) pairs
+// in an LDS hash indexed by the pair and flags species in a hash indexed by the species when a pair
+// reaches pm (collisions merge counters, so a dead match may survive but a live one never drops:
+// the sort kernels' exact pruning then runs on the survivors), and packs the survivors to the front
+// of the read's segment in place, staged through the (not yet written) output segment.
+// segLen[r] = survivors; reads at or below `chunk` get kSegSkip (sorted and pruned the usual way).
+constexpr int kThinLog = 14;  // 2^14 counters + 2^14 flags: 128 KB of LDS
+
+__global__ void __launch_bounds__(kLargeThreads) k_thin_big(mtb_match* __restrict__ io, mtb_match* __restrict__ stage,
+                                                            const uint64_t* __restrict__ mOff, uint32_t nReads,
+                                                            long chunk, uint32_t pm, uint32_t* __restrict__ segLen) {
+    __shared__ uint32_t cnt[1 << kThinLog], flag[1 << kThinLog];
+    __shared__ uint32_t sCount;
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = (long)(mOff[r + 1] - base);
+    if (n <= chunk) {
+        if (threadIdx.x == 0) segLen[r] = kSegSkip;
+        return;
+    }
+    constexpr uint32_t T = 1u << kThinLog;
+    for (uint32_t i = threadIdx.x; i < T; i += kLargeThreads) { cnt[i] = 0; flag[i] = 0; }
+    if (threadIdx.x == 0) sCount = 0;
+    __syncthreads();
+    auto pairSlot = [](const mtb_match& m) {
+        const uint64_t k = ((uint64_t)m.species_id << 3) | info_frame(m.qinfo);
+        return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - kThinLog));
+    };
+    auto spSlot = [](const mtb_match& m) {
+        return (uint32_t)(((uint64_t)m.species_id * 0xC2B2AE3D27D4EB4Full) >> (64 - kThinLog));
+    };
+    for (long i = threadIdx.x; i < n; i += kLargeThreads) atomicAdd(&cnt[pairSlot(io[base + i])], 1u);
+    __syncthreads();
+    for (long i = threadIdx.x; i < n; i += kLargeThreads) {
+        const mtb_match m = io[base + i];
+        if (cnt[pairSlot(m)] >= pm) flag[spSlot(m)] = 1;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (long i0 = 0; i0 < n; i0 += kLargeThreads) {  // survivors, one LDS atomic per wave
+        const long i = i0 + threadIdx.x;
+        mtb_match m;
+        bool keep = false;
+        if (i < n) {
+            m = io[base + i];
+            keep = flag[spSlot(m)] != 0;
+        }
+        const unsigned long long mk = __ballot(keep);
+        uint32_t at = 0;
+        if (lane == 0 && mk) at = atomicAdd(&sCount, (uint32_t)__popcll(mk));
+        at = __shfl(at, 0, 64);
+        if (keep) stage[base + at + (uint32_t)__popcll(mk & ((1ull << lane) - 1))] = m;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t surv = sCount;
+    for (long i = threadIdx.x; i < (long)surv; i += kLargeThreads) io[base + i] = stage[base + i];
+    if (threadIdx.x == 0) segLen[r] = surv;
+}
+
+__global__ void k_max_seg_len(const uint32_t* __restrict__ segLen, uint32_t n, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && segLen[i] != kSegSkip) atomicMax(out, segLen[i]);
+}
+
+// Sort (and, with liveCnt and no segLen, prune) the segments of the given lengths.
+static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
+                               uint64_t* gScratch, uint32_t maxSeg, uint32_t* liveCnt, long chunk, uint32_t pm,
+                               const uint32_t* segLen, hipStream_t s, const SegMatch* seg, const uint64_t* inOff,
+                               uint32_t inC) {
+    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
+    if (maxSeg > 128)
+        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
+    if (maxSeg > 256)
+        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
+    if (maxSeg > kSmallSeg)
+        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen);
+    if (maxSeg > kMidSeg)
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
+                                                         segLen);
+    MTB_HIP_RET(hipGetLastError());
+    if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, segLen, s);
+    return hipSuccess;
+}
+
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
-                          uint32_t pm, hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC) {
+                          uint32_t pm, hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC,
+                          uint32_t* segLen, uint32_t* maxTmp) {
     pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
     if (seg && (global || maxSeg > kSmallSeg)) return hipErrorInvalidValue;  // sparse input: register sorts only
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm);
+        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm,
+                                                         nullptr);
         return hipGetLastError();
     }
-    k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
-    if (maxSeg > 128)
-        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
-    if (maxSeg > 256)
-        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm);
-    if (maxSeg > kSmallSeg) k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm);
-    if (maxSeg > kMidSeg)
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm);
-    MTB_HIP_RET(hipGetLastError());
-    if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, s);
-    return hipSuccess;
+    if (!liveCnt || maxSeg <= (uint32_t)chunk || !segLen)
+        return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC);
+    // pruning with segments over one LDS sort: the others are sorted and pruned as usual; the big
+    // ones are thinned in place first (k_thin_big), then sorted and pruned on their survivors
+    MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)chunk, liveCnt, chunk, pm, nullptr, s, seg,
+                             inOff, inC));
+    mtb_match* io = const_cast<mtb_match*>(in);  // K5's input buffer: the caller's, free to overwrite
+    k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, chunk, pm, segLen);
+    MTB_HIP_RET(hipMemsetAsync(maxTmp, 0, sizeof(uint32_t), s));
+    k_max_seg_len<<<(nReads + 255) / 256, 256, 0, s>>>(segLen, nReads, maxTmp);
+    uint32_t maxSurv = 0;
+    MTB_HIP_RET(hipMemcpyAsync(&maxSurv, maxTmp, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MTB_HIP_RET(hipStreamSynchronize(s));
+    if (maxSurv == 0) return hipSuccess;
+    return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSurv, liveCnt, chunk, pm, segLen, s, nullptr, nullptr, 0);
 }
 
 // Live matches (front-packed in each sorted segment) into one dense array: a wave per read.
