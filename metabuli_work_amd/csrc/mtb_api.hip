@@ -474,10 +474,12 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     c->stats[11] = kM;
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(hipEventRecord(c->kev[12], s));
-    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
-    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mc + 1)));
-    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mc + 1) + 1)));
-    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Mc + 1) + n + Mc + 2)));
+    // K6 work lists: groups (<= matches) and the longest-first read order (n entries)
+    const uint64_t Mn = std::max<uint64_t>(Mc, n);
+    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mn + 1)));
+    HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mn + 1)));
+    HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mn + 1) + 1)));
+    HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Mn + 1) + n + Mn + 2)));
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
     AssignScratch sc{c->local.p,
                      c->paths.p,

@@ -1307,6 +1307,20 @@ __device__ __forceinline__ void trim_path(const mtb_match* __restrict__ M, Path&
     }
 }
 
+// trim_path with the end matches' rightEndHamming already at hand (rehS: p.sm's, rehE: p.em's)
+__device__ __forceinline__ void trim_path_reh(Path& p, const Path& c, int ol, uint32_t rehS, uint32_t rehE) {
+    const int range = ol / 3;
+    if (p.start < c.start) {
+        p.end = c.start - 1;
+        p.hd = max(0, p.hd - ham_fields(rehE, range, false));
+        p.score = p.score - score_fields(rehE, range, false) - (float)(ol % 3);
+    } else {
+        p.start = c.end + 1;
+        p.hd = max(0, p.hd - ham_fields(rehS, range, true));
+        p.score = p.score - score_fields(rehS, range, true) - (float)(ol % 3);
+    }
+}
+
 // combineMatchPaths (Taxonomer.cpp:410-468) on nP packed paths in global memory: the libstdc++
 // introsort emulation, then the greedy overlap pass. Returns the summed score.
 __device__ float combine_serial(const mtb_match* __restrict__ M, Path* Ps, long nP, Path* Cs) {
@@ -1398,10 +1412,13 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                                                      const uint32_t* __restrict__ qlen, AssignCfg cfg,
                                                      Path* __restrict__ P, Path* __restrict__ C,
                                                      float* __restrict__ spScore, uint8_t* __restrict__ spKeep,
-                                                     unsigned long long* __restrict__ stats) {
+                                                     unsigned long long* __restrict__ stats,
+                                                     const uint64_t* __restrict__ order) {
     __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
-    __shared__ uint32_t qsm[kWaveCombineMax], qem[kWaveCombineMax];
-    const uint64_t e = waveList[blockIdx.x];
+    // rightEndHamming of each sorted path's start / end match: a trim reads one (trimMatchPath), and
+    // a dependent global load per trim in the serial greedy pass would cost ~1 us each
+    __shared__ uint16_t qrs[kWaveCombineMax], qre[kWaveCombineMax];
+    const uint64_t e = waveList[order ? order[blockIdx.x] : blockIdx.x];  // largest runs first
     const uint64_t s = (uint32_t)e;
     const int nP = (int)(e >> 32);
     const uint64_t ss = sStart[s];
@@ -1469,7 +1486,9 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
         const int i = lane + 64 * t;
         if (i < nP) {
             const Path q = Ps[src[t]];
-            qs[i] = q.start; qe[i] = q.end; qsc[i] = q.score; qhd[i] = q.hd; qsm[i] = q.sm; qem[i] = q.em;
+            qs[i] = q.start; qe[i] = q.end; qsc[i] = q.score; qhd[i] = q.hd;
+            qrs[i] = M[q.sm].right_end_hamming;
+            qre[i] = M[q.em].right_end_hamming;
         }
     }
     __syncthreads();
@@ -1485,7 +1504,8 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
     int nC = 0;
     for (int pi = 0; pi < nP; pi++) {
         Path p;  // wave-uniform
-        p.start = qs[pi]; p.end = qe[pi]; p.score = qsc[pi]; p.hd = qhd[pi]; p.sm = qsm[pi]; p.em = qem[pi];
+        p.start = qs[pi]; p.end = qe[pi]; p.score = qsc[pi]; p.hd = qhd[pi]; p.sm = 0; p.em = 0;
+        const uint32_t rehS = qrs[pi], rehE = qre[pi];
         p.depth = 0;
         bool keep = true;
 #pragma unroll
@@ -1501,7 +1521,7 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                 if ((p.end < c.start) || (c.end < p.start)) continue;  // cleared by an earlier trim
                 const int ol = min(p.end, c.end) - max(p.start, c.start) + 1;
                 if (ol == p.end - p.start + 1) { keep = false; break; }
-                if (ol < 24) { trim_path(M, p, c, ol); continue; }
+                if (ol < 24) { trim_path_reh(p, c, ol, rehS, rehE); continue; }
                 keep = false;
             }
         }
@@ -1781,14 +1801,15 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
                                                           const uint8_t* __restrict__ spKeep, AssignCfg cfg,
                                                           TaxView tax, Clade* __restrict__ cladeP,
                                                           uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
-                                                          mtb_result* __restrict__ results) {
+                                                          mtb_result* __restrict__ results,
+                                                          const uint64_t* __restrict__ order) {
     __shared__ uint32_t qmin[kQuotLds];
     __shared__ int32_t qtax[kQuotLds];
     __shared__ int32_t hk[kTcHash];
     __shared__ uint32_t hc[kTcHash];
     __shared__ int sFlag;
-    const uint32_t r = blockIdx.x;
-    if (r >= nReads) return;
+    if (blockIdx.x >= nReads) return;
+    const uint32_t r = order ? (uint32_t)order[blockIdx.x] : blockIdx.x;  // reads with most matches first
     const int lane = threadIdx.x;
     const uint64_t base = mOff[r];
     const long n = (long)(mOff[r + 1] - base);
@@ -1943,6 +1964,24 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
     results[r] = res;
 }
 
+// Longest-first orders for the wave kernels (a wave kernel's time is otherwise set by its longest
+// waves, started last): keys = a size bound minus the size, a stable LSD radix sort of the indices.
+__global__ void k_wave_size_keys(const uint64_t* __restrict__ waveList, uint32_t n, uint64_t* __restrict__ keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = (uint64_t)(kWaveCombineMax - (uint32_t)(waveList[i] >> 32));
+}
+__global__ void k_read_size_keys(const uint64_t* __restrict__ mOff, uint32_t n, uint64_t* __restrict__ keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = 0xFFFFFFull - min<uint64_t>(mOff[i + 1] - mOff[i], 0xFFFFFFull);
+}
+
+static const uint64_t* longest_first(uint32_t n, int bits, const AssignScratch& s, hipStream_t st) {
+    bool inB = false;
+    radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, n, 0, bits, false, true, s.radixCounts, s.radixOffs,
+                     s.scanTmp, &inB, st);
+    return inB ? s.ordVB : s.ordVA;
+}
+
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
                    mtb_taxcnt* tcPool, mtb_result* results, unsigned long long* devStats, uint64_t* hostStats,
                    hipStream_t st) {
@@ -1985,9 +2024,12 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
             uint32_t nWave = 0;
             hipMemcpyAsync(&nWave, s.waveCount, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
             hipStreamSynchronize(st);
-            if (nWave)
+            if (nWave) {
+                k_wave_size_keys<<<(nWave + 255) / 256, 256, 0, st>>>(s.waveList, nWave, s.ordKA);
+                const uint64_t* order = longest_first(nWave, 16, s, st);
                 k_combine_wave<<<nWave, 64, 0, st>>>(matches, s.sStart, s.waveList, qlen, cfg, (Path*)s.paths,
-                                                     (Path*)s.comb, s.spScore, s.spKeep, devStats);
+                                                     (Path*)s.comb, s.spScore, s.spKeep, devStats, order);
+            }
             hostStats[3] = nWave;
         }
     } else {
@@ -1997,9 +2039,11 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     // thread per read would leave most SIMDs idle and serialise each read's best-species scan)
     const bool wave = a.waveTaxon >= 0 ? a.waveTaxon == 1 : (!a.generic && nM > (uint64_t)kWavePerReadMatches * nReads);
     if (wave) {
+        k_read_size_keys<<<(nReads + 255) / 256, 256, 0, st>>>(mOff, nReads, s.ordKA);
+        const uint64_t* order = longest_first(nReads, 24, s, st);
         k_choose_taxon_wave<<<nReads, 64, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart, s.gScan, s.gStart,
                                                    s.spScore, s.spKeep, cfg, tv, (Clade*)s.clade, s.cladePerMatch,
-                                                   tcPool, results);
+                                                   tcPool, results, order);
     } else {
         const unsigned ctT = nReads < 256u * 256u ? 64u : 256u;
         k_choose_taxon<<<(nReads + ctT - 1) / ctT, ctT, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
