@@ -77,6 +77,7 @@ struct mtb_ctx {
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
     int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1: K6 chooseBestTaxon thread / wave per read (tests; default auto)
+    int emulateAll = 0;          // MTB_EMULATE_SORT=1: k_combine_wave emulates std::sort for every run (tests)
     bool pruneCompact = true;    // MTB_PRUNE_COMPACT=0: big K5 segments are not thinned before their sort (tests)
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
@@ -240,6 +241,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
+    if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
@@ -409,6 +411,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     AssignArgs a = assign_args(c->par);
     a.generic = c->forceGeneric ? 1 : 0;
     a.waveTaxon = c->waveTaxon;
+    a.emulateAll = c->emulateAll;
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     const uint64_t Mc = std::max<uint64_t>(M, 1);

@@ -909,14 +909,17 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
                                                          nullptr);
         return hipGetLastError();
     }
-    if (!liveCnt || maxSeg <= (uint32_t)chunk || !segLen)
+    // segments over thinAbove matches are thinned first when pruning (most of a long read's matches
+    // are dead: sorting the survivors, mostly within one 2048-entry LDS tile, beats sorting all)
+    const long thinAbove = std::min<long>(chunk, kMidSeg);
+    if (!liveCnt || maxSeg <= (uint32_t)thinAbove || !segLen)
         return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC);
-    // pruning with segments over one LDS sort: the others are sorted and pruned as usual; the big
-    // ones are thinned in place first (k_thin_big), then sorted and pruned on their survivors
-    MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)chunk, liveCnt, chunk, pm, nullptr, s, seg,
-                             inOff, inC));
+    // the others are sorted and pruned as usual; the big ones are thinned in place first
+    // (k_thin_big), then sorted and pruned on their survivors
+    MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)thinAbove, liveCnt, chunk, pm, nullptr, s,
+                             seg, inOff, inC));
     mtb_match* io = const_cast<mtb_match*>(in);  // K5's input buffer: the caller's, free to overwrite
-    k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, chunk, pm, segLen);
+    k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, thinAbove, pm, segLen);
     MTB_HIP_RET(hipMemsetAsync(maxTmp, 0, sizeof(uint32_t), s));
     k_max_seg_len<<<(nReads + 255) / 256, 256, 0, s>>>(segLen, nReads, maxTmp);
     uint32_t maxSurv = 0;
@@ -995,6 +998,7 @@ struct AssignCfg {
     int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
     float minScore, minSpScore, tieRatio;
     int generic;  // 1: skip the register fast path (tests)
+    int emulateAll;  // 1: k_combine_wave takes the std::sort emulation for every run (tests)
 };
 
 struct Clade {
@@ -1414,7 +1418,9 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
                                                      float* __restrict__ spScore, uint8_t* __restrict__ spKeep,
                                                      unsigned long long* __restrict__ stats,
                                                      const uint64_t* __restrict__ order) {
-    __shared__ uint64_t kh[kWaveCombineMax], kl[kWaveCombineMax];
+    __shared__ uint64_t kbuf[2 * kWaveCombineMax];  // sort keys (kh, kl), or the emulation's compact keys
+    uint64_t* kh = kbuf;
+    uint64_t* kl = kbuf + kWaveCombineMax;
     // rightEndHamming of each sorted path's start / end match: a trim reads one (trimMatchPath), and
     // a dependent global load per trim in the serial greedy pass would cost ~1 us each
     __shared__ uint16_t qrs[kWaveCombineMax], qre[kWaveCombineMax];
@@ -1462,19 +1468,40 @@ __global__ void __launch_bounds__(64) k_combine_wave(const mtb_match* __restrict
         tie |= a.end != b.end || M[a.sm].right_end_hamming != M[b.sm].right_end_hamming ||
                M[a.em].right_end_hamming != M[b.em].right_end_hamming;
     }
-    if (__syncthreads_or(tie)) {  // the order of tied paths is whatever libstdc++'s introsort leaves
+    // The order of tied paths is whatever libstdc++'s introsort leaves: emulated (mtb_stdsort.h) on
+    // lane 0 over compact keys in LDS, from the paths' original order, in place of the bitonic
+    // result; the greedy pass below is the same either way.
+    struct EmuKey {
+        float score;
+        int hd, start;
+        uint32_t idx;
+    };
+    static_assert(sizeof(EmuKey) * kWaveCombineMax == sizeof(uint64_t) * 2 * kWaveCombineMax, "emulation keys fit");
+    EmuKey* K = reinterpret_cast<EmuKey*>(kbuf);
+    const bool emulate = __syncthreads_or(tie || cfg.emulateAll);
+    if (emulate) {
         if (lane == 0) atomicAdd(&stats[1], 1ull);
-        if (lane == 0) species_score(combine_serial(M, P + ss, nP, C + ss), readLength, cfg, spScore, spKeep, s);
-        return;
+        for (int i = lane; i < nP; i += 64) {
+            const Path q = Ps[i];
+            K[i] = EmuKey{q.score, q.hd, q.start, (uint32_t)i};
+        }
+        __syncthreads();
+        if (lane == 0)
+            stdsort::sort(K, K + nP, [](const EmuKey& a, const EmuKey& b) {
+                if (a.score != b.score) return a.score > b.score;
+                if (a.hd != b.hd) return a.hd < b.hd;
+                return a.start > b.start;
+            });
+        __syncthreads();
     }
-    // the paths themselves, in sorted order, into LDS (over the dead key arrays, plus sm/em) so the
-    // sequential pass below reads no global memory but for the rare trims
+    // the paths themselves, in sorted order, into LDS (over the dead key arrays, plus the end
+    // matches' rightEndHamming) so the sequential pass below reads no global memory
     constexpr int kPerLane = kWaveCombineMax / 64;
     uint32_t src[kPerLane];
 #pragma unroll
     for (int t = 0; t < kPerLane; t++) {
         const int i = lane + 64 * t;
-        src[t] = i < nP ? (uint32_t)kl[i] : 0u;
+        src[t] = i < nP ? (emulate ? K[i].idx : (uint32_t)kl[i]) : 0u;
     }
     __syncthreads();
     int* qs = reinterpret_cast<int*>(kh);
@@ -1988,7 +2015,7 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     for (int i = 0; i < 4; i++) hostStats[i] = 0;
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
-                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic};
+                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic, a.emulateAll};
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
     if (nM) {
         const unsigned bm = (unsigned)((nM + 255) / 256);

@@ -34,6 +34,7 @@ struct AssignArgs {
     float minScore, minSpScore, tieRatio;
     int generic;  // MTB_FORCE_GENERIC: general code paths only (parity tests of the fallbacks)
     int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread per read, 1 wave per read (K6 chooseBestTaxon)
+    int emulateAll = 0;  // MTB_EMULATE_SORT=1: every k_combine_wave run takes the std::sort emulation (tests)
 };
 
 struct AssignScratch {  // per match unless noted

@@ -249,12 +249,16 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
 
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt1", "long"),
                                           ("fmt2_syncmer", "long"), ("fmt2_syncmer", "paired")])
-@pytest.mark.parametrize("wave", ["0", "1"])
+@pytest.mark.parametrize("wave", ["0", "1", "1:emu"])
 def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
     """K6's chooseBestTaxon both ways — a thread per read (short reads) and a wave per read (long
     reads: parallel species scan, per-quotient LDS reduction for filterRedundantMatches) — forced
-    on every read kind with MTB_WAVE_TAXON, against the oracle."""
+    on every read kind with MTB_WAVE_TAXON, against the oracle; and k_combine_wave's libstdc++
+    introsort emulation forced for every run it takes (MTB_EMULATE_SORT)."""
+    wave, _, emu = wave.partition(":")
     monkeypatch.setenv("MTB_WAVE_TAXON", wave)
+    # every multi-path species run through k_combine_wave's std::sort emulation (tied paths)
+    monkeypatch.setenv("MTB_EMULATE_SORT", "1" if emu else "0")
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])
     odb = oc.OracleDb(db_dir)
