@@ -415,18 +415,6 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));
     const uint64_t Mc = std::max<uint64_t>(M, 1);
-    HIP_TRY(c->local.ensure(path_bytes() * Mc));
-    HIP_TRY(c->paths.ensure(path_bytes() * Mc));
-    HIP_TRY(c->comb.ensure(path_bytes() * Mc));
-    HIP_TRY(c->conn.ensure(Mc));
-    HIP_TRY(c->spScore.ensure(sizeof(float) * Mc));
-    HIP_TRY(c->spKeep.ensure(Mc));
-    HIP_TRY(c->waveList.ensure(sizeof(uint64_t) * Mc));
-    HIP_TRY(c->waveCount.ensure(sizeof(uint32_t)));
-    for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Mc + 1)));
-    for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mc + 1)));
-    HIP_TRY(c->clade.ensure(clade_bytes() * Mc * c->cladePerMatch));
-    HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Mc));
     HIP_TRY(c->results.ensure(sizeof(mtb_result) * std::max<uint32_t>(n, 1)));
     // K5: per-read segmented sort into compareMatches order
     HIP_TRY(c->matchesSorted.ensure(sizeof(mtb_match) * Mc));
@@ -475,10 +463,24 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     }
     c->liveM = kM;
     c->stats[11] = kM;
+    // K6 scratch, per match K6 reads: sized by the live matches (less than half of all at GTDB scale)
+    const uint64_t Kc = std::max<uint64_t>(kM, 1);
+    HIP_TRY(c->local.ensure(path_bytes() * Kc));
+    HIP_TRY(c->paths.ensure(path_bytes() * Kc));
+    HIP_TRY(c->comb.ensure(path_bytes() * Kc));
+    HIP_TRY(c->conn.ensure(Kc));
+    HIP_TRY(c->spScore.ensure(sizeof(float) * Kc));
+    HIP_TRY(c->spKeep.ensure(Kc));
+    HIP_TRY(c->waveList.ensure(sizeof(uint64_t) * Kc));
+    HIP_TRY(c->waveCount.ensure(sizeof(uint32_t)));
+    for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Kc + 1)));
+    for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Kc + 1)));
+    HIP_TRY(c->clade.ensure(clade_bytes() * Kc * c->cladePerMatch));
+    HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Kc));
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(hipEventRecord(c->kev[12], s));
-    // K6 work lists: groups (<= matches) and the longest-first read order (n entries)
-    const uint64_t Mn = std::max<uint64_t>(Mc, n);
+    // K6 work lists: groups (<= live matches) and the longest-first read order (n entries)
+    const uint64_t Mn = std::max<uint64_t>(Kc, n);
     for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mn + 1)));
     HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mn + 1)));
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mn + 1) + 1)));

@@ -2,10 +2,11 @@
 // the flat buffers mtb_classify_batch takes, and the per-read classification TSV writer.
 //
 // Reader: replaces QueryIndexer's counting pass plus KmerExtractor::loadChunkOfReads'
-// serial kseq loop (QueryIndexer.cpp:30-147, KmerExtractor.cpp:442-494): one streaming pass,
-// zlib's gzread (which also passes plain files through) into a large buffer, records split with
-// memchr, names cut at the first whitespace as kseq does. Mates are read in lock-step; unequal
-// read counts are an error, as in QueryIndexer.cpp:121-124.
+// serial kseq loop (QueryIndexer.cpp:30-147, KmerExtractor.cpp:442-494): one streaming pass over
+// a decompressed byte source (mtb_source.cpp: plain / gzip / BGZF inflated by a worker pool, read
+// ahead on a thread of its own), records split with memchr with kseq's semantics (names cut at the
+// first whitespace, wrapped FASTA and FASTQ). Mates are read in lock-step; unequal read counts are
+// an error, as in QueryIndexer.cpp:121-124. The threaded classify pipeline is mtb_pipeline.cpp.
 //
 // Writer: Reporter::writeReadClassification (Reporter.cpp:38-83), formatted by several threads
 // into per-thread strings and written in read order. Scores print as ostream << float (%g).
@@ -19,81 +20,73 @@
 #include <vector>
 
 #include "mtb_host.h"
+#include "mtb_io.h"
 
-namespace {
+namespace mtb {
 
-struct FastxStream {
-    gzFile f = nullptr;
-    std::vector<char> buf;  // unread bytes live in [pos, end)
-    size_t pos = 0, end = 0;
-    bool eof = false;
-    char kind = 0;  // '>' FASTA, '@' FASTQ
+bool FastxStream::open(const std::string& path, int threads, bool prefetch) {
+    src = open_source(path, threads, prefetch, err);
+    if (!src) return false;
+    buf.resize(64u << 20);
+    return true;
+}
 
-    bool open(const char* path) {
-        f = gzopen(path, "rb");
-        if (!f) return false;
-        gzbuffer(f, 1 << 20);
-        buf.resize(64u << 20);
-        return true;
+// Make at least `want` bytes available from pos (or everything left). Returns bytes available.
+size_t FastxStream::fill(size_t want) {
+    if (end - pos >= want || eof) return end - pos;
+    if (pos > 0) {
+        memmove(buf.data(), buf.data() + pos, end - pos);
+        end -= pos;
+        pos = 0;
     }
-    void close() {
-        if (f) gzclose(f);
-        f = nullptr;
-    }
-    // Make at least `want` bytes available from pos (or everything left). Returns bytes available.
-    size_t fill(size_t want) {
-        if (end - pos >= want || eof) return end - pos;
-        if (pos > 0) {
-            memmove(buf.data(), buf.data() + pos, end - pos);
-            end -= pos;
-            pos = 0;
+    if (buf.size() < want + (1u << 20)) buf.resize(want + (1u << 20));
+    while (end < buf.size() && !eof) {
+        const long got = src->read(buf.data() + end, std::min<size_t>(buf.size() - end, 1u << 30));
+        if (got < 0) err = src->err;
+        if (got <= 0) {
+            eof = true;
+            break;
         }
-        if (buf.size() < want + (1u << 20)) buf.resize(want + (1u << 20));
-        while (end < buf.size() && !eof) {
-            int got = gzread(f, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, 1u << 30));
-            if (got <= 0) {
-                eof = true;
-                break;
-            }
-            end += (size_t)got;
-            if (end - pos >= want) break;
-        }
-        return end - pos;
+        end += (size_t)got;
+        if (end - pos >= want) break;
     }
-    // Next line (without '\n' / '\r'); false at end of input.
-    bool line(const char*& p, size_t& n) {
-        for (size_t want = 1u << 16;; want *= 2) {
-            size_t avail = fill(want);
-            if (avail == 0) return false;
-            const char* s = buf.data() + pos;
-            const char* nl = (const char*)memchr(s, '\n', avail);
-            if (nl || eof) {
-                size_t len = nl ? (size_t)(nl - s) : avail;
-                pos += len + (nl ? 1 : 0);
-                if (len && s[len - 1] == '\r') len--;
-                p = s;
-                n = len;
-                return true;
-            }
-            if (avail < want) return false;
-        }
-    }
-    int peek() {
-        if (fill(1) == 0) return -1;
-        return (unsigned char)buf[pos];
-    }
-};
+    return end - pos;
+}
 
-// One record appended to (seq, names); false at end of input. Throws nothing: malformed input
-// sets err.
+// Next line (without '\n' / '\r'); false at end of input.
+bool FastxStream::line(const char*& p, size_t& n) {
+    for (size_t want = 1u << 16;; want *= 2) {
+        const size_t avail = fill(want);
+        if (avail == 0) return false;
+        const char* s = buf.data() + pos;
+        const char* nl = (const char*)memchr(s, '\n', avail);
+        if (nl || eof) {
+            size_t len = nl ? (size_t)(nl - s) : avail;
+            pos += len + (nl ? 1 : 0);
+            if (len && s[len - 1] == '\r') len--;
+            p = s;
+            n = len;
+            return true;
+        }
+        if (avail < want) return false;
+    }
+}
+
+int FastxStream::peek() {
+    if (fill(1) == 0) return -1;
+    return (unsigned char)buf[pos];
+}
+
 bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, std::string& names,
                  std::vector<uint64_t>& noff, std::string& err) {
     const char* p;
     size_t n;
-    // skip blank lines before a header
-    while (true) {
-        int c = s.peek();
-        if (c < 0) return false;
+    while (true) {  // skip blank lines before a header
+        const int c = s.peek();
+        if (c < 0) {
+            if (!s.err.empty()) err = s.err;
+            return false;
+        }
         if (c == '\n' || c == '\r') {
             s.line(p, n);
             continue;
@@ -105,36 +98,56 @@ bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, s
         err = "not a FASTA/FASTQ record header";
         return false;
     }
-    if (!s.kind) s.kind = p[0];
+    const bool fastq = p[0] == '@';
     size_t nameLen = 1;
     while (nameLen < n && p[nameLen] != ' ' && p[nameLen] != '\t') nameLen++;
     names.append(p + 1, nameLen - 1);
     noff.push_back(names.size());
-    if (s.kind == '@') {
-        if (!s.line(p, n)) {
+    const size_t seqStart = seq.size();
+    if (fastq) {  // sequence lines up to the '+' line, then quality lines until as long (kseq)
+        bool plus = false;
+        while (s.line(p, n)) {
+            if (n && p[0] == '+') {
+                plus = true;
+                break;
+            }
+            seq.append(p, n);
+        }
+        if (!plus) {
             err = "truncated FASTQ record";
             return false;
         }
-        seq.append(p, n);
-        const char* q;
-        size_t qn;
-        if (!s.line(q, qn) || qn == 0 || q[0] != '+' || !s.line(q, qn)) {
-            err = "truncated FASTQ record";
-            return false;
+        const size_t slen = seq.size() - seqStart;
+        size_t qlen = 0;
+        while (qlen < slen) {
+            if (!s.line(p, n)) {
+                err = "truncated FASTQ record";
+                return false;
+            }
+            qlen += n;
         }
     } else {
         while (true) {
-            int c = s.peek();
+            const int c = s.peek();
             if (c < 0 || c == '>') break;
             s.line(p, n);
             seq.append(p, n);
         }
     }
+    if (!s.err.empty()) {
+        err = s.err;
+        return false;
+    }
     off.push_back(seq.size());
     return true;
 }
 
-}  // namespace
+}  // namespace mtb
+
+using mtb::FastxStream;
+using mtb::next_record;
+
+static constexpr int kReaderThreads = 4;  // BGZF inflate workers per file
 
 struct mtb_reader {
     FastxStream a, b;
@@ -148,16 +161,15 @@ extern "C" {
 int mtb_reader_open(const char* path1, const char* path2, mtb_reader** out) {
     if (!path1 || !out) return MTB_ERR_ARG;
     mtb_reader* r = new mtb_reader();
-    if (!r->a.open(path1)) {
-        mtb::set_error(std::string("cannot open ") + path1);
+    if (!r->a.open(path1, kReaderThreads, true)) {
+        mtb::set_error(r->a.err);
         delete r;
         return MTB_ERR_IO;
     }
     if (path2) {
         r->paired = true;
-        if (!r->b.open(path2)) {
-            mtb::set_error(std::string("cannot open ") + path2);
-            r->a.close();
+        if (!r->b.open(path2, kReaderThreads, true)) {
+            mtb::set_error(r->b.err);
             delete r;
             return MTB_ERR_IO;
         }
@@ -207,12 +219,7 @@ int mtb_reader_next(mtb_reader* r, uint32_t max_reads, uint64_t max_bases, mtb_r
     return MTB_OK;
 }
 
-void mtb_reader_close(mtb_reader* r) {
-    if (!r) return;
-    r->a.close();
-    r->b.close();
-    delete r;
-}
+void mtb_reader_close(mtb_reader* r) { delete r; }
 
 int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
                               const mtb_result* res, const mtb_taxcnt* taxcnt, uint32_t flags) {

@@ -1,0 +1,47 @@
+// Host input around the device path: decompressed byte sources for FASTA/FASTQ
+// files (plain, gzip, or BGZF with its blocks inflated by a thread pool) and the record parser with
+// kseq's semantics, shared by the synchronous reader (mtb_reader_*) and the threaded pipeline
+// (mtb_start_classify, mtb_pipeline.cpp).
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace mtb {
+
+// Decompressed bytes of one input file, in order.
+struct ByteSource {
+    virtual ~ByteSource() {}
+    // Up to cap bytes into dst; 0 at end of input, -1 on error (err set).
+    virtual long read(char* dst, size_t cap) = 0;
+    std::string err;
+};
+
+// Plain files pass through; gzip (one or several members) inflates on one thread; BGZF (gzip
+// members carrying their block size in a "BC" extra field, as bgzip writes them) inflates up to
+// `threads` blocks at once. With prefetch, a thread of its own keeps the next chunks ready.
+std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bool prefetch, std::string& err);
+
+// Buffered line access over a ByteSource.
+struct FastxStream {
+    std::unique_ptr<ByteSource> src;
+    std::vector<char> buf;  // unread bytes live in [pos, end)
+    size_t pos = 0, end = 0;
+    bool eof = false;
+    std::string err;
+    bool open(const std::string& path, int threads, bool prefetch);
+    size_t fill(size_t want);
+    bool line(const char*& p, size_t& n);
+    int peek();
+};
+
+// One record appended to (seq, off) and (names, noff): kseq semantics — the name is the header up
+// to the first space or tab; FASTA sequence lines run to the next '>' header; FASTQ sequence lines
+// run to the '+' line, and quality lines follow until they are as long as the sequence (wrapped
+// records). false at the end of the input, or with err set on malformed input.
+bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, std::string& names,
+                 std::vector<uint64_t>& noff, std::string& err);
+
+}  // namespace mtb

@@ -1447,7 +1447,12 @@ void launch_probe(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* q
 }
 
 bool unstaged_join(bool lines, uint64_t D, uint64_t Q, uint32_t winCap) {
-    return lines && (D > (uint64_t)kStageFreeRatio * Q || winCap == 0);
+    // MTB_STAGE_FREE_RATIO (experiments): the D / Q ratio above which K4 goes unstaged
+    static const uint64_t ratio = [] {
+        const char* e = getenv("MTB_STAGE_FREE_RATIO");
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)kStageFreeRatio;
+    }();
+    return lines && (D > ratio * Q || winCap == 0);
 }
 
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }

@@ -395,3 +395,69 @@ def write_taxonomy_db(taxo: Taxonomy, path: str, internal2org: Optional[np.ndarr
         f.write(np.array([len(blob), len(enc), len(enc)], np.uint32).tobytes())
         f.write(blob)
         f.write(offs.tobytes())
+
+
+# ---- FASTQ files of synthetic reads (tests, end-to-end bench) ------------------------------------
+def fastq_bytes(seq: np.ndarray, off: np.ndarray, prefix: str = "r", qual: int = ord("I")) -> bytes:
+    """FASTQ text of reads (seq, off): "@<prefix><9-digit index>" headers, one sequence and one
+    quality line each. Vectorised for fixed-length reads, a loop otherwise."""
+    n = len(off) - 1
+    lens = np.diff(off.astype(np.int64))
+    if n and (lens == lens[0]).all():
+        L = int(lens[0])
+        hl = 1 + len(prefix) + 9 + 1
+        rec = hl + (L + 1) + 2 + (L + 1)
+        out = np.empty((n, rec), np.uint8)
+        out[:, 0] = ord("@")
+        out[:, 1:1 + len(prefix)] = np.frombuffer(prefix.encode(), np.uint8)
+        idx = np.arange(n, dtype=np.int64)
+        for k in range(9):
+            out[:, 1 + len(prefix) + k] = ord("0") + (idx // 10 ** (8 - k)) % 10
+        out[:, hl - 1] = ord("\n")
+        out[:, hl:hl + L] = seq[:n * L].reshape(n, L)
+        out[:, hl + L] = ord("\n")
+        out[:, hl + L + 1] = ord("+")
+        out[:, hl + L + 2] = ord("\n")
+        out[:, hl + L + 3:hl + 2 * L + 3] = qual
+        out[:, rec - 1] = ord("\n")
+        return out.tobytes()
+    parts = []
+    for i in range(n):
+        s = bytes(seq[int(off[i]):int(off[i + 1])])
+        parts.append(b"@%s%09d\n%s\n+\n%s\n" % (prefix.encode(), i, s, bytes([qual]) * len(s)))
+    return b"".join(parts)
+
+
+def _bgzf_block(data: bytes, level: int) -> bytes:
+    import struct
+    import zlib
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    cdata = c.compress(data) + c.flush()
+    bsize = 18 + len(cdata) + 8 - 1
+    hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", bsize)
+    return hdr + cdata + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data))
+
+
+def write_compressed(path: str, data: bytes, mode: str = "bgzf", level: int = 1, threads: int = 16) -> None:
+    """data to path: mode "plain", "gzip" (one member) or "bgzf" (64 KB members with their size in a
+    BC extra field, as bgzip writes; compressed by a thread pool: zlib releases the GIL)."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    if mode == "plain":
+        with open(path, "wb") as f:
+            f.write(data)
+        return
+    if mode == "gzip":
+        with open(path, "wb") as f:
+            c = zlib.compressobj(level, zlib.DEFLATED, 31)
+            mv = memoryview(data)
+            for i in range(0, len(data), 1 << 24):
+                f.write(c.compress(mv[i:i + (1 << 24)]))
+            f.write(c.flush())
+        return
+    blk = 65280
+    mv = memoryview(data)
+    with ThreadPoolExecutor(threads) as ex, open(path, "wb") as f:
+        for part in ex.map(lambda i: _bgzf_block(bytes(mv[i:i + blk]), level), range(0, len(data), blk)):
+            f.write(part)
+        f.write(_bgzf_block(b"", level))  # the BGZF end-of-file marker block

@@ -83,6 +83,42 @@ def test_fasta_multiline(tmp_path, reads):
     assert got_names == names and g1 == seqs and g2 == []
 
 
+def test_fastq_wrapped(tmp_path, reads):
+    """Wrapped FASTQ (sequence and quality split over several lines, as kseq accepts) reads the same
+    as one-line records."""
+    names = [f"w{i}" for i in range(reads.n)]
+    seqs = _mates(reads, 1)
+    p = str(tmp_path / "wrapped.fq")
+    with open(p, "w") as f:
+        for nm, sq in zip(names, seqs):
+            s = sq.decode()
+            f.write(f"@{nm} x\n" + "".join(s[i:i + 37] + "\n" for i in range(0, len(s), 37)) + "+\n" +
+                    "".join("I" * len(s[i:i + 41]) + "\n" for i in range(0, len(s), 41)))
+    got_names, g1, _ = _read_all(p, None, 257)
+    assert got_names == names and g1 == seqs
+
+
+@pytest.mark.parametrize("mode", ["plain", "gzip", "bgzf", "multi"])
+def test_compression_modes(tmp_path, reads, mode):
+    """Plain, single-member gzip, BGZF (blocks inflated by a worker pool) and multi-member gzip
+    inputs give the same records, for both mates."""
+    data1 = synth.fastq_bytes(reads.seq1, reads.off1)
+    data2 = synth.fastq_bytes(reads.seq2, reads.off2)
+    p1, p2 = str(tmp_path / "a.fq"), str(tmp_path / "b.fq")
+    if mode == "multi":  # two gzip members back to back
+        cut = len(data1) // 2
+        cut = data1.index(b"\n@", cut) + 1
+        with open(p1, "wb") as f:
+            f.write(gzip.compress(data1[:cut]) + gzip.compress(data1[cut:]))
+        synth.write_compressed(p2, data2, "gzip")
+    else:
+        synth.write_compressed(p1, data1, mode)
+        synth.write_compressed(p2, data2, mode)
+    names, g1, g2 = _read_all(p1, p2, 300)
+    assert names == [f"r{i:09d}" for i in range(reads.n)]
+    assert g1 == _mates(reads, 1) and g2 == _mates(reads, 2)
+
+
 def test_reader_errors(tmp_path, reads):
     names = [f"r{i}" for i in range(10)]
     seqs = _mates(reads, 1)[:10]
