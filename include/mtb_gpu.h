@@ -316,6 +316,33 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
 int mtb_write_report(const mtb_ctx* ctx, const char* path, uint64_t total_reads, const int32_t* tax_ids,
                      const uint32_t* counts, uint64_t n);
 
+/* ---- Classifier::startClassify over files ----------------------------------- */
+/* Classifier.cpp:44-164 as a threaded native pipeline: per mate file a reader (BGZF blocks inflated
+ * by a worker pool; gzip and plain files read ahead) and a parser; an assembler filling pinned
+ * batches of <= max_reads reads and <= max_bases bases (the reference's RAM-bounded QuerySplits,
+ * QueryIndexer.cpp:62-67,132-137) and uploading each on a copy stream; mtb_classify_batch on the
+ * calling thread; a writer emitting the per-read TSV (Reporter.cpp:38-83) while the next batch runs.
+ * With report_tsv, the per-taxon report of the run (Classifier.cpp:149). */
+typedef struct mtb_classify_opts {
+    const char* query1;       /* FASTA/FASTQ, plain or gzip (BGZF inflates in parallel)        */
+    const char* query2;       /* mate 2 (seq_mode 2), else NULL                                 */
+    const char* out_tsv;      /* per-read classifications                                       */
+    const char* report_tsv;   /* per-taxon report, or NULL                                      */
+    uint32_t max_reads;       /* reads per batch (0: 1,000,000)                                 */
+    uint32_t write_flags;     /* MTB_WRITE_LINEAGE                                              */
+    uint64_t max_bases;       /* bases per batch, both mates (0: from free HBM, < 2^30)         */
+    int32_t threads;          /* host threads for inflating (0: min(16, cores))                 */
+    int32_t reserved;
+} mtb_classify_opts;
+typedef struct mtb_classify_stats {
+    uint64_t reads, bases, batches;
+    double wall_s;            /* whole run                                                      */
+    double gpu_s;             /* mtb_classify_batch calls                                       */
+    double input_wait_s;      /* the GPU stage waiting for a parsed, uploaded batch             */
+    double write_s;           /* TSV formatting and writing (overlapped with the GPU stage)     */
+} mtb_classify_stats;
+int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

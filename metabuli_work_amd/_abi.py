@@ -100,3 +100,15 @@ class MtbReadBatch(ctypes.Structure):
         ("names", ctypes.c_void_p),
         ("name_off", ctypes.POINTER(ctypes.c_uint64)),
     ]
+
+
+class MtbClassifyOpts(ctypes.Structure):
+    _fields_ = [("query1", ctypes.c_char_p), ("query2", ctypes.c_char_p), ("out_tsv", ctypes.c_char_p),
+                ("report_tsv", ctypes.c_char_p), ("max_reads", ctypes.c_uint32), ("write_flags", ctypes.c_uint32),
+                ("max_bases", ctypes.c_uint64), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class MtbClassifyStats(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_uint64), ("bases", ctypes.c_uint64), ("batches", ctypes.c_uint64),
+                ("wall_s", ctypes.c_double), ("gpu_s", ctypes.c_double), ("input_wait_s", ctypes.c_double),
+                ("write_s", ctypes.c_double)]

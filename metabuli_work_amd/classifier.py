@@ -280,43 +280,24 @@ class Classifier:
         check(lib().mtb_write_report(self.handle, path.encode(), total_reads, ptr(ids), ptr(cnt), len(ids)),
               "mtb_write_report")
 
-    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None) -> int:
-        """Classifier::startClassify (Classifier.cpp:44-164): batches from the native FASTA/FASTQ(.gz)
-        reader (mtb_reader_*), one mtb_classify_batch each, TSV lines by mtb_write_classifications;
-        with report_tsv, the per-taxon report of the run (mtb_write_report, Classifier.cpp:149)."""
+    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None,
+                      max_bases: int = 0, threads: int = 0) -> int:
+        """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
+        (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
+        reads_per_batch reads and max_bases bases (0: sized from free HBM, the reference's
+        RAM-bounded QuerySplits) uploaded on a copy stream, mtb_classify_batch, and the TSV writer
+        (+ the per-taxon report, Classifier.cpp:149) overlapping each other. Returns the reads
+        classified; the run's timings are left in self.last_run."""
         par = self.par
-        q1 = par.filenames[0]
-        q2 = par.filenames[1] if par.seqMode == 2 else None
-        total = 0
-        first = True
-        tax_counts: dict = {}
-        with FastxReader(q1, q2) as rd:
-            while True:
-                b = rd.next(reads_per_batch)
-                if b.n_reads == 0:
-                    break
-                n = b.n_reads
-                res = np.zeros(n, RESULT_DTYPE)
-                check(lib().mtb_classify_batch(self.handle, b.seq1, b.off1, b.seq2, b.off2, n, 0, ptr(res)),
-                      "mtb_classify_batch")
-                tc = self.taxcnt()
-                check(lib().mtb_write_classifications(self.handle, out_tsv.encode(), 0 if first else 1,
-                                                      ctypes.byref(b), ptr(res), ptr(tc),
-                                                      _abi.MTB_WRITE_LINEAGE if par.printLineage else 0),
-                      "mtb_write_classifications")
-                first = False
-                total += n
-                cls, cnt = np.unique(np.where(res["is_classified"] != 0, res["classification"], 0),
-                                     return_counts=True)
-                for t, k in zip(cls.tolist(), cnt.tolist()):
-                    tax_counts[t] = tax_counts.get(t, 0) + k
-        if first:  # no reads: header only
-            with open(out_tsv, "w") as out:
-                out.write("#is_classified\tname\ttaxID\tquery_length\tscore\trank" +
-                          ("\tlineage" if par.printLineage else "") + "\ttaxID:match_count\n")
-        if report_tsv is not None:
-            self.write_report(report_tsv, total, tax_counts)
-        return total
+        opts = _abi.MtbClassifyOpts(
+            query1=par.filenames[0].encode(), query2=par.filenames[1].encode() if par.seqMode == 2 else None,
+            out_tsv=out_tsv.encode(), report_tsv=report_tsv.encode() if report_tsv else None,
+            max_reads=int(reads_per_batch), write_flags=_abi.MTB_WRITE_LINEAGE if par.printLineage else 0,
+            max_bases=int(max_bases), threads=int(threads))
+        st = _abi.MtbClassifyStats()
+        check(lib().mtb_start_classify(self.handle, ctypes.byref(opts), ctypes.byref(st)), "mtb_start_classify")
+        self.last_run = {f: getattr(st, f) for f, _ in _abi.MtbClassifyStats._fields_}
+        return int(st.reads)
 
     _rank_of = None
 

@@ -1,0 +1,417 @@
+// Classifier::startClassify (Classifier.cpp:44-164) as a native pipeline over files (SURVEY
+// §8(f)1-2): the reference indexes the input in one serial pass (QueryIndexer.cpp:30-147), then
+// re-reads it chunk by chunk on one thread (KmerExtractor.cpp:442-494) while the compute waits.
+// Here four kinds of threads overlap:
+//   * per mate file, a byte source (BGZF blocks inflated by a worker pool; gzip / plain read ahead)
+//     and a parser cutting records into blocks of kBlockReads reads;
+//   * an assembler filling pinned host batches (<= max_reads reads, <= max_bases bases: the
+//     reference's RAM-bounded QuerySplits, QueryIndexer.cpp:62-67,132-137) and uploading each to
+//     its own device buffers on a copy stream;
+//   * the calling thread running mtb_classify_batch on the uploaded batches (MTB_INPUT_DEVICE);
+//   * a writer formatting each classified batch into the per-read TSV (Reporter.cpp:38-83) and
+//     counting reads per taxon for the report (Classifier.cpp:149, Reporter.cpp:175-190).
+// Batches rotate through kSlots slots, so batch k+1 is parsed and uploaded and batch k-1 written
+// while batch k runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "mtb_host.h"
+#include "mtb_io.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+template <typename T>
+struct BoundedQueue {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<T> q;
+    size_t cap;
+    bool closed = false;
+    explicit BoundedQueue(size_t c) : cap(c) {}
+    bool push(T v) {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return closed || q.size() < cap; });
+        if (closed) return false;
+        q.push_back(std::move(v));
+        cv.notify_all();
+        return true;
+    }
+    bool pop(T& v) {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return closed || !q.empty(); });
+        if (q.empty()) return false;
+        v = std::move(q.front());
+        q.pop_front();
+        cv.notify_all();
+        return true;
+    }
+    void close() {
+        std::lock_guard<std::mutex> l(mu);
+        closed = true;
+        cv.notify_all();
+    }
+};
+
+// First error of any thread (the C-ABI's error string is per thread: the caller's is set at the end).
+struct ErrorBox {
+    std::mutex mu;
+    std::string msg;
+    int code = MTB_OK;
+    std::atomic<bool> failed{false};
+    void set(int c, const std::string& m) {
+        std::lock_guard<std::mutex> l(mu);
+        if (code == MTB_OK) {
+            code = c;
+            msg = m;
+        }
+        failed = true;
+    }
+};
+
+constexpr uint32_t kBlockReads = 8192;
+constexpr int kSlots = 3;
+
+struct RecordBlock {
+    std::string names, seq;
+    std::vector<uint64_t> noff{0}, off{0};
+    uint32_t n = 0;
+};
+
+struct MateReader {
+    mtb::FastxStream st;
+    BoundedQueue<std::shared_ptr<RecordBlock>> out{6};
+    std::thread t;
+    void run(ErrorBox* eb) {
+        std::string err;
+        while (!eb->failed) {
+            auto b = std::make_shared<RecordBlock>();
+            while (b->n < kBlockReads && mtb::next_record(st, b->seq, b->off, b->names, b->noff, err)) b->n++;
+            if (!err.empty()) {
+                eb->set(MTB_ERR_IO, err);
+                break;
+            }
+            if (b->n && !out.push(b)) break;
+            if (b->n < kBlockReads) break;
+        }
+        out.close();
+    }
+};
+
+template <typename T>
+struct Pinned {  // grow-only pinned host buffer
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = n + n / 4 + 1024;
+        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~Pinned() {
+        if (p) hipHostFree(p);
+    }
+};
+
+struct DevMem {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = bytes + bytes / 4 + 1024;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~DevMem() {
+        if (p) hipFree(p);
+    }
+};
+
+struct Slot {
+    Pinned<char> seq1, seq2;
+    Pinned<uint64_t> off1, off2;
+    std::string names;
+    std::vector<uint64_t> noff;
+    uint32_t n = 0;
+    uint64_t bases = 0;
+    DevMem dseq1, dseq2, doff1, doff2;
+    hipEvent_t uploaded = nullptr;
+    std::vector<mtb_result> res;
+    std::vector<mtb_taxcnt> tc;
+};
+
+// Reads of one mate's current block, consumed from `at`.
+struct Cursor {
+    std::shared_ptr<RecordBlock> b;
+    uint32_t at = 0;
+    bool next(MateReader& m) {
+        if (b && at < b->n) return true;
+        at = 0;
+        return m.out.pop(b);
+    }
+};
+
+}  // namespace
+
+extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mtb_classify_stats* stats) {
+    using mtb::set_error;
+    if (!ctx || !opt || !opt->query1 || !opt->out_tsv) {
+        set_error("null argument");
+        return MTB_ERR_ARG;
+    }
+    const auto t0 = Clock::now();
+    const bool paired = opt->query2 != nullptr;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int threads = opt->threads > 0 ? opt->threads : (int)std::min(16u, hw);
+    const uint32_t maxReads = opt->max_reads ? opt->max_reads : 1000000u;
+    uint64_t maxBases = opt->max_bases;
+    if (!maxBases) {  // ~140 device bytes of workspace per base at GTDB scale; slots < 2^31
+        size_t freeB = 0, totalB = 0;
+        hipMemGetInfo(&freeB, &totalB);
+        maxBases = std::min<uint64_t>((uint64_t)(0.5 * (double)freeB / 140.0), 1ull << 30);
+        maxBases = std::max<uint64_t>(maxBases, 1ull << 20);
+    }
+    ErrorBox eb;
+    MateReader m1, m2;
+    const int srcThreads = std::max(1, paired ? threads / 2 : threads);
+    if (!m1.st.open(opt->query1, srcThreads, true)) {
+        set_error(m1.st.err);
+        return MTB_ERR_IO;
+    }
+    if (paired && !m2.st.open(opt->query2, srcThreads, true)) {
+        set_error(m2.st.err);
+        return MTB_ERR_IO;
+    }
+    Slot slots[kSlots];
+    hipStream_t up = nullptr;
+    if (hipStreamCreateWithFlags(&up, hipStreamNonBlocking) != hipSuccess) {
+        set_error("cannot create the upload stream");
+        return MTB_ERR_HIP;
+    }
+    for (Slot& s : slots) hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming);
+    BoundedQueue<Slot*> freeQ(kSlots), readyQ(kSlots), writeQ(kSlots);
+    for (Slot& s : slots) freeQ.push(&s);
+
+    m1.t = std::thread([&] { m1.run(&eb); });
+    if (paired) m2.t = std::thread([&] { m2.run(&eb); });
+
+    // assembler: blocks -> pinned batches -> device buffers (copy stream)
+    std::thread assembler([&] {
+        Cursor c1, c2;
+        bool end = false;
+        while (!end && !eb.failed) {
+            Slot* s = nullptr;
+            if (!freeQ.pop(s)) break;
+            s->n = 0;
+            s->bases = 0;
+            s->names.clear();
+            s->noff.assign(1, 0);
+            uint64_t b1 = 0, b2 = 0;
+            std::vector<std::pair<std::shared_ptr<RecordBlock>, std::pair<uint32_t, uint32_t>>> take1, take2;
+            // which reads go in: whole block stretches until max_reads / max_bases
+            static const char* kUnequal = "paired-end inputs have different read counts (QueryIndexer.cpp:121-124)";
+            while (s->n < maxReads) {
+                const bool more1 = c1.next(m1);
+                const bool more2 = paired && c2.next(m2);
+                if (!more1) {
+                    if (more2) eb.set(MTB_ERR_IO, kUnequal);
+                    end = true;
+                    break;
+                }
+                // both mates are cut into blocks of kBlockReads: their stretches line up read by read
+                if (paired && (!more2 || c2.b->n - c2.at != c1.b->n - c1.at)) {
+                    eb.set(MTB_ERR_IO, kUnequal);
+                    end = true;
+                    break;
+                }
+                const RecordBlock& x = *c1.b;
+                uint32_t k = c1.at;
+                while (k < x.n && s->n + (k - c1.at) < maxReads) {
+                    uint64_t len = x.off[k + 1] - x.off[k];
+                    if (paired) len += c2.b->off[c2.at + (k - c1.at) + 1] - c2.b->off[c2.at + (k - c1.at)];
+                    if (s->bases + len > maxBases && s->n + (k - c1.at) > 0) break;
+                    s->bases += len;
+                    k++;
+                }
+                const uint32_t got = k - c1.at;
+                if (got == 0) break;  // the bases budget is full
+                take1.push_back({c1.b, {c1.at, k}});
+                b1 += x.off[k] - x.off[c1.at];
+                if (paired) {
+                    take2.push_back({c2.b, {c2.at, c2.at + got}});
+                    b2 += c2.b->off[c2.at + got] - c2.b->off[c2.at];
+                    c2.at += got;
+                }
+                s->n += got;
+                c1.at = k;
+                if (s->bases >= maxBases) break;
+            }
+            if (eb.failed) break;
+            if (s->n == 0) break;
+            auto fill = [&](auto& take, Pinned<char>& seq, Pinned<uint64_t>& off, uint64_t bytes, bool names) {
+                if (seq.ensure(bytes + 1) != hipSuccess || off.ensure((size_t)s->n + 1) != hipSuccess) return false;
+                uint64_t at = 0;
+                uint32_t r = 0;
+                off.p[0] = 0;
+                for (auto& tk : take) {
+                    const RecordBlock& b = *tk.first;
+                    const uint32_t lo = tk.second.first, hi = tk.second.second;
+                    const uint64_t base = b.off[lo];
+                    memcpy(seq.p + at, b.seq.data() + base, b.off[hi] - base);
+                    for (uint32_t i = lo; i < hi; i++) off.p[++r] = at + (b.off[i + 1] - base);
+                    at += b.off[hi] - base;
+                    if (names) {
+                        const uint64_t nb = b.noff[lo];
+                        const size_t o = s->names.size();
+                        s->names.append(b.names.data() + nb, b.noff[hi] - nb);
+                        for (uint32_t i = lo; i < hi; i++) s->noff.push_back(o + (b.noff[i + 1] - nb));
+                    }
+                }
+                return true;
+            };
+            if (!fill(take1, s->seq1, s->off1, b1, true) || (paired && !fill(take2, s->seq2, s->off2, b2, false))) {
+                eb.set(MTB_ERR_OOM, "cannot allocate pinned host batch buffers");
+                break;
+            }
+            const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
+            bool ok = s->dseq1.ensure(b1 + 1) == hipSuccess && s->doff1.ensure(on) == hipSuccess &&
+                      hipMemcpyAsync(s->dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up) == hipSuccess &&
+                      hipMemcpyAsync(s->doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up) == hipSuccess;
+            if (ok && paired)
+                ok = s->dseq2.ensure(b2 + 1) == hipSuccess && s->doff2.ensure(on) == hipSuccess &&
+                     hipMemcpyAsync(s->dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up) == hipSuccess &&
+                     hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up) == hipSuccess;
+            ok = ok && hipEventRecord(s->uploaded, up) == hipSuccess;
+            if (!ok) {
+                eb.set(MTB_ERR_HIP, "batch upload failed");
+                break;
+            }
+            if (!readyQ.push(s)) break;
+        }
+        readyQ.close();
+    });
+
+    // writer: TSV lines + per-taxon read counts
+    std::map<int32_t, uint64_t> taxCounts;
+    double writeS = 0;
+    std::thread writer([&] {
+        bool first = true;
+        Slot* s = nullptr;
+        while (writeQ.pop(s)) {
+            const auto w0 = Clock::now();
+            if (!eb.failed) {
+                mtb_read_batch b{};
+                b.n_reads = s->n;
+                b.names = s->names.data();
+                b.name_off = s->noff.data();
+                if (mtb_write_classifications(ctx, opt->out_tsv, first ? 0 : 1, &b, s->res.data(), s->tc.data(),
+                                              opt->write_flags) != MTB_OK)
+                    eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
+                first = false;
+                for (uint32_t i = 0; i < s->n; i++)  // ++taxCounts[classification] (Classifier.cpp:201-203)
+                    taxCounts[s->res[i].is_classified ? s->res[i].classification : 0]++;
+            }
+            writeS += secs(w0, Clock::now());
+            freeQ.push(s);
+        }
+        if (first && !eb.failed) {  // no reads: the header alone
+            mtb_read_batch b{};
+            std::vector<uint64_t> z(1, 0);
+            b.name_off = z.data();
+            b.names = "";
+            mtb_write_classifications(ctx, opt->out_tsv, 0, &b, nullptr, nullptr, opt->write_flags);
+        }
+    });
+
+    // the GPU stage on the calling thread
+    uint64_t reads = 0, bases = 0, batches = 0;
+    double gpuS = 0, waitS = 0;
+    Slot* s = nullptr;
+    while (true) {
+        const auto w0 = Clock::now();
+        if (!readyQ.pop(s)) break;
+        waitS += secs(w0, Clock::now());
+        if (eb.failed) {
+            freeQ.push(s);
+            continue;
+        }
+        const auto g0 = Clock::now();
+        int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
+        s->res.resize(s->n);
+        if (rc == MTB_OK)
+            rc = mtb_classify_batch(ctx, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
+                                    paired ? (const char*)s->dseq2.p : nullptr,
+                                    paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
+                                    s->res.data());
+        uint64_t nt = 0;
+        if (rc == MTB_OK) {
+            mtb_get_taxcnt(ctx, nullptr, 0, &nt);
+            s->tc.resize(std::max<uint64_t>(nt, 1));
+            rc = mtb_get_taxcnt(ctx, s->tc.data(), s->tc.size(), &nt);
+        }
+        gpuS += secs(g0, Clock::now());
+        if (rc != MTB_OK) {
+            eb.set(rc, mtb_last_error());
+            freeQ.push(s);
+            continue;
+        }
+        reads += s->n;
+        bases += s->bases;
+        batches++;
+        writeQ.push(s);
+    }
+    writeQ.close();
+    writer.join();
+    freeQ.close();
+    assembler.join();
+    m1.out.close();
+    m2.out.close();
+    m1.t.join();
+    if (paired) m2.t.join();
+    for (Slot& x : slots) hipEventDestroy(x.uploaded);
+    hipStreamDestroy(up);
+    if (eb.code != MTB_OK) {
+        set_error(eb.msg);
+        return eb.code;
+    }
+    if (opt->report_tsv) {
+        std::vector<int32_t> ids;
+        std::vector<uint32_t> cnt;
+        for (auto& kv : taxCounts) {
+            ids.push_back(kv.first);
+            cnt.push_back((uint32_t)kv.second);
+        }
+        const int rc = mtb_write_report(ctx, opt->report_tsv, reads, ids.data(), cnt.data(), ids.size());
+        if (rc != MTB_OK) return rc;
+    }
+    if (stats) {
+        stats->reads = reads;
+        stats->bases = bases;
+        stats->batches = batches;
+        stats->wall_s = secs(t0, Clock::now());
+        stats->gpu_s = gpuS;
+        stats->input_wait_s = waitS;
+        stats->write_s = writeS;
+    }
+    return MTB_OK;
+}

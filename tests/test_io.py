@@ -152,6 +152,7 @@ def test_start_classify_tsv(make_db, tmp_path):
     rep = str(tmp_path / "report.tsv")
     with Classifier(par, db_dir=db_dir) as clf:
         assert clf.startClassify(out, reads_per_batch=700, report_tsv=rep) == r.n
+        assert clf.last_run["batches"] == 4 and clf.last_run["reads"] == r.n
     odb = oc.OracleDb(db_dir)
     ores, otc = oc.classify(odb, par.to_c(), r)
     # the per-taxon report (Reporter::writeReportFile) of the oracle's classifications, byte for byte
@@ -182,3 +183,34 @@ def test_start_classify_tsv(make_db, tmp_path):
             assert f[6] == want
         else:
             assert f[5:] == ["-", "-", ""]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["bgzf", "gzip"])
+def test_start_classify_long_reads_batches(make_db, tmp_path, mode):
+    """A long-read (seq-mode 3) file larger than one batch: the pipeline cuts batches by bases
+    (max_bases, the reference's RAM-bounded QuerySplits) and the TSV is the oracle's, read by read."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_long_reads(gen, 120, n50=3000, min_len=400, seed=44)
+    p1 = str(tmp_path / ("long.fq.gz"))
+    synth.write_compressed(p1, synth.fastq_bytes(r.seq1, r.off1, prefix="L"), mode)
+    par = LocalParameters(seqMode=3, filenames=[p1, db_dir])
+    par.load_db_parameters(db_dir)
+    out = str(tmp_path / "long.tsv")
+    with Classifier(par, db_dir=db_dir) as clf:
+        assert clf.startClassify(out, max_bases=40_000, threads=4) == r.n
+        assert clf.last_run["batches"] > 5 and clf.last_run["bases"] == int(r.off1[-1])
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    body = [l for l in open(out).read().split("\n")[1:] if l]
+    assert len(body) == r.n
+    for i, line in enumerate(body):
+        f = line.split("\t")
+        o = ores[i]
+        assert f[1] == f"L{i:09d}"
+        assert int(f[2]) == (int(o["classification"]) if o["is_classified"] else 0)
+        assert f[4] == "%g" % float(o["score"])
+        if o["is_classified"]:
+            s = int(o["taxcnt_offset"])
+            assert f[6] == "".join(f"{int(t)}:{int(c)} " for t, c in otc[s:s + int(o["taxcnt_len"])])
