@@ -195,6 +195,10 @@ def main():
     ap.add_argument("--gtdb-true-species", type=int, default=1000)
     ap.add_argument("--gtdb-genome", type=int, default=3_000_000)
     ap.add_argument("--gtdb-cpu-sample", type=int, default=1_000_000, help="config 3: read pairs timed on the oracle")
+    ap.add_argument("--variants", default="syncmer,related",
+                    help="extra config-3 lines, comma-separated (GTDB_VARIANTS; empty = none)")
+    ap.add_argument("--variant-cpu-sample", type=int, default=200_000,
+                    help="read pairs of each variant line timed on the oracle (parity sample)")
     ap.add_argument("--e2e-pairs", type=int, default=10_000_000,
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
     ap.add_argument("--e2e-gzip-pairs", type=int, default=1_000_000,
@@ -213,6 +217,11 @@ def main():
         return
     torch.cuda.empty_cache()
     c3 = run_gtdb(args, world, rank, local, dev) if args.gtdb_kmers > 0 else None
+    if c3 is not None:
+        c3["variants"] = {}
+        for v in [x for x in args.variants.split(",") if x]:
+            torch.cuda.empty_cache()
+            c3["variants"][v] = run_gtdb(args, world, rank, local, dev, variant=v)
     if rank == 0:
         head = c3 if c3 is not None else c2
         if head is None:
@@ -445,7 +454,17 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
                         "seq mode 3"}
 
 
-def run_gtdb(args, world, rank, local, dev):
+GTDB_VARIANTS = {  # extra config-3 lines: the DB format users run, GTDB-like sharing
+    "syncmer": {"syncmer": 1, "smer_len": 5, "per_genus": 1, "species_div": 0.0,
+                "what": "Syncmer 1 DB (closed syncmers, s = 5: GTDB R226's DB format), reads classified with syncmer"},
+    "related": {"syncmer": 0, "smer_len": 5, "per_genus": 20, "species_div": 0.05,
+                "what": "true-signal species in genera of 20 sister species, each 5% diverged from its genus "
+                        "genome (~10% between sisters, GTDB's 5-15% within a genus): DB AA runs carry several "
+                        "species"},
+}
+
+
+def run_gtdb(args, world, rank, local, dev, variant=None):
     """Config 3, the configuration BASELINE.json's metric names: 10M x 150 bp pairs per
     GPU vs a GTDB-scale DB (~12G k-mers over a 129,671-species skeleton taxonomy: 1000 species x 2
     strains x ~3 Mbp of true-signal genomes through the GPU builder, the rest random valid metamers),
@@ -460,14 +479,18 @@ def run_gtdb(args, world, rank, local, dev):
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
         got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev)
-        if args.long_reads > 0:
+        if args.long_reads > 0 and not variant:
             got["long"] = make_long_reads_gpu(seq, off, args.long_reads, args.seed * 1000 + 37 + 17 * rank, dev)
 
+    vr = GTDB_VARIANTS[variant] if variant else {"syncmer": 0, "smer_len": 5, "per_genus": 1, "species_div": 0.0}
+    tag = f"config 3 [{variant}]" if variant else "config 3"
     rdb = build_gtdb_scale(dev, n_true_species=args.gtdb_true_species, genome_len=args.gtdb_genome,
                            total_species=args.gtdb_species, target_kmers=int(args.gtdb_kmers), seed=args.seed + 1,
-                           before_free=grab, log=lambda m: log(rank, f"[bench] {m} ({time.time() - t0:.1f}s)"))
+                           before_free=grab, log=lambda m: log(rank, f"[bench] {m} ({time.time() - t0:.1f}s)"),
+                           syncmer=vr["syncmer"], smer_len=vr["smer_len"], per_genus=vr["per_genus"],
+                           species_div=vr["species_div"])
     s1, o1, s2, o2 = got.pop("reads")
-    lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1, syncmer=vr["syncmer"], smerLen=vr["smer_len"])
     clf = Classifier(lp, db_resident=rdb, device=local)
     log(rank, f"[bench] GTDB-scale context open ({time.time() - t0:.1f}s)")
     L = 150
@@ -529,18 +552,26 @@ def run_gtdb(args, world, rank, local, dev):
                            live=tot_live / launches)
     rand_roof = random_roofline(kern, names, work, Qb, Mb, rdb.n)
     value = world * N * args.steps / elapsed
-    log(rank, f"[bench] config 3: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
+    log(rank, f"[bench] {tag}: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
               f"kernels {dict(zip(names, np.round(kern, 2)))}")
+    # whole pipeline against HBM: reads + query k-mers written and read (2 x 16 B) +
+    # the DB bytes the join asks for (28 B per query: two run-index entries, two records) + matches
+    # written and read (2 x 24 B) + 16 B per read, over the batch's device time (all stages)
+    pipe_bytes = 2 * L * B + 32 * Qb + 28 * Qb + 48 * Mb + 16 * B
+    pipe = {"achieved": round(pipe_bytes / (stage[4] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(pipe_bytes / (stage[4] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_batch": int(pipe_bytes),
+            "device_ms_per_batch": round(float(stage[4]), 3)}
 
     cpu = parity = odb = None
     cores = 1
-    if rank == 0 and args.cpu_sample > 0 and args.gtdb_cpu_sample > 0:
+    cpu_sample = args.variant_cpu_sample if variant else args.gtdb_cpu_sample
+    if rank == 0 and args.cpu_sample > 0 and cpu_sample > 0:
         from tests import oracle_ctypes as oc  # checker / baseline only
 
         te = time.perf_counter()
         odb = encode_into_oracle(rdb, oc.OracleDb)
         log(rank, f"[bench] oracle DB encoded on the host ({time.perf_counter() - te:.1f}s)")
-        S = min(args.gtdb_cpu_sample, N)
+        S = min(cpu_sample, N)
         h1 = s1[:S * L].cpu().numpy()
         h2 = s2[:S * L].cpu().numpy()
         ho = o1[:S + 1].cpu().numpy().astype(np.uint64)
@@ -562,11 +593,13 @@ def run_gtdb(args, world, rank, local, dev):
         parity = bool(np.array_equal(gb.results["classification"], ores["classification"])
                       and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
                       and np.array_equal(gb.taxcnt, otc))
-        log(rank, f"[bench] config 3 CPU oracle: {cpu['value']} reads/s, parity {parity}")
-    e2e = run_e2e(args, clf, s1, s2, L, N) if rank == 0 and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0) else None
+        log(rank, f"[bench] {tag} CPU oracle: {cpu['value']} reads/s, parity {parity}")
+    e2e = None
+    if rank == 0 and not variant and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0):
+        e2e = run_e2e(args, clf, s1, s2, L, N)
     clf.close()
     long_line = None
-    if "long" in got:
+    if "long" in got and not variant:
         ls1, lo1, n50 = got.pop("long")
         long_line = run_long_reads(args, lambda lpl: Classifier(lpl, db_resident=rdb, device=local), ls1, lo1, n50,
                                    world, rank, dev, odb, cores, "the GTDB-scale DB")
@@ -591,7 +624,13 @@ def run_gtdb(args, world, rank, local, dev):
         "work": work,
         "long_reads": long_line,
         "end_to_end": e2e,
+        "pipeline_roofline": pipe,
     }
+    if variant:
+        out = {"variant": variant, "what": vr["what"], "value": out["value"], "unit": "reads/s",
+               "ms_per_step": out["ms_per_step"], "config": out["config"], "roofline": roofline,
+               "pipeline_roofline": pipe, "random_roofline": rand_roof, "cpu_baseline": cpu, "parity_sample": parity,
+               "kernel_ms": out["kernel_ms"], "work": work}
     del rdb
     torch.cuda.empty_cache()
     return out

@@ -9,20 +9,36 @@ from . import synth
 
 
 # ---------------------------------------------------------------------------------------------
-def make_genomes_gpu(n_species, mean_len, strains, seed, dev, taxo=None):
+def make_genomes_gpu(n_species, mean_len, strains, seed, dev, taxo=None, per_genus=1, species_div=0.0):
     """Genomes of the first n_species species of `taxo` (made here when None), `strains` 2%-diverged
-    strains each, with gene blocks shared by a species' strains."""
+    strains each, with gene blocks shared by a species' strains. per_genus > 1: species come in
+    groups of per_genus (the genera of make_taxonomy(block_species=..., block_size=per_genus)) whose
+    genomes are species_div-diverged copies of one genus genome (GTDB-like: sister species share
+    most of their AA 8-mers, so a DB AA run holds several species)."""
     rng = np.random.default_rng(seed)
     if taxo is None:
         taxo = synth.make_taxonomy(n_species, strains, seed=seed)
-    lens = rng.integers(int(mean_len * 0.3), int(mean_len * 1.7), size=n_species).astype(np.int64)
+    per_genus = max(1, int(per_genus))
+    n_gen = (n_species + per_genus - 1) // per_genus
+    glens = rng.integers(int(mean_len * 0.3), int(mean_len * 1.7), size=n_gen).astype(np.int64)
+    lens = glens[np.arange(n_species) // per_genus]
     base_off = np.zeros(n_species + 1, np.int64)
     base_off[1:] = np.cumsum(lens)
     total = int(base_off[-1])
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     lut = torch.tensor([65, 67, 71, 84], dtype=torch.uint8, device=dev)
-    base = torch.randint(0, 4, (total,), dtype=torch.uint8, device=dev, generator=g)
+    if per_genus == 1:
+        base = torch.randint(0, 4, (total,), dtype=torch.uint8, device=dev, generator=g)
+    else:  # each species: its genus genome with species_div substitutions
+        base = torch.empty(total, dtype=torch.uint8, device=dev)
+        for gi in range(n_gen):
+            L = int(glens[gi])
+            gb = torch.randint(0, 4, (L,), dtype=torch.uint8, device=dev, generator=g)
+            for s in range(gi * per_genus, min(n_species, (gi + 1) * per_genus)):
+                m = torch.rand(L, device=dev, generator=g) < species_div
+                sh = torch.randint(1, 4, (L,), dtype=torch.uint8, device=dev, generator=g)
+                base[int(base_off[s]):int(base_off[s + 1])] = torch.where(m, (gb + sh) % 4, gb)
     seq = torch.empty(total * strains, dtype=torch.uint8, device=dev)
     chunk = 1 << 28
     for k in range(strains):

@@ -116,14 +116,19 @@ def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: 
                      total_species: int = 129_671, target_kmers: int = 12_000_000_000, strains: int = 2,
                      seed: int = 6, n_chunks: int = 64,
                      before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
-                     log: Callable[[str], None] = lambda s: None) -> ResidentDb:
+                     log: Callable[[str], None] = lambda s: None, syncmer: int = 0, smer_len: int = 5,
+                     per_genus: int = 1, species_div: float = 0.0) -> ResidentDb:
     """Build the DB on `dev`. before_free(seq, off) runs while the true-signal genomes are still in
-    HBM (the bench samples its reads there)."""
-    taxo = synth.make_taxonomy(total_species, strains, seed=seed)
-    taxo, gen, seq, off_t, _ = make_genomes_gpu(n_true_species, genome_len, strains, seed, dev, taxo=taxo)
+    HBM (the bench samples its reads there). syncmer: the true-signal part holds closed syncmers
+    only (a Syncmer 1 DB, the format of GTDB R226's DB); per_genus / species_div: sister species
+    of a genus share a diverged genus genome (make_genomes_gpu), so AA runs carry several species."""
+    taxo = synth.make_taxonomy(total_species, strains, seed=seed,
+                               block_species=n_true_species if per_genus > 1 else 0, block_size=per_genus)
+    taxo, gen, seq, off_t, _ = make_genomes_gpu(n_true_species, genome_len, strains, seed, dev, taxo=taxo,
+                                                per_genus=per_genus, species_div=species_div)
     if before_free is not None:
         before_free(seq, off_t)
-    par = default_params(kmer_format=2, seq_mode=2)
+    par = default_params(kmer_format=2, seq_mode=2, syncmer=syncmer, smer_len=smer_len)
     tv, ti = build_db_device(gen, taxo, par, device=dev.index or 0, device_seq=(seq, off_t))
     del seq, off_t
     torch.cuda.empty_cache()

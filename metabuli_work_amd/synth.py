@@ -78,14 +78,17 @@ class Reads:
 
 
 def make_taxonomy(n_species: int, strains_per_species: int, seed: int = 1, n_genera: Optional[int] = None,
-                  with_eukaryota: bool = True, accessions: int = 0) -> Taxonomy:
+                  with_eukaryota: bool = True, accessions: int = 0, block_species: int = 0,
+                  block_size: int = 1) -> Taxonomy:
     """Root 1 -> {Bacteria, Eukaryota} -> phylum -> class -> order -> family -> genus -> species
     -> strain ("no rank"). Species are spread over genera; the last 1/8 of the genera sit under
     Eukaryota so that the minConsCntEuk branch (Taxonomer.cpp:497-500) is exercised.
 
     accessions > 0: every strain (or strainless species) gets that many leaves of rank
     "accession", as an accession-level DB build adds them (IndexCreator.cpp:640-660: one new taxon
-    per genome accession, child of the genome's taxID); genomes are then made per accession."""
+    per genome accession, child of the genome's taxID); genomes are then made per accession.
+    block_species > 0: the first block_species species sit in genera of block_size species each
+    (species s in genus s // block_size), so sister species of a genus can share genomes' k-mers."""
     rng = np.random.default_rng(seed)
     n_genera = n_genera or max(1, n_species // 3)
     tax, par, rank, name = [1], [1], ["no rank"], ["root"]
@@ -109,7 +112,10 @@ def make_taxonomy(n_species: int, strains_per_species: int, seed: int = 1, n_gen
         fam = add(o, "family")
         genera.append(add(fam, "genus"))
     for s in range(n_species):
-        g = genera[int(rng.integers(0, n_genera))] if s >= n_genera else genera[s]
+        if s < block_species:
+            g = genera[(s // max(1, block_size)) % n_genera]
+        else:
+            g = genera[int(rng.integers(0, n_genera))] if s >= n_genera else genera[s]
         sp = add(g, "species")
         leaves = [add(sp, "no rank") for _ in range(strains_per_species)] or [sp]
         for lf in leaves:

@@ -48,7 +48,8 @@ def stage_of(seq):
             stage = "probe_join"
         elif k.startswith(("k_match_transpose", "k_compact_segments")):
             stage = "match_transpose"
-        elif k.startswith(("k_segsort", "k_max_seg", "k_pack_live", "k_chunk_sort", "k_merge_tiles", "k_merge_finish")):
+        elif k.startswith(("k_segsort", "k_max_seg", "k_pack_live", "k_chunk_sort", "k_merge_tiles", "k_merge_finish",
+                           "k_thin_big")):
             stage = "match_sort"
         elif stage == "match_sort" and not k.startswith("k_scan"):  # K5's live-count scan stays in K5
             stage = "assign"
