@@ -309,6 +309,7 @@ def run_config2(args, world, rank, local, dev):
     Qref, M = clf.last_counts()  # Qref: the reference's "Query k-mer number" (all non-blank windows)
     work = clf.stats()
     Q = work["query_kmers"]      # the query k-mers K4 consumes (AA 8-mer in the DB)
+    work["run_index_fallback_rate"] = round(work["gallop_queries"] / max(1, Q), 6)
     KERNELS = kernel_names(work)
     ms_per_step = elapsed / max(1, args.steps) * 1e3
     value = world * n * args.steps / elapsed
@@ -503,10 +504,10 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     c1 = ResultGather(dev, N) if world > 1 else None
     kern = np.zeros(7)
     stage = np.zeros(5)
-    tot_q = tot_m = tot_live = 0
+    tot_q = tot_m = tot_live = tot_gallop = 0
 
     def step(timed):
-        nonlocal kern, stage, tot_q, tot_m, tot_live
+        nonlocal kern, stage, tot_q, tot_m, tot_live, tot_gallop
         if world > 1:
             c1.reset()
         for a, b in spans:
@@ -519,6 +520,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                 st = clf.stats()
                 tot_q += st["query_kmers"]
                 tot_live += st["live_matches"]
+                tot_gallop += st["gallop_queries"]
                 tot_m += m
             if world > 1:
                 c1.add(clf, res_all[a:b])
@@ -546,6 +548,8 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     stage /= launches
     Qb, Mb = tot_q / launches, tot_m / launches  # per 1M-pair batch
     work = clf.stats()
+    # run-index fallback rate: query k-mers whose DB run the join found by a gallop (all timed batches)
+    work["run_index_fallback_rate"] = round(tot_gallop / max(1, tot_q), 6)
     names = kernel_names(work)
     roofline = roofline_of(kern, names, B, Qb, Mb, rdb.n,
                            load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}),

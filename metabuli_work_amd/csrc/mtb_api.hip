@@ -70,6 +70,7 @@ struct mtb_ctx {
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
+    uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
     bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
     uint32_t maxW = 0;           // the batch's most windows in one frame of one read
     int sortLoFine = kQuerySortLoFine;  // MTB_SORT_LO_FINE (experiments)
@@ -99,10 +100,11 @@ struct mtb_ctx {
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
-    static constexpr int kNumStats = 12;
+    static constexpr int kNumStats = 14;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
+    uint64_t spillCap = 0;     // direct join: spilled matches mStage holds (grows to the largest seen)
     DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
@@ -236,6 +238,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_DIRECT")) {  // 0: staged join; 2: direct, then rerun staged (tests the fallback)
         c->directJoin = atoi(e) != 0;
         c->directRetry = atoi(e) == 2;
+        c->spillShift = atoi(e) == 3 ? 2 : 0;
     }
     if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
@@ -437,7 +440,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     HIP_TRY(hipEventRecord(c->kev[10], s));
     if (c->sparse && (!prune || maxSeg > kSegSortRegs || c->segsortGlobal)) {  // K5 reads sparse segments only
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), c->chunkC,
-                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), s);
+                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), 0, s);  // sparse: no spills
         c->sparse = false;
     }
     HIP_TRY(launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
@@ -543,8 +546,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
-    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * kStatStripes));
-    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * (kStatStripes + 1)));
+    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
     // K1 extract: every window's key (the sentinel where no k-mer is emitted)
     HIP_TRY(hipEventRecord(c->kev[0], s));
     launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
@@ -614,17 +617,24 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         (void)hipGetLastError();  // no room for a slot-sized match buffer (e.g. a long-read batch): staged join
         direct = false;
     }
-    if (direct) {
+    if (direct) {  // + the spill buffer (queries past their read's stretch), in mStage / mRank
         HIP_TRY(c->ovFlag.ensure(sizeof(int)));
-    } else {
+        c->spillCap = std::max<uint64_t>(c->spillCap, std::max<uint64_t>(Q / 64, 1u << 16));
+        if (c->mStage.ensure(sizeof(mtb_match) * c->spillCap) != hipSuccess ||
+            c->mRank.ensure(sizeof(uint32_t) * c->spillCap) != hipSuccess) {
+            (void)hipGetLastError();
+            direct = false;
+        }
+    }
+    if (!direct) {
         HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
     }
     HIP_TRY(hipEventRecord(c->kev[6], s));
     if (!probe) launch_match_windows(qk, Q, c->db, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
-    uint64_t M = 0;
+    uint64_t M = 0, nSpill = 0;
     std::vector<unsigned long long> regTot(kStageRegions);
-    for (int attempt = 0; attempt < 3; attempt++) {
+    for (int attempt = 0; attempt < 4; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
         int overflow = 0;
@@ -638,20 +648,33 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->db, c->D, c->dir, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
-                         c->stageRegion, c->errFlag.as<int>(), c->matchWinCap, c->matchWin.as<uint64_t>(),
+                         direct ? c->spillCap : c->stageRegion, c->errFlag.as<int>(), c->matchWinCap,
+                         c->matchWin.as<uint64_t>(),
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
                          direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
-                         c->ovFlag.as<int>(), s);
+                         c->ovFlag.as<int>(), c->spillShift, s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (direct) {
+            nSpill = regTot[0];
             if (!overflow && !c->directRetry) break;
-            direct = false;  // a read outgrew its slot stretch: rerun staged
+            if (overflow && attempt == 0 && !c->directRetry) {  // the spill outgrew its buffer: once more, larger
+                const uint64_t want = nSpill + nSpill / 8;
+                if (c->mStage.ensure(sizeof(mtb_match) * want) == hipSuccess &&
+                    c->mRank.ensure(sizeof(uint32_t) * want) == hipSuccess) {
+                    c->spillCap = want;
+                    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+                    continue;
+                }
+                (void)hipGetLastError();
+            }
+            nSpill = 0;
+            direct = false;  // rerun staged
             HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
             HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
             continue;
         }
         M = 0;
@@ -664,7 +687,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
         HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kStatStripes, s));
+        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
     }
     HIP_TRY(hipEventRecord(c->kev[7], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
@@ -681,11 +704,14 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(hipEventRecord(c->kev[8], s));
     // a batch that goes on to K5 with pruning reads the direct join's segments in place (the
     // register sorts, segments of <= kSegSortRegs matches); otherwise they are compacted here
-    c->sparse = direct && !c->keepStages && !c->forceGeneric && !c->matchOnly;
-    if (direct && !c->sparse)
+    c->stats[13] = nSpill;
+    c->sparse = direct && nSpill == 0 && !c->keepStages && !c->forceGeneric && !c->matchOnly;
+    if (direct && !c->sparse) {
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
-                                c->matches.as<mtb_match>(), s);
-    else if (!direct)
+                                c->matches.as<mtb_match>(), c->spillShift, s);
+        launch_spill_scatter(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->mTotal.as<unsigned long long>(),
+                             nSpill, c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
+    } else if (!direct)
         launch_match_transpose(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->stageRegion,
                                c->mTotal.as<unsigned long long>(), c->mOff.as<uint64_t>(), n,
                                c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
@@ -796,10 +822,11 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipStreamSynchronize(s));
     c->stats[9] = dstat[1];
     {
-        std::vector<unsigned long long> ps(kStatStripes);
+        std::vector<unsigned long long> ps(kStatStripes + 1);
         HIP_TRY(hipMemcpy(ps.data(), c->probeStats.p, sizeof(unsigned long long) * ps.size(), hipMemcpyDeviceToHost));
         c->stats[2] = 0;
-        for (unsigned long long x : ps) c->stats[2] += x;  // queries with >= 1 match
+        for (uint32_t i = 0; i < kStatStripes; i++) c->stats[2] += ps[i];  // queries with >= 1 match
+        c->stats[12] = ps[kStatStripes];  // run-index fallbacks (gallop searches) of the probe join
     }
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));

@@ -971,7 +971,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const uint64_t* __restrict__ lineP, const uint16_t* __restrict__ runOff,
                                                int sortLo, unsigned long long* __restrict__ stats,
                                                SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
-                                               int* __restrict__ overflow) {
+                                               int* __restrict__ overflow, uint32_t capShift) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -999,6 +999,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint64_t winLo = kStage ? win[2 * blockIdx.x] : 0, winN = kStage ? win[2 * blockIdx.x + 1] - winLo : 0;
     const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
+    uint32_t nGallop = 0;  // probe-line queries whose run the run index does not hold (gallop fallback)
     if (kStage && staged) {
         constexpr int kLoad = kMatchWin / 256;
         uint64_t v[kLoad];
@@ -1067,6 +1068,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                     continue;
                 }
             }
+            nGallop++;
             const uint64_t from = line_lower_bound_at(pl, o);
             lo[j] = gallop_lower1(dbv, from, aa);
             hi[j] = gallop_lower1(dbv, lo[j], aa + (1ull << 24));
@@ -1126,17 +1128,45 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     for (int j = 0; j < kPer; j++) hit += c[j] != 0;
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
     if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
+    if (!kStage && lines) {  // the fallback counter sits past the stripes (rare: a lane-0 atomic per wave)
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) w += (uint32_t)__popcll(__ballot(nGallop > (uint32_t)j));
+        if (w && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)w);
+    }
     if (direct) {
         // each query's matches straight into its read's segment, at the ranks just reserved: the
-        // read's stretch of C slots per K1 unit (slotOff) bounds it; a read with more matches than
-        // that sets the overflow flag and the caller reruns the batch through the staging buffer
+        // read's stretch of C slots per K1 unit (slotOff) bounds it. A query whose ranks pass the
+        // stretch's end spills its matches, with their ranks, to buf (total[0] counts them, `region`
+        // bounds them; the caller scatters them after compacting the segments); a spill past that
+        // bound sets the overflow flag and the caller reruns the batch with a larger one
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             if (!c[j]) continue;
             const uint32_t r = info_seq(info[j]) - 1;
-            const uint64_t o = dirOff[r] * C, cap = dirOff[r + 1] * C - o;
+            const uint64_t o = dirOff[r] * C, cap = (dirOff[r + 1] * C - o) >> capShift;
             if (rk[j] + c[j] > cap) {
-                atomicExch(overflow, 1);
+                const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c[j]);
+                if (sp + c[j] > region) {
+                    atomicExch(overflow, 1);
+                    continue;
+                }
+                if (small[j]) {
+                    const bool rev = ((info_frame(info[j]) < 3) != (kmerFormat == 2));
+                    uint64_t wj = sp;
+                    uint32_t rj = rk[j];
+#pragma unroll
+                    for (int k = 0; k < 2; k++)
+                        if (rs[j][k] <= thr[j])
+                            emit_match(key[j], hr[j], info[j], rv[j][k], rt[j][k], rs[j][k], rev, spOf, maxTax, buf,
+                                       bufRank, wj++, rj++, err);
+                } else if (staged) {
+                    run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf,
+                             bufRank, sp, sp + c[j], rk[j], err);
+                } else {
+                    run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf,
+                             bufRank, sp, sp + c[j], rk[j], err);
+                }
                 continue;
             }
             SegMatch* out = direct + o;
@@ -1470,7 +1500,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  hipStream_t s) {
+                  uint32_t capShift, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -1480,13 +1510,13 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
-                                                        overflow);
+                                                        overflow, capShift);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
-                                                            stats, direct, dirOff, overflow);
+                                                            stats, direct, dirOff, overflow, capShift);
     }
 }
 
@@ -1496,16 +1526,40 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 __global__ void __launch_bounds__(256) k_compact_segments(const SegMatch* __restrict__ in,
                                                           const uint64_t* __restrict__ dirOff, uint32_t C,
                                                           const uint64_t* __restrict__ readOff, uint32_t nReads,
-                                                          mtb_match* __restrict__ out) {
+                                                          mtb_match* __restrict__ out, uint32_t capShift) {
     const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= nReads) return;
-    const uint64_t src = dirOff[r] * C, dst = readOff[r], n = readOff[r + 1] - dst;
+    const uint64_t src = dirOff[r] * C, dst = readOff[r];
+    const uint64_t n = min(readOff[r + 1] - dst, ((dirOff[r + 1] - dirOff[r]) * C) >> capShift);  // ranks past it: spilled
     for (uint64_t i = lane; i < n; i += 64) out[dst + i] = seg_expand(in[src + i], (uint64_t)(r + 1) << 32);
 }
 
+// The direct join's spilled matches (queries whose ranks passed their read's stretch) to their
+// ranks in the compacted segments, after k_compact_segments (which leaves those ranks stale).
+__global__ void k_spill_scatter(const mtb_match* __restrict__ spill, const uint32_t* __restrict__ spillRank,
+                                const unsigned long long* __restrict__ total, const uint64_t* __restrict__ readOff,
+                                uint32_t nReads, mtb_match* __restrict__ out, int* __restrict__ err) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total[0]) return;
+    const mtb_match m = spill[i];
+    const uint32_t r = info_seq(m.qinfo) - 1;
+    if (r >= nReads || readOff[r] + spillRank[i] >= readOff[r + 1]) {  // never write out of bounds
+        atomicExch(err, 2);
+        return;
+    }
+    out[readOff[r] + spillRank[i]] = m;
+}
+
+void launch_spill_scatter(const mtb_match* spill, const uint32_t* spillRank, const unsigned long long* total,
+                          uint64_t nSpill, const uint64_t* readOff, uint32_t nReads, mtb_match* out, int* err,
+                          hipStream_t s) {
+    if (nSpill) k_spill_scatter<<<(unsigned)((nSpill + 255) / 256), 256, 0, s>>>(spill, spillRank, total, readOff, nReads,
+                                                                               out, err);
+}
+
 void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
-                             uint32_t nReads, mtb_match* out, hipStream_t s) {
-    if (nReads) k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out);
+                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s) {
+    if (nReads) k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out, capShift);
 }
 
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,

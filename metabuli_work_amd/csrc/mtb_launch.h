@@ -202,12 +202,18 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  hipStream_t s);
+                  uint32_t capShift, hipStream_t s);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
-// slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A read whose matches do
-// not fit sets *overflow (nothing of it written): the caller reruns the batch staged.
+// slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A query whose ranks pass
+// its read's stretch spills its matches and their ranks to buf / bufRank (total[0] of them; at most
+// `region`, else *overflow is set and the caller reruns with a larger spill buffer or staged).
+// capShift (tests): stretches are taken as their size >> capShift, so that queries spill.
 void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
-                             uint32_t nReads, mtb_match* out, hipStream_t s);
+                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s);
+// the spilled matches to readOff[r] + rank (after launch_compact_segments)
+void launch_spill_scatter(const mtb_match* spill, const uint32_t* spillRank, const unsigned long long* total,
+                          uint64_t nSpill, const uint64_t* readOff, uint32_t nReads, mtb_match* out, int* err,
+                          hipStream_t s);
 // K4 runs without LDS DB windows (probe-line lower bounds, no window staging): a DB much larger
 // than the query stream; its queries are then sorted finer (kQuerySortLoFine: one more pass buys
 // DRAM-page locality for the random DB reads, measured 28.8 -> 26.5 ms per 1M pairs at GTDB scale)

@@ -142,20 +142,23 @@ def test_end_to_end_batches(make_db, db_name):
 
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
-@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:fine28", "64", "6144", "6144:staged"])
+@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "64", "6144",
+                                    "6144:staged", "6144:spill"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
     oracle's matches whatever the per-block window cap (0 forces the HBM path); and both outputs —
     matches written straight into each read's slot stretch (default), or staged + transposed
-    (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback);
+    (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback)
+    or queries past their read's stretch spill and are scattered after the compaction (MTB_DIRECT=3
+    quarters the stretches; the batch then classifies as the oracle does);
     and the unstaged join over queries sorted on a 32-bit AA-rank prefix (MTB_SORT_LO_FINE=28, its
     own block line ranges and LDS staging)."""
     window, _, mode = window.partition(":")
     monkeypatch.setenv("MTB_SORT_LO_FINE", "28" if mode == "fine28" else "36")
     monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
-    monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2"}.get(mode, "1"))
+    monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2", "spill": "3"}.get(mode, "1"))
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, 2)
     reads = _reads(gen, "paired", 2000, seed=9)
@@ -168,6 +171,12 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
         gm = clf.matches()
         assert len(gm) == len(omatches) == br.matches
         assert np.array_equal(gm, omatches)
+        if mode == "spill":
+            assert clf.stats()["spilled_matches"] > 0
+            ores, otc = oc.classify(odb, opar, reads)
+            br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+            assert clf.stats()["spilled_matches"] > 0
+            compare_results(br.results, br.taxcnt, ores, otc)
     odb.close()
 
 
@@ -239,6 +248,7 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
         assert clf.stats()["join_path"] == (0 if join == "probe" else 1)
         assert clf.stats()["query_kmers"] == len(ok)
+        assert clf.stats()["gallop_queries"] <= len(ok)  # run-index fallbacks (none on lines < 64K k-mers)
         assert br.query_kmers == int((info_seq(okmers["info"]) != 0).sum())
         gm = clf.matches()
         assert len(gm) == len(omatches) == br.matches

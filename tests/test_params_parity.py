@@ -37,6 +37,10 @@ CASES = [
     ("fmt1_acc", "single", {"accessionLevel": 1}),
     ("fmt2_acc", "paired", dict(ILLUMINA, accessionLevel=1)),
     ("fmt2_acc", "long", dict(ONT, accessionLevel=0)), ("fmt2_acc", "long", dict(ONT, accessionLevel=1)),
+    # --min-cons-cnt(-euk): the consecutive-match minimum of a path, and K5's pruning threshold with it
+    # (pm = 2, 7 and, with syncmers' codon shift of 3, 3)
+    ("fmt2", "paired", {"minConsCnt": 2}), ("fmt2", "long", dict(ONT, minConsCnt=7, minConsCntEuk=7)),
+    ("fmt2_syncmer", "paired", {"minConsCnt": 6}),
 ]
 SEQ_MODE = {"paired": 2, "single": 1, "long": 3}
 
