@@ -203,6 +203,7 @@ def main():
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
     ap.add_argument("--e2e-gzip-pairs", type=int, default=1_000_000,
                     help="config 3 file -> TSV line: read pairs written as single-member gzip FASTQ (0 = off)")
+    ap.add_argument("--variant-only", default="", help="experiments: run this config-3 variant line alone")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,6 +213,11 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.variant_only:
+        v = run_gtdb(args, world, rank, local, dev, variant=args.variant_only)
+        if rank == 0:
+            print(json.dumps(v))
+        return
     c2 = run_config2(args, world, rank, local, dev) if not args.skip_config2 or args.db_parts > 1 else None
     if args.db_parts > 1:
         return

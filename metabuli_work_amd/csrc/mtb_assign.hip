@@ -160,14 +160,22 @@ __device__ __forceinline__ void sort_live(mtb_match* __restrict__ out, uint64_t 
     }
 }
 
+// prune_then_sort's LDS: the hash tables while the matches are counted, then (the live flags held
+// in registers) the live keys gathered for the sort, in the same bytes: 20 B per match slot in all
+// (12 KB for a 512-match wave), so that several waves share a CU and hide the shuffles' latency.
 template <int E>
 struct PruneLds {
-    unsigned long long pairKey[128 * E];  // (species << 3 | frame) + 1
-    uint32_t pairCnt[128 * E];
-    uint32_t spKey[128 * E];  // species (> 0 for a valid DB)
-    uint32_t spLive[128 * E];
-    uint64_t cH[64 * E], cL[64 * E];
-    uint32_t cX[64 * E];
+    union {
+        struct {
+            uint32_t spKey[128 * E];    // species (> 0 for a valid DB) | live << 31
+            uint32_t pairKey[128 * E];  // (species slot << 3 | frame) + 1
+            uint32_t pairCnt[128 * E];
+        } t;
+        struct {
+            uint64_t cH[64 * E], cL[64 * E];
+            uint32_t cX[64 * E];
+        } c;
+    };
 };
 template <int E>
 __device__ __forceinline__ PruneLds<E>& prune_lds() {
@@ -184,15 +192,13 @@ template <int E, typename In>
 __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
                                                 uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
     constexpr uint32_t T = 128 * E;  // load <= 1/2
+    constexpr uint32_t kLive = 0x80000000u;
     PruneLds<E>& L = prune_lds<E>();  // one LDS instance per E whatever the input type
-    unsigned long long* pairKey = L.pairKey;
-    uint32_t *pairCnt = L.pairCnt, *spKey = L.spKey, *spLive = L.spLive, *cX = L.cX;
-    uint64_t *cH = L.cH, *cL = L.cL;
+    uint32_t *spKey = L.t.spKey, *pairKey = L.t.pairKey, *pairCnt = L.t.pairCnt;
     for (uint32_t i = lane; i < T; i += 64) {
+        spKey[i] = 0;
         pairKey[i] = 0;
         pairCnt[i] = 0;
-        spKey[i] = 0;
-        spLive[i] = 0;
     }
     __syncthreads();
     uint64_t h[E], l[E];
@@ -206,28 +212,32 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
             const mtb_match m = in.full((uint32_t)e);
             match_key(m, h[sl], l[sl]);
             rx[sl] = (uint32_t)m.right_end_hamming << 16;
-            ps[sl] = lds_insert<unsigned long long>(pairKey, T, (h[sl] >> 29) + 1);
-            atomicAdd(&pairCnt[ps[sl]], 1u);
             ss[sl] = lds_insert<uint32_t>(spKey, T, (uint32_t)(h[sl] >> 32));
+            ps[sl] = lds_insert<uint32_t>(pairKey, T, (ss[sl] << 3 | ((uint32_t)(h[sl] >> 29) & 7u)) + 1u);
+            atomicAdd(&pairCnt[ps[sl]], 1u);
         }
     }
     __syncthreads();
 #pragma unroll
     for (int sl = 0; sl < E; sl++)
-        if (64 * sl + lane < n && pairCnt[ps[sl]] >= pm) spLive[ss[sl]] = 1;
+        if (64 * sl + lane < n && pairCnt[ps[sl]] >= pm) spKey[ss[sl]] |= kLive;  // same value from every writer
     __syncthreads();
+    bool live[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) live[sl] = 64 * sl + lane < n && (spKey[ss[sl]] & kLive);
+    __syncthreads();  // the tables are dead: their bytes take the live keys
+    uint64_t *cH = L.c.cH, *cL = L.c.cL;
+    uint32_t* cX = L.c.cX;
     const uint64_t lt = (1ull << lane) - 1;
     int nLive = 0;
 #pragma unroll
     for (int sl = 0; sl < E; sl++) {
-        const int e = 64 * sl + lane;
-        const bool live = e < n && spLive[ss[sl]];
-        const uint64_t m = __ballot(live);
-        if (live) {
+        const uint64_t m = __ballot(live[sl]);
+        if (live[sl]) {
             const int p = nLive + (int)__popcll(m & lt);
             cH[p] = h[sl];
             cL[p] = l[sl];
-            cX[p] = rx[sl] | (uint32_t)e;
+            cX[p] = rx[sl] | (uint32_t)(64 * sl + lane);
         }
         nLive += (int)__popcll(m);
     }
@@ -241,10 +251,89 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
     if (lane == 0) liveCnt[r] = (uint32_t)nLive;
 }
 
+// Sort all, then prune on the sorted segment (kAfter, and E == 1): a (species, frame) group of >= pm
+// matches starts at e when e + pm - 1 holds its pair; a species run with such a group is live. Its
+// LDS is 64E bytes, so occupancy is bound by registers, not by prune_then_sort's hash tables.
 template <int E, typename In>
+__device__ __forceinline__ void sort_then_prune(const In& in, mtb_match* __restrict__ out, uint64_t base, int n,
+                                                int lane, uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
+    uint64_t h[E], l[E];
+    uint32_t x[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        h[sl] = ~0ull;
+        l[sl] = ~0ull;
+        x[sl] = 0;
+        if (e < n) {
+            const mtb_match m = in.full((uint32_t)e);
+            match_key(m, h[sl], l[sl]);
+            x[sl] = (uint32_t)m.right_end_hamming << 16;
+        }
+    }
+    const uint64_t seqBits = in.full(0).qinfo & (0x1FFFFFFFull << 32);
+    wave_bitonic_sort<E>(h, l, x, lane);
+    uint8_t* runLive = run_live_lds<E>();
+    const uint64_t lt = (1ull << lane) - 1;
+    const int far = lane + (int)pm - 1;  // pm <= 64 (the caller checks)
+    uint32_t rid[E];
+    bool pair[E];
+    uint32_t runs = 0;
+    uint64_t prevLast = ~0ull;  // the previous slot's last (species, frame)
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        const uint64_t sf = h[sl] >> 29;  // species << 3 | frame
+        const uint64_t a = __shfl(sf, far & 63, 64);
+        const uint64_t b = __shfl(h[sl + 1 < E ? sl + 1 : sl] >> 29, far & 63, 64);
+        uint64_t pv = __shfl_up(sf, 1, 64);
+        if (lane == 0) pv = prevLast;
+        prevLast = __shfl(sf, 63, 64);
+        pair[sl] = e + (int)pm - 1 < n && (far < 64 ? a : b) == sf;
+        const bool start = e < n && (e == 0 || (pv >> 3) != (sf >> 3));
+        const uint64_t m = __ballot(start);
+        rid[sl] = runs + (uint32_t)__popcll(m & lt) + (uint32_t)start - 1u;
+        runs += (uint32_t)__popcll(m);
+        runLive[64 * sl + lane] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sl = 0; sl < E; sl++)
+        if (pair[sl]) runLive[rid[sl]] = 1;
+    __syncthreads();
+    uint32_t kept = 0;
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        const bool live = e < n && runLive[rid[sl]];
+        const uint64_t m = __ballot(live);
+        if (live) {  // the record rebuilt from its key (+ rightEndHamming riding in x): no gather
+            mtb_match o;
+            o.qinfo = ((h[sl] >> 29) & 7ull) << 61 | seqBits | (uint32_t)(h[sl] & 0x1FFFFFFFu);
+            o.target_id = (uint32_t)l[sl];
+            o.species_id = (uint32_t)(h[sl] >> 32);
+            o.dna_encoding = (uint32_t)(l[sl] >> 32) & 0xFFFFFFu;
+            o.right_end_hamming = (uint16_t)(x[sl] >> 16);
+            o.hamming = (uint8_t)(l[sl] >> 56);
+            o.pad = 0;
+            out[base + kept + (uint32_t)__popcll(m & lt)] = o;
+        }
+        kept += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) liveCnt[r] = kept;
+}
+
+// kMode (E >= 2, with pruning): 0 = prune, then sort the live matches (prune_then_sort); 1 = sort
+// all, then prune (sort_then_prune).
+template <int E, typename In, int kMode = 0>
 __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
                                              uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
-    if constexpr (E >= 2) {
+    if constexpr (E >= 2 && kMode == 1) {
+        if (liveCnt && pm <= 64) {
+            sort_then_prune<E>(in, out, base, n, lane, liveCnt, r, pm);
+            return;
+        }
+    } else if constexpr (E >= 2) {
         if (liveCnt) {
             prune_then_sort<E>(in, out, base, n, lane, liveCnt, r, pm);
             return;
@@ -340,7 +429,7 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
 
 // 129..256 (E = 4) and 257..512 (E = 8) matches: the same register network with more slots per
 // lane, in kernels of their own so the small kernel keeps its register budget (occupancy).
-template <int E>
+template <int E, int kMode>
 __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict__ in, const uint64_t* __restrict__ mOff,
                                                      const SegMatch* __restrict__ seg,
                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
@@ -353,8 +442,11 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
     const long nl = seg_len(mOff, segLen, r);
     if (nl <= 32 * E || nl > 64 * E) return;
     const int n = (int)nl;
-    if (seg) segsort_regs<E>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
-    else segsort_regs<E>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
+    if (seg)
+        segsort_regs<E, SegIn, kMode>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n,
+                                       (int)threadIdx.x, liveCnt, r, pm);
+    else
+        segsort_regs<E, MatchIn, kMode>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
 }
 
 // One block per large segment (the block loops over the reads of its 256-read slice). Segments with
@@ -880,12 +972,19 @@ __global__ void k_max_seg_len(const uint32_t* __restrict__ segLen, uint32_t n, u
 static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                                uint64_t* gScratch, uint32_t maxSeg, uint32_t* liveCnt, long chunk, uint32_t pm,
                                const uint32_t* segLen, hipStream_t s, const SegMatch* seg, const uint64_t* inOff,
-                               uint32_t inC) {
+                               uint32_t inC, int mode) {
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
-    if (maxSeg > 128)
-        k_segsort_regs<4><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
-    if (maxSeg > 256)
-        k_segsort_regs<8><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
+    // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts
+#define MTB_REGS(E, M) k_segsort_regs<E, M><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen)
+    if (maxSeg > 128) {
+        if (mode == 1) MTB_REGS(4, 1);
+        else MTB_REGS(4, 0);
+    }
+    if (maxSeg > 256) {
+        if (mode == 1) MTB_REGS(8, 1);
+        else MTB_REGS(8, 0);
+    }
+#undef MTB_REGS
     if (maxSeg > kSmallSeg)
         k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen);
     if (maxSeg > kMidSeg)
@@ -899,7 +998,7 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
                           uint32_t pm, hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC,
-                          uint32_t* segLen, uint32_t* maxTmp) {
+                          uint32_t* segLen, uint32_t* maxTmp, int after) {
     pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
     if (seg && (global || maxSeg > kSmallSeg)) return hipErrorInvalidValue;  // sparse input: register sorts only
@@ -913,11 +1012,11 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
     // are dead: sorting the survivors, mostly within one 2048-entry LDS tile, beats sorting all)
     const long thinAbove = std::min<long>(chunk, kMidSeg);
     if (!liveCnt || maxSeg <= (uint32_t)thinAbove || !segLen)
-        return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC);
+        return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC, after);
     // the others are sorted and pruned as usual; the big ones are thinned in place first
     // (k_thin_big), then sorted and pruned on their survivors
     MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)thinAbove, liveCnt, chunk, pm, nullptr, s,
-                             seg, inOff, inC));
+                             seg, inOff, inC, after));
     mtb_match* io = const_cast<mtb_match*>(in);  // K5's input buffer: the caller's, free to overwrite
     k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, thinAbove, pm, segLen);
     MTB_HIP_RET(hipMemsetAsync(maxTmp, 0, sizeof(uint32_t), s));
@@ -926,7 +1025,7 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
     MTB_HIP_RET(hipMemcpyAsync(&maxSurv, maxTmp, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MTB_HIP_RET(hipStreamSynchronize(s));
     if (maxSurv == 0) return hipSuccess;
-    return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSurv, liveCnt, chunk, pm, segLen, s, nullptr, nullptr, 0);
+    return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSurv, liveCnt, chunk, pm, segLen, s, nullptr, nullptr, 0, after);
 }
 
 // Live matches (front-packed in each sorted segment) into one dense array: a wave per read.

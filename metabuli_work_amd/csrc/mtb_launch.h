@@ -243,11 +243,13 @@ uint64_t clade_bytes();
 // segLen / maxTmp (n u32 / 1 u32 device scratch, nullable): with pruning, segments over one LDS
 // sort (8192 matches, or mergeSeg) are thinned in place in `in` before they are sorted (k_thin_big);
 // `in` is overwritten then.
+// pruneAfter (A/B): segments of 129-512 matches are pruned (LDS hash counts), then their live
+// matches sorted (0, the default), or sorted whole, then pruned on the sorted order (1).
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
                           uint32_t pruneMin, hipStream_t s, const SegMatch* seg = nullptr,
                           const uint64_t* inOff = nullptr, uint32_t inC = 0, uint32_t* segLen = nullptr,
-                          uint32_t* maxTmp = nullptr);
+                          uint32_t* maxTmp = nullptr, int pruneAfter = 0);
 // The fewest matches a (species, frame) group needs for getMatchPaths to emit a path: a path of
 // depth d chains >= 1 + ceil((d - 1) / maxCodonShift) matches (each link adds a shift of at most
 // maxCodonShift codons, Taxonomer.cpp:487-648), paths are emitted at depth >= MIN_DEPTH

@@ -183,6 +183,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
 @pytest.mark.parametrize("compact", ["1", "0"])
 @pytest.mark.parametrize("db_name,kind,glob,merge", [
     ("fmt2", "paired", "1", "0"), ("fmt2", "long", "1", "0"), ("fmt1", "long", "1", "0"),
+    ("fmt2", "paired", "0", "after1"), ("fmt2", "long", "0", "after1"), ("fmt2_syncmer", "long", "0", "after1"),
     ("fmt2", "long", "0", "0"), ("fmt2_syncmer", "long", "0", "0"),
     ("fmt2", "long", "0", "512"), ("fmt1", "long", "0", "600"), ("fmt2_syncmer", "long", "0", "512")])
 def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monkeypatch):
@@ -191,9 +192,12 @@ def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monk
     sort; MTB_MERGE_SEG=n sends segments over n matches through the chunked LDS sorts + merge path
     (long reads' path above 8192 matches). Segments over that bound are thinned in place before
     their sort (k_thin_big: lossy LDS counts of the whole segment), or, with MTB_PRUNE_COMPACT=0,
-    sorted whole and pruned after the merge."""
+    sorted whole and pruned after the merge. The 129-512-match register sorts prune, then sort the
+    live matches (default), or with MTB_PRUNE_AFTER=1 sort whole segments and prune on the sorted
+    order."""
     monkeypatch.setenv("MTB_SEGSORT_GLOBAL", glob)
-    monkeypatch.setenv("MTB_MERGE_SEG", merge)
+    monkeypatch.setenv("MTB_PRUNE_AFTER", merge[5:] if merge.startswith("after") else "0")
+    monkeypatch.setenv("MTB_MERGE_SEG", "0" if merge.startswith("after") else merge)
     monkeypatch.setenv("MTB_PRUNE_COMPACT", compact)
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])

@@ -46,7 +46,7 @@ def stage_of(seq):
             stage = "match_join"
         elif k == "k_probe" or k.startswith("k_probe<"):
             stage = "probe_join"
-        elif k.startswith(("k_match_transpose", "k_compact_segments")):
+        elif k.startswith(("k_match_transpose", "k_compact_segments", "k_spill_scatter")):
             stage = "match_transpose"
         elif k.startswith(("k_segsort", "k_max_seg", "k_pack_live", "k_chunk_sort", "k_merge_tiles", "k_merge_finish",
                            "k_thin_big")):
