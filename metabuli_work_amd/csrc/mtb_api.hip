@@ -76,7 +76,6 @@ struct mtb_ctx {
     uint32_t maxW = 0;           // the batch's most windows in one frame of one read
     int sortLoFine = kQuerySortLoFine;  // MTB_SORT_LO_FINE (experiments)
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
-    bool noFilter = false;       // MTB_NO_FILTER=1: no K1F; the sort takes every window, the join's lines test membership
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
     int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1: K6 chooseBestTaxon thread / wave per read (tests; default auto)
@@ -233,7 +232,6 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
-    if (const char* e = getenv("MTB_NO_FILTER")) c->noFilter = atoi(e) != 0;
     if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix
         const int v = atoi(e);
         if (v >= 24 && v <= kQuerySortLo && (kQuerySortHi - v) % 8 == 0) c->sortLoFine = v;
@@ -565,9 +563,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     const uint32_t* qi = nullptr;
     const uint64_t* qf = nullptr;
     HIP_TRY(hipEventRecord(c->kev[2], s));
-    // without K1F (whole DB, sort-merge join) the join's LDS-staged probe lines test membership
-    const bool filter = c->lines && !(c->noFilter && !probe && c->rankLo == 0 && c->rankHi == ~0ull);
-    if (filter) {
+    if (c->lines) {
         if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
         Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
                           probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), c->rankLo,
@@ -586,7 +582,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                            ? c->sortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
-        if (filter) {
+        if (c->lines) {
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
                                  c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
@@ -594,7 +590,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
         } else {
             Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
-                                 c->valsB.as<uint32_t>(), R, c->lines ? sortLo : kQuerySortLo, kQuerySortHi, true, true,
+                                 c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
             qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
             qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();
