@@ -61,7 +61,8 @@ typedef struct mtb_params {
     int32_t min_cons_cnt_euk; /* --min-cons-cnt-euk (9)                                        */
     float tie_ratio;          /* --tie-ratio (0.95)                                            */
     int32_t accession_level;  /* 0, 1, or 2 (2 = DB has accessions but not requested)          */
-    int32_t em;               /* must be 0: EM reassignment is out of scope                    */
+    int32_t em;               /* --em: classified reads keep their best species (no lower-rank
+                                 BFS, Taxonomer.cpp:193-201) and record EM mappings (mtb_em)    */
     int32_t threads;          /* host threads (oracle / host parsing only)                     */
     int32_t mask_mode;        /* must be 0: tantan masking is out of scope                     */
     int32_t db_part;          /* range-partitioned DB: this context holds part db_part of      */
@@ -335,6 +336,12 @@ typedef struct mtb_classify_opts {
     uint64_t max_bases;       /* bases per batch, both mates (0: from free HBM, < 2^30)         */
     int32_t threads;          /* host threads for inflating (0: min(16, cores))                 */
     int32_t reserved;
+    /* --em outputs (context opened with em = 1; each NULL to skip): the reassigned reads
+     * (Reporter::writeReclassifyResults), the EM abundance report and the reassignment report
+     * (Reporter::writeReportFile with ReportType EM / EM_RECLASSIFY, Classifier.cpp:154-161) */
+    const char* em_tsv;
+    const char* em_report_tsv;
+    const char* em_reclassify_report_tsv;
 } mtb_classify_opts;
 typedef struct mtb_classify_stats {
     uint64_t reads, bases, batches;
@@ -344,6 +351,46 @@ typedef struct mtb_classify_stats {
     double write_s;           /* TSV formatting and writing (overlapped with the GPU stage)     */
 } mtb_classify_stats;
 int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify_stats* stats);
+
+/* ---- --em: EM re-estimation of species abundances and read reassignment ------------------------
+ * Replaces Reporter::writeMappings / Classifier::getTopSpecies (per batch) and Classifier::em +
+ * reclassify (Classifier.cpp:209-386) after the last batch. */
+typedef struct mtb_em_map {   /* MappingRes (common.h:24-28): 12 B */
+    uint32_t query_id;        /* read index over the whole run                                   */
+    int32_t species_id;       /* internal species taxID                                          */
+    float score;              /* species score squared                                           */
+} mtb_em_map;
+typedef struct mtb_em_read {  /* Classification's taxId / score (common.h:83-93) of one read      */
+    int32_t tax_id;           /* internal taxID of the reassignment, 0 = none                     */
+    int32_t mapped;           /* 0 no mappings; 1 reassigned; 2 mappings with a zero sum (taxID 0,
+                                 not counted in the reassignment report)                          */
+    double score;             /* probability mass of the species the LCA was taken over           */
+} mtb_em_read;
+typedef struct mtb_em_stats {
+    uint64_t query_count;     /* queries with a non-zero sum in the last iteration               */
+    uint32_t iterations;      /* EM iterations run (<= 1000; stops at delta < 1e-6)             */
+    uint32_t n_species;       /* top species (the abundance vector's support)                    */
+    double delta;             /* last iteration's sum |p_new - p|                                */
+} mtb_em_stats;
+/* The last batch's mappings (context opened with em = 1): for each classified read, in read order,
+ * its <= 10 best species by score (std::sort order: score descending, ties as libstdc++ leaves them)
+ * with score^2, query_id = query_offset + the read's batch index. n_out = mappings of the batch;
+ * returns MTB_RETRY (n_out set, nothing copied) when cap is too small. */
+int mtb_get_em_mappings(mtb_ctx* ctx, uint32_t query_offset, mtb_em_map* out, uint64_t cap, uint64_t* n_out);
+/* Classifier::em + reclassify over all mappings (query_id ascending, <= 10 per query): species
+ * length factors 1 / log(DB k-mers of the species) (dbDir/sp2uniqKmerCnt when present, else
+ * counted on the device and written there, as Classifier::countUniqueKmerPerSpecies does), the EM
+ * iterations on the device in double precision (per-species sums in query order, fixed order: run
+ * to run identical), then per query the reassignment. reads_out: total_reads entries. sp_ids /
+ * sp_probs / sp_counts (cap entries, ascending species; n_sp = the top species): final abundances
+ * and emTaxCounts (unsigned)(p * query_count). */
+int mtb_em(mtb_ctx* ctx, const mtb_em_map* maps, uint64_t n_maps, uint64_t total_reads, mtb_em_read* reads_out,
+           int32_t* sp_ids, double* sp_probs, uint32_t* sp_counts, uint64_t cap, uint64_t* n_sp, mtb_em_stats* stats);
+/* Reporter::writeReclassifyResults (Reporter.cpp:417-458): the reassigned reads, names and query
+ * lengths taken from the classification TSV written before (Classifier::loadOriginalResults,
+ * Classifier.cpp:450-480). flags: MTB_WRITE_LINEAGE. */
+int mtb_write_em_results(mtb_ctx* ctx, const char* path, const char* classification_tsv, const mtb_em_read* reads,
+                         uint64_t n_reads, uint32_t flags);
 
 #ifdef __cplusplus
 }

@@ -105,10 +105,22 @@ class MtbReadBatch(ctypes.Structure):
 class MtbClassifyOpts(ctypes.Structure):
     _fields_ = [("query1", ctypes.c_char_p), ("query2", ctypes.c_char_p), ("out_tsv", ctypes.c_char_p),
                 ("report_tsv", ctypes.c_char_p), ("max_reads", ctypes.c_uint32), ("write_flags", ctypes.c_uint32),
-                ("max_bases", ctypes.c_uint64), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("max_bases", ctypes.c_uint64), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("em_tsv", ctypes.c_char_p), ("em_report_tsv", ctypes.c_char_p),
+                ("em_reclassify_report_tsv", ctypes.c_char_p)]
 
 
 class MtbClassifyStats(ctypes.Structure):
     _fields_ = [("reads", ctypes.c_uint64), ("bases", ctypes.c_uint64), ("batches", ctypes.c_uint64),
                 ("wall_s", ctypes.c_double), ("gpu_s", ctypes.c_double), ("input_wait_s", ctypes.c_double),
                 ("write_s", ctypes.c_double)]
+
+
+# --em (include/mtb_gpu.h): MappingRes (common.h:24-28), the reassignment of one read, EM stats
+EM_MAP_DTYPE = np.dtype([("query_id", "<u4"), ("species_id", "<i4"), ("score", "<f4")])
+EM_READ_DTYPE = np.dtype([("tax_id", "<i4"), ("mapped", "<i4"), ("score", "<f8")])
+
+
+class MtbEmStats(ctypes.Structure):
+    _fields_ = [("query_count", ctypes.c_uint64), ("iterations", ctypes.c_uint32), ("n_species", ctypes.c_uint32),
+                ("delta", ctypes.c_double)]

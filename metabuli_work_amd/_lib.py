@@ -7,7 +7,7 @@ entry point raises. Build it with `python -c "import __graft_entry__ as g; g.bui
 import ctypes
 import pathlib
 
-from ._abi import MtbClassifyOpts, MtbClassifyStats, MtbDbHost, MtbDbResident, MtbParams, MtbReadBatch
+from ._abi import MtbClassifyOpts, MtbClassifyStats, MtbDbHost, MtbDbResident, MtbEmStats, MtbParams, MtbReadBatch
 
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libmtbgpu.so"
@@ -21,7 +21,7 @@ EXPORTED = [
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
-    "mtb_taxon_lineage", "mtb_start_classify",
+    "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
 ]
 
 
@@ -78,6 +78,9 @@ def lib() -> ctypes.CDLL:
     L.mtb_taxon_lineage.restype = ctypes.c_char_p
     L.mtb_start_classify.argtypes = [vp, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
+    L.mtb_get_em_mappings.argtypes = [vp, u32, vp, u64, P(u64)]
+    L.mtb_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, P(u64), P(MtbEmStats)]
+    L.mtb_write_em_results.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp, u64, u32]
     L.mtb_debug_tables.argtypes = [vp, vp, vp]
     L.mtb_debug_tables.restype = None
     _LIB = L

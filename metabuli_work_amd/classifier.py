@@ -281,20 +281,54 @@ class Classifier:
         check(lib().mtb_write_report(self.handle, path.encode(), total_reads, ptr(ids), ptr(cnt), len(ids)),
               "mtb_write_report")
 
+    def em_mappings(self, query_offset: int = 0) -> np.ndarray:
+        """The last batch's --em mappings (Reporter::writeMappings, Reporter.h:80-92): per classified
+        read its <= 10 best species (std::sort order) with score^2, query_id = query_offset + index."""
+        n = ctypes.c_uint64(0)
+        rc = check(lib().mtb_get_em_mappings(self.handle, int(query_offset), None, 0, ctypes.byref(n)),
+                   "mtb_get_em_mappings")
+        out = np.zeros(n.value, _abi.EM_MAP_DTYPE)
+        if rc == _abi.MTB_RETRY or n.value:
+            check(lib().mtb_get_em_mappings(self.handle, int(query_offset), out.ctypes.data, len(out),
+                                            ctypes.byref(n)), "mtb_get_em_mappings")
+        return out
+
+    def em(self, maps: np.ndarray, total_reads: int):
+        """Classifier::em + reclassify (Classifier.cpp:209-386) on the device over all mappings.
+        Returns (per-read EM_READ_DTYPE records, {species: (abundance, emTaxCount)}, stats dict)."""
+        maps = np.ascontiguousarray(maps, _abi.EM_MAP_DTYPE)
+        reads = np.zeros(max(int(total_reads), 1), _abi.EM_READ_DTYPE)
+        cap = len(maps) + 1
+        ids = np.zeros(cap, np.int32)
+        probs = np.zeros(cap, np.float64)
+        cnts = np.zeros(cap, np.uint32)
+        nsp = ctypes.c_uint64(0)
+        st = _abi.MtbEmStats()
+        check(lib().mtb_em(self.handle, maps.ctypes.data if len(maps) else None, len(maps), int(total_reads),
+                           reads.ctypes.data, ids.ctypes.data, probs.ctypes.data, cnts.ctypes.data, cap,
+                           ctypes.byref(nsp), ctypes.byref(st)), "mtb_em")
+        k = int(nsp.value)
+        sp = {int(ids[i]): (float(probs[i]), int(cnts[i])) for i in range(k)}
+        return reads[:int(total_reads)], sp, {f: getattr(st, f) for f, _ in _abi.MtbEmStats._fields_}
+
     def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None,
-                      max_bases: int = 0, threads: int = 0) -> int:
+                      max_bases: int = 0, threads: int = 0, em_tsv: Optional[str] = None,
+                      em_report_tsv: Optional[str] = None, em_reclassify_report_tsv: Optional[str] = None) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
         (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
         reads_per_batch reads and max_bases bases (0: sized from free HBM, the reference's
         RAM-bounded QuerySplits) uploaded on a copy stream, mtb_classify_batch, and the TSV writer
-        (+ the per-taxon report, Classifier.cpp:149) overlapping each other. Returns the reads
-        classified; the run's timings are left in self.last_run."""
+        (+ the per-taxon report, Classifier.cpp:149) overlapping each other; with --em (par.em) the
+        EM reassignment after the last batch and its TSV / reports (Classifier.cpp:152-161). Returns
+        the reads classified; the run's timings are left in self.last_run."""
         par = self.par
         opts = _abi.MtbClassifyOpts(
             query1=par.filenames[0].encode(), query2=par.filenames[1].encode() if par.seqMode == 2 else None,
             out_tsv=out_tsv.encode(), report_tsv=report_tsv.encode() if report_tsv else None,
             max_reads=int(reads_per_batch), write_flags=_abi.MTB_WRITE_LINEAGE if par.printLineage else 0,
-            max_bases=int(max_bases), threads=int(threads))
+            max_bases=int(max_bases), threads=int(threads),
+            em_tsv=em_tsv.encode() if em_tsv else None, em_report_tsv=em_report_tsv.encode() if em_report_tsv else None,
+            em_reclassify_report_tsv=em_reclassify_report_tsv.encode() if em_reclassify_report_tsv else None)
         st = _abi.MtbClassifyStats()
         check(lib().mtb_start_classify(self.handle, ctypes.byref(opts), ctypes.byref(st)), "mtb_start_classify")
         self.last_run = {f: getattr(st, f) for f, _ in _abi.MtbClassifyStats._fields_}

@@ -1,6 +1,7 @@
 // C-ABI of the MI355X classify path (include/mtb_gpu.h): context, DB residency in HBM and the
 // per-batch pipeline K0 read metadata -> K1 extract -> K2 radix sort -> K4 match (count, scan,
 // emit) -> K5/K6 per-read sort + assignment -> taxcnt compaction.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -106,6 +107,12 @@ struct mtb_ctx {
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
     uint64_t spillCap = 0;     // direct join: spilled matches mStage holds (grows to the largest seen)
+    // --em: the last batch's mappings (kEmTop {species, score^2} per read, their counts), the
+    // std::sort scratch (8 B per species run), DB k-mers per species (length factors)
+    DevBuf emMap, emCnt, emScratch;
+    bool emValid = false;
+    std::vector<uint32_t> spKmers;
+    std::string dbDir;
     DevBuf local, paths, comb, conn, spScore, spKeep,
         gFlag, sFlag, pathCnt, gScan, sScan, gStart, sStart, clade, tcPool, tcLen, tcOff, tcOut, results;
     // last batch
@@ -148,7 +155,7 @@ static hipError_t upload(T** dst, const std::vector<T>& v, hipStream_t s) {
 
 static int validate_params(const mtb_params* p) {
     if (p->reduced_aa) { set_error("reduced-AA DBs (ReducedKmerMatcher) are out of scope"); return MTB_ERR_UNSUPPORTED; }
-    if (p->em) { set_error("--em reassignment is out of scope"); return MTB_ERR_UNSUPPORTED; }
+    if (p->em && p->db_parts > 1) { set_error("--em needs the whole DB in one context"); return MTB_ERR_UNSUPPORTED; }
     if (p->mask_mode) { set_error("low-complexity masking is out of scope"); return MTB_ERR_UNSUPPORTED; }
     if (p->kmer_format != 1 && p->kmer_format != 2) { set_error("kmer_format must be 1 or 2"); return MTB_ERR_UNSUPPORTED; }
     if (p->syncmer && p->kmer_format != 2) { set_error("syncmer requires kmer_format 2"); return MTB_ERR_UNSUPPORTED; }
@@ -310,7 +317,9 @@ int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** ou
     if (!db_dir || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
     HostDb db;
     if (!load_db_files(db_dir, db)) return MTB_ERR_IO;
-    return open_common(db, par, device, out);
+    const int rc = open_common(db, par, device, out);
+    if (rc == MTB_OK) (*out)->dbDir = db_dir;  // --em: sp2uniqKmerCnt lives next to the DB files
+    return rc;
 }
 
 int mtb_open_host(const mtb_db_host* h, const mtb_params* par, int device, mtb_ctx** out) {
@@ -387,6 +396,7 @@ uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
 
 static AssignArgs assign_args(const mtb_params& p) {
     AssignArgs a;
+    a.em = p.em ? 1 : 0;
     a.kmerFormat = p.kmer_format;
     if (p.syncmer) {  // Taxonomer.cpp:34-42
         a.dnaShift = (8 - p.smer_len) * 3;
@@ -531,6 +541,17 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), kOff, c->results.as<mtb_result>(), c->tcOff.as<uint64_t>(), n,
                           c->tcOut.as<mtb_taxcnt>(), s);
     c->nTaxcnt = NT;
+    c->emValid = false;
+    if (c->par.em) {  // the mappings of Reporter::writeMappings (kEmTop best species per classified read)
+        const uint64_t nS = std::max<uint64_t>(c->stats[7], 1);
+        HIP_TRY(c->emScratch.ensure(8 * nS));
+        HIP_TRY(c->emMap.ensure(8 * (uint64_t)kEmTop * std::max<uint32_t>(n, 1)));
+        HIP_TRY(c->emCnt.ensure(std::max<uint32_t>(n, 1)));
+        launch_em_top(kIn, kOff, n, sc, c->results.as<mtb_result>(), c->emScratch.p, c->emMap.p,
+                      c->emCnt.as<uint8_t>(), s);
+        HIP_TRY(hipGetLastError());
+        c->emValid = true;
+    }
     return MTB_OK;
 }
 
@@ -1023,6 +1044,200 @@ int mtb_copy_results(mtb_ctx* c, void* dst, int dst_on_device) {
     HIP_TRY(hipMemcpyAsync(dst, c->results.p, sizeof(mtb_result) * c->nReads,
                            dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return MTB_OK;
+}
+
+int mtb_get_em_mappings(mtb_ctx* c, uint32_t query_offset, mtb_em_map* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (!c->par.em) { set_error("the context was opened without em"); return MTB_ERR_ARG; }
+    *n_out = 0;
+    const uint32_t n = c->nReads;
+    if (!c->emValid || n == 0) return MTB_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<uint8_t> cnt(n);
+    std::vector<std::pair<int32_t, float>> m((uint64_t)n * kEmTop);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), c->emCnt.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(m.data(), c->emMap.p, 8ull * kEmTop * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint64_t tot = 0;
+    for (uint32_t r = 0; r < n; r++) tot += cnt[r];
+    *n_out = tot;
+    if (tot > cap || (tot && !out)) return MTB_RETRY;
+    uint64_t w = 0;
+    for (uint32_t r = 0; r < n; r++)
+        for (uint32_t k = 0; k < cnt[r]; k++) {
+            const auto& e = m[(uint64_t)r * kEmTop + k];
+            out[w++] = mtb_em_map{query_offset + r, e.first, e.second};
+        }
+    return MTB_OK;
+}
+
+// DB k-mers per species: dbDir/sp2uniqKmerCnt ("taxID count" lines) when present, else counted on
+// the device and written there (Classifier::countUniqueKmerPerSpecies, Classifier.cpp:388-431).
+static int species_kmers(mtb_ctx* c) {
+    if (!c->spKmers.empty()) return MTB_OK;
+    c->spKmers.assign((size_t)c->maxTax + 1, 0);
+    const std::string path = c->dbDir.empty() ? std::string() : c->dbDir + "/sp2uniqKmerCnt";
+    if (!path.empty()) {
+        if (FILE* f = fopen(path.c_str(), "r")) {
+            long long t = 0;
+            unsigned long long k = 0;
+            while (fscanf(f, "%lld %llu", &t, &k) == 2)
+                if (t >= 0 && t < (long long)c->spKmers.size()) c->spKmers[(size_t)t] = (uint32_t)k;
+            fclose(f);
+            return MTB_OK;
+        }
+    }
+    DevBuf cnt;
+    HIP_TRY(cnt.ensure(sizeof(uint32_t) * c->spKmers.size()));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, sizeof(uint32_t) * c->spKmers.size(), c->stream));
+    launch_species_kmers(c->db, c->D, c->spOf, (uint32_t)c->maxTax, cnt.as<uint32_t>(), c->stream);
+    HIP_TRY(hipMemcpyAsync(c->spKmers.data(), cnt.p, sizeof(uint32_t) * c->spKmers.size(), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!path.empty()) {
+        if (FILE* f = fopen(path.c_str(), "w")) {
+            for (size_t i = 0; i < c->spKmers.size(); i++)
+                if (c->spKmers[i] > 0) fprintf(f, "%zu %u\n", i, c->spKmers[i]);
+            fclose(f);
+        }
+    }
+    return MTB_OK;
+}
+
+int mtb_em(mtb_ctx* c, const mtb_em_map* maps, uint64_t n_maps, uint64_t total_reads, mtb_em_read* reads_out,
+           int32_t* sp_ids, double* sp_probs, uint32_t* sp_counts, uint64_t cap, uint64_t* n_sp, mtb_em_stats* st) {
+    if (!c || (!maps && n_maps) || !reads_out || !n_sp) { set_error("null argument"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // queries (Classifier.cpp:224-233): runs of one query_id, ascending
+    std::vector<uint64_t> qOff;
+    std::vector<uint32_t> qId;
+    for (uint64_t j = 0; j < n_maps; j++) {
+        if (maps[j].query_id >= total_reads) { set_error("a mapping names a read past total_reads"); return MTB_ERR_ARG; }
+        if (j == 0 || maps[j].query_id != maps[j - 1].query_id) {
+            if (j && maps[j].query_id < maps[j - 1].query_id) { set_error("mappings must be in query order"); return MTB_ERR_ARG; }
+            qOff.push_back(j);
+            qId.push_back(maps[j].query_id);
+        } else if (j - qOff.back() >= (uint64_t)kEmTop) {
+            set_error("more than 10 mappings for one query");
+            return MTB_ERR_ARG;
+        }
+    }
+    const uint64_t nQ = qId.size();
+    qOff.push_back(n_maps);
+    // dense species (ascending taxID); the top species: each query's first mapping (getTopSpecies)
+    std::vector<int32_t> spTax(n_maps);
+    for (uint64_t j = 0; j < n_maps; j++) spTax[j] = maps[j].species_id;
+    std::sort(spTax.begin(), spTax.end());
+    spTax.erase(std::unique(spTax.begin(), spTax.end()), spTax.end());
+    const uint32_t S = (uint32_t)spTax.size();
+    std::vector<uint32_t> spIdx(n_maps);
+    std::vector<float> score(n_maps);
+    std::vector<uint64_t> spCnt(S + 1, 0);
+    for (uint64_t j = 0; j < n_maps; j++) {
+        spIdx[j] = (uint32_t)(std::lower_bound(spTax.begin(), spTax.end(), maps[j].species_id) - spTax.begin());
+        score[j] = maps[j].score;
+        spCnt[spIdx[j] + 1]++;
+    }
+    std::vector<uint8_t> isTop(S, 0);
+    for (uint64_t q = 0; q < nQ; q++) isTop[spIdx[qOff[q]]] = 1;
+    uint32_t nTop = 0;
+    for (uint32_t i = 0; i < S; i++) nTop += isTop[i];
+    // species order: each mapping's position (query order inside a species), slices of <= kSlice
+    constexpr uint64_t kSlice = 4096;
+    for (uint32_t i = 0; i < S; i++) spCnt[i + 1] += spCnt[i];
+    std::vector<uint64_t> pos(n_maps), cur(spCnt.begin(), spCnt.end() - 1);
+    for (uint64_t j = 0; j < n_maps; j++) pos[j] = cur[spIdx[j]]++;
+    std::vector<uint64_t> sliceOff, spSlice(S + 1, 0);
+    for (uint32_t i = 0; i < S; i++) {
+        spSlice[i] = sliceOff.size();
+        for (uint64_t a = spCnt[i]; a < spCnt[i + 1]; a += kSlice) sliceOff.push_back(a);
+    }
+    spSlice[S] = sliceOff.size();
+    const uint64_t nSl = sliceOff.size();
+    sliceOff.push_back(n_maps);
+    // length factors 1 / log(k-mers) (0 for a species without DB k-mers), initial abundances
+    int rc = species_kmers(c);
+    if (rc != MTB_OK) return rc;
+    std::vector<double> lf(S), p(S, 0.0);
+    for (uint32_t i = 0; i < S; i++) {
+        const int32_t t = spTax[i];
+        const uint32_t k = t >= 0 && t < (int32_t)c->spKmers.size() ? c->spKmers[(size_t)t] : 0;
+        lf[i] = k > 0 ? 1.0 / log((double)k) : 0.0;
+        if (isTop[i]) p[i] = 1.0 / (double)nTop;
+    }
+    // device arrays
+    DevBuf dScore, dSpIdx, dQOff, dPos, dLf, dP, dPNew, dW, dQc, dSliceOff, dPart, dSpSlice, dTop, dAbsd, dDelta,
+        dSpTax, dQId, dOut;
+    auto up = [&](DevBuf& b, const void* h, size_t bytes) -> hipError_t {
+        hipError_t e = b.ensure(std::max<size_t>(bytes, 8));
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, s);
+        return e;
+    };
+    HIP_TRY(up(dScore, score.data(), 4 * n_maps));
+    HIP_TRY(up(dSpIdx, spIdx.data(), 4 * n_maps));
+    HIP_TRY(up(dQOff, qOff.data(), 8 * qOff.size()));
+    HIP_TRY(up(dPos, pos.data(), 8 * n_maps));
+    HIP_TRY(up(dLf, lf.data(), 8 * S));
+    HIP_TRY(up(dP, p.data(), 8 * S));
+    HIP_TRY(dPNew.ensure(8 * std::max<uint32_t>(S, 1)));
+    HIP_TRY(dW.ensure(8 * std::max<uint64_t>(n_maps, 1)));
+    HIP_TRY(dQc.ensure(8));
+    HIP_TRY(up(dSliceOff, sliceOff.data(), 8 * sliceOff.size()));
+    HIP_TRY(dPart.ensure(8 * std::max<uint64_t>(nSl, 1)));
+    HIP_TRY(up(dSpSlice, spSlice.data(), 8 * spSlice.size()));
+    HIP_TRY(up(dTop, isTop.data(), S));
+    HIP_TRY(dAbsd.ensure(8 * std::max<uint32_t>(S, 1)));
+    HIP_TRY(dDelta.ensure(8));
+    // Classifier.cpp:247-309: at most 1000 iterations, until delta < 1e-6
+    uint32_t iters = 0;
+    double delta = 0.0;
+    unsigned long long qc = 0;
+    double *pa = dP.as<double>(), *pb = dPNew.as<double>();
+    for (uint32_t it = 0; it < 1000; it++) {
+        launch_em_iteration(dScore.as<float>(), dSpIdx.as<uint32_t>(), dQOff.as<uint64_t>(), nQ, dPos.as<uint64_t>(),
+                            pa, dLf.as<double>(), dW.as<double>(), dQc.as<unsigned long long>(),
+                            dSliceOff.as<uint64_t>(), nSl, dPart.as<double>(), dSpSlice.as<uint64_t>(), S,
+                            dTop.as<uint8_t>(), pb, dAbsd.as<double>(), it > 10 ? 1 : 0, dDelta.as<double>(), s);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&delta, dDelta.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&qc, dQc.p, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::swap(pa, pb);  // taxProbs.swap(Fnew)
+        iters++;
+        if (delta < 1e-6) break;
+    }
+    HIP_TRY(hipMemcpy(p.data(), pa, 8 * S, hipMemcpyDeviceToHost));
+    // per-read reassignment (Classifier::reclassify)
+    std::vector<int32_t> spTaxD(spTax.begin(), spTax.end());
+    HIP_TRY(up(dSpTax, spTaxD.data(), 4 * S));
+    HIP_TRY(up(dQId, qId.data(), 4 * nQ));
+    HIP_TRY(dOut.ensure(sizeof(mtb_em_read) * std::max<uint64_t>(total_reads, 1)));
+    HIP_TRY(hipMemsetAsync(dOut.p, 0, sizeof(mtb_em_read) * total_reads, s));
+    TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
+    launch_em_reclassify(dScore.as<float>(), dSpIdx.as<uint32_t>(), dSpTax.as<int32_t>(), dQOff.as<uint64_t>(),
+                         dQId.as<uint32_t>(), nQ, pa, dLf.as<double>(), t, dOut.as<mtb_em_read>(), s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(reads_out, dOut.p, sizeof(mtb_em_read) * total_reads, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // emTaxCounts (Classifier.cpp:312-318): the top species' (unsigned)(p * queryCount)
+    *n_sp = nTop;
+    if (st) {
+        st->query_count = qc;
+        st->iterations = iters;
+        st->n_species = nTop;
+        st->delta = delta;
+    }
+    if (nTop > cap) return MTB_RETRY;
+    uint64_t w = 0;
+    for (uint32_t i = 0; i < S; i++) {
+        if (!isTop[i]) continue;
+        if (sp_ids) sp_ids[w] = spTax[i];
+        if (sp_probs) sp_probs[w] = p[i];
+        if (sp_counts) sp_counts[w] = (unsigned int)(p[i] * (double)qc);
+        w++;
+    }
     return MTB_OK;
 }
 

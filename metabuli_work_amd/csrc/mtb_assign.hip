@@ -1098,6 +1098,7 @@ struct AssignCfg {
     float minScore, minSpScore, tieRatio;
     int generic;  // 1: skip the register fast path (tests)
     int emulateAll;  // 1: k_combine_wave takes the std::sort emulation for every run (tests)
+    int em;          // --em: a classified read keeps its best species (Taxonomer.cpp:193-201)
 };
 
 struct Clade {
@@ -1752,6 +1753,10 @@ __device__ void classify_tail(mtb_result& res, const mtb_taxcnt* __restrict__ tc
         res.classification = tax.exists(bestTax) ? tax.spParent[tax.nodeOf[bestTax]] : 0;
         return;
     }
+    if (cfg.em) {  // no lowerRankClassification under --em
+        res.classification = bestTax;
+        return;
+    }
     const int32_t spT = bestTax;
     long nCl = 0;
     auto findOrAdd = [&](int32_t t) -> long {
@@ -2114,7 +2119,7 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     for (int i = 0; i < 4; i++) hostStats[i] = 0;
     if (nReads == 0) return;
     AssignCfg cfg{a.kmerFormat, a.dnaShift, a.maxCodonShift, a.denominator, a.minConsCnt, a.minConsCntEuk,
-                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic, a.emulateAll};
+                  a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic, a.emulateAll, a.em};
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
     if (nM) {
         const unsigned bm = (unsigned)((nM + 255) / 256);
@@ -2241,6 +2246,197 @@ void launch_regroup_chunks(const mtb_match* src, const uint32_t* cnt, uint32_t n
     exclusive_scan_u32(tot, n, mOff, scanTmp, s);
     exclusive_scan_u32(cnt, (uint64_t)nChunks * n, srcOff, scanTmp, s);
     k_regroup_chunks<<<(n + 3) / 4, 256, 0, s>>>((const uint64_t*)src, cnt, srcOff, nChunks, n, mOff, (uint64_t*)dst);
+}
+
+// ------------------------------------------------------------------------------------------------
+// --em (Classifier.cpp:209-386, Taxonomer.cpp:377-386, Reporter.h:80-92): per classified read its
+// species scores sorted by std::sort (score descending; the comparator is not a total order, so the
+// libstdc++ emulation decides ties), the first ten kept as (species, score^2) "mappings"; then the
+// EM re-estimation of species abundances over all mappings and the per-read reassignment.
+// ------------------------------------------------------------------------------------------------
+struct EmPair {
+    int32_t sp;
+    float sc;
+};
+
+__global__ void k_em_top(const mtb_match* __restrict__ M, const uint64_t* __restrict__ mOff, uint32_t n,
+                         const uint64_t* __restrict__ sScan, const uint64_t* __restrict__ sStart,
+                         const float* __restrict__ spScore, const uint8_t* __restrict__ spKeep,
+                         const mtb_result* __restrict__ results, EmPair* __restrict__ scratch,
+                         EmPair* __restrict__ maps, uint8_t* __restrict__ cnt) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    cnt[r] = 0;
+    if (!results[r].is_classified) return;
+    const uint64_t base = mOff[r], end = mOff[r + 1];
+    const uint64_t s0 = sScan[base], s1 = sScan[end];
+    EmPair* v = scratch + s0;
+    long k = 0;
+    for (uint64_t s = s0; s < s1; s++)  // sp2score in species order (Taxonomer.cpp:330-369)
+        if (spKeep[s]) v[k++] = EmPair{(int32_t)M[sStart[s]].species_id, spScore[s]};
+    stdsort::sort(v, v + k, [](const EmPair& a, const EmPair& b) { return a.sc > b.sc; });
+    const long m = k < kEmTop ? k : kEmTop;
+    for (long i = 0; i < m; i++) maps[(uint64_t)r * kEmTop + i] = EmPair{v[i].sp, v[i].sc * v[i].sc};
+    cnt[r] = (uint8_t)m;
+}
+
+void launch_em_top(const mtb_match* M, const uint64_t* mOff, uint32_t n, const AssignScratch& s,
+                   const mtb_result* results, void* scratch, void* maps, uint8_t* cnt, hipStream_t st) {
+    if (!n) return;
+    k_em_top<<<(n + 255) / 256, 256, 0, st>>>(M, mOff, n, s.sScan, s.sStart, s.spScore, s.spKeep, results,
+                                              (EmPair*)scratch, (EmPair*)maps, cnt);
+}
+
+// DB k-mers per species (Classifier::countUniqueKmerPerSpecies, Classifier.cpp:388-431: every info
+// entry's species, taxID_list mapping; entries without a species are not counted).
+__global__ void k_species_kmers(const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf,
+                                uint32_t maxTax, uint32_t* __restrict__ cnt) {
+    MTB_GRID_STRIDE(i, D) {
+        const uint32_t t = db[i].tax;
+        const int32_t sp = t <= maxTax ? spOf[t] : 0;
+        if (sp > 0) atomicAdd(&cnt[sp], 1u);
+    }
+}
+
+void launch_species_kmers(const DbRec* db, uint64_t D, const int32_t* spOf, uint32_t maxTax, uint32_t* cnt,
+                          hipStream_t s) {
+    if (D) k_species_kmers<<<stride_grid(D), 256, 0, s>>>(db, D, spOf, maxTax, cnt);
+}
+
+// One EM iteration, E step per query (the reference's loop body, Classifier.cpp:268-280): the
+// query's terms score * p * lengthFactor summed in mapping order; a query with a zero sum adds
+// nothing, the others add term / sum to their species. Contributions go to their species-sorted
+// position (pos) so that the per-species sums below read them contiguously, in query order.
+__global__ void k_em_estep(const float* __restrict__ score, const uint32_t* __restrict__ spIdx,
+                           const uint64_t* __restrict__ qOff, uint64_t nQ, const uint64_t* __restrict__ pos,
+                           const double* __restrict__ p, const double* __restrict__ lf, double* __restrict__ wS,
+                           unsigned long long* __restrict__ qCount) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool counted = false;
+    if (q < nQ) {
+        const uint64_t a = qOff[q], b = qOff[q + 1];
+        double denom = 0.0;
+        for (uint64_t j = a; j < b; j++) denom += (double)score[j] * p[spIdx[j]] * lf[spIdx[j]];
+        counted = !(denom == 0.0);
+        for (uint64_t j = a; j < b; j++)
+            wS[pos[j]] = counted ? ((double)score[j] * p[spIdx[j]] * lf[spIdx[j]]) / denom : 0.0;
+    }
+    const int c = __syncthreads_count(counted);
+    if (threadIdx.x == 0 && c) atomicAdd(qCount, (unsigned long long)c);
+}
+
+// Per-species sums of the contributions: slices of <= kEmSlice consecutive entries of one species
+// summed in order, then each species' slices in order (a species of <= kEmSlice entries sums
+// exactly as the sequential loop does). M step (Classifier.cpp:291-309): top species divided by
+// the counted queries, |new - old| for the convergence delta, and after ten iterations abundances
+// below 1e-5 dropped to zero.
+__global__ void k_em_slices(const double* __restrict__ wS, const uint64_t* __restrict__ sliceOff, uint64_t nSl,
+                            double* __restrict__ part) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nSl) return;
+    double f = 0.0;
+    for (uint64_t j = sliceOff[i]; j < sliceOff[i + 1]; j++) f += wS[j];
+    part[i] = f;
+}
+
+__global__ void k_em_mstep(const double* __restrict__ part, const uint64_t* __restrict__ spSlice, uint32_t S,
+                           const uint8_t* __restrict__ isTop, const unsigned long long* __restrict__ qCount,
+                           const double* __restrict__ p, double* __restrict__ pNew, double* __restrict__ absd,
+                           int afterTen) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    double f = 0.0;
+    for (uint64_t k = spSlice[i]; k < spSlice[i + 1]; k++) f += part[k];
+    if (isTop[i]) {
+        f /= (double)*qCount;
+        absd[i] = fabs(f - p[i]);
+        if (afterTen && f < 1e-5) f = 0.0;
+    } else {
+        absd[i] = 0.0;
+    }
+    pNew[i] = f;
+}
+
+// delta = sum of absd in species order: 256 ordered chunk sums, then those in order (fixed order,
+// run to run identical)
+__global__ void __launch_bounds__(256) k_em_delta(const double* __restrict__ absd, uint32_t S, double* __restrict__ out) {
+    __shared__ double part[256];
+    const uint32_t per = (S + 255) / 256, a = threadIdx.x * per, b = min(S, a + per);
+    double d = 0.0;
+    for (uint32_t i = a; i < b; i++) d += absd[i];
+    part[threadIdx.x] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < 256; k++) t += part[k];
+        *out = t;
+    }
+}
+
+void launch_em_iteration(const float* score, const uint32_t* spIdx, const uint64_t* qOff, uint64_t nQ,
+                         const uint64_t* pos, const double* p, const double* lf, double* wS,
+                         unsigned long long* qCount, const uint64_t* sliceOff, uint64_t nSl, double* part,
+                         const uint64_t* spSlice, uint32_t S, const uint8_t* isTop, double* pNew, double* absd,
+                         int afterTen, double* delta, hipStream_t s) {
+    (void)hipMemsetAsync(qCount, 0, sizeof(unsigned long long), s);
+    if (nQ) k_em_estep<<<(unsigned)((nQ + 255) / 256), 256, 0, s>>>(score, spIdx, qOff, nQ, pos, p, lf, wS, qCount);
+    if (nSl) k_em_slices<<<(unsigned)((nSl + 255) / 256), 256, 0, s>>>(wS, sliceOff, nSl, part);
+    if (S) k_em_mstep<<<(S + 255) / 256, 256, 0, s>>>(part, spSlice, S, isTop, qCount, p, pNew, absd, afterTen);
+    k_em_delta<<<1, 256, 0, s>>>(absd, S, delta);
+}
+
+// Classifier::reclassify (Classifier.cpp:326-386) per query: p * score * lengthFactor normalised by
+// their sum, sorted descending (std::sort: emulated), the leading species until the sum reaches 0.5,
+// their LCA. mapped: 1 reassigned (counted in the reclassify report), 2 a zero sum (taxID 0, not
+// counted).
+struct EmPairD {
+    int32_t sp;
+    double pr;
+};
+
+__global__ void k_em_reclassify(const float* __restrict__ score, const uint32_t* __restrict__ spIdx,
+                                const int32_t* __restrict__ spTax, const uint64_t* __restrict__ qOff,
+                                const uint32_t* __restrict__ qId, uint64_t nQ, const double* __restrict__ p,
+                                const double* __restrict__ lf, TaxView tax, mtb_em_read* __restrict__ out) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nQ) return;
+    const uint64_t a = qOff[q], b = qOff[q + 1];
+    EmPairD v[kEmTop];
+    double denom = 0.0;
+    long k = 0;
+    for (uint64_t j = a; j < b && k < kEmTop; j++, k++) {
+        const double sc = p[spIdx[j]] * (double)score[j] * lf[spIdx[j]];
+        denom += sc;
+        v[k] = EmPairD{spTax[spIdx[j]], sc};
+    }
+    mtb_em_read r;
+    r.tax_id = 0;
+    r.score = 0.0;
+    if (denom == 0.0) {
+        r.mapped = 2;
+        out[qId[q]] = r;
+        return;
+    }
+    for (long i = 0; i < k; i++) v[i].pr /= denom;
+    stdsort::sort(v, v + k, [](const EmPairD& x, const EmPairD& y) { return x.pr > y.pr; });
+    double sum = 0.0;
+    int lcaNode = -1;
+    for (long i = 0; i < k && sum < 0.5; i++) {
+        sum += v[i].pr;
+        const int32_t t = v[i].sp;
+        if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
+    }
+    r.tax_id = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
+    r.score = sum;
+    r.mapped = 1;
+    out[qId[q]] = r;
+}
+
+void launch_em_reclassify(const float* score, const uint32_t* spIdx, const int32_t* spTax, const uint64_t* qOff,
+                          const uint32_t* qId, uint64_t nQ, const double* p, const double* lf, const TaxDevice& t,
+                          mtb_em_read* out, hipStream_t s) {
+    TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
+    if (nQ) k_em_reclassify<<<(unsigned)((nQ + 255) / 256), 256, 0, s>>>(score, spIdx, spTax, qOff, qId, nQ, p, lf, tv, out);
 }
 
 }  // namespace mtb

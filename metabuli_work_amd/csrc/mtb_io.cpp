@@ -286,4 +286,70 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
     return MTB_OK;
 }
 
+int mtb_write_em_results(mtb_ctx* ctx, const char* path, const char* classification_tsv, const mtb_em_read* reads,
+                         uint64_t n_reads, uint32_t flags) {
+    if (!ctx || !path || !classification_tsv || (!reads && n_reads)) return MTB_ERR_ARG;
+    // Classifier::loadOriginalResults (Classifier.cpp:450-480): name = column 2, query_length =
+    // column 4 of each non-comment line of the classification TSV
+    FILE* in = fopen(classification_tsv, "rb");
+    if (!in) {
+        mtb::set_error(std::string("cannot read ") + classification_tsv);
+        return MTB_ERR_IO;
+    }
+    FILE* f = fopen(path, "wb");
+    if (!f) {
+        fclose(in);
+        mtb::set_error(std::string("cannot write ") + path);
+        return MTB_ERR_IO;
+    }
+    const bool lineage = (flags & MTB_WRITE_LINEAGE) != 0;
+    fputs(lineage ? "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage\n"
+                  : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\n", f);
+    std::string o;
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t len;
+    uint64_t i = 0;
+    char tmp[96];
+    while ((len = getline(&line, &cap, in)) >= 0) {
+        if (len && line[len - 1] == '\n') line[--len] = 0;
+        if (len == 0 || line[0] == '#') continue;
+        const char* c0 = line;
+        const char* t1 = strchr(c0, '\t');
+        const char* t2 = t1 ? strchr(t1 + 1, '\t') : nullptr;
+        const char* t3 = t2 ? strchr(t2 + 1, '\t') : nullptr;
+        if (!t3) continue;  // "Invalid line format" (fewer than 4 columns): skipped
+        const std::string name(t1 + 1, t2);
+        const int length = atoi(t3 + 1);
+        const mtb_em_read r = i < n_reads ? reads[i] : mtb_em_read{0, 0, 0.0};
+        i++;
+        o += r.tax_id != 0 ? "1\t" : "0\t";
+        o += name;
+        snprintf(tmp, sizeof tmp, "\t%d\t%d\t%g\t", mtb_original_taxid(ctx, r.tax_id), length, r.score);
+        o += tmp;
+        if (r.tax_id != 0) {
+            o += mtb_taxon_rank(ctx, r.tax_id);
+            if (lineage) {
+                o += '\t';
+                o += mtb_taxon_lineage(ctx, r.tax_id);
+            }
+        } else {
+            o += lineage ? "-\t-" : "-";
+        }
+        o += '\n';
+        if (o.size() > (1u << 22)) {
+            fwrite(o.data(), 1, o.size(), f);
+            o.clear();
+        }
+    }
+    free(line);
+    fclose(in);
+    fwrite(o.data(), 1, o.size(), f);
+    if (fclose(f) != 0) {
+        mtb::set_error(std::string("write failed: ") + path);
+        return MTB_ERR_IO;
+    }
+    return MTB_OK;
+}
+
 }  // extern "C"

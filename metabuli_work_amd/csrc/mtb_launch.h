@@ -35,6 +35,7 @@ struct AssignArgs {
     int generic;  // MTB_FORCE_GENERIC: general code paths only (parity tests of the fallbacks)
     int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread per read, 1 wave per read (K6 chooseBestTaxon)
     int emulateAll = 0;  // MTB_EMULATE_SORT=1: every k_combine_wave run takes the std::sort emulation (tests)
+    int em = 0;          // --em: classified reads keep their best species; mappings for the EM
 };
 
 struct AssignScratch {  // per match unless noted
@@ -281,5 +282,27 @@ void launch_regroup_chunks(const mtb_match* src, const uint32_t* cnt, uint32_t n
 void launch_taxcnt_len(const mtb_result* results, uint32_t nReads, uint32_t* len, hipStream_t s);
 void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_result* results, const uint64_t* tcOff,
                            uint32_t nReads, mtb_taxcnt* out, hipStream_t s);
+
+// --em (mtb_assign.hip): per classified read its first kEmTop species by score (std::sort order)
+// as (species, score^2) into maps[r * kEmTop ..] (8-B {species, float}), cnt[r] of them; scratch:
+// 8 B per species run of the batch.
+constexpr int kEmTop = 10;
+void launch_em_top(const mtb_match* M, const uint64_t* mOff, uint32_t n, const AssignScratch& s,
+                   const mtb_result* results, void* scratch, void* maps, uint8_t* cnt, hipStream_t st);
+// DB k-mers per species taxID (cnt: maxTax + 1 u32, zeroed by the caller)
+void launch_species_kmers(const DbRec* db, uint64_t D, const int32_t* spOf, uint32_t maxTax, uint32_t* cnt,
+                          hipStream_t s);
+// One EM iteration over nQ queries' mappings (qOff: their ranges; spIdx: dense species; pos: each
+// mapping's position in species order; sliceOff: nSl slices of one species each; spSlice: each
+// species' slices): p -> pNew, *delta = sum |pNew - p| over the top species.
+void launch_em_iteration(const float* score, const uint32_t* spIdx, const uint64_t* qOff, uint64_t nQ,
+                         const uint64_t* pos, const double* p, const double* lf, double* wS,
+                         unsigned long long* qCount, const uint64_t* sliceOff, uint64_t nSl, double* part,
+                         const uint64_t* spSlice, uint32_t S, const uint8_t* isTop, double* pNew, double* absd,
+                         int afterTen, double* delta, hipStream_t s);
+// reassignment of each query (qId: its read) from the final abundances
+void launch_em_reclassify(const float* score, const uint32_t* spIdx, const int32_t* spTax, const uint64_t* qOff,
+                          const uint32_t* qId, uint64_t nQ, const double* p, const double* lf, const TaxDevice& t,
+                          mtb_em_read* out, hipStream_t s);
 
 }  // namespace mtb

@@ -343,6 +343,9 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
         }
     });
 
+    // --em outputs requested: the mappings of every batch (Reporter::writeMappings)
+    const bool em = opt->em_tsv || opt->em_report_tsv || opt->em_reclassify_report_tsv;
+    std::vector<mtb_em_map> emMaps;
     // the GPU stage on the calling thread
     uint64_t reads = 0, bases = 0, batches = 0;
     double gpuS = 0, waitS = 0;
@@ -368,6 +371,20 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
             mtb_get_taxcnt(ctx, nullptr, 0, &nt);
             s->tc.resize(std::max<uint64_t>(nt, 1));
             rc = mtb_get_taxcnt(ctx, s->tc.data(), s->tc.size(), &nt);
+        }
+        if (rc == MTB_OK && em) {
+            if (reads + s->n > 0xFFFFFFFFull) {
+                rc = MTB_ERR_ARG;
+                mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
+            } else {
+                uint64_t nm = 0;
+                rc = mtb_get_em_mappings(ctx, (uint32_t)reads, nullptr, 0, &nm);
+                if (rc == MTB_RETRY || (rc == MTB_OK && nm)) {
+                    const size_t at = emMaps.size();
+                    emMaps.resize(at + nm);
+                    rc = mtb_get_em_mappings(ctx, (uint32_t)reads, emMaps.data() + at, nm, &nm);
+                }
+            }
         }
         gpuS += secs(g0, Clock::now());
         if (rc != MTB_OK) {
@@ -403,6 +420,45 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
         }
         const int rc = mtb_write_report(ctx, opt->report_tsv, reads, ids.data(), cnt.data(), ids.size());
         if (rc != MTB_OK) return rc;
+    }
+    if (em) {  // Classifier.cpp:152-161: EM, the reassigned reads and both EM reports
+        std::vector<mtb_em_read> er(std::max<uint64_t>(reads, 1));
+        const size_t cap = emMaps.size() + 1;
+        std::vector<int32_t> spIds(cap);
+        std::vector<double> spP(cap);
+        std::vector<uint32_t> spC(cap);
+        uint64_t nSp = 0;
+        mtb_em_stats est{};
+        int rc = mtb_em(ctx, emMaps.data(), emMaps.size(), reads, er.data(), spIds.data(), spP.data(), spC.data(), cap,
+                        &nSp, &est);
+        if (rc != MTB_OK) return rc;
+        if (opt->em_tsv) {
+            rc = mtb_write_em_results(ctx, opt->em_tsv, opt->out_tsv, er.data(), reads, opt->write_flags);
+            if (rc != MTB_OK) return rc;
+        }
+        if (opt->em_report_tsv) {  // emTaxCounts: the top species, taxID 0 = the reads they leave unexplained
+            std::vector<int32_t> ids(spIds.begin(), spIds.begin() + nSp);
+            std::vector<uint32_t> cnt(spC.begin(), spC.begin() + nSp);
+            uint64_t explained = 0;
+            for (uint32_t c : cnt) explained += c;
+            ids.push_back(0);
+            cnt.push_back((uint32_t)(reads - explained));
+            rc = mtb_write_report(ctx, opt->em_report_tsv, reads, ids.data(), cnt.data(), ids.size());
+            if (rc != MTB_OK) return rc;
+        }
+        if (opt->em_reclassify_report_tsv) {  // reclassifyTaxCounts: the reassigned reads per taxID
+            std::map<int32_t, uint64_t> rc2;
+            for (uint64_t i = 0; i < reads; i++)
+                if (er[i].mapped == 1) rc2[er[i].tax_id]++;
+            std::vector<int32_t> ids;
+            std::vector<uint32_t> cnt;
+            for (auto& kv : rc2) {
+                ids.push_back(kv.first);
+                cnt.push_back((uint32_t)kv.second);
+            }
+            rc = mtb_write_report(ctx, opt->em_reclassify_report_tsv, reads, ids.data(), cnt.data(), ids.size());
+            if (rc != MTB_OK) return rc;
+        }
     }
     if (stats) {
         stats->reads = reads;

@@ -173,7 +173,14 @@ void orc_sort_matches(mtb_match* m, uint64_t n) {
     memcpy(m, v.data(), n * sizeof(mtb_match));
 }
 
+// --em: the last assignment's mappings (Reporter::writeMappings, Reporter.h:80-92), batch read indices
+static std::vector<mtb_em_map> g_lastMaps;
+
 static int exportResults(const std::vector<Query>& q, mtb_result* out, mtb_taxcnt* tc, uint64_t cap, uint64_t* n_tc) {
+    g_lastMaps.clear();
+    for (size_t i = 0; i < q.size(); i++)
+        if (q[i].isClassified)
+            for (auto& sp : q[i].species2Score) g_lastMaps.push_back(mtb_em_map{(uint32_t)i, sp.first, sp.second});
     uint64_t w = 0;
     bool overflow = false;
     for (size_t i = 0; i < q.size(); i++) {
@@ -237,6 +244,35 @@ int orc_classify(void* dbp, const mtb_params* par, const char* seq1, const uint6
         counts[1] = m.size();
     }
     return exportResults(q, out, tc, cap, n_tc);
+}
+
+// The last orc_classify / orc_assign's mappings (read indices of that batch).
+int orc_last_em_maps(mtb_em_map* out, uint64_t cap, uint64_t* n) {
+    *n = g_lastMaps.size();
+    if (g_lastMaps.size() > cap) return MTB_RETRY;
+    if (!g_lastMaps.empty()) memcpy(out, g_lastMaps.data(), g_lastMaps.size() * sizeof(mtb_em_map));
+    return MTB_OK;
+}
+
+// Classifier::em + reclassify: reads_out (total_reads), the top species' final abundance and
+// emTaxCounts (ascending taxID; cap entries), stats[0] = queryCount, stats[1] = iterations.
+int orc_em(void* dbp, const mtb_em_map* maps, uint64_t n, uint64_t total_reads, mtb_em_read* reads_out,
+           int32_t* sp_ids, double* sp_probs, uint32_t* sp_counts, uint64_t cap, uint64_t* n_sp, uint64_t* stats) {
+    EmOut o;
+    emReassign(*static_cast<Db*>(dbp), maps, n, total_reads, o);
+    memcpy(reads_out, o.reads.data(), total_reads * sizeof(mtb_em_read));
+    *n_sp = o.probs.size();
+    stats[0] = o.queryCount;
+    stats[1] = o.iterations;
+    if (o.probs.size() > cap) return MTB_RETRY;
+    uint64_t w = 0;
+    for (auto& kv : o.probs) {
+        sp_ids[w] = kv.first;
+        sp_probs[w] = kv.second;
+        sp_counts[w] = o.emTaxCounts[kv.first];
+        w++;
+    }
+    return MTB_OK;
 }
 
 int orc_threads(void) {

@@ -38,6 +38,8 @@ struct Query {
     bool isClassified = false;
     bool newSpecies = false;
     std::map<TaxID, int> taxCnt;
+    TaxID topSpeciesId = 0;                             // --em (common.h:104,110)
+    std::vector<std::pair<TaxID, float>> species2Score;
 };
 
 struct Reads {
@@ -60,6 +62,17 @@ bool compareMatches(const mtb_match& a, const mtb_match& b);
 // Classifier::assignTaxonomy (Classifier.cpp:166-208) with Taxonomer::chooseBestTaxon.
 void assignTaxonomy(const Db& db, const mtb_params& par, const mtb_match* matches, size_t n,
                     std::vector<Query>& queries);
+
+// --em (Classifier.cpp:209-386) over the mappings of all batches (MappingRes = mtb_em_map), one
+// thread: the reference's OpenMP sums in the order a single thread takes them.
+struct EmOut {
+    std::vector<mtb_em_read> reads;  // per read
+    std::map<TaxID, double> probs;   // top species -> final abundance
+    std::map<TaxID, unsigned int> emTaxCounts;
+    uint64_t queryCount = 0;
+    uint32_t iterations = 0;
+};
+void emReassign(const Db& db, const mtb_em_map* maps, size_t n, size_t totalReads, EmOut& out);
 
 // Synthetic reference DB writer (IndexCreator restatement, orc_dbwriter.cpp).
 struct BuildInput {

@@ -2,6 +2,7 @@
 // Classifier::assignTaxonomy (Classifier.cpp:166-208) and Taxonomer (Taxonomer.cpp:12-713,
 // Taxonomer.h:15-59), Match score helpers (Match.h:32-86).
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <limits>
 
@@ -162,7 +163,8 @@ void Taxonomer::chooseBestTaxon(uint32_t currentQuery, size_t offset, size_t end
     }
     q.isClassified = true; q.score = speciesScore.score; q.hammingDist = speciesScore.hammingDist;
     q.newSpecies = false;
-    q.classification = lowerRankClassification(speciesScore.taxId, q.queryLength + q.queryLength2);
+    q.classification = par.em ? speciesScore.taxId  // :193-201
+                              : lowerRankClassification(speciesScore.taxId, q.queryLength + q.queryLength2);
 }
 
 void Taxonomer::filterRedundantMatches(const mtb_match* ml, const std::pair<size_t, size_t>& range,
@@ -264,6 +266,13 @@ TaxonScore Taxonomer::getBestSpeciesMatches(std::pair<size_t, size_t>& bestSpeci
         }
     }
     if (meaningfulSpecies == 0) { bestScore.score = 0; return bestScore; }
+    if (par.em && !sp2score.empty()) {  // :377-386
+        std::sort(sp2score.begin(), sp2score.end(),
+                  [](const std::pair<TaxID, float>& a, const std::pair<TaxID, float>& b) { return a.second > b.second; });
+        query.topSpeciesId = sp2score[0].first;
+        for (size_t k = 0; k < 10 && k < sp2score.size(); k++)
+            query.species2Score.emplace_back(sp2score[k].first, sp2score[k].second * sp2score[k].second);
+    }
     maxSpecies.clear();
     for (size_t k = 0; k < sp2score.size(); k++) {
         if (sp2score[k].second >= bestSpScore * tieRatio) {
@@ -405,6 +414,91 @@ void assignTaxonomy(const Db& db, const mtb_params& par, const mtb_match* matchL
 #pragma omp for schedule(dynamic, 1)
         for (size_t i = 0; i < blocks.size(); ++i)
             t.chooseBestTaxon(blocks[i].id - 1, blocks[i].start, blocks[i].end, matchList, queryList);
+    }
+}
+
+}  // namespace orc
+
+namespace orc {
+
+void emReassign(const Db& db, const mtb_em_map* maps, size_t n, size_t totalQueryCnt, EmOut& out) {
+    // countUniqueKmerPerSpecies (Classifier.cpp:388-431): every info entry's species
+    std::unordered_map<TaxID, uint32_t> sp2uniq;
+    for (uint32_t t : db.info) {
+        if (t == 0) break;  // ReadBuffer<TaxID>::getNext() == 0 ends the loop
+        auto it = db.taxId2speciesId.find((TaxID)t);
+        if (it != db.taxId2speciesId.end() && it->second) sp2uniq[it->second]++;
+    }
+    auto lengthFactor = [&](TaxID sp) {
+        auto it = sp2uniq.find(sp);
+        return (it != sp2uniq.end() && it->second > 0) ? 1.0 / log((double)it->second) : 0.0;
+    };
+    std::vector<std::pair<size_t, size_t>> queryRanges;  // :224-233
+    for (size_t idx = 0; idx < n;) {
+        const uint32_t cur = maps[idx].query_id;
+        const size_t start = idx;
+        while (idx < n && maps[idx].query_id == cur) idx++;
+        queryRanges.emplace_back(start, idx);
+    }
+    std::map<TaxID, double> taxProbs, Fnew;  // species ascending (the reference's unordered_set order is arbitrary)
+    std::vector<TaxID> spList;
+    for (auto& r : queryRanges) taxProbs[maps[r.first].species_id] = 0;  // topSpeciesSet
+    for (auto& kv : taxProbs) spList.push_back(kv.first);
+    for (TaxID sp : spList) { taxProbs[sp] = 1.0 / spList.size(); Fnew[sp] = 0.0; }
+    auto prob = [&](TaxID sp) { auto it = taxProbs.find(sp); return it == taxProbs.end() ? 0.0 : it->second; };
+    size_t queryCount = 0;
+    for (size_t iter = 0; iter < 1000; ++iter) {  // :247-309
+        for (auto& kv : Fnew) kv.second = 0.0;
+        queryCount = 0;
+        for (auto& r : queryRanges) {
+            double denom = 0.0;
+            for (size_t j = r.first; j < r.second; ++j)
+                denom += maps[j].score * prob(maps[j].species_id) * lengthFactor(maps[j].species_id);
+            if (denom == 0.0) continue;
+            queryCount++;
+            for (size_t j = r.first; j < r.second; ++j)
+                Fnew[maps[j].species_id] +=
+                    (maps[j].score * prob(maps[j].species_id) * lengthFactor(maps[j].species_id)) / denom;
+        }
+        for (TaxID sp : spList) Fnew[sp] /= queryCount;
+        double delta = 0.0;
+        for (TaxID sp : spList) {
+            delta += fabs(Fnew[sp] - taxProbs[sp]);
+            if (iter > 10 && Fnew[sp] < 1e-5) Fnew[sp] = 0.0;
+        }
+        taxProbs.swap(Fnew);
+        out.iterations = (uint32_t)iter + 1;
+        if (delta < 1e-6) break;
+    }
+    size_t explained = 0;  // :312-318
+    for (TaxID sp : spList) {
+        out.probs[sp] = taxProbs[sp];
+        out.emTaxCounts[sp] = (unsigned int)(taxProbs[sp] * queryCount);
+        explained += out.emTaxCounts[sp];
+    }
+    out.emTaxCounts[0] = (unsigned int)(totalQueryCnt - explained);
+    out.queryCount = queryCount;
+    out.reads.assign(totalQueryCnt, mtb_em_read{0, 0, 0.0});
+    for (auto& r : queryRanges) {  // reclassify (:326-372)
+        const uint32_t q = maps[r.first].query_id;
+        double denom = 0.0;
+        std::vector<std::pair<TaxID, double>> sp2prob;
+        for (size_t j = r.first; j < r.second; ++j) {
+            const double sc = prob(maps[j].species_id) * maps[j].score * lengthFactor(maps[j].species_id);
+            denom += sc;
+            sp2prob.emplace_back(maps[j].species_id, sc);
+        }
+        if (denom == 0.0) { out.reads[q] = mtb_em_read{0, 2, 0.0}; continue; }
+        for (auto& sp : sp2prob) sp.second /= denom;
+        std::sort(sp2prob.begin(), sp2prob.end(),
+                  [](const std::pair<TaxID, double>& a, const std::pair<TaxID, double>& b) { return a.second > b.second; });
+        double sum = 0.0;
+        std::vector<TaxID> cand;
+        for (size_t j = 0; j < sp2prob.size() && sum < 0.5; ++j) {
+            sum += sp2prob[j].second;
+            cand.push_back(sp2prob[j].first);
+        }
+        out.reads[q] = mtb_em_read{db.tax.LCA(cand)->taxId, 1, sum};
     }
 }
 

@@ -48,6 +48,8 @@ def lib():
         L.orc_genetic_tables.argtypes = [vp, vp, vp, vp]
         L.orc_write_report.argtypes = [vp, ctypes.c_char_p, i32, vp, vp, u64]
         L.orc_write_report.restype = i32
+        L.orc_last_em_maps.argtypes = [vp, u64, ctypes.POINTER(u64)]
+        L.orc_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]
         _LIB = L
     return _LIB
 
@@ -196,3 +198,34 @@ def write_report(db: OracleDb, path: str, total_reads: int, tax_counts: dict) ->
     cnt = np.fromiter(tax_counts.values(), np.uint32, len(tax_counts))
     if lib().orc_write_report(db.h, path.encode(), total_reads, ids.ctypes.data, cnt.ctypes.data, len(ids)) != 0:
         raise RuntimeError("orc_write_report failed")
+
+
+def last_em_maps():
+    """The last classify/assign call's --em mappings (read indices of that batch)."""
+    from metabuli_work_amd import _abi
+    n = ctypes.c_uint64(0)
+    lib().orc_last_em_maps(None, 0, ctypes.byref(n))
+    out = np.zeros(n.value, _abi.EM_MAP_DTYPE)
+    if n.value:
+        lib().orc_last_em_maps(out.ctypes.data, len(out), ctypes.byref(n))
+    return out
+
+
+def em(db, maps, total_reads):
+    """Classifier::em + reclassify restated on one thread (oracle/orc_taxonomer.cpp)."""
+    from metabuli_work_amd import _abi
+    maps = np.ascontiguousarray(maps, _abi.EM_MAP_DTYPE)
+    reads = np.zeros(max(int(total_reads), 1), _abi.EM_READ_DTYPE)
+    cap = len(maps) + 1
+    ids = np.zeros(cap, np.int32)
+    probs = np.zeros(cap, np.float64)
+    cnts = np.zeros(cap, np.uint32)
+    nsp = ctypes.c_uint64(0)
+    st = np.zeros(2, np.uint64)
+    rc = lib().orc_em(db.h, maps.ctypes.data if len(maps) else None, len(maps), int(total_reads), reads.ctypes.data,
+                      ids.ctypes.data, probs.ctypes.data, cnts.ctypes.data, cap, ctypes.byref(nsp), st.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("orc_em failed")
+    k = int(nsp.value)
+    sp = {int(ids[i]): (float(probs[i]), int(cnts[i])) for i in range(k)}
+    return reads[:int(total_reads)], sp, {"query_count": int(st[0]), "iterations": int(st[1])}

@@ -1,0 +1,283 @@
+"""--em: EM re-estimation of species abundances and read reassignment.
+
+Reference: Taxonomer::getBestSpeciesMatches keeps, per classified read, its species sorted by
+score (std::sort) and the first ten as (species, score^2) (Taxonomer.cpp:377-386); chooseBestTaxon
+classifies to the best species without the lower-rank BFS (:193-201); Reporter::writeMappings
+stores them (Reporter.h:80-92); Classifier::em iterates the abundances and Classifier::reclassify
+reassigns each read to the LCA of its leading species (Classifier.cpp:209-386).
+
+The oracle restates all of it on one thread; a pure-Python restatement below checks the oracle's
+EM (CPU). The GPU tests hold the device mappings and results to the oracle bit for bit, the
+device EM to the oracle's (abundances within 1e-12 relative: the device sums large species in
+fixed slices, the reference's OpenMP sums in thread order, so no bitwise order exists), and the
+native pipeline's EM files to the oracle's. Parity unpinned beyond the restatements (no reference
+fixtures for --em).
+"""
+import collections
+import math
+
+import numpy as np
+import pytest
+
+from metabuli_work_amd import _abi, synth
+from metabuli_work_amd.classifier import Classifier, LocalParameters
+from tests import oracle_ctypes as oc
+from tests.test_gpu_parity import _reads, compare_results
+
+SEQ_MODE = {"paired": 2, "single": 1, "long": 3}
+
+
+def _par(db_dir, kind, em=1):
+    par = LocalParameters(seqMode=SEQ_MODE[kind], em=em)
+    par.load_db_parameters(db_dir)
+    return par
+
+
+def _batches(gen, kind, seed, sizes):
+    return [_reads(gen, kind, n, seed + i) for i, n in enumerate(sizes)]
+
+
+def _oracle_maps(odb, par, batches):
+    maps, results, off = [], [], 0
+    for r in batches:
+        ores, otc = oc.classify(odb, par.to_c(), r)
+        m = oc.last_em_maps()
+        m["query_id"] += off
+        maps.append(m)
+        results.append((ores, otc))
+        off += r.n
+    return np.concatenate(maps), results, off
+
+
+class _Tax:
+    def __init__(self, taxo):
+        self.parent = dict(zip(taxo.taxid.tolist(), taxo.parent.tolist()))
+        self.rank = dict(zip(taxo.taxid.tolist(), taxo.rank))
+
+    def species(self, t):
+        while t in self.parent:
+            if self.rank[t] == "species":
+                return t
+            if self.parent[t] == t:
+                return 0
+            t = self.parent[t]
+        return 0
+
+    def path(self, t):
+        p = [t]
+        while self.parent[t] != t:
+            t = self.parent[t]
+            p.append(t)
+        return p
+
+    def lca(self, ts):
+        common = None
+        for t in ts:
+            p = self.path(t)
+            common = p if common is None else [x for x in common if x in set(p)]
+        return common[0]
+
+
+def py_em(maps, sp_kmers, tax, total):
+    """Classifier::em + reclassify in Python (one thread, dict semantics)."""
+    lf = {s: (1.0 / math.log(k) if k > 0 else 0.0) for s, k in sp_kmers.items()}
+    ranges = []
+    i = 0
+    while i < len(maps):
+        j = i
+        while j < len(maps) and maps[j]["query_id"] == maps[i]["query_id"]:
+            j += 1
+        ranges.append((i, j))
+        i = j
+    top = sorted({int(maps[a]["species_id"]) for a, _ in ranges})
+    p = {s: 1.0 / len(top) for s in top}
+    rows = [[(int(maps[k]["species_id"]), float(maps[k]["score"])) for k in range(a, b)] for a, b in ranges]
+    qc = 0
+    iters = 0
+    for it in range(1000):
+        f = {s: 0.0 for s in top}
+        qc = 0
+        for row in rows:
+            den = 0.0
+            for s, sc in row:
+                den += sc * p.get(s, 0.0) * lf.get(s, 0.0)
+            if den == 0.0:
+                continue
+            qc += 1
+            for s, sc in row:
+                f[s] = f.get(s, 0.0) + (sc * p.get(s, 0.0) * lf.get(s, 0.0)) / den
+        for s in top:
+            f[s] /= qc
+        delta = 0.0
+        for s in top:
+            delta += abs(f[s] - p[s])
+            if it > 10 and f[s] < 1e-5:
+                f[s] = 0.0
+        p = f
+        iters = it + 1
+        if delta < 1e-6:
+            break
+    counts = {s: int(p[s] * qc) for s in top}
+    reads = np.zeros(total, _abi.EM_READ_DTYPE)
+    for (a, _), row in zip(ranges, rows):
+        q = int(maps[a]["query_id"])
+        sc = [(s, p.get(s, 0.0) * v * lf.get(s, 0.0)) for s, v in row]
+        den = 0.0
+        for _, v in sc:
+            den += v
+        if den == 0.0:
+            reads[q] = (0, 2, 0.0)
+            continue
+        pr = sorted(((s, v / den) for s, v in sc), key=lambda x: -x[1])  # <= 16: libstdc++ insertion sort, stable
+        tot, cand = 0.0, []
+        for s, v in pr:
+            if tot >= 0.5:
+                break
+            tot += v
+            cand.append(s)
+        reads[q] = (tax.lca(cand), 1, tot)
+    return reads, {s: (p[s], counts[s]) for s in top}, {"query_count": qc, "iterations": iters}
+
+
+def _sp_kmers(db_dir, tax):
+    info = np.fromfile(f"{db_dir}/info", np.uint32)
+    cnt = collections.Counter()
+    for t, k in zip(*np.unique(info, return_counts=True)):
+        s = tax.species(int(t))
+        if s:
+            cnt[s] += int(k)
+    return cnt
+
+
+def _check_maps(maps, results):
+    """Per query: <= 10 mappings, scores (squares) non-increasing; classified reads only."""
+    ores = np.concatenate([r[0] for r in results])
+    q, starts, counts = np.unique(maps["query_id"], return_index=True, return_counts=True)
+    assert counts.max() <= 10
+    assert np.all(ores["is_classified"][q] == 1)
+    for a, c in zip(starts, counts):
+        sc = maps["score"][a:a + c]
+        assert np.all(sc[:-1] >= sc[1:])
+
+
+@pytest.mark.parametrize("db_name,kind", [("fmt2_acc", "paired"), ("fmt2", "long")])
+def test_oracle_em_against_python(make_db, db_name, kind):
+    """CPU: the oracle's EM and reassignment equal an independent Python restatement."""
+    db_dir, taxo, gen = make_db(db_name)
+    par = _par(db_dir, kind)
+    odb = oc.OracleDb(db_dir)
+    maps, results, total = _oracle_maps(odb, par, _batches(gen, kind, 71, [300, 200] if kind != "long" else [20, 15]))
+    assert len(maps) > 0
+    _check_maps(maps, results)
+    got_reads, got_sp, got_st = oc.em(odb, maps, total)
+    odb.close()
+    tax = _Tax(taxo)
+    want_reads, want_sp, want_st = py_em(maps, _sp_kmers(db_dir, tax), tax, total)
+    assert got_st == want_st
+    assert got_sp.keys() == want_sp.keys()
+    for s, (pr, c) in want_sp.items():
+        assert got_sp[s][0] == pytest.approx(pr, rel=1e-13, abs=1e-300) and got_sp[s][1] == c
+    assert np.array_equal(got_reads["tax_id"], want_reads["tax_id"])
+    assert np.array_equal(got_reads["mapped"], want_reads["mapped"])
+    assert np.allclose(got_reads["score"], want_reads["score"], rtol=1e-13, atol=0)
+    assert (got_reads["mapped"] == 1).sum() > total // 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("db_name,kind", [("fmt2_acc", "paired"), ("fmt2", "single"), ("fmt2_syncmer", "paired"),
+                                          ("fmt1_acc", "paired"), ("fmt2", "long")])
+def test_em_device(make_db, db_name, kind):
+    """Device --em: per-batch results and mappings bit-exact vs the oracle; mtb_em vs the oracle's
+    EM on the same mappings."""
+    db_dir, taxo, gen = make_db(db_name)
+    par = _par(db_dir, kind)
+    odb = oc.OracleDb(db_dir)
+    batches = _batches(gen, kind, 81, [400, 250] if kind != "long" else [25, 15])
+    maps, results, total = _oracle_maps(odb, par, batches)
+    gmaps, off = [], 0
+    with Classifier(par, db_dir=db_dir) as clf:
+        for r, (ores, otc) in zip(batches, results):
+            br = clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+            compare_results(br.results, br.taxcnt, ores, otc)
+            gmaps.append(clf.em_mappings(off))
+            off += r.n
+        gm = np.concatenate(gmaps)
+        assert np.array_equal(gm["query_id"], maps["query_id"])
+        assert np.array_equal(gm["species_id"], maps["species_id"])
+        assert np.array_equal(gm["score"].view(np.uint32), maps["score"].view(np.uint32))
+        g_reads, g_sp, g_st = clf.em(maps, total)
+    o_reads, o_sp, o_st = oc.em(odb, maps, total)
+    odb.close()
+    assert g_st["query_count"] == o_st["query_count"] and g_st["iterations"] == o_st["iterations"]
+    assert g_sp.keys() == o_sp.keys()
+    for s, (pr, c) in o_sp.items():
+        assert g_sp[s][0] == pytest.approx(pr, rel=1e-12, abs=1e-300)
+        assert abs(g_sp[s][1] - c) <= (0 if abs(pr * o_st["query_count"] - round(pr * o_st["query_count"])) > 1e-6 else 1)
+    assert np.array_equal(g_reads["tax_id"], o_reads["tax_id"])
+    assert np.array_equal(g_reads["mapped"], o_reads["mapped"])
+    assert np.allclose(g_reads["score"], o_reads["score"], rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_em_rejects_bad_mappings(make_db):
+    db_dir, taxo, gen = make_db("fmt2")
+    par = _par(db_dir, "paired")
+    m = np.zeros(3, _abi.EM_MAP_DTYPE)
+    m["query_id"] = [2, 1, 1]
+    m["species_id"] = int(taxo.taxid[-1])
+    with Classifier(par, db_dir=db_dir) as clf:
+        with pytest.raises(Exception):
+            clf.em(m, 3)  # not in query order
+        m["query_id"] = [0, 1, 5]
+        with pytest.raises(Exception):
+            clf.em(m, 3)  # past total_reads
+
+
+@pytest.mark.gpu
+def test_start_classify_em(make_db, tmp_path):
+    """The native pipeline with --em: the classification TSV, the reassigned-reads TSV and both EM
+    reports, against the oracle's classification, EM and report writer."""
+    db_dir, taxo, gen = make_db("fmt2_acc")
+    r = synth.make_reads(gen, 1500, paired=True, seed=91, short_frac=0.02)
+    p1, p2 = str(tmp_path / "q1.fq.gz"), str(tmp_path / "q2.fq.gz")
+    synth.write_compressed(p1, synth.fastq_bytes(r.seq1, r.off1, prefix="q"), "bgzf")
+    synth.write_compressed(p2, synth.fastq_bytes(r.seq2, r.off2, prefix="q"), "bgzf")
+    par = LocalParameters(seqMode=2, em=1, printLineage=1, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    out, em_tsv = str(tmp_path / "cls.tsv"), str(tmp_path / "em.tsv")
+    em_rep, rc_rep = str(tmp_path / "em_report.tsv"), str(tmp_path / "em_rc_report.tsv")
+    with Classifier(par, db_dir=db_dir) as clf:
+        assert clf.startClassify(out, reads_per_batch=600, em_tsv=em_tsv, em_report_tsv=em_rep,
+                                 em_reclassify_report_tsv=rc_rep) == r.n
+        assert clf.last_run["batches"] == 3
+        lineage = {t: clf.lineage(t) for t in taxo.taxid.tolist()}
+    odb = oc.OracleDb(db_dir)
+    maps, results, total = _oracle_maps(odb, par, [synth.Reads(r.seq1, r.off1, r.seq2, r.off2, r.origin)])
+    o_reads, o_sp, o_st = oc.em(odb, maps, total)
+    ores = results[0][0]
+    # EM report: emTaxCounts + taxID 0 = the reads the top species leave unexplained
+    cnt = {s: c for s, (_, c) in o_sp.items()}
+    cnt[0] = total - sum(cnt.values())
+    want_rep = str(tmp_path / "o_em_report.tsv")
+    oc.write_report(odb, want_rep, total, cnt)
+    assert open(em_rep).read() == open(want_rep).read()
+    rc = collections.Counter(int(t) for t, m in zip(o_reads["tax_id"], o_reads["mapped"]) if m == 1)
+    want_rc = str(tmp_path / "o_rc_report.tsv")
+    oc.write_report(odb, want_rc, total, dict(rc))
+    assert open(rc_rep).read() == open(want_rc).read()
+    odb.close()
+    rank_of = dict(zip(taxo.taxid.tolist(), taxo.rank))
+    lines = open(em_tsv).read().split("\n")
+    assert lines[0] == "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage"
+    body = [l for l in lines[1:] if l]
+    assert len(body) == r.n
+    for i, line in enumerate(body):
+        f = line.split("\t")
+        t = int(o_reads["tax_id"][i])
+        assert f[0] == ("1" if t else "0") and f[1] == f"q{i:09d}"
+        assert int(f[2]) == t and int(f[3]) == int(ores["query_length"][i])
+        assert f[4] == "%g" % float(o_reads["score"][i])
+        assert f[5:] == ([rank_of[t], lineage[t]] if t else ["-", "-"])
+    # the classification TSV under --em: classified reads keep their best species (no BFS)
+    cls = [l.split("\t") for l in open(out).read().split("\n")[1:] if l]
+    assert [int(c[2]) for c in cls] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
