@@ -203,6 +203,8 @@ def main():
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
     ap.add_argument("--e2e-gzip-pairs", type=int, default=1_000_000,
                     help="config 3 file -> TSV line: read pairs written as single-member gzip FASTQ (0 = off)")
+    ap.add_argument("--em-pairs", type=int, default=10_000_000,
+                    help="config 3 --em line: read pairs classified with em and reassigned (0 = off)")
     ap.add_argument("--variant-only", default="", help="experiments: run this config-3 variant line alone")
     args = ap.parse_args()
 
@@ -608,6 +610,9 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     if rank == 0 and not variant and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0):
         e2e = run_e2e(args, clf, s1, s2, L, N)
     clf.close()
+    em_line = None
+    if rank == 0 and not variant and args.em_pairs > 0:
+        em_line = run_em(args, rdb, lp, s1, s2, o1, L, min(N, args.em_pairs), B, local)
     long_line = None
     if "long" in got and not variant:
         ls1, lo1, n50 = got.pop("long")
@@ -634,6 +639,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         "work": work,
         "long_reads": long_line,
         "end_to_end": e2e,
+        "em": em_line,
         "pipeline_roofline": pipe,
     }
     if variant:
@@ -643,6 +649,48 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                "kernel_ms": out["kernel_ms"], "work": work}
     del rdb
     torch.cuda.empty_cache()
+    return out
+
+
+def run_em(args, rdb, lp, s1, s2, o1, L, N, B, local):
+    """--em at config 3: the reads classified with em = 1 in B-pair batches, their
+    mappings collected (Reporter::writeMappings), then mtb_em timed: the EM iterations and the
+    reassignment on the device over all N reads' mappings (Classifier::em + reclassify)."""
+    import dataclasses
+    lpe = dataclasses.replace(lp, em=1)
+    clf = Classifier(lpe, db_resident=rdb, device=local)
+    maps = []
+    t_map = 0.0
+    ob = o1[:B + 1].contiguous()
+    b0 = min(N, B)  # warm-up batch: the new context's workspace grows to size outside the timing
+    clf.classify_batch(s1[:b0 * L], o1[:b0 + 1].contiguous(), s2[:b0 * L], o1[:b0 + 1].contiguous(),
+                       device_input=True, fetch=False)
+    clf.em_mappings(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a in range(0, N, B):
+        b = min(N, a + B)
+        obb = ob if b - a == B else o1[:b - a + 1].contiguous()
+        clf.classify_batch(s1[a * L:b * L], obb, s2[a * L:b * L], obb, device_input=True, fetch=False)
+        tm = time.perf_counter()
+        maps.append(clf.em_mappings(a))
+        t_map += time.perf_counter() - tm
+    torch.cuda.synchronize()
+    t_cls = time.perf_counter() - t0
+    maps = np.concatenate(maps)
+    clf.em(maps[:1], N)  # species k-mer counts (a pass over the DB, once per context) outside the timing
+    t1 = time.perf_counter()
+    reads, sp, st = clf.em(maps, N)
+    t_em = time.perf_counter() - t1
+    clf.close()
+    out = {"reads": int(N), "mappings": int(len(maps)), "top_species": int(st["n_species"]),
+           "iterations": int(st["iterations"]), "query_count": int(st["query_count"]),
+           "em_s": round(t_em, 3), "classify_with_mappings_reads_per_s": round(N / t_cls, 1),
+           "mapping_fetch_s": round(t_map, 3),
+           "reassigned": int((reads["mapped"] == 1).sum()),
+           "note": "mtb_em wall time (host setup + device iterations + reassignment) over all mappings; "
+                   "classification with em = 1 timed per batch with the mapping copy"}
+    log(0, f"[bench] em: {out}")
     return out
 
 

@@ -109,8 +109,10 @@ struct mtb_ctx {
     uint64_t spillCap = 0;     // direct join: spilled matches mStage holds (grows to the largest seen)
     // --em: the last batch's mappings (kEmTop {species, score^2} per read, their counts), the
     // std::sort scratch (8 B per species run), DB k-mers per species (length factors)
-    DevBuf emMap, emCnt, emScratch;
+    DevBuf emMap, emCnt, emScratch, emPacked, emCnt32, emOff;
     bool emValid = false;
+    bool emPackedValid = false;                // emHost holds the last batch's packed mappings
+    std::vector<mtb_em_map> emHost;
     std::vector<uint32_t> spKmers;
     std::string dbDir;
     DevBuf local, paths, comb, conn, spScore, spKeep,
@@ -367,7 +369,8 @@ void mtb_close(mtb_ctx* c) {
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
                       &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
-                      &c->tcOff, &c->tcOut, &c->results};
+                      &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
+                      &c->emCnt32, &c->emOff};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
@@ -542,6 +545,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
                           c->tcOut.as<mtb_taxcnt>(), s);
     c->nTaxcnt = NT;
     c->emValid = false;
+    c->emPackedValid = false;
     if (c->par.em) {  // the mappings of Reporter::writeMappings (kEmTop best species per classified read)
         const uint64_t nS = std::max<uint64_t>(c->stats[7], 1);
         HIP_TRY(c->emScratch.ensure(8 * nS));
@@ -1053,22 +1057,29 @@ int mtb_get_em_mappings(mtb_ctx* c, uint32_t query_offset, mtb_em_map* out, uint
     *n_out = 0;
     const uint32_t n = c->nReads;
     if (!c->emValid || n == 0) return MTB_OK;
-    HIP_TRY(hipSetDevice(c->device));
-    std::vector<uint8_t> cnt(n);
-    std::vector<std::pair<int32_t, float>> m((uint64_t)n * kEmTop);
-    HIP_TRY(hipMemcpyAsync(cnt.data(), c->emCnt.p, n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(m.data(), c->emMap.p, 8ull * kEmTop * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    uint64_t tot = 0;
-    for (uint32_t r = 0; r < n; r++) tot += cnt[r];
+    if (!c->emPackedValid) {  // packed on the device once per batch, then served from the host copy
+        HIP_TRY(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        HIP_TRY(c->emCnt32.ensure(sizeof(uint32_t) * (n + 1)));
+        HIP_TRY(c->emOff.ensure(sizeof(uint64_t) * (n + 1)));
+        HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
+        HIP_TRY(c->emPacked.ensure(sizeof(mtb_em_map) * (uint64_t)kEmTop * n));
+        launch_em_pack(c->emMap.p, c->emCnt.as<uint8_t>(), n, c->emCnt32.as<uint32_t>(), c->emOff.as<uint64_t>(),
+                       c->scanTmp.p, c->emPacked.as<mtb_em_map>(), s);
+        uint64_t tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, c->emOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->emHost.resize(tot);
+        if (tot) HIP_TRY(hipMemcpy(c->emHost.data(), c->emPacked.p, sizeof(mtb_em_map) * tot, hipMemcpyDeviceToHost));
+        c->emPackedValid = true;
+    }
+    const uint64_t tot = c->emHost.size();
     *n_out = tot;
     if (tot > cap || (tot && !out)) return MTB_RETRY;
-    uint64_t w = 0;
-    for (uint32_t r = 0; r < n; r++)
-        for (uint32_t k = 0; k < cnt[r]; k++) {
-            const auto& e = m[(uint64_t)r * kEmTop + k];
-            out[w++] = mtb_em_map{query_offset + r, e.first, e.second};
-        }
+    for (uint64_t w = 0; w < tot; w++) {
+        out[w] = c->emHost[w];
+        out[w].query_id += query_offset;
+    }
     return MTB_OK;
 }
 

@@ -2287,6 +2287,31 @@ void launch_em_top(const mtb_match* M, const uint64_t* mOff, uint32_t n, const A
                                               (EmPair*)scratch, (EmPair*)maps, cnt);
 }
 
+// The batch's mappings packed in read order (off: exclusive scan of cnt) as {read, species, score}.
+__global__ void k_em_pack(const EmPair* __restrict__ maps, const uint8_t* __restrict__ cnt,
+                          const uint64_t* __restrict__ off, uint32_t n, mtb_em_map* __restrict__ out) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t o = off[r];
+    for (uint32_t k = 0; k < cnt[r]; k++) {
+        const EmPair e = maps[(uint64_t)r * kEmTop + k];
+        out[o + k] = mtb_em_map{r, e.sp, e.sc};
+    }
+}
+
+__global__ void k_u8_to_u32(const uint8_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+void launch_em_pack(const void* maps, const uint8_t* cnt, uint32_t n, uint32_t* cnt32, uint64_t* off, void* scanTmp,
+                    mtb_em_map* out, hipStream_t s) {
+    if (!n) return;
+    k_u8_to_u32<<<(n + 255) / 256, 256, 0, s>>>(cnt, n, cnt32);
+    exclusive_scan_u32(cnt32, n, off, scanTmp, s);
+    k_em_pack<<<(n + 255) / 256, 256, 0, s>>>((const EmPair*)maps, cnt, off, n, out);
+}
+
 // DB k-mers per species (Classifier::countUniqueKmerPerSpecies, Classifier.cpp:388-431: every info
 // entry's species, taxID_list mapping; entries without a species are not counted).
 __global__ void k_species_kmers(const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf,

@@ -289,6 +289,10 @@ void launch_compact_taxcnt(const mtb_taxcnt* pool, const uint64_t* mOff, mtb_res
 constexpr int kEmTop = 10;
 void launch_em_top(const mtb_match* M, const uint64_t* mOff, uint32_t n, const AssignScratch& s,
                    const mtb_result* results, void* scratch, void* maps, uint8_t* cnt, hipStream_t st);
+// those mappings packed in read order as mtb_em_map {batch read, species, score^2}: cnt32 / off
+// (n u32 / n + 1 u64 scratch), out (sum of cnt entries; off[n] holds the total)
+void launch_em_pack(const void* maps, const uint8_t* cnt, uint32_t n, uint32_t* cnt32, uint64_t* off, void* scanTmp,
+                    mtb_em_map* out, hipStream_t s);
 // DB k-mers per species taxID (cnt: maxTax + 1 u32, zeroed by the caller)
 void launch_species_kmers(const DbRec* db, uint64_t D, const int32_t* spOf, uint32_t maxTax, uint32_t* cnt,
                           hipStream_t s);
