@@ -36,7 +36,9 @@ from metabuli_work_amd.dist import gather_results  # noqa: E402
 from metabuli_work_amd.gpu_synth import make_genomes_gpu, make_long_reads_gpu, make_reads_gpu  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r01", f) for f in ("stage_traffic.json", "stage_traffic_gtdb.json")]
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", *f) for f in (("r02", "stage_traffic_gtdb.json"),
+                                                                 ("r01", "stage_traffic.json"),
+                                                                 ("r01", "stage_traffic_gtdb.json"))]
 # the six timed kernels of mtb_last_kernel_ms, by join path (mtb_last_stats[10])
 KERNELS_SORT = ["extract", "filter", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpose", "match_sort", "assign"]

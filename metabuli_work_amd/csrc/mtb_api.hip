@@ -72,6 +72,7 @@ struct mtb_ctx {
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
     int pruneAfter = 0;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode
+    bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
     bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
     uint32_t maxW = 0;           // the batch's most windows in one frame of one read
@@ -254,6 +255,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
+    if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;
     if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : 0;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
@@ -575,11 +577,14 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
     HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * (kStatStripes + 1)));
     HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
-    // K1 extract: every window's key (the sentinel where no k-mer is emitted)
+    // K1 extract: every window's key (the sentinel where no k-mer is emitted); fused with K1F for
+    // the sort-merge join (the keys never reach HBM: timed as the filter)
+    const bool fused = c->lines && !probe && c->fuseFilter;
     HIP_TRY(hipEventRecord(c->kev[0], s));
-    launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
-                   c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer, c->par.smer_len,
-                   c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
+    if (!fused)
+        launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                       c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
+                       c->par.smer_len, c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[1], s));
     // K1F: the windows whose AA 8-mer the DB holds (MTB_FORCE_GENERIC: no filter, the sort's first
     // pass drops the sentinels)
@@ -588,7 +593,16 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     const uint32_t* qi = nullptr;
     const uint64_t* qf = nullptr;
     HIP_TRY(hipEventRecord(c->kev[2], s));
-    if (c->lines) {
+    if (fused) {
+        Q = launch_extract_filter(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                                  c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
+                                  c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
+                                  c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo, c->rankHi,
+                                  &c->Qall, s);
+        HIP_TRY(hipGetLastError());
+        qk = c->keysB.as<uint64_t>();
+        qi = c->valsB.as<uint32_t>();
+    } else if (c->lines) {
         if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
         Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
                           probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), c->rankLo,

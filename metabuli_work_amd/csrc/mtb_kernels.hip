@@ -249,19 +249,30 @@ __device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits,
     return w;
 }
 
-// The unit's windows in order: f(p, ok, key) for p = 0 .. nWin-1 (p relative to the chunk); ok
-// when the window is emitted, key = its resident rank-form key (AA rank << 24 | DNA part).
-template <typename F>
-__device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* sBase, const int8_t* sAA,
-                                          const int8_t* sNum, int syncmer, int smerLen, F&& f) {
-    const int nSm = 8 - smerLen + 1;
+// The unit's windows one at a time: the scanner state of MetamerScanner / OldMetamerScanner /
+// SyncmerScanner over the unit's codons in load order (the chunk's first window needs the 7
+// codons before its last one: loaded by the constructor). next(): the next window's emission and
+// its resident rank-form key (AA rank << 24 | DNA part; kSentinel when not emitted).
+struct WinScanner {
+    const UnitWindows& w;
+    const uint8_t* sBase;
+    const int8_t *sAA, *sNum;
+    int syncmer, nSm;
+    uint64_t smMask;
     uint64_t aaAcc = 0, dnaAcc = 0, smAcc = 0;
     uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
-    const uint64_t smMask = (smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1);
-    int run = 0;
-    const uint8_t* seq = w.seq;
-    for (int j = w.pFirst; j < w.pFirst + w.nWin + 7; j++) {
+    int run = 0, j;
+
+    __device__ __forceinline__ WinScanner(const UnitWindows& w_, const uint8_t* b, const int8_t* a, const int8_t* n,
+                                          int sync, int smerLen)
+        : w(w_), sBase(b), sAA(a), sNum(n), syncmer(sync), nSm(8 - smerLen + 1),
+          smMask((smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1)), j(w_.pFirst) {
+        if (w.nWin > 0)
+            for (int k = 0; k < 7; k++) codon();
+    }
+    __device__ __forceinline__ void codon() {
         const int c0 = w.fromLeft ? w.s0 + 3 * j : w.e0 - 3 * j;  // first base of the triplet in load order
+        const uint8_t* seq = w.seq;
         uint32_t b1, b2, b3;
         if (w.fromLeft) {
             const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + 1]], z = sBase[seq[c0 + 2]];
@@ -288,7 +299,10 @@ __device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* s
         if (syncmer) {
             sm7 = sm6; sm6 = sm5; sm5 = sm4; sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = sm0; sm0 = smAcc;
         }
-        if (j < w.pFirst + 7) continue;
+        j++;
+    }
+    __device__ __forceinline__ uint64_t next() {
+        codon();
         bool ok = run >= 8;
         if (ok && syncmer) {
             // s-mers of the window: positions p..p+nSm-1 end at codons j-nSm+1..j = sm[nSm-1]..sm0.
@@ -302,15 +316,23 @@ __device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* s
             }
             ok = (bestK == nSm - 1) || (bestK == 0);
         }
-        uint64_t key = kSentinel;
-        if (ok) {
-            // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
-            uint64_t aaPart = 0;
+        if (!ok) return kSentinel;
+        // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
+        uint64_t aaPart = 0;
 #pragma unroll
-            for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
-            key = (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
-        }
-        f(j - 7 - w.pFirst, ok, key);
+        for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
+        return (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
+    }
+};
+
+// The unit's windows in order: f(p, ok, key) for p = 0 .. nWin-1 (p relative to the chunk).
+template <typename F>
+__device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* sBase, const int8_t* sAA,
+                                          const int8_t* sNum, int syncmer, int smerLen, F&& f) {
+    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);
+    for (int p = 0; p < w.nWin; p++) {
+        const uint64_t key = sc.next();
+        f(p, key != kSentinel, key);
     }
 }
 
@@ -1303,6 +1325,92 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
         if (FROM) qfrom[pos] = line_lower_bound(lines, k[j] >> 24);
         pos++;
     }
+}
+
+// K1 + K1F fused (the sort-merge join's default): each thread scans its unit's windows as k_extract
+// does, 16 at a time, probes the 16 keys' lines together and packs the present ones (block scan,
+// one atomic per block and group) — the window keys never go through HBM. The block's threads
+// share C, so every thread takes part in every group's scan (a unit past its windows, or a padding
+// unit, contributes sentinels). Output: qkey / qslot as k_filter's (slot = the window's K1 slot).
+__global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
+                                                        const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
+                                                        const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
+                                                        const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
+                                                        ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
+                                                        uint64_t* __restrict__ unitInfo, const ProbeLine* __restrict__ lines,
+                                                        uint64_t* __restrict__ qkey, uint32_t* __restrict__ qslot,
+                                                        unsigned long long* __restrict__ counter, uint64_t rankLo,
+                                                        uint64_t rankHi) {
+    __shared__ uint8_t sBase[256];
+    __shared__ int8_t sAA[64], sNum[64];
+    __shared__ unsigned long long sOut;
+    load_extract_tables(tabs, sBase, sAA, sNum);
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
+    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
+    if (w.nWin > 0) unitInfo[u] = w.info0;
+    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
+    for (uint32_t g = 0; g < C; g += kFilterPer) {
+        uint64_t k[kFilterPer];
+#pragma unroll
+        for (int j = 0; j < kFilterPer; j++) k[j] = (int)(g + j) < w.nWin ? sc.next() : kSentinel;
+        uint32_t word[kFilterPer];
+#pragma unroll
+        for (int j = 0; j < kFilterPer; j++) {
+            word[j] = 0;
+            const uint64_t xr = k[j] >> 24;
+            if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {
+                const uint64_t L = xr / kLineRanks;
+                const uint32_t o = (uint32_t)(xr - L * kLineRanks);
+                word[j] = (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
+            }
+        }
+        uint32_t mask = 0, emitted = 0;
+#pragma unroll
+        for (int j = 0; j < kFilterPer; j++) {
+            mask |= word[j] << j;
+            emitted += k[j] != kSentinel;
+        }
+        unsigned long long tot;
+        const unsigned long long off =
+            block_exclusive_scan((unsigned long long)__popc(mask) | ((unsigned long long)emitted << 32), &tot) &
+            0xFFFFFFFFull;
+        if (threadIdx.x == 0) {
+            const unsigned long long present = tot & 0xFFFFFFFFull;
+            sOut = present ? atomicAdd(counter, present) : 0;
+            if (tot >> 32) atomicAdd(counter + 1, tot >> 32);
+        }
+        __syncthreads();
+        uint64_t pos = sOut + off;
+        __syncthreads();  // sOut is rewritten by the next group
+#pragma unroll
+        for (int j = 0; j < kFilterPer; j++) {
+            if (!((mask >> j) & 1u)) continue;
+            qkey[pos] = k[j];
+            qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+            pos++;
+        }
+    }
+}
+
+uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
+                               const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
+                               uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
+                               uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
+                               unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
+                               hipStream_t s) {
+    hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
+    if (nUnits) {
+        const uint64_t threads = (nUnits + 63) / 64 * 64;
+        k_extract_filter<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+            seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
+            unitInfo, lines, qkey, qslot, counter, rankLo, rankHi);
+    }
+    unsigned long long Q[2] = {0, 0};
+    hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    *emitted = Q[1];
+    return Q[0];
 }
 
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,

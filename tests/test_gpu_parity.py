@@ -142,8 +142,8 @@ def test_end_to_end_batches(make_db, db_name):
 
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
-@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "64", "6144",
-                                    "6144:staged", "6144:spill"])
+@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused", "64",
+                                    "6144", "6144:staged", "6144:spill", "6144:unfused"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
@@ -151,7 +151,8 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     matches written straight into each read's slot stretch (default), or staged + transposed
     (MTB_DIRECT=0), also when a direct join is rerun staged (MTB_DIRECT=2, the overflow fallback)
     or queries past their read's stretch spill and are scattered after the compaction (MTB_DIRECT=3
-    quarters the stretches; the batch then classifies as the oracle does);
+    quarters the stretches; the batch then classifies as the oracle does); K1 and K1F fused (the
+    default) or apart (MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back);
     and the unstaged join over queries sorted on a 32-bit AA-rank prefix (MTB_SORT_LO_FINE=28, its
     own block line ranges and LDS staging)."""
     window, _, mode = window.partition(":")
@@ -159,6 +160,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
     monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2", "spill": "3"}.get(mode, "1"))
+    monkeypatch.setenv("MTB_FUSE_FILTER", "0" if mode == "unfused" else "1")
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, 2)
     reads = _reads(gen, "paired", 2000, seed=9)
