@@ -1351,24 +1351,27 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
     if (w.nWin > 0) unitInfo[u] = w.info0;
     WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
     for (uint32_t g = 0; g < C; g += kFilterPer) {
+        // each window's probe is issued as soon as its key is known; the words are tested after the
+        // group's last key, so the 16 line reads overlap the scanning
         uint64_t k[kFilterPer];
-#pragma unroll
-        for (int j = 0; j < kFilterPer; j++) k[j] = (int)(g + j) < w.nWin ? sc.next() : kSentinel;
-        uint32_t word[kFilterPer];
+        uint32_t word[kFilterPer], sh[kFilterPer];
 #pragma unroll
         for (int j = 0; j < kFilterPer; j++) {
+            k[j] = (int)(g + j) < w.nWin ? sc.next() : kSentinel;
             word[j] = 0;
+            sh[j] = 32;
             const uint64_t xr = k[j] >> 24;
             if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {
                 const uint64_t L = xr / kLineRanks;
                 const uint32_t o = (uint32_t)(xr - L * kLineRanks);
-                word[j] = (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
+                word[j] = lines[L].bits[o >> 5];
+                sh[j] = o & 31u;
             }
         }
         uint32_t mask = 0, emitted = 0;
 #pragma unroll
         for (int j = 0; j < kFilterPer; j++) {
-            mask |= word[j] << j;
+            mask |= (sh[j] < 32u ? (word[j] >> sh[j]) & 1u : 0u) << j;
             emitted += k[j] != kSentinel;
         }
         unsigned long long tot;
