@@ -72,6 +72,7 @@ struct mtb_ctx {
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
     int pruneAfter = 0;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode
+    int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
     bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
@@ -255,6 +256,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
+    if (const char* e = getenv("MTB_BIG_GROUPS")) c->bigGroups = atoi(e) != 0;
     if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;
     if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : 0;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
@@ -431,6 +433,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     AssignArgs a = assign_args(c->par);
     a.generic = c->forceGeneric ? 1 : 0;
     a.waveTaxon = c->waveTaxon;
+    a.bigGroups = c->bigGroups;
     a.emulateAll = c->emulateAll;
     if (a.dnaShift <= 0) { set_error("syncmer smer_len 8 gives a zero dnaShift"); return MTB_ERR_ARG; }
     HIP_TRY(c->readCnt.ensure(sizeof(uint32_t) * (n + 1)));

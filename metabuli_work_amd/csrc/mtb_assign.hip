@@ -1191,6 +1191,7 @@ __device__ __forceinline__ bool consecutive(uint32_t dc, uint32_t dn, uint32_t s
 // having written nothing that counts, if a position group holds more than kRegPos matches; the
 // caller then reruns the group through the general version.
 constexpr int kRegPos = 4;
+constexpr uint64_t kBigGroup = 256;  // groups of at least this many matches: k_match_paths_wave
 
 __device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M, uint64_t start, uint64_t end,
                                                  const AssignCfg& cfg, int minDepth, bool fwd,
@@ -1299,32 +1300,19 @@ __device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M
     return true;
 }
 
-// getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
-// P[gs + k] in emission order; L and conn are indexed by match.
-__global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
-                                                     const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
-                                                     TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
-                                                     uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nWork) return;
-    const uint64_t g = (uint32_t)order[i];
-    const uint64_t start = gStart[g], end = gStart[g + 1];
-    const int32_t sp = (int32_t)M[start].species_id;
-    const uint32_t curFrame = info_frame(M[start].qinfo);
-    int minDepth = cfg.minConsCnt;
-    if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
-    const bool fwd = curFrame < 3;
-    {
-        uint64_t nPr = start;
-        if (!cfg.generic && match_paths_regs(M, start, end, cfg, minDepth, fwd, P, nPr)) {
-            pathCnt[g] = (uint32_t)(nPr - start);
-            return;
-        }
-    }
+// getMatchPaths' loop (Taxonomer.cpp:487-648) over the matches [start, end) of one (species,
+// frame) group, DP state in L / conn (indexed by match); paths to P from index start in emission
+// order; returns the end of the emitted paths. emitLone: [start, end) is a stretch of a larger group
+// that ends at a break (the next position is not within maxCodonShift codons): a stretch of a
+// single position group emits its paths too, as the whole group's loop would when it moves past it.
+__device__ uint64_t match_paths_serial(const mtb_match* __restrict__ M, uint64_t start, uint64_t end,
+                                       const AssignCfg& cfg, int minDepth, bool fwd, Path* __restrict__ L,
+                                       Path* __restrict__ P, uint8_t* __restrict__ conn, bool emitLone) {
     for (uint64_t x = start; x < end; x++) conn[x] = 0;
     uint64_t nP = start;
     uint64_t k = start;
     uint64_t currPos = info_pos(M[start].qinfo);
+    bool stepped = false;  // a next position group was processed
     auto initPath = [&](uint64_t idx) {
         Path p;
         p.start = (int)info_pos(M[idx].qinfo);
@@ -1343,6 +1331,7 @@ __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict
         const uint64_t nxS = k;
         while (k < end && info_pos(M[k].qinfo) == nextPos) { initPath(k); ++k; }
         const uint64_t nxE = k;
+        stepped = true;
         const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
         if (shift > 0 && shift <= cfg.maxCodonShift) {
             const uint32_t sh = 3u * (uint32_t)shift;
@@ -1392,7 +1381,91 @@ __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict
         curE = nxE;
         currPos = nextPos;
     }
+    if (!stepped && emitLone)
+        for (uint64_t cu = start; cu < end; cu++)
+            if (L[cu].depth >= minDepth) P[nP++] = L[cu];
+    return nP;
+}
+
+// getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
+// P[gs + k] in emission order; L and conn are indexed by match.
+__global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
+                                                     const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
+                                                     TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
+                                                     uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt,
+                                                     uint64_t* __restrict__ bigList, uint32_t* __restrict__ bigCount) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nWork) return;
+    const uint64_t g = (uint32_t)order[i];
+    const uint64_t start = gStart[g], end = gStart[g + 1];
+    if (bigList && end - start >= kBigGroup) {  // k_match_paths_wave takes it
+        bigList[atomicAdd(bigCount, 1u)] = g;
+        return;
+    }
+    const int32_t sp = (int32_t)M[start].species_id;
+    const uint32_t curFrame = info_frame(M[start].qinfo);
+    int minDepth = cfg.minConsCnt;
+    if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
+    const bool fwd = curFrame < 3;
+    {
+        uint64_t nPr = start;
+        if (!cfg.generic && match_paths_regs(M, start, end, cfg, minDepth, fwd, P, nPr)) {
+            pathCnt[g] = (uint32_t)(nPr - start);
+            return;
+        }
+    }
+    const uint64_t nP = match_paths_serial(M, start, end, cfg, minDepth, fwd, L, P, conn, false);
     pathCnt[g] = (uint32_t)(nP - start);
+}
+
+// A group of >= kBigGroup matches (long reads) with a wave: each lane takes a stretch of ~n/64
+// matches widened to whole break-delimited stretches (a break: the next position is not within
+// maxCodonShift codons, so no path crosses it and the serial loop's state restarts there), runs the
+// serial loop on it with its paths to P at the stretch's own offset, and the stretches' paths are
+// then packed in lane order (= the serial emission order) through L.
+__device__ __forceinline__ bool group_break(const mtb_match* __restrict__ M, uint64_t start, uint64_t i,
+                                            int maxCodonShift) {
+    if (i == start) return true;
+    const uint32_t p = info_pos(M[i].qinfo), pp = info_pos(M[i - 1].qinfo);
+    if (p == pp) return false;
+    const int shift = (int)((p - pp) / 3);
+    return !(shift > 0 && shift <= maxCodonShift);
+}
+
+__global__ void __launch_bounds__(64) k_match_paths_wave(const mtb_match* __restrict__ M,
+                                                         const uint64_t* __restrict__ gStart,
+                                                         const uint64_t* __restrict__ bigList, AssignCfg cfg,
+                                                         TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
+                                                         uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt) {
+    const uint64_t g = bigList[blockIdx.x];
+    const int lane = threadIdx.x;
+    const uint64_t start = gStart[g], end = gStart[g + 1], n = end - start;
+    const int32_t sp = (int32_t)M[start].species_id;
+    int minDepth = cfg.minConsCnt;
+    if (tax.exists(sp) && (tax.flags[tax.nodeOf[sp]] & 1u)) minDepth = cfg.minConsCntEuk;
+    const bool fwd = info_frame(M[start].qinfo) < 3;
+    const bool multi = info_pos(M[start].qinfo) != info_pos(M[end - 1].qinfo);
+    // this lane's stretch: from the first break at or after its nominal start
+    uint64_t a = start + n * (uint64_t)lane / 64;
+    while (a < end && !group_break(M, start, a, cfg.maxCodonShift)) a++;
+    uint64_t b = __shfl_down(a, 1, 64);
+    if (lane == 63) b = end;
+    if (b < a) b = a;
+    uint64_t cnt = 0;
+    if (a < b) cnt = match_paths_serial(M, a, b, cfg, minDepth, fwd, L, P, conn, multi) - a;
+    // exclusive scan of the counts over the lanes
+    uint64_t inc = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    const uint64_t off = inc - cnt, total = __shfl(inc, 63, 64);
+    __syncthreads();  // every stretch's DP done: L is free
+    for (uint64_t k = 0; k < cnt; k++) L[start + off + k] = P[a + k];
+    __syncthreads();
+    for (uint64_t k = lane; k < total; k += 64) P[start + k] = L[start + k];
+    if (lane == 0) pathCnt[g] = (uint32_t)total;
 }
 
 // trimMatchPath (Taxonomer.cpp:475-485): p overlaps c by ol < 24 bases at one end
@@ -2142,10 +2215,22 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
             const uint64_t heavy = radix_sort_pairs(s.ordKA, s.ordVA, s.ordKB, s.ordVB, cnt[0], 32, 40, true, false,
                                                     s.radixCounts, s.radixOffs, s.scanTmp, &inB, st);
             hostStats[1] = heavy;
-            if (heavy)
+            if (heavy) {
+                // groups of >= kBigGroup matches queue for a wave each (long reads' serial tail)
+                const bool waves = !a.generic && a.bigGroups && nM >= kBigGroup;
+                if (waves) hipMemsetAsync(s.waveCount, 0, sizeof(uint32_t), st);
                 k_match_paths<<<(unsigned)((heavy + 255) / 256), 256, 0, st>>>(
                     matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
-                    s.conn, s.pathCnt);
+                    s.conn, s.pathCnt, waves ? s.waveList : nullptr, s.waveCount);
+                if (waves) {
+                    uint32_t nBig = 0;
+                    hipMemcpyAsync(&nBig, s.waveCount, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+                    hipStreamSynchronize(st);
+                    if (nBig)
+                        k_match_paths_wave<<<nBig, 64, 0, st>>>(matches, s.gStart, s.waveList, cfg, tv, (Path*)s.local,
+                                                                (Path*)s.paths, s.conn, s.pathCnt);
+                }
+            }
         }
         if (cnt[1]) {
             hipMemsetAsync(s.waveCount, 0, sizeof(uint32_t), st);

@@ -36,6 +36,7 @@ struct AssignArgs {
     int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread per read, 1 wave per read (K6 chooseBestTaxon)
     int emulateAll = 0;  // MTB_EMULATE_SORT=1: every k_combine_wave run takes the std::sort emulation (tests)
     int em = 0;          // --em: classified reads keep their best species; mappings for the EM
+    int bigGroups = 1;   // MTB_BIG_GROUPS=0: every (species, frame) group on a thread (A/B, tests)
 };
 
 struct AssignScratch {  // per match unless noted

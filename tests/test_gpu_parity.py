@@ -186,6 +186,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
 @pytest.mark.parametrize("db_name,kind,glob,merge", [
     ("fmt2", "paired", "1", "0"), ("fmt2", "long", "1", "0"), ("fmt1", "long", "1", "0"),
     ("fmt2", "paired", "0", "after1"), ("fmt2", "long", "0", "after1"), ("fmt2_syncmer", "long", "0", "after1"),
+    ("fmt2", "long", "0", "big0"), ("fmt1", "long", "0", "big0"),
     ("fmt2", "long", "0", "0"), ("fmt2_syncmer", "long", "0", "0"),
     ("fmt2", "long", "0", "512"), ("fmt1", "long", "0", "600"), ("fmt2_syncmer", "long", "0", "512")])
 def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monkeypatch):
@@ -199,7 +200,9 @@ def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monk
     order."""
     monkeypatch.setenv("MTB_SEGSORT_GLOBAL", glob)
     monkeypatch.setenv("MTB_PRUNE_AFTER", merge[5:] if merge.startswith("after") else "0")
-    monkeypatch.setenv("MTB_MERGE_SEG", "0" if merge.startswith("after") else merge)
+    monkeypatch.setenv("MTB_MERGE_SEG", "0" if merge.startswith(("after", "big")) else merge)
+    # K6: groups of >= 256 matches on a wave each (default) or on a thread (MTB_BIG_GROUPS=0)
+    monkeypatch.setenv("MTB_BIG_GROUPS", "0" if merge == "big0" else "1")
     monkeypatch.setenv("MTB_PRUNE_COMPACT", compact)
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])
