@@ -1981,7 +1981,7 @@ __global__ void __launch_bounds__(256) k_choose_taxon(const mtb_match* __restric
 // taxCnt a small LDS hash of (taxon, count). Reads whose quotients or distinct taxa do not fit take
 // the serial code on lane 0.
 constexpr int kWavePerReadMatches = 256;  // live matches per read above which K6 goes wave per read
-constexpr int kQuotLds = 8192;   // quotients per read in LDS: reads of up to ~24.5 kb at dnaShift 3
+constexpr int kQuotLds = 4096;   // quotients per LDS window (a 12 kb read at dnaShift 3 in one pass)
 constexpr int kTcHash = 256;     // distinct taxa of one read's taxCnt in LDS
 
 __device__ __forceinline__ float wave_max_f(float x) {
@@ -2007,8 +2007,9 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
                                                           uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
                                                           mtb_result* __restrict__ results,
                                                           const uint64_t* __restrict__ order) {
-    __shared__ uint32_t qmin[kQuotLds];
-    __shared__ int32_t qtax[kQuotLds];
+    // per quotient: min hamming << 24 | the LCA of the taxIDs at that hamming (taxIDs < 2^24: the
+    // caller checks), one word (32 KB: twice the waves per CU of separate tables)
+    __shared__ uint32_t qw[kQuotLds];
     __shared__ int32_t hk[kTcHash];
     __shared__ uint32_t hc[kTcHash];
     __shared__ int sFlag;
@@ -2096,34 +2097,42 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
     const long nb = (long)(bestSecond - bestFirst);
     const mtb_match* B = M + bestFirst;
     long nTc = -1;  // -1: take the serial path
-    if (maxQ < kQuotLds) {
-        for (long q = lane; q <= maxQ; q += 64) { qmin[q] = 0xFFFFFFFFu; qtax[q] = 0; }
+    if (tax.maxTax < (1 << 24)) {
         for (int k = lane; k < kTcHash; k += 64) { hk[k] = 0; hc[k] = 0; }
         if (lane == 0) sFlag = 0;
-        __syncthreads();
-        for (long i = lane; i < nb; i += 64) {
-            const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
-            if (q > (uint32_t)maxQ) { sFlag = 1; continue; }
-            atomicMin(&qmin[q], (uint32_t)B[i].hamming);
-        }
-        __syncthreads();
-        if (!sFlag) {
+        // quotients in windows of kQuotLds (a read of > 12 kb takes several passes over its matches)
+        for (long q0 = 0; q0 <= maxQ; q0 += kQuotLds) {
+            const long q1 = min(maxQ + 1, q0 + (long)kQuotLds);
+            for (long q = q0 + lane; q < q1; q += 64) qw[q - q0] = 0xFFFFFFFFu;
+            __syncthreads();
             for (long i = lane; i < nb; i += 64) {
                 const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
-                if ((uint32_t)B[i].hamming != qmin[q]) continue;
+                if (q > (uint32_t)maxQ || B[i].hamming > 254u) { sFlag = 1; continue; }
+                if ((long)q < q0 || (long)q >= q1) continue;
+                atomicMin(&qw[q - q0], (uint32_t)B[i].hamming << 24 | 0xFFFFFFu);  // the minimum, taxon part empty
+            }
+            __syncthreads();
+            if (sFlag) break;
+            for (long i = lane; i < nb; i += 64) {
+                const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
+                if ((long)q < q0 || (long)q >= q1) continue;
+                const uint32_t h = (uint32_t)B[i].hamming << 24;
+                uint32_t old = qw[q - q0];
+                if ((old & 0xFF000000u) != h) continue;
                 const int32_t t = (int32_t)B[i].target_id;
-                int32_t old = qtax[q];
-                while (true) {  // qtax[q] = LCA(qtax[q], t), 0 = empty
-                    const int32_t nv = old == 0 ? t : tax.lca(old, t);
+                while (true) {  // taxon part = LCA(taxon part, t), 0xFFFFFF = empty
+                    const uint32_t cur = old & 0xFFFFFFu;
+                    const uint32_t nv = h | (uint32_t)(cur == 0xFFFFFFu ? t : tax.lca((int32_t)cur, t));
                     if (nv == old) break;
-                    const int32_t prev = atomicCAS(&qtax[q], old, nv);
+                    const uint32_t prev = atomicCAS(&qw[q - q0], old, nv);
                     if (prev == old) break;
                     old = prev;
                 }
             }
             __syncthreads();
-            for (long q = lane; q <= maxQ; q += 64) {
-                const int32_t t = qtax[q];
+            for (long q = q0 + lane; q < q1; q += 64) {
+                const uint32_t wq = qw[q - q0];
+                const int32_t t = wq == 0xFFFFFFFFu ? 0 : (int32_t)(wq & 0xFFFFFFu);
                 if (t == 0) continue;
                 uint32_t h = ((uint32_t)t * 2654435761u) & (kTcHash - 1);
                 int probes = 0;
@@ -2134,7 +2143,8 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
                     if (++probes == kTcHash) { sFlag = 1; break; }
                 }
             }
-            __syncthreads();
+            __syncthreads();  // qw is rewritten by the next window
+            if (sFlag) break;
         }
         if (!sFlag) {  // entries out in slot order, then std::map order (ascending taxID) on lane 0
             long at = 0;

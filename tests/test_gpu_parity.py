@@ -267,21 +267,26 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
 
 
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt1", "long"),
-                                          ("fmt2_syncmer", "long"), ("fmt2_syncmer", "paired")])
+                                          ("fmt2_syncmer", "long"), ("fmt2_syncmer", "paired"), ("fmt2", "verylong"),
+                                          ("fmt1", "verylong")])
 @pytest.mark.parametrize("wave", ["0", "1", "1:emu"])
 def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
     """K6's chooseBestTaxon both ways — a thread per read (short reads) and a wave per read (long
     reads: parallel species scan, per-quotient LDS reduction for filterRedundantMatches) — forced
     on every read kind with MTB_WAVE_TAXON, against the oracle; and k_combine_wave's libstdc++
-    introsort emulation forced for every run it takes (MTB_EMULATE_SORT)."""
+    introsort emulation forced for every run it takes (MTB_EMULATE_SORT). "verylong": reads of
+    12-20 kb, whose quotients take several LDS windows in the wave kernel."""
     wave, _, emu = wave.partition(":")
     monkeypatch.setenv("MTB_WAVE_TAXON", wave)
     # every multi-path species run through k_combine_wave's std::sort emulation (tied paths)
     monkeypatch.setenv("MTB_EMULATE_SORT", "1" if emu else "0")
     db_dir, taxo, gen = make_db(db_name)
-    par = _params(db_dir, SEQ_MODE[kind])
+    par = _params(db_dir, SEQ_MODE["long" if kind == "verylong" else kind])
     odb = oc.OracleDb(db_dir)
-    reads = _reads(gen, kind, 1500 if kind != "long" else 80, 55)
+    if kind == "verylong":
+        reads = synth.make_long_reads(gen, 10, n50=16000, min_len=12500, seed=57)
+    else:
+        reads = _reads(gen, kind, 1500 if kind != "long" else 80, 55)
     ores, otc = oc.classify(odb, par.to_c(), reads)
     with Classifier(par, db_dir=db_dir) as clf:
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
