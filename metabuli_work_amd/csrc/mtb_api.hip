@@ -496,7 +496,8 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     HIP_TRY(c->spKeep.ensure(Kc));
     HIP_TRY(c->waveList.ensure(sizeof(uint64_t) * Kc));
     HIP_TRY(c->waveCount.ensure(sizeof(uint32_t)));
-    for (DevBuf* b : {&c->gFlag, &c->sFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Kc + 1)));
+    for (DevBuf* b : {&c->gFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Kc + 1)));
+    HIP_TRY(c->sFlag.ensure(std::max<uint64_t>(sizeof(uint32_t) * (Kc + 1), run_index_tmp_bytes(Kc))));
     for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Kc + 1)));
     HIP_TRY(c->clade.ensure(clade_bytes() * Kc * c->cladePerMatch));
     HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Kc));

@@ -1129,36 +1129,8 @@ __device__ __forceinline__ int ham_fields(uint32_t reh, int range, bool left) {
 // match array instead of 64 unrelated per-read segments.
 // ------------------------------------------------------------------------------------------------
 
-// Run boundaries: group starts where the read, species or frame changes; species runs where the
-// read or species changes.
-__global__ void k_run_flags(const mtb_match* __restrict__ M, uint64_t nM, uint32_t* __restrict__ gFlag,
-                            uint32_t* __restrict__ sFlag) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nM) return;
-    uint32_t g = 1, sp = 1;
-    if (i > 0) {
-        const mtb_match a = M[i - 1], b = M[i];
-        const bool newSp = info_seq(a.qinfo) != info_seq(b.qinfo) || a.species_id != b.species_id;
-        sp = newSp;
-        g = newSp || info_frame(a.qinfo) != info_frame(b.qinfo);
-    }
-    gFlag[i] = g;
-    sFlag[i] = sp;
-}
-
-__global__ void k_run_starts(const uint32_t* __restrict__ gFlag, const uint32_t* __restrict__ sFlag,
-                             const uint64_t* __restrict__ gScan, const uint64_t* __restrict__ sScan, uint64_t nM,
-                             uint64_t* __restrict__ gStart, uint64_t* __restrict__ sStart) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nM) {
-        if (gFlag[i]) gStart[gScan[i]] = i;
-        if (sFlag[i]) sStart[sScan[i]] = i;
-    }
-    if (i == 0) {
-        gStart[gScan[nM]] = nM;
-        sStart[sScan[nM]] = nM;
-    }
-}
+// Run boundaries (group and species-run starts, their exclusive counts): launch_run_index,
+// mtb_kernels.hip.
 
 // Work list for k_match_paths: the groups that can emit a path (>= prune_min_matches matches: a
 // single match is never searched, and fewer matches cannot chain MIN_DEPTH codons) in batch order,
@@ -2205,11 +2177,9 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                   a.accessionLevel, a.minScore, a.minSpScore, a.tieRatio, a.generic, a.emulateAll, a.em};
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
     if (nM) {
-        const unsigned bm = (unsigned)((nM + 255) / 256);
-        k_run_flags<<<bm, 256, 0, st>>>(matches, nM, s.gFlag, s.sFlag);
-        exclusive_scan_u32(s.gFlag, nM, s.gScan, s.scanTmp, st);
-        exclusive_scan_u32(s.sFlag, nM, s.sScan, s.scanTmp, st);
-        k_run_starts<<<bm, 256, 0, st>>>(s.gFlag, s.sFlag, s.gScan, s.sScan, nM, s.gStart, s.sStart);
+        // gFlag holds the flag bytes, sFlag the packed tile sums (run_index_tmp_bytes)
+        launch_run_index(matches, nM, reinterpret_cast<uint8_t*>(s.gFlag),
+                         reinterpret_cast<unsigned long long*>(s.sFlag), s.gScan, s.sScan, s.gStart, s.sStart, st);
         // groups and runs never outnumber matches: size the grids by nM, threads past the count exit
         uint64_t cnt[2] = {0, 0};
         hipMemcpyAsync(&cnt[0], s.gScan + nM, sizeof(uint64_t), hipMemcpyDeviceToHost, st);

@@ -70,6 +70,11 @@ inline unsigned stride_grid(uint64_t n, unsigned block = 256) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (uint64_t)gridDim.x * blockDim.x)
 void exclusive_scan_u32(const uint32_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
 void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp, hipStream_t s);
+// K6 run index of nM sorted matches: flags nM bytes, tileSum run_index_tmp_bytes(nM); writes
+// gScan/sScan (nM + 1) and gStart/sStart (count + 1)
+uint64_t run_index_tmp_bytes(uint64_t nM);
+void launch_run_index(const mtb_match* M, uint64_t nM, uint8_t* flags, unsigned long long* tileSum, uint64_t* gScan,
+                      uint64_t* sScan, uint64_t* gStart, uint64_t* sStart, hipStream_t s);
 
 void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
                       uint32_t* qlen, uint32_t* maxW, hipStream_t s);
