@@ -685,177 +685,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     for (uint32_t i = tid; i < sKept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sV[i];
 }
 
-// ------------------------------------------------------------------------------------------------
-// One-sweep variant (no sentinel filter, stored values): one read of the keys builds the digit
-// histograms of every pass; each pass is then a single scatter launch whose tiles take their
-// per-digit global offsets by decoupled look-back over the tiles before them (tile order = the
-// order blocks start, from a ticket), so the per-pass histogram launch, its scan over 256 x tiles
-// counts and their HBM round trip go away. Status words: bit 63 = prefix complete, bit 62 = tile
-// aggregate only, low bits the count. A block publishes its aggregate before it looks back, and
-// every tile before it has already started (tickets), so the look-back always terminates.
-// ------------------------------------------------------------------------------------------------
-constexpr int kMaxSweepPasses = 4;
-constexpr unsigned long long kStAgg = 1ull << 62, kStPrefix = 1ull << 63, kStCount = (1ull << 62) - 1;
-
-__global__ void __launch_bounds__(256) k_radix_hist_all(const uint64_t* __restrict__ keys, uint64_t n, int shift0,
-                                                        int passes, uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t hist[kMaxSweepPasses][256];
-    for (int p = 0; p < kMaxSweepPasses; p++) hist[p][threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-    uint64_t key[kRadixItems];
-#pragma unroll
-    for (int k = 0; k < kRadixItems; k++) {
-        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
-        key[k] = i < n ? keys[i] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kRadixItems; k++) {
-        const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
-        if (i < n)
-            for (int p = 0; p < passes; p++) atomicAdd(&hist[p][radix_digit(key[k], shift0 + 8 * p)], 1u);
-    }
-    __syncthreads();
-    for (int p = 0; p < passes; p++)
-        if (hist[p][threadIdx.x]) atomicAdd(&ghist[p * 256 + threadIdx.x], hist[p][threadIdx.x]);
-}
-
-// digit bases of every pass: exclusive scans of the 256-bin histograms (one block)
-__global__ void __launch_bounds__(256) k_radix_digit_base(const uint32_t* __restrict__ ghist, int passes,
-                                                          uint32_t* __restrict__ gbase) {
-    for (int p = 0; p < passes; p++) {
-        unsigned long long tot;
-        gbase[p * 256 + threadIdx.x] = (uint32_t)block_exclusive_scan(ghist[p * 256 + threadIdx.x], &tot);
-    }
-}
-
-template <typename V>
-__global__ void __launch_bounds__(256) k_radix_onesweep(const uint64_t* __restrict__ keysIn, const V* __restrict__ valsIn,
-                                                        uint64_t n, int shift, const uint32_t* __restrict__ gbase,
-                                                        unsigned long long* __restrict__ status,
-                                                        uint32_t* __restrict__ ticket, uint64_t* __restrict__ keysOut,
-                                                        V* __restrict__ valsOut) {
-    __shared__ uint64_t sKV[kRadixTile];
-    __shared__ uint8_t sDig[kRadixTile];
-    __shared__ uint32_t waveHist[kWaves][256];
-    __shared__ uint64_t sDst[256];
-    __shared__ uint32_t sTile;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) sTile = atomicAdd(ticket, 1u);
-    for (int x = tid; x < kWaves * 256; x += kBlock) (&waveHist[0][0])[x] = 0;
-    __syncthreads();
-    const uint32_t tile = sTile;
-    const uint64_t base = (uint64_t)tile * kRadixTile + (uint64_t)w * kRadixSlice;
-    const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t k[kRadixItems];
-    V v[kRadixItems];
-    uint32_t rk[kRadixItems];
-    if ((uint64_t)(tile + 1) * kRadixTile <= n) {
-#pragma unroll
-        for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
-#pragma unroll
-        for (int r = 0; r < kRadixItems; r++) v[r] = valsIn[base + (uint64_t)r * 64 + lane];
-    } else {
-#pragma unroll
-        for (int r = 0; r < kRadixItems; r++) {
-            const uint64_t i = base + (uint64_t)r * 64 + lane;
-            k[r] = i < n ? keysIn[i] : kSentinel;
-            v[r] = i < n ? valsIn[i] : (V)0;
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
-        const uint64_t i = base + (uint64_t)r * 64 + lane;
-        const bool valid = i < n;
-        const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
-        unsigned long long peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            unsigned long long m = __ballot(valid && ((d >> b) & 1u));
-            peers &= ((d >> b) & 1u) ? m : ~m;
-        }
-        const uint32_t before = valid ? waveHist[w][d] : 0u;
-        const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
-        if (valid && rankInWave == 0) waveHist[w][d] = before + (uint32_t)__popcll(peers);
-        rk[r] = valid ? (d << 16 | (before + rankInWave)) : ~0u;
-    }
-    __syncthreads();
-    {
-        uint32_t c[kWaves], sum = 0;
-#pragma unroll
-        for (int ww = 0; ww < kWaves; ww++) { c[ww] = waveHist[ww][tid]; sum += c[ww]; }
-        // publish this tile's count of digit tid, then look back for the tiles before it
-        unsigned long long* st = status + (uint64_t)tile * 256 + tid;
-        __hip_atomic_store(st, (tile == 0 ? kStPrefix : kStAgg) | sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long excl = 0;
-        if (tile > 0) {
-            int64_t j = (int64_t)tile - 1;
-            while (true) {
-                const unsigned long long x =
-                    __hip_atomic_load(status + (uint64_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!(x & (kStAgg | kStPrefix))) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += x & kStCount;
-                if (x & kStPrefix) break;
-                j--;
-            }
-            __hip_atomic_store(st, kStPrefix | (excl + sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        unsigned long long tot;
-        const uint32_t start = (uint32_t)block_exclusive_scan(sum, &tot);
-        sDst[tid] = (uint64_t)gbase[tid] + excl - start;
-        uint32_t run = start;
-#pragma unroll
-        for (int ww = 0; ww < kWaves; ww++) { waveHist[ww][tid] = run; run += c[ww]; }
-    }
-    __syncthreads();
-    const uint32_t kept = (uint32_t)min<uint64_t>(kRadixTile, n - (uint64_t)tile * kRadixTile);
-#pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
-        if (rk[r] == ~0u) continue;
-        const uint32_t d = rk[r] >> 16;
-        rk[r] = waveHist[w][d] + (rk[r] & 0xFFFFu);
-        sKV[rk[r]] = k[r];
-        sDig[rk[r]] = (uint8_t)d;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < kept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
-    __syncthreads();
-    V* sV = reinterpret_cast<V*>(sKV);
-#pragma unroll
-    for (int r = 0; r < kRadixItems; r++)
-        if (rk[r] != ~0u) sV[rk[r]] = v[r];
-    __syncthreads();
-    for (uint32_t i = tid; i < kept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sV[i];
-}
-
 uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) / kRadixTile) + 1; }
 
-// counts: ghist, gbase (passes x 256 u32 each) and one ticket per pass; offs: the tile status
-template <typename V>
-static void radix_onesweep_pairs(uint64_t* ki, V* vi, uint64_t* ko, V* vo, uint64_t n, int bitLo, int passes,
-                                 uint32_t* counts, uint64_t* offs, bool* inB, hipStream_t s) {
-    const uint32_t nTiles = (uint32_t)((n + kRadixTile - 1) / kRadixTile);
-    uint32_t* ghist = counts;
-    uint32_t* gbase = counts + kMaxSweepPasses * 256;
-    uint32_t* tickets = counts + 2 * kMaxSweepPasses * 256;
-    hipMemsetAsync(counts, 0, sizeof(uint32_t) * (2 * kMaxSweepPasses * 256 + kMaxSweepPasses), s);
-    k_radix_hist_all<<<nTiles, kBlock, 0, s>>>(ki, n, bitLo, passes, ghist);
-    k_radix_digit_base<<<1, kBlock, 0, s>>>(ghist, passes, gbase);
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(offs);
-    for (int p = 0; p < passes; p++) {
-        hipMemsetAsync(status, 0, sizeof(unsigned long long) * 256ull * nTiles, s);
-        k_radix_onesweep<V><<<nTiles, kBlock, 0, s>>>(ki, vi, n, bitLo + 8 * p, gbase + p * 256, status, tickets + p,
-                                                      ko, vo);
-        std::swap(ki, ko);
-        std::swap(vi, vo);
-        *inB = !*inB;
-    }
-}
-
-bool g_radix_onesweep = false;  // MTB_ONESWEEP=1: one histogram read + decoupled look-back scatters
 
 // Sorts n pairs by key bits [bitLo, bitHi). Returns the kept count (sentinels dropped when
 // filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
@@ -869,15 +700,6 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
     V *vi = valsA, *vo = valsB;
     bool first = true;
     *inB = false;
-    {
-        const int passes = (bitHi - bitLo + 7) / 8;
-        const uint64_t nTiles = (n + kRadixTile - 1) / kRadixTile;
-        if (g_radix_onesweep && !filter && !genVals && passes >= 1 && passes <= kMaxSweepPasses && nTiles >= 16 &&
-            n < (1ull << 32)) {
-            radix_onesweep_pairs<V>(ki, vi, ko, vo, n, bitLo, passes, counts, offs, inB, s);
-            return n;
-        }
-    }
     for (int shift = bitLo; shift < bitHi; shift += 8) {
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
