@@ -82,7 +82,7 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def alg_bytes(n, Q, M, D, live=None, probe=False, heads=None):
+def alg_bytes(n, Q, M, D, live=None, probe=False):
     """Algorithmic bytes per launch of each timed kernel for a batch of n 150-bp pairs (R reserved
     k-mer slots, Q kept query k-mers, M matches, live = matches K6 reads after K5's pruning, D DB
     k-mers)."""
@@ -101,11 +101,8 @@ def alg_bytes(n, Q, M, D, live=None, probe=False, heads=None):
         # queries, the DB (12-B value + taxID records) read once through the block windows, or, when
         # the DB is much larger than the query stream (D > 24 Q), each query's run: its two
         # run-index entries (4 B) and the run's first two records (24 B); the 16-B segment matches
-        # written into the reads' segments (direct join). Head-first lines (heads = the queries whose
-        # run has more than one record): the run's head record (12 B) per query, plus two run-index
-        # entries and the run's second record (16 B) for those heads
-        "match_join": 12 * Q + ((28 * Q if heads is None else 12 * Q + 16 * heads) if D > 24 * Q else 12 * D)
-                      + 16 * M,
+        # written into the reads' segments (direct join)
+        "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 16 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 16 * M + 24 * M + 8 * (n + 1),        # each read's segment matches read, live ones written
         "assign": 24 * live + 32 * n + 4 * n + 8 * n,       # live sorted matches read, results + lengths
@@ -127,9 +124,9 @@ def load_traffic(match):
     return None, None
 
 
-def roofline_of(kern, names, n, Q, M, D, traffic, live=None, heads=None):
+def roofline_of(kern, names, n, Q, M, D, traffic, live=None):
     """Roofline of the dominant kernel: algorithmic bytes per launch / its event-timed duration."""
-    alg = alg_bytes(n, Q, M, D, live=live, probe=names is KERNELS_PROBE, heads=heads)
+    alg = alg_bytes(n, Q, M, D, live=live, probe=names is KERNELS_PROBE)
     dom = int(np.argmax(kern))
     dname = names[dom]
     achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
@@ -162,11 +159,7 @@ def random_roofline(kern, names, work, Q, M, D):
     out = {}
     req = {"filter": (float(work.get("slots", 0)), 5.4)}
     if D > 24 * Q:
-        # head-first lines: one record line per query, plus the run-index entry and the run's
-        # other records for the head_runs queries whose run has more than one record
-        heads = float(work.get("head_runs", 0)) if work.get("head_first") else -1.0
-        lookups = 2.0 * Q if heads < 0 else Q + 2.0 * heads
-        req["match_join"] = (lookups + float(work.get("matched_queries", 0)) + M, 144.0)
+        req["match_join"] = (2.0 * Q + float(work.get("matched_queries", 0)) + M, 144.0)
     for k, (r, gb) in req.items():
         if k not in names or r <= 0:
             continue
@@ -567,12 +560,10 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     work = clf.stats()
     # run-index fallback rate: query k-mers whose DB run the join found by a gallop (all timed batches)
     work["run_index_fallback_rate"] = round(tot_gallop / max(1, tot_q), 6)
-    perm_env = os.environ.get("MTB_PERMUTE")
-    work["head_first"] = perm_env == "1" or (perm_env != "0" and rdb.n >= 1 << 32)
     names = kernel_names(work)
     roofline = roofline_of(kern, names, B, Qb, Mb, rdb.n,
                            load_traffic({"workload": "gtdb", "kmers": rdb.n, "batch_pairs": B}),
-                           live=tot_live / launches, heads=work["head_runs"] if work["head_first"] else None)
+                           live=tot_live / launches)
     rand_roof = random_roofline(kern, names, work, Qb, Mb, rdb.n)
     value = world * N * args.steps / elapsed
     log(rank, f"[bench] {tag}: {value / 1e6:.2f}M reads/s, {elapsed / args.steps * 1e3:.1f} ms/step, "
@@ -592,10 +583,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         from tests import oracle_ctypes as oc  # checker / baseline only
 
         te = time.perf_counter()
-        clf.db_order(False)  # the oracle reads the records sorted (the context may hold them head-first)
         odb = encode_into_oracle(rdb, oc.OracleDb)
-        if rdb.n >= 1 << 32 and os.environ.get("MTB_PERMUTE", "1") != "0":
-            clf.db_order(True)
         log(rank, f"[bench] oracle DB encoded on the host ({time.perf_counter() - te:.1f}s)")
         S = min(cpu_sample, N)
         h1 = s1[:S * L].cpu().numpy()

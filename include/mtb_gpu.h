@@ -152,13 +152,6 @@ int mtb_open_host(const mtb_db_host* db, const mtb_params* par, int device, mtb_
 int mtb_open_resident(const mtb_db_resident* db, const mtb_db_host* taxonomy, const mtb_params* par, int device,
                       mtb_ctx** out);
 void mtb_close(mtb_ctx* ctx);
-/* Record order of a context's DB (no reference counterpart: the resident-DB extension). A DB of
- * >= 4G k-mers (or MTB_PERMUTE=1) is held head-first: each AA run's first record at its
- * present-rank slot of its probe line, so the unstaged join reads one record instead of a run-index
- * entry and a record. head_first = 0 restores the sorted order (the caller of mtb_open_resident
- * reads its records; mtb_close restores it too; a no-op on a DB that is never held head-first),
- * 1 re-applies it (MTB_ERR_ARG for a context that never held it). */
-int mtb_db_order(mtb_ctx* ctx, int head_first);
 const char* mtb_last_error(void);
 int mtb_set_stream(mtb_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
 uint64_t mtb_db_kmers(const mtb_ctx* ctx);             /* number of reference k-mers          */
@@ -186,10 +179,8 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
  * default; 0 probe join, MTB_JOIN=probe), [11] matches K6 read (live: their species has a frame
  * run of >= 2 matches; = [3] with MTB_KEEP_STAGES), [12] query k-mers whose DB run the unstaged
  * join found by a gallop over the DB (the run index covers probe lines of < 64K DB k-mers; queries
- * on longer lines fall back), [13] matches the direct join spilled, [14] query k-mers on head-first
- * lines (mtb_db_order) whose run has more than one record (they read the run index and the rest of
- * the run; the others read only the head record). Query k-mers = windows whose AA 8-mer the DB
- * holds. Counts [5]..[9] are over the live matches. */
+ * on longer lines fall back). Query k-mers = windows whose AA 8-mer the DB holds. Counts [5]..[9]
+ * are over the live matches. */
 int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):
  * [0] extract, [1] k-mer sort, [2] match, [3] match sort + assign, [4] total. */

@@ -22,7 +22,6 @@ EXPORTED = [
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
-    "mtb_db_order",
 ]
 
 
@@ -47,7 +46,6 @@ def lib() -> ctypes.CDLL:
     L.mtb_open_resident.argtypes = [P(MtbDbResident), P(MtbDbHost), P(MtbParams), i32, P(vp)]
     L.mtb_close.argtypes = [vp]
     L.mtb_close.restype = None
-    L.mtb_db_order.argtypes = [vp, i32]
     L.mtb_last_error.restype = ctypes.c_char_p
     L.mtb_set_stream.argtypes = [vp, vp]
     L.mtb_db_kmers.argtypes = [vp]

@@ -119,11 +119,6 @@ class Classifier:
             lib().mtb_close(self.handle)
             self.handle = ctypes.c_void_p()
 
-    def db_order(self, head_first: bool) -> None:
-        """Sorted (False) or head-first (True) record order of a DB the context holds head-first
-        (mtb_db_order): a resident DB's owner reads its records sorted."""
-        check(lib().mtb_db_order(self.handle, int(head_first)), "mtb_db_order")
-
     def __enter__(self):
         return self
 
@@ -176,7 +171,7 @@ class Classifier:
 
     STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
              "species_runs", "wave_runs", "wave_runs_emulated", "join_path", "live_matches", "gallop_queries",
-             "spilled_matches", "head_runs"]
+             "spilled_matches"]
 
     def stats(self) -> dict:
         """Work counts of the last batch (mtb_last_stats)."""

@@ -65,8 +65,6 @@ struct mtb_ctx {
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
     uint16_t* runOff = nullptr;  // ... and each present rank's run start in its line (2 B per present rank)
-    bool permuted = false;       // head-first lines (permute_lines): the unstaged join only
-    bool canPermute = false;     // the context chose head-first lines at open (mtb_db_order)
     AADir dir{};
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
@@ -106,7 +104,7 @@ struct mtb_ctx {
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
-    static constexpr int kNumStats = 15;
+    static constexpr int kNumStats = 14;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -140,12 +138,6 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
-    if (c->permuted && c->borrowedDb && c->db && c->lines && c->lineP && c->runOff && c->stream) {
-        // the caller's records go back in their sorted order (head-first lines restored)
-        permute_lines(c->db, c->D, c->lines, c->lineP, c->runOff, false, c->stream);
-        hipStreamSynchronize(c->stream);
-    }
-    c->permuted = false;
     if (c->borrowedDb) c->db = nullptr;  // caller-owned (mtb_open_resident)
     void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
@@ -293,16 +285,6 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
             hipFree(tmp);
             HIP_TRY(hipMalloc(&c->runOff, (P + 1) * sizeof(uint16_t)));
             build_run_offsets(c->db, c->D, c->lines, c->lineP, c->runOff, s);
-            // head-first lines: a DB far larger than any batch's query stream always takes the
-            // unstaged join, whose queries then read their run's head record without the run-index
-            // entry (MTB_PERMUTE=1 forces it, with the unstaged join, on any DB: tests; 0: off)
-            const char* pe = getenv("MTB_PERMUTE");
-            const bool perm = pe ? atoi(pe) != 0 : c->D >= kPermuteMinKmers;
-            if (perm && par->db_parts <= 1 && c->joinMode != 2) {
-                permute_lines(c->db, c->D, c->lines, c->lineP, c->runOff, true, s);
-                c->permuted = c->canPermute = true;
-                c->matchWinCap = 0;  // no LDS windows over a head-first DB
-            }
         }
     }
     HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
@@ -363,21 +345,6 @@ int mtb_open_host(const mtb_db_host* h, const mtb_params* par, int device, mtb_c
         !build_species_map(db))
         return MTB_ERR_DB;
     return open_common(db, par, device, out);
-}
-
-int mtb_db_order(mtb_ctx* c, int head_first) {
-    if (c && !c->canPermute && !head_first) return MTB_OK;  // always sorted
-    if (!c || !c->canPermute) {
-        set_error("mtb_db_order: the context's DB is not held head-first");
-        return MTB_ERR_ARG;
-    }
-    if ((head_first != 0) != c->permuted) {
-        permute_lines(c->db, c->D, c->lines, c->lineP, c->runOff, head_first != 0, c->stream);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        c->permuted = head_first != 0;
-    }
-    return MTB_OK;
 }
 
 int mtb_open_resident(const mtb_db_resident* r, const mtb_db_host* h, const mtb_params* par, int device,
@@ -612,8 +579,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
-    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * (kStatStripes + 2)));
-    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 2), s));
+    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * (kStatStripes + 1)));
+    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
     // K1 extract: every window's key (the sentinel where no k-mer is emitted); fused with K1F for
     // the sort-merge join (the keys never reach HBM: timed as the filter)
     const bool fused = c->lines && !probe && c->fuseFilter;
@@ -745,7 +712,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                 if (c->mStage.ensure(sizeof(mtb_match) * want) == hipSuccess &&
                     c->mRank.ensure(sizeof(uint32_t) * want) == hipSuccess) {
                     c->spillCap = want;
-                    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 2), s));
+                    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
                     continue;
                 }
                 (void)hipGetLastError();
@@ -754,7 +721,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             direct = false;  // rerun staged
             HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
             HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 2), s));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
             continue;
         }
         M = 0;
@@ -767,7 +734,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
         HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 2), s));
+        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
     }
     HIP_TRY(hipEventRecord(c->kev[7], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
@@ -902,12 +869,11 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     HIP_TRY(hipStreamSynchronize(s));
     c->stats[9] = dstat[1];
     {
-        std::vector<unsigned long long> ps(kStatStripes + 2);
+        std::vector<unsigned long long> ps(kStatStripes + 1);
         HIP_TRY(hipMemcpy(ps.data(), c->probeStats.p, sizeof(unsigned long long) * ps.size(), hipMemcpyDeviceToHost));
         c->stats[2] = 0;
         for (uint32_t i = 0; i < kStatStripes; i++) c->stats[2] += ps[i];  // queries with >= 1 match
         c->stats[12] = ps[kStatStripes];  // run-index fallbacks (gallop searches) of the probe join
-        c->stats[14] = ps[kStatStripes + 1];  // head-first runs of > 1 record (index + rest read)
     }
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));

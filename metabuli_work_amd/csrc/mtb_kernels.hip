@@ -955,58 +955,6 @@ void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, cons
     if (D) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(db, D, lines, lineP, runOff);
 }
 
-// One wave per line (grid-stride): the line's records staged in LDS, then each lane moves the runs
-// of the present ranks k = lane, lane + 64, ... (run k = [runOff[k], runOff[k + 1]) of the sorted
-// line; head slot k; other records from pc + runOff[k] - k). The inverse move restores the order.
-__global__ void __launch_bounds__(64) k_permute_lines(DbRec* __restrict__ db, uint64_t D,
-                                                      const ProbeLine* __restrict__ lines, uint64_t* __restrict__ lineP,
-                                                      const uint16_t* __restrict__ runOff, int forward) {
-    __shared__ uint32_t sLo[kPermMax], sHi[kPermMax], sTax[kPermMax];
-    const uint32_t lane = threadIdx.x;
-    for (uint64_t L = blockIdx.x; L + 1 < kProbeLines; L += gridDim.x) {
-        const uint64_t head = lines[L].base;
-        const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
-        const uint64_t lp0 = lineP[L];
-        if (forward ? (cnt == 0 || cnt > kPermMax || base + cnt >= D || (lp0 & kLinePermuted))
-                    : !(lp0 & kLinePermuted))
-            continue;
-        const uint64_t lp = lp0 & ~kLinePermuted;
-        uint32_t pc = 0;
-#pragma unroll
-        for (int i = 0; i < (int)(kLineRanks / 32); i++) pc += __popc(lines[L].bits[i]);
-        if (pc < cnt) {  // a line of single-record runs is already head-first
-            for (uint32_t i = lane; i < cnt; i += 64) {
-                const DbRec r = db[base + i];
-                sLo[i] = r.lo;
-                sHi[i] = r.hi;
-                sTax[i] = r.tax;
-            }
-            __syncthreads();
-            for (uint32_t k = lane; k < pc; k += 64) {
-                const uint32_t s0 = runOff[lp + k], s1 = k + 1 < pc ? runOff[lp + k + 1] : (uint32_t)cnt;
-                const uint32_t ex = pc + s0 - k;  // the run's second record, head-first
-                if (forward) {
-                    db[base + k] = DbRec{sLo[s0], sHi[s0] | (s1 - s0 > 1 ? kHeadMore : 0u), sTax[s0]};
-                    for (uint32_t t = 1; t < s1 - s0; t++)
-                        db[base + ex + t - 1] = DbRec{sLo[s0 + t], sHi[s0 + t], sTax[s0 + t]};
-                } else {
-                    db[base + s0] = DbRec{sLo[k], sHi[k] & ~kHeadMore, sTax[k]};
-                    for (uint32_t t = 1; t < s1 - s0; t++)
-                        db[base + s0 + t] = DbRec{sLo[ex + t - 1], sHi[ex + t - 1], sTax[ex + t - 1]};
-                }
-            }
-            __syncthreads();
-        }
-        if (lane == 0) lineP[L] = forward ? (lp | kLinePermuted) : lp;
-    }
-}
-
-void permute_lines(DbRec* db, uint64_t D, const ProbeLine* lines, uint64_t* lineP, const uint16_t* runOff,
-                   bool forward, hipStream_t s) {
-    if (D < 2) return;
-    k_permute_lines<<<8192, 64, 0, s>>>(db, D, lines, lineP, runOff, forward ? 1 : 0);
-}
-
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
 // of that range (found with two directory lookups per block) are staged in LDS with coalesced
 // loads and every query of the block searches LDS. A block whose range holds more than kMatchWin
@@ -1101,51 +1049,6 @@ __device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, ui
     return w;
 }
 
-// A head-first run: its head (value v0, in registers) plus the records [lo, hi): run_select's
-// threshold and count over those candidates (the emission order is free: K5 sorts each read).
-template <typename V>
-__device__ __forceinline__ uint32_t head_select(const HamRows& hr, uint64_t v0, const V& vals, uint64_t lo,
-                                                uint64_t hi, uint32_t& thr) {
-    const uint32_t s0 = hamming_sum_rows(hr, v0);
-    uint32_t minSum = s0;
-    uint64_t tally = s0 <= 7 ? 1ull << (8 * s0) : 0ull;
-    for (uint64_t t = lo; t < hi; t++) {
-        const uint32_t s = hamming_sum_rows(hr, vals[t]);
-        minSum = min(minSum, s);
-        if (s <= 7) tally += 1ull << (8 * s);
-    }
-    thr = min(minSum * 2u, 7u);
-    uint32_t c = 0;
-    if (hi - lo < 255) {
-#pragma unroll
-        for (uint32_t s = 0; s < 8; s++)
-            if (s <= thr) c += (uint32_t)(tally >> (8 * s)) & 0xFFu;
-    } else {
-        c = s0 <= thr;
-        for (uint64_t t = lo; t < hi; t++) c += hamming_sum_rows(hr, vals[t]) <= thr;
-    }
-    return c;
-}
-
-template <typename V, typename T, typename O>
-__device__ __forceinline__ uint64_t head_emit(uint64_t key, const HamRows& hr, uint64_t info, uint64_t v0, uint32_t t0,
-                                              const V& vals, const T& infos, uint64_t lo, uint64_t hi, uint32_t thr,
-                                              const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
-                                              O* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
-                                              uint64_t wEnd, uint32_t rank, int* __restrict__ err) {
-    const uint32_t s0 = hamming_sum_rows(hr, v0);
-    if (s0 <= thr) {
-        if (w >= wEnd) {
-            atomicExch(err, 4);
-            return w;
-        }
-        const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
-        emit_match(key, hr, info, v0, t0, s0, rev, spOf, maxTax, out, outRank, w++, rank++, err);
-    }
-    return run_emit(key, hr, info, vals, infos, lo, hi, thr, spOf, maxTax, kmerFormat, out, outRank, w, wEnd, rank,
-                    err);
-}
-
 // Both ends of an AA run in an LDS window of n sorted values: lower bounds of aa and aa + 2^24 by
 // a fixed-trip binary search (the trip count depends only on n, so the two chains, and the
 // chains of a thread's other queries, interleave instead of waiting on each other).
@@ -1225,12 +1128,6 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const uint64_t winLo = kStage ? win[2 * blockIdx.x] : 0, winN = kStage ? win[2 * blockIdx.x + 1] - winLo : 0;
     const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
-    // head-first lines: the run's head record, its run-index entry, and base + pc - before (the
-    // run's other records start there plus the entry); hf = ~0 for every other query
-    uint64_t hf[kPer], hp[kPer], hx[kPer];
-    uint32_t he[kPer];  // the run's end offset when it is the line's last run, else ~0 (read the index)
-#pragma unroll
-    for (int j = 0; j < kPer; j++) hf[j] = ~0ull;
     uint32_t nGallop = 0;  // probe-line queries whose run the run index does not hold (gallop fallback)
     if (kStage && staged) {
         constexpr int kLoad = kMatchWin / 256;
@@ -1291,19 +1188,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 bool present;
                 const uint64_t head = line_scan(pl, o, before, pc, present);
                 const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
-                const uint64_t lpv = inLds ? sLineP[L - L0] : lineP[L];
-                if (lpv & kLinePermuted) {  // one read: the head record at base + before
-                    lo[j] = hi[j] = 0;
-                    if (present) {
-                        hf[j] = base + before;
-                        hp[j] = (lpv & ~kLinePermuted) + before;
-                        hx[j] = base + pc - before;
-                        he[j] = before + 1 < pc ? ~0u : (uint32_t)cnt;
-                    }
-                    continue;
-                }
                 if (cnt <= kRunIdxMax) {
-                    const uint64_t p = (lpv & ~kLinePermuted) + before;
+                    const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
                     const uint32_t a = runOff[p];
                     const uint32_t b = before + 1 < pc ? runOff[p + 1] : (uint32_t)cnt;
                     lo[j] = base + a;
@@ -1330,34 +1216,13 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     // unstaged: a run at GTDB scale is 1-2 k-mers, so the run's first two records (value + taxID,
     // 24 contiguous bytes; the pad makes lo + 1 readable) are read at once
     uint64_t rv[kPer][2];
-    uint32_t rt[kPer][2], rs[kPer][2], nr[kPer];
+    uint32_t rt[kPer][2], rs[kPer][2];
     bool small[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
-        if (hf[j] != ~0ull) {  // head-first: the head, then (runs of > 1) the index and the rest
-            const DbRec r0 = db[hf[j]];
-            rv[j][0] = (uint64_t)(r0.hi & ~kHeadMore) << 32 | r0.lo;
-            rt[j][0] = r0.tax;
-            nr[j] = 1;
-            if (r0.hi & kHeadMore) {
-                const uint32_t a = runOff[hp[j]];
-                const uint32_t b = he[j] != ~0u ? he[j] : runOff[hp[j] + 1];
-                nr[j] = b - a;
-                lo[j] = hx[j] + a;  // the run's other nr - 1 records
-                hi[j] = lo[j] + nr[j] - 1;
-                if (nr[j] == 2) {
-                    const DbRec r1 = db[lo[j]];
-                    rv[j][1] = (uint64_t)r1.hi << 32 | r1.lo;
-                    rt[j][1] = r1.tax;
-                }
-            }
-            small[j] = nr[j] <= 2;
-            continue;
-        }
         if (hi[j] + vOff > D - 1) hi[j] = D - 1 - vOff;  // the last DB k-mer is never a candidate
         if (lo[j] > hi[j]) hi[j] = lo[j];
         small[j] = !staged && live[j] && hi[j] - lo[j] <= 2;
-        nr[j] = (uint32_t)(hi[j] - lo[j]);
         if (small[j]) {
             const DbRec r0 = db[lo[j]], r1 = db[lo[j] + 1];
             rv[j][0] = (uint64_t)r0.hi << 32 | r0.lo;
@@ -1372,16 +1237,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     for (int j = 0; j < kPer; j++) {
         hr[j] = hamming_rows(key[j]);
         if (small[j]) {  // run_select on the two registers
-            const uint32_t n = nr[j];
+            const uint32_t n = (uint32_t)(hi[j] - lo[j]);
             rs[j][0] = n > 0 ? hamming_sum_rows(hr[j], rv[j][0]) : 255u;
             rs[j][1] = n > 1 ? hamming_sum_rows(hr[j], rv[j][1]) : 255u;
             thr[j] = min(min(rs[j][0], rs[j][1]) * 2u, 7u);
             c[j] = (uint32_t)(rs[j][0] <= thr[j]) + (uint32_t)(rs[j][1] <= thr[j]);
         } else {
-            c[j] = !live[j]          ? 0
-                   : hf[j] != ~0ull ? head_select(hr[j], rv[j][0], dbv, lo[j], hi[j], thr[j])
-                   : staged         ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
-                                    : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
+            c[j] = !live[j] ? 0
+                   : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
+                            : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
         info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
         // the returned count is the query's first rank inside its read's segment
@@ -1394,14 +1258,10 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
     if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
     if (!kStage && lines) {  // the fallback counter sits past the stripes (rare: a lane-0 atomic per wave)
-        uint32_t w = 0, h = 0;
+        uint32_t w = 0;
 #pragma unroll
-        for (int j = 0; j < kPer; j++) {
-            w += (uint32_t)__popcll(__ballot(nGallop > (uint32_t)j));
-            h += (uint32_t)__popcll(__ballot(hf[j] != ~0ull && nr[j] > 1));
-        }
+        for (int j = 0; j < kPer; j++) w += (uint32_t)__popcll(__ballot(nGallop > (uint32_t)j));
         if (w && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)w);
-        if (h && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes + 1], (unsigned long long)h);
     }
     if (direct) {
         // each query's matches straight into its read's segment, at the ranks just reserved: the
@@ -1432,9 +1292,6 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 } else if (staged) {
                     run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf,
                              bufRank, sp, sp + c[j], rk[j], err);
-                } else if (hf[j] != ~0ull) {
-                    head_emit(key[j], hr[j], info[j], rv[j][0], rt[j][0], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax,
-                              kmerFormat, buf, bufRank, sp, sp + c[j], rk[j], err);
                 } else {
                     run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf,
                              bufRank, sp, sp + c[j], rk[j], err);
@@ -1453,9 +1310,6 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             } else if (staged) {
                 run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
                          nullptr, rk[j], rk[j] + c[j], 0, err);
-            } else if (hf[j] != ~0ull) {
-                head_emit(key[j], hr[j], info[j], rv[j][0], rt[j][0], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax,
-                          kmerFormat, out, nullptr, rk[j], rk[j] + c[j], 0, err);
             } else {
                 run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
                          nullptr, rk[j], rk[j] + c[j], 0, err);
@@ -1485,9 +1339,6 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         } else if (staged) {
             run_emit(key[j], hr[j], info[j], sDb, sInfo, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
                      w, w + c[j], rk[j], err);
-        } else if (hf[j] != ~0ull) {
-            head_emit(key[j], hr[j], info[j], rv[j][0], rt[j][0], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax,
-                      kmerFormat, buf, bufRank, w, w + c[j], rk[j], err);
         } else {
             run_emit(key[j], hr[j], info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank,
                      w, w + c[j], rk[j], err);

@@ -154,19 +154,6 @@ constexpr uint64_t kRunIdxMax = 0xFFFF;
 void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s);
 void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s);
-// Head-first lines (the unstaged K4 of a DB much larger than the query stream): inside each eligible
-// line's record stretch, the first record of every present rank's run moves to base + k (k = the
-// rank's index among the line's present ranks: computable from the probe line alone), the runs'
-// other records follow in run order from base + pc, and the head's value carries kHeadMore (bit 31
-// of its high word) when its run has more records. lineP[L] carries kLinePermuted. Eligible: 1 to
-// kPermMax k-mers, and not the line holding the DB's last k-mer (never a candidate). forward = false
-// restores the sorted order (a caller-owned resident DB is handed back sorted at mtb_close).
-constexpr uint64_t kLinePermuted = 1ull << 63;
-constexpr uint32_t kHeadMore = 1u << 31;
-constexpr uint32_t kPermMax = 2048;
-constexpr uint64_t kPermuteMinKmers = 1ull << 32;  // default: head-first lines for DBs of >= 4G k-mers
-void permute_lines(DbRec* db, uint64_t D, const ProbeLine* lines, uint64_t* lineP, const uint16_t* runOff,
-                   bool forward, hipStream_t s);
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count and sets

@@ -142,9 +142,8 @@ def test_end_to_end_batches(make_db, db_name):
 
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
-@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused", "0:perm",
-                                    "0:perm_staged", "0:perm_spill", "64", "6144", "6144:staged", "6144:spill",
-                                    "6144:unfused"])
+@pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused", "64",
+                                    "6144", "6144:staged", "6144:spill", "6144:unfused"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
@@ -155,11 +154,8 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     quarters the stretches; the batch then classifies as the oracle does); K1 and K1F fused (the
     default) or apart (MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back);
     and the unstaged join over queries sorted on a 32-bit AA-rank prefix (MTB_SORT_LO_FINE=28, its
-    own block line ranges and LDS staging); and head-first lines (MTB_PERMUTE=1: each run's head
-    record at its present-rank slot, the rest behind the line's heads), with each output."""
+    own block line ranges and LDS staging)."""
     window, _, mode = window.partition(":")
-    monkeypatch.setenv("MTB_PERMUTE", "1" if mode.startswith("perm") else "0")
-    mode = {"perm_staged": "staged", "perm_spill": "spill"}.get(mode, mode)
     monkeypatch.setenv("MTB_SORT_LO_FINE", "28" if mode == "fine28" else "36")
     monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
