@@ -215,6 +215,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
+        if args.db_parts <= 1:
+            # the scaling runs time the headline lines (config 3 short and long reads) only: the CPU
+            # baseline, the config-2 line, the DB variants, the file -> TSV and --em lines are
+            # single-GPU measurements (their per-rank DB rebuilds and host files would only
+            # lengthen the run)
+            args.cpu_sample = 0
+            args.skip_config2 = True
+            args.variants = ""
+            args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.variant_only:
