@@ -155,6 +155,7 @@ void mtb_close(mtb_ctx* ctx);
 const char* mtb_last_error(void);
 int mtb_set_stream(mtb_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
 uint64_t mtb_db_kmers(const mtb_ctx* ctx);             /* number of reference k-mers          */
+int mtb_ctx_device(const mtb_ctx* ctx);                /* the HIP device the context runs on  */
 
 /* ---- the hot path ------------------------------------------------------------------------- */
 /* One QuerySplit worth of reads (Classifier.cpp:81-133): extract (K1) + sort (K2) + match
@@ -351,6 +352,13 @@ typedef struct mtb_classify_stats {
     double write_s;           /* TSV formatting and writing (overlapped with the GPU stage)     */
 } mtb_classify_stats;
 int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify_stats* stats);
+/* The same run over n_ctx contexts, one per GPU of the node (each holding the DB, or the same
+ * device twice in tests): batch k runs on ctxs[k mod n_ctx] — the QuerySplit loop of
+ * Classifier.cpp:81-133 spread over the GPUs — while one parser feeds them all and one writer emits
+ * the batches in input order, so the TSV, the report and the --em outputs are byte-identical to a
+ * one-context run. ctxs[0] supplies the taxonomy for the writers and runs --em. */
+int mtb_start_classify_multi(mtb_ctx* const* ctxs, int n_ctx, const mtb_classify_opts* opts,
+                             mtb_classify_stats* stats);
 
 /* ---- --em: EM re-estimation of species abundances and read reassignment ------------------------
  * Replaces Reporter::writeMappings / Classifier::getTopSpecies (per batch) and Classifier::em +

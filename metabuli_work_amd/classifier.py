@@ -313,14 +313,18 @@ class Classifier:
 
     def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None,
                       max_bases: int = 0, threads: int = 0, em_tsv: Optional[str] = None,
-                      em_report_tsv: Optional[str] = None, em_reclassify_report_tsv: Optional[str] = None) -> int:
+                      em_report_tsv: Optional[str] = None, em_reclassify_report_tsv: Optional[str] = None,
+                      peers: Optional[List["Classifier"]] = None) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
         (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
         reads_per_batch reads and max_bases bases (0: sized from free HBM, the reference's
         RAM-bounded QuerySplits) uploaded on a copy stream, mtb_classify_batch, and the TSV writer
         (+ the per-taxon report, Classifier.cpp:149) overlapping each other; with --em (par.em) the
         EM reassignment after the last batch and its TSV / reports (Classifier.cpp:152-161). Returns
-        the reads classified; the run's timings are left in self.last_run."""
+        the reads classified; the run's timings are left in self.last_run.
+
+        peers: more classifiers over the same DB, one per further GPU (mtb_start_classify_multi):
+        batch k runs on [self] + peers at k mod (1 + len(peers)), the output is the same files."""
         par = self.par
         opts = _abi.MtbClassifyOpts(
             query1=par.filenames[0].encode(), query2=par.filenames[1].encode() if par.seqMode == 2 else None,
@@ -330,7 +334,12 @@ class Classifier:
             em_tsv=em_tsv.encode() if em_tsv else None, em_report_tsv=em_report_tsv.encode() if em_report_tsv else None,
             em_reclassify_report_tsv=em_reclassify_report_tsv.encode() if em_reclassify_report_tsv else None)
         st = _abi.MtbClassifyStats()
-        check(lib().mtb_start_classify(self.handle, ctypes.byref(opts), ctypes.byref(st)), "mtb_start_classify")
+        if peers:
+            hs = (ctypes.c_void_p * (1 + len(peers)))(self.handle, *[c.handle for c in peers])
+            check(lib().mtb_start_classify_multi(hs, len(hs), ctypes.byref(opts), ctypes.byref(st)),
+                  "mtb_start_classify_multi")
+        else:
+            check(lib().mtb_start_classify(self.handle, ctypes.byref(opts), ctypes.byref(st)), "mtb_start_classify")
         self.last_run = {f: getattr(st, f) for f, _ in _abi.MtbClassifyStats._fields_}
         return int(st.reads)
 

@@ -399,6 +399,8 @@ int mtb_set_stream(mtb_ctx* c, void* stream) {
 
 uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
 
+int mtb_ctx_device(const mtb_ctx* c) { return c ? c->device : 0; }
+
 }  // extern "C"
 
 static AssignArgs assign_args(const mtb_params& p) {

@@ -2077,7 +2077,7 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
     const long nb = (long)(bestSecond - bestFirst);
     const mtb_match* B = M + bestFirst;
     long nTc = -1;  // -1: take the serial path
-    if (tax.maxTax < (1 << 24)) {
+    if (tax.maxTax < 0xFFFFFF) {  // taxID 0xFFFFFF is the packed word's "empty" mark
         for (int k = lane; k < kTcHash; k += 64) { hk[k] = 0; hc[k] = 0; }
         if (lane == 0) sFlag = 0;
         // quotients in windows of kQuotLds (a read of > 12 kb takes several passes over its matches)

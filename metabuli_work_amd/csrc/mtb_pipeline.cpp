@@ -6,12 +6,15 @@
 //     and a parser cutting records into blocks of kBlockReads reads;
 //   * an assembler filling pinned host batches (<= max_reads reads, <= max_bases bases: the
 //     reference's RAM-bounded QuerySplits, QueryIndexer.cpp:62-67,132-137) and uploading each to
-//     its own device buffers on a copy stream;
-//   * the calling thread running mtb_classify_batch on the uploaded batches (MTB_INPUT_DEVICE);
-//   * a writer formatting each classified batch into the per-read TSV (Reporter.cpp:38-83) and
-//     counting reads per taxon for the report (Classifier.cpp:149, Reporter.cpp:175-190).
-// Batches rotate through kSlots slots, so batch k+1 is parsed and uploaded and batch k-1 written
-// while batch k runs on the GPU.
+//     its device's buffers on that device's copy stream;
+//   * per context (one per GPU) a worker running mtb_classify_batch on the uploaded batches
+//     (MTB_INPUT_DEVICE): batch k goes to context k mod n — the reference's QuerySplit loop
+//     (Classifier.cpp:81-133) spread over the GPUs of one node;
+//   * a writer taking the classified batches back in batch order, formatting the per-read TSV
+//     (Reporter.cpp:38-83) and counting reads per taxon for the report (Classifier.cpp:149,
+//     Reporter.cpp:175-190), so the output is the one a single context writes.
+// Batches rotate through kSlots slots per context, so on every GPU batch k+n is parsed and uploaded
+// and batch k-n written while batch k runs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -120,7 +123,7 @@ struct Pinned {  // grow-only pinned host buffer
         p = nullptr;
         cap = 0;
         const size_t want = n + n / 4 + 1024;
-        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocPortable);
         if (e == hipSuccess) cap = want;
         return e;
     }
@@ -148,6 +151,13 @@ struct DevMem {
 };
 
 struct Slot {
+    int ctx = 0;             // the context (GPU) the slot's batches run on
+    uint64_t index = 0;      // batch number in input order
+    uint64_t firstRead = 0;  // run-wide index of the batch's first read (--em query IDs)
+    int rc = MTB_OK;         // the batch's classify status
+    std::string err;
+    double gpuS = 0;
+    std::vector<mtb_em_map> em;
     Pinned<char> seq1, seq2;
     Pinned<uint64_t> off1, off2;
     std::string names;
@@ -174,11 +184,22 @@ struct Cursor {
 }  // namespace
 
 extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mtb_classify_stats* stats) {
+    return mtb_start_classify_multi(&ctx, 1, opt, stats);
+}
+
+extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opts* opt,
+                                        mtb_classify_stats* stats) {
     using mtb::set_error;
-    if (!ctx || !opt || !opt->query1 || !opt->out_tsv) {
+    if (!ctxs || nCtx < 1 || !opt || !opt->query1 || !opt->out_tsv) {
         set_error("null argument");
         return MTB_ERR_ARG;
     }
+    for (int d = 0; d < nCtx; d++)
+        if (!ctxs[d]) {
+            set_error("null context");
+            return MTB_ERR_ARG;
+        }
+    mtb_ctx* const ctx0 = ctxs[0];  // the writers' taxonomy, the report and --em
     const auto t0 = Clock::now();
     const bool paired = opt->query2 != nullptr;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -186,9 +207,15 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
     const uint32_t maxReads = opt->max_reads ? opt->max_reads : 1000000u;
     uint64_t maxBases = opt->max_bases;
     if (!maxBases) {  // ~140 device bytes of workspace per base at GTDB scale; slots < 2^31
-        size_t freeB = 0, totalB = 0;
-        hipMemGetInfo(&freeB, &totalB);
-        maxBases = std::min<uint64_t>((uint64_t)(0.5 * (double)freeB / 140.0), 1ull << 30);
+        maxBases = 1ull << 30;
+        for (int d = 0; d < nCtx; d++) {  // the smallest free HBM of the devices
+            size_t freeB = 0, totalB = 0;
+            if (hipSetDevice(mtb_ctx_device(ctxs[d])) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess) {
+                set_error("cannot query device memory");
+                return MTB_ERR_HIP;
+            }
+            maxBases = std::min<uint64_t>(maxBases, (uint64_t)(0.5 * (double)freeB / 140.0));
+        }
         maxBases = std::max<uint64_t>(maxBases, 1ull << 20);
     }
     ErrorBox eb;
@@ -202,26 +229,41 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
         set_error(m2.st.err);
         return MTB_ERR_IO;
     }
-    Slot slots[kSlots];
-    hipStream_t up = nullptr;
-    if (hipStreamCreateWithFlags(&up, hipStreamNonBlocking) != hipSuccess) {
-        set_error("cannot create the upload stream");
-        return MTB_ERR_HIP;
+    // per context: kSlots slots, a copy stream on its device, free and ready queues
+    std::vector<std::unique_ptr<Slot>> slotMem;
+    std::vector<hipStream_t> up(nCtx, nullptr);
+    std::vector<std::unique_ptr<BoundedQueue<Slot*>>> freeQ, readyQ;
+    for (int d = 0; d < nCtx; d++) {
+        if (hipSetDevice(mtb_ctx_device(ctxs[d])) != hipSuccess ||
+            hipStreamCreateWithFlags(&up[d], hipStreamNonBlocking) != hipSuccess) {
+            for (int e = 0; e < d; e++) hipStreamDestroy(up[e]);
+            set_error("cannot create the upload stream");
+            return MTB_ERR_HIP;
+        }
+        freeQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
+        readyQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
+        for (int k = 0; k < kSlots; k++) {
+            slotMem.emplace_back(new Slot());
+            Slot* s = slotMem.back().get();
+            s->ctx = d;
+            hipEventCreateWithFlags(&s->uploaded, hipEventDisableTiming);
+            freeQ[d]->push(s);
+        }
     }
-    for (Slot& s : slots) hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming);
-    BoundedQueue<Slot*> freeQ(kSlots), readyQ(kSlots), writeQ(kSlots);
-    for (Slot& s : slots) freeQ.push(&s);
+    BoundedQueue<Slot*> writeQ(slotMem.size() + 1);
 
     m1.t = std::thread([&] { m1.run(&eb); });
     if (paired) m2.t = std::thread([&] { m2.run(&eb); });
 
-    // assembler: blocks -> pinned batches -> device buffers (copy stream)
+    // assembler: blocks -> pinned batches -> device buffers of context (batch mod n)
     std::thread assembler([&] {
         Cursor c1, c2;
         bool end = false;
+        uint64_t index = 0, firstRead = 0;
         while (!end && !eb.failed) {
+            const int d = (int)(index % (uint64_t)nCtx);
             Slot* s = nullptr;
-            if (!freeQ.pop(s)) break;
+            if (!freeQ[d]->pop(s)) break;
             s->n = 0;
             s->bases = 0;
             s->names.clear();
@@ -266,8 +308,10 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
                 c1.at = k;
                 if (s->bases >= maxBases) break;
             }
-            if (eb.failed) break;
-            if (s->n == 0) break;
+            if (eb.failed || s->n == 0) {
+                freeQ[d]->push(s);
+                break;
+            }
             auto fill = [&](auto& take, Pinned<char>& seq, Pinned<uint64_t>& off, uint64_t bytes, bool names) {
                 if (seq.ensure(bytes + 1) != hipSuccess || off.ensure((size_t)s->n + 1) != hipSuccess) return false;
                 uint64_t at = 0;
@@ -291,122 +335,160 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
             };
             if (!fill(take1, s->seq1, s->off1, b1, true) || (paired && !fill(take2, s->seq2, s->off2, b2, false))) {
                 eb.set(MTB_ERR_OOM, "cannot allocate pinned host batch buffers");
+                freeQ[d]->push(s);
                 break;
             }
+            // the slot's device buffers live on its context's device (a new thread starts on device 0)
             const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
-            bool ok = s->dseq1.ensure(b1 + 1) == hipSuccess && s->doff1.ensure(on) == hipSuccess &&
-                      hipMemcpyAsync(s->dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up) == hipSuccess &&
-                      hipMemcpyAsync(s->doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up) == hipSuccess;
+            bool ok = hipSetDevice(mtb_ctx_device(ctxs[d])) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
+                      s->doff1.ensure(on) == hipSuccess &&
+                      hipMemcpyAsync(s->dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
+                      hipMemcpyAsync(s->doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
             if (ok && paired)
                 ok = s->dseq2.ensure(b2 + 1) == hipSuccess && s->doff2.ensure(on) == hipSuccess &&
-                     hipMemcpyAsync(s->dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up) == hipSuccess &&
-                     hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up) == hipSuccess;
-            ok = ok && hipEventRecord(s->uploaded, up) == hipSuccess;
+                     hipMemcpyAsync(s->dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
+                     hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
+            ok = ok && hipEventRecord(s->uploaded, up[d]) == hipSuccess;
             if (!ok) {
                 eb.set(MTB_ERR_HIP, "batch upload failed");
+                freeQ[d]->push(s);
                 break;
             }
-            if (!readyQ.push(s)) break;
+            s->index = index++;
+            s->firstRead = firstRead;
+            firstRead += s->n;
+            if (!readyQ[d]->push(s)) break;
         }
-        readyQ.close();
+        for (auto& q : readyQ) q->close();
     });
 
-    // writer: TSV lines + per-taxon read counts
+    // --em outputs requested: the mappings of every batch (Reporter::writeMappings)
+    const bool em = opt->em_tsv || opt->em_report_tsv || opt->em_reclassify_report_tsv;
+    // GPU workers, one per context: every batch they take goes on to the writer
+    std::vector<double> waitS(nCtx, 0.0);
+    std::vector<std::thread> workers;
+    for (int d = 0; d < nCtx; d++)
+        workers.emplace_back([&, d] {
+            mtb_ctx* c = ctxs[d];
+            if (hipSetDevice(mtb_ctx_device(c)) != hipSuccess) eb.set(MTB_ERR_HIP, "cannot select the device");
+            Slot* s = nullptr;
+            while (true) {
+                const auto w0 = Clock::now();
+                if (!readyQ[d]->pop(s)) break;
+                waitS[d] += secs(w0, Clock::now());
+                s->rc = MTB_OK;
+                s->gpuS = 0;
+                s->em.clear();
+                if (eb.failed) {
+                    s->rc = MTB_ERR_INTERNAL;  // skipped: an earlier failure ends the run
+                    writeQ.push(s);
+                    continue;
+                }
+                const auto g0 = Clock::now();
+                int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
+                s->res.resize(s->n);
+                if (rc == MTB_OK)
+                    rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
+                                            paired ? (const char*)s->dseq2.p : nullptr,
+                                            paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
+                                            s->res.data());
+                uint64_t nt = 0;
+                if (rc == MTB_OK) {
+                    mtb_get_taxcnt(c, nullptr, 0, &nt);
+                    s->tc.resize(std::max<uint64_t>(nt, 1));
+                    rc = mtb_get_taxcnt(c, s->tc.data(), s->tc.size(), &nt);
+                }
+                if (rc == MTB_OK && em) {
+                    if (s->firstRead + s->n > 0xFFFFFFFFull) {
+                        rc = MTB_ERR_ARG;
+                        mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
+                    } else {
+                        uint64_t nm = 0;
+                        rc = mtb_get_em_mappings(c, (uint32_t)s->firstRead, nullptr, 0, &nm);
+                        if (rc == MTB_RETRY || (rc == MTB_OK && nm)) {
+                            s->em.resize(nm);
+                            rc = mtb_get_em_mappings(c, (uint32_t)s->firstRead, s->em.data(), nm, &nm);
+                        }
+                    }
+                }
+                s->gpuS = secs(g0, Clock::now());
+                s->rc = rc;
+                if (rc != MTB_OK) {
+                    s->err = mtb_last_error();  // the error string is per thread
+                    eb.set(rc, s->err);
+                }
+                writeQ.push(s);
+            }
+        });
+
+    // writer: the batches in input order -> TSV lines + per-taxon read counts (+ --em mappings)
     std::map<int32_t, uint64_t> taxCounts;
-    double writeS = 0;
+    std::vector<mtb_em_map> emMaps;
+    uint64_t reads = 0, bases = 0, batches = 0;
+    double writeS = 0, gpuS = 0;
     std::thread writer([&] {
         bool first = true;
+        uint64_t next = 0;
+        std::map<uint64_t, Slot*> held;  // classified batches waiting for an earlier one
         Slot* s = nullptr;
         while (writeQ.pop(s)) {
-            const auto w0 = Clock::now();
-            if (!eb.failed) {
-                mtb_read_batch b{};
-                b.n_reads = s->n;
-                b.names = s->names.data();
-                b.name_off = s->noff.data();
-                if (mtb_write_classifications(ctx, opt->out_tsv, first ? 0 : 1, &b, s->res.data(), s->tc.data(),
-                                              opt->write_flags) != MTB_OK)
-                    eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
-                first = false;
-                for (uint32_t i = 0; i < s->n; i++)  // ++taxCounts[classification] (Classifier.cpp:201-203)
-                    taxCounts[s->res[i].is_classified ? s->res[i].classification : 0]++;
+            held[s->index] = s;
+            while (!held.empty() && held.begin()->first == next) {
+                s = held.begin()->second;
+                held.erase(held.begin());
+                next++;
+                const auto w0 = Clock::now();
+                if (!eb.failed && s->rc == MTB_OK) {
+                    mtb_read_batch b{};
+                    b.n_reads = s->n;
+                    b.names = s->names.data();
+                    b.name_off = s->noff.data();
+                    if (mtb_write_classifications(ctx0, opt->out_tsv, first ? 0 : 1, &b, s->res.data(), s->tc.data(),
+                                                  opt->write_flags) != MTB_OK)
+                        eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
+                    first = false;
+                    for (uint32_t i = 0; i < s->n; i++)  // ++taxCounts[classification] (Classifier.cpp:201-203)
+                        taxCounts[s->res[i].is_classified ? s->res[i].classification : 0]++;
+                    emMaps.insert(emMaps.end(), s->em.begin(), s->em.end());
+                    reads += s->n;
+                    bases += s->bases;
+                    batches++;
+                    gpuS += s->gpuS;
+                }
+                writeS += secs(w0, Clock::now());
+                freeQ[s->ctx]->push(s);
             }
-            writeS += secs(w0, Clock::now());
-            freeQ.push(s);
         }
+        for (auto& kv : held) freeQ[kv.second->ctx]->push(kv.second);  // a failed run: batches never written
         if (first && !eb.failed) {  // no reads: the header alone
             mtb_read_batch b{};
             std::vector<uint64_t> z(1, 0);
             b.name_off = z.data();
             b.names = "";
-            mtb_write_classifications(ctx, opt->out_tsv, 0, &b, nullptr, nullptr, opt->write_flags);
+            mtb_write_classifications(ctx0, opt->out_tsv, 0, &b, nullptr, nullptr, opt->write_flags);
         }
     });
 
-    // --em outputs requested: the mappings of every batch (Reporter::writeMappings)
-    const bool em = opt->em_tsv || opt->em_report_tsv || opt->em_reclassify_report_tsv;
-    std::vector<mtb_em_map> emMaps;
-    // the GPU stage on the calling thread
-    uint64_t reads = 0, bases = 0, batches = 0;
-    double gpuS = 0, waitS = 0;
-    Slot* s = nullptr;
-    while (true) {
-        const auto w0 = Clock::now();
-        if (!readyQ.pop(s)) break;
-        waitS += secs(w0, Clock::now());
-        if (eb.failed) {
-            freeQ.push(s);
-            continue;
-        }
-        const auto g0 = Clock::now();
-        int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
-        s->res.resize(s->n);
-        if (rc == MTB_OK)
-            rc = mtb_classify_batch(ctx, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
-                                    paired ? (const char*)s->dseq2.p : nullptr,
-                                    paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
-                                    s->res.data());
-        uint64_t nt = 0;
-        if (rc == MTB_OK) {
-            mtb_get_taxcnt(ctx, nullptr, 0, &nt);
-            s->tc.resize(std::max<uint64_t>(nt, 1));
-            rc = mtb_get_taxcnt(ctx, s->tc.data(), s->tc.size(), &nt);
-        }
-        if (rc == MTB_OK && em) {
-            if (reads + s->n > 0xFFFFFFFFull) {
-                rc = MTB_ERR_ARG;
-                mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
-            } else {
-                uint64_t nm = 0;
-                rc = mtb_get_em_mappings(ctx, (uint32_t)reads, nullptr, 0, &nm);
-                if (rc == MTB_RETRY || (rc == MTB_OK && nm)) {
-                    const size_t at = emMaps.size();
-                    emMaps.resize(at + nm);
-                    rc = mtb_get_em_mappings(ctx, (uint32_t)reads, emMaps.data() + at, nm, &nm);
-                }
-            }
-        }
-        gpuS += secs(g0, Clock::now());
-        if (rc != MTB_OK) {
-            eb.set(rc, mtb_last_error());
-            freeQ.push(s);
-            continue;
-        }
-        reads += s->n;
-        bases += s->bases;
-        batches++;
-        writeQ.push(s);
-    }
+    assembler.join();
+    for (auto& w : workers) w.join();
     writeQ.close();
     writer.join();
-    freeQ.close();
-    assembler.join();
+    for (auto& q : freeQ) q->close();
     m1.out.close();
     m2.out.close();
     m1.t.join();
     if (paired) m2.t.join();
-    for (Slot& x : slots) hipEventDestroy(x.uploaded);
-    hipStreamDestroy(up);
+    for (int d = 0; d < nCtx; d++) {
+        hipSetDevice(mtb_ctx_device(ctxs[d]));
+        hipStreamSynchronize(up[d]);
+        hipStreamDestroy(up[d]);
+    }
+    for (auto& s : slotMem) {  // device buffers are freed on their own device
+        hipSetDevice(mtb_ctx_device(ctxs[s->ctx]));
+        hipEventDestroy(s->uploaded);
+        s.reset();
+    }
+    hipSetDevice(mtb_ctx_device(ctx0));
     if (eb.code != MTB_OK) {
         set_error(eb.msg);
         return eb.code;
@@ -418,7 +500,7 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
             ids.push_back(kv.first);
             cnt.push_back((uint32_t)kv.second);
         }
-        const int rc = mtb_write_report(ctx, opt->report_tsv, reads, ids.data(), cnt.data(), ids.size());
+        const int rc = mtb_write_report(ctx0, opt->report_tsv, reads, ids.data(), cnt.data(), ids.size());
         if (rc != MTB_OK) return rc;
     }
     if (em) {  // Classifier.cpp:152-161: EM, the reassigned reads and both EM reports
@@ -429,11 +511,11 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
         std::vector<uint32_t> spC(cap);
         uint64_t nSp = 0;
         mtb_em_stats est{};
-        int rc = mtb_em(ctx, emMaps.data(), emMaps.size(), reads, er.data(), spIds.data(), spP.data(), spC.data(), cap,
+        int rc = mtb_em(ctx0, emMaps.data(), emMaps.size(), reads, er.data(), spIds.data(), spP.data(), spC.data(), cap,
                         &nSp, &est);
         if (rc != MTB_OK) return rc;
         if (opt->em_tsv) {
-            rc = mtb_write_em_results(ctx, opt->em_tsv, opt->out_tsv, er.data(), reads, opt->write_flags);
+            rc = mtb_write_em_results(ctx0, opt->em_tsv, opt->out_tsv, er.data(), reads, opt->write_flags);
             if (rc != MTB_OK) return rc;
         }
         if (opt->em_report_tsv) {  // emTaxCounts: the top species, taxID 0 = the reads they leave unexplained
@@ -443,7 +525,7 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
             for (uint32_t c : cnt) explained += c;
             ids.push_back(0);
             cnt.push_back((uint32_t)(reads - explained));
-            rc = mtb_write_report(ctx, opt->em_report_tsv, reads, ids.data(), cnt.data(), ids.size());
+            rc = mtb_write_report(ctx0, opt->em_report_tsv, reads, ids.data(), cnt.data(), ids.size());
             if (rc != MTB_OK) return rc;
         }
         if (opt->em_reclassify_report_tsv) {  // reclassifyTaxCounts: the reassigned reads per taxID
@@ -456,17 +538,19 @@ extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mt
                 ids.push_back(kv.first);
                 cnt.push_back((uint32_t)kv.second);
             }
-            rc = mtb_write_report(ctx, opt->em_reclassify_report_tsv, reads, ids.data(), cnt.data(), ids.size());
+            rc = mtb_write_report(ctx0, opt->em_reclassify_report_tsv, reads, ids.data(), cnt.data(), ids.size());
             if (rc != MTB_OK) return rc;
         }
     }
     if (stats) {
+        double w = 0;
+        for (double x : waitS) w += x;
         stats->reads = reads;
         stats->bases = bases;
         stats->batches = batches;
         stats->wall_s = secs(t0, Clock::now());
         stats->gpu_s = gpuS;
-        stats->input_wait_s = waitS;
+        stats->input_wait_s = w;
         stats->write_s = writeS;
     }
     return MTB_OK;

@@ -6,6 +6,7 @@
 
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -36,7 +37,8 @@ struct GzSource : ByteSource {
     FILE* f = nullptr;
     z_stream zs{};
     bool init = false, done = false;
-    std::vector<unsigned char> in = std::vector<unsigned char>(4u << 20);
+    std::vector<unsigned char> in;
+    explicit GzSource(size_t bufBytes) : in(std::max<size_t>(bufBytes, 16)) {}
     ~GzSource() override {
         if (init) inflateEnd(&zs);
         if (f) fclose(f);
@@ -47,6 +49,16 @@ struct GzSource : ByteSource {
         zs.next_in = in.data();
         zs.avail_in = (uInt)got;
         return got > 0;
+    }
+    // at least `k` input bytes buffered (the leftover moved to the front), unless the file ends first
+    bool need(uInt k) {
+        if (zs.avail_in >= k) return true;
+        const uInt have = zs.avail_in;
+        memmove(in.data(), zs.next_in, have);
+        const size_t got = fread(in.data() + have, 1, in.size() - have, f);
+        zs.next_in = in.data();
+        zs.avail_in = (uInt)(have + got);
+        return zs.avail_in >= k;
     }
     long read(char* dst, size_t cap) override {
         if (done) return 0;
@@ -61,7 +73,7 @@ struct GzSource : ByteSource {
             const int rc = inflate(&zs, Z_NO_FLUSH);
             if (rc == Z_STREAM_END) {
                 // another member may follow (multi-member gzip); anything else ends the input
-                if (!refill() || zs.avail_in < 2 || zs.next_in[0] != 0x1f || zs.next_in[1] != 0x8b) {
+                if (!need(2) || zs.next_in[0] != 0x1f || zs.next_in[1] != 0x8b) {
                     done = true;
                     break;
                 }
@@ -99,7 +111,7 @@ struct BgzfSource : ByteSource {
     std::shared_ptr<Group> cur;
     size_t curPos = 0;
 
-    static constexpr size_t kGroupBytes = 4u << 20;  // compressed bytes per group
+    size_t kGroupBytes = 4u << 20;  // compressed bytes per group (MTB_BGZF_GROUP: tests)
     size_t maxPending() const { return (size_t)nThreads * 3; }
 
     ~BgzfSource() override {
@@ -172,6 +184,11 @@ struct BgzfSource : ByteSource {
             g->out.resize(total);
             size_t o = 0;
             for (uint32_t e : g->memberEnd) {
+                const unsigned char* t = g->comp.data() + e - 4;
+                if ((t[0] | t[1] | t[2] | t[3]) == 0) {  // ISIZE 0 (e.g. the EOF marker): no output to make
+                    beg = e;
+                    continue;
+                }
                 inflateReset(&zs);
                 zs.next_in = g->comp.data() + beg;
                 zs.avail_in = (uInt)(e - beg);
@@ -317,14 +334,19 @@ std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bo
     std::unique_ptr<ByteSource> s;
     const bool gz = got >= 2 && h[0] == 0x1f && h[1] == 0x8b;
     const bool bgzf = gz && got >= 18 && (h[3] & 4) && h[12] == 'B' && h[13] == 'C' && h[14] == 2;
+    // test knobs: the gzip input buffer and the BGZF group size, so member / group boundaries can be
+    // placed at buffer edges
+    const char* gzBuf = getenv("MTB_GZ_BUFFER");
+    const char* bgzfGroup = getenv("MTB_BGZF_GROUP");
     if (bgzf) {
         auto b = std::make_unique<BgzfSource>();
         b->f = f;
+        if (bgzfGroup) b->kGroupBytes = std::max<size_t>(1, strtoull(bgzfGroup, nullptr, 10));
         b->start(threads);
         return b;  // the pool reads ahead already
     }
     if (gz) {
-        auto g = std::make_unique<GzSource>();
+        auto g = std::make_unique<GzSource>(gzBuf ? strtoull(gzBuf, nullptr, 10) : (4u << 20));
         g->f = f;
         if (inflateInit2(&g->zs, 15 + 32) != Z_OK) {
             err = "zlib init failed";

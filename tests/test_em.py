@@ -281,3 +281,30 @@ def test_start_classify_em(make_db, tmp_path):
     # the classification TSV under --em: classified reads keep their best species (no BFS)
     cls = [l.split("\t") for l in open(out).read().split("\n")[1:] if l]
     assert [int(c[2]) for c in cls] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
+
+
+@pytest.mark.gpu
+def test_start_classify_em_multi(make_db, tmp_path):
+    """--em through mtb_start_classify_multi (two contexts on cuda:0): the per-batch mappings are
+    collected in batch order with run-wide query IDs, so every output file equals the one-context
+    run's."""
+    db_dir, taxo, gen = make_db("fmt2_acc")
+    r = synth.make_reads(gen, 1300, paired=True, seed=93, short_frac=0.02)
+    p1, p2 = str(tmp_path / "q1.fq"), str(tmp_path / "q2.fq")
+    synth.write_compressed(p1, synth.fastq_bytes(r.seq1, r.off1, prefix="q"), "plain")
+    synth.write_compressed(p2, synth.fastq_bytes(r.seq2, r.off2, prefix="q"), "plain")
+    par = LocalParameters(seqMode=2, em=1, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    outs = {}
+    clfs = [Classifier(par, db_dir=db_dir) for _ in range(2)]
+    try:
+        for tag, peers in (("one", None), ("two", clfs[1:])):
+            f = {k: str(tmp_path / f"{tag}_{k}.tsv") for k in ("cls", "em", "emrep", "rcrep")}
+            assert clfs[0].startClassify(f["cls"], reads_per_batch=250, em_tsv=f["em"], em_report_tsv=f["emrep"],
+                                         em_reclassify_report_tsv=f["rcrep"], peers=peers) == r.n
+            outs[tag] = {k: open(v, "rb").read() for k, v in f.items()}
+    finally:
+        for c in clfs:
+            c.close()
+    assert outs["two"] == outs["one"]
+    assert len(outs["one"]["em"].split(b"\n")) > r.n

@@ -119,6 +119,39 @@ def test_compression_modes(tmp_path, reads, mode):
     assert g1 == _mates(reads, 1) and g2 == _mates(reads, 2)
 
 
+def test_bgzf_empty_and_eof_groups(tmp_path, reads, monkeypatch):
+    """A bgzipped file holding only the EOF marker reads as empty input; a file whose last data
+    member closes an inflate group (the EOF marker alone in the next group, or every member its own
+    group) reads completely (gzread reads both, as the reference's kseq does)."""
+    empty = str(tmp_path / "empty.fq.gz")
+    synth.write_compressed(empty, b"", "bgzf")
+    assert _read_all(empty, None, 100) == ([], [], [])
+    data = synth.fastq_bytes(reads.seq1, reads.off1)
+    p = str(tmp_path / "a.fq.gz")
+    synth.write_compressed(p, data, "bgzf")
+    import os
+    for group in (1, os.path.getsize(p) - 28):  # 28 B: the EOF marker block
+        monkeypatch.setenv("MTB_BGZF_GROUP", str(group))
+        names, g1, _ = _read_all(p, None, 300)
+        assert names == [f"r{i:09d}" for i in range(reads.n)] and g1 == _mates(reads, 1)
+
+
+def test_gzip_member_at_buffer_edge(tmp_path, reads, monkeypatch):
+    """Multi-member gzip whose second member starts one byte before the end of the input buffer:
+    the reader keeps that byte and refills before testing for the next member's magic (all members
+    are read, as gzread does)."""
+    data = synth.fastq_bytes(reads.seq1, reads.off1)
+    cut = data.index(b"\n@", len(data) // 3) + 1
+    m1, m2 = gzip.compress(data[:cut]), gzip.compress(data[cut:])
+    p = str(tmp_path / "m.fq.gz")
+    with open(p, "wb") as f:
+        f.write(m1 + m2)
+    for extra in (1, 2):
+        monkeypatch.setenv("MTB_GZ_BUFFER", str(len(m1) + extra))
+        names, g1, _ = _read_all(p, None, 300)
+        assert g1 == _mates(reads, 1) and len(names) == reads.n
+
+
 def test_reader_errors(tmp_path, reads):
     names = [f"r{i}" for i in range(10)]
     seqs = _mates(reads, 1)[:10]
@@ -214,3 +247,36 @@ def test_start_classify_long_reads_batches(make_db, tmp_path, mode):
         if o["is_classified"]:
             s = int(o["taxcnt_offset"])
             assert f[6] == "".join(f"{int(t)}:{int(c)} " for t, c in otc[s:s + int(o["taxcnt_len"])])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_start_classify_multi(make_db, tmp_path, n_ctx):
+    """mtb_start_classify_multi: the QuerySplit loop spread over several contexts (here all on
+    cuda:0; one per GPU in production), batch k on context k mod n. The TSV and the report are
+    byte-identical to the one-context run (which test_start_classify_tsv pins to the oracle) and
+    the classifications are the oracle's."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 2300, paired=True, seed=47, short_frac=0.02)
+    p1, p2 = str(tmp_path / "q1.fq.gz"), str(tmp_path / "q2.fq.gz")
+    synth.write_compressed(p1, synth.fastq_bytes(r.seq1, r.off1, prefix="m"), "bgzf")
+    synth.write_compressed(p2, synth.fastq_bytes(r.seq2, r.off2, prefix="m"), "bgzf")
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    one, many = str(tmp_path / "one.tsv"), str(tmp_path / "many.tsv")
+    rep1, repn = str(tmp_path / "one_report.tsv"), str(tmp_path / "many_report.tsv")
+    clfs = [Classifier(par, db_dir=db_dir, device=0) for _ in range(n_ctx)]
+    try:
+        assert clfs[0].startClassify(one, reads_per_batch=257, report_tsv=rep1) == r.n
+        assert clfs[0].startClassify(many, reads_per_batch=257, report_tsv=repn, peers=clfs[1:]) == r.n
+        assert clfs[0].last_run["batches"] == (r.n + 256) // 257
+    finally:
+        for c in clfs:
+            c.close()
+    assert open(many, "rb").read() == open(one, "rb").read()
+    assert open(repn, "rb").read() == open(rep1, "rb").read()
+    odb = oc.OracleDb(db_dir)
+    ores, _ = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    body = [l.split("\t") for l in open(many).read().split("\n")[1:] if l]
+    assert [int(f[2]) for f in body] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
