@@ -69,6 +69,14 @@ def setClassifyDefaults() -> LocalParameters:
     return LocalParameters()
 
 
+def _after_torch(t) -> None:
+    """Device tensors handed to the library were made on torch's current stream (or RCCL's, which
+    torch's current stream waits for); the library runs on its own non-blocking stream, so that
+    work must be complete before the call."""
+    import torch
+    torch.cuda.current_stream(t.device).synchronize()
+
+
 @dataclasses.dataclass
 class BatchResult:
     results: np.ndarray   # RESULT_DTYPE per read
@@ -98,6 +106,7 @@ class Classifier:
         if db_resident is not None:
             self._resident = db_resident
             cp = par.to_c()
+            cp.db_part, cp.db_parts = int(db_part[0]), int(db_part[1])  # a resident part of a partitioned DB
             check(lib().mtb_open_resident(ctypes.byref(db_resident.c_resident()),
                                           ctypes.byref(db_resident.host.c_struct()), ctypes.byref(cp), device,
                                           ctypes.byref(self.handle)), "mtb_open_resident")
@@ -144,6 +153,7 @@ class Classifier:
             flags |= _abi.MTB_MATCH_ONLY
             fetch = False
         if device_input:
+            _after_torch(seq1)
             ptrs = [ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
                     for t in (seq1, off1, seq2, off2)]
         else:
@@ -251,6 +261,7 @@ class Classifier:
         no dead-match pruning, so matches() returns every match afterwards."""
         on_dev = not isinstance(matches, np.ndarray)
         if on_dev:
+            _after_torch(matches)
             ps = [ctypes.c_void_p(t.data_ptr()) for t in (matches, chunk_counts, query_len)]
         else:
             self._keep = tuple(np.ascontiguousarray(a) for a in (matches, chunk_counts, query_len))

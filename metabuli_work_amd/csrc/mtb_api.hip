@@ -173,7 +173,9 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     int rc = validate_params(par);
     if (rc != MTB_OK) return rc;
     if (res) {
-        if (par->db_parts > 1) { set_error("a resident DB cannot be range-partitioned: pass each part's arrays"); return MTB_ERR_ARG; }
+        // a resident part of a range-partitioned DB (db_parts > 1): the caller passes the part's own
+        // records, its last one the next part's first k-mer (as slice_db_part keeps it), or none
+        // after the last part
         if (!res->records || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
     } else {
         if (!check_db(db)) return MTB_ERR_DB;

@@ -108,6 +108,51 @@ def classify_sharded(clf, seq1, off1, seq2=None, off2=None, group=None):
             all_tc.cpu().numpy().reshape(-1).view(TAXCNT_DTYPE))
 
 
+def classify_batches_sharded(clf, batches, group=None, device_input: bool = False):
+    """Replicated DB, sharded by batch index: `batches` yields the run's batches in input order —
+    (seq1, off1, seq2, off2) tuples, or callables returning one, so a rank never materialises the
+    batches it skips — and rank r classifies batches r, r + N, r + 2N, ... (the reference's
+    QuerySplit loop, Classifier.cpp:81-133, dealt round-robin over the GPUs). The result records and
+    taxID:count lists are gathered (C1) and put back in batch order. Returns (results
+    RESULT_DTYPE numpy, taxcnt TAXCNT_DTYPE numpy) of the whole run on every rank. (For files on one
+    node, mtb_start_classify_multi is the native form: one parser feeding every GPU.)"""
+    from ._abi import RESULT_DTYPE, TAXCNT_DTYPE
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    recs, pool, sizes, used = [], [], [], 0
+    for k, b in enumerate(batches):
+        if k % world != rank:
+            continue
+        b = b() if callable(b) else b
+        br = clf.classify_batch(*b, device_input=device_input)
+        rec = br.results.view(np.uint8).reshape(-1, RESULT_BYTES).copy()
+        rec.view(np.int32).reshape(-1, RESULT_BYTES // 4)[:, _TC_OFFSET_COL] += used  # onto the rank's pool
+        used += len(br.taxcnt)
+        recs.append(rec)
+        pool.append(br.taxcnt.view(np.uint8).reshape(-1, TAXCNT_BYTES))
+        sizes.append(len(rec))
+    rec = torch.from_numpy(np.concatenate(recs) if recs else np.zeros((0, RESULT_BYTES), np.uint8))
+    tc = torch.from_numpy(np.concatenate(pool) if pool else np.zeros((0, TAXCNT_BYTES), np.uint8))
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rec, tc = rec.to(dev), tc.to(dev)
+    all_rec, all_tc = gather_results(rec, tc, group)
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, sizes, group=group)
+    # rank-ordered gathered records -> batch order (the taxcnt offsets index the gathered pool, so
+    # the records move without rebasing)
+    base, start = 0, {}
+    for r in range(world):
+        for j, n in enumerate(per_rank[r]):
+            start[r + j * world] = (base, n)
+            base += n
+    order = np.concatenate([np.arange(a, a + n) for a, n in (start[k] for k in sorted(start))]) if start else \
+        np.zeros(0, np.int64)
+    all_rec = all_rec.cpu().numpy()[order]
+    return all_rec.reshape(-1).view(RESULT_DTYPE), all_tc.cpu().numpy().reshape(-1).view(TAXCNT_DTYPE)
+
+
 # ---------------------------------------------------------------------------------------------
 # Range-partitioned DB (SURVEY §8(e), config 5): rank r holds DB part r (AA-aligned k-mer range,
 # mtb_partition_bounds) and matches EVERY read of the batch against it; the matches then go

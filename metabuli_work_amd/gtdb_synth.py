@@ -112,66 +112,197 @@ def _filler_chunk(lo: int, hi: int, count: int, g: torch.Generator, cnt_t: torch
     return v, tax
 
 
+class GtdbRecipe:
+    """The GTDB-scale DB as a recipe that builds any AA-rank range of it on demand: the true-signal
+    part (built once, kept sorted in HBM) plus filler generated per chunk of the AA-rank space with a
+    per-chunk seed, so a chunk's k-mers do not depend on which other chunks were built. The whole DB
+    is chunks [0, n_chunks) (config 3); a range-partitioned DB (config 5: more k-mers than one GPU
+    holds) is built one part at a time, each part a run of whole chunks — AA-aligned, as the
+    reference's split entries are (IndexCreator.cpp:843-851) — plus its guard k-mer."""
+
+    def __init__(self, dev: torch.device, n_true_species: int = 1000, genome_len: int = 3_000_000,
+                 total_species: int = 129_671, target_kmers: int = 12_000_000_000, strains: int = 2, seed: int = 6,
+                 n_chunks: int = 64, before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
+                 log: Callable[[str], None] = lambda s: None, syncmer: int = 0, smer_len: int = 5,
+                 per_genus: int = 1, species_div: float = 0.0):
+        self.dev, self.seed, self.n_chunks, self.log = dev, seed, n_chunks, log
+        taxo = synth.make_taxonomy(total_species, strains, seed=seed,
+                                   block_species=n_true_species if per_genus > 1 else 0, block_size=per_genus)
+        taxo, gen, seq, off_t, _ = make_genomes_gpu(n_true_species, genome_len, strains, seed, dev, taxo=taxo,
+                                                    per_genus=per_genus, species_div=species_div)
+        if before_free is not None:
+            before_free(seq, off_t)
+        par = default_params(kmer_format=2, seq_mode=2, syncmer=syncmer, smer_len=smer_len)
+        self.tv, self.ti = build_db_device(gen, taxo, par, device=dev.index or 0, device_seq=(seq, off_t))
+        del seq, off_t
+        torch.cuda.empty_cache()
+        self.n_true = self.tv.numel()
+        log(f"true-signal DB part: {self.n_true / 1e9:.3f}G k-mers")
+        # filler strains: those of the skeleton species beyond the true-signal ones
+        rank = np.array(taxo.rank)
+        sp_all = taxo.taxid[rank == "species"]
+        self.n_species = len(sp_all)
+        filler_sp = set(sp_all[n_true_species:].tolist())
+        strains_f = np.array([t for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank)
+                              if r == "no rank" and p in filler_sp], np.int32)
+        self.strain_t = torch.from_numpy(strains_f).to(dev)
+        self.cnt_t = torch.from_numpy(codon_counts().astype(np.float32)).to(dev)
+        n_fill = max(0, int(target_kmers) - self.n_true)
+        self.per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
+        self.edges = [c * AA_RANKS // n_chunks for c in range(n_chunks + 1)]
+        e_t = torch.tensor(self.edges, dtype=torch.int64, device=dev)
+        self.cut = torch.searchsorted(self.tv, e_t << 24).cpu().tolist()  # true-signal records per chunk
+        ids = np.unique(np.concatenate([gen.taxid.astype(np.int32), strains_f]))
+        self.host = HostDb(taxo, taxid_list=ids.astype(np.int32))
+
+    def _chunk(self, c: int):
+        """Chunk c's records as (sorted values, taxIDs): its true-signal k-mers and its filler."""
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(self.seed * 7919 + 1 + 104729 * c)
+        fv, ft = _filler_chunk(self.edges[c], self.edges[c + 1], self.per[c], g, self.cnt_t, self.strain_t)
+        a, b = self.cut[c], self.cut[c + 1]
+        v = torch.cat([self.tv[a:b], fv])
+        t = torch.cat([self.ti[a:b], ft])
+        del fv, ft
+        # stable: a value held by a true-signal species and a filler species keeps species order
+        # (true-signal species have the smaller taxIDs), as the builder's (value, species) sort does
+        vs, order = torch.sort(v, stable=True)
+        return vs, t[order]
+
+    def chunk_sizes(self) -> list:
+        return [self.cut[c + 1] - self.cut[c] + self.per[c] for c in range(self.n_chunks)]
+
+    def part_chunks(self, parts: int) -> list:
+        """Chunk ranges of `parts` parts of about equal k-mer count."""
+        cs = np.cumsum([0] + self.chunk_sizes())
+        bounds = [0] + [int(np.searchsorted(cs, cs[-1] * p / parts)) for p in range(1, parts)] + [self.n_chunks]
+        for i in range(1, len(bounds)):
+            bounds[i] = min(max(bounds[i], bounds[i - 1] + 1), self.n_chunks - (len(bounds) - 1 - i))
+        return [(bounds[p], bounds[p + 1]) for p in range(parts)]
+
+    def build(self, c0: int = 0, c1: Optional[int] = None, guard: bool = False) -> "ResidentDb":
+        """Records of chunks [c0, c1) — with guard and c1 < n_chunks, plus the first k-mer of chunk
+        c1: the part's last resident k-mer, never a candidate (the reference's reader stops before
+        the DB's last k-mer, KmerMatcher.cpp:363,378), so the next part matches its AA run."""
+        c1 = self.n_chunks if c1 is None else c1
+        sizes = self.chunk_sizes()
+        g_add = 1 if guard and c1 < self.n_chunks else 0
+        n = sum(sizes[c0:c1])
+        rec = torch.empty(n + g_add + 8, 3, dtype=torch.int32, device=self.dev)
+        pos = 0
+        for c in range(c0, c1):
+            vs, ts = self._chunk(c)
+            m = vs.numel()
+            put_records(rec, pos, vs, ts)
+            pos += m
+            del vs, ts
+        if g_add:
+            vs, ts = self._chunk(c1)
+            put_records(rec, pos, vs[:1], ts[:1])
+            pos += 1
+            del vs, ts
+        torch.cuda.empty_cache()
+        rdb = ResidentDb(rec, pos, self.host, sum(self.cut[c + 1] - self.cut[c] for c in range(c0, c1)))
+        rdb.rank_range = (self.edges[c0], self.edges[c1])
+        return rdb
+
+    def free_true(self) -> None:
+        del self.tv, self.ti
+        torch.cuda.empty_cache()
+
+
 def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: int = 3_000_000,
                      total_species: int = 129_671, target_kmers: int = 12_000_000_000, strains: int = 2,
                      seed: int = 6, n_chunks: int = 64,
                      before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
                      log: Callable[[str], None] = lambda s: None, syncmer: int = 0, smer_len: int = 5,
                      per_genus: int = 1, species_div: float = 0.0) -> ResidentDb:
-    """Build the DB on `dev`. before_free(seq, off) runs while the true-signal genomes are still in
-    HBM (the bench samples its reads there). syncmer: the true-signal part holds closed syncmers
-    only (a Syncmer 1 DB, the format of GTDB R226's DB); per_genus / species_div: sister species
-    of a genus share a diverged genus genome (make_genomes_gpu), so AA runs carry several species."""
-    taxo = synth.make_taxonomy(total_species, strains, seed=seed,
-                               block_species=n_true_species if per_genus > 1 else 0, block_size=per_genus)
-    taxo, gen, seq, off_t, _ = make_genomes_gpu(n_true_species, genome_len, strains, seed, dev, taxo=taxo,
-                                                per_genus=per_genus, species_div=species_div)
-    if before_free is not None:
-        before_free(seq, off_t)
-    par = default_params(kmer_format=2, seq_mode=2, syncmer=syncmer, smer_len=smer_len)
-    tv, ti = build_db_device(gen, taxo, par, device=dev.index or 0, device_seq=(seq, off_t))
-    del seq, off_t
-    torch.cuda.empty_cache()
-    n_true = tv.numel()
-    log(f"true-signal DB part: {n_true / 1e9:.3f}G k-mers")
-    # filler strains: those of the skeleton species beyond the true-signal ones
-    rank = np.array(taxo.rank)
-    sp_all = taxo.taxid[rank == "species"]
-    filler_sp = set(sp_all[n_true_species:].tolist())
-    strains_f = np.array([t for t, p, r in zip(taxo.taxid.tolist(), taxo.parent.tolist(), taxo.rank)
-                          if r == "no rank" and p in filler_sp], np.int32)
-    strain_t = torch.from_numpy(strains_f).to(dev)
-    cnt_t = torch.from_numpy(codon_counts().astype(np.float32)).to(dev)
-    n_fill = max(0, int(target_kmers) - n_true)
-    per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
-    cap = n_true + n_fill + 8
-    rec = torch.empty(cap, 3, dtype=torch.int32, device=dev)
-    edges = torch.tensor([c * AA_RANKS // n_chunks for c in range(n_chunks + 1)], dtype=torch.int64, device=dev)
-    cut = torch.searchsorted(tv, edges << 24).cpu().tolist()
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed * 7919 + 1)
-    pos = 0
-    for c in range(n_chunks):
-        lo, hi = int(edges[c].item()), int(edges[c + 1].item())
-        fv, ft = _filler_chunk(lo, hi, per[c], g, cnt_t, strain_t)
-        a, b = cut[c], cut[c + 1]
-        v = torch.cat([tv[a:b], fv])
-        t = torch.cat([ti[a:b], ft])
-        del fv, ft
-        # stable: a value held by a true-signal species and a filler species keeps species order
-        # (true-signal species have the smaller taxIDs), as the builder's (value, species) sort does
-        vs, order = torch.sort(v, stable=True)
-        m = vs.numel()
-        put_records(rec, pos, vs, t[order])
-        pos += m
-        del v, t, vs, order
-    del tv, ti
-    torch.cuda.empty_cache()
-    ids = np.unique(np.concatenate([gen.taxid.astype(np.int32), strains_f]))
-    host = HostDb(taxo, taxid_list=ids.astype(np.int32))
-    log(f"GTDB-scale DB: {pos / 1e9:.3f}G k-mers ({n_true / 1e9:.3f}G true signal), "
-        f"{len(sp_all)} species in the taxonomy")
-    return ResidentDb(rec, pos, host, n_true)
+    """Build the whole DB on `dev` (GtdbRecipe, all chunks). before_free(seq, off) runs while the
+    true-signal genomes are still in HBM (the bench samples its reads there). syncmer: the
+    true-signal part holds closed syncmers only (a Syncmer 1 DB, the format of GTDB R226's DB);
+    per_genus / species_div: sister species of a genus share a diverged genus genome
+    (make_genomes_gpu), so AA runs carry several species."""
+    rc = GtdbRecipe(dev, n_true_species, genome_len, total_species, target_kmers, strains, seed, n_chunks,
+                    before_free, log, syncmer, smer_len, per_genus, species_div)
+    rdb = rc.build()
+    rc.free_true()
+    log(f"GTDB-scale DB: {rdb.n / 1e9:.3f}G k-mers ({rdb.n_true / 1e9:.3f}G true signal), "
+        f"{rc.n_species} species in the taxonomy")
+    return rdb
+
+
+def to_rank_fmt2(v: torch.Tensor) -> torch.Tensor:
+    """Format-2 values (int64 bit patterns) -> the resident rank form (the inverse of to_native_fmt2)."""
+    aa = _lsr(v, 24)
+    r = torch.zeros_like(aa)
+    mul = 1
+    for k in range(8):
+        r += ((aa >> (5 * k)) & 31) * mul
+        mul *= 21
+    return (r << 24) | (v & 0xFFFFFF)
+
+
+class SubDb:
+    """Parity helper (test / bench infrastructure): the DB runs of a set of AA 8-mers, collected from
+    resident DB parts, as a small DB for the oracle. A query k-mer can only match DB k-mers of its own
+    AA 8-mer (matchKmers compares AA parts first, KmerMatcher.cpp:381-400), so the oracle classifies
+    reads against the runs of their k-mers' AA 8-mers exactly as against the whole DB — provided no
+    run is cut and the last k-mer (never a candidate, KmerMatcher.cpp:363,378) is not one of them: a
+    sentinel past every collected run closes the DB."""
+
+    def __init__(self, host, ranks: torch.Tensor):
+        self.host = host
+        self.ranks = torch.unique(ranks)  # sorted AA ranks of the sample's query k-mers
+        self.vals, self.infos = [], []
+
+    @classmethod
+    def of_kmers(cls, host, kmers: np.ndarray, dev: torch.device) -> "SubDb":
+        """kmers: the oracle's extracted query k-mers (format-2 values) of the sample reads; the
+        blank slots ({0, 0}) are dropped."""
+        kmers = kmers[(kmers["value"] != 0) | (kmers["info"] != 0)]
+        v = torch.from_numpy(kmers["value"].view(np.int64).copy()).to(dev)
+        return cls(host, _lsr(to_rank_fmt2(v), 24))
+
+    def collect(self, rdb: ResidentDb, rank_lo: int = 0, rank_hi: int = AA_RANKS, db_end: bool = True,
+                chunk: int = 1 << 27) -> None:
+        """The runs of the sample's AA ranks in [rank_lo, rank_hi) from a resident DB (part).
+        db_end: rdb's last record is the DB's last k-mer, which is never a candidate: left out (the
+        sentinel takes its place)."""
+        rk = self.ranks[(self.ranks >= rank_lo) & (self.ranks < rank_hi)]
+        if rk.numel() == 0:
+            return
+        lo_k, hi_k = rk << 24, (rk + 1) << 24
+        lo = torch.zeros_like(rk)
+        hi = torch.zeros_like(rk)
+        for a in range(0, rdb.n, chunk):  # global lower bounds = sums of the chunks' counts below
+            vals = rdb.values(a, min(rdb.n, a + chunk))
+            lo += torch.searchsorted(vals, lo_k)
+            hi += torch.searchsorted(vals, hi_k)
+            del vals
+        if db_end:
+            hi = torch.clamp(hi, max=rdb.n - 1)
+        cnt = hi - lo
+        keep = cnt > 0
+        lo, cnt = lo[keep], cnt[keep]
+        if lo.numel() == 0:
+            return
+        idx = torch.repeat_interleave(lo, cnt) + (torch.arange(int(cnt.sum().item()), device=lo.device) -
+                                                   torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt))
+        self.vals.append(rdb.value_at(idx))
+        self.infos.append(rdb.records[idx, 2].clone())
+
+    def oracle_db(self, oracle_cls):
+        v = torch.cat(self.vals) if self.vals else torch.zeros(0, dtype=torch.int64, device=self.ranks.device)
+        t = torch.cat(self.infos) if self.infos else torch.zeros(0, dtype=torch.int32, device=self.ranks.device)
+        order = torch.argsort(v, stable=True)  # parts arrive in rank order already; keeps species order
+        v, t = v[order], t[order]
+        last = int((v[-1] >> 24).item()) if v.numel() else -1
+        assert last + 1 < AA_RANKS, "sample hits the last AA 8-mer rank: no room for the sentinel"
+        sent = torch.tensor([(last + 1) << 24], dtype=torch.int64, device=v.device)
+        v = torch.cat([v, sent])
+        t = torch.cat([t, t[:1] if t.numel() else torch.ones(1, dtype=torch.int32, device=v.device)])
+        sub = ResidentDb.from_arrays(v, t, self.host)
+        return encode_into_oracle(sub, oracle_cls, chunk=1 << 24), sub.n
 
 
 # ---------------------------------------------------------------------------------------------

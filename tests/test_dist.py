@@ -191,3 +191,62 @@ def test_bench_result_gather_gloo():
     for r in range(world):
         res = items[r][0].reshape(-1).view(RESULT_DTYPE)
         assert _lists(res, items[r][1].reshape(-1).view(TAXCNT_DTYPE)) == want
+
+
+class _FakeBatchClf:
+    """Stands in for Classifier.classify_batch: per read (classification = global read index + 1,
+    taxcnt list derived from it), pooled the way mtb_classify_batch pools a batch."""
+
+    def classify_batch(self, first, n, *_, device_input=False):
+        from metabuli_work_amd.classifier import BatchResult
+        res = np.zeros(n, RESULT_DTYPE)
+        lens = (np.arange(first, first + n) % 3).astype(np.uint32)
+        res["taxcnt_len"] = lens
+        res["taxcnt_offset"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        res["classification"] = np.arange(first, first + n) + 1
+        tc = np.zeros(int(lens.sum()), TAXCNT_DTYPE)
+        tc["tax_id"] = np.repeat(res["classification"], lens)
+        tc["count"] = np.concatenate([np.arange(1, k + 1) for k in lens]) if n else []
+        return BatchResult(res, tc, 0, 0, np.zeros(5, np.float32))
+
+
+def _batch_shard_worker(rank, world, port, sizes, q):
+    from metabuli_work_amd.dist import classify_batches_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+    touched = []
+
+    def batch(k):
+        touched.append(k)
+        return (starts[k], sizes[k])
+
+    res, tc = classify_batches_sharded(_FakeBatchClf(), [(lambda k=k: batch(k)) for k in range(len(sizes))])
+    q.put((rank, touched, res.view(np.uint8).copy(), tc.view(np.uint8).copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_batches_sharded_gloo(world):
+    """Batch-index sharding (dist.classify_batches_sharded): rank r materialises only batches
+    r, r + N, ...; the gathered records come back in batch order with their taxID:count lists."""
+    sizes = [4, 0, 7, 3, 5, 1, 6]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_shard_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, touched, rec, tcb in got:
+        assert touched == list(range(rank, len(sizes), world))
+        res = rec.view(RESULT_DTYPE).reshape(-1)
+        tc = tcb.view(TAXCNT_DTYPE).reshape(-1)
+        n = sum(sizes)
+        assert np.array_equal(res["classification"], np.arange(n) + 1)
+        for i, r in enumerate(res):
+            lst = tc[r["taxcnt_offset"]:r["taxcnt_offset"] + r["taxcnt_len"]]
+            assert lst["tax_id"].tolist() == [i + 1] * (i % 3) and lst["count"].tolist() == list(range(1, i % 3 + 1))

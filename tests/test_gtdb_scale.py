@@ -75,3 +75,66 @@ def test_gtdb_shaped_resident_db_parity():
     odb.close()
     compare_results(br.results, br.taxcnt, ores, otc)
     assert br.results["is_classified"].mean() > 0.5
+
+
+def test_partitioned_resident_parts_parity():
+    """Config 5's path at test scale: the GTDB-shaped DB built one AA-aligned part at a time
+    (GtdbRecipe.build with its guard k-mer), each part opened alone (mtb_open_resident, db_part),
+    the reads matched against every part (MTB_MATCH_ONLY), the per-part match segments scored
+    together (mtb_assign_chunks, the all-to-all receive layout). Results equal the oracle's on the
+    whole DB, and the oracle on the sub-DB of the reads' AA runs (gtdb_synth.SubDb, the bench's
+    config-5 parity check) gives the same results too."""
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+    from metabuli_work_amd.gpu_synth import make_reads_gpu
+    from metabuli_work_amd.gtdb_synth import GtdbRecipe, SubDb, encode_into_oracle
+    from tests.test_gpu_parity import compare_results
+
+    dev = torch.device("cuda", 0)
+    got = {}
+
+    def grab(seq, off):
+        got["reads"] = make_reads_gpu(seq, off, 2500, 77, dev)
+
+    rc = GtdbRecipe(dev, n_true_species=10, genome_len=30000, total_species=300, target_kmers=4_000_000,
+                    n_chunks=12, before_free=grab)
+    reads = _host_reads(*got["reads"])
+    n = reads.n
+    par = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    ext, _, _ = oc.extract(par.to_c(), reads)
+    sub = SubDb.of_kmers(rc.host, ext, dev)
+    P = 3
+    parts = rc.part_chunks(P)
+    assert parts[0][0] == 0 and parts[-1][1] == rc.n_chunks
+    chunks, counts, ql = [], [], None
+    for p, (c0, c1) in enumerate(parts):
+        part = rc.build(c0, c1, guard=True)
+        lo_r, hi_r = part.rank_range
+        sub.collect(part, lo_r, hi_r, db_end=(p == P - 1))
+        with Classifier(par, db_resident=part, db_part=(p, P)) as clf:
+            clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, match_only=True)
+            _, m = clf.last_counts()
+            mt = np.zeros((m, 24), np.uint8)
+            ct = np.zeros(n, np.uint32)
+            qt = np.zeros(n, np.uint32)
+            clf.copy_matches(mt, ct, qt)
+        chunks.append(mt)
+        counts.append(ct)
+        ql = qt
+        del part
+        torch.cuda.empty_cache()
+    allm = np.concatenate(chunks)
+    whole = rc.build()
+    with Classifier(par, db_resident=whole) as clf:
+        br = clf.assign_chunks(allm, len(allm), np.concatenate(counts), P, ql, n)
+        full = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+    assert np.array_equal(br.results, full.results) and np.array_equal(br.taxcnt, full.taxcnt)
+    odb = encode_into_oracle(whole, oc.OracleDb, chunk=1 << 20)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    odb.close()
+    compare_results(br.results, br.taxcnt, ores, otc)
+    sdb, sub_n = sub.oracle_db(oc.OracleDb)
+    assert sub_n < whole.n
+    sres, stc = oc.classify(sdb, par.to_c(), reads)
+    sdb.close()
+    compare_results(sres, stc, ores, otc)
+    assert br.results["is_classified"].mean() > 0.5

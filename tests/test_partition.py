@@ -226,6 +226,31 @@ def _replica_worker(rank, world, port, db_dir, seed, q):
     dist.destroy_process_group()
 
 
+def _long_reads(gen, seed):
+    from metabuli_work_amd import synth
+    return synth.make_long_reads(gen, 90, n50=3000, min_len=400, seed=seed)
+
+
+def _long_replica_worker(rank, world, port, db_dir, seed, q):
+    """Config 4's shape: seq-mode-3 reads, DB replicated, batches dealt round-robin over the ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from metabuli_work_amd import synth
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+    from metabuli_work_amd.dist import classify_batches_sharded, shard_reads
+
+    taxo = synth.make_taxonomy(14, 2, seed=11)
+    gen = synth.make_genomes(taxo, genome_len=24000, seed=12)
+    reads = _long_reads(gen, seed)
+    par = LocalParameters(seqMode=3).load_db_parameters(db_dir)
+    cuts = [(a, min(reads.n, a + 13)) for a in range(0, reads.n, 13)]  # 7 batches: ranks take 4 and 3
+    batches = [(lambda a=a, b=b: shard_reads(reads.seq1, reads.off1, a, b) + (None, None)) for a, b in cuts]
+    with Classifier(par, db_dir=db_dir, device=0) as clf:
+        res, tc = classify_batches_sharded(clf, batches)
+    q.put((rank, res.view(np.uint8).copy(), tc.view(np.uint8).copy()))
+    dist.destroy_process_group()
+
+
 def _run_two_ranks(target, db_dir, seed):
     from metabuli_work_amd._abi import RESULT_DTYPE, TAXCNT_DTYPE
 
@@ -244,22 +269,25 @@ def _run_two_ranks(target, db_dir, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["partitioned", "replicated"])
+@pytest.mark.parametrize("mode", ["partitioned", "replicated", "replicated_long"])
 def test_classify_two_ranks(make_db, mode):
     """Two processes on cuda:0 over gloo. partitioned: each holds half of the DB, matches go
     all-to-all to the read owners (config 5); replicated: each holds the whole DB and classifies
-    half of the reads (configs 2-4). Either way rank 0's gathered results AND taxID:count lists
+    half of the reads (configs 2-3); replicated_long: seq-mode-3 long reads in batches dealt
+    round-robin over the ranks (config 4, classify_batches_sharded). Either way rank 0's gathered results AND taxID:count lists
     are the oracle's, element by element — what one GPU writes to the TSV."""
     from tests.test_gpu_parity import compare_results
     from metabuli_work_amd.classifier import LocalParameters
 
     db_dir, taxo, gen = make_db("fmt2")  # DB_CONFIGS["fmt2"]: 14 species x 2 strains, 24 kb, seeds 11/12
-    reads = _reads(gen, 43)
-    par_c = LocalParameters(seqMode=2).load_db_parameters(db_dir).to_c()
+    long = mode == "replicated_long"
+    reads = _long_reads(gen, 43) if long else _reads(gen, 43)
+    par_c = LocalParameters(seqMode=3 if long else 2).load_db_parameters(db_dir).to_c()
     odb = oc.OracleDb(db_dir)
     ores, otc = oc.classify(odb, par_c, reads)
     odb.close()
-    res, tc = _run_two_ranks(_part_worker if mode == "partitioned" else _replica_worker, db_dir, 43)
+    target = {"partitioned": _part_worker, "replicated": _replica_worker, "replicated_long": _long_replica_worker}[mode]
+    res, tc = _run_two_ranks(target, db_dir, 43)
     assert len(res) == len(ores)
     assert int(res["taxcnt_len"].sum()) == len(tc)
     compare_results(res, tc, ores, otc)
