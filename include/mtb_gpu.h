@@ -64,10 +64,11 @@ typedef struct mtb_params {
     int32_t em;               /* --em: classified reads keep their best species (no lower-rank
                                  BFS, Taxonomer.cpp:193-201) and record EM mappings (mtb_em)    */
     int32_t threads;          /* host threads (oracle / host parsing only)                     */
-    int32_t mask_mode;        /* must be 0: tantan masking is out of scope                     */
+    int32_t mask_mode;        /* --mask-residues 1: tantan low-complexity masking of the reads
+                                 before extraction (KmerExtractor.cpp:328-335)                  */
     int32_t db_part;          /* range-partitioned DB: this context holds part db_part of      */
     int32_t db_parts;         /* db_parts AA-aligned k-mer ranges (0 or 1 = the whole DB)      */
-    int32_t reserved[1];
+    float mask_prob;          /* --mask-prob (0.9): tantan's minMaskProb                       */
 } mtb_params;
 
 /* Query k-mer: 16 B, same layout as Kmer{uint64 value; QueryKmerInfo} (Kmer.h:11-31,45-46).
@@ -211,6 +212,11 @@ int mtb_get_matches(mtb_ctx* ctx, mtb_match* out, uint64_t capacity, uint64_t* n
  * of read i (seqID i+1). Keeps every match (mtb_get_matches returns them in compareMatches order). */
 int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matches,
                        const uint32_t* query_len, uint32_t n_reads, mtb_result* results);
+
+/* K0M alone: SeqIterator::maskLowComplexityRegions (SeqIterator.cpp:154-175; tantan, restated:
+ * parity unpinned) of n reads with the context's mask_prob, on the device. seq/off/out are host
+ * arrays; out receives off[n] bytes: 'N' where masked (or not A/C/G/T/U), else the input letter. */
+int mtb_mask_reads(mtb_ctx* ctx, const char* seq, const uint64_t* off, uint32_t n_reads, char* out);
 
 /* ---- range-partitioned DB across GPUs ---------------------------- */
 /* A DB larger than one GPU's HBM is cut at split entries (DiffIdxSplit, Kmer.h:111-119; written

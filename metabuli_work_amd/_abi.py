@@ -23,7 +23,7 @@ class MtbParams(ctypes.Structure):
         ("mask_mode", ctypes.c_int32),
         ("db_part", ctypes.c_int32),
         ("db_parts", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 1),
+        ("mask_prob", ctypes.c_float),
     ]
 
 
@@ -65,7 +65,7 @@ def default_params(**kw) -> MtbParams:
     """setClassifyDefaults (classify.cpp:10-37)."""
     p = MtbParams(seq_mode=2, kmer_format=1, syncmer=0, smer_len=5, reduced_aa=0, skip_redundancy=0,
                   min_score=0.0, min_sp_score=0.0, min_cons_cnt=4, min_cons_cnt_euk=9, tie_ratio=0.95,
-                  accession_level=0, em=0, threads=1, mask_mode=0)
+                  accession_level=0, em=0, threads=1, mask_mode=0, mask_prob=0.9)
     for k, v in kw.items():
         setattr(p, k, v)
     return p

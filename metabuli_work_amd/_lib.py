@@ -22,7 +22,7 @@ EXPORTED = [
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
-    "mtb_ctx_device", "mtb_start_classify_multi",
+    "mtb_ctx_device", "mtb_start_classify_multi", "mtb_mask_reads",
 ]
 
 
@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_start_classify.argtypes = [vp, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_start_classify_multi.argtypes = [P(vp), i32, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_ctx_device.argtypes = [vp]
+    L.mtb_mask_reads.argtypes = [vp, vp, vp, u32, vp]
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
     L.mtb_get_em_mappings.argtypes = [vp, u32, vp, u64, P(u64)]
     L.mtb_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, P(u64), P(MtbEmStats)]

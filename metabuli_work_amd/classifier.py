@@ -45,6 +45,7 @@ class LocalParameters:
     em: int = 0
     threads: int = 1
     maskMode: int = 0
+    maskProb: float = 0.9   # --mask-prob (classify.cpp:32)
     printLineage: int = 0   # --lineage: the TSV's lineage column (Reporter.cpp:41-43,59-61)
     filenames: List[str] = dataclasses.field(default_factory=list)
 
@@ -54,7 +55,7 @@ class LocalParameters:
                          min_score=self.minScore, min_sp_score=self.minSpScore, min_cons_cnt=self.minConsCnt,
                          min_cons_cnt_euk=self.minConsCntEuk, tie_ratio=self.tieRatio,
                          accession_level=self.accessionLevel, em=self.em, threads=self.threads,
-                         mask_mode=self.maskMode)
+                         mask_mode=self.maskMode, mask_prob=self.maskProb)
 
     def load_db_parameters(self, db_dir: str) -> "LocalParameters":
         p = self.to_c()

@@ -71,7 +71,7 @@ struct mtb_ctx {
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
-    int pruneAfter = 0;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode
+    int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune)
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
@@ -103,6 +103,7 @@ struct mtb_ctx {
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
+    DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
     static constexpr int kNumStats = 14;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
@@ -160,7 +161,7 @@ static hipError_t upload(T** dst, const std::vector<T>& v, hipStream_t s) {
 static int validate_params(const mtb_params* p) {
     if (p->reduced_aa) { set_error("reduced-AA DBs (ReducedKmerMatcher) are out of scope"); return MTB_ERR_UNSUPPORTED; }
     if (p->em && p->db_parts > 1) { set_error("--em needs the whole DB in one context"); return MTB_ERR_UNSUPPORTED; }
-    if (p->mask_mode) { set_error("low-complexity masking is out of scope"); return MTB_ERR_UNSUPPORTED; }
+    if (p->mask_mode && !(p->mask_prob > 0.0f && p->mask_prob <= 1.0f)) { set_error("mask_prob must be in (0, 1]"); return MTB_ERR_ARG; }
     if (p->kmer_format != 1 && p->kmer_format != 2) { set_error("kmer_format must be 1 or 2"); return MTB_ERR_UNSUPPORTED; }
     if (p->syncmer && p->kmer_format != 2) { set_error("syncmer requires kmer_format 2"); return MTB_ERR_UNSUPPORTED; }
     if (p->syncmer && (p->smer_len < 1 || p->smer_len > 8)) { set_error("smer_len must be in [1, 8]"); return MTB_ERR_ARG; }
@@ -260,7 +261,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
     if (const char* e = getenv("MTB_BIG_GROUPS")) c->bigGroups = atoi(e) != 0;
     if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;
-    if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : 0;
+    if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : atoi(e) == 0 ? 0 : 2;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
@@ -376,7 +377,7 @@ void mtb_close(mtb_ctx* c) {
                       &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
-                      &c->emCnt32, &c->emOff};
+                      &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
@@ -779,7 +780,51 @@ static int check_err_flag(mtb_ctx* c) {
     return MTB_OK;
 }
 
+// SeqIterator::maskLowComplexityRegions on the device for the batch's mates: masked copies in
+// maskOut1/2 (the extraction reads those), tantan's scratch sized by the longer mate array.
+static int mask_mates(mtb_ctx* c, const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
+                      uint32_t n, const uint8_t** out1, const uint8_t** out2) {
+    hipStream_t s = c->stream;
+    uint64_t nb[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&nb[0], off1 + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (seq2) HIP_TRY(hipMemcpyAsync(&nb[1], off2 + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t most = std::max(nb[0], nb[1]);
+    HIP_TRY(c->maskProb.ensure(sizeof(float) * (most + 1)));
+    HIP_TRY(c->maskScale.ensure(sizeof(double) * tantan_scale_elems(most, n)));
+    const TantanTables tt = make_tantan_tables(c->par.mask_prob);
+    HIP_TRY(c->maskOut1.ensure(nb[0] + 1));
+    launch_tantan_mask(seq1, off1, n, tt, c->maskProb.as<float>(), c->maskScale.as<double>(), c->maskOut1.as<uint8_t>(), s);
+    *out1 = c->maskOut1.as<uint8_t>();
+    if (seq2) {
+        HIP_TRY(c->maskOut2.ensure(nb[1] + 1));
+        launch_tantan_mask(seq2, off2, n, tt, c->maskProb.as<float>(), c->maskScale.as<double>(),
+                           c->maskOut2.as<uint8_t>(), s);
+        *out2 = c->maskOut2.as<uint8_t>();
+    }
+    HIP_TRY(hipGetLastError());
+    return MTB_OK;
+}
+
 extern "C" {
+
+int mtb_mask_reads(mtb_ctx* c, const char* seq, const uint64_t* off, uint32_t n, char* out) {
+    if (!c || (n && (!seq || !off || !out))) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (!n) return MTB_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t nb = off[n];
+    HIP_TRY(c->seq1.ensure(nb + 1));
+    HIP_TRY(c->off1.ensure(sizeof(uint64_t) * (n + 1)));
+    HIP_TRY(hipMemcpyAsync(c->seq1.p, seq, nb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->off1.p, off, sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, s));
+    const uint8_t *m1 = nullptr, *m2 = nullptr;
+    int rc = mask_mates(c, c->seq1.as<uint8_t>(), c->off1.as<uint64_t>(), nullptr, nullptr, n, &m1, &m2);
+    if (rc != MTB_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out, m1, nb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MTB_OK;
+}
 
 int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const char* seq2, const uint64_t* off2,
                        uint32_t n, uint32_t flags, mtb_result* results) {
@@ -815,6 +860,10 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
             dSeq2 = c->seq2.as<uint8_t>();
             dOff2 = c->off2.as<uint64_t>();
         }
+    }
+    if (c->par.mask_mode) {  // K0M: tantan masking of every mate (KmerExtractor.cpp:328-335)
+        int rc = mask_mates(c, dSeq1, dOff1, dSeq2, dOff2, n, &dSeq1, &dSeq2);
+        if (rc != MTB_OK) return rc;
     }
     for (uint64_t& x : c->stats) x = 0;
     HIP_TRY(c->devStats.ensure(sizeof(unsigned long long) * 4));

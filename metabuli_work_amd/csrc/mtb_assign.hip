@@ -251,6 +251,201 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
     if (lane == 0) liveCnt[r] = (uint32_t)nLive;
 }
 
+// Bitonic sort of one key per element (no payload: the keys carry their record's index), the
+// network of wave_bitonic_sort: element e = 64 * slot + lane.
+template <int E, typename K>
+__device__ __forceinline__ void wave_bitonic_keys(K (&k)[E], int lane) {
+#pragma unroll
+    for (int kk = 2; kk <= 64 * E; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int js = j >> 6;
+#pragma unroll
+                for (int sl = 0; sl < E; sl++) {
+                    if (sl & js) continue;
+                    const int s2 = sl | js;
+                    const bool up = ((64 * sl + lane) & kk) == 0;
+                    if ((k[sl] > k[s2]) == up) {
+                        const K t = k[sl];
+                        k[sl] = k[s2];
+                        k[s2] = t;
+                    }
+                }
+            } else {
+                const bool lower = (lane & j) == 0;
+#pragma unroll
+                for (int sl = 0; sl < E; sl++) {
+                    const bool up = ((64 * sl + lane) & kk) == 0;
+                    const K pk = __shfl_xor(k[sl], j, 64);
+                    if ((k[sl] > pk) == (lower == up)) k[sl] = pk;
+                }
+            }
+        }
+    }
+}
+
+// n (<= 64 ES) keys of LDS array a sorted in place by one wave.
+template <int ES, typename K>
+__device__ __forceinline__ void lds_sort_keys(K* a, int n, int lane) {
+    K k[ES];
+#pragma unroll
+    for (int sl = 0; sl < ES; sl++) {
+        const int e = 64 * sl + lane;
+        k[sl] = e < n ? a[e] : (K)~(K)0;
+    }
+    wave_bitonic_keys<ES, K>(k, lane);
+#pragma unroll
+    for (int sl = 0; sl < ES; sl++) {
+        const int e = 64 * sl + lane;
+        if (e < n) a[e] = k[sl];
+    }
+}
+
+template <int E, typename K>
+__device__ __forceinline__ void lds_sort_keys_n(K* a, int n, int lane) {
+    if (n <= 64) lds_sort_keys<1, K>(a, n, lane);
+    else if (E >= 2 && n <= 128) lds_sort_keys<(E >= 2 ? 2 : 1), K>(a, n, lane);
+    else if (E >= 4 && n <= 256) lds_sort_keys<(E >= 4 ? 4 : 1), K>(a, n, lane);
+    else lds_sort_keys<E, K>(a, n, lane);
+}
+
+// The pruned sort on compact keys (the default for 65-512 matches): prune as prune_then_sort does
+// (LDS hash counts of (species, frame) pairs), then replace each live species by its rank among the
+// read's live species (the distinct species sorted once, usually a few dozen), so that
+// (rank:9 | frame:3 | pos:29 | record:9) is one 64-bit key in (species, frame, pos) order whose low
+// bits name the LDS record: the network moves one 64-bit value per element instead of a 128-bit key
+// and an index (fewer cross-lane shuffles, a third of the sort registers). Elements tied on
+// (species, frame, pos) — one query k-mer matching several DB k-mers of the species — take their
+// places inside the tie by (hamming, dna, target), the rest of compareMatches' order, counted from
+// the LDS records (ties are short runs of neighbours). Same output as prune_then_sort.
+template <int E>
+struct RankLds {
+    union {
+        struct {
+            uint32_t spKey[128 * E];    // species | live << 31
+            uint32_t pairKey[128 * E];  // (species slot << 3 | frame) + 1; then the rank of a species slot
+            uint32_t pairCnt[128 * E];  // pair counts; then the live species list
+        } t;
+        struct {
+            uint64_t key[64 * E];  // the live matches' keys, sorted in place
+            uint64_t lo[64 * E];   // record: hamming:8 | dna:24 | target:32
+            uint32_t sp[64 * E];   // record: species
+            uint32_t rx[64 * E];   // record: rightEndHamming << 16
+        } c;
+    };
+};
+
+template <int E>
+__device__ __forceinline__ RankLds<E>& rank_lds() {  // one LDS instance per E whatever the input type
+    __shared__ RankLds<E> lds;
+    return lds;
+}
+
+template <int E, typename In>
+__device__ __forceinline__ void prune_rank_sort(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
+                                                uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
+    constexpr uint32_t T = 128 * E;  // load <= 1/2
+    constexpr uint32_t kLive = 0x80000000u;
+    RankLds<E>& L = rank_lds<E>();
+    uint32_t *spKey = L.t.spKey, *pairKey = L.t.pairKey, *pairCnt = L.t.pairCnt;
+    for (uint32_t i = lane; i < T; i += 64) {
+        spKey[i] = 0;
+        pairKey[i] = 0;
+        pairCnt[i] = 0;
+    }
+    __syncthreads();
+    uint64_t h[E], l[E];
+    uint32_t ps[E], ss[E], rx[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const int e = 64 * sl + lane;
+        h[sl] = l[sl] = 0;
+        ps[sl] = ss[sl] = rx[sl] = 0;
+        if (e < n) {
+            const mtb_match m = in.full((uint32_t)e);
+            match_key(m, h[sl], l[sl]);
+            rx[sl] = (uint32_t)m.right_end_hamming << 16;
+            ss[sl] = lds_insert<uint32_t>(spKey, T, (uint32_t)(h[sl] >> 32));
+            ps[sl] = lds_insert<uint32_t>(pairKey, T, (ss[sl] << 3 | ((uint32_t)(h[sl] >> 29) & 7u)) + 1u);
+            atomicAdd(&pairCnt[ps[sl]], 1u);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sl = 0; sl < E; sl++)
+        if (64 * sl + lane < n && pairCnt[ps[sl]] >= pm) spKey[ss[sl]] |= kLive;  // same value from every writer
+    __syncthreads();
+    bool live[E];
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) live[sl] = 64 * sl + lane < n && (spKey[ss[sl]] & kLive);
+    // the live species, sorted: their ranks (pairKey and pairCnt are dead now)
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t* spList = pairCnt;
+    int S = 0;
+    for (uint32_t i0 = 0; i0 < T; i0 += 64) {
+        const uint32_t v = spKey[i0 + lane];
+        const bool lv = (v & kLive) != 0;
+        const uint64_t m = __ballot(lv);
+        if (lv) spList[S + (int)__popcll(m & lt)] = v & ~kLive;
+        S += (int)__popcll(m);
+    }
+    __syncthreads();
+    lds_sort_keys_n<E, uint32_t>(spList, S, lane);
+    __syncthreads();
+    for (int e = lane; e < S; e += 64) {  // rank of each live species, stored at its table slot
+        const uint32_t v = spList[e];
+        uint32_t i = (uint32_t)(((uint64_t)v * 0x9E3779B97F4A7C15ull) >> 40) & (T - 1);
+        while ((spKey[i] & ~kLive) != v) i = (i + 1) & (T - 1);
+        pairKey[i] = (uint32_t)e;
+    }
+    __syncthreads();
+    uint64_t key[E];
+    int nLive = 0;
+#pragma unroll
+    for (int sl = 0; sl < E; sl++) {
+        const uint64_t m = __ballot(live[sl]);
+        const uint32_t p = (uint32_t)(nLive + (int)__popcll(m & lt));
+        key[sl] = live[sl] ? ((uint64_t)pairKey[ss[sl]] << 41 | ((h[sl] >> 29) & 7ull) << 38 |
+                              (h[sl] & 0x1FFFFFFFull) << 9 | p)
+                           : 0;
+        nLive += (int)__popcll(m);
+    }
+    __syncthreads();  // the tables are dead: their bytes take the live records and keys
+#pragma unroll
+    for (int sl = 0; sl < E; sl++)
+        if (live[sl]) {
+            const uint32_t p = (uint32_t)(key[sl] & 511u);
+            L.c.key[p] = key[sl];
+            L.c.lo[p] = l[sl];
+            L.c.sp[p] = (uint32_t)(h[sl] >> 32);
+            L.c.rx[p] = rx[sl];
+        }
+    __syncthreads();
+    lds_sort_keys_n<E, uint64_t>(L.c.key, nLive, lane);
+    __syncthreads();
+    // the segment's read (every match of a segment carries it); the keys and records hold the rest
+    const uint64_t seqBits = nLive ? in.full(0).qinfo & (0x1FFFFFFFull << 32) : 0;
+    for (int e = lane; e < nLive; e += 64) {
+        const uint64_t k = L.c.key[e];
+        const uint32_t p = (uint32_t)(k & 511u);
+        const uint64_t pre = k >> 9, lo = L.c.lo[p];
+        int at = e;  // place inside a (species, frame, pos) tie: by (hamming, dna, target)
+        for (int j = e - 1; j >= 0 && (L.c.key[j] >> 9) == pre; j--) at -= L.c.lo[L.c.key[j] & 511u] > lo;
+        for (int j = e + 1; j < nLive && (L.c.key[j] >> 9) == pre; j++) at += L.c.lo[L.c.key[j] & 511u] < lo;
+        mtb_match m;
+        m.qinfo = ((k >> 38) & 7ull) << 61 | seqBits | (uint32_t)((k >> 9) & 0x1FFFFFFFu);
+        m.target_id = (uint32_t)lo;
+        m.species_id = L.c.sp[p];
+        m.dna_encoding = (uint32_t)(lo >> 32) & 0xFFFFFFu;
+        m.right_end_hamming = (uint16_t)(L.c.rx[p] >> 16);
+        m.hamming = (uint8_t)(lo >> 56);
+        m.pad = 0;
+        out[base + at] = m;
+    }
+    if (lane == 0) liveCnt[r] = (uint32_t)nLive;
+}
+
 // Sort all, then prune on the sorted segment (kAfter, and E == 1): a (species, frame) group of >= pm
 // matches starts at e when e + pm - 1 holds its pair; a species run with such a group is live. Its
 // LDS is 64E bytes, so occupancy is bound by registers, not by prune_then_sort's hash tables.
@@ -323,21 +518,33 @@ __device__ __forceinline__ void sort_then_prune(const In& in, mtb_match* __restr
     if (lane == 0) liveCnt[r] = kept;
 }
 
-// kMode (E >= 2, with pruning): 0 = prune, then sort the live matches (prune_then_sort); 1 = sort
-// all, then prune (sort_then_prune).
-template <int E, typename In, int kMode = 0>
+// kMode (E >= 2, with pruning): 2 = prune, then sort the live matches on compact rank keys
+// (prune_rank_sort, the default); 0 = prune, then sort the live matches' full keys
+// (prune_then_sort); 1 = sort all, then prune (sort_then_prune).
+// kMode 3: no pruning (the full sort below), a kernel of its own so that its 128-bit network does not
+// set the pruned kernels' register budget.
+template <int E, typename In, int kMode = 2>
 __device__ __forceinline__ void segsort_regs(const In& in, mtb_match* __restrict__ out, uint64_t base, int n, int lane,
                                              uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
-    if constexpr (E >= 2 && kMode == 1) {
+    if constexpr (E >= 2 && kMode == 2) {
+        if (liveCnt) {
+            prune_rank_sort<E>(in, out, base, n, lane, liveCnt, r, pm);
+            return;
+        }
+        // unpruned: the small kernel (E 2) falls through to the full sort; launch_sorts sends the
+        // E 4 / 8 kernels' unpruned batches to kMode 3
+        if constexpr (E > 2) return;
+    } else if constexpr (E >= 2 && kMode == 1) {
         if (liveCnt && pm <= 64) {
             sort_then_prune<E>(in, out, base, n, lane, liveCnt, r, pm);
             return;
         }
-    } else if constexpr (E >= 2) {
+    } else if constexpr (E >= 2 && kMode == 0) {
         if (liveCnt) {
             prune_then_sort<E>(in, out, base, n, lane, liveCnt, r, pm);
             return;
         }
+        if constexpr (E > 2) return;
     }
     uint64_t h[E], l[E];
     uint32_t x[E];
@@ -984,13 +1191,18 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
     // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts
 #define MTB_REGS(E, M) k_segsort_regs<E, M><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen)
+    if (!liveCnt) mode = 3;  // no pruning: the full-key sort
     if (maxSeg > 128) {
         if (mode == 1) MTB_REGS(4, 1);
-        else MTB_REGS(4, 0);
+        else if (mode == 0) MTB_REGS(4, 0);
+        else if (mode == 3) MTB_REGS(4, 3);
+        else MTB_REGS(4, 2);
     }
     if (maxSeg > 256) {
         if (mode == 1) MTB_REGS(8, 1);
-        else MTB_REGS(8, 0);
+        else if (mode == 0) MTB_REGS(8, 0);
+        else if (mode == 3) MTB_REGS(8, 3);
+        else MTB_REGS(8, 2);
     }
 #undef MTB_REGS
     if (maxSeg > kSmallSeg)

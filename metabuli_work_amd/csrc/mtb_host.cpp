@@ -427,6 +427,40 @@ bool slice_db_part(HostDb& db, int part, int parts) {
 
 }  // namespace mtb
 
+namespace mtb {
+
+// tantan's parameters as SeqIterator::maskLowComplexityRegions passes them (SeqIterator.cpp:160-172)
+// and the nucleotide likelihood ratios exp(lambda * score): +2 match, -3 mismatch over ACGT, -1
+// against N, lambda of that scoring at uniform base frequencies (MMseqs2's NucleotideMatrix /
+// ProbabilityMatrix are not in the mount: an assumption).
+TantanTables make_tantan_tables(float maskProb) {
+    TantanTables t{};
+    const double repeatProb = 0.005, repeatEndProb = 0.05, decay = 0.9;
+    double lo = 0.1, hi = 2.0;  // 0.25 e^{2 lambda} + 0.75 e^{-3 lambda} = 1
+    for (int it = 0; it < 200; it++) {
+        const double mid = 0.5 * (lo + hi);
+        if (0.25 * std::exp(2 * mid) + 0.75 * std::exp(-3 * mid) > 1.0) hi = mid; else lo = mid;
+    }
+    const double lambda = 0.5 * (lo + hi);
+    for (int a = 0; a < 5; a++)
+        for (int b = 0; b < 5; b++) {
+            const int sc = (a == 4 || b == 4) ? -1 : (a == b ? 2 : -3);
+            t.lr[5 * a + b] = std::exp(lambda * sc);
+        }
+    double p = repeatProb * (1 - decay) / (1 - std::pow(decay, kTantanOffsets));  // firstRepeatOffsetProb
+    for (int i = 0; i < kTantanOffsets; i++) {
+        t.b2f[i] = p;
+        p *= decay;
+    }
+    t.b2b = 1 - repeatProb;
+    t.f2b = repeatEndProb;
+    t.f2f = 1 - repeatEndProb;
+    t.minMask = (double)maskProb;
+    return t;
+}
+
+}  // namespace mtb
+
 using namespace mtb;
 
 extern "C" {
@@ -448,6 +482,7 @@ void mtb_default_params(mtb_params* p) {  // setClassifyDefaults (classify.cpp:1
     p->em = 0;
     p->threads = 1;
     p->mask_mode = 0;
+    p->mask_prob = 0.9f;
 }
 
 int mtb_load_db_parameters(const char* dir, mtb_params* par) {  // loadDbParameters (common.cpp:88-133)

@@ -323,4 +323,19 @@ void launch_em_reclassify(const float* score, const uint32_t* spIdx, const int32
                           const uint32_t* qId, uint64_t nQ, const double* p, const double* lf, const TaxDevice& t,
                           mtb_em_read* out, hipStream_t s);
 
+// ---- K0M: tantan low-complexity masking of the reads (mtb_mask.hip; --mask-residues 1) ----------
+constexpr int kTantanOffsets = 50;  // tantan's maxCycleLength (SeqIterator.cpp:163)
+struct TantanTables {
+    double lr[25];               // likelihood ratios of letter codes (A C G T N) a, b: lr[5 a + b]
+    double b2f[kTantanOffsets];  // background -> repeat offset i + 1
+    double b2b, f2b, f2f;        // background stays, repeat ends, repeat continues
+    double minMask;              // maskProb (minMaskProb) as the comparison uses it
+};
+TantanTables make_tantan_tables(float maskProb);  // mtb_host.cpp
+uint64_t tantan_scale_elems(uint64_t bases, uint32_t n);
+// masked copy of a batch's mate: out[b] = 'N' where tantan's repeat probability >= maskProb or the
+// letter is not A/C/G/T/U, else seq[b]; prob: 4 B per base, scale: tantan_scale_elems doubles
+void launch_tantan_mask(const uint8_t* seq, const uint64_t* off, uint32_t n, const TantanTables& tt, float* prob,
+                        double* scale, uint8_t* out, hipStream_t s);
+
 }  // namespace mtb

@@ -156,6 +156,25 @@ int orc_extract(const mtb_params* par, const char* seq1, const uint64_t* off1, c
     return MTB_OK;
 }
 
+// SeqIterator::maskLowComplexityRegions over a batch of reads (test entry point): masked bases and,
+// if probs is non-NULL, tantan's per-letter repeat probabilities.
+void orc_tantan(const char* seq, const uint64_t* off, uint32_t n, float mask_prob, char* out, float* probs) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        const int len = (int)(off[i + 1] - off[i]);
+        maskLowComplexityRegions(seq + off[i], len, mask_prob, out + off[i]);
+        if (probs) {
+            std::vector<unsigned char> x(len);
+            for (int k = 0; k < len; k++) {
+                const char c = seq[off[i] + k];
+                x[k] = (c == 'A' || c == 'a') ? 0 : (c == 'C' || c == 'c') ? 1 : (c == 'G' || c == 'g') ? 2
+                     : (c == 'T' || c == 't' || c == 'U' || c == 'u') ? 3 : 4;
+            }
+            tantanRepeatProbs(x.data(), len, probs + off[i]);
+        }
+    }
+}
+
 int orc_match(void* dbp, const mtb_params* par, const mtb_kmer* kmers, uint64_t n, mtb_match* out, uint64_t cap,
               uint64_t* n_out, char* err, int errlen) {
     std::vector<mtb_match> m;

@@ -73,15 +73,28 @@ void extractQueryKmers(const mtb_params& par, const Reads& reads, std::vector<mt
 #pragma omp parallel
     {
         std::unique_ptr<Scanner> sc = makeScanner(par);
+        std::vector<char> m1, m2;  // masked copies (processSequence, KmerExtractor.cpp:328-335)
 #pragma omp for schedule(dynamic, 256)
         for (int64_t i = 0; i < (int64_t)reads.n; i++) {
             if (empty[i]) continue;  // processSequence (KmerExtractor.cpp:324)
             const Query& q = queries[i];
             mtb_kmer* out = buf.data() + reserveOff[i];
             const char* s1 = reads.seq1 + reads.off1[i];
-            fillQueryKmerBuffer(*sc, s1, (int)(reads.off1[i + 1] - reads.off1[i]), out, (uint32_t)i + 1, 0);
+            const int l1 = (int)(reads.off1[i + 1] - reads.off1[i]);
+            if (par.mask_mode) {
+                m1.resize(l1 + 1);
+                maskLowComplexityRegions(s1, l1, par.mask_prob, m1.data());
+                s1 = m1.data();
+            }
+            fillQueryKmerBuffer(*sc, s1, l1, out, (uint32_t)i + 1, 0);
             if (paired) {
                 const char* s2 = reads.seq2 + reads.off2[i];
+                if (par.mask_mode) {
+                    const int l2 = (int)(reads.off2[i + 1] - reads.off2[i]);
+                    m2.resize(l2 + 1);
+                    maskLowComplexityRegions(s2, l2, par.mask_prob, m2.data());
+                    s2 = m2.data();
+                }
                 fillQueryKmerBuffer(*sc, s2, (int)(reads.off2[i + 1] - reads.off2[i]), out + q.kmerCnt,
                                     (uint32_t)i + 1, (uint32_t)q.queryLength + 3);
             }

@@ -53,6 +53,11 @@ struct Reads {
 void extractQueryKmers(const mtb_params& par, const Reads& reads, std::vector<mtb_kmer>& buf,
                        std::vector<Query>& queries, bool sort);
 
+// SeqIterator::maskLowComplexityRegions (SeqIterator.cpp:154-175) of one read (orc_mask.cpp), and
+// tantan's per-letter repeat probabilities of a coded sequence.
+void maskLowComplexityRegions(const char* seq, int n, float maskProb, char* out);
+void tantanRepeatProbs(const unsigned char* x, int n, float* prob);
+
 // KmerMatcher::matchKmers (KmerMatcher.cpp:123-481) over in-memory files.
 bool matchKmers(const Db& db, const mtb_params& par, const mtb_kmer* kmers, size_t nKmers,
                 std::vector<mtb_match>& matches, std::string* err);

@@ -50,8 +50,21 @@ def lib():
         L.orc_write_report.restype = i32
         L.orc_last_em_maps.argtypes = [vp, u64, ctypes.POINTER(u64)]
         L.orc_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]
+        L.orc_tantan.argtypes = [vp, vp, u32, ctypes.c_float, vp, vp]
+        L.orc_tantan.restype = None
         _LIB = L
     return _LIB
+
+
+def tantan(seq: np.ndarray, off: np.ndarray, mask_prob: float = 0.9):
+    """SeqIterator::maskLowComplexityRegions of every read (the oracle's tantan restatement): the
+    masked bases and tantan's per-letter repeat probabilities."""
+    seq = np.ascontiguousarray(seq, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    out = np.zeros(len(seq), np.uint8)
+    probs = np.zeros(len(seq), np.float32)
+    lib().orc_tantan(ptr(seq), ptr(off), len(off) - 1, float(mask_prob), ptr(out), ptr(probs))
+    return out, probs
 
 
 def load_db_parameters(db_dir: str, par: MtbParams) -> MtbParams:

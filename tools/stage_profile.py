@@ -38,6 +38,8 @@ def stage_of(seq):
             continue
         if k.startswith("k_read_meta"):
             stage, after_extract = "extract", False
+        elif k.startswith("k_extract_filter"):  # the fused K1 + K1F: bench.py times it as the filter
+            stage, after_extract = "filter", True
         elif k.startswith("k_extract"):
             stage, after_extract = "extract", True
         elif k.startswith("k_filter"):
