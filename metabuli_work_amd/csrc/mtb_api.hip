@@ -463,16 +463,19 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
-    if (c->sparse && (!prune || maxSeg > kSegSortRegs || c->segsortGlobal)) {  // K5 reads sparse segments only
+    if (c->sparse && (!prune || maxSeg > kSegSortSparse || c->segsortGlobal ||
+                      (c->mergeSeg && maxSeg > c->mergeSeg))) {  // K5 reads sparse segments up to kSegSortSparse
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), c->chunkC,
-                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), 0, s);  // sparse: no spills
+                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->spillShift, s);
+        // (the spilled ranks of the reads that overflowed their stretch are in place already)
         c->sparse = false;
     }
     HIP_TRY(launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
                            c->segScratch.as<uint64_t>(), maxSeg, c->forceGeneric || c->segsortGlobal,
                            prune ? c->liveCnt.as<uint32_t>() : nullptr, c->mergeSeg,
                            prune_min_matches(a.minConsCnt, a.minConsCntEuk, a.maxCodonShift), s,
-                           c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(), c->chunkC,
+                           c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
+                           c->chunkC | c->spillShift << 16,
                            compact ? c->segLen.as<uint32_t>() : nullptr,
                            c->maxSeg.as<uint32_t>(), c->pruneAfter));
     c->sparse = false;
@@ -755,10 +758,15 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->matches.ensure(sizeof(mtb_match) * std::max<uint64_t>(M, 1)));
     HIP_TRY(hipEventRecord(c->kev[8], s));
     // a batch that goes on to K5 with pruning reads the direct join's segments in place (the
-    // register sorts, segments of <= kSegSortRegs matches); otherwise they are compacted here
+    // register and mid sorts, segments of <= kSegSortSparse matches); otherwise they are compacted here
     c->stats[13] = nSpill;
-    c->sparse = direct && nSpill == 0 && !c->keepStages && !c->forceGeneric && !c->matchOnly;
-    if (direct && !c->sparse) {
+    c->sparse = direct && !c->keepStages && !c->forceGeneric && !c->matchOnly;
+    if (c->sparse && nSpill) {  // only the reads that overflowed their stretch: compacted + their spills
+        launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
+                                c->matches.as<mtb_match>(), c->spillShift, s, true);
+        launch_spill_scatter(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->mTotal.as<unsigned long long>(),
+                             nSpill, c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
+    } else if (direct && !c->sparse) {
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
                                 c->matches.as<mtb_match>(), c->spillShift, s);
         launch_spill_scatter(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->mTotal.as<unsigned long long>(),

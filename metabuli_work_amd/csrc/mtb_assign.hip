@@ -111,6 +111,21 @@ struct SegIn {
     __device__ __forceinline__ mtb_match full(uint32_t e) const { return seg_expand(p[base + e], seqBits); }
 };
 
+// The direct join's sparse input (seg: 16-B records in per-read slot stretches, read r's at
+// seg + inOff[r] * C): inCS = C | capShift << 16. A read whose matches passed its stretch (some were
+// spilled: n > the stretch) was compacted into the match array at mOff[r] with its spills, so K5 reads
+// it from there; every other read is read in place.
+__device__ __forceinline__ bool sparse_read(const SegMatch* seg, const uint64_t* __restrict__ inOff, uint32_t inCS,
+                                            uint32_t r, long n) {
+    if (!seg) return false;
+    const uint64_t cap = ((inOff[r + 1] - inOff[r]) * (inCS & 0xFFFFu)) >> (inCS >> 16);
+    return (uint64_t)n <= cap;
+}
+__device__ __forceinline__ SegIn sparse_in(const SegMatch* seg, const uint64_t* __restrict__ inOff, uint32_t inCS,
+                                           uint32_t r) {
+    return SegIn{seg, inOff[r] * (inCS & 0xFFFFu), (uint64_t)(r + 1) << 32};
+}
+
 // Open-addressing insert into a wave's LDS table of tn (power of two) slots, key 0 = empty; returns
 // the key's slot.
 template <typename K>
@@ -630,7 +645,7 @@ __global__ void __launch_bounds__(64) k_segsort_small(const mtb_match* __restric
     const long nl = seg_len(mOff, segLen, r);
     if (nl < 0 || nl > 128) return;
     const int n = (int)nl;
-    if (seg) segsort_small_run(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n, threadIdx.x, liveCnt, r, pm);
+    if (sparse_read(seg, inOff, inC, r, n)) segsort_small_run(sparse_in(seg, inOff, inC, r), out, base, n, threadIdx.x, liveCnt, r, pm);
     else segsort_small_run(MatchIn{in, base}, out, base, n, threadIdx.x, liveCnt, r, pm);
 }
 
@@ -649,8 +664,8 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
     const long nl = seg_len(mOff, segLen, r);
     if (nl <= 32 * E || nl > 64 * E) return;
     const int n = (int)nl;
-    if (seg)
-        segsort_regs<E, SegIn, kMode>(SegIn{seg, inOff[r] * inC, (uint64_t)(r + 1) << 32}, out, base, n,
+    if (sparse_read(seg, inOff, inC, r, n))
+        segsort_regs<E, SegIn, kMode>(sparse_in(seg, inOff, inC, r), out, base, n,
                                        (int)threadIdx.x, liveCnt, r, pm);
     else
         segsort_regs<E, MatchIn, kMode>(MatchIn{in, base}, out, base, n, (int)threadIdx.x, liveCnt, r, pm);
@@ -714,9 +729,9 @@ __device__ uint32_t block_scan_u32(uint32_t x, uint32_t* total, uint32_t* sWave)
 // takes a contiguous chunk: species-run ids by a block scan of run starts, a flag per run that has
 // a (species, frame) pair, then the live elements written in order. rid: n words, runLive: n bytes
 // of scratch. Returns the live count.
-template <int kThreads, typename Idx>
+template <int kThreads, typename Idx, typename In>
 __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* rid, uint8_t* runLive, long n,
-                                     const mtb_match* __restrict__ in, mtb_match* __restrict__ out, uint64_t base,
+                                     const In& in, mtb_match* __restrict__ out, uint64_t base,
                                      uint32_t* sWave, uint32_t pm) {
     const long per = (n + kThreads - 1) / kThreads;
     const long b = (long)threadIdx.x * per, e = min(n, b + per);
@@ -740,7 +755,7 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
     uint32_t kept;
     uint32_t at = block_scan_u32<kThreads>(mine, &kept, sWave);
     for (long i = b; i < e; i++)
-        if (runLive[rid[i]]) out[base + at++] = in[base + I[i]];
+        if (runLive[rid[i]]) out[base + at++] = in.full((uint32_t)I[i]);
     return kept;
 }
 
@@ -750,8 +765,8 @@ __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* 
 // exact pruning after the sort still drops it), never drop a live one. The tables (T u32 each)
 // live in the LDS the sort uses afterwards; each thread keeps its <= 8 elements' keys in registers,
 // and the live ones are then written compacted into H / L / I. Returns the live count.
-template <int kThreads, int kPer, typename Idx>
-__device__ long preprune_load(const mtb_match* __restrict__ in, uint64_t base, long n, uint32_t* cnt, uint32_t* flag,
+template <int kThreads, int kPer, typename Idx, typename In>
+__device__ long preprune_load(const In& in, long n, uint32_t* cnt, uint32_t* flag,
                               uint32_t logT, uint64_t* H, uint64_t* L, Idx* I, uint32_t* sWave, uint32_t pm) {
     const uint32_t T = 1u << logT;
     for (uint32_t i = threadIdx.x; i < T; i += kThreads) {
@@ -766,7 +781,7 @@ __device__ long preprune_load(const mtb_match* __restrict__ in, uint64_t base, l
         h[k] = l[k] = 0;
         hp[k] = hs[k] = 0;
         if (b + k < n) {
-            match_key(in[base + b + k], h[k], l[k]);
+            match_key(in.full((uint32_t)(b + k)), h[k], l[k]);
             hp[k] = (uint32_t)(((h[k] >> 29) * 0x9E3779B97F4A7C15ull) >> (64 - logT));
             hs[k] = (uint32_t)(((h[k] >> 32) * 0xC2B2AE3D27D4EB4Full) >> (64 - logT));
         }
@@ -806,24 +821,24 @@ constexpr int kLargeThreads = 1024;
 // blocks share a CU (the 8192-entry kernel holds 147 KB of LDS: one block per CU).
 constexpr int kMidSeg = 2048;
 constexpr int kMidThreads = 256;
-__global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
-                                                             const uint64_t* __restrict__ mOff, uint32_t nReads,
-                                                             mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
-                                                             long mergeSeg, uint32_t pm,
-                                                             const uint32_t* __restrict__ segLen) {
-    __shared__ uint64_t sh[kMidSeg], sl[kMidSeg];
-    __shared__ uint16_t si[kMidSeg];
-    __shared__ uint32_t sWave[kMidThreads / 64 + 1];
-    const uint32_t r = blockIdx.x;
-    if (r >= nReads) return;
-    const uint64_t base = mOff[r];
-    long n = seg_len(mOff, segLen, r);
-    if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
+static_assert(kMidSeg == (int)kSegSortSparse, "the sparse-input bound of launch_segsort");
+
+struct MidLds {
+    uint64_t sh[kMidSeg], sl[kMidSeg];
+    uint16_t si[kMidSeg];
+    uint32_t sWave[kMidThreads / 64 + 1];
+};
+
+template <typename In>
+__device__ __forceinline__ void segsort_mid_run(const In& in, MidLds& L, mtb_match* __restrict__ out, uint64_t base,
+                                                long n, uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
+    uint64_t *sh = L.sh, *sl = L.sl;
+    uint16_t* si = L.si;
     long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
     if (liveCnt) {
         static_assert(kMidSeg / kMidThreads == 8 && 2 * kMidSeg == 4096, "pre-prune geometry");
-        m = preprune_load<kMidThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
-                                                    reinterpret_cast<uint32_t*>(sl), 12, sh, sl, si, sWave, pm);
+        m = preprune_load<kMidThreads, 8, uint16_t>(in, n, reinterpret_cast<uint32_t*>(sh),
+                                                    reinterpret_cast<uint32_t*>(sl), 12, sh, sl, si, L.sWave, pm);
         if (m == 0) {
             if (threadIdx.x == 0) liveCnt[r] = 0;
             return;
@@ -834,7 +849,7 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
     for (long i = threadIdx.x; i < p2; i += kMidThreads) {
         if (liveCnt && i < m) continue;  // loaded by the pre-prune
         uint64_t h = ~0ull, l = ~0ull;
-        if (i < m) match_key(in[base + i], h, l);
+        if (i < m) match_key(in.full((uint32_t)i), h, l);
         sh[i] = h; sl[i] = l; si[i] = (uint16_t)i;
     }
     __syncthreads();
@@ -843,11 +858,30 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
         n = m;
         uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
         const uint32_t kept = prune_pack_block<kMidThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n), n,
-                                                                      in, out, base, sWave, pm);
+                                                                      in, out, base, L.sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
-    for (long i = threadIdx.x; i < n; i += kMidThreads) out[base + i] = in[base + si[i]];
+    for (long i = threadIdx.x; i < n; i += kMidThreads) out[base + i] = in.full(si[i]);
+}
+
+// seg (nullable): the direct join's sparse per-read stretches (seg + inOff[r] * inC), as
+// k_segsort_small reads them, so that batches of <= kMidSeg matches per read need no compaction.
+__global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
+                                                             const uint64_t* __restrict__ mOff, uint32_t nReads,
+                                                             mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
+                                                             long mergeSeg, uint32_t pm,
+                                                             const uint32_t* __restrict__ segLen,
+                                                             const SegMatch* __restrict__ seg,
+                                                             const uint64_t* __restrict__ inOff, uint32_t inC) {
+    __shared__ MidLds L;
+    const uint32_t r = blockIdx.x;
+    if (r >= nReads) return;
+    const uint64_t base = mOff[r];
+    const long n = seg_len(mOff, segLen, r);
+    if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
+    if (sparse_read(seg, inOff, inC, r, n)) segsort_mid_run(sparse_in(seg, inOff, inC, r), L, out, base, n, liveCnt, r, pm);
+    else segsort_mid_run(MatchIn{in, base}, L, out, base, n, liveCnt, r, pm);
 }
 
 __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match* __restrict__ in,
@@ -873,7 +907,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
         long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
         if (liveCnt) {
             static_assert(kBlockSeg / kLargeThreads == 8 && 2 * kBlockSeg == 16384, "pre-prune geometry");
-            m = preprune_load<kLargeThreads, 8, uint16_t>(in, base, n, reinterpret_cast<uint32_t*>(sh),
+            m = preprune_load<kLargeThreads, 8, uint16_t>(MatchIn{in, base}, n, reinterpret_cast<uint32_t*>(sh),
                                                           reinterpret_cast<uint32_t*>(sl), 14, sh, sl, si, sWave, pm);
             if (m == 0) {
                 if (threadIdx.x == 0) liveCnt[r] = 0;
@@ -894,7 +928,7 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
         if (liveCnt) {  // the lo keys are no longer needed: their LDS holds the run ids and flags
             uint32_t* rid = reinterpret_cast<uint32_t*>(sl);
             const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t>(sh, si, rid, reinterpret_cast<uint8_t*>(rid + n),
-                                                                            n, in, out, base, sWave, pm);
+                                                                            n, MatchIn{in, base}, out, base, sWave, pm);
             if (threadIdx.x == 0) liveCnt[r] = kept;
             return;
         }
@@ -915,7 +949,8 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     if (liveCnt) {  // run ids and flags in the lo-key scratch (2 * p2 words, p2 >= n)
         uint32_t* rid = reinterpret_cast<uint32_t*>(Lo);
         const uint32_t kept =
-            prune_pack_block<kLargeThreads, uint32_t>(H, I, rid, reinterpret_cast<uint8_t*>(rid + n), n, in, out, base, sWave, pm);
+            prune_pack_block<kLargeThreads, uint32_t>(H, I, rid, reinterpret_cast<uint8_t*>(rid + n), n, MatchIn{in, base},
+                                                      out, base, sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
@@ -1032,8 +1067,8 @@ __global__ void __launch_bounds__(kLargeThreads) k_merge_finish(const mtb_match*
     if (liveCnt) {
         uint32_t* rid = reinterpret_cast<uint32_t*>(T.l + base);
         const uint32_t kept = prune_pack_block<kLargeThreads, uint32_t>(S.h + base, S.x + base, rid,
-                                                                        reinterpret_cast<uint8_t*>(rid + n), n, in,
-                                                                        out, base, sWave, pm);
+                                                                        reinterpret_cast<uint8_t*>(rid + n), n,
+                                                                        MatchIn{in, base}, out, base, sWave, pm);
         if (threadIdx.x == 0) liveCnt[r] = kept;
         return;
     }
@@ -1206,7 +1241,7 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
     }
 #undef MTB_REGS
     if (maxSeg > kSmallSeg)
-        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen);
+        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
                                                          segLen);
@@ -1221,7 +1256,8 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
                           uint32_t* segLen, uint32_t* maxTmp, int after) {
     pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
-    if (seg && (global || maxSeg > kSmallSeg)) return hipErrorInvalidValue;  // sparse input: register sorts only
+    // sparse input: the register sorts and the mid sort (segments of <= kSegSortSparse, no thinning)
+    if (seg && (global || maxSeg > kSegSortSparse)) return hipErrorInvalidValue;
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm,
@@ -1385,7 +1421,28 @@ __device__ __forceinline__ bool consecutive(uint32_t dc, uint32_t dn, uint32_t s
 constexpr int kRegPos = 4;
 constexpr uint64_t kBigGroup = 256;  // groups of at least this many matches: k_match_paths_wave
 
-__device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M, uint64_t start, uint64_t end,
+// The fields getMatchPaths reads of match k: from the match array, or from a wave's LDS copy of
+// its groups' span (k_match_paths: one coalesced load of the span instead of per-lane record loads).
+struct GlobalRecs {
+    const mtb_match* __restrict__ M;
+    __device__ __forceinline__ uint32_t pos(uint64_t k) const { return info_pos(M[k].qinfo); }
+    __device__ __forceinline__ uint32_t dna(uint64_t k) const { return M[k].dna_encoding; }
+    __device__ __forceinline__ uint32_t reh(uint64_t k) const { return M[k].right_end_hamming; }
+    __device__ __forceinline__ uint32_t ham(uint64_t k) const { return M[k].hamming; }
+};
+struct LdsRecs {
+    const uint32_t* p;   // pos
+    const uint32_t* dh;  // dna | hamming << 24
+    const uint16_t* rh;  // rightEndHamming
+    uint64_t base;       // match index of entry 0
+    __device__ __forceinline__ uint32_t pos(uint64_t k) const { return p[k - base]; }
+    __device__ __forceinline__ uint32_t dna(uint64_t k) const { return dh[k - base] & 0xFFFFFFu; }
+    __device__ __forceinline__ uint32_t reh(uint64_t k) const { return rh[k - base]; }
+    __device__ __forceinline__ uint32_t ham(uint64_t k) const { return dh[k - base] >> 24; }
+};
+
+template <typename R>
+__device__ __forceinline__ bool match_paths_regs(const R& M, uint64_t start, uint64_t end,
                                                  const AssignCfg& cfg, int minDepth, bool fwd,
                                                  Path* __restrict__ P, uint64_t& nPout) {
     Path cp[kRegPos], np[kRegPos];
@@ -1394,45 +1451,45 @@ __device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M
     int nc = 0, nn = 0;
     uint64_t nP = start;
     uint64_t k = start;
-    uint32_t currPos = info_pos(M[k].qinfo);
+    uint32_t currPos = M.pos(k);
     // first position group
     while (k < end) {
-        const mtb_match m = M[k];
-        if (info_pos(m.qinfo) != currPos) break;
+        if (M.pos(k) != currPos) break;
         if (nc == kRegPos) return false;
+        const uint32_t mreh = M.reh(k), mham = M.ham(k), mdna = M.dna(k);
 #pragma unroll
         for (int x = 0; x < kRegPos; x++)
             if (x == nc) {
                 cp[x].start = (int)currPos;
                 cp[x].end = (int)currPos + 23;
-                cp[x].score = score_fields(m.right_end_hamming, 8, false);
-                cp[x].hd = m.hamming;
+                cp[x].score = score_fields(mreh, 8, false);
+                cp[x].hd = (int)mham;
                 cp[x].depth = 1;
                 cp[x].sm = cp[x].em = (uint32_t)k;
-                cd[x] = m.dna_encoding;
+                cd[x] = mdna;
                 cc[x] = false;
             }
         nc++;
         k++;
     }
     while (k < end) {
-        const uint32_t nextPos = info_pos(M[k].qinfo);
+        const uint32_t nextPos = M.pos(k);
         nn = 0;
         while (k < end) {
-            const mtb_match m = M[k];
-            if (info_pos(m.qinfo) != nextPos) break;
+            if (M.pos(k) != nextPos) break;
             if (nn == kRegPos) return false;
+            const uint32_t mreh = M.reh(k), mham = M.ham(k), mdna = M.dna(k);
 #pragma unroll
             for (int x = 0; x < kRegPos; x++)
                 if (x == nn) {
                     np[x].start = (int)nextPos;
                     np[x].end = (int)nextPos + 23;
-                    np[x].score = score_fields(m.right_end_hamming, 8, false);
-                    np[x].hd = m.hamming;
+                    np[x].score = score_fields(mreh, 8, false);
+                    np[x].hd = (int)mham;
                     np[x].depth = 1;
                     np[x].sm = np[x].em = (uint32_t)k;
-                    nd[x] = m.dna_encoding;
-                    nr[x] = m.right_end_hamming;
+                    nd[x] = mdna;
+                    nr[x] = mreh;
                 }
             nn++;
             k++;
@@ -1497,31 +1554,32 @@ __device__ __forceinline__ bool match_paths_regs(const mtb_match* __restrict__ M
 // order; returns the end of the emitted paths. emitLone: [start, end) is a stretch of a larger group
 // that ends at a break (the next position is not within maxCodonShift codons): a stretch of a
 // single position group emits its paths too, as the whole group's loop would when it moves past it.
-__device__ uint64_t match_paths_serial(const mtb_match* __restrict__ M, uint64_t start, uint64_t end,
+template <typename R>
+__device__ uint64_t match_paths_serial(const R& M, uint64_t start, uint64_t end,
                                        const AssignCfg& cfg, int minDepth, bool fwd, Path* __restrict__ L,
                                        Path* __restrict__ P, uint8_t* __restrict__ conn, bool emitLone) {
     for (uint64_t x = start; x < end; x++) conn[x] = 0;
     uint64_t nP = start;
     uint64_t k = start;
-    uint64_t currPos = info_pos(M[start].qinfo);
+    uint64_t currPos = M.pos(start);
     bool stepped = false;  // a next position group was processed
     auto initPath = [&](uint64_t idx) {
         Path p;
-        p.start = (int)info_pos(M[idx].qinfo);
+        p.start = (int)M.pos(idx);
         p.end = p.start + 23;
-        p.score = score_fields(M[idx].right_end_hamming, 8, false);
-        p.hd = M[idx].hamming;
+        p.score = score_fields(M.reh(idx), 8, false);
+        p.hd = (int)M.ham(idx);
         p.depth = 1;
         p.sm = p.em = (uint32_t)idx;
         L[idx] = p;
     };
     uint64_t curS = k;
-    while (k < end && info_pos(M[k].qinfo) == currPos) { initPath(k); ++k; }
+    while (k < end && M.pos(k) == currPos) { initPath(k); ++k; }
     uint64_t curE = k;
     while (k < end) {
-        const uint32_t nextPos = info_pos(M[k].qinfo);
+        const uint32_t nextPos = M.pos(k);
         const uint64_t nxS = k;
-        while (k < end && info_pos(M[k].qinfo) == nextPos) { initPath(k); ++k; }
+        while (k < end && M.pos(k) == nextPos) { initPath(k); ++k; }
         const uint64_t nxE = k;
         stepped = true;
         const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
@@ -1529,7 +1587,7 @@ __device__ uint64_t match_paths_serial(const mtb_match* __restrict__ M, uint64_t
             const uint32_t sh = 3u * (uint32_t)shift;
             const uint32_t lowMask = (1u << (24u - sh)) - 1u;
             for (uint64_t nx = nxS; nx < nxE; nx++) {
-                const uint32_t nreh = M[nx].right_end_hamming;
+                const uint32_t nreh = M.reh(nx);
                 float inc = 0.0f;
                 int hinc = 0;
                 for (int c = 0; c < shift; c++) {
@@ -1539,9 +1597,9 @@ __device__ uint64_t match_paths_serial(const mtb_match* __restrict__ M, uint64_t
                 }
                 int64_t best = -1;
                 float bestScore = 0.0f;
-                const uint32_t dn = M[nx].dna_encoding;
+                const uint32_t dn = M.dna(nx);
                 for (uint64_t cu = curS; cu < curE; cu++) {
-                    const uint32_t dc = M[cu].dna_encoding;
+                    const uint32_t dc = M.dna(cu);
                     bool cons;
                     if (cfg.kmerFormat == 2) {  // isConsecutive2 (Taxonomer.cpp:692-699)
                         cons = fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
@@ -1581,19 +1639,11 @@ __device__ uint64_t match_paths_serial(const mtb_match* __restrict__ M, uint64_t
 
 // getMatchPaths (Taxonomer.cpp:487-648) on one (read, species, frame) group [gs, ge). Paths go to
 // P[gs + k] in emission order; L and conn are indexed by match.
-__global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
-                                                     const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
-                                                     TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
-                                                     uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt,
-                                                     uint64_t* __restrict__ bigList, uint32_t* __restrict__ bigCount) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nWork) return;
-    const uint64_t g = (uint32_t)order[i];
-    const uint64_t start = gStart[g], end = gStart[g + 1];
-    if (bigList && end - start >= kBigGroup) {  // k_match_paths_wave takes it
-        bigList[atomicAdd(bigCount, 1u)] = g;
-        return;
-    }
+template <typename R>
+__device__ __forceinline__ void match_paths_group(const R& recs, const mtb_match* __restrict__ M, uint64_t g,
+                                                  uint64_t start, uint64_t end, const AssignCfg& cfg,
+                                                  const TaxView& tax, Path* __restrict__ L, Path* __restrict__ P,
+                                                  uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt) {
     const int32_t sp = (int32_t)M[start].species_id;
     const uint32_t curFrame = info_frame(M[start].qinfo);
     int minDepth = cfg.minConsCnt;
@@ -1601,13 +1651,53 @@ __global__ void __launch_bounds__(256) k_match_paths(const mtb_match* __restrict
     const bool fwd = curFrame < 3;
     {
         uint64_t nPr = start;
-        if (!cfg.generic && match_paths_regs(M, start, end, cfg, minDepth, fwd, P, nPr)) {
+        if (!cfg.generic && match_paths_regs(recs, start, end, cfg, minDepth, fwd, P, nPr)) {
             pathCnt[g] = (uint32_t)(nPr - start);
             return;
         }
     }
-    const uint64_t nP = match_paths_serial(M, start, end, cfg, minDepth, fwd, L, P, conn, false);
+    const uint64_t nP = match_paths_serial(recs, start, end, cfg, minDepth, fwd, L, P, conn, false);
     pathCnt[g] = (uint32_t)(nP - start);
+}
+
+// A wave per 64 work items (groups in batch order, so their matches form one stretch of the array):
+// the stretch's pos / dna / hamming / rightEndHamming are staged in LDS with coalesced loads (the
+// groups' own loads would be 64 scattered lines per instruction), unless it is longer than
+// kPathStage matches.
+constexpr int kPathStage = 1024;
+
+__global__ void __launch_bounds__(64) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
+                                                    const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
+                                                    TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
+                                                    uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt,
+                                                    uint64_t* __restrict__ bigList, uint32_t* __restrict__ bigCount) {
+    __shared__ uint32_t sPos[kPathStage], sDh[kPathStage];
+    __shared__ uint16_t sReh[kPathStage];
+    const uint64_t w0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t i = w0 + threadIdx.x;
+    const uint64_t wLast = min(w0 + 63, nWork - 1);
+    const uint64_t spanLo = gStart[(uint32_t)order[w0]], spanHi = gStart[(uint32_t)order[wLast] + 1];
+    const bool staged = spanHi - spanLo <= (uint64_t)kPathStage;
+    if (staged) {
+        for (uint64_t k = spanLo + threadIdx.x; k < spanHi; k += 64) {
+            const mtb_match m = M[k];
+            sPos[k - spanLo] = info_pos(m.qinfo);
+            sDh[k - spanLo] = (m.dna_encoding & 0xFFFFFFu) | ((uint32_t)m.hamming << 24);
+            sReh[k - spanLo] = m.right_end_hamming;
+        }
+        __syncthreads();
+    }
+    if (i >= nWork) return;
+    const uint64_t g = (uint32_t)order[i];
+    const uint64_t start = gStart[g], end = gStart[g + 1];
+    if (bigList && end - start >= kBigGroup) {  // k_match_paths_wave takes it
+        bigList[atomicAdd(bigCount, 1u)] = g;
+        return;
+    }
+    if (staged)
+        match_paths_group(LdsRecs{sPos, sDh, sReh, spanLo}, M, g, start, end, cfg, tax, L, P, conn, pathCnt);
+    else
+        match_paths_group(GlobalRecs{M}, M, g, start, end, cfg, tax, L, P, conn, pathCnt);
 }
 
 // A group of >= kBigGroup matches (long reads) with a wave: each lane takes a stretch of ~n/64
@@ -1644,7 +1734,7 @@ __global__ void __launch_bounds__(64) k_match_paths_wave(const mtb_match* __rest
     if (lane == 63) b = end;
     if (b < a) b = a;
     uint64_t cnt = 0;
-    if (a < b) cnt = match_paths_serial(M, a, b, cfg, minDepth, fwd, L, P, conn, multi) - a;
+    if (a < b) cnt = match_paths_serial(GlobalRecs{M}, a, b, cfg, minDepth, fwd, L, P, conn, multi) - a;
     // exclusive scan of the counts over the lanes
     uint64_t inc = cnt;
 #pragma unroll
@@ -2419,7 +2509,7 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                 // groups of >= kBigGroup matches queue for a wave each (long reads' serial tail)
                 const bool waves = !a.generic && a.bigGroups && nM >= kBigGroup;
                 if (waves) hipMemsetAsync(s.waveCount, 0, sizeof(uint32_t), st);
-                k_match_paths<<<(unsigned)((heavy + 255) / 256), 256, 0, st>>>(
+                k_match_paths<<<(unsigned)((heavy + 63) / 64), 64, 0, st>>>(
                     matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
                     s.conn, s.pathCnt, waves ? s.waveList : nullptr, s.waveCount);
                 if (waves) {

@@ -224,7 +224,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 // `region`, else *overflow is set and the caller reruns with a larger spill buffer or staged).
 // capShift (tests): stretches are taken as their size >> capShift, so that queries spill.
 void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
-                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s);
+                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s, bool onlyOver = false);
 // the spilled matches to readOff[r] + rank (after launch_compact_segments)
 void launch_spill_scatter(const mtb_match* spill, const uint32_t* spillRank, const unsigned long long* total,
                           uint64_t nSpill, const uint64_t* readOff, uint32_t nReads, mtb_match* out, int* err,
@@ -263,7 +263,8 @@ uint64_t clade_bytes();
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
                           uint32_t pruneMin, hipStream_t s, const SegMatch* seg = nullptr,
-                          const uint64_t* inOff = nullptr, uint32_t inC = 0, uint32_t* segLen = nullptr,
+                          const uint64_t* inOff = nullptr, uint32_t inC = 0 /* C | capShift << 16 */,
+                          uint32_t* segLen = nullptr,
                           uint32_t* maxTmp = nullptr, int pruneAfter = 0);
 // The fewest matches a (species, frame) group needs for getMatchPaths to emit a path: a path of
 // depth d chains >= 1 + ceil((d - 1) / maxCodonShift) matches (each link adds a shift of at most
@@ -284,6 +285,7 @@ void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s)
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s);
 constexpr uint32_t kSegSortLds = 8192;
 constexpr uint32_t kSegSortRegs = 512;  // segments up to this many matches sort in registers (sparse input allowed)
+constexpr uint32_t kSegSortSparse = 2048;  // K5 reads the direct join's sparse segments up to this many matches
 // K6 indexes matches and groups with 32 bits
 constexpr uint64_t kMaxBatchMatches = 0xFFFFFFFFull;  // segments up to this many matches sort in LDS
 void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_t* qlen, uint32_t nReads, uint64_t nM, const AssignArgs& a, const TaxDevice& t, const AssignScratch& s,
