@@ -237,7 +237,7 @@ def main():
     ap.add_argument("--gtdb-true-species", type=int, default=1000)
     ap.add_argument("--gtdb-genome", type=int, default=3_000_000)
     ap.add_argument("--gtdb-cpu-sample", type=int, default=1_000_000, help="config 3: read pairs timed on the oracle")
-    ap.add_argument("--variants", default="syncmer,related",
+    ap.add_argument("--variants", default="syncmer,related,conserved",
                     help="extra config-3 lines, comma-separated (GTDB_VARIANTS; empty = none)")
     ap.add_argument("--variant-cpu-sample", type=int, default=200_000,
                     help="read pairs of each variant line timed on the oracle (parity sample)")
@@ -548,6 +548,10 @@ GTDB_VARIANTS = {  # extra config-3 lines: the DB format us
                 "what": "true-signal species in genera of 20 sister species, each 5% diverged from its genus "
                         "genome (~10% between sisters, GTDB's 5-15% within a genus): DB AA runs carry several "
                         "species"},
+    "conserved": {"syncmer": 0, "smer_len": 5, "per_genus": 1, "species_div": 0.0, "conserved": 1_000_000,
+                  "what": "heavy-tailed sharing: 1M AA 8-mers of the true-signal genomes are also held by 100 to "
+                          "10,000 filler species each (log-uniform), as conserved genes' AA 8-mers are across "
+                          "GTDB: DB runs of 10^2-10^4 k-mers, queries selecting among thousands of candidates"},
 }
 
 
@@ -558,7 +562,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     built in place in HBM (gtdb_synth.build_gtdb_scale) and used there (mtb_open_resident). One step
     = the rank's 10M pairs as 1M-pair QuerySplits (Classifier.cpp:81-133), plus, with N > 1, the
     all-gather of the per-read result records."""
-    from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle
+    from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle, run_length_histogram
 
     t0 = time.time()
     N, B = args.gtdb_pairs, min(args.gtdb_batch, args.gtdb_pairs)
@@ -575,7 +579,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                            total_species=args.gtdb_species, target_kmers=int(args.gtdb_kmers), seed=args.seed + 1,
                            before_free=grab, log=lambda m: log(rank, f"[bench] {m} ({time.time() - t0:.1f}s)"),
                            syncmer=vr["syncmer"], smer_len=vr["smer_len"], per_genus=vr["per_genus"],
-                           species_div=vr["species_div"])
+                           species_div=vr["species_div"], conserved=vr.get("conserved", 0))
     s1, o1, s2, o2 = got.pop("reads")
     lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1, syncmer=vr["syncmer"], smerLen=vr["smer_len"])
     clf = Classifier(lp, db_resident=rdb, device=local)
@@ -722,6 +726,8 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                "ms_per_step": out["ms_per_step"], "config": out["config"], "roofline": roofline,
                "pipeline_roofline": pipe, "random_roofline": rand_roof, "cpu_baseline": cpu, "parity_sample": parity,
                "kernel_ms": out["kernel_ms"], "work": work}
+        if rank == 0 and variant == "conserved":  # the heavy tail: DB AA runs by length
+            out["db_run_lengths"] = run_length_histogram(rdb)
     del rdb
     torch.cuda.empty_cache()
     return out

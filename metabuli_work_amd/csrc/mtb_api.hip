@@ -100,6 +100,8 @@ struct mtb_ctx {
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
     DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, mDirect, ovFlag, waveList, waveCount, devStats;
     DevBuf qFrom, probeStats;
+    DevBuf longList, longCnt;  // the direct join's long-run queries (k_match_long)
+    uint32_t longCap = 0;
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
@@ -374,7 +376,7 @@ void mtb_close(mtb_ctx* c) {
     free_db(c);
     DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
@@ -689,11 +691,18 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         launch_match_windows(qk, Q, c->db, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     uint64_t M = 0, nSpill = 0;
     std::vector<unsigned long long> regTot(kStageRegions);
+    if (direct) {  // the long-run list: grown to the largest seen
+        c->longCap = std::max<uint32_t>(c->longCap, (uint32_t)std::min<uint64_t>(std::max<uint64_t>(Q / 256, 1u << 16), 1u << 30));
+        HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
+        HIP_TRY(c->longCnt.ensure(sizeof(uint32_t)));
+    }
     for (int attempt = 0; attempt < 4; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
         int overflow = 0;
+        uint32_t longN = 0;
         if (direct) HIP_TRY(hipMemsetAsync(c->ovFlag.p, 0, sizeof(int), s));
+        if (direct) HIP_TRY(hipMemsetAsync(c->longCnt.p, 0, sizeof(uint32_t), s));
         if (probe)
             launch_probe(qk, qi, qf, Q, c->unitInfo.as<uint64_t>(), C, c->db, c->D, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
@@ -707,11 +716,30 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->matchWin.as<uint64_t>(),
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
                          direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
-                         c->ovFlag.as<int>(), c->spillShift, s);
+                         c->ovFlag.as<int>(), c->spillShift, direct ? c->longList.as<LongRun>() : nullptr,
+                         c->longCap, c->longCnt.as<uint32_t>(), s);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        if (direct) HIP_TRY(hipMemcpyAsync(&longN, c->longCnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (direct && longN > c->longCap) {  // the list outgrew its buffer: once more, larger
+            c->longCap = longN + longN / 8;
+            HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+            continue;
+        }
+        if (direct && longN) {  // the long runs, a wave each; then the spill count and flag again
+            launch_match_long(c->longList.as<LongRun>(), longN, qk, qi, c->unitInfo.as<uint64_t>(), C, c->db, c->spOf,
+                              (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
+                              c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
+                              c->spillCap, c->errFlag.as<int>(), c->mDirect.as<SegMatch>(),
+                              c->slotOff.as<uint64_t>(), c->ovFlag.as<int>(), c->spillShift,
+                              c->probeStats.as<unsigned long long>(), s);
+            HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
         if (direct) {
             nSpill = regTot[0];
             if (!overflow && !c->directRetry) break;

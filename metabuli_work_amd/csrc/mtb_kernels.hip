@@ -1081,6 +1081,89 @@ __global__ void k_match_windows(const uint64_t* __restrict__ qkey, uint64_t Q, c
     win[i] = r >= kRankEnd ? D : db_lower_bound(dbv, d, r << 24);
 }
 
+// Long AA runs (conserved AA 8-mers shared by hundreds to thousands of species): one query's run is
+// scanned by its whole wave instead of serially by its lane (a lane looping over 10^4 candidates
+// held its wave — and the block's other queries — for the whole scan). The wave takes the long
+// queries of its lanes one after another: min Hamming sum and selected count by wave reductions
+// over coalesced strides of the run, one rank reservation, and the selected candidates written at
+// ballot-prefix positions (into the read's stretch, or spilled past it like the lane path's).
+constexpr uint64_t kLongRun = 48;
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+    return v;
+}
+
+template <typename V, typename T>
+__device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, uint64_t lo, uint64_t hi, const V& vals,
+                                                  const T& infos, const uint64_t* __restrict__ unitInfo, uint32_t C,
+                                                  const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                                  uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
+                                                  mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
+                                                  uint64_t region, int* __restrict__ err, SegMatch* __restrict__ direct,
+                                                  const uint64_t* __restrict__ dirOff, int* __restrict__ overflow,
+                                                  uint32_t capShift, int lane) {
+    const HamRows hr = hamming_rows(key);
+    uint32_t mn = 255;
+    for (uint64_t t = lo + lane; t < hi; t += 64) mn = min(mn, hamming_sum_rows(hr, vals[t]));
+    const uint32_t thr = min(wave_min_u32(mn) * 2u, 7u);
+    uint32_t cnt = 0;
+    for (uint64_t t = lo + lane; t < hi; t += 64) cnt += hamming_sum_rows(hr, vals[t]) <= thr;
+    const uint32_t c = wave_sum_u32(cnt);
+    if (c == 0) return 0;
+    const uint64_t info = slot_info(slot, C, unitInfo, kmerFormat);
+    const uint32_t r = info_seq(info) - 1;
+    uint32_t rk = 0;
+    if (lane == 0) rk = atomicAdd(&readCnt[r], c);
+    rk = (uint32_t)__shfl((int)rk, 0, 64);
+    // staged join (direct == nullptr): the block's staging stretch is claimed by the caller's count;
+    // here only the direct join's long runs come (the staged path keeps them on the lane)
+    const uint64_t o = dirOff[r] * C, cap = (dirOff[r + 1] * C - o) >> capShift;
+    const bool spill = rk + c > cap;
+    uint64_t w0 = rk;
+    if (spill) {
+        unsigned long long sp = 0;
+        if (lane == 0) sp = atomicAdd(&total[0], (unsigned long long)c);
+        sp = __shfl(sp, 0, 64);
+        if (sp + c > region) {
+            if (lane == 0) atomicExch(overflow, 1);
+            return c;
+        }
+        w0 = sp;
+    }
+    const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
+    const uint64_t lt = (1ull << lane) - 1;
+    uint64_t done = 0;
+    for (uint64_t t0 = lo; t0 < hi; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        uint64_t tv = 0;
+        uint32_t hs = 255;
+        if (t < hi) {
+            tv = vals[t];
+            hs = hamming_sum_rows(hr, tv);
+        }
+        const bool sel = hs <= thr;
+        const uint64_t m = __ballot(sel);
+        if (sel) {
+            const uint64_t k = done + (uint64_t)__popcll(m & lt);
+            if (spill)
+                emit_match(key, hr, info, tv, infos[t], hs, rev, spOf, maxTax, buf, bufRank, w0 + k,
+                           rk + (uint32_t)k, err);
+            else
+                emit_match(key, hr, info, tv, infos[t], hs, rev, spOf, maxTax, direct + o, (uint32_t*)nullptr,
+                           w0 + k, 0, err);
+        }
+        done += (uint64_t)__popcll(m);
+    }
+    return c;
+}
+
 // The join in one pass. Each block selects its queries' candidates, counts them (per read with
 // atomics, per thread for the block), claims one contiguous stretch of the staging buffer with a
 // single atomic, and writes its matches there with the lanes' stretches adjacent. The buffer is
@@ -1100,7 +1183,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                const uint64_t* __restrict__ lineP, const uint16_t* __restrict__ runOff,
                                                int sortLo, unsigned long long* __restrict__ stats,
                                                SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
-                                               int* __restrict__ overflow, uint32_t capShift) {
+                                               int* __restrict__ overflow, uint32_t capShift,
+                                               LongRun* __restrict__ longList, uint32_t longCap,
+                                               uint32_t* __restrict__ longCnt) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -1231,12 +1316,18 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             rt[j][1] = r1.tax;
         }
     }
+    // long runs (direct join): scanned by the whole wave below, not by the lane
+    bool longq[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) longq[j] = longList && direct && !kStage && live[j] && hi[j] - lo[j] > kLongRun;
     uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
     HamRows hr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         hr[j] = hamming_rows(key[j]);
-        if (small[j]) {  // run_select on the two registers
+        if (longq[j]) {
+            c[j] = 0;
+        } else if (small[j]) {  // run_select on the two registers
             const uint32_t n = (uint32_t)(hi[j] - lo[j]);
             rs[j][0] = n > 0 ? hamming_sum_rows(hr[j], rv[j][0]) : 255u;
             rs[j][1] = n > 1 ? hamming_sum_rows(hr[j], rv[j][1]) : 255u;
@@ -1254,7 +1345,17 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     }
     int hit = 0;
 #pragma unroll
-    for (int j = 0; j < kPer; j++) hit += c[j] != 0;
+    for (int j = 0; j < kPer; j++) {
+        hit += c[j] != 0;
+        const uint64_t lm = __ballot(longq[j]);
+        if (lm) {  // the wave's long queries to the long-run list (one atomic per wave), for k_match_long
+            const int lane = (int)(threadIdx.x & 63);
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(longCnt, (uint32_t)__popcll(lm));
+            at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(lm & ((1ull << lane) - 1));
+            if (longq[j] && at < longCap) longList[at] = LongRun{q0 + threadIdx.x + (uint64_t)j * 256, lo[j], hi[j]};
+        }
+    }
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
     if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
     if (!kStage && lines) {  // the fallback counter sits past the stripes (rare: a lane-0 atomic per wave)
@@ -1345,6 +1446,33 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         }
         w += c[j];
     }
+}
+
+// The long-run list of the direct join: one wave per long query (wave_long_run).
+__global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ list, const uint64_t* __restrict__ qkey,
+                                                   const uint32_t* __restrict__ qslot,
+                                                   const uint64_t* __restrict__ unitInfo, uint32_t C,
+                                                   const DbRec* __restrict__ db, const int32_t* __restrict__ spOf,
+                                                   uint32_t maxTax, int kmerFormat, uint32_t* __restrict__ readCnt,
+                                                   unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
+                                                   uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
+                                                   SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
+                                                   int* __restrict__ overflow, uint32_t capShift,
+                                                   unsigned long long* __restrict__ stats) {
+    const LongRun lr = list[blockIdx.x];
+    const uint32_t got = wave_long_run(qkey[lr.q], qslot[lr.q], lr.lo, lr.hi, DbVal{db}, DbTax{db}, unitInfo, C, spOf,
+                                       maxTax, kmerFormat, readCnt, total, buf, bufRank, region, err, direct, dirOff,
+                                       overflow, capShift, (int)threadIdx.x);
+    if (threadIdx.x == 0 && got) atomicAdd(&stats[blockIdx.x % kStatStripes], 1ull);  // a matched query
+}
+
+void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, const uint32_t* qslot,
+                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, const int32_t* spOf, uint32_t maxTax,
+                       int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint32_t* bufRank,
+                       uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
+                       uint32_t capShift, unsigned long long* stats, hipStream_t s) {
+    if (n) k_match_long<<<n, 64, 0, s>>>(list, qkey, qslot, unitInfo, C, db, spOf, maxTax, kmerFormat, readCnt, total, buf,
+                                         bufRank, region, err, direct, dirOff, overflow, capShift, stats);
 }
 
 // Each staged match into its read's segment at the rank the join reserved for it (no atomics);
@@ -1718,7 +1846,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  uint32_t capShift, hipStream_t s) {
+                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -1728,13 +1856,14 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
-                                                        overflow, capShift);
+                                                        overflow, capShift, longList, longCap, longCnt);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
-                                                            stats, direct, dirOff, overflow, capShift);
+                                                            stats, direct, dirOff, overflow, capShift, nullptr, 0,
+                                                            longCnt);
     }
 }
 

@@ -211,13 +211,24 @@ __host__ __device__ inline mtb_match seg_expand(const SegMatch& s, uint64_t seqB
 // winCap: max DB values staged in LDS per block.
 constexpr uint32_t kStageRegions = 256;
 // qslot: each query's K1 slot (its info is slot_info(slot, C, unitInfo))
+// A direct-join query whose AA run is longer than kLongRun (mtb_kernels.hip) is deferred to the
+// long-run list and scanned by a wave of its own (launch_match_long).
+struct LongRun {
+    uint64_t q;       // index into the sorted query arrays
+    uint64_t lo, hi;  // its DB run
+};
+void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, const uint32_t* qslot,
+                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, const int32_t* spOf, uint32_t maxTax,
+                       int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint32_t* bufRank,
+                       uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
+                       uint32_t capShift, unsigned long long* stats, hipStream_t s);
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  uint32_t capShift, hipStream_t s);
+                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
 // slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A query whose ranks pass
 // its read's stretch spills its matches and their ranks to buf / bufRank (total[0] of them; at most

@@ -124,7 +124,12 @@ class GtdbRecipe:
                  total_species: int = 129_671, target_kmers: int = 12_000_000_000, strains: int = 2, seed: int = 6,
                  n_chunks: int = 64, before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
                  log: Callable[[str], None] = lambda s: None, syncmer: int = 0, smer_len: int = 5,
-                 per_genus: int = 1, species_div: float = 0.0):
+                 per_genus: int = 1, species_div: float = 0.0, conserved: int = 0, cons_min: int = 100,
+                 cons_max: int = 10_000):
+        """conserved > 0: that many AA 8-mers of the true-signal genomes are also held by cons_min to
+        cons_max filler species each (log-uniform: a heavy tail), as conserved genes' AA 8-mers are
+        shared across GTDB's species; their DB runs are long and their reads' queries select among
+        thousands of candidates."""
         self.dev, self.seed, self.n_chunks, self.log = dev, seed, n_chunks, log
         taxo = synth.make_taxonomy(total_species, strains, seed=seed,
                                    block_species=n_true_species if per_genus > 1 else 0, block_size=per_genus)
@@ -147,20 +152,93 @@ class GtdbRecipe:
                               if r == "no rank" and p in filler_sp], np.int32)
         self.strain_t = torch.from_numpy(strains_f).to(dev)
         self.cnt_t = torch.from_numpy(codon_counts().astype(np.float32)).to(dev)
-        n_fill = max(0, int(target_kmers) - self.n_true)
-        self.per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
         self.edges = [c * AA_RANKS // n_chunks for c in range(n_chunks + 1)]
         e_t = torch.tensor(self.edges, dtype=torch.int64, device=dev)
         self.cut = torch.searchsorted(self.tv, e_t << 24).cpu().tolist()  # true-signal records per chunk
+        self.conserved = conserved
+        n_cons = 0
+        self.cons_cut = [0] * (n_chunks + 1)
+        if conserved > 0:
+            # the filler species' strains (two per species, consecutive in the taxonomy), and the
+            # species of every taxID (for the (value, species) order of the merged records)
+            par = taxo.parent.astype(np.int64)
+            tid = taxo.taxid.astype(np.int64)
+            sp_of = np.zeros(int(tid.max()) + 1, np.int64)
+            rk = np.array(taxo.rank)
+            sp_of[tid[rk == "species"]] = tid[rk == "species"]
+            strain = rk == "no rank"
+            sp_of[tid[strain]] = par[strain]
+            self.sp_of_t = torch.from_numpy(sp_of).to(dev)
+            self.cons_strains = torch.from_numpy(strains_f.reshape(-1, strains).astype(np.int32)).to(dev)
+            gc = torch.Generator(device=dev)
+            gc.manual_seed(seed * 31337 + 7)
+            pick = torch.randint(0, self.n_true, (2 * conserved,), generator=gc, device=dev)
+            ranks = torch.unique(self.tv[pick] >> 24)
+            ranks = ranks[torch.randperm(ranks.numel(), generator=gc, device=dev)[:conserved]]
+            self.cons_rank, _ = torch.sort(ranks)
+            u = torch.rand(self.cons_rank.numel(), generator=gc, device=dev, dtype=torch.float64)
+            self.cons_k = (cons_min * torch.exp(u * float(np.log(cons_max / cons_min)))).long()
+            self.cons_base = torch.randint(0, self.cons_strains.shape[0], (self.cons_rank.numel(),), generator=gc,
+                                           device=dev)
+            self.cons_cut = torch.searchsorted(self.cons_rank, e_t).cpu().tolist()
+            ck = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(self.cons_k, 0)])
+            self.cons_kcut = ck[torch.tensor(self.cons_cut, device=dev)].cpu().tolist()  # conserved records per chunk
+            n_cons = int(ck[-1].item())
+            log(f"conserved AA 8-mers: {self.cons_rank.numel()} x {cons_min}-{cons_max} species "
+                f"({n_cons / 1e9:.3f}G k-mers)")
+        n_fill = max(0, int(target_kmers) - self.n_true - n_cons)
+        self.per = [n_fill // n_chunks + (1 if c < n_fill % n_chunks else 0) for c in range(n_chunks)]
         ids = np.unique(np.concatenate([gen.taxid.astype(np.int32), strains_f]))
         self.host = HostDb(taxo, taxid_list=ids.astype(np.int32))
 
+    def _conserved_chunk(self, c: int, g: torch.Generator):
+        """The conserved AA 8-mers of chunk c: per AA rank k consecutive filler species (distinct),
+        one strain each, each entry a random synonymous DNA of the AA 8-mer."""
+        a, b = self.cons_cut[c], self.cons_cut[c + 1]
+        if a == b:
+            e = torch.zeros(0, dtype=torch.int64, device=self.dev)
+            return e, e.int()
+        k = self.cons_k[a:b]
+        rr = torch.repeat_interleave(self.cons_rank[a:b], k)
+        first = torch.cumsum(k, 0) - k
+        j = torch.arange(rr.numel(), device=self.dev) - torch.repeat_interleave(first, k)
+        S = self.cons_strains.shape[0]
+        sp = (torch.repeat_interleave(self.cons_base[a:b], k) + j) % S
+        coin = torch.randint(0, self.cons_strains.shape[1], (rr.numel(),), generator=g, device=self.dev)
+        tax = self.cons_strains[sp, coin]
+        dna = torch.zeros_like(rr)
+        rem = rr.clone()
+        for q in range(8):  # least significant base-21 digit = the last codon = DNA bits 0..2
+            d = rem % 21
+            rem = rem // 21
+            cdn = (torch.rand(rr.numel(), generator=g, device=self.dev) * self.cnt_t[d]).long().clamp_(max=7)
+            dna |= cdn << (3 * q)
+        return (rr << 24) | dna, tax
+
     def _chunk(self, c: int):
-        """Chunk c's records as (sorted values, taxIDs): its true-signal k-mers and its filler."""
+        """Chunk c's records as (sorted values, taxIDs): its true-signal k-mers and its filler
+        (+ its conserved AA 8-mers' entries)."""
         g = torch.Generator(device=self.dev)
         g.manual_seed(self.seed * 7919 + 1 + 104729 * c)
         fv, ft = _filler_chunk(self.edges[c], self.edges[c + 1], self.per[c], g, self.cnt_t, self.strain_t)
         a, b = self.cut[c], self.cut[c + 1]
+        if self.conserved:
+            cv, ct = self._conserved_chunk(c, g)
+            v = torch.cat([self.tv[a:b], cv, fv])
+            t = torch.cat([self.ti[a:b], ct, ft])
+            del fv, ft, cv, ct
+            # (value, species) order, one entry per (value, species) (IndexCreator.h:617-624): a
+            # conserved entry that meets a filler entry of the same value and species is dropped
+            sp = self.sp_of_t[t.long()]
+            o1 = torch.argsort(sp, stable=True)
+            o2 = torch.argsort(v[o1], stable=True)
+            order = o1[o2]
+            del o1, o2
+            vs, ts, sps = v[order], t[order], sp[order]
+            dup = torch.zeros_like(vs, dtype=torch.bool)
+            dup[1:] = (vs[1:] == vs[:-1]) & (sps[1:] == sps[:-1])
+            keep = ~dup
+            return vs[keep], ts[keep]
         v = torch.cat([self.tv[a:b], fv])
         t = torch.cat([self.ti[a:b], ft])
         del fv, ft
@@ -170,7 +248,9 @@ class GtdbRecipe:
         return vs, t[order]
 
     def chunk_sizes(self) -> list:
-        return [self.cut[c + 1] - self.cut[c] + self.per[c] for c in range(self.n_chunks)]
+        """Records per chunk (an upper bound with conserved AA 8-mers: a rare duplicate is dropped)."""
+        cons = [(self.cons_kcut[c + 1] - self.cons_kcut[c]) if self.conserved else 0 for c in range(self.n_chunks)]
+        return [self.cut[c + 1] - self.cut[c] + self.per[c] + cons[c] for c in range(self.n_chunks)]
 
     def part_chunks(self, parts: int) -> list:
         """Chunk ranges of `parts` parts of about equal k-mer count."""
@@ -216,19 +296,65 @@ def build_gtdb_scale(dev: torch.device, n_true_species: int = 1000, genome_len: 
                      seed: int = 6, n_chunks: int = 64,
                      before_free: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None,
                      log: Callable[[str], None] = lambda s: None, syncmer: int = 0, smer_len: int = 5,
-                     per_genus: int = 1, species_div: float = 0.0) -> ResidentDb:
+                     per_genus: int = 1, species_div: float = 0.0, conserved: int = 0) -> ResidentDb:
     """Build the whole DB on `dev` (GtdbRecipe, all chunks). before_free(seq, off) runs while the
     true-signal genomes are still in HBM (the bench samples its reads there). syncmer: the
     true-signal part holds closed syncmers only (a Syncmer 1 DB, the format of GTDB R226's DB);
     per_genus / species_div: sister species of a genus share a diverged genus genome
     (make_genomes_gpu), so AA runs carry several species."""
     rc = GtdbRecipe(dev, n_true_species, genome_len, total_species, target_kmers, strains, seed, n_chunks,
-                    before_free, log, syncmer, smer_len, per_genus, species_div)
+                    before_free, log, syncmer, smer_len, per_genus, species_div, conserved)
     rdb = rc.build()
     rc.free_true()
     log(f"GTDB-scale DB: {rdb.n / 1e9:.3f}G k-mers ({rdb.n_true / 1e9:.3f}G true signal), "
         f"{rc.n_species} species in the taxonomy")
     return rdb
+
+
+def run_length_histogram(rdb: ResidentDb, chunk: int = 1 << 27) -> dict:
+    """AA runs of a resident DB (k-mers sharing an AA 8-mer: the candidates one query k-mer scans)
+    by length, in log2 bins: {"1": runs, "2-3": runs, ...} plus the k-mers in runs of each bin and
+    the longest run."""
+    dev = rdb.records.device
+    edges = torch.tensor([1 << b for b in range(40)], dtype=torch.int64, device=dev)
+    runs = torch.zeros(40, dtype=torch.int64, device=dev)
+    kmers = torch.zeros(40, dtype=torch.int64, device=dev)
+    longest = 0
+
+    def add(lens):
+        nonlocal longest
+        if lens.numel() == 0:
+            return
+        b = torch.bucketize(lens, edges, right=True) - 1
+        runs.index_add_(0, b, torch.ones_like(lens))
+        kmers.index_add_(0, b, lens)
+        longest = max(longest, int(lens.max().item()))
+
+    carry, prev = 0, -1
+    for a in range(0, rdb.n, chunk):
+        r = _lsr(rdb.values(a, min(rdb.n, a + chunk)), 24)
+        n = r.numel()
+        starts = torch.nonzero(r[1:] != r[:-1]).flatten() + 1
+        bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), starts,
+                            torch.full((1,), n, dtype=torch.int64, device=dev)])
+        lens = bounds[1:] - bounds[:-1]
+        if int(r[0].item()) == prev:
+            lens[0] += carry
+        elif carry:
+            add(torch.tensor([carry], dtype=torch.int64, device=dev))
+        carry = int(lens[-1].item())
+        add(lens[:-1])
+        prev = int(r[-1].item())
+        del r, starts, bounds, lens
+    if carry:
+        add(torch.tensor([carry], dtype=torch.int64, device=dev))
+    rc, kc = runs.cpu().tolist(), kmers.cpu().tolist()
+    out = {}
+    for b in range(40):
+        if rc[b]:
+            lo, hi = 1 << b, (1 << (b + 1)) - 1
+            out[str(lo) if lo == hi else f"{lo}-{hi}"] = {"runs": rc[b], "kmers": kc[b]}
+    return {"bins": out, "longest_run": longest}
 
 
 def to_rank_fmt2(v: torch.Tensor) -> torch.Tensor:

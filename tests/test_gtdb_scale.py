@@ -138,3 +138,39 @@ def test_partitioned_resident_parts_parity():
     sdb.close()
     compare_results(sres, stc, ores, otc)
     assert br.results["is_classified"].mean() > 0.5
+
+
+def test_conserved_heavy_tail_parity():
+    """The heavy-tailed variant at test scale: AA 8-mers of the true-signal genomes shared by 20 to
+    2000 filler species each (long DB runs: the join's long-run selection path, many matches per
+    query), classified through the resident DB against the oracle on the same DB; the run-length
+    histogram accounts for every k-mer."""
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+    from metabuli_work_amd.gpu_synth import make_reads_gpu
+    from metabuli_work_amd.gtdb_synth import GtdbRecipe, encode_into_oracle, run_length_histogram
+    from tests.test_gpu_parity import compare_results
+
+    dev = torch.device("cuda", 0)
+    got = {}
+
+    def grab(seq, off):
+        got["reads"] = make_reads_gpu(seq, off, 2000, 91, dev)
+
+    rc = GtdbRecipe(dev, n_true_species=10, genome_len=30000, total_species=3000, target_kmers=4_000_000,
+                    n_chunks=4, before_free=grab, conserved=400, cons_min=20, cons_max=2000)
+    rdb = rc.build()
+    v = rdb.values()
+    assert bool((v[1:] >= v[:-1]).all())
+    h = run_length_histogram(rdb, chunk=1 << 20)
+    assert sum(b["kmers"] for b in h["bins"].values()) == rdb.n
+    assert h["longest_run"] >= 500
+    reads = _host_reads(*got["reads"])
+    par = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    with Classifier(par, db_resident=rdb) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        st = clf.stats()
+    odb = encode_into_oracle(rdb, oc.OracleDb, chunk=1 << 20)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    odb.close()
+    compare_results(br.results, br.taxcnt, ores, otc)
+    assert st["max_read_matches"] > 50
