@@ -687,7 +687,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         log(rank, f"[bench] {tag} CPU oracle: {cpu['value'] if cpu else '-'} reads/s, parity {parity}")
     e2e = None
     if rank == 0 and not variant and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0):
-        e2e = run_e2e(args, clf, s1, s2, L, N)
+        e2e = run_e2e(args, clf, s1, s2, L, N, (ores, otc) if cpu is not None else None)
     clf.close()
     em_line = None
     if rank == 0 and not variant and args.em_pairs > 0:
@@ -775,12 +775,36 @@ def run_em(args, rdb, lp, s1, s2, o1, L, N, B, local):
     return out
 
 
-def run_e2e(args, clf, s1, s2, L, N):
+def tsv_matches_oracle(tsv, ores, otc):
+    """The first len(ores) lines of a classification TSV against the oracle's results for the same
+    reads, field by field (Reporter::writeReadClassification, Reporter.cpp:38-83: classified flag,
+    taxID, query length, score as %g, taxID:count list)."""
+    n = len(ores)
+    with open(tsv) as f:
+        f.readline()
+        for i in range(n):
+            fld = f.readline().rstrip("\n").split("\t")
+            o = ores[i]
+            cl = bool(o["is_classified"])
+            if fld[0] != ("1" if cl else "0") or int(fld[2]) != (int(o["classification"]) if cl else 0):
+                return False
+            if int(fld[3]) != int(o["query_length"]) or fld[4] != "%g" % float(o["score"]):
+                return False
+            if cl:
+                a = int(o["taxcnt_offset"])
+                want = "".join(f"{int(t)}:{int(c)} " for t, c in otc[a:a + int(o["taxcnt_len"])])
+                if fld[6] != want:
+                    return False
+    return True
+
+
+def run_e2e(args, clf, s1, s2, L, N, check=None):
     """File -> TSV (SURVEY §8(d) "end-to-end reads/s including host parse and write"): the rank's
     first read pairs written as FASTQ mate files (BGZF, plain, single-member gzip), then
     Classifier.startClassify = the native pipeline (mtb_start_classify: readers/parsers, pinned
     batches uploaded on a copy stream, mtb_classify_batch, TSV writer + report) timed wall-clock.
-    Files live in /dev/shm (page cache speed, no disk in the measurement)."""
+    Files live in /dev/shm (page cache speed, no disk in the measurement). With check = (ores, otc),
+    the oracle's results for the first read pairs, the TSV's first lines are compared with them."""
     import shutil
     import tempfile
 
@@ -814,6 +838,9 @@ def run_e2e(args, clf, s1, s2, L, N):
                          "input_bytes": size, "batches": int(lr["batches"]), "gpu_s": round(lr["gpu_s"], 3),
                          "input_wait_s": round(lr["input_wait_s"], 3), "write_s": round(lr["write_s"], 3),
                          "tsv_lines_ok": lines == got + 1, "file_prep_s": round(prep, 1)}
+            if check is not None:  # the file's first reads are the oracle sample's
+                out[mode]["tsv_oracle_lines"] = len(check[0])
+                out[mode]["tsv_matches_oracle"] = tsv_matches_oracle(tsv, *check)
             log(0, f"[bench] end to end ({mode}): {got / wall / 1e6:.2f}M read pairs/s, {out[mode]}")
             for p in (p1, p2, tsv, rep):
                 os.remove(p)

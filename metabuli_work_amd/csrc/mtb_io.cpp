@@ -143,6 +143,123 @@ bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, s
     return true;
 }
 
+namespace {
+
+// Lines of an in-memory range: next() gives the line at `pos` without '\n' / '\r'. kIncomplete
+// when the range holds no '\n' after pos and is not the end of the input.
+enum LineRc { kLine, kEnd, kIncomplete };
+
+struct MemLines {
+    const char* p;
+    size_t n, pos;
+    bool eof;
+    LineRc next(const char*& s, size_t& len) {
+        if (pos == n) return eof ? kEnd : kIncomplete;
+        s = p + pos;
+        const char* nl = (const char*)memchr(s, '\n', n - pos);
+        if (!nl && !eof) return kIncomplete;
+        len = nl ? (size_t)(nl - s) : n - pos;
+        pos += len + (nl ? 1 : 0);
+        if (len && s[len - 1] == '\r') len--;
+        return kLine;
+    }
+};
+
+// next_record's semantics over p[0, n): whole records only, at most maxRecs of them. kParse
+// appends them to the block buffers; without it the records are only counted (the splitter's
+// boundary pass). Returns the bytes the whole records (and blank lines before them) span.
+template <bool kParse>
+size_t walk_records(const char* p, size_t n, bool eof, uint32_t maxRecs, uint32_t* recs, std::string* seq,
+                    std::vector<uint64_t>* off, std::string* names, std::vector<uint64_t>* noff, std::string& err) {
+    MemLines m{p, n, 0, eof};
+    size_t done = 0;
+    uint32_t k = 0;
+    const char* s;
+    size_t len;
+    while (k < maxRecs) {
+        // blank lines before a header (a line starting with '\r' counts as blank, as in next_record)
+        while (m.pos < n && (p[m.pos] == '\n' || p[m.pos] == '\r')) {
+            if (m.next(s, len) == kIncomplete) break;
+        }
+        if (m.pos == n || (m.pos < n && (p[m.pos] == '\n' || p[m.pos] == '\r'))) {
+            if (m.pos == n && eof) done = n;  // trailing blank lines end the input
+            break;
+        }
+        const LineRc h = m.next(s, len);
+        if (h != kLine) break;
+        if (len == 0 || (s[0] != '>' && s[0] != '@')) {
+            err = "not a FASTA/FASTQ record header";
+            break;
+        }
+        const bool fastq = s[0] == '@';
+        const char* name = s + 1;
+        size_t nameLen = 1;
+        while (nameLen < len && s[nameLen] != ' ' && s[nameLen] != '\t') nameLen++;
+        nameLen--;
+        const size_t seqStart = kParse ? seq->size() : 0;
+        bool complete = true;
+        if (fastq) {
+            size_t slen = 0;
+            LineRc rc;
+            while ((rc = m.next(s, len)) == kLine && !(len && s[0] == '+')) {
+                if (kParse) seq->append(s, len);
+                slen += len;
+            }
+            if (rc != kLine) {
+                if (rc == kEnd) err = "truncated FASTQ record";
+                complete = false;
+            }
+            for (size_t qlen = 0; complete && qlen < slen;) {
+                rc = m.next(s, len);
+                if (rc != kLine) {
+                    if (rc == kEnd) err = "truncated FASTQ record";
+                    complete = false;
+                }
+                qlen += len;
+            }
+        } else {
+            while (true) {  // sequence lines up to the next '>' (a record at the input's end is whole)
+                if (m.pos == n) {
+                    complete = eof;
+                    break;
+                }
+                if (p[m.pos] == '>') break;
+                if (m.next(s, len) != kLine) {
+                    complete = false;
+                    break;
+                }
+                if (kParse) seq->append(s, len);
+            }
+        }
+        if (!complete) {
+            if (kParse) seq->resize(seqStart);
+            break;
+        }
+        if (kParse) {
+            names->append(name, nameLen);
+            noff->push_back(names->size());
+            off->push_back(seq->size());
+        }
+        k++;
+        done = m.pos;
+    }
+    *recs = k;
+    return done;
+}
+
+}  // namespace
+
+size_t scan_records(const char* p, size_t n, bool eof, uint32_t maxRecs, uint32_t* recs, std::string& err) {
+    return walk_records<false>(p, n, eof, maxRecs, recs, nullptr, nullptr, nullptr, nullptr, err);
+}
+
+uint32_t parse_records(const char* p, size_t n, std::string& seq, std::vector<uint64_t>& off, std::string& names,
+                       std::vector<uint64_t>& noff, std::string& err) {
+    uint32_t k = 0;
+    walk_records<true>(p, n, true, 0xFFFFFFFFu, &k, &seq, &off, &names, &noff, err);
+    return k;
+}
+
 }  // namespace mtb
 
 using mtb::FastxStream;

@@ -44,4 +44,13 @@ struct FastxStream {
 bool next_record(FastxStream& s, std::string& seq, std::vector<uint64_t>& off, std::string& names,
                  std::vector<uint64_t>& noff, std::string& err);
 
+// The same semantics over an in-memory range, split in two passes so records can be parsed in
+// parallel: scan_records counts up to maxRecs whole records at the front of p[0, n) (eof: the
+// range ends the input) and returns the bytes they span — a record the range does not complete
+// is left for the next range; parse_records appends every record of a range scan_records cut.
+// err is set on malformed input.
+size_t scan_records(const char* p, size_t n, bool eof, uint32_t maxRecs, uint32_t* recs, std::string& err);
+uint32_t parse_records(const char* p, size_t n, std::string& seq, std::vector<uint64_t>& off, std::string& names,
+                       std::vector<uint64_t>& noff, std::string& err);
+
 }  // namespace mtb

@@ -2,9 +2,10 @@
 // §8(f)1-2): the reference indexes the input in one serial pass (QueryIndexer.cpp:30-147), then
 // re-reads it chunk by chunk on one thread (KmerExtractor.cpp:442-494) while the compute waits.
 // Here four kinds of threads overlap:
-//   * per mate file, a byte source (BGZF blocks inflated by a worker pool; gzip / plain read ahead)
-//     and a parser cutting records into blocks of kBlockReads reads;
-//   * an assembler filling pinned host batches (<= max_reads reads, <= max_bases bases: the
+//   * per mate file, a byte source (BGZF blocks inflated by a worker pool; gzip / plain read ahead),
+//     a splitter cutting the bytes at record boundaries and a pool of parse workers turning each
+//     cut into a block of up to kBlockReads records;
+//   * an assembler filling pinned host batches (the copies split over kCopyThreads threads) (<= max_reads reads, <= max_bases bases: the
 //     reference's RAM-bounded QuerySplits, QueryIndexer.cpp:62-67,132-137) and uploading each to
 //     its device's buffers on that device's copy stream;
 //   * per context (one per GPU) a worker running mtb_classify_batch on the uploaded batches
@@ -21,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -86,6 +88,7 @@ struct ErrorBox {
 
 constexpr uint32_t kBlockReads = 8192;
 constexpr int kSlots = 3;
+constexpr size_t kCopyThreads = 4;  // threads filling one pinned batch
 
 struct RecordBlock {
     std::string names, seq;
@@ -93,22 +96,113 @@ struct RecordBlock {
     uint32_t n = 0;
 };
 
-struct MateReader {
-    mtb::FastxStream st;
-    BoundedQueue<std::shared_ptr<RecordBlock>> out{6};
-    std::thread t;
-    void run(ErrorBox* eb) {
-        std::string err;
-        while (!eb->failed) {
-            auto b = std::make_shared<RecordBlock>();
-            while (b->n < kBlockReads && mtb::next_record(st, b->seq, b->off, b->names, b->noff, err)) b->n++;
-            if (!err.empty()) {
-                eb->set(MTB_ERR_IO, err);
-                break;
-            }
-            if (b->n && !out.push(b)) break;
-            if (b->n < kBlockReads) break;
+// A raw byte range of the input in memory, shared by the parse jobs cut from it.
+struct RawBuf {
+    std::unique_ptr<char[]> p;
+    size_t cap;
+    explicit RawBuf(size_t c) : p(new char[c]), cap(c) {}
+};
+
+// Whole records p[b, e) of a raw buffer, parsed into blk by a parse worker.
+struct ParseJob {
+    std::shared_ptr<RawBuf> raw;
+    size_t b = 0, e = 0;
+    uint32_t recs = 0;  // as counted by the splitter
+    RecordBlock blk;
+    std::string err;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    void finish() {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            done = true;
         }
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return done; });
+    }
+};
+
+// One mate file: a splitter thread cuts the decompressed bytes at record boundaries into jobs of
+// kBlockReads records (scan_records: a boundary pass with next_record's semantics, no copying) and
+// a pool of parse workers fills the jobs' blocks (parse_records); `out` hands the jobs on in file
+// order, each to be waited for. The reference parses every record on one thread
+// (KmerExtractor.cpp:442-494).
+struct MateReader {
+    size_t rawBytes = 32u << 20;  // raw buffer (MTB_PARSE_BUFFER: tests cut records at buffer ends)
+    std::unique_ptr<mtb::ByteSource> src;
+    BoundedQueue<std::shared_ptr<ParseJob>> out{32}, work{32};
+    std::thread t;
+    std::vector<std::thread> parsers;
+    void run(ErrorBox* eb, int nParsers) {
+        for (int i = 0; i < nParsers; i++)
+            parsers.emplace_back([this, eb] {
+                std::shared_ptr<ParseJob> j;
+                while (work.pop(j)) {
+                    if (!eb->failed) {
+                        RecordBlock& b = j->blk;  // a record's sequence is under half its FASTQ bytes
+                        b.seq.reserve((j->e - j->b) / 2 + 64);
+                        b.off.reserve(j->recs + 1);
+                        b.noff.reserve(j->recs + 1);
+                        j->blk.n = mtb::parse_records(j->raw->p.get() + j->b, j->e - j->b, j->blk.seq, j->blk.off,
+                                                      j->blk.names, j->blk.noff, j->err);
+                    }
+                    j->raw.reset();
+                    j->finish();
+                }
+            });
+        std::string err;
+        auto buf = std::make_shared<RawBuf>(rawBytes);
+        size_t have = 0;
+        bool eof = false, stopped = false;
+        while (!eb->failed && !stopped) {
+            while (have < buf->cap && !eof) {
+                const long got = src->read(buf->p.get() + have, buf->cap - have);
+                if (got < 0) {
+                    err = src->err.empty() ? "read error" : src->err;
+                    break;
+                }
+                if (got == 0) eof = true;
+                have += (size_t)got;
+            }
+            if (!err.empty()) break;
+            size_t pos = 0;
+            while (!stopped) {
+                uint32_t recs = 0;
+                const size_t used = mtb::scan_records(buf->p.get() + pos, have - pos, eof, kBlockReads, &recs, err);
+                if (!err.empty() || recs == 0) {
+                    pos += used;  // trailing blank lines at the end of the input
+                    break;
+                }
+                auto j = std::make_shared<ParseJob>();
+                j->raw = buf;
+                j->b = pos;
+                j->e = pos + used;
+                j->recs = recs;
+                pos += used;
+                if (!out.push(j)) {
+                    stopped = true;
+                } else if (!work.push(j)) {
+                    j->err = "input stopped";
+                    j->finish();
+                    stopped = true;
+                }
+                if (recs < kBlockReads) break;  // the buffer ends inside a record (or the input ends)
+            }
+            if (!err.empty() || eof) break;
+            // the unfinished record moves to the front of a fresh buffer (grown when it fills half)
+            const size_t rest = have - pos;
+            auto nb = std::make_shared<RawBuf>(rest > buf->cap / 2 ? buf->cap * 2 : buf->cap);
+            memcpy(nb->p.get(), buf->p.get() + pos, rest);
+            buf = nb;
+            have = rest;
+        }
+        if (!err.empty()) eb->set(MTB_ERR_IO, err);
+        work.close();
+        for (auto& p : parsers) p.join();
         out.close();
     }
 };
@@ -174,10 +268,22 @@ struct Slot {
 struct Cursor {
     std::shared_ptr<RecordBlock> b;
     uint32_t at = 0;
-    bool next(MateReader& m) {
+    bool next(MateReader& m, ErrorBox& eb) {
         if (b && at < b->n) return true;
         at = 0;
-        return m.out.pop(b);
+        std::shared_ptr<ParseJob> j;
+        while (m.out.pop(j)) {
+            j->wait();
+            if (!j->err.empty()) {
+                eb.set(MTB_ERR_IO, j->err);
+                return false;
+            }
+            if (!j->blk.n) continue;
+            b = std::shared_ptr<RecordBlock>(j, &j->blk);
+            return true;
+        }
+        b.reset();
+        return false;
     }
 };
 
@@ -221,13 +327,14 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     ErrorBox eb;
     MateReader m1, m2;
     const int srcThreads = std::max(1, paired ? threads / 2 : threads);
-    if (!m1.st.open(opt->query1, srcThreads, true)) {
-        set_error(m1.st.err);
-        return MTB_ERR_IO;
-    }
-    if (paired && !m2.st.open(opt->query2, srcThreads, true)) {
-        set_error(m2.st.err);
-        return MTB_ERR_IO;
+    const int parseThreads = std::max(2, srcThreads / 2);  // per mate
+    {
+        std::string err;
+        if (!(m1.src = mtb::open_source(opt->query1, srcThreads, true, err)) ||
+            (paired && !(m2.src = mtb::open_source(opt->query2, srcThreads, true, err)))) {
+            set_error(err);
+            return MTB_ERR_IO;
+        }
     }
     // per context: kSlots slots, a copy stream on its device, free and ready queues
     std::vector<std::unique_ptr<Slot>> slotMem;
@@ -252,8 +359,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     }
     BoundedQueue<Slot*> writeQ(slotMem.size() + 1);
 
-    m1.t = std::thread([&] { m1.run(&eb); });
-    if (paired) m2.t = std::thread([&] { m2.run(&eb); });
+    if (const char* e = getenv("MTB_PARSE_BUFFER")) m1.rawBytes = m2.rawBytes = std::max<size_t>(1, strtoull(e, nullptr, 10));
+    m1.t = std::thread([&] { m1.run(&eb, parseThreads); });
+    if (paired) m2.t = std::thread([&] { m2.run(&eb, parseThreads); });
 
     // assembler: blocks -> pinned batches -> device buffers of context (batch mod n)
     std::thread assembler([&] {
@@ -272,23 +380,27 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             std::vector<std::pair<std::shared_ptr<RecordBlock>, std::pair<uint32_t, uint32_t>>> take1, take2;
             // which reads go in: whole block stretches until max_reads / max_bases
             static const char* kUnequal = "paired-end inputs have different read counts (QueryIndexer.cpp:121-124)";
-            while (s->n < maxReads) {
-                const bool more1 = c1.next(m1);
-                const bool more2 = paired && c2.next(m2);
-                if (!more1) {
-                    if (more2) eb.set(MTB_ERR_IO, kUnequal);
+            // with the default batch size the first batches ramp up (1/8, 1/4, 1/2 of it): the GPU
+            // starts after a small parse instead of a full batch's; a read's result does not depend
+            // on its batch
+            const uint32_t cap = !opt->max_reads && index < 3 ? std::max<uint32_t>(1, maxReads >> (3 - index)) : maxReads;
+            while (s->n < cap) {
+                const bool more1 = c1.next(m1, eb);
+                const bool more2 = paired && c2.next(m2, eb);
+                if (eb.failed) {
                     end = true;
                     break;
                 }
-                // both mates are cut into blocks of kBlockReads: their stretches line up read by read
-                if (paired && (!more2 || c2.b->n - c2.at != c1.b->n - c1.at)) {
-                    eb.set(MTB_ERR_IO, kUnequal);
+                if (!more1 || (paired && !more2)) {
+                    if (more1 || more2) eb.set(MTB_ERR_IO, kUnequal);
                     end = true;
                     break;
                 }
+                // the mates' blocks may be cut at different reads: take the stretch both still hold
                 const RecordBlock& x = *c1.b;
+                const uint32_t lim = paired ? std::min(x.n, c1.at + (c2.b->n - c2.at)) : x.n;
                 uint32_t k = c1.at;
-                while (k < x.n && s->n + (k - c1.at) < maxReads) {
+                while (k < lim && s->n + (k - c1.at) < cap) {
                     uint64_t len = x.off[k + 1] - x.off[k];
                     if (paired) len += c2.b->off[c2.at + (k - c1.at) + 1] - c2.b->off[c2.at + (k - c1.at)];
                     if (s->bases + len > maxBases && s->n + (k - c1.at) > 0) break;
@@ -312,32 +424,64 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 freeQ[d]->push(s);
                 break;
             }
-            auto fill = [&](auto& take, Pinned<char>& seq, Pinned<uint64_t>& off, uint64_t bytes, bool names) {
-                if (seq.ensure(bytes + 1) != hipSuccess || off.ensure((size_t)s->n + 1) != hipSuccess) return false;
+            // the blocks' stretches are copied into the pinned batch by a few threads at once
+            struct Piece {
+                const RecordBlock* b;
+                uint32_t lo, hi, r;  // r: the batch index of read lo
+                uint64_t seqAt, nameAt;
+                int mate;
+            };
+            std::vector<Piece> pieces;
+            uint64_t nameBytes = 0;
+            for (int mate = 0; mate < (paired ? 2 : 1); mate++) {
                 uint64_t at = 0;
                 uint32_t r = 0;
-                off.p[0] = 0;
-                for (auto& tk : take) {
+                for (auto& tk : mate ? take2 : take1) {
                     const RecordBlock& b = *tk.first;
                     const uint32_t lo = tk.second.first, hi = tk.second.second;
-                    const uint64_t base = b.off[lo];
-                    memcpy(seq.p + at, b.seq.data() + base, b.off[hi] - base);
-                    for (uint32_t i = lo; i < hi; i++) off.p[++r] = at + (b.off[i + 1] - base);
-                    at += b.off[hi] - base;
-                    if (names) {
-                        const uint64_t nb = b.noff[lo];
-                        const size_t o = s->names.size();
-                        s->names.append(b.names.data() + nb, b.noff[hi] - nb);
-                        for (uint32_t i = lo; i < hi; i++) s->noff.push_back(o + (b.noff[i + 1] - nb));
-                    }
+                    pieces.push_back({&b, lo, hi, r, at, nameBytes, mate});
+                    at += b.off[hi] - b.off[lo];
+                    r += hi - lo;
+                    if (!mate) nameBytes += b.noff[hi] - b.noff[lo];
                 }
-                return true;
-            };
-            if (!fill(take1, s->seq1, s->off1, b1, true) || (paired && !fill(take2, s->seq2, s->off2, b2, false))) {
+            }
+            if (s->seq1.ensure(b1 + 1) != hipSuccess || s->off1.ensure((size_t)s->n + 1) != hipSuccess ||
+                (paired && (s->seq2.ensure(b2 + 1) != hipSuccess || s->off2.ensure((size_t)s->n + 1) != hipSuccess))) {
                 eb.set(MTB_ERR_OOM, "cannot allocate pinned host batch buffers");
                 freeQ[d]->push(s);
                 break;
             }
+            s->names.resize(nameBytes);
+            s->noff.resize((size_t)s->n + 1);
+            s->off1.p[0] = 0;
+            if (paired) s->off2.p[0] = 0;
+            std::atomic<size_t> nextPiece{0};
+            auto copy = [&] {
+                for (size_t i; (i = nextPiece.fetch_add(1)) < pieces.size();) {
+                    const Piece& pc = pieces[i];
+                    const RecordBlock& b = *pc.b;
+                    char* seq = pc.mate ? s->seq2.p : s->seq1.p;
+                    uint64_t* off = pc.mate ? s->off2.p : s->off1.p;
+                    const uint64_t base = b.off[pc.lo];
+                    memcpy(seq + pc.seqAt, b.seq.data() + base, b.off[pc.hi] - base);
+                    for (uint32_t k = pc.lo; k < pc.hi; k++) off[pc.r + 1 + (k - pc.lo)] = pc.seqAt + (b.off[k + 1] - base);
+                    if (!pc.mate) {
+                        const uint64_t nb = b.noff[pc.lo];
+                        memcpy(&s->names[pc.nameAt], b.names.data() + nb, b.noff[pc.hi] - nb);
+                        for (uint32_t k = pc.lo; k < pc.hi; k++)
+                            s->noff[pc.r + 1 + (k - pc.lo)] = pc.nameAt + (b.noff[k + 1] - nb);
+                    }
+                }
+            };
+            {
+                std::vector<std::thread> cp;
+                const size_t nCopy = std::min<size_t>(pieces.size(), kCopyThreads);
+                for (size_t t = 1; t < nCopy; t++) cp.emplace_back(copy);
+                copy();
+                for (auto& t : cp) t.join();
+            }
+            take1.clear();
+            take2.clear();
             // the slot's device buffers live on its context's device (a new thread starts on device 0)
             const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
             bool ok = hipSetDevice(mtb_ctx_device(ctxs[d])) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
@@ -423,6 +567,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
 
     // writer: the batches in input order -> TSV lines + per-taxon read counts (+ --em mappings)
     std::map<int32_t, uint64_t> taxCounts;
+    std::vector<uint64_t> denseCounts;
     std::vector<mtb_em_map> emMaps;
     uint64_t reads = 0, bases = 0, batches = 0;
     double writeS = 0, gpuS = 0;
@@ -447,8 +592,15 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                                                   opt->write_flags) != MTB_OK)
                         eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
                     first = false;
-                    for (uint32_t i = 0; i < s->n; i++)  // ++taxCounts[classification] (Classifier.cpp:201-203)
-                        taxCounts[s->res[i].is_classified ? s->res[i].classification : 0]++;
+                    for (uint32_t i = 0; i < s->n; i++) {  // ++taxCounts[classification] (Classifier.cpp:201-203)
+                        const int32_t t = s->res[i].is_classified ? s->res[i].classification : 0;
+                        if (t >= 0 && t < (1 << 26)) {  // internal taxIDs are dense: a flat table
+                            if ((size_t)t >= denseCounts.size()) denseCounts.resize((size_t)t * 2 + 1024, 0);
+                            denseCounts[t]++;
+                        } else {
+                            taxCounts[t]++;
+                        }
+                    }
                     emMaps.insert(emMaps.end(), s->em.begin(), s->em.end());
                     reads += s->n;
                     bases += s->bases;
@@ -493,6 +645,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         set_error(eb.msg);
         return eb.code;
     }
+    for (size_t t = 0; t < denseCounts.size(); t++)
+        if (denseCounts[t]) taxCounts[(int32_t)t] += denseCounts[t];
     if (opt->report_tsv) {
         std::vector<int32_t> ids;
         std::vector<uint32_t> cnt;

@@ -280,3 +280,37 @@ def test_start_classify_multi(make_db, tmp_path, n_ctx):
     odb.close()
     body = [l.split("\t") for l in open(many).read().split("\n")[1:] if l]
     assert [int(f[2]) for f in body] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("raw", [600, 7001])
+def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
+    """The pipeline's record split (splitter + parse workers): raw buffers of a few hundred bytes cut
+    records at every kind of position, and the two mates (one wrapped, one not) are cut at different
+    reads, so the assembler joins blocks that do not line up. The TSV is the default run's byte for
+    byte; unequal mate counts still fail (QueryIndexer.cpp:121-124)."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 900, paired=True, seed=53, short_frac=0.02)
+    names = [f"e{i}" for i in range(r.n)]
+    p1, p2 = str(tmp_path / "q1.fq"), str(tmp_path / "q2.fq")
+    with open(p1, "w") as f:
+        for nm, sq in zip(names, _mates(r, 1)):
+            s = sq.decode()
+            f.write(f"@{nm} x\n" + "".join(s[i:i + 29] + "\n" for i in range(0, len(s), 29)) + "+\n" +
+                    "".join("I" * len(s[i:i + 31]) + "\n" for i in range(0, len(s), 31)))
+    _write_fastq(p2, names, _mates(r, 2))
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    ref, got = str(tmp_path / "ref.tsv"), str(tmp_path / "got.tsv")
+    with Classifier(par, db_dir=db_dir) as clf:
+        assert clf.startClassify(ref, reads_per_batch=301) == r.n
+        monkeypatch.setenv("MTB_PARSE_BUFFER", str(raw))
+        assert clf.startClassify(got, reads_per_batch=301) == r.n
+        assert open(got, "rb").read() == open(ref, "rb").read()
+        short = str(tmp_path / "short.fq")
+        _write_fastq(short, names[:-1], _mates(r, 2)[:-1])
+        par2 = LocalParameters(seqMode=2, filenames=[p1, short, db_dir])
+        par2.load_db_parameters(db_dir)
+        clf.par = par2
+        with pytest.raises(MtbError, match="different read counts"):
+            clf.startClassify(str(tmp_path / "bad.tsv"), reads_per_batch=301)
