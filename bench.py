@@ -837,6 +837,8 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
             out[mode] = {"reads_per_s": round(got / wall, 1), "read_pairs": got, "wall_s": round(wall, 3),
                          "input_bytes": size, "batches": int(lr["batches"]), "gpu_s": round(lr["gpu_s"], 3),
                          "input_wait_s": round(lr["input_wait_s"], 3), "write_s": round(lr["write_s"], 3),
+                         "host_stages_s": {k: round(lr[k], 3) for k in ("source_s", "scan_s", "parse_s", "fill_s",
+                                                                        "first_batch_s")},
                          "tsv_lines_ok": lines == got + 1, "file_prep_s": round(prep, 1)}
             if check is not None:  # the file's first reads are the oracle sample's
                 out[mode]["tsv_oracle_lines"] = len(check[0])

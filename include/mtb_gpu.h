@@ -328,7 +328,8 @@ int mtb_write_report(const mtb_ctx* ctx, const char* path, uint64_t total_reads,
 
 /* ---- Classifier::startClassify over files ----------------------------------- */
 /* Classifier.cpp:44-164 as a threaded native pipeline: per mate file a reader (BGZF blocks inflated
- * by a worker pool; gzip and plain files read ahead) and a parser; an assembler filling pinned
+ * by a worker pool; gzip and plain files read ahead), a splitter cutting the bytes at record
+ * boundaries and a pool of parse workers; an assembler filling pinned
  * batches of <= max_reads reads and <= max_bases bases (the reference's RAM-bounded QuerySplits,
  * QueryIndexer.cpp:62-67,132-137) and uploading each on a copy stream; mtb_classify_batch on the
  * calling thread; a writer emitting the per-read TSV (Reporter.cpp:38-83) while the next batch runs.
@@ -338,10 +339,12 @@ typedef struct mtb_classify_opts {
     const char* query2;       /* mate 2 (seq_mode 2), else NULL                                 */
     const char* out_tsv;      /* per-read classifications                                       */
     const char* report_tsv;   /* per-taxon report, or NULL                                      */
-    uint32_t max_reads;       /* reads per batch (0: 1,000,000)                                 */
+    uint32_t max_reads;       /* reads per batch (0: 1,000,000, the first three batches ramping
+                                 up from 1/8 of it so the GPU starts early)                       */
     uint32_t write_flags;     /* MTB_WRITE_LINEAGE                                              */
     uint64_t max_bases;       /* bases per batch, both mates (0: from free HBM, < 2^30)         */
-    int32_t threads;          /* host threads for inflating (0: min(16, cores))                 */
+    int32_t threads;          /* host threads for inflating, per run (0: min(16, cores)); each
+                                 mate also gets max(2, threads / 4) parse workers                 */
     int32_t reserved;
     /* --em outputs (context opened with em = 1; each NULL to skip): the reassigned reads
      * (Reporter::writeReclassifyResults), the EM abundance report and the reassignment report
@@ -356,6 +359,12 @@ typedef struct mtb_classify_stats {
     double gpu_s;             /* mtb_classify_batch calls                                       */
     double input_wait_s;      /* the GPU stage waiting for a parsed, uploaded batch             */
     double write_s;           /* TSV formatting and writing (overlapped with the GPU stage)     */
+    /* host input stages, summed over the mates (and over the parse workers for parse_s)           */
+    double source_s;          /* decompressed bytes from the file sources                       */
+    double scan_s;            /* record-boundary scans (splitters)                              */
+    double parse_s;           /* record parsing (parse workers)                                 */
+    double fill_s;            /* pinned batch filling and upload issue (assembler)              */
+    double first_batch_s;     /* run start until the first batch is uploaded                    */
 } mtb_classify_stats;
 int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify_stats* stats);
 /* The same run over n_ctx contexts, one per GPU of the node (each holding the DB, or the same

@@ -323,13 +323,14 @@ class Classifier:
         sp = {int(ids[i]): (float(probs[i]), int(cnts[i])) for i in range(k)}
         return reads[:int(total_reads)], sp, {f: getattr(st, f) for f, _ in _abi.MtbEmStats._fields_}
 
-    def startClassify(self, out_tsv: str, reads_per_batch: int = 1_000_000, report_tsv: Optional[str] = None,
+    def startClassify(self, out_tsv: str, reads_per_batch: int = 0, report_tsv: Optional[str] = None,
                       max_bases: int = 0, threads: int = 0, em_tsv: Optional[str] = None,
                       em_report_tsv: Optional[str] = None, em_reclassify_report_tsv: Optional[str] = None,
                       peers: Optional[List["Classifier"]] = None) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
         (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
-        reads_per_batch reads and max_bases bases (0: sized from free HBM, the reference's
+        reads_per_batch reads (0: 1M, the first three batches ramping up from 1/8 of that) and
+        max_bases bases (0: sized from free HBM, the reference's
         RAM-bounded QuerySplits) uploaded on a copy stream, mtb_classify_batch, and the TSV writer
         (+ the per-taxon report, Classifier.cpp:149) overlapping each other; with --em (par.em) the
         EM reassignment after the last batch and its TSV / reports (Classifier.cpp:152-161). Returns

@@ -358,7 +358,10 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
     if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const uint32_t per = (n + nt - 1) / nt;
-    std::vector<std::string> part(nt);
+    // the formatted parts stay allocated per calling thread: a pipeline's writer reuses warm memory
+    static thread_local std::vector<std::string> part;
+    part.resize(nt);
+    for (auto& x : part) x.clear();
     auto work = [&](unsigned t) {
         std::string& o = part[t];
         char tmp[64];

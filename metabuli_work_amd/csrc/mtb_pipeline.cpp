@@ -113,6 +113,18 @@ struct ParseJob {
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
+    void reset() {
+        raw.reset();
+        b = e = 0;
+        recs = 0;
+        blk.n = 0;
+        blk.seq.clear();  // the capacities stay: a recycled job's parse writes into warm memory
+        blk.names.clear();
+        blk.off.assign(1, 0);
+        blk.noff.assign(1, 0);
+        err.clear();
+        done = false;
+    }
     void finish() {
         {
             std::lock_guard<std::mutex> l(mu);
@@ -126,58 +138,139 @@ struct ParseJob {
     }
 };
 
-// One mate file: a splitter thread cuts the decompressed bytes at record boundaries into jobs of
-// kBlockReads records (scan_records: a boundary pass with next_record's semantics, no copying) and
-// a pool of parse workers fills the jobs' blocks (parse_records); `out` hands the jobs on in file
-// order, each to be waited for. The reference parses every record on one thread
-// (KmerExtractor.cpp:442-494).
+// A free list of T: objects come back when their last shared_ptr goes, so the input's bytes flow
+// through the same few buffers instead of freshly mapped (page-faulting) ones per chunk.
+template <typename T>
+struct Recycler : std::enable_shared_from_this<Recycler<T>> {
+    std::mutex mu;
+    std::vector<std::unique_ptr<T>> idle;
+    template <typename Make>
+    std::shared_ptr<T> get(Make make) {
+        std::unique_ptr<T> x;
+        {
+            std::lock_guard<std::mutex> l(mu);
+            if (!idle.empty()) {
+                x = std::move(idle.back());
+                idle.pop_back();
+            }
+        }
+        if (!x) x.reset(make());
+        auto self = this->shared_from_this();
+        return std::shared_ptr<T>(x.release(), [self](T* t) {
+            std::lock_guard<std::mutex> l(self->mu);
+            self->idle.emplace_back(t);
+        });
+    }
+};
+
+// One mate file, three stages:
+//   * a reader thread filling recycled raw buffers from the byte source, past `head` bytes of
+//     headroom at the front;
+//   * a splitter moving the previous buffer's unfinished record into that headroom and cutting the
+//     bytes at record boundaries into jobs of kBlockReads records (scan_records: a boundary pass
+//     with next_record's semantics, no copying);
+//   * a pool of parse workers filling the jobs' blocks (parse_records).
+// `out` hands the jobs on in file order, each to be waited for. The reference parses every record
+// on one thread (KmerExtractor.cpp:442-494).
 struct MateReader {
+    size_t head = 1u << 20;       // headroom for the unfinished record of the previous buffer
     size_t rawBytes = 32u << 20;  // raw buffer (MTB_PARSE_BUFFER: tests cut records at buffer ends)
     std::unique_ptr<mtb::ByteSource> src;
     BoundedQueue<std::shared_ptr<ParseJob>> out{32}, work{32};
-    std::thread t;
+    struct Chunk {
+        std::shared_ptr<RawBuf> buf;
+        size_t got = 0;  // bytes at buf->p + head
+        bool eof = false;
+    };
+    BoundedQueue<Chunk> chunks{3};
+    std::shared_ptr<Recycler<RawBuf>> raws = std::make_shared<Recycler<RawBuf>>();
+    std::shared_ptr<Recycler<ParseJob>> jobs = std::make_shared<Recycler<ParseJob>>();
+    std::thread t, reader;
     std::vector<std::thread> parsers;
+    double sourceS = 0, scanS = 0;
+    std::atomic<uint64_t> parseNs{0};
+    std::string readErr;
+
+    void read_loop(ErrorBox* eb) {
+        while (!eb->failed) {
+            Chunk c;
+            c.buf = raws->get([&] { return new RawBuf(head + rawBytes); });
+            const auto r0 = Clock::now();
+            while (c.got < rawBytes) {
+                const long got = src->read(c.buf->p.get() + head + c.got, rawBytes - c.got);
+                if (got < 0) {
+                    readErr = src->err.empty() ? "read error" : src->err;
+                    break;
+                }
+                if (got == 0) {
+                    c.eof = true;
+                    break;
+                }
+                c.got += (size_t)got;
+            }
+            sourceS += secs(r0, Clock::now());
+            const bool last = c.eof;
+            if (!readErr.empty() || !chunks.push(std::move(c)) || last) break;
+        }
+        chunks.close();
+    }
+
     void run(ErrorBox* eb, int nParsers) {
+        reader = std::thread([this, eb] { read_loop(eb); });
         for (int i = 0; i < nParsers; i++)
             parsers.emplace_back([this, eb] {
                 std::shared_ptr<ParseJob> j;
                 while (work.pop(j)) {
+                    const auto p0 = Clock::now();
                     if (!eb->failed) {
                         RecordBlock& b = j->blk;  // a record's sequence is under half its FASTQ bytes
                         b.seq.reserve((j->e - j->b) / 2 + 64);
                         b.off.reserve(j->recs + 1);
                         b.noff.reserve(j->recs + 1);
-                        j->blk.n = mtb::parse_records(j->raw->p.get() + j->b, j->e - j->b, j->blk.seq, j->blk.off,
-                                                      j->blk.names, j->blk.noff, j->err);
+                        b.n = mtb::parse_records(j->raw->p.get() + j->b, j->e - j->b, b.seq, b.off, b.names, b.noff,
+                                                 j->err);
                     }
                     j->raw.reset();
+                    parseNs += (uint64_t)(secs(p0, Clock::now()) * 1e9);
                     j->finish();
                 }
             });
         std::string err;
-        auto buf = std::make_shared<RawBuf>(rawBytes);
-        size_t have = 0;
-        bool eof = false, stopped = false;
-        while (!eb->failed && !stopped) {
-            while (have < buf->cap && !eof) {
-                const long got = src->read(buf->p.get() + have, buf->cap - have);
-                if (got < 0) {
-                    err = src->err.empty() ? "read error" : src->err;
-                    break;
-                }
-                if (got == 0) eof = true;
-                have += (size_t)got;
+        std::shared_ptr<RawBuf> prev;  // holds the unfinished record [pos, end)
+        size_t pos = 0, end = 0;
+        bool stopped = false;
+        Chunk c;
+        while (!eb->failed && !stopped && chunks.pop(c)) {
+            // the unfinished record goes in front of the new bytes: in the headroom, or (a record
+            // longer than the headroom) into a buffer of its own
+            const size_t rest = end - pos;
+            std::shared_ptr<RawBuf> buf;
+            size_t beg;
+            if (rest <= head) {
+                buf = c.buf;
+                beg = head - rest;
+                if (rest) memcpy(buf->p.get() + beg, prev->p.get() + pos, rest);
+            } else {
+                buf = std::make_shared<RawBuf>(rest + c.got + 1);
+                beg = 0;
+                memcpy(buf->p.get(), prev->p.get() + pos, rest);
+                memcpy(buf->p.get() + rest, c.buf->p.get() + head, c.got);
+                c.buf.reset();
             }
-            if (!err.empty()) break;
-            size_t pos = 0;
+            prev.reset();
+            pos = beg;
+            end = beg + rest + c.got;
             while (!stopped) {
                 uint32_t recs = 0;
-                const size_t used = mtb::scan_records(buf->p.get() + pos, have - pos, eof, kBlockReads, &recs, err);
+                const auto s0 = Clock::now();
+                const size_t used = mtb::scan_records(buf->p.get() + pos, end - pos, c.eof, kBlockReads, &recs, err);
+                scanS += secs(s0, Clock::now());
                 if (!err.empty() || recs == 0) {
                     pos += used;  // trailing blank lines at the end of the input
                     break;
                 }
-                auto j = std::make_shared<ParseJob>();
+                auto j = jobs->get([] { return new ParseJob(); });
+                j->reset();
                 j->raw = buf;
                 j->b = pos;
                 j->e = pos + used;
@@ -192,14 +285,13 @@ struct MateReader {
                 }
                 if (recs < kBlockReads) break;  // the buffer ends inside a record (or the input ends)
             }
-            if (!err.empty() || eof) break;
-            // the unfinished record moves to the front of a fresh buffer (grown when it fills half)
-            const size_t rest = have - pos;
-            auto nb = std::make_shared<RawBuf>(rest > buf->cap / 2 ? buf->cap * 2 : buf->cap);
-            memcpy(nb->p.get(), buf->p.get() + pos, rest);
-            buf = nb;
-            have = rest;
+            if (!err.empty() || c.eof) break;
+            prev = buf;
         }
+        prev.reset();
+        chunks.close();  // a stopped splitter releases the reader
+        reader.join();
+        if (err.empty()) err = readErr;
         if (!err.empty()) eb->set(MTB_ERR_IO, err);
         work.close();
         for (auto& p : parsers) p.join();
@@ -330,8 +422,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     const int parseThreads = std::max(2, srcThreads / 2);  // per mate
     {
         std::string err;
-        if (!(m1.src = mtb::open_source(opt->query1, srcThreads, true, err)) ||
-            (paired && !(m2.src = mtb::open_source(opt->query2, srcThreads, true, err)))) {
+        // no prefetch thread: the reader thread of each MateReader reads ahead into recycled buffers
+        if (!(m1.src = mtb::open_source(opt->query1, srcThreads, false, err)) ||
+            (paired && !(m2.src = mtb::open_source(opt->query2, srcThreads, false, err)))) {
             set_error(err);
             return MTB_ERR_IO;
         }
@@ -359,11 +452,15 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     }
     BoundedQueue<Slot*> writeQ(slotMem.size() + 1);
 
-    if (const char* e = getenv("MTB_PARSE_BUFFER")) m1.rawBytes = m2.rawBytes = std::max<size_t>(1, strtoull(e, nullptr, 10));
+    if (const char* e = getenv("MTB_PARSE_BUFFER")) {  // tests: records straddle buffers and outgrow the headroom
+        m1.rawBytes = m2.rawBytes = std::max<size_t>(1, strtoull(e, nullptr, 10));
+        m1.head = m2.head = std::min(m1.head, m1.rawBytes);
+    }
     m1.t = std::thread([&] { m1.run(&eb, parseThreads); });
     if (paired) m2.t = std::thread([&] { m2.run(&eb, parseThreads); });
 
     // assembler: blocks -> pinned batches -> device buffers of context (batch mod n)
+    double fillS = 0, firstBatchS = 0;
     std::thread assembler([&] {
         Cursor c1, c2;
         bool end = false;
@@ -424,6 +521,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 freeQ[d]->push(s);
                 break;
             }
+            const auto f0 = Clock::now();
             // the blocks' stretches are copied into the pinned batch by a few threads at once
             struct Piece {
                 const RecordBlock* b;
@@ -498,6 +596,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 freeQ[d]->push(s);
                 break;
             }
+            fillS += secs(f0, Clock::now());
+            if (index == 0) firstBatchS = secs(t0, Clock::now());
             s->index = index++;
             s->firstRead = firstRead;
             firstRead += s->n;
@@ -706,6 +806,11 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         stats->gpu_s = gpuS;
         stats->input_wait_s = w;
         stats->write_s = writeS;
+        stats->source_s = m1.sourceS + m2.sourceS;
+        stats->scan_s = m1.scanS + m2.scanS;
+        stats->parse_s = (double)(m1.parseNs + m2.parseNs) * 1e-9;
+        stats->fill_s = fillS;
+        stats->first_batch_s = firstBatchS;
     }
     return MTB_OK;
 }

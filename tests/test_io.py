@@ -283,10 +283,10 @@ def test_start_classify_multi(make_db, tmp_path, n_ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("raw", [600, 7001])
+@pytest.mark.parametrize("raw", [150, 600, 7001])
 def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
     """The pipeline's record split (splitter + parse workers): raw buffers of a few hundred bytes cut
-    records at every kind of position, and the two mates (one wrapped, one not) are cut at different
+    records at every kind of position (150: records longer than the buffer's headroom), and the two mates (one wrapped, one not) are cut at different
     reads, so the assembler joins blocks that do not line up. The TSV is the default run's byte for
     byte; unequal mate counts still fail (QueryIndexer.cpp:121-124)."""
     db_dir, taxo, gen = make_db("fmt2")
