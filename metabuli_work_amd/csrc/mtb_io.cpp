@@ -359,7 +359,10 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const uint32_t per = (n + nt - 1) / nt;
     // the formatted parts stay allocated per calling thread: a pipeline's writer reuses warm memory
-    static thread_local std::vector<std::string> part;
+    // (the lambda below runs on other threads: it must reach this thread's vector through a
+    // captured reference, not by the thread_local's name)
+    static thread_local std::vector<std::string> partCache;
+    std::vector<std::string>& part = partCache;
     part.resize(nt);
     for (auto& x : part) x.clear();
     auto work = [&](unsigned t) {
