@@ -24,6 +24,15 @@ struct ByteSource {
 // `threads` blocks at once. With prefetch, a thread of its own keeps the next chunks ready.
 std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bool prefetch, std::string& err);
 
+// Ordinary (non-BGZF) gzip inflated by `threads` workers at once (mtb_gunzip.cpp): the file is
+// cut into chunks of chunkBytes compressed bytes, each decoded from the first block boundary found
+// in it, and checked against the true boundaries, CRC-32 and ISIZE in stream order.
+std::unique_ptr<ByteSource> open_parallel_gzip(const std::string& path, int threads, size_t chunkBytes,
+                                               std::string& err);
+
+// gzip's CRC-32 (libdeflate's folded carry-less multiply when it loads, zlib's otherwise).
+uint32_t crc32_bytes(uint32_t crc, const uint8_t* p, size_t n);
+
 // Buffered line access over a ByteSource.
 struct FastxStream {
     std::unique_ptr<ByteSource> src;

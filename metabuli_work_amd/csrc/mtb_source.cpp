@@ -24,6 +24,7 @@ struct Libdeflate {
     void* (*alloc)() = nullptr;
     void (*free_)(void*) = nullptr;
     int (*gunzip)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    uint32_t (*crc)(uint32_t, const void*, size_t) = nullptr;  // carry-less-multiply CRC-32
     Libdeflate() {
         if (getenv("MTB_NO_LIBDEFLATE")) return;  // A/B and the zlib path's tests
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
@@ -31,6 +32,7 @@ struct Libdeflate {
         alloc = (void* (*)())dlsym(h, "libdeflate_alloc_decompressor");
         free_ = (void (*)(void*))dlsym(h, "libdeflate_free_decompressor");
         gunzip = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(h, "libdeflate_gzip_decompress");
+        crc = (uint32_t(*)(uint32_t, const void*, size_t))dlsym(h, "libdeflate_crc32");
         if (!alloc || !free_ || !gunzip) alloc = nullptr;
     }
     bool ok() const { return alloc != nullptr; }
@@ -361,6 +363,12 @@ struct PrefetchSource : ByteSource {
 
 }  // namespace
 
+uint32_t crc32_bytes(uint32_t crc, const uint8_t* p, size_t n) {
+    const Libdeflate& ld = libdeflate();
+    if (ld.crc) return ld.crc(crc, p, n);
+    return (uint32_t)crc32_z(crc, p, n);
+}
+
 std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bool prefetch, std::string& err) {
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) {
@@ -385,6 +393,17 @@ std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bo
         return b;  // the pool reads ahead already
     }
     if (gz) {
+        // a file of several chunks with threads to spare inflates in parallel (MTB_GZ_SERIAL: the
+        // one-thread zlib path; MTB_GZ_CHUNK: the chunk size, tests)
+        const char* gzChunk = getenv("MTB_GZ_CHUNK");
+        const size_t chunk = gzChunk ? strtoull(gzChunk, nullptr, 10) : (1u << 20);
+        fseek(f, 0, SEEK_END);
+        const long size = ftell(f);
+        rewind(f);
+        if (threads >= 2 && !getenv("MTB_GZ_SERIAL") && size > 0 && (size_t)size >= 4 * chunk) {
+            fclose(f);
+            return open_parallel_gzip(path, threads, chunk, err);
+        }
         auto g = std::make_unique<GzSource>(gzBuf ? strtoull(gzBuf, nullptr, 10) : (4u << 20));
         g->f = f;
         if (inflateInit2(&g->zs, 15 + 32) != Z_OK) {

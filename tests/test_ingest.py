@@ -1,7 +1,11 @@
-"""The pipeline's parallel record split (scan_records + parse_records, mtb_pipeline.cpp MateReader)
-against the serial record reader (next_record, kseq semantics, KmerExtractor.cpp:442-494): the same
-records, names and errors for wrapped / CRLF / blank-line / truncated inputs, cut at raw buffer
-sizes down to a few bytes so records straddle buffer ends (tools/ingest_check.cpp; CPU only)."""
+"""Host ingest on the CPU:
+* the pipeline's parallel record split (scan_records + parse_records, mtb_pipeline.cpp MateReader)
+  against the serial record reader (next_record, kseq semantics, KmerExtractor.cpp:442-494): the
+  same records, names and errors for wrapped / CRLF / blank-line / truncated inputs, cut at raw
+  buffer sizes down to a few bytes so records straddle buffer ends (tools/ingest_check.cpp);
+* the parallel gzip inflate (mtb_gunzip.cpp) against Python's zlib and the one-thread zlib source,
+  byte for byte: compression levels 0/1/9, several members, empty members, trailing garbage,
+  truncation anywhere, CRC-32 / ISIZE errors, chunks down to 4 KB (tools/gunzip_check.cpp)."""
 import os
 import pathlib
 import subprocess
@@ -21,6 +25,16 @@ def checker(tmp_path_factory):
         pytest.skip("libmtbgpu.so not built")
     exe = tmp_path_factory.mktemp("ingest") / "ingest_check"
     subprocess.run(["g++", "-O1", "-std=c++17", "-o", str(exe), str(ROOT / "tools" / "ingest_check.cpp"),
+                    f"-L{LIB}", "-lmtbgpu", f"-Wl,-rpath,{LIB}"], check=True, capture_output=True)
+    return exe
+
+
+@pytest.fixture(scope="module")
+def gunzip(tmp_path_factory):
+    if not (LIB / "libmtbgpu.so").exists():
+        pytest.skip("libmtbgpu.so not built")
+    exe = tmp_path_factory.mktemp("gunzip") / "gunzip_check"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", str(exe), str(ROOT / "tools" / "gunzip_check.cpp"),
                     f"-L{LIB}", "-lmtbgpu", f"-Wl,-rpath,{LIB}"], check=True, capture_output=True)
     return exe
 
@@ -105,3 +119,60 @@ def test_split_errors_match(checker, tmp_path, text, msg, buf):
     p.write_bytes(text.encode())
     rc, out = _run(checker, p, buf, 1)
     assert rc == 0 and "same=1" in out and f'err="{msg}"' in out, out
+
+
+def _gz(data, level=6):
+    import zlib
+    c = zlib.compressobj(level, zlib.DEFLATED, 31)
+    return c.compress(data) + c.flush()
+
+
+@pytest.fixture(scope="module")
+def fastq_bytes():
+    rng = np.random.default_rng(11)
+    return _fastq(rng, 6000, wrap=0).encode() + _fastq(rng, 2000, wrap=9).encode()
+
+
+def _gz_cases(b):
+    g = _gz(b, 1)
+    bad_crc, bad_len = bytearray(g), bytearray(g)
+    bad_crc[-6] ^= 1
+    bad_len[-2] ^= 1
+    empty = _gz(b"")
+    third = len(b) // 3
+    return {
+        "level0": _gz(b, 0), "level1": g, "level9": _gz(b, 9),
+        "members": _gz(b[:third], 1) + _gz(b[third:2 * third], 9) + _gz(b[2 * third:], 6),
+        "empty_members": empty + g + empty + empty,
+        "garbage_after": g + b"\x00\x01 not gzip",
+        "truncated_mid": g[:len(g) // 2 + 777],
+        "truncated_trailer": g[:-3],
+        "truncated_at_trailer": g[:-8],
+        "bad_crc": bytes(bad_crc), "bad_isize": bytes(bad_len),
+    }
+
+
+@pytest.mark.parametrize("chunk,threads", [(4096, 3), (65536, 2), (1 << 20, 4)])
+def test_parallel_gunzip_matches_zlib(gunzip, tmp_path, fastq_bytes, chunk, threads):
+    import zlib
+    for name, data in _gz_cases(fastq_bytes).items():
+        p = tmp_path / f"{name}.gz"
+        p.write_bytes(data)
+        got = {}
+        for mode in ("par", "ser"):
+            out = tmp_path / f"{name}.{mode}"
+            env = dict(os.environ, SERIAL="1") if mode == "ser" else None
+            r = subprocess.run([str(gunzip), str(p), str(threads), str(chunk), str(out)], capture_output=True,
+                               text=True, timeout=120, env=env)
+            got[mode] = (r.stdout.strip(), out.read_bytes())
+        assert got["par"] == got["ser"], (name, got["par"][0], got["ser"][0])
+        if name.startswith("bad"):
+            assert "rc=-1" in got["par"][0] and "check" in got["par"][0], (name, got["par"][0])
+        elif not name.startswith("truncated"):
+            d = zlib.decompressobj(31)
+            want, rest = b"", data
+            while rest[:2] == b"\x1f\x8b":  # members in sequence, as gzip.decompress (without its garbage check)
+                d = zlib.decompressobj(31)
+                want += d.decompress(rest)
+                rest = d.unused_data
+            assert got["par"][1] == want, name

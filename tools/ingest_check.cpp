@@ -45,17 +45,23 @@ int main(int argc, char** argv) {
     const double serialS = secs(t0);
     // the whole decompressed input in memory, then cut and parsed as the pipeline does
     std::string all;
+    const int srcThreads = getenv("INGEST_THREADS") ? atoi(getenv("INGEST_THREADS")) : 4;
+    auto ts = Clock::now();
     {
         std::string e;
-        auto src = mtb::open_source(argv[1], 4, true, e);
+        // INGEST_PGZ=<chunk bytes>: the parallel gzip source at any thread count (timing)
+        auto src = getenv("INGEST_PGZ") ? mtb::open_parallel_gzip(argv[1], srcThreads, strtoull(getenv("INGEST_PGZ"), nullptr, 10), e)
+                                        : mtb::open_source(argv[1], srcThreads, true, e);
         if (!src) {
             printf("open failed: %s\n", e.c_str());
             return 1;
         }
         std::vector<char> tmp(1u << 24);
         long got;
+        all.reserve(1u << 28);
         while ((got = src->read(tmp.data(), tmp.size())) > 0) all.append(tmp.data(), (size_t)got);
     }
+    const double sourceS = secs(ts);
     Out b;
     double scanS = 0, parseS = 0;
     size_t fed = 0;  // bytes of `all` moved into buffers so far
@@ -101,7 +107,7 @@ int main(int argc, char** argv) {
     a.names.resize(a.noff.back());
     a.seq.resize(a.off.back());
     const bool same = a.seq == b.seq && a.names == b.names && a.off == b.off && a.noff == b.noff && a.err == b.err;
-    printf("records=%zu bytes=%zu serial_s=%.4f scan_s=%.4f parse_s=%.4f same=%d err=\"%s\" err2=\"%s\"\n",
-           a.off.size() - 1, all.size(), serialS, scanS, parseS, same ? 1 : 0, a.err.c_str(), b.err.c_str());
+    printf("records=%zu bytes=%zu serial_s=%.4f source_s=%.4f scan_s=%.4f parse_s=%.4f same=%d err=\"%s\" err2=\"%s\"\n",
+           a.off.size() - 1, all.size(), serialS, sourceS, scanS, parseS, same ? 1 : 0, a.err.c_str(), b.err.c_str());
     return same ? 0 : 3;
 }
