@@ -243,7 +243,7 @@ def main():
                     help="read pairs of each variant line timed on the oracle (parity sample)")
     ap.add_argument("--e2e-pairs", type=int, default=10_000_000,
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
-    ap.add_argument("--e2e-gzip-pairs", type=int, default=1_000_000,
+    ap.add_argument("--e2e-gzip-pairs", type=int, default=10_000_000,
                     help="config 3 file -> TSV line: read pairs written as single-member gzip FASTQ (0 = off)")
     ap.add_argument("--em-pairs", type=int, default=10_000_000,
                     help="config 3 --em line: read pairs classified with em and reassigned (0 = off)")

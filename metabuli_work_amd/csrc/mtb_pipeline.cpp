@@ -352,8 +352,8 @@ struct Slot {
     uint64_t bases = 0;
     DevMem dseq1, dseq2, doff1, doff2;
     hipEvent_t uploaded = nullptr;
-    std::vector<mtb_result> res;
-    std::vector<mtb_taxcnt> tc;
+    Pinned<mtb_result> res;  // pinned: the device-to-host copies run at full PCIe rate
+    Pinned<mtb_taxcnt> tc;
 };
 
 // Reads of one mate's current block, consumed from `at`.
@@ -630,17 +630,18 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 }
                 const auto g0 = Clock::now();
                 int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
-                s->res.resize(s->n);
+                if (s->res.ensure(std::max<uint32_t>(s->n, 1)) != hipSuccess) rc = MTB_ERR_OOM;
                 if (rc == MTB_OK)
                     rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
                                             paired ? (const char*)s->dseq2.p : nullptr,
                                             paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
-                                            s->res.data());
+                                            s->res.p);
                 uint64_t nt = 0;
                 if (rc == MTB_OK) {
                     mtb_get_taxcnt(c, nullptr, 0, &nt);
-                    s->tc.resize(std::max<uint64_t>(nt, 1));
-                    rc = mtb_get_taxcnt(c, s->tc.data(), s->tc.size(), &nt);
+                    rc = s->tc.ensure(std::max<uint64_t>(nt, 1)) == hipSuccess
+                             ? mtb_get_taxcnt(c, s->tc.p, s->tc.cap, &nt)
+                             : MTB_ERR_OOM;
                 }
                 if (rc == MTB_OK && em) {
                     if (s->firstRead + s->n > 0xFFFFFFFFull) {
@@ -688,12 +689,12 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     b.n_reads = s->n;
                     b.names = s->names.data();
                     b.name_off = s->noff.data();
-                    if (mtb_write_classifications(ctx0, opt->out_tsv, first ? 0 : 1, &b, s->res.data(), s->tc.data(),
+                    if (mtb_write_classifications(ctx0, opt->out_tsv, first ? 0 : 1, &b, s->res.p, s->tc.p,
                                                   opt->write_flags) != MTB_OK)
                         eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
                     first = false;
                     for (uint32_t i = 0; i < s->n; i++) {  // ++taxCounts[classification] (Classifier.cpp:201-203)
-                        const int32_t t = s->res[i].is_classified ? s->res[i].classification : 0;
+                        const int32_t t = s->res.p[i].is_classified ? s->res.p[i].classification : 0;
                         if (t >= 0 && t < (1 << 26)) {  // internal taxIDs are dense: a flat table
                             if ((size_t)t >= denseCounts.size()) denseCounts.resize((size_t)t * 2 + 1024, 0);
                             denseCounts[t]++;

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import struct
 from typing import List, Optional
 
 import numpy as np
@@ -454,12 +455,24 @@ def write_compressed(path: str, data: bytes, mode: str = "bgzf", level: int = 1,
             f.write(data)
         return
     if mode == "gzip":
-        with open(path, "wb") as f:
-            c = zlib.compressobj(level, zlib.DEFLATED, 31)
-            mv = memoryview(data)
-            for i in range(0, len(data), 1 << 24):
-                f.write(c.compress(mv[i:i + (1 << 24)]))
-            f.write(c.flush())
+        # one gzip member, its deflate stream compressed in 64 MB segments by a thread pool (as pigz
+        # does: each segment ends with a sync flush, the last one finishes the stream)
+        seg = 1 << 26
+        mv = memoryview(data)
+        starts = list(range(0, len(data), seg)) or [0]
+
+        def deflate(i):
+            c = zlib.compressobj(level, zlib.DEFLATED, -15)
+            out = c.compress(mv[i:i + seg])
+            return out + c.flush(zlib.Z_FINISH if i == starts[-1] else zlib.Z_SYNC_FLUSH)
+        with ThreadPoolExecutor(threads) as ex, open(path, "wb") as f:
+            f.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\xff")  # no flags, no mtime, OS unknown
+            for part in ex.map(deflate, starts):
+                f.write(part)
+            crc = 0
+            for i in range(0, len(data), seg):
+                crc = zlib.crc32(mv[i:i + seg], crc)
+            f.write(struct.pack("<II", crc & 0xFFFFFFFF, len(data) & 0xFFFFFFFF))
         return
     blk = 65280
     mv = memoryview(data)
