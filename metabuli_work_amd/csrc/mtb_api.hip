@@ -81,7 +81,7 @@ struct mtb_ctx {
     bool forceGeneric = false;   // MTB_FORCE_GENERIC=1: fast paths off, fallbacks only (tests)
     bool segsortGlobal = false;  // MTB_SEGSORT_GLOBAL=1: every K5 segment through global scratch (tests)
     uint32_t mergeSeg = 0;       // MTB_MERGE_SEG=<n>: K5 merge path above n matches (tests; default 8192)
-    int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1: K6 chooseBestTaxon thread / wave per read (tests; default auto)
+    int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1/2: K6 chooseBestTaxon thread / wave / 16-lane group per read (default auto)
     int emulateAll = 0;          // MTB_EMULATE_SORT=1: k_combine_wave emulates std::sort for every run (tests)
     bool pruneCompact = true;    // MTB_PRUNE_COMPACT=0: big K5 segments are not thinned before their sort (tests)
     int32_t* spOf = nullptr;
@@ -246,6 +246,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->rankLo = ((uint64_t)ends[0].hi << 32 | ends[0].lo) >> 24;
         c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
+    if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e) != 0);  // A/B only: invalid results
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix
@@ -259,7 +260,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     if (const char* e = getenv("MTB_SEGSORT_GLOBAL")) c->segsortGlobal = atoi(e) != 0;
     if (const char* e = getenv("MTB_MERGE_SEG")) c->mergeSeg = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("MTB_WAVE_TAXON")) c->waveTaxon = atoi(e) == 2 ? 2 : atoi(e) ? 1 : 0;
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
     if (const char* e = getenv("MTB_BIG_GROUPS")) c->bigGroups = atoi(e) != 0;
     if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;

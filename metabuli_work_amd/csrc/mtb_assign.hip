@@ -2460,6 +2460,219 @@ __global__ void __launch_bounds__(64) k_choose_taxon_wave(const mtb_match* __res
     results[r] = res;
 }
 
+// The same for short reads with kGroupLanes lanes per read (16 reads per 256-thread block): the
+// species-run scan, the tie set and filterRedundantMatches' per-quotient reduction as in the wave
+// kernel, on a 16-lane group with per-group LDS tables (kGroupQ quotients, kGroupHash taxa); the
+// group's first lane runs the tail. A read whose quotients or taxa do not fit takes the serial
+// filter on that lane. Block-wide barriers order the LDS phases (every thread reaches them).
+constexpr int kGroupLanes = 16;
+constexpr int kGroupQ = 128;    // quotients of a read (a 2 x 150 bp pair at dnaShift 3: 101)
+constexpr int kGroupHash = 64;  // distinct taxa of one read's taxCnt
+
+__device__ __forceinline__ float group_max_f(float x) {
+#pragma unroll
+    for (int d = kGroupLanes / 2; d > 0; d >>= 1) x = fmaxf(x, __shfl_xor(x, d, kGroupLanes));
+    return x;
+}
+__device__ __forceinline__ long group_sum_l(long x) {
+#pragma unroll
+    for (int d = kGroupLanes / 2; d > 0; d >>= 1) x += __shfl_xor(x, d, kGroupLanes);
+    return x;
+}
+
+__global__ void __launch_bounds__(256) k_choose_taxon_group(const mtb_match* __restrict__ M,
+                                                            const uint64_t* __restrict__ mOff,
+                                                            const uint32_t* __restrict__ qlen, uint32_t nReads,
+                                                            const uint64_t* __restrict__ sScan,
+                                                            const uint64_t* __restrict__ sStart,
+                                                            const uint64_t* __restrict__ gScan,
+                                                            const uint64_t* __restrict__ gStart,
+                                                            const float* __restrict__ spScore,
+                                                            const uint8_t* __restrict__ spKeep, AssignCfg cfg,
+                                                            TaxView tax, Clade* __restrict__ cladeP,
+                                                            uint32_t cladePerMatch, mtb_taxcnt* __restrict__ tcP,
+                                                            mtb_result* __restrict__ results) {
+    constexpr int kGroups = 256 / kGroupLanes;
+    __shared__ uint32_t qw[kGroups][kGroupQ];  // min hamming << 24 | LCA of the taxa at it (as the wave kernel)
+    __shared__ int32_t hk[kGroups][kGroupHash];
+    __shared__ uint32_t hc[kGroups][kGroupHash];
+    __shared__ int gFlag[kGroups];
+    const int g = threadIdx.x / kGroupLanes, gl = threadIdx.x % kGroupLanes;
+    const int gLane0 = (threadIdx.x & 63) & ~(kGroupLanes - 1);  // the group's first lane in its wave
+    const uint32_t r = blockIdx.x * kGroups + g;
+    const bool valid = r < nReads;
+    const uint64_t base = valid ? mOff[r] : 0;
+    const long n = valid ? (long)(mOff[r + 1] - base) : 0;
+    const int readLength = valid ? (int)qlen[r] : 0;
+    mtb_result res = empty_result(readLength);
+    float spTotal = 0.0f;
+    int32_t bestTax = 0;
+    bool isLCA = false, filter = false;
+    uint64_t bestFirst = 0, bestSecond = 0;
+    if (n > 0) {
+        const uint64_t s0 = sScan[base], s1 = sScan[base + n];
+        long meaningful = 0;
+        float bestSpScore = 0.0f;
+        for (uint64_t s = s0 + gl; s < s1; s += kGroupLanes) {
+            if (!spKeep[s]) continue;
+            const float score = spScore[s];
+            meaningful += score > 0.f;
+            bestSpScore = fmaxf(bestSpScore, score);
+        }
+        meaningful = group_sum_l(meaningful);
+        bestSpScore = group_max_f(bestSpScore);
+        if (meaningful > 0) {
+            for (uint64_t c = s0; c < s1; c += kGroupLanes) {  // the first species run at the maximum
+                const uint64_t s = c + gl;
+                const bool hit = s < s1 && spKeep[s] && spScore[s] == bestSpScore;
+                const uint32_t m = (uint32_t)(__ballot(hit) >> gLane0) & 0xFFFFu;
+                if (m) {
+                    const uint64_t sb = c + (uint64_t)(__ffs((int)m) - 1);
+                    bestFirst = sStart[sb];
+                    bestSecond = sStart[sb + 1];
+                    break;
+                }
+            }
+            const float thr = bestSpScore * cfg.tieRatio;  // the tie set in species order
+            long cnt = 0;
+            int lcaNode = -1;
+            for (uint64_t c = s0; c < s1; c += kGroupLanes) {
+                const uint64_t s = c + gl;
+                const bool in = s < s1 && spKeep[s] && spScore[s] >= thr;
+                const float sc = in ? spScore[s] : 0.0f;
+                const int32_t sp = in ? (int32_t)M[sStart[s]].species_id : 0;
+                uint32_t m = (uint32_t)(__ballot(in) >> gLane0) & 0xFFFFu;
+                while (m) {
+                    const int b = __ffs((int)m) - 1;
+                    m &= m - 1;
+                    const float v = __shfl(sc, b, kGroupLanes);
+                    const int32_t t = __shfl(sp, b, kGroupLanes);
+                    cnt++;
+                    spTotal += v;
+                    if (cnt == 1) bestTax = t;
+                    if (tax.exists(t)) lcaNode = lcaNode < 0 ? tax.nodeOf[t] : tax.lca_node(lcaNode, tax.nodeOf[t]);
+                }
+            }
+            if (cnt > 1) {
+                isLCA = true;
+                bestTax = lcaNode >= 0 ? tax.nodeTax[lcaNode] : 0;
+                spTotal = spTotal / (float)cnt;
+            }
+        }
+        filter = !(spTotal == 0 || spTotal < cfg.minScore || isLCA);
+    }
+    // filterRedundantMatches over the best species' matches, in the group's LDS tables
+    const uint32_t dnaShift = (uint32_t)cfg.dnaShift;
+    const long maxQ = (readLength + 3) / (long)dnaShift;
+    const long nb = (long)(bestSecond - bestFirst);
+    const mtb_match* B = M + bestFirst;
+    const bool lds = filter && maxQ < kGroupQ && tax.maxTax < 0xFFFFFF;
+    if (lds) {
+        for (long q = gl; q <= maxQ; q += kGroupLanes) qw[g][q] = 0xFFFFFFFFu;
+        for (int k = gl; k < kGroupHash; k += kGroupLanes) {
+            hk[g][k] = 0;
+            hc[g][k] = 0;
+        }
+        if (gl == 0) gFlag[g] = 0;
+    }
+    __syncthreads();
+    if (lds) {
+        for (long i = gl; i < nb; i += kGroupLanes) {
+            const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
+            if (q > (uint32_t)maxQ || B[i].hamming > 254u) {
+                gFlag[g] = 1;
+                continue;
+            }
+            atomicMin(&qw[g][q], (uint32_t)B[i].hamming << 24 | 0xFFFFFFu);
+        }
+    }
+    __syncthreads();
+    const bool ok = lds && !gFlag[g];
+    if (ok) {
+        for (long i = gl; i < nb; i += kGroupLanes) {
+            const uint32_t q = info_pos(B[i].qinfo) / dnaShift;
+            const uint32_t h = (uint32_t)B[i].hamming << 24;
+            uint32_t old = qw[g][q];
+            if ((old & 0xFF000000u) != h) continue;
+            const int32_t t = (int32_t)B[i].target_id;
+            while (true) {  // taxon part = LCA(taxon part, t), 0xFFFFFF = empty
+                const uint32_t cur = old & 0xFFFFFFu;
+                const uint32_t nv = h | (uint32_t)(cur == 0xFFFFFFu ? t : tax.lca((int32_t)cur, t));
+                if (nv == old) break;
+                const uint32_t prev = atomicCAS(&qw[g][q], old, nv);
+                if (prev == old) break;
+                old = prev;
+            }
+        }
+    }
+    __syncthreads();
+    if (ok) {
+        for (long q = gl; q <= maxQ; q += kGroupLanes) {
+            const uint32_t wq = qw[g][q];
+            const int32_t t = wq == 0xFFFFFFFFu ? 0 : (int32_t)(wq & 0xFFFFFFu);
+            if (t == 0) continue;
+            uint32_t h = ((uint32_t)t * 2654435761u) & (kGroupHash - 1);
+            int probes = 0;
+            while (true) {
+                const int32_t prev = atomicCAS(&hk[g][h], 0, t);
+                if (prev == 0 || prev == t) {
+                    atomicAdd(&hc[g][h], 1u);
+                    break;
+                }
+                h = (h + 1) & (kGroupHash - 1);
+                if (++probes == kGroupHash) {
+                    gFlag[g] = 1;
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    mtb_taxcnt* tc = tcP + base;  // capacity n
+    long nTc = -1;                // -1: the serial filter
+    if (ok && !gFlag[g]) {        // entries out in slot order (std::map order on the first lane below)
+        long at = 0;
+        for (int k0 = 0; k0 < kGroupHash; k0 += kGroupLanes) {
+            const int k = k0 + gl;
+            const bool v = hk[g][k] != 0;
+            const uint32_t m = (uint32_t)(__ballot(v) >> gLane0) & 0xFFFFu;
+            if (v) {
+                const long p = at + (long)__popc(m & ((1u << gl) - 1));
+                tc[p].tax_id = hk[g][k];
+                tc[p].count = hc[g][k];
+            }
+            at += (long)__popc(m);
+        }
+        nTc = at;
+    }
+    if (gl != 0 || !valid) return;
+    if (!filter) {
+        res.score = spTotal;
+        if (isLCA && n > 0 && !(spTotal == 0 || spTotal < cfg.minScore)) {
+            res.is_classified = 1;
+            res.classification = bestTax;
+        }
+        results[r] = res;
+        return;
+    }
+    if (nTc < 0) {
+        nTc = filter_redundant_serial(M, bestFirst, bestSecond, gScan, gStart, dnaShift, tax, tc);
+    } else {
+        for (long a = 1; a < nTc; a++) {
+            mtb_taxcnt v = tc[a];
+            long b = a;
+            while (b > 0 && tc[b - 1].tax_id > v.tax_id) {
+                tc[b] = tc[b - 1];
+                b--;
+            }
+            tc[b] = v;
+        }
+    }
+    classify_tail(res, tc, nTc, spTotal, bestTax, readLength, cfg, tax, cladeP + base * cladePerMatch,
+                  n * (long)cladePerMatch);
+    results[r] = res;
+}
+
 // Longest-first orders for the wave kernels (a wave kernel's time is otherwise set by its longest
 // waves, started last): keys = a size bound minus the size, a stable LSD radix sort of the indices.
 __global__ void k_wave_size_keys(const uint64_t* __restrict__ waveList, uint32_t n, uint64_t* __restrict__ keys) {
@@ -2544,7 +2757,11 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     // one thread per read, or one wave per read when reads carry many matches (long reads: a
     // thread per read would leave most SIMDs idle and serialise each read's best-species scan)
     const bool wave = a.waveTaxon >= 0 ? a.waveTaxon == 1 : (!a.generic && nM > (uint64_t)kWavePerReadMatches * nReads);
-    if (wave) {
+    if (a.waveTaxon == 2) {  // a 16-lane group per read (MTB_WAVE_TAXON=2)
+        k_choose_taxon_group<<<(nReads + 15) / 16, 256, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
+                                                                 s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
+                                                                 (Clade*)s.clade, s.cladePerMatch, tcPool, results);
+    } else if (wave) {
         k_read_size_keys<<<(nReads + 255) / 256, 256, 0, st>>>(mOff, nReads, s.ordKA);
         const uint64_t* order = longest_first(nReads, 24, s, st);
         k_choose_taxon_wave<<<nReads, 64, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart, s.gScan, s.gStart,

@@ -1171,6 +1171,13 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // kStageRegions), so the claims do not all queue on one address. A later pass moves each match
 // into its read's segment (k_match_transpose). A region that would overflow is not written; the
 // caller grows the regions to the largest count and reruns.
+// A/B only (MTB_AB_RANK_FREE): k_match takes a query's rank in its read's segment
+// without the readCnt atomic (a wrong rank: the results are invalid), bounding what any scheme
+// that removes the atomic could save in the join.
+__device__ int g_abRankFree = 0;
+
+void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int)); }
+
 template <bool kStage, int kPer>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
@@ -1321,6 +1328,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int j = 0; j < kPer; j++) longq[j] = longList && direct && !kStage && live[j] && hi[j] - lo[j] > kLongRun;
     uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
+    const int abFree = g_abRankFree;
     HamRows hr[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
@@ -1340,7 +1348,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         }
         info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
         // the returned count is the query's first rank inside its read's segment
-        rk[j] = c[j] ? atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]) : 0;
+        rk[j] = !c[j] ? 0 : abFree ? (slot[j] & 7u) : atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
     }
     int hit = 0;

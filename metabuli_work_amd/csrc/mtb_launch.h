@@ -33,7 +33,7 @@ struct AssignArgs {
     int kmerFormat, dnaShift, maxCodonShift, denominator, minConsCnt, minConsCntEuk, accessionLevel;
     float minScore, minSpScore, tieRatio;
     int generic;  // MTB_FORCE_GENERIC: general code paths only (parity tests of the fallbacks)
-    int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread per read, 1 wave per read (K6 chooseBestTaxon)
+    int waveTaxon = -1;  // MTB_WAVE_TAXON: -1 auto, 0 thread, 1 wave, 2 16-lane group per read (K6 chooseBestTaxon)
     int emulateAll = 0;  // MTB_EMULATE_SORT=1: every k_combine_wave run takes the std::sort emulation (tests)
     int em = 0;          // --em: classified reads keep their best species; mappings for the EM
     int bigGroups = 1;   // MTB_BIG_GROUPS=0: every (species, frame) group on a thread (A/B, tests)
@@ -213,6 +213,8 @@ constexpr uint32_t kStageRegions = 256;
 // qslot: each query's K1 slot (its info is slot_info(slot, C, unitInfo))
 // A direct-join query whose AA run is longer than kLongRun (mtb_kernels.hip) is deferred to the
 // long-run list and scanned by a wave of its own (launch_match_long).
+void set_ab_rank_free(int on);  // A/B only: k_match without the per-read rank atomic (invalid results)
+
 struct LongRun {
     uint64_t q;       // index into the sorted query arrays
     uint64_t lo, hi;  // its DB run

@@ -269,11 +269,12 @@ def test_join_paths(make_db, db_name, kind, join, monkeypatch):
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt1", "long"),
                                           ("fmt2_syncmer", "long"), ("fmt2_syncmer", "paired"), ("fmt2", "verylong"),
                                           ("fmt1", "verylong")])
-@pytest.mark.parametrize("wave", ["0", "1", "1:emu"])
+@pytest.mark.parametrize("wave", ["0", "1", "1:emu", "2"])
 def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
-    """K6's chooseBestTaxon both ways — a thread per read (short reads) and a wave per read (long
-    reads: parallel species scan, per-quotient LDS reduction for filterRedundantMatches) — forced
-    on every read kind with MTB_WAVE_TAXON, against the oracle; and k_combine_wave's libstdc++
+    """K6's chooseBestTaxon every way — a thread per read (short reads), a wave per read (long
+    reads: parallel species scan, per-quotient LDS reduction for filterRedundantMatches) and a
+    16-lane group per read (the same reductions per group; reads past its LDS tables take the
+    serial filter) — forced on every read kind with MTB_WAVE_TAXON, against the oracle; and k_combine_wave's libstdc++
     introsort emulation forced for every run it takes (MTB_EMULATE_SORT). "verylong": reads of
     12-20 kb, whose quotients take several LDS windows in the wave kernel."""
     wave, _, emu = wave.partition(":")
