@@ -2754,10 +2754,14 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
     } else {
         hipMemsetAsync(s.sScan, 0, sizeof(uint64_t), st);
     }
-    // one thread per read, or one wave per read when reads carry many matches (long reads: a
-    // thread per read would leave most SIMDs idle and serialise each read's best-species scan)
+    // a wave per read when reads carry many matches (long reads: a thread per read would leave most
+    // SIMDs idle and serialise each read's best-species scan), else a 16-lane group per read (a
+    // thread per read with MTB_WAVE_TAXON=0, or under MTB_FORCE_GENERIC)
     const bool wave = a.waveTaxon >= 0 ? a.waveTaxon == 1 : (!a.generic && nM > (uint64_t)kWavePerReadMatches * nReads);
-    if (a.waveTaxon == 2) {  // a 16-lane group per read (MTB_WAVE_TAXON=2)
+    // short reads: a 16-lane group per read by default (config 3: 1.78 -> 1.09 ms, 10.4 -> 2.5 GB
+    // fetched per batch against a thread per read; profiles/r03/ab_k6_group.json)
+    const bool group = a.waveTaxon == 2 || (a.waveTaxon < 0 && !wave && !a.generic);
+    if (group) {
         k_choose_taxon_group<<<(nReads + 15) / 16, 256, 0, st>>>(matches, mOff, qlen, nReads, s.sScan, s.sStart,
                                                                  s.gScan, s.gStart, s.spScore, s.spKeep, cfg, tv,
                                                                  (Clade*)s.clade, s.cladePerMatch, tcPool, results);
