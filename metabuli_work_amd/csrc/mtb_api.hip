@@ -246,7 +246,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->rankLo = ((uint64_t)ends[0].hi << 32 | ends[0].lo) >> 24;
         c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
-    if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e) != 0);  // A/B only: invalid results
+    if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e));  // A/B only: invalid results
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix

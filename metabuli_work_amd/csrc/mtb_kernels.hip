@@ -1173,7 +1173,7 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // caller grows the regions to the largest count and reruns.
 // A/B only (MTB_AB_RANK_FREE): k_match takes a query's rank in its read's segment
 // without the readCnt atomic (a wrong rank: the results are invalid), bounding what any scheme
-// that removes the atomic could save in the join.
+// that removes the atomic could save in the join; 2: nor the read's stretch bounds (dirOff).
 __device__ int g_abRankFree = 0;
 
 void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int)); }
@@ -1382,7 +1382,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         for (int j = 0; j < kPer; j++) {
             if (!c[j]) continue;
             const uint32_t r = info_seq(info[j]) - 1;
-            const uint64_t o = dirOff[r] * C, cap = (dirOff[r + 1] * C - o) >> capShift;
+            const uint64_t o = abFree == 2 ? 0 : dirOff[r] * C;
+            const uint64_t cap = abFree == 2 ? (1u << 20) : (dirOff[r + 1] * C - o) >> capShift;
             if (rk[j] + c[j] > cap) {
                 const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c[j]);
                 if (sp + c[j] > region) {

@@ -5,6 +5,7 @@
 #   k6group   K6 chooseBestTaxon on a 16-lane group per read (MTB_WAVE_TAXON=2) instead of a thread
 #   rankfree  K4 without the per-read rank atomic (MTB_AB_RANK_FREE=1: ranks are wrong and the results
 #             invalid; an upper bound of what removing the atomic can save in the join)
+#   dirfree   nor the read's stretch bounds (MTB_AB_RANK_FREE=2: no dirOff reads; invalid results)
 # Usage: tools/ab_r03.sh [variant ...]. Output: gpurun_out/r03/ab/<variant>/ab.json
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -15,6 +16,7 @@ declare -A ENVS
 ENVS[base]="MTB_AB_NONE=1"
 ENVS[k6group]="MTB_WAVE_TAXON=2"
 ENVS[rankfree]="MTB_AB_RANK_FREE=1"
+ENVS[dirfree]="MTB_AB_RANK_FREE=2"
 for v in ${@:-base k6group rankfree}; do
   D=$O/$v
   mkdir -p $D
