@@ -605,8 +605,15 @@ struct ParallelGzSource : ByteSource {
 
     void start() {
         nChunks = (n + chunkBytes - 1) / chunkBytes;
-        for (int i = 0; i < nThreads; i++) workers.emplace_back([this] { work(); });
-        coord = std::thread([this] { coordinate(); });
+        for (int i = 0; i < nThreads; i++)
+            workers.emplace_back([this] {
+                background_thread();
+                work();
+            });
+        coord = std::thread([this] {
+            background_thread();
+            coordinate();
+        });
     }
 
     void queue_decodes(uint64_t upTo) {  // holds mu

@@ -356,7 +356,8 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
         fputs(lineage ? "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage\ttaxID:match_count\n"
                       : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n", f);
     if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
-    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // 8 threads format ~1M lines in a few ms; more would take cores from the input threads
+    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     const uint32_t per = (n + nt - 1) / nt;
     // the formatted parts stay allocated per calling thread: a pipeline's writer reuses warm memory
     // (the lambda below runs on other threads: it must reach this thread's vector through a

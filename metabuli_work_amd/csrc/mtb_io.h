@@ -30,6 +30,11 @@ std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bo
 std::unique_ptr<ByteSource> open_parallel_gzip(const std::string& path, int threads, size_t chunkBytes,
                                                std::string& err);
 
+// Helper threads of the input path (inflate, read-ahead, record split, parse, batch fill) run one
+// nice level below the caller's threads, so the threads that feed and drain the GPU are scheduled
+// first when the host's cores are all busy.
+void background_thread();
+
 // gzip's CRC-32 (libdeflate's folded carry-less multiply when it loads, zlib's otherwise).
 uint32_t crc32_bytes(uint32_t crc, const uint8_t* p, size_t n);
 

@@ -216,9 +216,14 @@ struct MateReader {
     }
 
     void run(ErrorBox* eb, int nParsers) {
-        reader = std::thread([this, eb] { read_loop(eb); });
+        mtb::background_thread();  // the splitter
+        reader = std::thread([this, eb] {
+            mtb::background_thread();
+            read_loop(eb);
+        });
         for (int i = 0; i < nParsers; i++)
             parsers.emplace_back([this, eb] {
+                mtb::background_thread();
                 std::shared_ptr<ParseJob> j;
                 while (work.pop(j)) {
                     const auto p0 = Clock::now();
@@ -574,7 +579,11 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             {
                 std::vector<std::thread> cp;
                 const size_t nCopy = std::min<size_t>(pieces.size(), kCopyThreads);
-                for (size_t t = 1; t < nCopy; t++) cp.emplace_back(copy);
+                for (size_t t = 1; t < nCopy; t++)
+                    cp.emplace_back([&] {
+                        mtb::background_thread();
+                        copy();
+                    });
                 copy();
                 for (auto& t : cp) t.join();
             }

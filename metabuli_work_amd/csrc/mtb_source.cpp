@@ -3,9 +3,13 @@
 // prefetch thread. Replaces the serial kseq/gzread input of QueryIndexer.cpp:30-147 and
 // KmerExtractor::loadChunkOfReads (KmerExtractor.cpp:442-494).
 #include <dlfcn.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <condition_variable>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -151,8 +155,15 @@ struct BgzfSource : ByteSource {
     }
     void start(int n) {
         nThreads = n < 1 ? 1 : n;
-        threads.emplace_back([this] { reader(); });
-        for (int i = 0; i < nThreads; i++) threads.emplace_back([this] { worker(); });
+        threads.emplace_back([this] {
+            background_thread();
+            reader();
+        });
+        for (int i = 0; i < nThreads; i++)
+            threads.emplace_back([this] {
+                background_thread();
+                worker();
+            });
     }
     void reader() {
         std::vector<unsigned char> hdr(18);
@@ -307,6 +318,7 @@ struct PrefetchSource : ByteSource {
 
     explicit PrefetchSource(std::unique_ptr<ByteSource> s) : inner(std::move(s)) {
         t = std::thread([this] {
+            background_thread();
             while (true) {
                 std::vector<char> c(kChunk);
                 const long got = inner->read(c.data(), c.size());
@@ -362,6 +374,13 @@ struct PrefetchSource : ByteSource {
 };
 
 }  // namespace
+
+void background_thread() {
+    const id_t tid = (id_t)syscall(SYS_gettid);
+    errno = 0;
+    const int now = getpriority(PRIO_PROCESS, tid);
+    if (errno == 0 && now < 19) setpriority(PRIO_PROCESS, tid, now + 5 > 19 ? 19 : now + 5);  // best effort
+}
 
 uint32_t crc32_bytes(uint32_t crc, const uint8_t* p, size_t n) {
     const Libdeflate& ld = libdeflate();
