@@ -835,6 +835,7 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
             with open(tsv, "rb") as f:
                 lines = sum(buf.count(b"\n") for buf in iter(lambda: f.read(1 << 24), b""))
             out[mode] = {"reads_per_s": round(got / wall, 1), "read_pairs": got, "wall_s": round(wall, 3),
+                         "native_wall_s": round(lr["wall_s"], 3),
                          "input_bytes": size, "batches": int(lr["batches"]), "gpu_s": round(lr["gpu_s"], 3),
                          "input_wait_s": round(lr["input_wait_s"], 3), "write_s": round(lr["write_s"], 3),
                          "host_stages_s": {k: round(lr[k], 3) for k in ("source_s", "scan_s", "parse_s", "fill_s",
