@@ -932,7 +932,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     if (R >= 0xFFFFFFFFull) { set_error("batch has >= 2^32 k-mer slots: split it"); return MTB_ERR_ARG; }
     c->chunkC = C;
     c->stats[0] = R;
-    HIP_TRY(c->unitInfo.ensure(8 * std::max<uint64_t>(U, 1)));
+    HIP_TRY(c->unitInfo.ensure(16 * std::max<uint64_t>(U, 1)));  // 16-B unit records (mtb_device.h)
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
     HIP_TRY(c->mOff.ensure(sizeof(uint64_t) * (n + 1)));

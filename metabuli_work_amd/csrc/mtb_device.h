@@ -22,14 +22,28 @@ __host__ __device__ inline uint32_t info_frame(uint64_t x) { return (uint32_t)(x
 // K1 slot layout: work unit u owns window p of its chunk at slot (u / 64) * 64C + 64p + u % 64.
 // A unit's info (pack_info of its first window) plus the frame's direction gives every window's
 // info, so the sort carries 32-bit slots and K4 rebuilds the info of the queries that matched.
-__host__ __device__ inline uint64_t slot_info(uint32_t slot, uint32_t C, const uint64_t* unitInfo, int kmerFormat) {
-    const uint32_t wave = slot / (64u * C), rem = slot - wave * 64u * C;
-    const uint32_t p = rem >> 6, u = wave * 64u + (rem & 63u);
-    const uint64_t ui = unitInfo[u];
+// Unit records are 16 B: {pack_info of the unit's first window, the unit's read's slot stretch:
+// its first unit (low 40 bits) | its unit count << 40} — the join's segment bounds come with the
+// info in one aligned load instead of a second random read of the read's unit offsets.
+constexpr uint64_t kStretchLoMask = (1ull << 40) - 1;
+
+__host__ __device__ inline uint64_t unit_info_at(uint64_t ui, uint32_t p, int kmerFormat) {
     const uint32_t frame = (uint32_t)(ui >> 61);
     const bool fromLeft = (kmerFormat == 2) ? frame < 3 : frame >= 3;
     const uint32_t pos = fromLeft ? (uint32_t)ui + 3u * p : (uint32_t)ui - 3u * p;
     return (ui & ~0xFFFFFFFFull) | pos;
+}
+
+__host__ __device__ inline uint32_t slot_unit(uint32_t slot, uint32_t C, uint32_t& p) {
+    const uint32_t wave = slot / (64u * C), rem = slot - wave * 64u * C;
+    p = rem >> 6;
+    return wave * 64u + (rem & 63u);
+}
+
+__host__ __device__ inline uint64_t slot_info(uint32_t slot, uint32_t C, const uint64_t* unitInfo, int kmerFormat) {
+    uint32_t p;
+    const uint32_t u = slot_unit(slot, C, p);
+    return unit_info_at(unitInfo[2 * (uint64_t)u], p, kmerFormat);
 }
 
 // getMaxCoveredLength / getQueryKmerNumber (LocalUtil.h:45-59)

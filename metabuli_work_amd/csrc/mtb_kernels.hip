@@ -315,6 +315,7 @@ struct UnitWindows {
     int pFirst, nWin;    // first window of the chunk, windows in the chunk (0: nothing to do)
     bool fromLeft, comp;
     uint64_t info0;      // pack_info of the chunk's first window (window p: pos0 +- 3p, slot_info)
+    uint64_t stretch;    // the read's first unit | its unit count << 40 (mtb_device.h)
 };
 
 __device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits, uint32_t C,
@@ -326,7 +327,9 @@ __device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits,
     if (u >= nUnits) return w;
     const uint32_t r = unitRead[u];
     const ReadMeta m = meta[r];
-    uint32_t local = (uint32_t)(u - uOff[r]);
+    const uint64_t first = uOff[r];
+    w.stretch = first | (uOff[r + 1] - first) << 40;
+    uint32_t local = (uint32_t)(u - first);
     const uint32_t c1 = (uint32_t)(m.w1 + C - 1) / C, c2 = (uint32_t)(m.w2 + C - 1) / C;
     uint32_t cpf = c1;
     int mate = 0;
@@ -531,7 +534,7 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
     // slots of this unit past its windows (and of padding units) hold the sentinel
     for (int p = max(w.nWin, 0); p < (int)C; p++) keys[slotBase + 64ull * p] = kSentinel;
     if (w.nWin <= 0) return;
-    unitInfo[u] = w.info0;
+    reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
     unit_scan(w, sBase, sAA, sNum, syncmer, smerLen,
               [&](int p, bool ok, uint64_t key) { keys[slotBase + 64ull * p] = ok ? key : kSentinel; });
 }
@@ -1328,6 +1331,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
     for (int j = 0; j < kPer; j++) longq[j] = longList && direct && !kStage && live[j] && hi[j] - lo[j] > kLongRun;
     uint32_t c[kPer], thr[kPer], rk[kPer], mine = 0;
+    uint64_t stretch[kPer];
     const int abFree = g_abRankFree;
     HamRows hr[kPer];
 #pragma unroll
@@ -1346,7 +1350,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                    : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
                             : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
-        info[j] = c[j] ? slot_info(slot[j], C, unitInfo, kmerFormat) : 0;  // only matched queries need it
+        if (c[j]) {  // only matched queries need their info and their read's segment bounds (one 16-B load)
+            uint32_t p;
+            const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot[j], C, p)];
+            info[j] = unit_info_at(ur.x, p, kmerFormat);
+            stretch[j] = ur.y;
+        } else {
+            info[j] = 0;
+            stretch[j] = 0;
+        }
         // the returned count is the query's first rank inside its read's segment
         rk[j] = !c[j] ? 0 : abFree ? (slot[j] & 7u) : atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
@@ -1381,9 +1393,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             if (!c[j]) continue;
-            const uint32_t r = info_seq(info[j]) - 1;
-            const uint64_t o = abFree == 2 ? 0 : dirOff[r] * C;
-            const uint64_t cap = abFree == 2 ? (1u << 20) : (dirOff[r + 1] * C - o) >> capShift;
+            const uint64_t o = abFree == 2 ? 0 : (stretch[j] & kStretchLoMask) * C;
+            const uint64_t cap = abFree == 2 ? (1u << 20) : ((stretch[j] >> 40) * C) >> capShift;
             if (rk[j] + c[j] > cap) {
                 const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c[j]);
                 if (sp + c[j] > region) {
@@ -1592,7 +1603,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
     const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
-    if (w.nWin > 0) unitInfo[u] = w.info0;
+    if (w.nWin > 0) reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
     WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
     for (uint32_t g = 0; g < C; g += kFilterPer) {
         // each window's probe is issued as soon as its key is known; the words are tested after the
