@@ -107,7 +107,7 @@ struct mtb_ctx {
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
-    static constexpr int kNumStats = 14;
+    static constexpr int kNumStats = 15;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -730,6 +730,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
             continue;
         }
+        c->stats[14] = direct ? longN : 0;
         if (direct && longN) {  // the long runs, a wave each; then the spill count and flag again
             launch_match_long(c->longList.as<LongRun>(), longN, qk, qi, c->unitInfo.as<uint64_t>(), C, c->db, c->spOf,
                               (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
