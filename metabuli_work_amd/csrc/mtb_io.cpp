@@ -412,7 +412,11 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
         }
     };
     std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+    for (unsigned t = 1; t < nt; t++)
+        th.emplace_back([&, t] {
+            mtb::background_thread();  // helpers of the calling thread
+            work(t);
+        });
     work(0);
     for (auto& x : th) x.join();
     for (auto& s : part) fwrite(s.data(), 1, s.size(), f);

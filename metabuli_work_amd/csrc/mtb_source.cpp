@@ -376,6 +376,8 @@ struct PrefetchSource : ByteSource {
 }  // namespace
 
 void background_thread() {
+    static const bool off = getenv("MTB_NO_NICE") != nullptr;  // A/B
+    if (off) return;
     const id_t tid = (id_t)syscall(SYS_gettid);
     errno = 0;
     const int now = getpriority(PRIO_PROCESS, tid);
