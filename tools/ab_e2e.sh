@@ -5,6 +5,6 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r03/e2e_ab
 mkdir -p $O
-B="python -u bench.py --skip-config2 --steps 1 --warmup 1 --variants= --em-pairs 0 --c5-kmers 0 --long-reads 0 --cpu-sample 0 --e2e-repeat 2"
+B="python -u bench.py --skip-config2 --steps 1 --warmup 1 --variants= --em-pairs 0 --c5-kmers 0 --long-reads 0 --cpu-sample 0 --e2e-repeat 3"
 timeout -k 10 500 env $B > $O/default.json 2> $O/default.log &&
 timeout -k 10 500 env MTB_NO_NICE=1 $B > $O/nonice.json 2> $O/nonice.log
