@@ -265,6 +265,82 @@ uint32_t parse_records(const char* p, size_t n, std::string& seq, std::vector<ui
 using mtb::FastxStream;
 using mtb::next_record;
 
+namespace mtb {
+
+const char* classification_header(bool lineage) {
+    return lineage ? "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage\ttaxID:match_count\n"
+                   : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n";
+}
+
+void format_classifications(const mtb_ctx* ctx, const mtb_read_batch& batch, const mtb_result* res,
+                            const mtb_taxcnt* taxcnt, uint32_t flags, std::vector<std::string>& part,
+                            unsigned threads) {
+    const uint32_t n = batch.n_reads;
+    const char* names = batch.names;
+    const uint64_t* name_off = batch.name_off;
+    const bool lineage = (flags & MTB_WRITE_LINEAGE) != 0;
+    if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
+    const unsigned nt = std::max(1u, std::min(threads, std::thread::hardware_concurrency()));
+    const uint32_t per = (n + nt - 1) / nt;
+    part.resize(nt);
+    for (auto& x : part) x.clear();
+    auto work = [&](unsigned t) {
+        std::string& o = part[t];
+        char tmp[64];
+        const uint32_t lo = t * per, hi = std::min<uint32_t>(n, lo + per);
+        o.reserve((size_t)(hi > lo ? hi - lo : 0) * 64);
+        // std::to_chars: the ostream's default float format (6 significant digits, %g) and decimal
+        // integers, without snprintf's format parsing (the writer's cost: ~4 conversions per line)
+        auto num = [&](auto v) {
+            const auto r = std::to_chars(tmp, tmp + sizeof tmp, v);
+            o.append(tmp, r.ptr);
+        };
+        for (uint32_t i = lo; i < hi; i++) {
+            const mtb_result& r = res[i];
+            o += r.is_classified ? "1\t" : "0\t";
+            o.append(names + name_off[i], names + name_off[i + 1]);
+            // taxIDs print through getOriginalTaxID (Reporter.cpp:55,65,72); the std::map order of
+            // the taxID:count list is the internal one, as the reference's
+            o += '\t';
+            num(mtb_original_taxid(ctx, r.is_classified ? r.classification : 0));
+            o += '\t';
+            num(r.query_length);
+            o += '\t';
+            const auto fr = std::to_chars(tmp, tmp + sizeof tmp, (double)r.score, std::chars_format::general, 6);
+            o.append(tmp, fr.ptr);
+            o += '\t';
+            if (r.is_classified) {
+                o += mtb_taxon_rank(ctx, r.classification);
+                o += '\t';
+                if (lineage) {
+                    o += mtb_taxon_lineage(ctx, r.classification);
+                    o += '\t';
+                }
+                for (uint32_t k = 0; k < r.taxcnt_len; k++) {
+                    const mtb_taxcnt& c = taxcnt[r.taxcnt_offset + k];
+                    num(mtb_original_taxid(ctx, c.tax_id));
+                    o += ':';
+                    num(c.count);
+                    o += ' ';
+                }
+                o += '\n';
+            } else {
+                o += lineage ? "-\t-\t-\t\n" : "-\t-\t\n";
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++)
+        th.emplace_back([&, t] {
+            background_thread();  // helpers of the calling thread
+            work(t);
+        });
+    work(0);
+    for (auto& x : th) x.join();
+}
+
+}  // namespace mtb
+
 static constexpr int kReaderThreads = 4;  // BGZF inflate workers per file
 
 struct mtb_reader {
@@ -342,83 +418,15 @@ void mtb_reader_close(mtb_reader* r) { delete r; }
 int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, const mtb_read_batch* batch,
                               const mtb_result* res, const mtb_taxcnt* taxcnt, uint32_t flags) {
     if (!ctx || !path || !batch || (!res && batch->n_reads)) return MTB_ERR_ARG;
-    const uint32_t n = batch->n_reads;
-    const char* names = batch->names;
-    const uint64_t* name_off = batch->name_off;
-    const int header = !append;
     FILE* f = fopen(path, append ? "ab" : "wb");
     if (!f) {
         mtb::set_error(std::string("cannot write ") + path);
         return MTB_ERR_IO;
     }
-    const bool lineage = (flags & MTB_WRITE_LINEAGE) != 0;
-    if (header)
-        fputs(lineage ? "#is_classified\tname\ttaxID\tquery_length\tscore\trank\tlineage\ttaxID:match_count\n"
-                      : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n", f);
-    if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
-    // 8 threads format ~1M lines in a few ms; more would take cores from the input threads
-    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    const uint32_t per = (n + nt - 1) / nt;
-    // the formatted parts stay allocated per calling thread: a pipeline's writer reuses warm memory
-    // (the lambda below runs on other threads: it must reach this thread's vector through a
-    // captured reference, not by the thread_local's name)
-    static thread_local std::vector<std::string> partCache;
-    std::vector<std::string>& part = partCache;
-    part.resize(nt);
-    for (auto& x : part) x.clear();
-    auto work = [&](unsigned t) {
-        std::string& o = part[t];
-        char tmp[64];
-        const uint32_t lo = t * per, hi = std::min<uint32_t>(n, lo + per);
-        o.reserve((size_t)(hi > lo ? hi - lo : 0) * 64);
-        // std::to_chars: the ostream's default float format (6 significant digits, %g) and decimal
-        // integers, without snprintf's format parsing (the writer's cost: ~4 conversions per line)
-        auto num = [&](auto v) {
-            const auto r = std::to_chars(tmp, tmp + sizeof tmp, v);
-            o.append(tmp, r.ptr);
-        };
-        for (uint32_t i = lo; i < hi; i++) {
-            const mtb_result& r = res[i];
-            o += r.is_classified ? "1\t" : "0\t";
-            o.append(names + name_off[i], names + name_off[i + 1]);
-            // taxIDs print through getOriginalTaxID (Reporter.cpp:55,65,72); the std::map order of
-            // the taxID:count list is the internal one, as the reference's
-            o += '\t';
-            num(mtb_original_taxid(ctx, r.is_classified ? r.classification : 0));
-            o += '\t';
-            num(r.query_length);
-            o += '\t';
-            const auto fr = std::to_chars(tmp, tmp + sizeof tmp, (double)r.score, std::chars_format::general, 6);
-            o.append(tmp, fr.ptr);
-            o += '\t';
-            if (r.is_classified) {
-                o += mtb_taxon_rank(ctx, r.classification);
-                o += '\t';
-                if (lineage) {
-                    o += mtb_taxon_lineage(ctx, r.classification);
-                    o += '\t';
-                }
-                for (uint32_t k = 0; k < r.taxcnt_len; k++) {
-                    const mtb_taxcnt& c = taxcnt[r.taxcnt_offset + k];
-                    num(mtb_original_taxid(ctx, c.tax_id));
-                    o += ':';
-                    num(c.count);
-                    o += ' ';
-                }
-                o += '\n';
-            } else {
-                o += lineage ? "-\t-\t-\t\n" : "-\t-\t\n";
-            }
-        }
-    };
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; t++)
-        th.emplace_back([&, t] {
-            mtb::background_thread();  // helpers of the calling thread
-            work(t);
-        });
-    work(0);
-    for (auto& x : th) x.join();
+    if (!append) fputs(mtb::classification_header((flags & MTB_WRITE_LINEAGE) != 0), f);
+    // the formatted parts stay allocated per calling thread: repeated calls reuse warm memory
+    static thread_local std::vector<std::string> part;
+    mtb::format_classifications(ctx, *batch, res, taxcnt, flags, part, 8);
     for (auto& s : part) fwrite(s.data(), 1, s.size(), f);
     const bool ok = fclose(f) == 0;
     if (!ok) {

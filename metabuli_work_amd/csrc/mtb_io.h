@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include "../../include/mtb_gpu.h"
+
 namespace mtb {
 
 // Decompressed bytes of one input file, in order.
@@ -30,10 +32,18 @@ std::unique_ptr<ByteSource> open_source(const std::string& path, int threads, bo
 std::unique_ptr<ByteSource> open_parallel_gzip(const std::string& path, int threads, size_t chunkBytes,
                                                std::string& err);
 
-// Helper threads of the input path (inflate, read-ahead, record split, parse, batch fill) run one
-// nice level below the caller's threads, so the threads that feed and drain the GPU are scheduled
-// first when the host's cores are all busy.
+// With MTB_NICE set, helper threads of the input path (inflate, read-ahead, record split, parse,
+// batch fill, TSV formatting) run five nice levels below the caller's threads, so the threads that
+// feed and drain the GPU are scheduled first when the host's cores are all busy (off by default:
+// the same-box A/B, profiles/r03/e2e_ab.json, measured no gain).
 void background_thread();
+
+// The per-read classification TSV (Reporter::writeReadClassification, Reporter.cpp:38-83): its
+// header line, and one batch's lines formatted by `threads` threads into part[0..) in read order.
+const char* classification_header(bool lineage);
+void format_classifications(const mtb_ctx* ctx, const mtb_read_batch& batch, const mtb_result* res,
+                            const mtb_taxcnt* taxcnt, uint32_t flags, std::vector<std::string>& part,
+                            unsigned threads);
 
 // gzip's CRC-32 (libdeflate's folded carry-less multiply when it loads, zlib's otherwise).
 uint32_t crc32_bytes(uint32_t crc, const uint8_t* p, size_t n);

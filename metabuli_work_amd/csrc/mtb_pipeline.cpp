@@ -88,7 +88,8 @@ struct ErrorBox {
 
 constexpr uint32_t kBlockReads = 8192;
 constexpr int kSlots = 3;
-constexpr size_t kCopyThreads = 4;  // threads filling one pinned batch
+constexpr size_t kCopyThreads = 4;     // threads filling one pinned batch
+constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines
 
 struct RecordBlock {
     std::string names, seq;
@@ -675,14 +676,37 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             }
         });
 
-    // writer: the batches in input order -> TSV lines + per-taxon read counts (+ --em mappings)
+    // writer: the batches in input order -> TSV lines + per-taxon read counts (+ --em mappings).
+    // The lines of a batch are formatted into one of two part sets while a flusher thread writes
+    // the other set's lines of the batch before (Reporter.cpp:38-83 writes as it classifies).
     std::map<int32_t, uint64_t> taxCounts;
     std::vector<uint64_t> denseCounts;
     std::vector<mtb_em_map> emMaps;
     uint64_t reads = 0, bases = 0, batches = 0;
     double writeS = 0, gpuS = 0;
+    FILE* tsv = fopen(opt->out_tsv, "wb");
+    if (!tsv) {
+        eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
+    } else if (fputs(mtb::classification_header((opt->write_flags & MTB_WRITE_LINEAGE) != 0), tsv) < 0) {
+        eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
+    }
+    std::vector<std::string> partSets[2];
+    BoundedQueue<std::vector<std::string>*> toFlush(2), freeParts(2);
+    freeParts.push(&partSets[0]);
+    freeParts.push(&partSets[1]);
+    std::thread flusher([&] {
+        std::vector<std::string>* ps = nullptr;
+        while (toFlush.pop(ps)) {
+            if (tsv && !eb.failed)
+                for (auto& x : *ps)
+                    if (fwrite(x.data(), 1, x.size(), tsv) != x.size()) {
+                        eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
+                        break;
+                    }
+            freeParts.push(ps);
+        }
+    });
     std::thread writer([&] {
-        bool first = true;
         uint64_t next = 0;
         std::map<uint64_t, Slot*> held;  // classified batches waiting for an earlier one
         Slot* s = nullptr;
@@ -698,10 +722,11 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     b.n_reads = s->n;
                     b.names = s->names.data();
                     b.name_off = s->noff.data();
-                    if (mtb_write_classifications(ctx0, opt->out_tsv, first ? 0 : 1, &b, s->res.p, s->tc.p,
-                                                  opt->write_flags) != MTB_OK)
-                        eb.set(MTB_ERR_IO, std::string("cannot write ") + opt->out_tsv);
-                    first = false;
+                    std::vector<std::string>* ps = nullptr;
+                    if (freeParts.pop(ps)) {
+                        mtb::format_classifications(ctx0, b, s->res.p, s->tc.p, opt->write_flags, *ps, kFormatThreads);
+                        toFlush.push(ps);
+                    }
                     for (uint32_t i = 0; i < s->n; i++) {  // ++taxCounts[classification] (Classifier.cpp:201-203)
                         const int32_t t = s->res.p[i].is_classified ? s->res.p[i].classification : 0;
                         if (t >= 0 && t < (1 << 26)) {  // internal taxIDs are dense: a flat table
@@ -722,19 +747,15 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             }
         }
         for (auto& kv : held) freeQ[kv.second->ctx]->push(kv.second);  // a failed run: batches never written
-        if (first && !eb.failed) {  // no reads: the header alone
-            mtb_read_batch b{};
-            std::vector<uint64_t> z(1, 0);
-            b.name_off = z.data();
-            b.names = "";
-            mtb_write_classifications(ctx0, opt->out_tsv, 0, &b, nullptr, nullptr, opt->write_flags);
-        }
+        toFlush.close();
     });
 
     assembler.join();
     for (auto& w : workers) w.join();
     writeQ.close();
     writer.join();
+    flusher.join();
+    if (tsv && fclose(tsv) != 0) eb.set(MTB_ERR_IO, std::string("write failed: ") + opt->out_tsv);
     for (auto& q : freeQ) q->close();
     m1.out.close();
     m2.out.close();

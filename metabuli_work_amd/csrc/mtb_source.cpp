@@ -376,8 +376,8 @@ struct PrefetchSource : ByteSource {
 }  // namespace
 
 void background_thread() {
-    static const bool off = getenv("MTB_NO_NICE") != nullptr;  // A/B
-    if (off) return;
+    static const bool on = getenv("MTB_NICE") != nullptr;  // opt-in: not better in the e2e A/B
+    if (!on) return;
     const id_t tid = (id_t)syscall(SYS_gettid);
     errno = 0;
     const int now = getpriority(PRIO_PROCESS, tid);
