@@ -16,7 +16,11 @@
 //     Reporter.cpp:175-190), so the output is the one a single context writes.
 // Batches rotate through kSlots slots per context, so on every GPU batch k+n is parsed and uploaded
 // and batch k-n written while batch k runs.
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -106,7 +110,8 @@ struct RawBuf {
 
 // Whole records p[b, e) of a raw buffer, parsed into blk by a parse worker.
 struct ParseJob {
-    std::shared_ptr<RawBuf> raw;
+    std::shared_ptr<void> raw;  // keeps the bytes alive: a raw buffer, or the file's mapping
+    const char* data = nullptr;  // the job's records, [data, data + (e - b))
     size_t b = 0, e = 0;
     uint32_t recs = 0;  // as counted by the splitter
     RecordBlock blk;
@@ -116,6 +121,7 @@ struct ParseJob {
     bool done = false;
     void reset() {
         raw.reset();
+        data = nullptr;
         b = e = 0;
         recs = 0;
         blk.n = 0;
@@ -138,6 +144,42 @@ struct ParseJob {
         cv.wait(l, [&] { return done; });
     }
 };
+
+// A plain (uncompressed) query file mapped whole: the splitter cuts records in the page cache's
+// own pages, with no read copy and no carried records.
+struct Mapping {
+    const char* p = nullptr;
+    size_t n = 0;
+    ~Mapping() {
+        if (p) munmap((void*)p, n);
+    }
+};
+
+// The mapping of a plain file; nullptr for gzip / BGZF (or a file that cannot be mapped).
+std::shared_ptr<Mapping> map_plain(const char* path) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return nullptr;
+    struct stat st;
+    unsigned char magic[2] = {0, 0};
+    std::shared_ptr<Mapping> m;
+    if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && (st.st_size < 2 || pread(fd, magic, 2, 0) == 2) &&
+        !(magic[0] == 0x1f && magic[1] == 0x8b)) {
+        m = std::make_shared<Mapping>();
+        m->n = (size_t)st.st_size;
+        if (m->n) {
+            void* p = mmap(nullptr, m->n, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (p == MAP_FAILED) {
+                m.reset();
+            } else {
+                m->p = (const char*)p;
+                madvise(p, m->n, MADV_SEQUENTIAL);
+                madvise(p, m->n, MADV_WILLNEED);
+            }
+        }
+    }
+    close(fd);
+    return m;
+}
 
 // A free list of T: objects come back when their last shared_ptr goes, so the input's bytes flow
 // through the same few buffers instead of freshly mapped (page-faulting) ones per chunk.
@@ -216,12 +258,43 @@ struct MateReader {
         chunks.close();
     }
 
+    std::shared_ptr<Mapping> mapped;  // a plain file: split in place
+
+    // The mapped file's records cut into jobs (the whole file is in view: no carries).
+    void split_mapped(ErrorBox* eb, std::string& err) {
+        const char* p = mapped->p;
+        const size_t n = mapped->n;
+        size_t pos = 0;
+        while (!eb->failed && pos < n) {
+            uint32_t recs = 0;
+            const auto s0 = Clock::now();
+            const size_t used = mtb::scan_records(p + pos, n - pos, true, kBlockReads, &recs, err);
+            scanS += secs(s0, Clock::now());
+            if (!err.empty() || recs == 0) break;  // trailing blank lines (or an error)
+            auto j = jobs->get([] { return new ParseJob(); });
+            j->reset();
+            j->raw = mapped;
+            j->data = p + pos;
+            j->b = pos;
+            j->e = pos + used;
+            j->recs = recs;
+            pos += used;
+            if (!out.push(j)) break;
+            if (!work.push(j)) {
+                j->err = "input stopped";
+                j->finish();
+                break;
+            }
+        }
+    }
+
     void run(ErrorBox* eb, int nParsers) {
         mtb::background_thread();  // the splitter
-        reader = std::thread([this, eb] {
-            mtb::background_thread();
-            read_loop(eb);
-        });
+        if (!mapped)
+            reader = std::thread([this, eb] {
+                mtb::background_thread();
+                read_loop(eb);
+            });
         for (int i = 0; i < nParsers; i++)
             parsers.emplace_back([this, eb] {
                 mtb::background_thread();
@@ -233,7 +306,7 @@ struct MateReader {
                         b.seq.reserve((j->e - j->b) / 2 + 64);
                         b.off.reserve(j->recs + 1);
                         b.noff.reserve(j->recs + 1);
-                        b.n = mtb::parse_records(j->raw->p.get() + j->b, j->e - j->b, b.seq, b.off, b.names, b.noff,
+                        b.n = mtb::parse_records(j->data, j->e - j->b, b.seq, b.off, b.names, b.noff,
                                                  j->err);
                     }
                     j->raw.reset();
@@ -242,6 +315,14 @@ struct MateReader {
                 }
             });
         std::string err;
+        if (mapped) {
+            split_mapped(eb, err);
+            if (!err.empty()) eb->set(MTB_ERR_IO, err);
+            work.close();
+            for (auto& p : parsers) p.join();
+            out.close();
+            return;
+        }
         std::shared_ptr<RawBuf> prev;  // holds the unfinished record [pos, end)
         size_t pos = 0, end = 0;
         bool stopped = false;
@@ -278,6 +359,7 @@ struct MateReader {
                 auto j = jobs->get([] { return new ParseJob(); });
                 j->reset();
                 j->raw = buf;
+                j->data = buf->p.get() + pos;
                 j->b = pos;
                 j->e = pos + used;
                 j->recs = recs;
@@ -428,9 +510,14 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     const int parseThreads = std::max(2, srcThreads / 2);  // per mate
     {
         std::string err;
-        // no prefetch thread: the reader thread of each MateReader reads ahead into recycled buffers
-        if (!(m1.src = mtb::open_source(opt->query1, srcThreads, false, err)) ||
-            (paired && !(m2.src = mtb::open_source(opt->query2, srcThreads, false, err)))) {
+        // plain files are mapped and split in place; compressed ones read through a byte source (no
+        // prefetch thread: the reader thread of each MateReader reads ahead into recycled buffers)
+        if (!getenv("MTB_NO_MMAP")) {
+            m1.mapped = map_plain(opt->query1);
+            if (paired) m2.mapped = map_plain(opt->query2);
+        }
+        if ((!m1.mapped && !(m1.src = mtb::open_source(opt->query1, srcThreads, false, err))) ||
+            (paired && !m2.mapped && !(m2.src = mtb::open_source(opt->query2, srcThreads, false, err)))) {
             set_error(err);
             return MTB_ERR_IO;
         }

@@ -283,10 +283,11 @@ def test_start_classify_multi(make_db, tmp_path, n_ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("raw", [150, 600, 7001])
+@pytest.mark.parametrize("raw", [150, 600, 7001, 0])
 def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
     """The pipeline's record split (splitter + parse workers): raw buffers of a few hundred bytes cut
-    records at every kind of position (150: records longer than the buffer's headroom), and the two mates (one wrapped, one not) are cut at different
+    records at every kind of position (150: records longer than the buffer's headroom; plain files
+    are read through the buffers with MTB_NO_MMAP, raw 0: mapped and split in place), and the two mates (one wrapped, one not) are cut at different
     reads, so the assembler joins blocks that do not line up. The TSV is the default run's byte for
     byte; unequal mate counts still fail (QueryIndexer.cpp:121-124)."""
     db_dir, taxo, gen = make_db("fmt2")
@@ -303,8 +304,12 @@ def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
     par.load_db_parameters(db_dir)
     ref, got = str(tmp_path / "ref.tsv"), str(tmp_path / "got.tsv")
     with Classifier(par, db_dir=db_dir) as clf:
+        monkeypatch.setenv("MTB_NO_MMAP", "1")  # the reference run: default buffers
         assert clf.startClassify(ref, reads_per_batch=301) == r.n
-        monkeypatch.setenv("MTB_PARSE_BUFFER", str(raw))
+        if raw:
+            monkeypatch.setenv("MTB_PARSE_BUFFER", str(raw))
+        else:
+            monkeypatch.delenv("MTB_NO_MMAP")
         assert clf.startClassify(got, reads_per_batch=301) == r.n
         assert open(got, "rb").read() == open(ref, "rb").read()
         short = str(tmp_path / "short.fq")
