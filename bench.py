@@ -243,6 +243,8 @@ def main():
                     help="read pairs of each variant line timed on the oracle (parity sample)")
     ap.add_argument("--e2e-pairs", type=int, default=10_000_000,
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
+    ap.add_argument("--e2e-contexts", type=int, default=2,
+                    help="contexts on the GPU for the file -> TSV lines (mtb_clone: two batches in flight)")
     ap.add_argument("--e2e-repeat", type=int, default=1,
                     help="file -> TSV runs per format (A/B: the line reports the median, and every run)")
     ap.add_argument("--e2e-gzip-pairs", type=int, default=10_000_000,
@@ -813,6 +815,7 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
     base = "/dev/shm" if os.path.isdir("/dev/shm") else None
     d = tempfile.mkdtemp(prefix="mtb_e2e_", dir=base)
     out = {}
+    peers = [clf.clone() for _ in range(max(1, args.e2e_contexts) - 1)]  # the same DB, own workspaces
     try:
         n_max = min(N, max(args.e2e_pairs, args.e2e_gzip_pairs))
         h1 = s1[:n_max * L].cpu().numpy()
@@ -833,7 +836,7 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
             runs = []
             for _ in range(max(1, args.e2e_repeat)):
                 t0 = time.perf_counter()
-                got = clf.startClassify(tsv, report_tsv=rep)
+                got = clf.startClassify(tsv, report_tsv=rep, peers=peers)
                 runs.append((time.perf_counter() - t0, clf.last_run))
             runs_rate = [round(got / w, 1) for w, _ in runs]
             wall, lr = sorted(runs, key=lambda x: x[0])[len(runs) // 2]  # the median run
@@ -854,8 +857,12 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
                 os.remove(p)
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    out["note"] = ("file -> TSV wall clock of mtb_start_classify on the GPU box's host (16 threads), mate files "
-                   "in /dev/shm, DB resident in HBM; headline value is the device-resident rate")
+        for c in peers:
+            c.close()
+    out["contexts"] = 1 + len(peers)
+    out["note"] = ("file -> TSV wall clock of mtb_start_classify_multi on the GPU box's host (16 threads), mate "
+                   f"files in /dev/shm, DB resident in HBM, {1 + len(peers)} context(s) on the GPU sharing it "
+                   "(mtb_clone: two batches in flight); headline value is the device-resident rate")
     return out
 
 

@@ -327,6 +327,13 @@ int mtb_write_classifications(const mtb_ctx* ctx, const char* path, int append, 
 int mtb_write_report(const mtb_ctx* ctx, const char* path, uint64_t total_reads, const int32_t* tax_ids,
                      const uint32_t* counts, uint64_t n);
 
+/* A second context over the same DB on the same device: its own stream and batch workspace, the
+ * DB-derived device arrays (records, AA directory, probe lines, run index, species map, taxonomy)
+ * shared, freed with the last context holding them (any close order). Two contexts on one GPU let
+ * mtb_start_classify_multi keep two batches in flight: one batch's host round trips and result
+ * copies overlap the other's kernels. */
+int mtb_clone(const mtb_ctx* src, mtb_ctx** out);
+
 /* ---- Classifier::startClassify over files ----------------------------------- */
 /* Classifier.cpp:44-164 as a threaded native pipeline: per mate file a reader (BGZF blocks inflated
  * by a worker pool; gzip and plain files read ahead), a splitter cutting the bytes at record

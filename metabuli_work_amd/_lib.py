@@ -17,7 +17,7 @@ _LIB = None
 EXPORTED = [
     "mtb_default_params", "mtb_load_db_parameters", "mtb_open", "mtb_open_host", "mtb_close", "mtb_last_error",
     "mtb_set_stream", "mtb_db_kmers", "mtb_classify_batch", "mtb_get_taxcnt", "mtb_device_results",
-    "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
+    "mtb_clone", "mtb_last_counts", "mtb_last_stats", "mtb_last_stage_ms", "mtb_last_kernel_ms", "mtb_copy_results", "mtb_get_query_kmers",
     "mtb_get_matches", "mtb_assign_matches", "mtb_build_db", "mtb_free_built", "mtb_reader_open", "mtb_reader_next",
     "mtb_reader_close", "mtb_taxon_rank", "mtb_write_classifications", "mtb_partition_bounds", "mtb_copy_matches",
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
@@ -46,6 +46,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_open_host.argtypes = [P(MtbDbHost), P(MtbParams), i32, P(vp)]
     L.mtb_open_resident.argtypes = [P(MtbDbResident), P(MtbDbHost), P(MtbParams), i32, P(vp)]
     L.mtb_close.argtypes = [vp]
+    L.mtb_clone.argtypes = [vp, P(vp)]
     L.mtb_close.restype = None
     L.mtb_last_error.restype = ctypes.c_char_p
     L.mtb_set_stream.argtypes = [vp, vp]

@@ -129,6 +129,18 @@ class Classifier:
             lib().mtb_close(self.handle)
             self.handle = ctypes.c_void_p()
 
+    def clone(self) -> "Classifier":
+        """A second classifier over the same DB on the same device (mtb_clone): own stream and batch
+        workspace, the DB-derived arrays shared; as a startClassify peer it keeps two batches in
+        flight on one GPU."""
+        c = Classifier.__new__(Classifier)
+        c.par, c.device, c.db_part = self.par, self.device, self.db_part
+        c.handle = ctypes.c_void_p()
+        if hasattr(self, "_resident"):
+            c._resident = self._resident  # the caller-owned records stay alive with every holder
+        check(lib().mtb_clone(self.handle, ctypes.byref(c.handle)), "mtb_clone")
+        return c
+
     def __enter__(self):
         return self
 

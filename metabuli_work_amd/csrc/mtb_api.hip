@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 
@@ -49,6 +50,19 @@ struct DevBuf {  // grow-only device allocation
     T* as() const { return (T*)p; }
 };
 
+// The DB-derived device arrays a context reads but never writes (records unless the caller owns
+// them, AA directory, probe lines, run index, species map, taxonomy): freed with the last context
+// holding them — a context and its clones (mtb_clone).
+struct DbArrays {
+    int device = 0;
+    std::vector<void*> own;
+    ~DbArrays() {
+        hipSetDevice(device);
+        for (void* p : own)
+            if (p) hipFree(p);
+    }
+};
+
 }  // namespace
 
 struct mtb_ctx {
@@ -61,6 +75,7 @@ struct mtb_ctx {
     uint64_t D = 0;
     DbRec* db = nullptr;      // D + kDbPad records: value (rank form) + taxID & mask
     bool borrowedDb = false;  // db belongs to the caller (mtb_open_resident)
+    std::shared_ptr<DbArrays> dbArrays;  // owner of the DB-derived arrays below, shared with clones
     uint64_t* dirMem = nullptr;
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
@@ -141,6 +156,15 @@ struct mtb_ctx {
 };
 
 static void free_db(mtb_ctx* c) {
+    if (c->dbArrays) {  // the last holder frees them
+        c->dbArrays.reset();
+        c->db = nullptr;
+        c->dirMem = nullptr;
+        c->lines = nullptr;
+        c->lineP = nullptr;
+        c->runOff = nullptr;
+        return;
+    }
     if (c->borrowedDb) c->db = nullptr;  // caller-owned (mtb_open_resident)
     void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
@@ -319,6 +343,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     c->cladePerMatch = (uint32_t)(maxSub + 1);
     HIP_TRY(hipStreamSynchronize(s));
+    c->dbArrays = std::make_shared<DbArrays>();
+    c->dbArrays->device = device;
+    c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf,
+                        c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     *out = c;
     return MTB_OK;
 }
@@ -368,6 +396,63 @@ int mtb_open_resident(const mtb_db_resident* r, const mtb_db_host* h, const mtb_
         !build_species_map(db))
         return MTB_ERR_DB;
     return open_common(db, par, device, out, r);
+}
+
+int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
+    if (!src || !out) { set_error("null argument"); return MTB_ERR_ARG; }
+    mtb_ctx* c = new mtb_ctx();
+    c->device = src->device;
+    c->par = src->par;
+    c->tables = src->tables;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->ownStream = true;
+    for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : c->kev) HIP_TRY(hipEventCreate(&e));
+    // the DB, its directory, probe lines and run index, the species map and the taxonomy: shared
+    c->dbArrays = src->dbArrays;
+    c->D = src->D;
+    c->db = src->db;
+    c->borrowedDb = src->borrowedDb;
+    c->dirMem = src->dirMem;
+    c->lines = src->lines;
+    c->lineP = src->lineP;
+    c->runOff = src->runOff;
+    c->dir = src->dir;
+    c->rankLo = src->rankLo;
+    c->rankHi = src->rankHi;
+    c->spOf = src->spOf;
+    c->maxTax = src->maxTax;
+    c->tNodeOf = src->tNodeOf;
+    c->tNodeTax = src->tNodeTax;
+    c->tParent = src->tParent;
+    c->tDepth = src->tDepth;
+    c->tSpParent = src->tSpParent;
+    c->tFlags = src->tFlags;
+    c->cladePerMatch = src->cladePerMatch;
+    c->hNodeOf = src->hNodeOf;
+    c->hRank = src->hRank;
+    c->hTax = src->hTax;
+    c->dbDir = src->dbDir;
+    c->spKmers = src->spKmers;
+    // the opening's knobs
+    c->joinMode = src->joinMode;
+    c->matchWinCap = src->matchWinCap;
+    c->directJoin = src->directJoin;
+    c->directRetry = src->directRetry;
+    c->pruneAfter = src->pruneAfter;
+    c->bigGroups = src->bigGroups;
+    c->fuseFilter = src->fuseFilter;
+    c->spillShift = src->spillShift;
+    c->sortLoFine = src->sortLoFine;
+    c->forceGeneric = src->forceGeneric;
+    c->segsortGlobal = src->segsortGlobal;
+    c->mergeSeg = src->mergeSeg;
+    c->waveTaxon = src->waveTaxon;
+    c->emulateAll = src->emulateAll;
+    c->pruneCompact = src->pruneCompact;
+    *out = c;
+    return MTB_OK;
 }
 
 void mtb_close(mtb_ctx* c) {

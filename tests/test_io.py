@@ -319,3 +319,35 @@ def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
         clf.par = par2
         with pytest.raises(MtbError, match="different read counts"):
             clf.startClassify(str(tmp_path / "bad.tsv"), reads_per_batch=301)
+
+
+@pytest.mark.gpu
+def test_clone_shares_db(make_db, tmp_path):
+    """mtb_clone: a second context over the same DB arrays, with its own stream and workspace. Two
+    batches in flight on one GPU through mtb_start_classify_multi write the one-context TSV and
+    report; the clone keeps working after its parent closed (the shared arrays go with the last
+    holder)."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 1500, paired=True, seed=61, short_frac=0.02)
+    p1, p2 = str(tmp_path / "c1.fq.gz"), str(tmp_path / "c2.fq.gz")
+    synth.write_compressed(p1, synth.fastq_bytes(r.seq1, r.off1, prefix="c"), "bgzf")
+    synth.write_compressed(p2, synth.fastq_bytes(r.seq2, r.off2, prefix="c"), "bgzf")
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    one, two = str(tmp_path / "one.tsv"), str(tmp_path / "two.tsv")
+    rep1, rep2 = str(tmp_path / "one_report.tsv"), str(tmp_path / "two_report.tsv")
+    clf = Classifier(par, db_dir=db_dir)
+    twin = clf.clone()
+    try:
+        assert clf.startClassify(one, reads_per_batch=211, report_tsv=rep1) == r.n
+        assert clf.startClassify(two, reads_per_batch=211, report_tsv=rep2, peers=[twin]) == r.n
+        assert open(two, "rb").read() == open(one, "rb").read()
+        assert open(rep2, "rb").read() == open(rep1, "rb").read()
+        b1 = clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        res1, tc1 = b1.results.copy(), b1.taxcnt.copy()
+        clf.close()
+        b2 = twin.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        assert np.array_equal(b2.results, res1) and np.array_equal(b2.taxcnt, tc1)
+    finally:
+        clf.close()
+        twin.close()
