@@ -6,6 +6,7 @@
 #   long     config 4: 25k ONT-like reads vs the same DB
 #   related  config 3's "related" DB variant
 #   syncmer  config 3's syncmer DB variant
+#   conserved config 3's heavy-tailed "conserved" DB variant
 #   config2  config 2: 1M pairs vs the 0.98G-k-mer DB
 # Usage: tools/measure_r03.sh [workload ...]   (default: all). Output: gpurun_out/r03/prof/<workload>/
 set -e
@@ -22,9 +23,11 @@ CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs 
 STEP[related]=1; BATCH[related]=1000000
 CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
 STEP[syncmer]=1; BATCH[syncmer]=1000000
+CMD[conserved]="bench.py --variant-only conserved --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
+STEP[conserved]=1; BATCH[conserved]=1000000
 CMD[config2]="bench.py --gtdb-kmers 0 --steps 1 --warmup 1 --long-reads 0 $Q"
 STEP[config2]=1; BATCH[config2]=1000000
-W="${@:-gtdb long related syncmer config2}"
+W="${@:-gtdb long related syncmer conserved config2}"
 for w in $W; do
   D=$O/$w
   mkdir -p $D
