@@ -551,8 +551,9 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
     HIP_TRY(hipEventRecord(c->kev[10], s));
-    if (c->sparse && (!prune || maxSeg > kSegSortSparse || c->segsortGlobal ||
-                      (c->mergeSeg && maxSeg > c->mergeSeg))) {  // K5 reads sparse segments up to kSegSortSparse
+    // K5 reads sparse segments up to kSegSortSparse, and thins bigger ones straight from their stretches
+    if (c->sparse && (!prune || (maxSeg > kSegSortSparse && !compact) || c->segsortGlobal ||
+                      (c->mergeSeg && maxSeg > c->mergeSeg))) {
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), c->chunkC,
                                 c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->spillShift, s);
         // (the spilled ranks of the reads that overflowed their stretch are in place already)

@@ -1160,9 +1160,18 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
 // segLen[r] = survivors; reads at or below `chunk` get kSegSkip (sorted and pruned the usual way).
 constexpr int kThinLog = 14;  // 2^14 counters + 2^14 flags: 128 KB of LDS
 
+template <typename In>
+__device__ void thin_run(const In& in, bool inPlace, mtb_match* __restrict__ io, mtb_match* __restrict__ stage,
+                         uint64_t base, long n, uint32_t pm, uint32_t* __restrict__ segLen, uint32_t r, uint32_t* cnt,
+                         uint32_t* flag, uint32_t& sCount);
+
+// seg (nullable): the direct join's sparse stretches; a read that fits its stretch is read there
+// (no compaction of the batch first) and its survivors are written straight to io.
 __global__ void __launch_bounds__(kLargeThreads) k_thin_big(mtb_match* __restrict__ io, mtb_match* __restrict__ stage,
                                                             const uint64_t* __restrict__ mOff, uint32_t nReads,
-                                                            long chunk, uint32_t pm, uint32_t* __restrict__ segLen) {
+                                                            long chunk, uint32_t pm, uint32_t* __restrict__ segLen,
+                                                            const SegMatch* __restrict__ seg,
+                                                            const uint64_t* __restrict__ inOff, uint32_t inC) {
     __shared__ uint32_t cnt[1 << kThinLog], flag[1 << kThinLog];
     __shared__ uint32_t sCount;
     const uint32_t r = blockIdx.x;
@@ -1173,6 +1182,16 @@ __global__ void __launch_bounds__(kLargeThreads) k_thin_big(mtb_match* __restric
         if (threadIdx.x == 0) segLen[r] = kSegSkip;
         return;
     }
+    if (sparse_read(seg, inOff, inC, r, n))
+        thin_run(sparse_in(seg, inOff, inC, r), false, io, stage, base, n, pm, segLen, r, cnt, flag, sCount);
+    else
+        thin_run(MatchIn{io, base}, true, io, stage, base, n, pm, segLen, r, cnt, flag, sCount);
+}
+
+template <typename In>
+__device__ void thin_run(const In& in, bool inPlace, mtb_match* __restrict__ io, mtb_match* __restrict__ stage,
+                         uint64_t base, long n, uint32_t pm, uint32_t* __restrict__ segLen, uint32_t r, uint32_t* cnt,
+                         uint32_t* flag, uint32_t& sCount) {
     constexpr uint32_t T = 1u << kThinLog;
     for (uint32_t i = threadIdx.x; i < T; i += kLargeThreads) { cnt[i] = 0; flag[i] = 0; }
     if (threadIdx.x == 0) sCount = 0;
@@ -1184,32 +1203,36 @@ __global__ void __launch_bounds__(kLargeThreads) k_thin_big(mtb_match* __restric
     auto spSlot = [](const mtb_match& m) {
         return (uint32_t)(((uint64_t)m.species_id * 0xC2B2AE3D27D4EB4Full) >> (64 - kThinLog));
     };
-    for (long i = threadIdx.x; i < n; i += kLargeThreads) atomicAdd(&cnt[pairSlot(io[base + i])], 1u);
+    for (long i = threadIdx.x; i < n; i += kLargeThreads) atomicAdd(&cnt[pairSlot(in.full((uint32_t)i))], 1u);
     __syncthreads();
     for (long i = threadIdx.x; i < n; i += kLargeThreads) {
-        const mtb_match m = io[base + i];
+        const mtb_match m = in.full((uint32_t)i);
         if (cnt[pairSlot(m)] >= pm) flag[spSlot(m)] = 1;
     }
     __syncthreads();
+    // survivors, one LDS atomic per wave: staged through the (not yet written) output segment when
+    // they overwrite their own input, else straight to io
+    mtb_match* dst = inPlace ? stage : io;
     const int lane = threadIdx.x & 63;
-    for (long i0 = 0; i0 < n; i0 += kLargeThreads) {  // survivors, one LDS atomic per wave
+    for (long i0 = 0; i0 < n; i0 += kLargeThreads) {
         const long i = i0 + threadIdx.x;
         mtb_match m;
         bool keep = false;
         if (i < n) {
-            m = io[base + i];
+            m = in.full((uint32_t)i);
             keep = flag[spSlot(m)] != 0;
         }
         const unsigned long long mk = __ballot(keep);
         uint32_t at = 0;
         if (lane == 0 && mk) at = atomicAdd(&sCount, (uint32_t)__popcll(mk));
         at = __shfl(at, 0, 64);
-        if (keep) stage[base + at + (uint32_t)__popcll(mk & ((1ull << lane) - 1))] = m;
+        if (keep) dst[base + at + (uint32_t)__popcll(mk & ((1ull << lane) - 1))] = m;
     }
     __threadfence_block();
     __syncthreads();
     const uint32_t surv = sCount;
-    for (long i = threadIdx.x; i < (long)surv; i += kLargeThreads) io[base + i] = stage[base + i];
+    if (inPlace)
+        for (long i = threadIdx.x; i < (long)surv; i += kLargeThreads) io[base + i] = stage[base + i];
     if (threadIdx.x == 0) segLen[r] = surv;
 }
 
@@ -1256,8 +1279,10 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
                           uint32_t* segLen, uint32_t* maxTmp, int after) {
     pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
-    // sparse input: the register sorts and the mid sort (segments of <= kSegSortSparse, no thinning)
-    if (seg && (global || maxSeg > kSegSortSparse)) return hipErrorInvalidValue;
+    // sparse input: the register sorts and the mid sort (segments of <= kSegSortSparse), and the
+    // thinning of the bigger ones (read in their stretches, survivors compacted)
+    const bool thin = liveCnt && segLen;
+    if (seg && (global || (maxSeg > kSegSortSparse && !thin))) return hipErrorInvalidValue;
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm,
@@ -1274,7 +1299,7 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
     MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)thinAbove, liveCnt, chunk, pm, nullptr, s,
                              seg, inOff, inC, after));
     mtb_match* io = const_cast<mtb_match*>(in);  // K5's input buffer: the caller's, free to overwrite
-    k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, thinAbove, pm, segLen);
+    k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, thinAbove, pm, segLen, seg, inOff, inC);
     MTB_HIP_RET(hipMemsetAsync(maxTmp, 0, sizeof(uint32_t), s));
     k_max_seg_len<<<(nReads + 255) / 256, 256, 0, s>>>(segLen, nReads, maxTmp);
     uint32_t maxSurv = 0;
