@@ -93,7 +93,7 @@ struct ErrorBox {
 constexpr uint32_t kBlockReads = 8192;
 constexpr int kSlots = 3;
 constexpr size_t kCopyThreads = 4;     // threads filling one pinned batch
-constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines
+constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines (MTB_FORMAT_THREADS)
 
 struct RecordBlock {
     std::string names, seq;
@@ -793,6 +793,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             freeParts.push(ps);
         }
     });
+    const char* ft = getenv("MTB_FORMAT_THREADS");
+    const unsigned formatThreads = ft && atoi(ft) > 0 ? (unsigned)atoi(ft) : kFormatThreads;
     std::thread writer([&] {
         uint64_t next = 0;
         std::map<uint64_t, Slot*> held;  // classified batches waiting for an earlier one
@@ -811,7 +813,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     b.name_off = s->noff.data();
                     std::vector<std::string>* ps = nullptr;
                     if (freeParts.pop(ps)) {
-                        mtb::format_classifications(ctx0, b, s->res.p, s->tc.p, opt->write_flags, *ps, kFormatThreads);
+                        mtb::format_classifications(ctx0, b, s->res.p, s->tc.p, opt->write_flags, *ps, formatThreads);
                         toFlush.push(ps);
                     }
                     for (uint32_t i = 0; i < s->n; i++) {  // ++taxCounts[classification] (Classifier.cpp:201-203)
