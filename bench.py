@@ -232,7 +232,11 @@ def main():
     ap.add_argument("--gtdb-kmers", type=float, default=12e9,
                     help="config 3: k-mers of the GTDB-scale DB (0 = skip config 3; config 2 is then the headline)")
     ap.add_argument("--gtdb-pairs", type=int, default=10_000_000, help="config 3: read pairs per rank per step")
-    ap.add_argument("--gtdb-batch", type=int, default=1_000_000, help="config 3: read pairs per mtb_classify_batch")
+    ap.add_argument("--gtdb-batch", type=int, default=2_000_000,
+                    help="config 3 (and config 5): read pairs per mtb_classify_batch (the QuerySplit; 2M fits "
+                         "beside the 170 GB of DB arrays, profiles/r03/batch_sweep.json)")
+    ap.add_argument("--variant-batch", type=int, default=1_000_000,
+                    help="config-3 DB variants and --em: read pairs per mtb_classify_batch")
     ap.add_argument("--gtdb-species", type=int, default=129_671)
     ap.add_argument("--gtdb-true-species", type=int, default=1000)
     ap.add_argument("--gtdb-genome", type=int, default=3_000_000)
@@ -569,7 +573,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle, run_length_histogram
 
     t0 = time.time()
-    N, B = args.gtdb_pairs, min(args.gtdb_batch, args.gtdb_pairs)
+    N, B = args.gtdb_pairs, min(args.variant_batch if variant else args.gtdb_batch, args.gtdb_pairs)
     got = {}
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
@@ -695,7 +699,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     clf.close()
     em_line = None
     if rank == 0 and not variant and args.em_pairs > 0:
-        em_line = run_em(args, rdb, lp, s1, s2, o1, L, min(N, args.em_pairs), B, local)
+        em_line = run_em(args, rdb, lp, s1, s2, o1, L, min(N, args.em_pairs), min(B, args.variant_batch), local)
     long_line = None
     if "long" in got and not variant:
         ls1, lo1, n50 = got.pop("long")
@@ -817,6 +821,13 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
     out = {}
     peers = [clf.clone() for _ in range(max(1, args.e2e_contexts) - 1)]  # the same DB, own workspaces
     try:
+        # the peers' workspaces grown outside the timing, as the headline context's were (a server
+        # keeps its contexts warm); startClassify trims a context holding more than its share
+        wb = min(N, 1_000_000)
+        wo = torch.arange(wb + 1, dtype=torch.int64, device=s1.device) * L
+        for c in peers:
+            c.classify_batch(s1[:wb * L], wo, s2[:wb * L], wo, device_input=True, fetch=False)
+        torch.cuda.synchronize()
         n_max = min(N, max(args.e2e_pairs, args.e2e_gzip_pairs))
         h1 = s1[:n_max * L].cpu().numpy()
         h2 = s2[:n_max * L].cpu().numpy()

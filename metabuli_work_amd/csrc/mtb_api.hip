@@ -8,6 +8,7 @@
 #include <vector>
 #include <algorithm>
 #include <memory>
+#include <charconv>
 #include <mutex>
 #include <unordered_map>
 
@@ -109,6 +110,8 @@ struct mtb_ctx {
     HostTaxonomy hTax;             // the report (mtb_write_report): names, parents, nodes.dmp order
     mutable std::vector<std::string> lineage;  // per node, built on first use (mtb_taxon_lineage)
     mutable std::once_flag lineageOnce;
+    mutable mtb::TaxText taxText;  // per taxID: original ID digits + rank, built on first use
+    mutable std::once_flag taxTextOnce;
     // batch workspace
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
@@ -122,7 +125,7 @@ struct mtb_ctx {
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
-    static constexpr int kNumStats = 15;
+    static constexpr int kNumStats = 16;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -141,6 +144,7 @@ struct mtb_ctx {
     uint32_t nReads = 0;
     uint64_t Q = 0, M = 0, nTaxcnt = 0;
     uint64_t Qall = 0;  // non-blank query k-mers (KmerMatcher.cpp:143-152), before the AA filter
+    double presentShare = 0.5;  // the fused filter's output capacity, a share of the slots (grows)
     const uint64_t* qKeys = nullptr;   // the last batch's query k-mers (sorted on the sort-merge path)
     const uint32_t* qSlots = nullptr;
     bool keepStages = false;
@@ -288,6 +292,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_PRUNE_COMPACT")) c->pruneCompact = atoi(e) != 0;
     if (const char* e = getenv("MTB_BIG_GROUPS")) c->bigGroups = atoi(e) != 0;
     if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;
+    if (const char* e = getenv("MTB_PRESENT_SHARE")) c->presentShare = std::max(1e-6, atof(e));  // tests: filter reruns
     if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : atoi(e) == 0 ? 0 : 2;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
     if (c->forceGeneric) c->matchWinCap = 0;
@@ -443,6 +448,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->pruneAfter = src->pruneAfter;
     c->bigGroups = src->bigGroups;
     c->fuseFilter = src->fuseFilter;
+    c->presentShare = src->presentShare;
     c->spillShift = src->spillShift;
     c->sortLoFine = src->sortLoFine;
     c->forceGeneric = src->forceGeneric;
@@ -455,18 +461,23 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     return MTB_OK;
 }
 
-void mtb_close(mtb_ctx* c) {
-    if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    free_db(c);
-    DevBuf* bufs[] = {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
+// Every grow-only batch buffer of a context (freed by mtb_close; their sum is the context's
+// workspace, mtb::ctx_workspace_bytes).
+static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
+    return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
                       &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
-    for (DevBuf* b : bufs) b->release();
+}
+
+void mtb_close(mtb_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_db(c);
+    for (DevBuf* b : batch_bufs(c)) b->release();
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : c->kev)
@@ -668,10 +679,17 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                       const uint64_t* dOff2, uint32_t n, uint64_t U, uint32_t C, uint64_t R, uint64_t Rc) {
     hipStream_t s = c->stream;
     const bool probe = c->probed;
-    HIP_TRY(c->keysA.ensure(8 * Rc));
-    HIP_TRY(c->valsA.ensure(4 * Rc));
-    HIP_TRY(c->keysB.ensure(8 * Rc));
-    HIP_TRY(c->valsB.ensure(4 * Rc));
+    const bool fused = c->lines && !probe && c->fuseFilter;
+    // The fused K1 + K1F writes only the present windows (Q, about half the slots at GTDB scale):
+    // its output is sized by the largest present share seen (+1/8) instead of every slot, and the
+    // sort's other side by Q once it is known; a batch past that share reruns the filter into a
+    // larger buffer. The unfused paths write a key per slot.
+    if (!fused) {
+        HIP_TRY(c->keysA.ensure(8 * Rc));
+        HIP_TRY(c->valsA.ensure(4 * Rc));
+        HIP_TRY(c->keysB.ensure(8 * Rc));
+        HIP_TRY(c->valsB.ensure(4 * Rc));
+    }
     HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Rc)));
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
@@ -680,7 +698,6 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
     // K1 extract: every window's key (the sentinel where no k-mer is emitted); fused with K1F for
     // the sort-merge join (the keys never reach HBM: timed as the filter)
-    const bool fused = c->lines && !probe && c->fuseFilter;
     HIP_TRY(hipEventRecord(c->kev[0], s));
     if (!fused)
         launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
@@ -695,12 +712,24 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     const uint64_t* qf = nullptr;
     HIP_TRY(hipEventRecord(c->kev[2], s));
     if (fused) {
-        Q = launch_extract_filter(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
-                                  c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
-                                  c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
-                                  c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo, c->rankHi,
-                                  &c->Qall, s);
-        HIP_TRY(hipGetLastError());
+        uint64_t cap = std::min<uint64_t>(R, (uint64_t)((double)R * c->presentShare) + 4096);
+        for (int pass = 0; pass < 2; pass++) {
+            HIP_TRY(c->keysB.ensure(8 * cap));
+            HIP_TRY(c->valsB.ensure(4 * cap));
+            cap = std::min<uint64_t>(c->keysB.bytes / 8, c->valsB.bytes / 4);  // all the buffers hold
+            Q = launch_extract_filter(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                                      c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
+                                      c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
+                                      c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
+                                      c->rankHi, &c->Qall, cap, s);
+            HIP_TRY(hipGetLastError());
+            if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
+            if (Q <= cap) break;
+            cap = std::min<uint64_t>(R, Q + Q / 8);  // Q <= R: the second pass fits
+            c->stats[15]++;                          // filter reruns (a batch past the present share)
+        }
+        HIP_TRY(c->keysA.ensure(8 * std::max<uint64_t>(Q, 1)));
+        HIP_TRY(c->valsA.ensure(4 * std::max<uint64_t>(Q, 1)));
         qk = c->keysB.as<uint64_t>();
         qi = c->valsB.as<uint32_t>();
     } else if (c->lines) {
@@ -1019,6 +1048,7 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     if (R >= 0xFFFFFFFFull) { set_error("batch has >= 2^32 k-mer slots: split it"); return MTB_ERR_ARG; }
     c->chunkC = C;
     c->stats[0] = R;
+    c->stats[15] = 0;
     HIP_TRY(c->unitInfo.ensure(16 * std::max<uint64_t>(U, 1)));  // 16-B unit records (mtb_device.h)
     HIP_TRY(c->errFlag.ensure(sizeof(int)));
     HIP_TRY(hipMemsetAsync(c->errFlag.p, 0, sizeof(int), s));
@@ -1221,6 +1251,47 @@ const char* mtb_taxon_lineage(const mtb_ctx* c, int32_t t) {
     });
     return c->lineage[T.nodeOf[t]].c_str();
 }
+
+}  // extern "C"
+
+namespace mtb {
+const TaxText& tax_text(const mtb_ctx* c) {
+    std::call_once(c->taxTextOnce, [c] {
+        TaxText& x = c->taxText;
+        const HostTaxonomy& T = c->hTax;
+        x.n = T.maxTax >= 0 && T.maxTax < (1 << 26) ? (uint32_t)T.maxTax + 1 : 0;  // else: formatted per line
+        x.idOff.resize(x.n + 1);
+        x.rankOff.resize(x.n + 1);
+        char tmp[16];
+        for (uint32_t t = 0; t < x.n; t++) {
+            x.idOff[t] = (uint32_t)x.buf.size();
+            const auto r = std::to_chars(tmp, tmp + sizeof tmp, T.original((int32_t)t));
+            x.buf.append(tmp, r.ptr);
+        }
+        x.idOff[x.n] = (uint32_t)x.buf.size();
+        for (uint32_t t = 0; t < x.n; t++) {
+            x.rankOff[t] = (uint32_t)x.buf.size();
+            x.buf += mtb_taxon_rank(c, (int32_t)t);
+        }
+        x.rankOff[x.n] = (uint32_t)x.buf.size();
+    });
+    return c->taxText;
+}
+
+void ctx_release_workspace(mtb_ctx* c) {
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (DevBuf* b : batch_bufs(c)) b->release();
+}
+
+uint64_t ctx_workspace_bytes(const mtb_ctx* c) {
+    uint64_t b = 0;
+    for (DevBuf* x : batch_bufs(const_cast<mtb_ctx*>(c))) b += x->bytes;
+    return b;
+}
+}  // namespace mtb
+
+extern "C" {
 
 int mtb_last_stats(const mtb_ctx* c, uint64_t* out, int n) {
     if (!c || !out) return MTB_ERR_ARG;

@@ -43,6 +43,20 @@ struct HostDb {
     std::vector<int32_t> speciesOf;  // dense taxId2speciesId (KmerMatcher::loadTaxIdList)
 };
 
+// The TSV writer's text per taxID, built once per context (mtb_tax_text): taxID t in [0, n) has
+// its original ID's decimal digits at buf[idOff[t], idOff[t + 1]) and its rank name at
+// buf[rankOff[t], rankOff[t + 1]) ("-" for an absent taxID, as mtb_taxon_rank).
+struct TaxText {
+    uint32_t n = 0;
+    std::vector<uint32_t> idOff, rankOff;
+    std::string buf;
+};
+const TaxText& tax_text(const mtb_ctx* c);
+// Device bytes a context's grow-only batch buffers hold now (reused by its next batches).
+uint64_t ctx_workspace_bytes(const mtb_ctx* c);
+// Frees those buffers (a context holding more than its share of a device shared with others).
+void ctx_release_workspace(mtb_ctx* c);
+
 void set_error(const std::string& msg);
 HostTables make_tables();
 

@@ -16,6 +16,7 @@
 #include <charconv>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -272,6 +273,36 @@ const char* classification_header(bool lineage) {
                    : "#is_classified\tname\ttaxID\tquery_length\tscore\trank\ttaxID:match_count\n";
 }
 
+namespace {
+
+// ostream << float text (%g, 6 significant digits) of the scores a thread has seen: a read's score
+// is a sum of multiples of 0.5 over its length, so a batch holds few distinct values.
+struct ScoreText {
+    struct Entry {
+        uint32_t bits = 0xFFFFFFFFu;  // a NaN pattern no score has
+        uint8_t len = 0;              // kLong: the text did not fit (formatted in place instead)
+        char s[12];
+    };
+    static constexpr uint8_t kLong = 0xFF;
+    Entry e[4096];
+    const Entry& get(float v) {
+        uint32_t b;
+        memcpy(&b, &v, 4);
+        Entry& x = e[(b ^ (b >> 12) ^ (b >> 24)) & 4095u];
+        if (x.bits != b) {
+            char tmp[32];
+            const auto r = std::to_chars(tmp, tmp + sizeof tmp, (double)v, std::chars_format::general, 6);
+            const size_t len = (size_t)(r.ptr - tmp);
+            x.bits = b;
+            x.len = len <= sizeof x.s ? (uint8_t)len : kLong;
+            if (x.len != kLong) memcpy(x.s, tmp, len);
+        }
+        return x;
+    }
+};
+
+}  // namespace
+
 void format_classifications(const mtb_ctx* ctx, const mtb_read_batch& batch, const mtb_result* res,
                             const mtb_taxcnt* taxcnt, uint32_t flags, std::vector<std::string>& part,
                             unsigned threads) {
@@ -280,54 +311,87 @@ void format_classifications(const mtb_ctx* ctx, const mtb_read_batch& batch, con
     const uint64_t* name_off = batch.name_off;
     const bool lineage = (flags & MTB_WRITE_LINEAGE) != 0;
     if (lineage && n) mtb_taxon_lineage(ctx, 1);  // build the per-node lineages before the threads
+    const TaxText& tt = tax_text(ctx);
     const unsigned nt = std::max(1u, std::min(threads, std::thread::hardware_concurrency()));
     const uint32_t per = (n + nt - 1) / nt;
     part.resize(nt);
-    for (auto& x : part) x.clear();
     auto work = [&](unsigned t) {
         std::string& o = part[t];
-        char tmp[64];
         const uint32_t lo = t * per, hi = std::min<uint32_t>(n, lo + per);
-        o.reserve((size_t)(hi > lo ? hi - lo : 0) * 64);
-        // std::to_chars: the ostream's default float format (6 significant digits, %g) and decimal
-        // integers, without snprintf's format parsing (the writer's cost: ~4 conversions per line)
-        auto num = [&](auto v) {
-            const auto r = std::to_chars(tmp, tmp + sizeof tmp, v);
-            o.append(tmp, r.ptr);
+        static thread_local std::unique_ptr<ScoreText> scores;
+        if (!scores) scores.reset(new ScoreText());
+        // the lines go through a raw cursor into o (grown by doubling, cut to size at the end):
+        // per field a memcpy of precomputed text (taxIDs' original IDs, ranks, scores) instead of a
+        // conversion, the integers left through std::to_chars
+        size_t pos = 0;
+        o.resize(std::max<size_t>(o.capacity(), (size_t)(hi > lo ? hi - lo : 0) * 64 + 256));
+        char* w = &o[0];
+        auto room = [&](size_t need) {
+            if (pos + need > o.size()) {
+                o.resize(std::max(2 * o.size(), pos + need));
+                w = &o[0];
+            }
+        };
+        auto put = [&](const char* p, size_t len) {
+            memcpy(w + pos, p, len);
+            pos += len;
+        };
+        auto num = [&](auto v) { pos = (size_t)(std::to_chars(w + pos, w + pos + 24, v).ptr - w); };
+        auto taxid = [&](int32_t x) {  // getOriginalTaxID (Reporter.cpp:55,65,72)
+            if (x >= 0 && (uint32_t)x < tt.n) put(tt.buf.data() + tt.idOff[x], tt.idOff[x + 1] - tt.idOff[x]);
+            else num(mtb_original_taxid(ctx, x));
         };
         for (uint32_t i = lo; i < hi; i++) {
             const mtb_result& r = res[i];
-            o += r.is_classified ? "1\t" : "0\t";
-            o.append(names + name_off[i], names + name_off[i + 1]);
-            // taxIDs print through getOriginalTaxID (Reporter.cpp:55,65,72); the std::map order of
-            // the taxID:count list is the internal one, as the reference's
-            o += '\t';
-            num(mtb_original_taxid(ctx, r.is_classified ? r.classification : 0));
-            o += '\t';
+            const size_t nameLen = name_off[i + 1] - name_off[i];
+            const char* lin = r.is_classified && lineage ? mtb_taxon_lineage(ctx, r.classification) : nullptr;
+            const size_t linLen = lin ? strlen(lin) : 0;
+            const int32_t cls = r.is_classified ? r.classification : 0;
+            const size_t rankLen = cls >= 0 && (uint32_t)cls < tt.n ? tt.rankOff[cls + 1] - tt.rankOff[cls] : 64;
+            room(nameLen + linLen + rankLen + 96 + (size_t)(r.is_classified ? r.taxcnt_len : 0) * 24);
+            w[pos++] = r.is_classified ? '1' : '0';
+            w[pos++] = '\t';
+            put(names + name_off[i], nameLen);
+            // the std::map order of the taxID:count list is the internal one, as the reference's
+            w[pos++] = '\t';
+            taxid(cls);
+            w[pos++] = '\t';
             num(r.query_length);
-            o += '\t';
-            const auto fr = std::to_chars(tmp, tmp + sizeof tmp, (double)r.score, std::chars_format::general, 6);
-            o.append(tmp, fr.ptr);
-            o += '\t';
+            w[pos++] = '\t';
+            const ScoreText::Entry& sc = scores->get(r.score);
+            if (sc.len != ScoreText::kLong) {
+                put(sc.s, sc.len);
+            } else {
+                room(64);
+                pos = (size_t)(std::to_chars(w + pos, w + pos + 32, (double)r.score, std::chars_format::general, 6).ptr - w);
+            }
+            w[pos++] = '\t';
             if (r.is_classified) {
-                o += mtb_taxon_rank(ctx, r.classification);
-                o += '\t';
+                if ((uint32_t)cls < tt.n) {
+                    put(tt.buf.data() + tt.rankOff[cls], rankLen);
+                } else {
+                    const char* rk = mtb_taxon_rank(ctx, cls);
+                    room(strlen(rk) + 64 + (size_t)r.taxcnt_len * 24);
+                    put(rk, strlen(rk));
+                }
+                w[pos++] = '\t';
                 if (lineage) {
-                    o += mtb_taxon_lineage(ctx, r.classification);
-                    o += '\t';
+                    put(lin, linLen);
+                    w[pos++] = '\t';
                 }
                 for (uint32_t k = 0; k < r.taxcnt_len; k++) {
                     const mtb_taxcnt& c = taxcnt[r.taxcnt_offset + k];
-                    num(mtb_original_taxid(ctx, c.tax_id));
-                    o += ':';
+                    taxid(c.tax_id);
+                    w[pos++] = ':';
                     num(c.count);
-                    o += ' ';
+                    w[pos++] = ' ';
                 }
-                o += '\n';
+                w[pos++] = '\n';
             } else {
-                o += lineage ? "-\t-\t-\t\n" : "-\t-\t\n";
+                lineage ? put("-\t-\t-\t\n", 7) : put("-\t-\t\n", 5);
             }
         }
+        o.resize(pos);
     };
     std::vector<std::thread> th;
     for (unsigned t = 1; t < nt; t++)

@@ -1595,7 +1595,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                                                         uint64_t* __restrict__ unitInfo, const ProbeLine* __restrict__ lines,
                                                         uint64_t* __restrict__ qkey, uint32_t* __restrict__ qslot,
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
-                                                        uint64_t rankHi) {
+                                                        uint64_t rankHi, uint64_t cap) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     __shared__ unsigned long long sOut;
@@ -1644,8 +1644,10 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
 #pragma unroll
         for (int j = 0; j < kFilterPer; j++) {
             if (!((mask >> j) & 1u)) continue;
-            qkey[pos] = k[j];
-            qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+            if (pos < cap) {  // past the output's capacity: counted only (the caller grows it and reruns)
+                qkey[pos] = k[j];
+                qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+            }
             pos++;
         }
     }
@@ -1656,13 +1658,13 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               hipStream_t s) {
+                               uint64_t cap, hipStream_t s) {
     hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     if (nUnits) {
         const uint64_t threads = (nUnits + 63) / 64 * 64;
         k_extract_filter<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
             seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-            unitInfo, lines, qkey, qslot, counter, rankLo, rankHi);
+            unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
     }
     unsigned long long Q[2] = {0, 0};
     hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);

@@ -431,6 +431,7 @@ struct Slot {
     int rc = MTB_OK;         // the batch's classify status
     std::string err;
     double gpuS = 0;
+    double tReady = 0, tGpu0 = 0, tGpu1 = 0, tW0 = 0, tW1 = 0;  // MTB_PIPE_TRACE: seconds since the start
     std::vector<mtb_em_map> em;
     Pinned<char> seq1, seq2;
     Pinned<uint64_t> off1, off2;
@@ -493,16 +494,31 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     const uint32_t maxReads = opt->max_reads ? opt->max_reads : 1000000u;
     uint64_t maxBases = opt->max_bases;
     if (!maxBases) {  // ~140 device bytes of workspace per base at GTDB scale; slots < 2^31
-        maxBases = 1ull << 30;
-        for (int d = 0; d < nCtx; d++) {  // the smallest free HBM of the devices
-            size_t freeB = 0, totalB = 0;
-            if (hipSetDevice(mtb_ctx_device(ctxs[d])) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess) {
-                set_error("cannot query device memory");
-                return MTB_ERR_HIP;
+        // per device: its free HBM plus what its contexts' grow-only workspaces already hold (their
+        // next batches reuse it), shared by those contexts; 3/4 of a share for a context's batch
+        std::map<int, std::pair<uint64_t, int>> avail;  // device -> (bytes, contexts)
+        for (int d = 0; d < nCtx; d++) {
+            const int dev = mtb_ctx_device(ctxs[d]);
+            if (!avail.count(dev)) {
+                size_t freeB = 0, totalB = 0;
+                if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess) {
+                    set_error("cannot query device memory");
+                    return MTB_ERR_HIP;
+                }
+                avail[dev] = {freeB, 0};
             }
-            maxBases = std::min<uint64_t>(maxBases, (uint64_t)(0.5 * (double)freeB / 140.0));
+            avail[dev].first += mtb::ctx_workspace_bytes(ctxs[d]);
+            avail[dev].second++;
         }
+        maxBases = 1ull << 30;
+        for (auto& kv : avail)
+            maxBases = std::min<uint64_t>(maxBases, (uint64_t)(0.75 * (double)kv.second.first / kv.second.second / 140.0));
         maxBases = std::max<uint64_t>(maxBases, 1ull << 20);
+        // a context holding more than its share (e.g. grown by larger batches before) gives it back
+        for (int d = 0; d < nCtx; d++) {
+            const auto& a = avail[mtb_ctx_device(ctxs[d])];
+            if (a.second > 1 && mtb::ctx_workspace_bytes(ctxs[d]) > a.first / a.second) mtb::ctx_release_workspace(ctxs[d]);
+        }
     }
     ErrorBox eb;
     MateReader m1, m2;
@@ -696,6 +712,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             fillS += secs(f0, Clock::now());
             if (index == 0) firstBatchS = secs(t0, Clock::now());
             s->index = index++;
+            s->tReady = secs(t0, Clock::now());
             s->firstRead = firstRead;
             firstRead += s->n;
             if (!readyQ[d]->push(s)) break;
@@ -726,6 +743,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     continue;
                 }
                 const auto g0 = Clock::now();
+                s->tGpu0 = secs(t0, g0);
                 int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
                 if (s->res.ensure(std::max<uint32_t>(s->n, 1)) != hipSuccess) rc = MTB_ERR_OOM;
                 if (rc == MTB_OK)
@@ -754,6 +772,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     }
                 }
                 s->gpuS = secs(g0, Clock::now());
+                s->tGpu1 = s->tGpu0 + s->gpuS;
                 s->rc = rc;
                 if (rc != MTB_OK) {
                     s->err = mtb_last_error();  // the error string is per thread
@@ -793,6 +812,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             freeParts.push(ps);
         }
     });
+    // MTB_PIPE_TRACE=<file> (experiments): one line per batch with its stage times
+    FILE* trace = getenv("MTB_PIPE_TRACE") ? fopen(getenv("MTB_PIPE_TRACE"), "a") : nullptr;
     const char* ft = getenv("MTB_FORMAT_THREADS");
     const unsigned formatThreads = ft && atoi(ft) > 0 ? (unsigned)atoi(ft) : kFormatThreads;
     std::thread writer([&] {
@@ -832,6 +853,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                     gpuS += s->gpuS;
                 }
                 writeS += secs(w0, Clock::now());
+                if (trace)
+                    fprintf(trace, "%llu %d %u ready %.4f gpu %.4f %.4f write %.4f %.4f\n", (unsigned long long)s->index,
+                            s->ctx, s->n, s->tReady, s->tGpu0, s->tGpu1, secs(t0, w0), secs(t0, Clock::now()));
                 freeQ[s->ctx]->push(s);
             }
         }
@@ -845,6 +869,10 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     writer.join();
     flusher.join();
     if (tsv && fclose(tsv) != 0) eb.set(MTB_ERR_IO, std::string("write failed: ") + opt->out_tsv);
+    if (trace) {
+        fprintf(trace, "end %.4f\n", secs(t0, Clock::now()));
+        fclose(trace);
+    }
     for (auto& q : freeQ) q->close();
     m1.out.close();
     m2.out.close();

@@ -182,6 +182,31 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     odb.close()
 
 
+@pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2_syncmer", "long"), ("fmt1", "paired")])
+def test_filter_output_rerun(make_db, db_name, kind, monkeypatch):
+    """The fused K1 + K1F writes into a buffer sized from the present share of earlier batches; a
+    batch whose present windows outgrow it reruns the filter into a larger one (MTB_PRESENT_SHARE
+    starts the share far too small): the k-mers, matches and results stay the oracle's, and the
+    next batch fits without a rerun."""
+    monkeypatch.setenv("MTB_PRESENT_SHARE", "0.001")
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    opar = par.to_c()
+    odb = oc.OracleDb(db_dir)
+    with Classifier(par, db_dir=db_dir) as clf:
+        for i, seed in enumerate((31, 32)):
+            reads = _reads(gen, kind, 600 if kind != "long" else 40, seed=seed)
+            okmers, ql1, ql2 = oc.extract(opar, reads)
+            omatches = oc.match(odb, opar, okmers)
+            br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
+            assert clf.stats()["filter_reruns"] == (1 if i == 0 else 0)
+            assert np.array_equal(clf.matches(), omatches)
+            ores, otc = oc.classify(odb, opar, reads)
+            br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+            compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
+
+
 @pytest.mark.parametrize("compact", ["1", "0"])
 @pytest.mark.parametrize("db_name,kind,glob,merge", [
     ("fmt2", "paired", "1", "0"), ("fmt2", "long", "1", "0"), ("fmt1", "long", "1", "0"),
