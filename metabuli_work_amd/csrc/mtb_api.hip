@@ -110,6 +110,7 @@ struct mtb_ctx {
     HostTaxonomy hTax;             // the report (mtb_write_report): names, parents, nodes.dmp order
     mutable std::vector<std::string> lineage;  // per node, built on first use (mtb_taxon_lineage)
     mutable std::once_flag lineageOnce;
+    std::shared_ptr<void> pipelineCache;  // mtb_pipeline.cpp's slots, kept between runs
     mutable mtb::TaxText taxText;  // per taxID: original ID digits + rank, built on first use
     mutable std::once_flag taxTextOnce;
     // batch workspace
@@ -477,6 +478,8 @@ void mtb_close(mtb_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     free_db(c);
+    c->pipelineCache.reset();  // pinned slots and their device buffers (on c->device)
+    hipSetDevice(c->device);
     for (DevBuf* b : batch_bufs(c)) b->release();
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
@@ -1283,6 +1286,8 @@ void ctx_release_workspace(mtb_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : batch_bufs(c)) b->release();
 }
+
+std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache; }
 
 uint64_t ctx_workspace_bytes(const mtb_ctx* c) {
     uint64_t b = 0;

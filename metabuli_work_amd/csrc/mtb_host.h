@@ -3,6 +3,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -56,6 +57,9 @@ const TaxText& tax_text(const mtb_ctx* c);
 uint64_t ctx_workspace_bytes(const mtb_ctx* c);
 // Frees those buffers (a context holding more than its share of a device shared with others).
 void ctx_release_workspace(mtb_ctx* c);
+// Host-side state the file pipeline keeps in a context between runs (its pinned batch slots),
+// destroyed with the context on its device.
+std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c);
 
 void set_error(const std::string& msg);
 HostTables make_tables();

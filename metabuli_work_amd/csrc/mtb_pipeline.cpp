@@ -91,6 +91,9 @@ struct ErrorBox {
 };
 
 constexpr uint32_t kBlockReads = 8192;
+// parsed jobs a mate may hold ahead of the assembler: more than a 1M-read batch (~122 jobs), so the
+// splitter and the parsers keep going while the assembler fills and uploads a batch
+constexpr size_t kJobsAhead = 160;
 constexpr int kSlots = 3;
 constexpr size_t kCopyThreads = 4;     // threads filling one pinned batch
 constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines (MTB_FORMAT_THREADS)
@@ -219,7 +222,7 @@ struct MateReader {
     size_t head = 1u << 20;       // headroom for the unfinished record of the previous buffer
     size_t rawBytes = 32u << 20;  // raw buffer (MTB_PARSE_BUFFER: tests cut records at buffer ends)
     std::unique_ptr<mtb::ByteSource> src;
-    BoundedQueue<std::shared_ptr<ParseJob>> out{32}, work{32};
+    BoundedQueue<std::shared_ptr<ParseJob>> out{kJobsAhead}, work{kJobsAhead};
     struct Chunk {
         std::shared_ptr<RawBuf> buf;
         size_t got = 0;  // bytes at buf->p + head
@@ -445,6 +448,19 @@ struct Slot {
     Pinned<mtb_taxcnt> tc;
 };
 
+// A context's slots, kept between runs (mtb::ctx_pipeline_cache): their pinned host buffers and
+// device input buffers are grown once, not re-pinned (hipHostMalloc) batch by batch every run.
+struct SlotPool {
+    int device = 0;
+    std::vector<std::unique_ptr<Slot>> slots;
+    ~SlotPool() {
+        hipSetDevice(device);
+        for (auto& s : slots)
+            if (s->uploaded) hipEventDestroy(s->uploaded);
+        slots.clear();  // the buffers are freed on the context's device
+    }
+};
+
 // Reads of one mate's current block, consumed from `at`.
 struct Cursor {
     std::shared_ptr<RecordBlock> b;
@@ -538,8 +554,15 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             return MTB_ERR_IO;
         }
     }
-    // per context: kSlots slots, a copy stream on its device, free and ready queues
-    std::vector<std::unique_ptr<Slot>> slotMem;
+    for (int d = 0; d < nCtx; d++)
+        for (int e = 0; e < d; e++)
+            if (ctxs[d] == ctxs[e]) {
+                set_error("a context is listed twice");
+                return MTB_ERR_ARG;
+            }
+    // per context: kSlots slots (kept in the context between runs), a copy stream on its device,
+    // free and ready queues
+    std::vector<Slot*> slotMem;
     std::vector<hipStream_t> up(nCtx, nullptr);
     std::vector<std::unique_ptr<BoundedQueue<Slot*>>> freeQ, readyQ;
     for (int d = 0; d < nCtx; d++) {
@@ -551,11 +574,20 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         }
         freeQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
         readyQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
-        for (int k = 0; k < kSlots; k++) {
-            slotMem.emplace_back(new Slot());
-            Slot* s = slotMem.back().get();
+        std::shared_ptr<void>& cache = mtb::ctx_pipeline_cache(ctxs[d]);
+        if (!cache) {
+            auto pool = std::make_shared<SlotPool>();
+            pool->device = mtb_ctx_device(ctxs[d]);
+            for (int k = 0; k < kSlots; k++) {
+                pool->slots.emplace_back(new Slot());
+                hipEventCreateWithFlags(&pool->slots.back()->uploaded, hipEventDisableTiming);
+            }
+            cache = pool;
+        }
+        for (auto& x : std::static_pointer_cast<SlotPool>(cache)->slots) {
+            Slot* s = x.get();
             s->ctx = d;
-            hipEventCreateWithFlags(&s->uploaded, hipEventDisableTiming);
+            slotMem.push_back(s);
             freeQ[d]->push(s);
         }
     }
@@ -883,10 +915,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         hipStreamSynchronize(up[d]);
         hipStreamDestroy(up[d]);
     }
-    for (auto& s : slotMem) {  // device buffers are freed on their own device
-        hipSetDevice(mtb_ctx_device(ctxs[s->ctx]));
-        hipEventDestroy(s->uploaded);
-        s.reset();
+    for (Slot* s : slotMem) {  // back to the context's pool: the batch data is not kept
+        s->em.clear();
+        s->names.clear();
     }
     hipSetDevice(mtb_ctx_device(ctx0));
     if (eb.code != MTB_OK) {

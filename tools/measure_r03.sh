@@ -2,7 +2,7 @@
 # Round-3 measurement: per workload, a rocprofv3 kernel trace and separate FETCH_SIZE / WRITE_SIZE
 # passes (each its own run; no tracing domains with --pmc) of one timed batch after one warm-up
 # batch; summarised into profiles-ready JSON by tools/traffic_json.py.
-#   gtdb     config 3: 1M pairs vs the 12G-k-mer GTDB-scale DB
+#   gtdb     config 3: one 2M-pair batch (the bench's QuerySplit) vs the 12G-k-mer GTDB-scale DB
 #   long     config 4: 25k ONT-like reads vs the same DB
 #   related  config 3's "related" DB variant
 #   syncmer  config 3's syncmer DB variant
@@ -15,8 +15,8 @@ O=gpurun_out/r03/prof
 mkdir -p $O
 Q="--cpu-sample 0 --e2e-pairs 0 --e2e-gzip-pairs 0 --em-pairs 0 --c5-kmers 0"
 declare -A CMD STEP BATCH
-CMD[gtdb]="bench.py --skip-config2 --steps 1 --warmup 1 --long-reads 0 --variants= --gtdb-pairs 1000000 $Q"
-STEP[gtdb]=1; BATCH[gtdb]=1000000
+CMD[gtdb]="bench.py --skip-config2 --steps 1 --warmup 1 --long-reads 0 --variants= --gtdb-pairs 2000000 --gtdb-batch 2000000 $Q"
+STEP[gtdb]=1; BATCH[gtdb]=2000000
 CMD[long]="bench.py --skip-config2 --steps 1 --warmup 0 --gtdb-pairs 2000 --gtdb-batch 1000 --variants= --long-reads 25000 --long-batch 25000 $Q"
 STEP[long]=3; BATCH[long]=25000
 CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
