@@ -94,6 +94,8 @@ constexpr uint32_t kBlockReads = 8192;
 // parsed jobs a mate may hold ahead of the assembler: more than a 1M-read batch (~122 jobs), so the
 // splitter and the parsers keep going while the assembler fills and uploads a batch
 constexpr size_t kJobsAhead = 160;
+// and at most this many raw bytes per job (long reads: 8192 records would be ~80 MB a job)
+constexpr size_t kJobBytes = 4u << 20;
 constexpr int kSlots = 3;
 constexpr size_t kCopyThreads = 4;     // threads filling one pinned batch
 constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines (MTB_FORMAT_THREADS)
@@ -190,14 +192,17 @@ template <typename T>
 struct Recycler : std::enable_shared_from_this<Recycler<T>> {
     std::mutex mu;
     std::vector<std::unique_ptr<T>> idle;
-    template <typename Make>
-    std::shared_ptr<T> get(Make make) {
+    // an idle object `fits` accepts (others are dropped: e.g. raw buffers of a smaller size kept
+    // from an earlier run), else make()
+    template <typename Make, typename Fits>
+    std::shared_ptr<T> get(Make make, Fits fits) {
         std::unique_ptr<T> x;
         {
             std::lock_guard<std::mutex> l(mu);
-            if (!idle.empty()) {
+            while (!idle.empty() && !x) {
                 x = std::move(idle.back());
                 idle.pop_back();
+                if (!fits(*x)) x.reset();
             }
         }
         if (!x) x.reset(make());
@@ -240,7 +245,8 @@ struct MateReader {
     void read_loop(ErrorBox* eb) {
         while (!eb->failed) {
             Chunk c;
-            c.buf = raws->get([&] { return new RawBuf(head + rawBytes); });
+            c.buf = raws->get([&] { return new RawBuf(head + rawBytes); },
+                              [&](const RawBuf& b) { return b.cap == head + rawBytes; });
             const auto r0 = Clock::now();
             while (c.got < rawBytes) {
                 const long got = src->read(c.buf->p.get() + head + c.got, rawBytes - c.got);
@@ -271,10 +277,13 @@ struct MateReader {
         while (!eb->failed && pos < n) {
             uint32_t recs = 0;
             const auto s0 = Clock::now();
-            const size_t used = mtb::scan_records(p + pos, n - pos, true, kBlockReads, &recs, err);
+            const bool capped = n - pos > kJobBytes;
+            size_t used = mtb::scan_records(p + pos, capped ? kJobBytes : n - pos, !capped, kBlockReads, &recs, err);
+            if (recs == 0 && capped && err.empty())  // a record longer than the cap: the rest of the file
+                used = mtb::scan_records(p + pos, n - pos, true, kBlockReads, &recs, err);
             scanS += secs(s0, Clock::now());
             if (!err.empty() || recs == 0) break;  // trailing blank lines (or an error)
-            auto j = jobs->get([] { return new ParseJob(); });
+            auto j = jobs->get([] { return new ParseJob(); }, [](const ParseJob&) { return true; });
             j->reset();
             j->raw = mapped;
             j->data = p + pos;
@@ -353,13 +362,19 @@ struct MateReader {
             while (!stopped) {
                 uint32_t recs = 0;
                 const auto s0 = Clock::now();
-                const size_t used = mtb::scan_records(buf->p.get() + pos, end - pos, c.eof, kBlockReads, &recs, err);
+                bool capped = end - pos > kJobBytes;
+                size_t used = mtb::scan_records(buf->p.get() + pos, capped ? kJobBytes : end - pos, c.eof && !capped,
+                                                kBlockReads, &recs, err);
+                if (recs == 0 && capped && err.empty()) {  // a record longer than the cap: the whole buffer
+                    used = mtb::scan_records(buf->p.get() + pos, end - pos, c.eof, kBlockReads, &recs, err);
+                    capped = false;
+                }
                 scanS += secs(s0, Clock::now());
                 if (!err.empty() || recs == 0) {
                     pos += used;  // trailing blank lines at the end of the input
                     break;
                 }
-                auto j = jobs->get([] { return new ParseJob(); });
+                auto j = jobs->get([] { return new ParseJob(); }, [](const ParseJob&) { return true; });
                 j->reset();
                 j->raw = buf;
                 j->data = buf->p.get() + pos;
@@ -374,7 +389,7 @@ struct MateReader {
                     j->finish();
                     stopped = true;
                 }
-                if (recs < kBlockReads) break;  // the buffer ends inside a record (or the input ends)
+                if (!capped && recs < kBlockReads) break;  // the buffer ends inside a record (or the input ends)
             }
             if (!err.empty() || c.eof) break;
             prev = buf;
@@ -453,6 +468,11 @@ struct Slot {
 struct SlotPool {
     int device = 0;
     std::vector<std::unique_ptr<Slot>> slots;
+    // the mates' raw buffers and parse jobs (warm host memory instead of freshly faulted pages)
+    std::shared_ptr<Recycler<RawBuf>> raws[2] = {std::make_shared<Recycler<RawBuf>>(),
+                                                 std::make_shared<Recycler<RawBuf>>()};
+    std::shared_ptr<Recycler<ParseJob>> jobs[2] = {std::make_shared<Recycler<ParseJob>>(),
+                                                   std::make_shared<Recycler<ParseJob>>()};
     ~SlotPool() {
         hipSetDevice(device);
         for (auto& s : slots)
@@ -593,6 +613,13 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     }
     BoundedQueue<Slot*> writeQ(slotMem.size() + 1);
 
+    {  // the mates' buffers come from the first context's pool
+        auto pool = std::static_pointer_cast<SlotPool>(mtb::ctx_pipeline_cache(ctx0));
+        m1.raws = pool->raws[0];
+        m1.jobs = pool->jobs[0];
+        m2.raws = pool->raws[1];
+        m2.jobs = pool->jobs[1];
+    }
     if (const char* e = getenv("MTB_PARSE_BUFFER")) {  // tests: records straddle buffers and outgrow the headroom
         m1.rawBytes = m2.rawBytes = std::max<size_t>(1, strtoull(e, nullptr, 10));
         m1.head = m2.head = std::min(m1.head, m1.rawBytes);
