@@ -224,7 +224,9 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--long-reads", type=int, default=125_000,
                     help="config 4: ONT-style reads (N50 ~10 kb) per rank for the long-read line (1M / 8; 0 = off)")
-    ap.add_argument("--long-batch", type=int, default=25_000, help="long reads per mtb_classify_batch")
+    ap.add_argument("--long-batch", type=int, default=62_500,
+                    help="long reads per mtb_classify_batch (62.5k: 2 batches per 125k-read shard; 25k: 494.6k vs 527.8k "
+                         "reads/s same box, profiles/r03/long_batch_sweep.json)")
     ap.add_argument("--db-parts", type=int, default=0,
                     help="config-5 mode: the DB range-partitioned into this many parts (= the number of ranks; "
                          "on one GPU every part is timed in turn)")
