@@ -3,7 +3,7 @@
 # passes (each its own run; no tracing domains with --pmc) of one timed batch after one warm-up
 # batch; summarised into profiles-ready JSON by tools/traffic_json.py.
 #   gtdb     config 3: one 2M-pair batch (the bench's QuerySplit) vs the 12G-k-mer GTDB-scale DB
-#   long     config 4: 25k ONT-like reads vs the same DB
+#   long     config 4: one 62.5k-read batch of ONT-like reads vs the same DB
 #   related  config 3's "related" DB variant
 #   syncmer  config 3's syncmer DB variant
 #   conserved config 3's heavy-tailed "conserved" DB variant
@@ -17,8 +17,8 @@ Q="--cpu-sample 0 --e2e-pairs 0 --e2e-gzip-pairs 0 --em-pairs 0 --c5-kmers 0"
 declare -A CMD STEP BATCH
 CMD[gtdb]="bench.py --skip-config2 --steps 1 --warmup 1 --long-reads 0 --variants= --gtdb-pairs 2000000 --gtdb-batch 2000000 $Q"
 STEP[gtdb]=1; BATCH[gtdb]=2000000
-CMD[long]="bench.py --skip-config2 --steps 1 --warmup 0 --gtdb-pairs 2000 --gtdb-batch 1000 --variants= --long-reads 25000 --long-batch 25000 $Q"
-STEP[long]=3; BATCH[long]=25000
+CMD[long]="bench.py --skip-config2 --steps 1 --warmup 0 --gtdb-pairs 2000 --gtdb-batch 1000 --variants= --long-reads 62500 --long-batch 62500 $Q"
+STEP[long]=3; BATCH[long]=62500
 CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
 STEP[related]=1; BATCH[related]=1000000
 CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
