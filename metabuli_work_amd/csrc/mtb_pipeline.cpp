@@ -114,8 +114,11 @@ struct RawBuf {
 };
 
 // Whole records p[b, e) of a raw buffer, parsed into blk by a parse worker.
+struct Mapping;
+
 struct ParseJob {
     std::shared_ptr<void> raw;  // keeps the bytes alive: a raw buffer, or the file's mapping
+    Mapping* map = nullptr;     // the mapping whose parts [b, e) this job holds (released after the parse)
     const char* data = nullptr;  // the job's records, [data, data + (e - b))
     size_t b = 0, e = 0;
     uint32_t recs = 0;  // as counted by the splitter
@@ -126,6 +129,7 @@ struct ParseJob {
     bool done = false;
     void reset() {
         raw.reset();
+        map = nullptr;
         data = nullptr;
         b = e = 0;
         recs = 0;
@@ -151,12 +155,41 @@ struct ParseJob {
 };
 
 // A plain (uncompressed) query file mapped whole: the splitter cuts records in the page cache's
-// own pages, with no read copy and no carried records.
+// own pages, with no read copy and no carried records. The mapping is given back in parts of kPart
+// bytes as soon as the splitter is past a part and the parse jobs reading it are done (their
+// records are copied into blocks): the page-table teardown of a multi-GB mapping then runs on the
+// parse workers during the run, not as one munmap after the last batch.
 struct Mapping {
+    static constexpr size_t kPart = 64u << 20;
     const char* p = nullptr;
-    size_t n = 0;
+    size_t n = 0, parts = 0;
+    std::unique_ptr<std::atomic<int>[]> refs;   // per part: its jobs + 1 while the splitter is not past it
+    std::unique_ptr<std::atomic<bool>[]> gone;  // per part: unmapped
+    void init() {
+        parts = (n + kPart - 1) / kPart;
+        refs.reset(new std::atomic<int>[parts]);
+        gone.reset(new std::atomic<bool>[parts]);
+        for (size_t c = 0; c < parts; c++) {
+            refs[c] = 1;
+            gone[c] = false;
+        }
+    }
+    void drop(size_t c) {
+        if (!gone[c].exchange(true)) munmap((void*)(p + c * kPart), std::min(kPart, n - c * kPart));
+    }
+    void hold(size_t b, size_t e) {  // a job's bytes [b, e)
+        for (size_t c = b / kPart; c < parts && c * kPart < e; c++) refs[c]++;
+    }
+    void release(size_t b, size_t e) {
+        for (size_t c = b / kPart; c < parts && c * kPart < e; c++)
+            if (--refs[c] == 0) drop(c);
+    }
+    void release_part(size_t c) {  // the splitter is past part c
+        if (--refs[c] == 0) drop(c);
+    }
     ~Mapping() {
-        if (p) munmap((void*)p, n);
+        for (size_t c = 0; c < parts; c++)
+            if (!gone[c]) munmap((void*)(p + c * kPart), std::min(kPart, n - c * kPart));
     }
 };
 
@@ -177,6 +210,7 @@ std::shared_ptr<Mapping> map_plain(const char* path) {
                 m.reset();
             } else {
                 m->p = (const char*)p;
+                m->init();
                 madvise(p, m->n, MADV_SEQUENTIAL);
                 madvise(p, m->n, MADV_WILLNEED);
             }
@@ -273,7 +307,7 @@ struct MateReader {
     void split_mapped(ErrorBox* eb, std::string& err) {
         const char* p = mapped->p;
         const size_t n = mapped->n;
-        size_t pos = 0;
+        size_t pos = 0, passed = 0;  // parts the splitter is past
         while (!eb->failed && pos < n) {
             uint32_t recs = 0;
             const auto s0 = Clock::now();
@@ -286,11 +320,14 @@ struct MateReader {
             auto j = jobs->get([] { return new ParseJob(); }, [](const ParseJob&) { return true; });
             j->reset();
             j->raw = mapped;
+            j->map = mapped.get();
             j->data = p + pos;
             j->b = pos;
             j->e = pos + used;
             j->recs = recs;
+            mapped->hold(j->b, j->e);
             pos += used;
+            for (; passed < mapped->parts && (passed + 1) * Mapping::kPart <= pos; passed++) mapped->release_part(passed);
             if (!out.push(j)) break;
             if (!work.push(j)) {
                 j->err = "input stopped";
@@ -298,6 +335,7 @@ struct MateReader {
                 break;
             }
         }
+        for (; passed < mapped->parts; passed++) mapped->release_part(passed);
     }
 
     void run(ErrorBox* eb, int nParsers) {
@@ -321,6 +359,8 @@ struct MateReader {
                         b.n = mtb::parse_records(j->data, j->e - j->b, b.seq, b.off, b.names, b.noff,
                                                  j->err);
                     }
+                    if (j->map) j->map->release(j->b, j->e);  // its parts may be unmapped now
+                    j->map = nullptr;
                     j->raw.reset();
                     parseNs += (uint64_t)(secs(p0, Clock::now()) * 1e9);
                     j->finish();

@@ -9,8 +9,11 @@ T=${TMPDIR:-/tmp}/mtb_asan
 mkdir -p $T
 cat > $T/stubs.cpp <<'CPP'
 #include <string>
-#include "include/mtb_gpu.h"
-namespace mtb { void set_error(const std::string&) {} }
+#include "metabuli_work_amd/csrc/mtb_host.h"
+namespace mtb {
+void set_error(const std::string&) {}
+const TaxText& tax_text(const mtb_ctx*) { static TaxText t; return t; }
+}
 extern "C" {
 int32_t mtb_original_taxid(const mtb_ctx*, int32_t t) { return t; }
 const char* mtb_taxon_rank(const mtb_ctx*, int32_t) { return "-"; }
