@@ -237,6 +237,9 @@ def main():
     ap.add_argument("--gtdb-batch", type=int, default=2_000_000,
                     help="config 3 (and config 5): read pairs per mtb_classify_batch (the QuerySplit; 2M fits "
                          "beside the 170 GB of DB arrays, profiles/r03/batch_sweep.json)")
+    ap.add_argument("--gtdb-contexts", type=int, default=1,
+                    help="experiments: config-3 batches spread over this many contexts on the GPU (mtb_clone), "
+                         "each driven by a thread of its own (two batches in flight)")
     ap.add_argument("--variant-batch", type=int, default=1_000_000,
                     help="config-3 DB variants and --em: read pairs per mtb_classify_batch")
     ap.add_argument("--gtdb-species", type=int, default=129_671)
@@ -604,9 +607,27 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     c1 = ResultGather(dev, N) if world > 1 else None
     tally = Tally()
 
+    peers = [clf.clone() for _ in range(args.gtdb_contexts - 1)] if not variant and world == 1 else []
+
     def step(timed):
         if world > 1:
             c1.reset()
+        if peers:  # experiments: batch k on context k mod K, one host thread per context
+            import threading
+            ctxs = [clf] + peers
+
+            def run(ci):
+                for a, b in spans[ci::len(ctxs)]:
+                    ob = offs[b - a]
+                    ctxs[ci].classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
+                    if timed and ci == 0:
+                        tally.add(clf, 2 * L * (b - a), b - a)
+            th = [threading.Thread(target=run, args=(ci,)) for ci in range(len(ctxs))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            return
         for a, b in spans:
             ob = offs[b - a]
             clf.classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
@@ -696,6 +717,8 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                       and np.array_equal(gb.taxcnt, otc))
         log(rank, f"[bench] {tag} CPU oracle: {cpu['value'] if cpu else '-'} reads/s, parity {parity}")
     e2e = None
+    for c in peers:
+        c.close()
     if rank == 0 and not variant and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0):
         e2e = run_e2e(args, clf, s1, s2, L, N, (ores, otc) if cpu is not None else None)
     clf.close()
