@@ -652,6 +652,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         }
     }
     BoundedQueue<Slot*> writeQ(slotMem.size() + 1);
+    std::map<int, std::unique_ptr<std::mutex>> growMu;  // per device: workspace growth runs alone
+    for (int d = 0; d < nCtx; d++)
+        if (!growMu.count(mtb_ctx_device(ctxs[d]))) growMu[mtb_ctx_device(ctxs[d])].reset(new std::mutex());
 
     {  // the mates' buffers come from the first context's pool
         auto pool = std::static_pointer_cast<SlotPool>(mtb::ctx_pipeline_cache(ctx0));
@@ -794,6 +797,11 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             take2.clear();
             // the slot's device buffers live on its context's device (a new thread starts on device 0)
             const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
+            // growing them frees the smaller ones, and hipFree waits for the whole device: not while
+            // another context's batch runs there (growMu, below)
+            std::unique_lock<std::mutex> gl(*growMu[mtb_ctx_device(ctxs[d])], std::defer_lock);
+            if (s->dseq1.cap < b1 + 1 || s->doff1.cap < on || (paired && (s->dseq2.cap < b2 + 1 || s->doff2.cap < on)))
+                gl.lock();
             bool ok = hipSetDevice(mtb_ctx_device(ctxs[d])) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
                       s->doff1.ensure(on) == hipSuccess &&
                       hipMemcpyAsync(s->dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
@@ -803,6 +811,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                      hipMemcpyAsync(s->dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
                      hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
             ok = ok && hipEventRecord(s->uploaded, up[d]) == hipSuccess;
+            if (gl.owns_lock()) gl.unlock();
             if (!ok) {
                 eb.set(MTB_ERR_HIP, "batch upload failed");
                 freeQ[d]->push(s);
@@ -845,11 +854,18 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 s->tGpu0 = secs(t0, g0);
                 int rc = hipEventSynchronize(s->uploaded) == hipSuccess ? MTB_OK : MTB_ERR_HIP;
                 if (s->res.ensure(std::max<uint32_t>(s->n, 1)) != hipSuccess) rc = MTB_ERR_OOM;
+                // the ramp and every context's first full-size batch run alone on their device: they
+                // grow the contexts' workspaces, and each growth step's hipFree waits for the whole
+                // device — with two contexts on one GPU, for the other's batch every time (a cold
+                // first run took 3 s longer); later batches reuse the workspace and overlap
+                std::unique_lock<std::mutex> gl(*growMu[mtb_ctx_device(c)], std::defer_lock);
+                if (s->index < 3 + (uint64_t)nCtx) gl.lock();
                 if (rc == MTB_OK)
                     rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
                                             paired ? (const char*)s->dseq2.p : nullptr,
                                             paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
                                             s->res.p);
+                if (gl.owns_lock()) gl.unlock();
                 uint64_t nt = 0;
                 if (rc == MTB_OK) {
                     mtb_get_taxcnt(c, nullptr, 0, &nt);
