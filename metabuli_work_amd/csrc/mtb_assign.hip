@@ -53,42 +53,55 @@ __device__ __forceinline__ long seg_len(const uint64_t* __restrict__ mOff, const
 }
 
 // Segments of up to 64E matches sort in registers: element e = 64*slot + lane. Exchanges at
-// distance j < 64 swap with lane ^ j through cross-lane shuffles, j >= 64 swap slots inside a lane;
+// distance j < 64 swap with lane ^ j through DPP / permlane moves (xor_lane: no LDS crossbar),
+// j >= 64 swap slots inside a lane;
 // the network is unrolled at compile time so the slots stay in VGPRs. No LDS, no barriers.
+// The (k, j) stages of a bitonic network over 64E elements, in order, as compile-time constants
+// (f(k, j) per stage: the cross-lane moves need j as a template argument).
+template <int K, int J, int E, typename F>
+__device__ __forceinline__ void bitonic_stages(F& f) {
+    f(std::integral_constant<int, K>{}, std::integral_constant<int, J>{});
+    if constexpr (J > 1) bitonic_stages<K, J / 2, E>(f);
+    else if constexpr (K < 64 * E) bitonic_stages<K * 2, K, E>(f);
+}
+
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64c(uint64_t v, int lane) {
+    return (uint64_t)xor_lane<J>((uint32_t)(v >> 32), lane) << 32 | xor_lane<J>((uint32_t)v, lane);
+}
+
 template <int E>
 __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&h)[E], uint64_t (&l)[E], uint32_t (&x)[E], int lane) {
+    auto stage = [&](auto kc, auto jc) {
+        constexpr int k = decltype(kc)::value, j = decltype(jc)::value;
+        if constexpr (j >= 64) {
+            constexpr int js = j >> 6;
 #pragma unroll
-    for (int k = 2; k <= 64 * E; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= 64) {
-                const int js = j >> 6;
-#pragma unroll
-                for (int sl = 0; sl < E; sl++) {
-                    if (sl & js) continue;
-                    const int s2 = sl | js;
-                    const bool up = ((64 * sl + lane) & k) == 0;
-                    if (key_gt(h[sl], l[sl], h[s2], l[s2]) == up) {
-                        const uint64_t th = h[sl], tl = l[sl];
-                        const uint32_t tx = x[sl];
-                        h[sl] = h[s2]; l[sl] = l[s2]; x[sl] = x[s2];
-                        h[s2] = th; l[s2] = tl; x[s2] = tx;
-                    }
-                }
-            } else {
-                const bool lower = (lane & j) == 0;
-#pragma unroll
-                for (int sl = 0; sl < E; sl++) {
-                    const bool up = ((64 * sl + lane) & k) == 0;
-                    const uint64_t ph = __shfl_xor(h[sl], j, 64), pl = __shfl_xor(l[sl], j, 64);
-                    const uint32_t px = (uint32_t)__shfl_xor((int)x[sl], j, 64);
-                    // the lower lane of the pair keeps the smaller key when ascending
-                    const bool takeP = (key_gt(h[sl], l[sl], ph, pl) == (lower == up));
-                    if (takeP) { h[sl] = ph; l[sl] = pl; x[sl] = px; }
+            for (int sl = 0; sl < E; sl++) {
+                if (sl & js) continue;
+                const int s2 = sl | js;
+                const bool up = ((64 * sl + lane) & k) == 0;
+                if (key_gt(h[sl], l[sl], h[s2], l[s2]) == up) {
+                    const uint64_t th = h[sl], tl = l[sl];
+                    const uint32_t tx = x[sl];
+                    h[sl] = h[s2]; l[sl] = l[s2]; x[sl] = x[s2];
+                    h[s2] = th; l[s2] = tl; x[s2] = tx;
                 }
             }
+        } else {
+            const bool lower = (lane & j) == 0;
+#pragma unroll
+            for (int sl = 0; sl < E; sl++) {
+                const bool up = ((64 * sl + lane) & k) == 0;
+                const uint64_t ph = xor_lane64c<j>(h[sl], lane), pl = xor_lane64c<j>(l[sl], lane);
+                const uint32_t px = xor_lane<j>(x[sl], lane);
+                // the lower lane of the pair keeps the smaller key when ascending
+                const bool takeP = (key_gt(h[sl], l[sl], ph, pl) == (lower == up));
+                if (takeP) { h[sl] = ph; l[sl] = pl; x[sl] = px; }
+            }
         }
-    }
+    };
+    bitonic_stages<2, 1, E>(stage);
 }
 
 // Dead matches: a (species, frame) run of one match is never given to getMatchPaths
@@ -270,34 +283,34 @@ __device__ __forceinline__ void prune_then_sort(const In& in, mtb_match* __restr
 // network of wave_bitonic_sort: element e = 64 * slot + lane.
 template <int E, typename K>
 __device__ __forceinline__ void wave_bitonic_keys(K (&k)[E], int lane) {
+    auto stage = [&](auto kc, auto jc) {
+        constexpr int kk = decltype(kc)::value, j = decltype(jc)::value;
+        if constexpr (j >= 64) {
+            constexpr int js = j >> 6;
 #pragma unroll
-    for (int kk = 2; kk <= 64 * E; kk <<= 1) {
-#pragma unroll
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            if (j >= 64) {
-                const int js = j >> 6;
-#pragma unroll
-                for (int sl = 0; sl < E; sl++) {
-                    if (sl & js) continue;
-                    const int s2 = sl | js;
-                    const bool up = ((64 * sl + lane) & kk) == 0;
-                    if ((k[sl] > k[s2]) == up) {
-                        const K t = k[sl];
-                        k[sl] = k[s2];
-                        k[s2] = t;
-                    }
-                }
-            } else {
-                const bool lower = (lane & j) == 0;
-#pragma unroll
-                for (int sl = 0; sl < E; sl++) {
-                    const bool up = ((64 * sl + lane) & kk) == 0;
-                    const K pk = __shfl_xor(k[sl], j, 64);
-                    if ((k[sl] > pk) == (lower == up)) k[sl] = pk;
+            for (int sl = 0; sl < E; sl++) {
+                if (sl & js) continue;
+                const int s2 = sl | js;
+                const bool up = ((64 * sl + lane) & kk) == 0;
+                if ((k[sl] > k[s2]) == up) {
+                    const K t = k[sl];
+                    k[sl] = k[s2];
+                    k[s2] = t;
                 }
             }
+        } else {
+            const bool lower = (lane & j) == 0;
+#pragma unroll
+            for (int sl = 0; sl < E; sl++) {
+                const bool up = ((64 * sl + lane) & kk) == 0;
+                K pk;
+                if constexpr (sizeof(K) == 8) pk = (K)xor_lane64c<j>((uint64_t)k[sl], lane);
+                else pk = (K)xor_lane<j>((uint32_t)k[sl], lane);
+                if ((k[sl] > pk) == (lower == up)) k[sl] = pk;
+            }
         }
-    }
+    };
+    bitonic_stages<2, 1, E>(stage);
 }
 
 // n (<= 64 ES) keys of LDS array a sorted in place by one wave.

@@ -152,4 +152,45 @@ __device__ __forceinline__ uint32_t hammings(uint64_t a, uint64_t b, bool revers
 // Match::getScore and partial scores (Match.h:32-70): 3 for an exact codon, else 2 - 0.5h.
 __host__ __device__ inline float codon_score(uint32_t h) { return h == 0 ? 3.0f : 2.0f - 0.5f * (float)h; }
 
+// The value of lane ^ J (J = 1..32) without the LDS crossbar (__shfl_xor is a ds_bpermute): DPP
+// quad_perm for 1 and 2, row_shl / row_shr for 4, row_ror:8 for 8 (a rotation by half a 16-lane row
+// is the xor), and gfx950's v_permlane16_swap / v_permlane32_swap for 16 and 32 (a swap of v with
+// itself leaves the other half's value in each lane's [1] (lower half) or [0] (upper half)).
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
+    static_assert(J == 1 || J == 2 || J == 4 || J == 8 || J == 16 || J == 32, "a power of two below 64");
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, false);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+        return (lane & 4) ? dn : up;
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? p[0] : p[1];
+    } else {
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? p[0] : p[1];
+    }
+}
+
+// The same for a run-time j (a constant after unrolling: the switch folds away) and 32/64-bit values.
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v, int j, int lane) {
+    switch (j) {
+        case 1: return xor_lane<1>(v, lane);
+        case 2: return xor_lane<2>(v, lane);
+        case 4: return xor_lane<4>(v, lane);
+        case 8: return xor_lane<8>(v, lane);
+        case 16: return xor_lane<16>(v, lane);
+        default: return xor_lane<32>(v, lane);
+    }
+}
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int j, int lane) {
+    return (uint64_t)xor_lane32((uint32_t)(v >> 32), j, lane) << 32 | xor_lane32((uint32_t)v, j, lane);
+}
+
 }  // namespace mtb
