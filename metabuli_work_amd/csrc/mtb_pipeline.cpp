@@ -490,6 +490,8 @@ struct Slot {
     std::string err;
     double gpuS = 0;
     double tReady = 0, tGpu0 = 0, tGpu1 = 0, tW0 = 0, tW1 = 0;  // MTB_PIPE_TRACE: seconds since the start
+    float devMs = 0;     // MTB_PIPE_TRACE: the batch's device time (HIP events)
+    uint64_t ws = 0;     // MTB_PIPE_TRACE: the context's workspace bytes after the batch
     std::vector<mtb_em_map> em;
     Pinned<char> seq1, seq2;
     Pinned<uint64_t> off1, off2;
@@ -670,6 +672,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     m1.t = std::thread([&] { m1.run(&eb, parseThreads); });
     if (paired) m2.t = std::thread([&] { m2.run(&eb, parseThreads); });
 
+    // MTB_PIPE_TRACE=<file> (experiments): one line per batch with its stage times
+    FILE* trace = getenv("MTB_PIPE_TRACE") ? fopen(getenv("MTB_PIPE_TRACE"), "a") : nullptr;
     // assembler: blocks -> pinned batches -> device buffers of context (batch mod n)
     double fillS = 0, firstBatchS = 0;
     std::thread assembler([&] {
@@ -888,6 +892,12 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 }
                 s->gpuS = secs(g0, Clock::now());
                 s->tGpu1 = s->tGpu0 + s->gpuS;
+                if (trace) {
+                    float ms[5] = {0, 0, 0, 0, 0};
+                    mtb_last_stage_ms(c, ms, 5);
+                    s->devMs = ms[4];
+                    s->ws = mtb::ctx_workspace_bytes(c);
+                }
                 s->rc = rc;
                 if (rc != MTB_OK) {
                     s->err = mtb_last_error();  // the error string is per thread
@@ -927,8 +937,6 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             freeParts.push(ps);
         }
     });
-    // MTB_PIPE_TRACE=<file> (experiments): one line per batch with its stage times
-    FILE* trace = getenv("MTB_PIPE_TRACE") ? fopen(getenv("MTB_PIPE_TRACE"), "a") : nullptr;
     const char* ft = getenv("MTB_FORMAT_THREADS");
     const unsigned formatThreads = ft && atoi(ft) > 0 ? (unsigned)atoi(ft) : kFormatThreads;
     std::thread writer([&] {
@@ -969,8 +977,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 }
                 writeS += secs(w0, Clock::now());
                 if (trace)
-                    fprintf(trace, "%llu %d %u ready %.4f gpu %.4f %.4f write %.4f %.4f\n", (unsigned long long)s->index,
-                            s->ctx, s->n, s->tReady, s->tGpu0, s->tGpu1, secs(t0, w0), secs(t0, Clock::now()));
+                    fprintf(trace, "%llu %d %u ready %.4f gpu %.4f %.4f write %.4f %.4f dev_ms %.1f ws_gb %.1f\n",
+                            (unsigned long long)s->index, s->ctx, s->n, s->tReady, s->tGpu0, s->tGpu1, secs(t0, w0),
+                            secs(t0, Clock::now()), s->devMs, s->ws * 1e-9);
                 freeQ[s->ctx]->push(s);
             }
         }
