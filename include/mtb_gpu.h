@@ -348,8 +348,8 @@ typedef struct mtb_classify_opts {
     const char* query2;       /* mate 2 (seq_mode 2), else NULL                                 */
     const char* out_tsv;      /* per-read classifications                                       */
     const char* report_tsv;   /* per-taxon report, or NULL                                      */
-    uint32_t max_reads;       /* reads per batch (0: 1,000,000, the first three batches ramping
-                                 up from 1/8 of it so the GPU starts early)                       */
+    uint32_t max_reads;       /* reads per batch (0: 4,000,000, bounded by max_bases; the first
+                                 five batches ramp up from 1/32 of it so the GPU starts early)     */
     uint32_t write_flags;     /* MTB_WRITE_LINEAGE                                              */
     uint64_t max_bases;       /* bases per batch, both mates (0: from free HBM, < 2^30)         */
     int32_t threads;          /* host threads for inflating, per run (0: min(16, cores)); each

@@ -341,7 +341,8 @@ class Classifier:
                       peers: Optional[List["Classifier"]] = None) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
         (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
-        reads_per_batch reads (0: 1M, the first three batches ramping up from 1/8 of that) and
+        reads_per_batch reads (0: 4M, in practice bounded by max_bases; the first five batches ramping up
+        from 1/32 of that) and
         max_bases bases (0: sized from free HBM, the reference's
         RAM-bounded QuerySplits) uploaded on a copy stream, mtb_classify_batch, and the TSV writer
         (+ the per-taxon report, Classifier.cpp:149) overlapping each other; with --em (par.em) the

@@ -97,6 +97,7 @@ constexpr size_t kJobsAhead = 160;
 // and at most this many raw bytes per job (long reads: 8192 records would be ~80 MB a job)
 constexpr size_t kJobBytes = 4u << 20;
 constexpr int kSlots = 3;
+constexpr uint64_t kRamp = 5;  // default batch size: the first kRamp batches ramp up from 1/32 of it
 constexpr size_t kCopyThreads = 4;     // threads filling one pinned batch
 constexpr unsigned kFormatThreads = 8;  // threads formatting one batch's TSV lines (MTB_FORMAT_THREADS)
 
@@ -569,7 +570,9 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     const bool paired = opt->query2 != nullptr;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const int threads = opt->threads > 0 ? opt->threads : (int)std::min(16u, hw);
-    const uint32_t maxReads = opt->max_reads ? opt->max_reads : 1000000u;
+    // default: up to 4M reads a batch, in practice bounded by max_bases (from free HBM: ~2M pairs
+    // beside a GTDB-scale DB), reached through a ramp of kRamp batches from 1/32 of it
+    const uint32_t maxReads = opt->max_reads ? opt->max_reads : 4000000u;
     uint64_t maxBases = opt->max_bases;
     if (!maxBases) {  // ~140 device bytes of workspace per base at GTDB scale; slots < 2^31
         // per device: its free HBM plus what its contexts' grow-only workspaces already hold (their
@@ -692,10 +695,10 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             std::vector<std::pair<std::shared_ptr<RecordBlock>, std::pair<uint32_t, uint32_t>>> take1, take2;
             // which reads go in: whole block stretches until max_reads / max_bases
             static const char* kUnequal = "paired-end inputs have different read counts (QueryIndexer.cpp:121-124)";
-            // with the default batch size the first batches ramp up (1/8, 1/4, 1/2 of it): the GPU
+            // with the default batch size the first batches ramp up (1/32 ... 1/2 of it): the GPU
             // starts after a small parse instead of a full batch's; a read's result does not depend
             // on its batch
-            const uint32_t cap = !opt->max_reads && index < 3 ? std::max<uint32_t>(1, maxReads >> (3 - index)) : maxReads;
+            const uint32_t cap = !opt->max_reads && index < kRamp ? std::max<uint32_t>(1, maxReads >> (kRamp - index)) : maxReads;
             while (s->n < cap) {
                 const bool more1 = c1.next(m1, eb);
                 const bool more2 = paired && c2.next(m2, eb);
@@ -863,7 +866,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 // device — with two contexts on one GPU, for the other's batch every time (a cold
                 // first run took 3 s longer); later batches reuse the workspace and overlap
                 std::unique_lock<std::mutex> gl(*growMu[mtb_ctx_device(c)], std::defer_lock);
-                if (s->index < 3 + (uint64_t)nCtx) gl.lock();
+                if (s->index < kRamp + (uint64_t)nCtx) gl.lock();
                 if (rc == MTB_OK)
                     rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
                                             paired ? (const char*)s->dseq2.p : nullptr,
