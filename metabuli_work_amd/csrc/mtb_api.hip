@@ -1,6 +1,7 @@
 // C-ABI of the MI355X classify path (include/mtb_gpu.h): context, DB residency in HBM and the
 // per-batch pipeline K0 read metadata -> K1 extract -> K2 radix sort -> K4 match (count, scan,
 // emit) -> K5/K6 per-read sort + assignment -> taxcnt compaction.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -34,12 +35,21 @@ struct DevBuf {  // grow-only device allocation
     size_t bytes = 0;
     hipError_t ensure(size_t need) {
         if (need <= bytes) return hipSuccess;
+        static const bool trace = getenv("MTB_ALLOC_TRACE") != nullptr;  // experiments: slow growth steps
+        const auto t0 = std::chrono::steady_clock::now();
+        const size_t old = bytes;
         if (p) hipFree(p);
+        const auto t1 = std::chrono::steady_clock::now();
         p = nullptr;
         bytes = 0;
         size_t b = need + need / 8 + 256;
         hipError_t e = hipMalloc(&p, b);
         if (e == hipSuccess) bytes = b;
+        if (trace) {
+            const auto t2 = std::chrono::steady_clock::now();
+            const double f = std::chrono::duration<double>(t1 - t0).count(), m = std::chrono::duration<double>(t2 - t1).count();
+            if (f + m > 0.02) fprintf(stderr, "[alloc] %.3f GB -> %.3f GB: free %.3f s, malloc %.3f s\n", old * 1e-9, b * 1e-9, f, m);
+        }
         return e;
     }
     void release() {
