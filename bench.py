@@ -254,7 +254,7 @@ def main():
                     help="config 3 file -> TSV line: read pairs written as BGZF / plain FASTQ (0 = off)")
     ap.add_argument("--e2e-contexts", type=int, default=2,
                     help="contexts on the GPU for the file -> TSV lines (mtb_clone: two batches in flight)")
-    ap.add_argument("--e2e-repeat", type=int, default=1,
+    ap.add_argument("--e2e-repeat", type=int, default=3,
                     help="file -> TSV runs per format (A/B: the line reports the median, and every run)")
     ap.add_argument("--e2e-gzip-pairs", type=int, default=10_000_000,
                     help="config 3 file -> TSV line: read pairs written as single-member gzip FASTQ (0 = off)")
