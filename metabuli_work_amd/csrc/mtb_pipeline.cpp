@@ -565,6 +565,12 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             set_error("null context");
             return MTB_ERR_ARG;
         }
+    for (int d = 0; d < nCtx; d++)
+        for (int e = 0; e < d; e++)
+            if (ctxs[d] == ctxs[e]) {
+                set_error("a context is listed twice");
+                return MTB_ERR_ARG;
+            }
     mtb_ctx* const ctx0 = ctxs[0];  // the writers' taxonomy, the report and --em
     const auto t0 = Clock::now();
     const bool paired = opt->query2 != nullptr;
@@ -619,12 +625,6 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             return MTB_ERR_IO;
         }
     }
-    for (int d = 0; d < nCtx; d++)
-        for (int e = 0; e < d; e++)
-            if (ctxs[d] == ctxs[e]) {
-                set_error("a context is listed twice");
-                return MTB_ERR_ARG;
-            }
     // per context: kSlots slots (kept in the context between runs), a copy stream on its device,
     // free and ready queues
     std::vector<Slot*> slotMem;
@@ -806,7 +806,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
             const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
             // growing them frees the smaller ones, and hipFree waits for the whole device: not while
             // another context's batch runs there (growMu, below)
-            std::unique_lock<std::mutex> gl(*growMu[mtb_ctx_device(ctxs[d])], std::defer_lock);
+            std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(ctxs[d])), std::defer_lock);
             if (s->dseq1.cap < b1 + 1 || s->doff1.cap < on || (paired && (s->dseq2.cap < b2 + 1 || s->doff2.cap < on)))
                 gl.lock();
             bool ok = hipSetDevice(mtb_ctx_device(ctxs[d])) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
@@ -865,7 +865,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 // grow the contexts' workspaces, and each growth step's hipFree waits for the whole
                 // device — with two contexts on one GPU, for the other's batch every time (a cold
                 // first run took 3 s longer); later batches reuse the workspace and overlap
-                std::unique_lock<std::mutex> gl(*growMu[mtb_ctx_device(c)], std::defer_lock);
+                std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(c)), std::defer_lock);
                 if (s->index < kRamp + (uint64_t)nCtx) gl.lock();
                 if (rc == MTB_OK)
                     rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,

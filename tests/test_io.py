@@ -270,6 +270,12 @@ def test_start_classify_multi(make_db, tmp_path, n_ctx):
         assert clfs[0].startClassify(one, reads_per_batch=257, report_tsv=rep1) == r.n
         assert clfs[0].startClassify(many, reads_per_batch=257, report_tsv=repn, peers=clfs[1:]) == r.n
         assert clfs[0].last_run["batches"] == (r.n + 256) // 257
+        # a second run reuses the contexts' pooled slots and parse buffers: the same bytes
+        again = str(tmp_path / "again.tsv")
+        assert clfs[0].startClassify(again, reads_per_batch=257, peers=clfs[1:]) == r.n
+        assert open(again, "rb").read() == open(one, "rb").read()
+        with pytest.raises(MtbError, match="listed twice"):
+            clfs[0].startClassify(again, peers=[clfs[0]])
     finally:
         for c in clfs:
             c.close()
