@@ -1587,6 +1587,7 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 // one atomic per block and group) — the window keys never go through HBM. The block's threads
 // share C, so every thread takes part in every group's scan (a unit past its windows, or a padding
 // unit, contributes sentinels). Output: qkey / qslot as k_filter's (slot = the window's K1 slot).
+template <int kPer>
 __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -1605,13 +1606,13 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
     const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
     if (w.nWin > 0) reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
     WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
-    for (uint32_t g = 0; g < C; g += kFilterPer) {
+    for (uint32_t g = 0; g < C; g += kPer) {
         // each window's probe is issued as soon as its key is known; the words are tested after the
         // group's last key, so the 16 line reads overlap the scanning
-        uint64_t k[kFilterPer];
-        uint32_t word[kFilterPer], sh[kFilterPer];
+        uint64_t k[kPer];
+        uint32_t word[kPer], sh[kPer];
 #pragma unroll
-        for (int j = 0; j < kFilterPer; j++) {
+        for (int j = 0; j < kPer; j++) {
             k[j] = (int)(g + j) < w.nWin ? sc.next() : kSentinel;
             word[j] = 0;
             sh[j] = 32;
@@ -1625,7 +1626,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
         }
         uint32_t mask = 0, emitted = 0;
 #pragma unroll
-        for (int j = 0; j < kFilterPer; j++) {
+        for (int j = 0; j < kPer; j++) {
             mask |= (sh[j] < 32u ? (word[j] >> sh[j]) & 1u : 0u) << j;
             emitted += k[j] != kSentinel;
         }
@@ -1642,7 +1643,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
         uint64_t pos = sOut + off;
         __syncthreads();  // sOut is rewritten by the next group
 #pragma unroll
-        for (int j = 0; j < kFilterPer; j++) {
+        for (int j = 0; j < kPer; j++) {
             if (!((mask >> j) & 1u)) continue;
             if (pos < cap) {  // past the output's capacity: counted only (the caller grows it and reruns)
                 qkey[pos] = k[j];
@@ -1662,9 +1663,16 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     if (nUnits) {
         const uint64_t threads = (nUnits + 63) / 64 * 64;
-        k_extract_filter<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-            seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-            unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
+        // MTB_FILTER_PER (A/B): windows per probe group (16: the default; 8: fewer registers, more waves)
+        static const int per = getenv("MTB_FILTER_PER") && atoi(getenv("MTB_FILTER_PER")) == 8 ? 8 : 16;
+        if (per == 8)
+            k_extract_filter<8><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+                seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
+                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
+        else
+            k_extract_filter<kFilterPer><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+                seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
+                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
     }
     unsigned long long Q[2] = {0, 0};
     hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
