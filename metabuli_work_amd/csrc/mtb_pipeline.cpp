@@ -863,8 +863,8 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 if (s->res.ensure(std::max<uint32_t>(s->n, 1)) != hipSuccess) rc = MTB_ERR_OOM;
                 // the ramp and every context's first full-size batch run alone on their device: they
                 // grow the contexts' workspaces, and each growth step's hipFree waits for the whole
-                // device — with two contexts on one GPU, for the other's batch every time (a cold
-                // first run took 3 s longer); later batches reuse the workspace and overlap
+                // device — with two contexts on one GPU, for the other's batch; later batches reuse
+                // the workspace and overlap
                 std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(c)), std::defer_lock);
                 if (s->index < kRamp + (uint64_t)nCtx) gl.lock();
                 if (rc == MTB_OK)
