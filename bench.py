@@ -268,6 +268,9 @@ def main():
                     help="config 5 on one GPU: DB parts, each timed in turn (with N >= 4 GPUs: one part per rank)")
     ap.add_argument("--c5-sample", type=int, default=24_000, help="config 5: read pairs of the oracle parity sample")
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r04", "bench_detail.json"),
+                    help="side file for the full result tree (per-kernel splits, work counters, config-5 parts, "
+                         "e2e host stages); the stdout line keeps the headline and one-line summaries")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -332,9 +335,102 @@ def main():
         else:
             out["long_reads"] = c2.get("long_reads") if c2 is not None else None
         out["config5"] = c5
-        print(json.dumps(out), flush=True)
+        print(json.dumps(compact_line(out, args.detail)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+LINE_CAP = 8000  # the driver keeps only the tail of stdout (~15.5 KB): the one JSON line stays well under it
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _roof(r):
+    return _pick(r, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+                     "alg_bytes_per_launch", "avg_launch_ms"))
+
+
+def _cpu(c):
+    if not isinstance(c, dict):
+        return c
+    s = _pick(c, ("value", "unit", "cores", "kind", "sample"))
+    if isinstance(s.get("sample"), str) and len(s["sample"]) > 160:
+        s["sample"] = s["sample"][:157] + "..."
+    return s
+
+
+def _line(v):
+    """One-line summary of a secondary bench line (config 2, a DB variant, config 4)."""
+    if not isinstance(v, dict):
+        return v
+    s = _pick(v, ("value", "unit", "ms_per_step", "parity_sample"))
+    if "roofline" in v:
+        s["roofline"] = _pick(v["roofline"], ("kernel", "frac", "achieved"))
+    if "cpu_baseline" in v and isinstance(v["cpu_baseline"], dict):
+        s["cpu_baseline"] = _pick(v["cpu_baseline"], ("value", "cores", "kind"))
+    return s
+
+
+def compact_line(out, detail_path):
+    """The stdout JSON line: the headline with its roofline, CPU baseline and parity sample, the
+    long-read line in full, one-line summaries of the rest. Everything else (kernel and stage splits,
+    work counters, config-5 parts, e2e host stages) goes to the detail file the line names."""
+    if detail_path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail_path)), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError as e:
+            log(0, f"[bench] detail file not written: {e}")
+            detail_path = None
+    line = _pick(out, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                       "scaling", "vs_baseline", "dtype", "data", "config", "parity_sample"))
+    line["roofline"] = _roof(out.get("roofline"))
+    line["cpu_baseline"] = _cpu(out.get("cpu_baseline"))
+    if isinstance(out.get("random_roofline"), dict):
+        line["random_roofline"] = {k: _pick(v, ("frac", "achieved_greq_per_s", "ceiling_greq_per_s"))
+                                   for k, v in out["random_roofline"].items()}
+    if isinstance(out.get("pipeline_roofline"), dict):
+        line["pipeline_roofline"] = _pick(out["pipeline_roofline"], ("achieved", "frac", "alg_bytes"))
+    if "kernel_ms" in out:
+        line["kernel_ms"] = out["kernel_ms"]
+    lr = out.get("long_reads")
+    if isinstance(lr, dict):
+        line["long_reads"] = _pick(lr, ("value", "unit", "ms_per_step", "parity_sample", "workload"))
+        line["long_reads"]["roofline"] = _roof(lr.get("roofline"))
+        line["long_reads"]["cpu_baseline"] = _cpu(lr.get("cpu_baseline"))
+        if "parity_sample" not in lr and isinstance(lr.get("cpu_baseline"), dict):
+            line["long_reads"]["parity_sample"] = lr["cpu_baseline"].get("parity_sample")
+    if isinstance(out.get("config2"), dict):
+        line["config2"] = _line(out["config2"])
+    if out.get("variants"):
+        line["variants"] = {k: _line(v) for k, v in out["variants"].items()}
+    e2e = out.get("end_to_end")
+    if isinstance(e2e, dict):
+        line["end_to_end"] = {k: (_pick(v, ("reads_per_s", "tsv_matches_oracle", "first_run_reads_per_s"))
+                                  if isinstance(v, dict) else v) for k, v in e2e.items() if k != "note"}
+    if isinstance(out.get("cold_run"), dict):
+        line["cold_run"] = _pick(out["cold_run"], ("open_s", "first_run_reads_per_s", "steady_reads_per_s",
+                                                   "tsv_matches_oracle"))
+    if isinstance(out.get("em"), dict):
+        line["em"] = _pick(out["em"], ("classify_with_mappings_reads_per_s", "em_s", "reassigned"))
+    c5 = out.get("config5")
+    if isinstance(c5, dict):
+        line["config5"] = _pick(c5, ("value", "unit", "ms_per_step", "parity_sample", "scaling"))
+        line["config5"]["workload"] = "10M pairs vs a 35G-k-mer DB in 8 AA-aligned parts (detail: config5)"
+    line["detail"] = os.path.relpath(detail_path, ROOT) if detail_path else None
+    # never overflow the driver's capture: drop the summaries, least important first
+    for k in ("end_to_end", "em", "random_roofline", "pipeline_roofline", "kernel_ms", "variants", "config5",
+              "config2", "cold_run"):
+        if len(json.dumps(line)) <= LINE_CAP:
+            break
+        line.pop(k, None)
+    if isinstance(line.get("config"), dict) and len(json.dumps(line)) > LINE_CAP:
+        line["config"] = _pick(line["config"], ("workload", "read_pairs_per_gpu", "batch_pairs", "db_kmers",
+                                                "parallelism"))
+    return line
 
 
 def run_config2(args, world, rank, local, dev):

@@ -1,0 +1,45 @@
+"""bench.py's stdout line stays parseable by the driver (a 20.8-KB line overflowed
+its ~15.5-KB stdout capture): under LINE_CAP with the headline fields, roofline and cpu_baseline, the
+full tree in the detail file it names."""
+import importlib.util
+import json
+import pathlib
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_compact_line_under_cap(tmp_path):
+    b = _bench()
+    full = json.loads((ROOT / "profiles" / "r03" / "bench_default.json").read_text())
+    detail = tmp_path / "detail.json"
+    line = b.compact_line(full, str(detail))
+    s = json.dumps(line)
+    assert len(s) <= b.LINE_CAP
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "parity_sample", "long_reads"):
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    assert line["long_reads"]["parity_sample"] is True
+    assert json.loads(detail.read_text()) == full
+
+
+def test_compact_line_drops_summaries_before_headline(tmp_path):
+    b = _bench()
+    full = json.loads((ROOT / "profiles" / "r03" / "bench_default.json").read_text())
+    # an oversized summary section is dropped, the headline fields stay
+    full["variants"] = {f"v{i}": dict(full["variants"]["related"], value=i) for i in range(200)}
+    line = b.compact_line(full, str(tmp_path / "d.json"))
+    assert len(json.dumps(line)) <= b.LINE_CAP
+    assert "variants" not in line
+    assert line["roofline"]["frac"] == full["roofline"]["frac"]
+    assert line["cpu_baseline"]["value"] == full["cpu_baseline"]["value"]
