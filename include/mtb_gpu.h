@@ -156,6 +156,14 @@ void mtb_close(mtb_ctx* ctx);
 const char* mtb_last_error(void);
 int mtb_set_stream(mtb_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
 uint64_t mtb_db_kmers(const mtb_ctx* ctx);             /* number of reference k-mers          */
+/* Device bytes the context's batch workspace holds now (grow-only buffers, reused by the next
+ * batch), and a cap on them (0 = none; MTB_WORKSPACE_CAP=<bytes>[K|M|G] sets it at open): a batch
+ * whose workspace would pass the cap, or the device's free memory, returns MTB_RETRY from
+ * mtb_classify_batch with the workspace given back — the caller classifies it in smaller pieces,
+ * as the reference re-searches a split after its match buffer ran out (Classifier.cpp:127-130,
+ * KmerMatcher.cpp:474-476); mtb_start_classify* halve such a batch down to one read. */
+uint64_t mtb_workspace_bytes(const mtb_ctx* ctx);
+int mtb_set_workspace_cap(mtb_ctx* ctx, uint64_t bytes);
 int mtb_ctx_device(const mtb_ctx* ctx);                /* the HIP device the context runs on  */
 
 /* ---- the hot path ------------------------------------------------------------------------- */
@@ -374,6 +382,7 @@ typedef struct mtb_classify_stats {
     double parse_s;           /* record parsing (parse workers)                                 */
     double fill_s;            /* pinned batch filling and upload issue (assembler)              */
     double first_batch_s;     /* run start until the first batch is uploaded                    */
+    uint64_t split_batches;   /* batches classified in pieces (their workspace did not fit)     */
 } mtb_classify_stats;
 int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify_stats* stats);
 /* The same run over n_ctx contexts, one per GPU of the node (each holding the DB, or the same

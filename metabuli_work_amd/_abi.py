@@ -114,7 +114,8 @@ class MtbClassifyStats(ctypes.Structure):
     _fields_ = [("reads", ctypes.c_uint64), ("bases", ctypes.c_uint64), ("batches", ctypes.c_uint64),
                 ("wall_s", ctypes.c_double), ("gpu_s", ctypes.c_double), ("input_wait_s", ctypes.c_double),
                 ("write_s", ctypes.c_double), ("source_s", ctypes.c_double), ("scan_s", ctypes.c_double),
-                ("parse_s", ctypes.c_double), ("fill_s", ctypes.c_double), ("first_batch_s", ctypes.c_double)]
+                ("parse_s", ctypes.c_double), ("fill_s", ctypes.c_double), ("first_batch_s", ctypes.c_double),
+                ("split_batches", ctypes.c_uint64)]
 
 
 # --em (include/mtb_gpu.h): MappingRes (common.h:24-28), the reassignment of one read, EM stats

@@ -151,6 +151,15 @@ class Classifier:
     def db_kmers(self) -> int:
         return int(lib().mtb_db_kmers(self.handle))
 
+    @property
+    def workspace_bytes(self) -> int:
+        """Device bytes of the batch workspace the context holds (mtb_workspace_bytes)."""
+        return int(lib().mtb_workspace_bytes(self.handle))
+
+    def set_workspace_cap(self, nbytes: int) -> None:
+        """Cap the batch workspace (0 = none): a batch past it is classified in pieces."""
+        check(lib().mtb_set_workspace_cap(self.handle, int(nbytes)), "mtb_set_workspace_cap")
+
     def set_stream(self, stream_ptr: int) -> None:
         check(lib().mtb_set_stream(self.handle, ctypes.c_void_p(stream_ptr)), "mtb_set_stream")
 
@@ -174,11 +183,32 @@ class Classifier:
                     for a in (seq1, off1, seq2, off2)]
             self._keep = (seq1, off1, seq2, off2)
         res = np.zeros(n, RESULT_DTYPE) if fetch else None
-        check(lib().mtb_classify_batch(self.handle, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, flags,
-                                       ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_classify_batch")
+        rc = check(lib().mtb_classify_batch(self.handle, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, flags,
+                                            ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_classify_batch")
+        if rc == _abi.MTB_RETRY:
+            # out of HBM for the batch's workspace: Classifier.cpp:127-130 searches the split again
+            # with a larger match buffer; here the batch is classified in halves (results fetched)
+            if not fetch or keep_stages or n < 2:
+                raise MtbError(f"mtb_classify_batch: {lib().mtb_last_error().decode()}")
+            return self._classify_halves(seq1, off1, seq2, off2, n, device_input)
         if not fetch:
             return None
         return BatchResult(res, self.taxcnt(), *self.last_counts(), self.stage_ms())
+
+    def _classify_halves(self, seq1, off1, seq2, off2, n, device_input) -> BatchResult:
+        """The batch as two read ranges (offsets stay absolute into the same bases), each split
+        again if it still does not fit; taxID:count lists concatenated with rebased offsets."""
+        mid = n // 2
+        parts = []
+        for lo, hi in ((0, mid), (mid, n)):
+            o1 = off1[lo:hi + 1]
+            o2 = off2[lo:hi + 1] if off2 is not None else None
+            parts.append(self.classify_batch(seq1, o1, seq2, o2, device_input=device_input))
+        a, b = parts
+        rb = b.results.copy()
+        rb["taxcnt_offset"] += len(a.taxcnt)
+        return BatchResult(np.concatenate([a.results, rb]), np.concatenate([a.taxcnt, b.taxcnt]),
+                           a.query_kmers + b.query_kmers, a.matches + b.matches, a.stage_ms + b.stage_ms)
 
     def taxcnt(self) -> np.ndarray:
         nt = ctypes.c_uint64(0)

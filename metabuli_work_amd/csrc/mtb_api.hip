@@ -19,20 +19,31 @@
 
 using namespace mtb;
 
+// A failed HIP call ends the entry point: MTB_ERR_OOM when the device ran out of memory (a batch
+// entry point turns that into MTB_RETRY: the caller splits the batch), MTB_ERR_HIP otherwise.
 #define HIP_TRY(x)                                                                                   \
     do {                                                                                             \
         hipError_t e_ = (x);                                                                         \
         if (e_ != hipSuccess) {                                                                      \
             set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x);                 \
-            return MTB_ERR_HIP;                                                                      \
+            return e_ == hipErrorOutOfMemory ? MTB_ERR_OOM : MTB_ERR_HIP;                            \
         }                                                                                            \
     } while (0)
 
 namespace {
 
+// A context's batch workspace: the bytes its grow-only buffers hold, and an optional cap on them
+// (MTB_WORKSPACE_CAP: a growth step past it fails as out of memory, so tests force the split that
+// a full device causes).
+struct WsBudget {
+    size_t cap = 0;  // 0: the device's memory is the only limit
+    size_t used = 0;
+};
+
 struct DevBuf {  // grow-only device allocation
     void* p = nullptr;
     size_t bytes = 0;
+    WsBudget* budget = nullptr;  // the owning context's (batch buffers only)
     hipError_t ensure(size_t need) {
         if (need <= bytes) return hipSuccess;
         static const bool trace = getenv("MTB_ALLOC_TRACE") != nullptr;  // experiments: slow growth steps
@@ -41,10 +52,13 @@ struct DevBuf {  // grow-only device allocation
         if (p) hipFree(p);
         const auto t1 = std::chrono::steady_clock::now();
         p = nullptr;
+        if (budget) budget->used -= bytes;
         bytes = 0;
         size_t b = need + need / 8 + 256;
+        if (budget && budget->cap && budget->used + b > budget->cap) return hipErrorOutOfMemory;
         hipError_t e = hipMalloc(&p, b);
         if (e == hipSuccess) bytes = b;
+        if (e == hipSuccess && budget) budget->used += b;
         if (trace) {
             const auto t2 = std::chrono::steady_clock::now();
             const double f = std::chrono::duration<double>(t1 - t0).count(), m = std::chrono::duration<double>(t2 - t1).count();
@@ -55,6 +69,7 @@ struct DevBuf {  // grow-only device allocation
     void release() {
         if (p) hipFree(p);
         p = nullptr;
+        if (budget) budget->used -= bytes;
         bytes = 0;
     }
     template <typename T>
@@ -135,7 +150,8 @@ struct mtb_ctx {
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
-    uint64_t liveM = 0;                     // matches K6 read in the last batch  // probe join: DB lower bounds of the filtered queries; striped counters
+    uint64_t liveM = 0;                     // matches K6 read in the last batch
+    WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
     static constexpr int kNumStats = 16;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
@@ -169,6 +185,22 @@ struct mtb_ctx {
     float kernMs[kNumKern] = {0, 0, 0, 0, 0, 0, 0};
     hipEvent_t kev[2 * kNumKern]{};
 };
+
+static std::vector<DevBuf*> batch_bufs(mtb_ctx* c);
+
+// The batch buffers account their bytes to the context's budget; MTB_WORKSPACE_CAP=<bytes>[K|M|G]
+// caps it (tests: a batch past the cap returns MTB_RETRY, as one past the device's memory does).
+static void bind_workspace(mtb_ctx* c, size_t cap) {
+    c->ws.cap = cap;
+    if (const char* e = getenv("MTB_WORKSPACE_CAP")) {
+        char* end = nullptr;
+        double v = strtod(e, &end);
+        const char u = end ? *end : 0;
+        v *= u == 'G' || u == 'g' ? 1e9 : u == 'M' || u == 'm' ? 1e6 : u == 'K' || u == 'k' ? 1e3 : 1.0;
+        c->ws.cap = v > 0 ? (size_t)v : 0;
+    }
+    for (DevBuf* b : batch_bufs(c)) b->budget = &c->ws;
+}
 
 static void free_db(mtb_ctx* c) {
     if (c->dbArrays) {  // the last holder frees them
@@ -363,6 +395,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     c->dbArrays->device = device;
     c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf,
                         c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    bind_workspace(c, 0);
     *out = c;
     return MTB_OK;
 }
@@ -468,6 +501,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->waveTaxon = src->waveTaxon;
     c->emulateAll = src->emulateAll;
     c->pruneCompact = src->pruneCompact;
+    bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
 }
@@ -513,6 +547,14 @@ int mtb_set_stream(mtb_ctx* c, void* stream) {
 }
 
 uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
+
+uint64_t mtb_workspace_bytes(const mtb_ctx* c) { return c ? c->ws.used : 0; }
+
+int mtb_set_workspace_cap(mtb_ctx* c, uint64_t bytes) {
+    if (!c) return MTB_ERR_ARG;
+    c->ws.cap = bytes;
+    return MTB_OK;
+}
 
 int mtb_ctx_device(const mtb_ctx* c) { return c ? c->device : 0; }
 
@@ -825,7 +867,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
         HIP_TRY(c->longCnt.ensure(sizeof(uint32_t)));
     }
-    for (int attempt = 0; attempt < 4; attempt++) {
+    bool spillGrown = false;  // the spill buffer grows once per batch (then the staged join)
+    for (int attempt = 0; attempt < 5; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
         int overflow = 0;
@@ -873,7 +916,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         if (direct) {
             nSpill = regTot[0];
             if (!overflow && !c->directRetry) break;
-            if (overflow && attempt == 0 && !c->directRetry) {  // the spill outgrew its buffer: once more, larger
+            if (overflow && !spillGrown && !c->directRetry) {  // the spill outgrew its buffer: once more, larger
+                spillGrown = true;
                 const uint64_t want = nSpill + nSpill / 8;
                 if (c->mStage.ensure(sizeof(mtb_match) * want) == hipSuccess &&
                     c->mRank.ensure(sizeof(uint32_t) * want) == hipSuccess) {
@@ -992,8 +1036,8 @@ int mtb_mask_reads(mtb_ctx* c, const char* seq, const uint64_t* off, uint32_t n,
     return MTB_OK;
 }
 
-int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const char* seq2, const uint64_t* off2,
-                       uint32_t n, uint32_t flags, mtb_result* results) {
+static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const char* seq2, const uint64_t* off2,
+                          uint32_t n, uint32_t flags, mtb_result* results) {
     if (!c || !off || !seq) { set_error("null argument"); return MTB_ERR_ARG; }
     const bool paired = c->par.seq_mode == 2;
     if (paired && (!seq2 || !off2)) { set_error("seq_mode 2 needs both mates"); return MTB_ERR_ARG; }
@@ -1113,6 +1157,32 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
         return MTB_ERR_DB;
     }
     return MTB_OK;
+}
+
+// The reference's match-buffer exhaustion is a retry (KmerMatcher.cpp:474-476 returns false,
+// Classifier.cpp:127-130 enlarges matchPerKmer and searches that split again). Here the batch
+// workspace grows with the batch's matches, so running out of HBM (or of MTB_WORKSPACE_CAP) is
+// MTB_RETRY: the context stays usable (the failed buffer is gone, the others are reused, every
+// stage is rerun by the next call) and the caller classifies the batch in smaller pieces
+// (mtb_start_classify halves it down to one read).
+int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const char* seq2, const uint64_t* off2,
+                       uint32_t n, uint32_t flags, mtb_result* results) {
+    const int rc = classify_batch(c, seq, off, seq2, off2, n, flags, results);
+    if (rc != MTB_ERR_OOM) return rc;
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(c->stream);
+    // the buffers the failed attempt grew would otherwise stay at its size: the pieces start clean
+    const double held = c->ws.used * 1e-9;
+    for (DevBuf* b : batch_bufs(c)) b->release();
+    c->nReads = 0;
+    c->M = c->Q = c->Qall = c->nTaxcnt = 0;
+    c->sparse = false;
+    c->emValid = c->emPackedValid = false;
+    char msg[200];
+    snprintf(msg, sizeof msg, "out of HBM for the workspace of a %u-read batch (%.2f GB held%s): classify it in smaller "
+             "pieces", n, held, c->ws.cap ? ", capped" : "");
+    set_error(msg);
+    return MTB_RETRY;
 }
 
 int mtb_get_taxcnt(mtb_ctx* c, mtb_taxcnt* out, uint64_t cap, uint64_t* n_out) {
@@ -1298,6 +1368,8 @@ void ctx_release_workspace(mtb_ctx* c) {
 }
 
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache; }
+
+const mtb_params& ctx_params(const mtb_ctx* c) { return c->par; }
 
 uint64_t ctx_workspace_bytes(const mtb_ctx* c) {
     uint64_t b = 0;

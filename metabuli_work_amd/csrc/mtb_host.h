@@ -60,6 +60,7 @@ void ctx_release_workspace(mtb_ctx* c);
 // Host-side state the file pipeline keeps in a context between runs (its pinned batch slots),
 // destroyed with the context on its device.
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c);
+const mtb_params& ctx_params(const mtb_ctx* c);
 
 void set_error(const std::string& msg);
 HostTables make_tables();

@@ -221,6 +221,15 @@ std::shared_ptr<Mapping> map_plain(const char* path) {
     return m;
 }
 
+// What an idle object must not keep: a parse job that was never parsed (a stopped or failed run)
+// still holds its raw buffer or the file's mapping, and its hold on the mapping's parts.
+inline void on_idle(RawBuf&) {}
+inline void on_idle(ParseJob& j) {
+    if (j.map) j.map->release(j.b, j.e);
+    j.map = nullptr;
+    j.raw.reset();
+}
+
 // A free list of T: objects come back when their last shared_ptr goes, so the input's bytes flow
 // through the same few buffers instead of freshly mapped (page-faulting) ones per chunk.
 template <typename T>
@@ -243,6 +252,7 @@ struct Recycler : std::enable_shared_from_this<Recycler<T>> {
         if (!x) x.reset(make());
         auto self = this->shared_from_this();
         return std::shared_ptr<T>(x.release(), [self](T* t) {
+            on_idle(*t);
             std::lock_guard<std::mutex> l(self->mu);
             self->idle.emplace_back(t);
         });
@@ -547,6 +557,81 @@ struct Cursor {
     }
 };
 
+// One uploaded batch on its context: results into s->res, its taxID:count lists into s->tc, its
+// --em mappings into s->em. A batch whose workspace does not fit (MTB_RETRY: out of HBM) is
+// classified in halves, recursively down to one read, as the reference searches a split again
+// after its match buffer ran out (Classifier.cpp:127-130); the piece size that fitted bounds the
+// context's later batches (cap, as matchPerKmer stays raised). Pieces are read ranges of the
+// uploaded batch (the offsets stay absolute), their lists appended with rebased offsets.
+static int classify_piece(mtb_ctx* c, Slot* s, bool paired, uint32_t lo, uint32_t hi) {
+    return mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p + lo,
+                              paired ? (const char*)s->dseq2.p : nullptr,
+                              paired ? (const uint64_t*)s->doff2.p + lo : nullptr, hi - lo, MTB_INPUT_DEVICE,
+                              s->res.p + lo);
+}
+
+static int piece_mappings(mtb_ctx* c, Slot* s, uint32_t lo) {
+    uint64_t nm = 0;
+    int rc = mtb_get_em_mappings(c, (uint32_t)(s->firstRead + lo), nullptr, 0, &nm);
+    if (rc == MTB_RETRY || (rc == MTB_OK && nm)) {
+        const size_t at = s->em.size();
+        s->em.resize(at + nm);
+        rc = mtb_get_em_mappings(c, (uint32_t)(s->firstRead + lo), s->em.data() + at, nm, &nm);
+    }
+    return rc;
+}
+
+static int classify_slot(mtb_ctx* c, Slot* s, bool paired, bool em, uint32_t& cap, std::atomic<uint64_t>& split) {
+    if (!cap || s->n <= cap) {  // the whole batch at once (the usual case)
+        int rc = classify_piece(c, s, paired, 0, s->n);
+        if (rc == MTB_OK) {
+            uint64_t nt = 0;
+            mtb_get_taxcnt(c, nullptr, 0, &nt);
+            rc = s->tc.ensure(std::max<uint64_t>(nt, 1)) == hipSuccess ? mtb_get_taxcnt(c, s->tc.p, s->tc.cap, &nt)
+                                                                     : MTB_ERR_OOM;
+            if (rc == MTB_OK && em) rc = piece_mappings(c, s, 0);
+            return rc;
+        }
+        if (rc != MTB_RETRY || s->n < 2) return rc == MTB_RETRY ? MTB_ERR_OOM : rc;
+        cap = s->n / 2;
+        fprintf(stderr, "[mtb] batch %llu: %s; classifying it in pieces of <= %u reads\n",
+                (unsigned long long)s->index, mtb_last_error(), cap);
+    }
+    split++;
+    std::deque<std::pair<uint32_t, uint32_t>> todo;
+    for (uint32_t lo = 0; lo < s->n; lo += cap) todo.push_back({lo, std::min<uint32_t>(s->n, lo + cap)});
+    std::vector<mtb_taxcnt> tc;
+    while (!todo.empty()) {
+        const uint32_t lo = todo.front().first, hi = todo.front().second;
+        int rc = classify_piece(c, s, paired, lo, hi);
+        if (rc == MTB_RETRY && hi - lo > 1) {  // halve the piece, and every later one
+            const uint32_t mid = lo + (hi - lo) / 2;
+            todo.pop_front();
+            todo.push_front({mid, hi});
+            todo.push_front({lo, mid});
+            if (mid - lo < cap) {
+                cap = mid - lo;
+                fprintf(stderr, "[mtb] batch %llu: %s; pieces of <= %u reads\n", (unsigned long long)s->index,
+                        mtb_last_error(), cap);
+            }
+            continue;
+        }
+        if (rc != MTB_OK) return rc == MTB_RETRY ? MTB_ERR_OOM : rc;
+        todo.pop_front();
+        uint64_t nt = 0;
+        mtb_get_taxcnt(c, nullptr, 0, &nt);
+        const size_t at = tc.size();
+        tc.resize(at + nt);
+        rc = mtb_get_taxcnt(c, tc.data() + at, nt, &nt);
+        if (rc != MTB_OK) return rc;
+        for (uint32_t i = lo; i < hi; i++) s->res.p[i].taxcnt_offset += (uint32_t)at;
+        if (em && (rc = piece_mappings(c, s, lo)) != MTB_OK) return rc;
+    }
+    if (s->tc.ensure(std::max<size_t>(tc.size(), 1)) != hipSuccess) return MTB_ERR_OOM;
+    std::copy(tc.begin(), tc.end(), s->tc.p);
+    return MTB_OK;
+}
+
 }  // namespace
 
 extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mtb_classify_stats* stats) {
@@ -572,6 +657,20 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 return MTB_ERR_ARG;
             }
     mtb_ctx* const ctx0 = ctxs[0];  // the writers' taxonomy, the report and --em
+    // every context must classify a batch as ctx0 would: the same parameters (host threads aside)
+    // over the whole of the same DB
+    for (int d = 0; d < nCtx; d++) {
+        mtb_params a = mtb::ctx_params(ctxs[d]), b = mtb::ctx_params(ctx0);
+        if (a.db_parts > 1) {
+            set_error("a context holds one part of a range-partitioned DB: use mtb_start_classify_partitioned");
+            return MTB_ERR_ARG;
+        }
+        a.threads = b.threads = 0;
+        if (memcmp(&a, &b, sizeof a) != 0 || mtb_db_kmers(ctxs[d]) != mtb_db_kmers(ctx0)) {
+            set_error("the contexts differ in their parameters or DB: batches would be classified differently");
+            return MTB_ERR_ARG;
+        }
+    }
     const auto t0 = Clock::now();
     const bool paired = opt->query2 != nullptr;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -839,6 +938,10 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     const bool em = opt->em_tsv || opt->em_report_tsv || opt->em_reclassify_report_tsv;
     // GPU workers, one per context: every batch they take goes on to the writer
     std::vector<double> waitS(nCtx, 0.0);
+    // per context: the most reads a batch piece may hold after the workspace ran out (0: no limit)
+    std::vector<uint32_t> pieceCap(nCtx, 0);
+    std::atomic<uint64_t> splitBatches{0};
+    if (const char* e = getenv("MTB_PIECE_READS")) pieceCap.assign(nCtx, (uint32_t)strtoul(e, nullptr, 10));  // tests
     std::vector<std::thread> workers;
     for (int d = 0; d < nCtx; d++)
         workers.emplace_back([&, d] {
@@ -867,32 +970,12 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                 // the workspace and overlap
                 std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(c)), std::defer_lock);
                 if (s->index < kRamp + (uint64_t)nCtx) gl.lock();
-                if (rc == MTB_OK)
-                    rc = mtb_classify_batch(c, (const char*)s->dseq1.p, (const uint64_t*)s->doff1.p,
-                                            paired ? (const char*)s->dseq2.p : nullptr,
-                                            paired ? (const uint64_t*)s->doff2.p : nullptr, s->n, MTB_INPUT_DEVICE,
-                                            s->res.p);
+                if (rc == MTB_OK && em && s->firstRead + s->n > 0xFFFFFFFFull) {
+                    rc = MTB_ERR_ARG;
+                    mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
+                }
+                if (rc == MTB_OK) rc = classify_slot(c, s, paired, em, pieceCap[d], splitBatches);
                 if (gl.owns_lock()) gl.unlock();
-                uint64_t nt = 0;
-                if (rc == MTB_OK) {
-                    mtb_get_taxcnt(c, nullptr, 0, &nt);
-                    rc = s->tc.ensure(std::max<uint64_t>(nt, 1)) == hipSuccess
-                             ? mtb_get_taxcnt(c, s->tc.p, s->tc.cap, &nt)
-                             : MTB_ERR_OOM;
-                }
-                if (rc == MTB_OK && em) {
-                    if (s->firstRead + s->n > 0xFFFFFFFFull) {
-                        rc = MTB_ERR_ARG;
-                        mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
-                    } else {
-                        uint64_t nm = 0;
-                        rc = mtb_get_em_mappings(c, (uint32_t)s->firstRead, nullptr, 0, &nm);
-                        if (rc == MTB_RETRY || (rc == MTB_OK && nm)) {
-                            s->em.resize(nm);
-                            rc = mtb_get_em_mappings(c, (uint32_t)s->firstRead, s->em.data(), nm, &nm);
-                        }
-                    }
-                }
                 s->gpuS = secs(g0, Clock::now());
                 s->tGpu1 = s->tGpu0 + s->gpuS;
                 if (trace) {
@@ -1085,6 +1168,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         stats->parse_s = (double)(m1.parseNs + m2.parseNs) * 1e-9;
         stats->fill_s = fillS;
         stats->first_batch_s = firstBatchS;
+        stats->split_batches = splitBatches;
     }
     return MTB_OK;
 }

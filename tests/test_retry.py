@@ -1,0 +1,88 @@
+"""HBM exhaustion as the reference's retry (KmerMatcher.cpp:474-476 returns false, Classifier.cpp:127-130
+searches the split again): a batch whose workspace passes the context's cap (mtb_set_workspace_cap,
+MTB_WORKSPACE_CAP) returns MTB_RETRY with the context usable, and the callers classify it in pieces —
+Classifier.classify_batch in halves, mtb_start_classify halving down to one read. The results equal the
+one-batch run and the oracle's."""
+import numpy as np
+import pytest
+
+from metabuli_work_amd import synth
+from metabuli_work_amd.classifier import Classifier, LocalParameters
+from tests import oracle_ctypes as oc
+
+
+def _same(a, b):
+    assert np.array_equal(a.results["classification"], b.results["classification"])
+    assert np.array_equal(a.results["score"].view(np.uint32), b.results["score"].view(np.uint32))
+    assert np.array_equal(a.results["hamming_dist"], b.results["hamming_dist"])
+    for i in range(len(a.results)):
+        assert a.taxcnt_of(i) == b.taxcnt_of(i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frac", [0.6, 0.3])
+def test_classify_batch_split_on_retry(make_db, frac):
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 1500, paired=True, seed=61, short_frac=0.03)
+    par = LocalParameters(seqMode=2)
+    par.load_db_parameters(db_dir)
+    with Classifier(par, db_dir=db_dir) as full:
+        ref = full.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        ws = full.workspace_bytes
+    assert ws > 0
+    with Classifier(par, db_dir=db_dir) as capped:
+        capped.set_workspace_cap(int(ws * frac))
+        got = capped.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        assert capped.workspace_bytes <= int(ws * frac)
+        _same(got, ref)
+        # the context stays usable: a batch that fits runs whole
+        small = capped.classify_batch(r.seq1, r.off1[:101], r.seq2, r.off2[:101])
+        assert np.array_equal(small.results["classification"], ref.results["classification"][:100])
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    assert np.array_equal(got.results["classification"], ores["classification"])
+    assert np.array_equal(got.results["score"].view(np.uint32), ores["score"].view(np.uint32))
+    assert np.array_equal(got.taxcnt, otc)
+
+
+@pytest.mark.gpu
+def test_classify_batch_retry_raises_when_one_read_does_not_fit(make_db):
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 64, paired=True, seed=62)
+    par = LocalParameters(seqMode=2)
+    par.load_db_parameters(db_dir)
+    from metabuli_work_amd._lib import MtbError
+    with Classifier(par, db_dir=db_dir) as clf:
+        clf.set_workspace_cap(4096)
+        with pytest.raises(MtbError, match="out of HBM"):
+            clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        clf.set_workspace_cap(0)  # usable again once it fits
+        assert len(clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2).results) == r.n
+
+
+@pytest.mark.gpu
+def test_start_classify_splits_on_retry(make_db, tmp_path):
+    """The file pipeline halves a batch that does not fit and bounds the later batches by the piece
+    that did; the TSV and report are byte-identical to the uncapped run."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 2400, paired=True, seed=63, short_frac=0.02)
+    p1, p2 = str(tmp_path / "q1.fq"), str(tmp_path / "q2.fq")
+    with open(p1, "wb") as f:
+        f.write(synth.fastq_bytes(r.seq1, r.off1, prefix="s"))
+    with open(p2, "wb") as f:
+        f.write(synth.fastq_bytes(r.seq2, r.off2, prefix="s"))
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    one, cut = str(tmp_path / "one.tsv"), str(tmp_path / "cut.tsv")
+    rep1, repc = str(tmp_path / "one_rep.tsv"), str(tmp_path / "cut_rep.tsv")
+    with Classifier(par, db_dir=db_dir) as clf:
+        assert clf.startClassify(one, reads_per_batch=800, report_tsv=rep1) == r.n
+        assert clf.last_run["split_batches"] == 0
+        ws = clf.workspace_bytes
+    with Classifier(par, db_dir=db_dir) as clf:
+        clf.set_workspace_cap(int(ws * 0.45))
+        assert clf.startClassify(cut, reads_per_batch=800, report_tsv=repc) == r.n
+        assert clf.last_run["split_batches"] >= 1
+    assert open(cut, "rb").read() == open(one, "rb").read()
+    assert open(repc, "rb").read() == open(rep1, "rb").read()
