@@ -125,6 +125,8 @@ struct mtb_ctx {
     int waveTaxon = -1;          // MTB_WAVE_TAXON=0/1/2: K6 chooseBestTaxon thread / wave / 16-lane group per read (default auto)
     int emulateAll = 0;          // MTB_EMULATE_SORT=1: k_combine_wave emulates std::sort for every run (tests)
     bool pruneCompact = true;    // MTB_PRUNE_COMPACT=0: big K5 segments are not thinned before their sort (tests)
+    bool noAlias = false;        // MTB_K6_ALIAS=0: K6 scratch in buffers of its own (A/B, tests)
+    uint64_t aliasBytes = 0;     // K6 scratch bytes of the last batch carved out of dead buffers
     int32_t* spOf = nullptr;
     int32_t maxTax = 0;
     int32_t *tNodeOf = nullptr, *tNodeTax = nullptr, *tParent = nullptr, *tDepth = nullptr, *tSpParent = nullptr;
@@ -338,6 +340,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_PRESENT_SHARE")) c->presentShare = std::max(1e-6, atof(e));  // tests: filter reruns
     if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : atoi(e) == 0 ? 0 : 2;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
+    if (const char* e = getenv("MTB_K6_ALIAS")) c->noAlias = atoi(e) == 0;
     if (c->forceGeneric) c->matchWinCap = 0;
     c->dir = make_aa_dir(c->D, par->kmer_format);
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
@@ -501,6 +504,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->waveTaxon = src->waveTaxon;
     c->emulateAll = src->emulateAll;
     c->pruneCompact = src->pruneCompact;
+    c->noAlias = src->noAlias;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -649,57 +653,104 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     }
     c->liveM = kM;
     c->stats[11] = kM;
-    // K6 scratch, per match K6 reads: sized by the live matches (less than half of all at GTDB scale)
+    // K6 scratch, per match K6 reads: sized by the live matches (less than half of all at GTDB scale).
+    // It is carved out of the batch buffers K5 left dead — the direct join's slot-sized segments,
+    // the query keys and slots, the unpruned sorted matches, K5's global scratch, the spill — and
+    // only what does not fit there takes buffers of its own: at GTDB scale that is ~25 GB per
+    // 2M-pair batch that the larger QuerySplits need.
     const uint64_t Kc = std::max<uint64_t>(kM, 1);
-    HIP_TRY(c->local.ensure(path_bytes() * Kc));
-    HIP_TRY(c->paths.ensure(path_bytes() * Kc));
-    HIP_TRY(c->comb.ensure(path_bytes() * Kc));
-    HIP_TRY(c->conn.ensure(Kc));
-    HIP_TRY(c->spScore.ensure(sizeof(float) * Kc));
-    HIP_TRY(c->spKeep.ensure(Kc));
-    HIP_TRY(c->waveList.ensure(sizeof(uint64_t) * Kc));
+    const uint64_t Mn = std::max<uint64_t>(Kc, n);  // K6 work lists: groups (<= live matches) and the read order
+    std::vector<std::pair<char*, size_t>> dead;      // (next free byte, bytes left) per dead buffer
+    if (!c->noAlias) {
+        std::vector<DevBuf*> d = {&c->mDirect, &c->segScratch, &c->mStage, &c->mRank, &c->matchWin, &c->chunkIn};
+        if (prune) {  // else the sorted matches are the result and the query keys stay readable (mtb_get_*)
+            for (DevBuf* b : {&c->matchesSorted, &c->keysA, &c->valsA, &c->keysB, &c->valsB}) d.push_back(b);
+        } else {
+            d.push_back(&c->matches);
+        }
+        for (DevBuf* b : d)
+            if (b->p && b->bytes >= (1u << 20)) dead.push_back({b->as<char>(), b->bytes});
+        std::sort(dead.begin(), dead.end(), [](auto& a, auto& b) { return a.second > b.second; });
+    }
+    struct Need {
+        DevBuf* own;
+        uint64_t bytes;
+        void* p;
+    };
+    Need need[] = {{&c->local, path_bytes() * Kc, nullptr},
+                   {&c->paths, path_bytes() * Kc, nullptr},
+                   {&c->comb, path_bytes() * Kc, nullptr},
+                   {&c->conn, Kc, nullptr},
+                   {&c->spScore, sizeof(float) * Kc, nullptr},
+                   {&c->spKeep, Kc, nullptr},
+                   {&c->waveList, sizeof(uint64_t) * Kc, nullptr},
+                   {&c->gFlag, sizeof(uint32_t) * (Kc + 1), nullptr},
+                   {&c->pathCnt, sizeof(uint32_t) * (Kc + 1), nullptr},
+                   {&c->sFlag, std::max<uint64_t>(sizeof(uint32_t) * (Kc + 1), run_index_tmp_bytes(Kc)), nullptr},
+                   {&c->gScan, sizeof(uint64_t) * (Kc + 1), nullptr},
+                   {&c->sScan, sizeof(uint64_t) * (Kc + 1), nullptr},
+                   {&c->gStart, sizeof(uint64_t) * (Kc + 1), nullptr},
+                   {&c->sStart, sizeof(uint64_t) * (Kc + 1), nullptr},
+                   {&c->clade, clade_bytes() * Kc * c->cladePerMatch, nullptr},
+                   {&c->tcPool, sizeof(mtb_taxcnt) * Kc, nullptr},
+                   {&c->ordKA, sizeof(uint64_t) * (Mn + 1), nullptr},
+                   {&c->ordVA, sizeof(uint64_t) * (Mn + 1), nullptr},
+                   {&c->ordKB, sizeof(uint64_t) * (Mn + 1), nullptr},
+                   {&c->ordVB, sizeof(uint64_t) * (Mn + 1), nullptr}};
+    std::vector<Need*> order;
+    for (Need& x : need) order.push_back(&x);
+    std::stable_sort(order.begin(), order.end(), [](Need* a, Need* b) { return a->bytes > b->bytes; });
+    c->aliasBytes = 0;
+    for (Need* x : order) {  // first fit, largest first; 256-B aligned pieces
+        const size_t b = (x->bytes + 255) & ~(size_t)255;
+        for (auto& r : dead)
+            if (r.second >= b) {
+                x->p = r.first;
+                r.first += b;
+                r.second -= b;
+                c->aliasBytes += b;
+                break;
+            }
+        if (!x->p) {
+            HIP_TRY(x->own->ensure(x->bytes));
+            x->p = x->own->p;
+        }
+    }
     HIP_TRY(c->waveCount.ensure(sizeof(uint32_t)));
-    for (DevBuf* b : {&c->gFlag, &c->pathCnt}) HIP_TRY(b->ensure(sizeof(uint32_t) * (Kc + 1)));
-    HIP_TRY(c->sFlag.ensure(std::max<uint64_t>(sizeof(uint32_t) * (Kc + 1), run_index_tmp_bytes(Kc))));
-    for (DevBuf* b : {&c->gScan, &c->sScan, &c->gStart, &c->sStart}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Kc + 1)));
-    HIP_TRY(c->clade.ensure(clade_bytes() * Kc * c->cladePerMatch));
-    HIP_TRY(c->tcPool.ensure(sizeof(mtb_taxcnt) * Kc));
     HIP_TRY(hipEventRecord(c->kev[11], s));
     HIP_TRY(hipEventRecord(c->kev[12], s));
-    // K6 work lists: groups (<= live matches) and the longest-first read order (n entries)
-    const uint64_t Mn = std::max<uint64_t>(Kc, n);
-    for (DevBuf* b : {&c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB}) HIP_TRY(b->ensure(sizeof(uint64_t) * (Mn + 1)));
     HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * radix_counts_elems(Mn + 1)));
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Mn + 1) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Mn + 1) + n + Mn + 2)));
     TaxDevice t{c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tFlags, c->tSpParent, c->maxTax};
-    AssignScratch sc{c->local.p,
-                     c->paths.p,
-                     c->comb.p,
-                     c->conn.as<uint8_t>(),
-                     c->gFlag.as<uint32_t>(),
-                     c->sFlag.as<uint32_t>(),
-                     c->pathCnt.as<uint32_t>(),
-                     c->gScan.as<uint64_t>(),
-                     c->sScan.as<uint64_t>(),
-                     c->gStart.as<uint64_t>(),
-                     c->sStart.as<uint64_t>(),
-                     c->spScore.as<float>(),
-                     c->waveList.as<uint64_t>(),
+    AssignScratch sc{need[0].p,
+                     need[1].p,
+                     need[2].p,
+                     (uint8_t*)need[3].p,
+                     (uint32_t*)need[7].p,
+                     (uint32_t*)need[9].p,
+                     (uint32_t*)need[8].p,
+                     (uint64_t*)need[10].p,
+                     (uint64_t*)need[11].p,
+                     (uint64_t*)need[12].p,
+                     (uint64_t*)need[13].p,
+                     (float*)need[4].p,
+                     (uint64_t*)need[6].p,
                      c->waveCount.as<uint32_t>(),
-                     c->spKeep.as<uint8_t>(),
+                     (uint8_t*)need[5].p,
                      c->scanTmp.p,
-                     c->ordKA.as<uint64_t>(),
-                     c->ordVA.as<uint64_t>(),
-                     c->ordKB.as<uint64_t>(),
-                     c->ordVB.as<uint64_t>(),
+                     (uint64_t*)need[16].p,
+                     (uint64_t*)need[17].p,
+                     (uint64_t*)need[18].p,
+                     (uint64_t*)need[19].p,
                      c->radixCounts.as<uint32_t>(),
                      c->radixOffs.as<uint64_t>(),
-                     c->clade.p,
+                     need[14].p,
                      c->cladePerMatch};
+    mtb_taxcnt* tcPool = (mtb_taxcnt*)need[15].p;
     c->stats[3] = M;
     c->stats[4] = maxSeg;
-    launch_assign(kIn, kOff, c->qlen.as<uint32_t>(), n, kM, a, t, sc, c->tcPool.as<mtb_taxcnt>(),
+    launch_assign(kIn, kOff, c->qlen.as<uint32_t>(), n, kM, a, t, sc, tcPool,
                   c->results.as<mtb_result>(), c->devStats.as<unsigned long long>(), c->stats + 5, s);
     HIP_TRY(hipEventRecord(c->kev[13], s));
     HIP_TRY(c->tcLen.ensure(sizeof(uint32_t) * (n + 1)));
@@ -710,7 +761,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     HIP_TRY(hipMemcpyAsync(&NT, c->tcOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(c->tcOut.ensure(sizeof(mtb_taxcnt) * std::max<uint64_t>(NT, 1)));
-    launch_compact_taxcnt(c->tcPool.as<mtb_taxcnt>(), kOff, c->results.as<mtb_result>(), c->tcOff.as<uint64_t>(), n,
+    launch_compact_taxcnt(tcPool, kOff, c->results.as<mtb_result>(), c->tcOff.as<uint64_t>(), n,
                           c->tcOut.as<mtb_taxcnt>(), s);
     c->nTaxcnt = NT;
     c->emValid = false;

@@ -84,3 +84,44 @@ def test_open_rejects_out_of_scope_params(tmp_path):
     p = _abi.default_params(reduced_aa=1)
     rc = lib().mtb_open(str(tmp_path).encode(), ctypes.byref(p), 0, ctypes.byref(h))
     assert rc < 0
+
+
+def abi_caller() -> pathlib.Path:
+    """tests/_abi_caller: the compiled C caller of include/mtb_gpu.h (built by __graft_entry__.build();
+    rebuilt here when missing or older than its source)."""
+    import __graft_entry__ as g
+
+    return g.build_abi_caller()
+
+
+def _mirrors():
+    from metabuli_work_amd import dbbuild
+
+    ct = {"mtb_params": _abi.MtbParams, "mtb_db_host": _abi.MtbDbHost, "mtb_db_resident": _abi.MtbDbResident,
+          "mtb_read_batch": _abi.MtbReadBatch, "mtb_classify_opts": _abi.MtbClassifyOpts,
+          "mtb_classify_stats": _abi.MtbClassifyStats, "mtb_em_stats": _abi.MtbEmStats,
+          "mtb_build_input": dbbuild.MtbBuildInput, "mtb_db_built": dbbuild.MtbDbBuilt}
+    nd = {"mtb_kmer": _abi.KMER_DTYPE, "mtb_match": _abi.MATCH_DTYPE, "mtb_result": _abi.RESULT_DTYPE,
+          "mtb_taxcnt": _abi.TAXCNT_DTYPE, "mtb_em_map": _abi.EM_MAP_DTYPE, "mtb_em_read": _abi.EM_READ_DTYPE}
+    return ct, nd
+
+
+def test_struct_layouts_match_compiled_c():
+    """sizeof / offsetof of every public struct as a C compiler lays out include/mtb_gpu.h equal the
+    Python mirrors the tests and bench pass through ctypes (a layout drift fails here)."""
+    import subprocess
+
+    out = subprocess.run([str(abi_caller()), "--layout"], check=True, capture_output=True, text=True).stdout
+    lay = json.loads(out)
+    ct, nd = _mirrors()
+    assert set(lay) == set(ct) | set(nd)
+    for name, cls in ct.items():
+        assert lay[name]["size"] == ctypes.sizeof(cls), name
+        assert list(lay[name]["fields"]) == [f for f, _ in cls._fields_], name
+        for f, off in lay[name]["fields"].items():
+            assert getattr(cls, f).offset == off, f"{name}.{f}"
+    for name, dt in nd.items():
+        assert lay[name]["size"] == dt.itemsize, name
+        assert list(lay[name]["fields"]) == list(dt.names), name
+        for f, off in lay[name]["fields"].items():
+            assert dt.fields[f][1] == off, f"{name}.{f}"
