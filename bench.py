@@ -268,6 +268,8 @@ def main():
                     help="config 5 on one GPU: DB parts, each timed in turn (with N >= 4 GPUs: one part per rank)")
     ap.add_argument("--c5-sample", type=int, default=24_000, help="config 5: read pairs of the oracle parity sample")
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
+    ap.add_argument("--cold-pairs", type=int, default=10_000_000,
+                    help="cold one-shot line: read pairs of the file classified by a freshly opened context (0 = off)")
     ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r04", "bench_detail.json"),
                     help="side file for the full result tree (per-kernel splits, work counters, config-5 parts, "
                          "e2e host stages); the stdout line keeps the headline and one-line summaries")
@@ -286,7 +288,7 @@ def main():
             args.cpu_sample = 0
             args.skip_config2 = True
             args.variants = ""
-            args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = 0
+            args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = args.cold_pairs = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.c5_only:
@@ -326,8 +328,10 @@ def main():
         for k, v in head.items():
             if k not in ("value", "ms_per_step"):
                 out[k] = v
+        if c2 is not None and c2.get("cold_run"):
+            out["cold_run"] = c2["cold_run"]
         if c3 is not None and c2 is not None:
-            out["config2"] = {k: v for k, v in c2.items() if k != "long_reads"}
+            out["config2"] = {k: v for k, v in c2.items() if k not in ("long_reads", "cold_run")}
         if c3 is not None and c3.get("long_reads") is not None:
             out["long_reads"] = c3["long_reads"]
             if c2 is not None and c2.get("long_reads") is not None:
@@ -533,8 +537,11 @@ def run_config2(args, world, rank, local, dev):
 
     # ---- long reads (seq mode 3, same DB): reads/s of the same pipeline on ~10 kb reads ----
     long_line = None
+    clf.close()
+    cold = None
+    if rank == 0 and world == 1 and args.cold_pairs > 0:
+        cold = run_cold(args, hdb, par, lp, s1, s2, n, (ores, otc) if parity is not None else None)
     if args.long_reads > 0:
-        clf.close()
         long_line = run_long_reads(args, lambda lpl: Classifier(lpl, db_host=hdb.c_struct(), device=local), ls1, lo1,
                                    long_n50, world, rank, dev, odb, cores, "the config-2 DB", hdb.n_kmers,
                                    "config2_long")
@@ -556,9 +563,68 @@ def run_config2(args, world, rank, local, dev):
         "parity_sample": parity,
         "work": work,
         "long_reads": long_line,
+        "cold_run": cold,
     }
-    clf.close()
     return out
+
+
+def run_cold(args, hdb, par, lp, s1, s2, n, check=None):
+    """A one-shot classify as a user runs it: the config-2 DB written as the
+    reference's files (diffIdx, info, split, taxID_list, taxonomy/*.dmp; /dev/shm, so the page cache
+    and not a disk is read), mtb_open from that directory into a fresh context, then the context's
+    first mtb_start_classify over a 10M-pair plain FASTQ (the config-2 batch's pairs, repeated) and a
+    second, steady one. open_s has its phases (mtb_open_phases); first_run is what one CLI call pays
+    after the open; steady is a warm context's rate."""
+    import shutil
+    import tempfile
+
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    d = tempfile.mkdtemp(prefix="mtb_cold_", dir=base)
+    L = 150
+    try:
+        tw = time.perf_counter()
+        hdb.write(os.path.join(d, "db"), par)
+        reps = max(1, args.cold_pairs // n)
+        off = np.arange(n + 1, dtype=np.uint64) * L
+        for mate, (sq, pre) in enumerate(((s1, "a"), (s2, "b"))):
+            body = synth.fastq_bytes(sq[:n * L].cpu().numpy(), off, prefix=pre)
+            with open(os.path.join(d, f"q{mate + 1}.fq"), "wb") as f:
+                for _ in range(reps):
+                    f.write(body)
+            del body
+        prep = time.perf_counter() - tw
+        q1, q2 = os.path.join(d, "q1.fq"), os.path.join(d, "q2.fq")
+        lpc = LocalParameters(seqMode=2, filenames=[q1, q2, os.path.join(d, "db")])
+        t0 = time.perf_counter()
+        clf = Classifier(lpc, db_dir=os.path.join(d, "db"))
+        open_s = time.perf_counter() - t0
+        phases = clf.open_phases()
+        tsv = os.path.join(d, "out.tsv")
+        runs = []
+        try:
+            for _ in range(3):
+                t1 = time.perf_counter()
+                got = clf.startClassify(tsv, report_tsv=os.path.join(d, "report.tsv"))
+                runs.append((time.perf_counter() - t1, dict(clf.last_run)))
+                if len(runs) == 1 and check is not None:
+                    ok = tsv_matches_oracle(tsv, *check)
+        finally:
+            clf.close()
+        steady = sorted(w for w, _ in runs[1:])[len(runs[1:]) // 2]
+        out = {"open_s": round(open_s, 3), "open_phases_s": phases,
+               "first_run_reads_per_s": round(got / runs[0][0], 1), "steady_reads_per_s": round(got / steady, 1),
+               "one_shot_reads_per_s": round(got / (open_s + runs[0][0]), 1),
+               "read_pairs": got, "db_kmers": hdb.n_kmers, "db_file_bytes": hdb.nbytes,
+               "first_run": {k: round(v, 3) for k, v in runs[0][1].items() if k.endswith("_s")},
+               "first_run_batches": int(runs[0][1]["batches"]), "file_prep_s": round(prep, 1),
+               "tsv_matches_oracle": ok if check is not None else None,
+               "what": "config-2 DB as files in /dev/shm, mtb_open into a fresh context, its first startClassify "
+                       f"over {got} read pairs (plain FASTQ), then two more (steady: the faster)"}
+        log(0, f"[bench] cold run: open {open_s:.2f}s {phases}, first {out['first_run_reads_per_s'] / 1e6:.2f}M, "
+               f"steady {out['steady_reads_per_s'] / 1e6:.2f}M pairs/s")
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, db_name, db_kmers, workload):

@@ -156,6 +156,14 @@ class Classifier:
         """Device bytes of the batch workspace the context holds (mtb_workspace_bytes)."""
         return int(lib().mtb_workspace_bytes(self.handle))
 
+    OPEN_PHASES = ["read_s", "decode_s", "directory_s", "probe_lines_s", "run_index_s", "taxonomy_s", "total_s"]
+
+    def open_phases(self) -> dict:
+        """Seconds of the context's open by phase (mtb_open_phases)."""
+        out = (ctypes.c_double * len(self.OPEN_PHASES))()
+        lib().mtb_open_phases(self.handle, out, len(self.OPEN_PHASES))
+        return {k: round(float(v), 3) for k, v in zip(self.OPEN_PHASES, out)}
+
     def set_workspace_cap(self, nbytes: int) -> None:
         """Cap the batch workspace (0 = none): a batch past it is classified in pieces."""
         check(lib().mtb_set_workspace_cap(self.handle, int(nbytes)), "mtb_set_workspace_cap")

@@ -154,6 +154,9 @@ struct mtb_ctx {
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
+    // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
+    // probe lines, run index, taxonomy + species map, and the whole open
+    double openS[7] = {0, 0, 0, 0, 0, 0, 0};
     static constexpr int kNumStats = 16;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
@@ -244,8 +247,16 @@ static int validate_params(const mtb_params* p) {
     return MTB_OK;
 }
 
+static double since(std::chrono::steady_clock::time_point& t) {
+    const auto now = std::chrono::steady_clock::now();
+    const double d = std::chrono::duration<double>(now - t).count();
+    t = now;
+    return d;
+}
+
 static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out,
-                       const mtb_db_resident* res = nullptr) {
+                       const mtb_db_resident* res = nullptr, double readS = 0) {
+    auto t0 = std::chrono::steady_clock::now(), tp = t0;
     int rc = validate_params(par);
     if (rc != MTB_OK) return rc;
     if (res) {
@@ -262,6 +273,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     c->device = device;
     c->par = *par;
     c->tables = make_tables();
+    c->openS[0] = readS;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->ownStream = true;
@@ -319,6 +331,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->rankLo = ((uint64_t)ends[0].hi << 32 | ends[0].lo) >> 24;
         c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
+    c->openS[1] = since(tp);
     if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e));  // A/B only: invalid results
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
@@ -346,11 +359,15 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     HIP_TRY(hipMalloc(&c->dirMem, (c->dir.R + 1) * sizeof(uint64_t)));
     c->dir.dir = c->dirMem;
     build_aa_dir(c->db, c->D, c->dir, c->dirMem, s);
+    HIP_TRY(hipStreamSynchronize(s));
+    c->openS[2] = since(tp);
     if (const char* e = getenv("MTB_JOIN")) c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : 0;
     if (!c->forceGeneric) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
         build_probe_lines(c->db, c->D, c->dir, c->lines, s);
+        HIP_TRY(hipStreamSynchronize(s));
+        c->openS[3] = since(tp);
         const char* ri = getenv("MTB_RUN_INDEX");  // 0: no run index (the unstaged join gallops)
         if (!ri || atoi(ri) != 0) {
             uint32_t* pop = nullptr;
@@ -370,6 +387,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
     HIP_TRY(hipStreamSynchronize(s));
+    c->openS[4] = since(tp);
     // taxonomy + taxId2speciesId
     const HostTaxonomy& T = db.tax;
     c->maxTax = T.maxTax;
@@ -399,6 +417,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf,
                         c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     bind_workspace(c, 0);
+    c->openS[5] = since(tp);
+    c->openS[6] = readS + std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *out = c;
     return MTB_OK;
 }
@@ -408,8 +428,10 @@ extern "C" {
 int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** out) {
     if (!db_dir || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
     HostDb db;
+    const auto t0 = std::chrono::steady_clock::now();
     if (!load_db_files(db_dir, db)) return MTB_ERR_IO;
-    const int rc = open_common(db, par, device, out);
+    const double readS = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const int rc = open_common(db, par, device, out, nullptr, readS);
     if (rc == MTB_OK) (*out)->dbDir = db_dir;  // --em: sp2uniqKmerCnt lives next to the DB files
     return rc;
 }
@@ -553,6 +575,12 @@ int mtb_set_stream(mtb_ctx* c, void* stream) {
 uint64_t mtb_db_kmers(const mtb_ctx* c) { return c ? c->D : 0; }
 
 uint64_t mtb_workspace_bytes(const mtb_ctx* c) { return c ? c->ws.used : 0; }
+
+int mtb_open_phases(const mtb_ctx* c, double* sec, int n) {
+    if (!c || !sec) return MTB_ERR_ARG;
+    for (int i = 0; i < n && i < 7; i++) sec[i] = c->openS[i];
+    return MTB_OK;
+}
 
 int mtb_set_workspace_cap(mtb_ctx* c, uint64_t bytes) {
     if (!c) return MTB_ERR_ARG;
