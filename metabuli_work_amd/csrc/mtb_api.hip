@@ -266,7 +266,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         if (!res->records || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
     } else {
         if (!check_db(db)) return MTB_ERR_DB;
-        if (db.info.size() < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
+        if (db.nInfo < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
         if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
     }
     mtb_ctx* c = new mtb_ctx();
@@ -290,28 +290,44 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         launch_rec_mask_info(c->db, c->D, mask, s);
         if (par->kmer_format == 2 && !res->rank_form) launch_rec_rank_form(c->db, c->D, s);
     } else {
-        c->D = db.info.size();
+        c->D = db.nInfo;
         // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381), then one record per k-mer
         uint16_t* dDiff = nullptr;
         uint32_t* dFlag = nullptr;
         uint64_t *dIdx = nullptr, *dVal = nullptr;
         uint32_t* dInfo = nullptr;
         void* dTmp = nullptr;
-        const uint64_t nDiff = db.diffIdx.size();
+        const uint64_t nDiff = db.nDiff;
         HIP_TRY(hipMalloc(&dVal, c->D * sizeof(uint64_t)));
         HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
         HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
         HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
-        HIP_TRY(hipMemcpyAsync(dDiff, db.diffIdx.data(), nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-        decode_diff_idx(dDiff, nDiff, dVal, c->D, dFlag, dIdx, dTmp, s);
+        if (!db.diffFile.empty()) {
+            HIP_TRY(hipStreamSynchronize(s));
+            if (!read_to_device(db.diffFile, dDiff, nDiff * sizeof(uint16_t))) return MTB_ERR_IO;
+        } else {
+            HIP_TRY(hipMemcpyAsync(dDiff, db.diffP, nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+        }
+        const uint64_t terms = decode_diff_idx(dDiff, nDiff, dVal, c->D, dFlag, dIdx, dTmp, s);
+        if (terms != c->D) {  // validateDatabase.cpp:78-131 (checked before the decode writes by k-mer index)
+            set_error(terms == ~0ull ? "diffIdx ends mid k-mer"
+                                     : "diffIdx k-mer count " + std::to_string(terms) + " != info entries " +
+                                           std::to_string(c->D));
+            hipFree(dDiff); hipFree(dFlag); hipFree(dIdx); hipFree(dTmp); hipFree(dVal);
+            return MTB_ERR_DB;
+        }
         HIP_TRY(hipStreamSynchronize(s));
         hipFree(dDiff);
         hipFree(dFlag);
         hipFree(dIdx);
         hipFree(dTmp);
         HIP_TRY(hipMalloc(&dInfo, c->D * sizeof(uint32_t)));
-        HIP_TRY(hipMemcpyAsync(dInfo, db.info.data(), c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        if (!db.infoFile.empty()) {
+            if (!read_to_device(db.infoFile, dInfo, c->D * sizeof(uint32_t))) return MTB_ERR_IO;
+        } else {
+            HIP_TRY(hipMemcpyAsync(dInfo, db.infoP, c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        }
         launch_mask_info(dInfo, c->D, mask, s);
         if (par->kmer_format == 2) launch_to_rank_form(dVal, c->D, s);
         HIP_TRY(hipMalloc(&c->db, (c->D + kDbPad) * sizeof(DbRec)));
@@ -429,7 +445,8 @@ int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** ou
     if (!db_dir || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
     HostDb db;
     const auto t0 = std::chrono::steady_clock::now();
-    if (!load_db_files(db_dir, db)) return MTB_ERR_IO;
+    // a whole-DB context reads diffIdx / info straight into HBM; a partition is cut on the host
+    if (!load_db_files(db_dir, db, par->db_parts <= 1)) return MTB_ERR_IO;
     const double readS = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const int rc = open_common(db, par, device, out, nullptr, readS);
     if (rc == MTB_OK) (*out)->dbDir = db_dir;  // --em: sp2uniqKmerCnt lives next to the DB files
@@ -439,8 +456,16 @@ int mtb_open(const char* db_dir, const mtb_params* par, int device, mtb_ctx** ou
 int mtb_open_host(const mtb_db_host* h, const mtb_params* par, int device, mtb_ctx** out) {
     if (!h || !par || !out) { set_error("null argument"); return MTB_ERR_ARG; }
     HostDb db;
-    db.diffIdx.assign(h->diff_idx, h->diff_idx + h->n_diff_idx);
-    db.info.assign(h->info, h->info + h->n_info);
+    if (par->db_parts > 1) {  // the part is cut from host copies
+        db.diffIdx.assign(h->diff_idx, h->diff_idx + h->n_diff_idx);
+        db.info.assign(h->info, h->info + h->n_info);
+        db.use_vectors();
+    } else {  // the caller's arrays, uploaded in place
+        db.diffP = h->diff_idx;
+        db.nDiff = h->n_diff_idx;
+        db.infoP = h->info;
+        db.nInfo = h->n_info;
+    }
     if (h->split) db.split.assign(h->split, h->split + 3 * h->n_split);
     db.taxIdList.assign(h->taxid_list, h->taxid_list + h->n_taxid_list);
     std::vector<std::string> ranks(h->n_nodes), names(h->n_nodes);

@@ -10,8 +10,15 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <fstream>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
 
 namespace mtb {
@@ -309,10 +316,22 @@ bool build_species_map(HostDb& db) {
     return true;
 }
 
-bool load_db_files(const std::string& dir, HostDb& db) {
-    if (!read_file(dir + "/diffIdx", db.diffIdx) || !read_file(dir + "/info", db.info)) {
+bool load_db_files(const std::string& dir, HostDb& db, bool stream) {
+    if (stream) {
+        struct stat a, b;
+        if (stat((dir + "/diffIdx").c_str(), &a) != 0 || stat((dir + "/info").c_str(), &b) != 0) {
+            set_error("cannot read " + dir + "/diffIdx or /info");
+            return false;
+        }
+        db.diffFile = dir + "/diffIdx";
+        db.infoFile = dir + "/info";
+        db.nDiff = (uint64_t)a.st_size / sizeof(uint16_t);
+        db.nInfo = (uint64_t)b.st_size / sizeof(uint32_t);
+    } else if (!read_file(dir + "/diffIdx", db.diffIdx) || !read_file(dir + "/info", db.info)) {
         set_error("cannot read " + dir + "/diffIdx or /info");
         return false;
+    } else {
+        db.use_vectors();
     }
     read_file(dir + "/split", db.split);
     std::ifstream tl(dir + "/taxID_list");
@@ -330,15 +349,75 @@ bool load_db_files(const std::string& dir, HostDb& db) {
 }
 
 bool check_db(const HostDb& db) {
-    // validateDatabase.cpp:78-131: terminal 0x8000 fragments == info entries.
+    // validateDatabase.cpp:78-131: terminal 0x8000 fragments == info entries (a streamed DB is
+    // checked on the device, before its decode writes by k-mer index: decode_diff_idx)
+    if (!db.diffP) {
+        if (db.nDiff == 0 && db.nInfo > 0) { set_error("diffIdx is empty but info is not"); return false; }
+        return true;
+    }
     uint64_t terms = 0;
-    for (uint16_t w : db.diffIdx) terms += (w & 0x8000u) ? 1 : 0;
-    if (terms != db.info.size()) {
-        set_error("diffIdx k-mer count " + std::to_string(terms) + " != info entries " + std::to_string(db.info.size()));
+    for (uint64_t i = 0; i < db.nDiff; i++) terms += (db.diffP[i] & 0x8000u) ? 1 : 0;
+    if (terms != db.nInfo) {
+        set_error("diffIdx k-mer count " + std::to_string(terms) + " != info entries " + std::to_string(db.nInfo));
         return false;
     }
-    if (!db.diffIdx.empty() && !(db.diffIdx.back() & 0x8000u)) { set_error("diffIdx ends mid k-mer"); return false; }
+    if (db.nDiff && !(db.diffP[db.nDiff - 1] & 0x8000u)) { set_error("diffIdx ends mid k-mer"); return false; }
     return true;
+}
+
+bool read_to_device(const std::string& path, void* dst, uint64_t bytes) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) { set_error("cannot read " + path); return false; }
+    constexpr uint64_t kChunk = 32ull << 20;
+    const unsigned nThreads = (unsigned)std::min<uint64_t>(8, (bytes + kChunk - 1) / kChunk);
+    std::atomic<uint64_t> next{0};
+    std::atomic<bool> ok{true};
+    std::string err;
+    std::mutex errMu;
+    int dev = 0;
+    hipGetDevice(&dev);
+    auto work = [&] {
+        hipSetDevice(dev);
+        hipStream_t st = nullptr;
+        char* buf[2] = {nullptr, nullptr};
+        hipEvent_t done[2] = {nullptr, nullptr};
+        bool good = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+        for (int k = 0; k < 2 && good; k++)
+            good = hipHostMalloc((void**)&buf[k], kChunk, hipHostMallocDefault) == hipSuccess &&
+                   hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; good && ok;) {  // alternate two buffers: read one while the other uploads
+            const uint64_t at = next.fetch_add(kChunk);
+            if (at >= bytes) break;
+            const uint64_t len = std::min(kChunk, bytes - at);
+            if (hipEventSynchronize(done[k]) != hipSuccess) { good = false; break; }
+            for (uint64_t got = 0; got < len;) {
+                const ssize_t r = pread(fd, buf[k] + got, len - got, (off_t)(at + got));
+                if (r <= 0) { good = false; break; }
+                got += (uint64_t)r;
+            }
+            good = good && hipMemcpyAsync((char*)dst + at, buf[k], len, hipMemcpyHostToDevice, st) == hipSuccess &&
+                   hipEventRecord(done[k], st) == hipSuccess;
+            k ^= 1;
+        }
+        if (st) good = hipStreamSynchronize(st) == hipSuccess && good;
+        for (int k = 0; k < 2; k++) {
+            if (buf[k]) hipHostFree(buf[k]);
+            if (done[k]) hipEventDestroy(done[k]);
+        }
+        if (st) hipStreamDestroy(st);
+        if (!good) {
+            ok = false;
+            std::lock_guard<std::mutex> l(errMu);
+            err = "cannot read or upload " + path;
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nThreads; t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    close(fd);
+    if (!ok) set_error(err);
+    return ok;
 }
 
 // ---- range partition of the DB at split entries -------------------------
@@ -396,6 +475,7 @@ bool slice_db_part(HostDb& db, int part, int parts) {
     if (parts <= 1) return true;
     if (part < 0 || part >= parts) { set_error("db_part out of range"); return false; }
     if (db.split.size() < 6) { set_error("partitioned DB needs the split file"); return false; }
+    if (db.diffIdx.size() != db.nDiff) { set_error("internal: a partitioned open needs the host diffIdx"); return false; }
     const uint64_t D = db.info.size(), nSplit = db.split.size() / 3;
     std::vector<uint64_t> start, entry;
     if (!partition_bounds(db.split.data(), nSplit, D, parts, start, entry)) return false;
@@ -422,6 +502,7 @@ bool slice_db_part(HostDb& db, int part, int parts) {
     std::vector<uint32_t> info(db.info.begin() + s0, db.info.begin() + iEnd);
     db.diffIdx.swap(diff);
     db.info.swap(info);
+    db.use_vectors();
     return check_db(db);  // terminal words == info entries
 }
 

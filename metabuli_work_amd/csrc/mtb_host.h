@@ -38,6 +38,19 @@ struct HostTaxonomy {
 struct HostDb {
     std::vector<uint16_t> diffIdx;
     std::vector<uint32_t> info;
+    // diffIdx / info as the open reads them: views of the vectors above or of the caller's arrays
+    // (mtb_open_host), or, with the file names set, read straight into device memory (mtb_open:
+    // the host never holds them)
+    const uint16_t* diffP = nullptr;
+    const uint32_t* infoP = nullptr;
+    uint64_t nDiff = 0, nInfo = 0;
+    std::string diffFile, infoFile;
+    void use_vectors() {
+        diffP = diffIdx.data();
+        nDiff = diffIdx.size();
+        infoP = info.data();
+        nInfo = info.size();
+    }
     std::vector<uint64_t> split;  // 3 words per DiffIdxSplit
     std::vector<int32_t> taxIdList;
     HostTaxonomy tax;
@@ -72,7 +85,11 @@ bool load_dmp(const std::string& dir, HostTaxonomy& out);
 constexpr int32_t kTaxonomyDbVersion = 2;  // NcbiTaxonomy::SERIALIZATION_VERSION (MMseqs2, unpinned)
 int load_taxonomy_db(const std::string& path, HostTaxonomy& out);
 bool build_species_map(HostDb& db);
-bool load_db_files(const std::string& dir, HostDb& db);
+// stream: diffIdx / info are left in their files (read_to_device at open) instead of host vectors
+bool load_db_files(const std::string& dir, HostDb& db, bool stream = false);
+// `bytes` of a file into device memory: parallel reads into pinned staging buffers, each uploaded
+// as soon as it is full (the file read and the PCIe upload overlap); false + set_error on failure
+bool read_to_device(const std::string& path, void* dst, uint64_t bytes);
 bool check_db(const HostDb& db);
 bool partition_bounds(const uint64_t* split, uint64_t nSplit, uint64_t D, int parts, std::vector<uint64_t>& start,
                       std::vector<uint64_t>& entry);

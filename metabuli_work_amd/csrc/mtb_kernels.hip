@@ -757,15 +757,23 @@ __global__ void k_deltas(const uint16_t* __restrict__ diff, uint64_t n, const ui
     }
 }
 
-void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
-                     uint64_t* idxTmp, void* scanTmp, hipStream_t s) {
-    if (nDiff == 0) return;
+uint64_t decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
+                         uint64_t* idxTmp, void* scanTmp, hipStream_t s) {
+    if (nDiff == 0) return 0;
     k_term_flags<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, flagTmp);
     exclusive_scan_u32(flagTmp, nDiff, idxTmp, scanTmp, s);
+    uint64_t terms = 0;
+    uint16_t lastWord = 0;
+    hipMemcpyAsync(&terms, idxTmp + nDiff, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&lastWord, diff + nDiff - 1, sizeof(uint16_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (!(lastWord & 0x8000u)) return ~0ull;
+    if (terms != nKmers) return terms;
     k_deltas<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, idxTmp, values);
     // inclusive scan of deltas = exclusive scan shifted by one: scan into idxTmp then take [1..]
     exclusive_scan_u64(values, nKmers, idxTmp, scanTmp, s);
     hipMemcpyAsync(values, idxTmp + 1, nKmers * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+    return terms;
 }
 
 // ------------------------------------------------------------------------------------------------

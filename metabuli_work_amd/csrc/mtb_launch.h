@@ -102,8 +102,10 @@ constexpr uint64_t kAARankEnd = 37822859361ull;
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
 constexpr int kQuerySortLoFine = 36;  // unstaged K4 sort prefix: 3 passes (4 passes, 28, measured 1.5 ms slower with the run index)
 
-void decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
-                     uint64_t* idxTmp, void* scanTmp, hipStream_t s);
+// returns the terminal words of diff (the k-mers it holds; ~0 if its last word is not one) and decodes
+// only when that equals nKmers
+uint64_t decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
+                         uint64_t* idxTmp, void* scanTmp, hipStream_t s);
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s);
 
 // A resident DB k-mer: its value in rank form (low / high 32 bits) and its taxID (info & mask) in
