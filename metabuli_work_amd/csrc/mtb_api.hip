@@ -108,7 +108,13 @@ struct mtb_ctx {
     uint16_t* runOff = nullptr;  // ... and each present rank's run start in its line (2 B per present rank)
     AADir dir{};
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
-    int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe
+    int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe, 3 sweep
+    // K4S DB-sweep join: DB tiles (built at the first sweep batch) and the nominal tile size
+    uint64_t* tileRec = nullptr;
+    uint32_t* tilePre = nullptr;
+    uint64_t nTiles = 0;
+    uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
+    uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
@@ -147,6 +153,7 @@ struct mtb_ctx {
     DevBuf ordKA, ordVA, ordKB, ordVB, matchWin, unitRead, unitInfo, mStage, mRank, mTotal, mDirect, ovFlag, waveList, waveCount, devStats;
     DevBuf qFrom, probeStats;
     DevBuf longList, longCnt;  // the direct join's long-run queries (k_match_long)
+    DevBuf qStart;             // K4S: the sorted queries' sort-prefix bucket starts
     uint32_t longCap = 0;
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
@@ -377,7 +384,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     build_aa_dir(c->db, c->D, c->dir, c->dirMem, s);
     HIP_TRY(hipStreamSynchronize(s));
     c->openS[2] = since(tp);
-    if (const char* e = getenv("MTB_JOIN")) c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : 0;
+    if (const char* e = getenv("MTB_JOIN"))
+        c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : !strcmp(e, "sweep") ? 3 : 0;
+    if (const char* e = getenv("MTB_SWEEP_NOM")) c->sweepNom = std::max(64u, std::min(4096u, (uint32_t)atoi(e)));
+    if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
     if (!c->forceGeneric) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
@@ -385,7 +395,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         HIP_TRY(hipStreamSynchronize(s));
         c->openS[3] = since(tp);
         const char* ri = getenv("MTB_RUN_INDEX");  // 0: no run index (the unstaged join gallops)
-        if (!ri || atoi(ri) != 0) {
+        if ((!ri || atoi(ri) != 0) && c->joinMode != 3) {  // the sweep join reads no run index
             uint32_t* pop = nullptr;
             void* tmp = nullptr;
             uint64_t P = 0;
@@ -536,6 +546,8 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->spKmers = src->spKmers;
     // the opening's knobs
     c->joinMode = src->joinMode;
+    c->sweepNom = src->sweepNom;
+    c->sweepLdsCap = src->sweepLdsCap;
     c->matchWinCap = src->matchWinCap;
     c->directJoin = src->directJoin;
     c->directRetry = src->directRetry;
@@ -562,7 +574,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
     return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
@@ -573,6 +585,8 @@ void mtb_close(mtb_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     free_db(c);
+    if (c->tileRec) hipFree(c->tileRec);
+    if (c->tilePre) hipFree(c->tilePre);
     c->pipelineCache.reset();  // pinned slots and their device buffers (on c->device)
     hipSetDevice(c->device);
     for (DevBuf* b : batch_bufs(c)) b->release();
@@ -906,7 +920,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // not need a total order (K5 puts each read's matches in compareMatches order); a sort prefix
     // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[4], s));
-    const int sortLo = unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
+    const bool sweepJoin = c->joinMode == 3 && c->lines && !probe && c->directJoin && !c->forceGeneric;
+    const int sortLo = !sweepJoin && unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
                            ? c->sortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
@@ -962,10 +977,25 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     }
     HIP_TRY(hipEventRecord(c->kev[6], s));
     // the windows only serve the staged join
-    if (!probe && !unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072)))
+    if (!probe && !(sweepJoin && direct) && !unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072)))
         launch_match_windows(qk, Q, c->db, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
     uint64_t M = 0, nSpill = 0;
     std::vector<unsigned long long> regTot(kStageRegions);
+    const bool sweep = sweepJoin && direct;
+    if (sweep) {  // K4S: the DB's tiles (once per context) and this batch's query bucket starts
+        if (!c->tileRec) {
+            const uint64_t nT = sweep_tiles(c->D, c->sweepNom);
+            DevBuf tmp;
+            HIP_TRY(tmp.ensure(sizeof(uint64_t) * kSweepStarts));
+            HIP_TRY(hipMalloc(&c->tileRec, sizeof(uint64_t) * (nT + 1)));
+            HIP_TRY(hipMalloc(&c->tilePre, sizeof(uint32_t) * (nT + 1)));
+            build_sweep_tiles(c->db, c->D, c->sweepNom, tmp.as<uint64_t>(), c->tileRec, c->tilePre, s);
+            HIP_TRY(hipStreamSynchronize(s));
+            c->nTiles = nT;
+        }
+        HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * kSweepStarts));
+        build_query_starts(qk, Q, c->qStart.as<uint32_t>(), s);
+    }
     if (direct) {  // the long-run list: grown to the largest seen
         c->longCap = std::max<uint32_t>(c->longCap, (uint32_t)std::min<uint64_t>(std::max<uint64_t>(Q / 256, 1u << 16), 1u << 30));
         HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
@@ -984,6 +1014,13 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(), s);
+        else if (sweep && direct)
+            launch_sweep(c->tileRec, c->tilePre, c->nTiles, c->qStart.as<uint32_t>(), qk, qi, c->unitInfo.as<uint64_t>(),
+                         C, c->db, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
+                         c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
+                         c->spillCap, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(),
+                         c->mDirect.as<SegMatch>(), c->ovFlag.as<int>(), c->spillShift, c->longList.as<LongRun>(),
+                         c->longCap, c->longCnt.as<uint32_t>(), c->sweepLdsCap, s);
         else
             launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->db, c->D, c->dir, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),

@@ -1967,4 +1967,188 @@ void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s) 
     if (n) k_mask_info<<<stride_grid(n), 256, 0, s>>>(info, n, mask);
 }
 
+// ------------------------------------------------------------------------------------------------
+// K4S DB-sweep join (MTB_JOIN=sweep): the reference's own shape — matchKmers streams the whole
+// diffIdx past each sorted query split (KmerMatcher.cpp:363-406) — as one pass over the resident
+// records in DB order. The DB is cut once into tiles of ~kSweepNom records that end at sort-prefix
+// bucket bounds (value >> kQuerySortLo: the query keys' sort prefix), so a tile's queries are one
+// contiguous stretch of the sorted query array (qStart, per batch). A block stages its tile in LDS
+// with coalesced 16-B loads (every load in flight before the first LDS write), then each of the
+// tile's queries finds its AA run by a fixed-trip binary search in LDS and selects / emits as the
+// random-access join does. A tile without queries costs two loads and no DB bytes. No run index,
+// no probe lines, no per-query random DB reads.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kSweepCap = 4096;  // records a tile stages in LDS (48 KB); a longer tile searches HBM
+constexpr uint64_t kSweepPrefixes = 1ull << (kQuerySortHi - kQuerySortLo);
+
+__device__ __forceinline__ uint32_t key_prefix(uint64_t v) { return (uint32_t)(v >> kQuerySortLo); }
+
+// starts[p] = first index i of the sorted array with prefix(a[i]) >= p, for p in [0, 2^24]
+template <typename A>
+__global__ void k_prefix_starts(A a, uint64_t n, uint64_t* __restrict__ starts64, uint32_t* __restrict__ starts32) {
+    MTB_GRID_STRIDE(i, n + 1) {
+        const uint64_t p = i < n ? key_prefix(a[i]) : kSweepPrefixes;
+        const uint64_t from = i ? (uint64_t)key_prefix(a[i - 1]) + 1 : 0;
+        for (uint64_t x = from; x <= p; x++) {
+            if (starts64) starts64[x] = i;
+            if (starts32) starts32[x] = (uint32_t)i;
+        }
+    }
+}
+
+struct KeyArr {
+    const uint64_t* __restrict__ k;
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const { return k[i]; }
+};
+
+// tile j = DB records [tileRec[j], tileRec[j + 1]) = prefix buckets [tilePre[j], tilePre[j + 1]): the
+// nominal start j * nom snapped down to the start of its bucket (a bucket longer than nom leaves
+// empty tiles behind it, which no query names)
+__global__ void k_sweep_tiles(const DbRec* __restrict__ db, uint64_t D, const uint64_t* __restrict__ pstart,
+                              uint64_t nTiles, uint32_t nom, uint64_t* __restrict__ tileRec,
+                              uint32_t* __restrict__ tilePre) {
+    MTB_GRID_STRIDE(j, nTiles + 1) {
+        if (j == nTiles) {
+            tileRec[j] = D;
+            tilePre[j] = (uint32_t)kSweepPrefixes;
+        } else {
+            const uint32_t p = key_prefix((uint64_t)db[j * nom].hi << 32 | db[j * nom].lo);
+            tileRec[j] = pstart[p];
+            tilePre[j] = p;
+        }
+    }
+}
+
+// One query of a tile against the tile's records (LDS or HBM view; vOff = DB index of view[0]).
+template <typename V, typename T>
+__device__ __forceinline__ bool sweep_query(uint64_t q, const uint64_t* __restrict__ qkey,
+                                            const uint32_t* __restrict__ qslot, const V& vals, const T& taxs,
+                                            uint32_t n, uint32_t pow2, uint64_t vOff, const uint64_t* __restrict__ unitInfo,
+                                            uint32_t C, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
+                                            int kmerFormat, uint32_t* __restrict__ readCnt,
+                                            unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
+                                            uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
+                                            SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
+                                            LongRun* __restrict__ longList, uint32_t longCap,
+                                            uint32_t* __restrict__ longCnt) {
+    const uint64_t key = qkey[q];
+    const uint32_t slot = qslot[q];
+    const uint64_t aa = key & kAAMask, aa2 = aa + (1ull << 24);
+    uint32_t p1 = 0, p2 = 0;  // lower bounds of aa and aa2: two fixed-trip searches, interleaved
+    for (uint32_t step = pow2; step > 0; step >>= 1) {
+        const uint32_t i1 = p1 + step, i2 = p2 + step;
+        if (i1 <= n && vals[i1 - 1] < aa) p1 = i1;
+        if (i2 <= n && vals[i2 - 1] < aa2) p2 = i2;
+    }
+    uint64_t lo = p1, hi = p2;
+    if (hi - lo > kLongRun) {  // a long run: scanned by a wave of its own (k_match_long), from HBM
+        const uint32_t at = atomicAdd(longCnt, 1u);
+        if (at < longCap) longList[at] = LongRun{q, lo + vOff, hi + vOff};
+        return false;
+    }
+    const HamRows hr = hamming_rows(key);
+    uint32_t thr = 0;
+    const uint32_t c = run_select(hr, vals, vOff, lo, hi, D, thr);
+    if (!c) return false;
+    uint32_t pu;
+    const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, pu)];
+    const uint64_t info = unit_info_at(ur.x, pu, kmerFormat);
+    const uint32_t rk = atomicAdd(&readCnt[info_seq(info) - 1], c);
+    const uint64_t o = (ur.y & kStretchLoMask) * C, cap = ((ur.y >> 40) * C) >> capShift;
+    if (rk + c > cap) {  // past the read's stretch: spilled with the ranks (scattered after compaction)
+        const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c);
+        if (sp + c > region) {
+            atomicExch(overflow, 1);
+            return true;
+        }
+        run_emit(key, hr, info, vals, taxs, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, sp, sp + c, rk, err);
+        return true;
+    }
+    run_emit(key, hr, info, vals, taxs, lo, hi, thr, spOf, maxTax, kmerFormat, direct + o, (uint32_t*)nullptr,
+             (uint64_t)rk, (uint64_t)rk + c, 0, err);
+    return true;
+}
+
+__global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tilePre,
+                                               const uint32_t* __restrict__ qStart, const uint64_t* __restrict__ qkey,
+                                               const uint32_t* __restrict__ qslot, const uint64_t* __restrict__ unitInfo,
+                                               uint32_t C, const DbRec* __restrict__ db, uint64_t D,
+                                               const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                               uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
+                                               mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
+                                               uint64_t region, int* __restrict__ err,
+                                               unsigned long long* __restrict__ stats, SegMatch* __restrict__ direct,
+                                               int* __restrict__ overflow, uint32_t capShift,
+                                               LongRun* __restrict__ longList, uint32_t longCap,
+                                               uint32_t* __restrict__ longCnt, uint32_t ldsCap) {
+    constexpr uint32_t kVec = kSweepCap * 12 / 16 + 1;  // 16-B vectors of a full tile (+1: unaligned start)
+    constexpr int kLoad = (int)((kVec + 255) / 256);
+    __shared__ uint4 sRaw[kVec];
+    const uint64_t t = blockIdx.x;
+    const uint32_t q0 = qStart[tilePre[t]], q1 = qStart[tilePre[t + 1]];
+    if (q0 >= q1) return;  // no query in the tile's buckets: its records are not read
+    const uint64_t r0 = tileRec[t], r1 = tileRec[t + 1];
+    const uint32_t n = (uint32_t)(r1 - r0);
+    uint32_t pow2 = 1;
+    while (pow2 * 2 <= n) pow2 *= 2;
+    uint32_t hits = 0;
+    if (n <= ldsCap) {
+        const uint64_t b0 = (r0 * 12) & ~15ull;
+        const uint32_t nv = (uint32_t)((r1 * 12 - b0 + 15) >> 4);  // the pad records make the tail readable
+        const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(db) + b0);
+        uint4 v[kLoad];
+#pragma unroll
+        for (int j = 0; j < kLoad; j++)  // clamped (not predicated): every load is issued, all in flight
+            v[j] = src[min(threadIdx.x + (uint32_t)j * 256, nv - 1)];
+#pragma unroll
+        for (int j = 0; j < kLoad; j++) {
+            const uint32_t i = threadIdx.x + (uint32_t)j * 256;
+            if (i < nv) sRaw[i] = v[j];
+        }
+        __syncthreads();
+        const DbRec* rec = reinterpret_cast<const DbRec*>(reinterpret_cast<const char*>(sRaw) + (r0 * 12 - b0));
+        const DbVal vals{rec};
+        const DbTax taxs{rec};
+        for (uint64_t q = q0 + threadIdx.x; q < q1; q += 256)
+            hits += sweep_query(q, qkey, qslot, vals, taxs, n, pow2, r0, unitInfo, C, D, spOf, maxTax, kmerFormat,
+                                readCnt, total, buf, bufRank, region, err, direct, overflow, capShift, longList, longCap,
+                                longCnt);
+    } else {  // one sort-prefix bucket longer than an LDS tile (heavily shared AA 8-mers): from HBM
+        const DbVal vals{db + r0};
+        const DbTax taxs{db + r0};
+        for (uint64_t q = q0 + threadIdx.x; q < q1; q += 256)
+            hits += sweep_query(q, qkey, qslot, vals, taxs, n, pow2, r0, unitInfo, C, D, spOf, maxTax, kmerFormat,
+                                readCnt, total, buf, bufRank, region, err, direct, overflow, capShift, longList, longCap,
+                                longCnt);
+    }
+    const uint32_t w = wave_sum_u32(hits);
+    if ((threadIdx.x & 63) == 0 && w) atomicAdd(&stats[t % kStatStripes], (unsigned long long)w);
+}
+
+uint64_t sweep_tiles(uint64_t D, uint32_t nom) { return D ? (D + nom - 1) / nom : 0; }
+
+void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
+                       uint32_t* tilePre, hipStream_t s) {
+    k_prefix_starts<<<stride_grid(D + 1), 256, 0, s>>>(DbVal{db}, D, pstartTmp, nullptr);
+    const uint64_t nT = sweep_tiles(D, nom);
+    k_sweep_tiles<<<stride_grid(nT + 1), 256, 0, s>>>(db, D, pstartTmp, nT, nom, tileRec, tilePre);
+}
+
+void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s) {
+    k_prefix_starts<<<stride_grid(Q + 1), 256, 0, s>>>(KeyArr{qkey}, Q, nullptr, qStart);
+}
+
+void launch_sweep(const uint64_t* tileRec, const uint32_t* tilePre, uint64_t nTiles, const uint32_t* qStart,
+                  const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db,
+                  uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt,
+                  unsigned long long* total, mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err,
+                  unsigned long long* stats, SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList,
+                  uint32_t longCap, uint32_t* longCnt, uint32_t ldsCap, hipStream_t s) {
+    if (!nTiles || D < 2) return;
+    k_sweep<<<(unsigned)nTiles, 256, 0, s>>>(tileRec, tilePre, qStart, qkey, qslot, unitInfo, C, db, D, spOf, maxTax,
+                                             kmerFormat, readCnt, total, buf, bufRank, region, err, stats, direct,
+                                             overflow, capShift, longList, longCap, longCnt,
+                                             std::min<uint32_t>(ldsCap, kSweepCap));
+}
+
 }  // namespace mtb

@@ -227,6 +227,21 @@ void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, co
                        int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint32_t* bufRank,
                        uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                        uint32_t capShift, unsigned long long* stats, hipStream_t s);
+// K4S DB-sweep join (MTB_JOIN=sweep; direct output only): tiles of ~nom DB records ending at
+// sort-prefix bucket bounds, built once per context (pstartTmp: 2^24 + 1 u64 scratch; tileRec
+// sweep_tiles + 1 u64, tilePre sweep_tiles + 1 u32); per batch the sorted queries' bucket starts
+// (qStart: 2^24 + 1 u32), then one block per tile.
+uint64_t sweep_tiles(uint64_t D, uint32_t nom);
+constexpr uint64_t kSweepStarts = (1ull << 24) + 1;
+void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
+                       uint32_t* tilePre, hipStream_t s);
+void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s);
+void launch_sweep(const uint64_t* tileRec, const uint32_t* tilePre, uint64_t nTiles, const uint32_t* qStart,
+                  const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db,
+                  uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt,
+                  unsigned long long* total, mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err,
+                  unsigned long long* stats, SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList,
+                  uint32_t longCap, uint32_t* longCnt, uint32_t ldsCap, hipStream_t s);  // ldsCap: tests (HBM tiles)
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,

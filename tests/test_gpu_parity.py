@@ -318,3 +318,38 @@ def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
         compare_results(br.results, br.taxcnt, ores, otc)
     odb.close()
+
+
+@pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt2_syncmer", "paired"),
+                                          ("fmt1", "paired"), ("fmt1", "single")])
+@pytest.mark.parametrize("mode", ["default", "nom64", "hbm", "mixed", "spill"])
+def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
+    """K4S, the DB-sweep join (MTB_JOIN=sweep: DB tiles ending at sort-prefix bucket bounds staged in
+    LDS, each tile's queries searched there): the oracle's matches and results with tiles of the
+    default size, many small tiles (MTB_SWEEP_NOM=64), every tile searched in HBM (MTB_SWEEP_LDS=0:
+    the path of a bucket longer than an LDS tile), a mix (MTB_SWEEP_LDS=80), and queries spilling
+    past their read's stretch (MTB_DIRECT=3)."""
+    monkeypatch.setenv("MTB_JOIN", "sweep")
+    monkeypatch.setenv("MTB_SWEEP_NOM", "64" if mode in ("nom64", "mixed") else "2048")
+    monkeypatch.setenv("MTB_SWEEP_LDS", {"hbm": "0", "mixed": "80"}.get(mode, "4096"))
+    monkeypatch.setenv("MTB_DIRECT", "3" if mode == "spill" else "1")
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    reads = _reads(gen, kind, 1500 if kind != "long" else 60, seed=79)
+    opar = par.to_c()
+    odb = oc.OracleDb(db_dir)
+    okmers, ql1, ql2 = oc.extract(opar, reads)
+    omatches = oc.match(odb, opar, okmers)
+    ores, otc = oc.classify(odb, opar, reads)
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
+        gm = clf.matches()
+        assert len(gm) == len(omatches) == br.matches
+        assert np.array_equal(gm, omatches)
+        matched = clf.stats()["matched_queries"]
+        assert 0 < matched <= clf.stats()["query_kmers"]
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        if mode == "spill":
+            assert clf.stats()["spilled_matches"] > 0
+        compare_results(br.results, br.taxcnt, ores, otc)
+    odb.close()
