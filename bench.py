@@ -82,7 +82,7 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2):
+def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2, dbread=0):
     """Algorithmic bytes per launch of each timed kernel for a batch of n reads of `bases` bases in
     all (Qall = windows the scanners emitted, the reference's "Query k-mer number"; Q = kept query
     k-mers, whose AA 8-mer the DB holds; M matches; live = matches K6 reads after K5's pruning; D
@@ -103,7 +103,9 @@ def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2):
         # the DB is much larger than the query stream (D > 24 Q), each query's run: its two
         # run-index entries (4 B) and the run's first two records (24 B); the 16-B segment matches
         # written into the reads' segments (direct join)
-        "match_join": 12 * Q + (28 * Q if D > 24 * Q else 12 * D) + 16 * M,
+        # the DB-sweep join (MTB_JOIN=sweep) reads the records of every tile that holds queries once,
+        # coalesced (dbread of them: all D at these batch sizes)
+        "match_join": 12 * Q + (12 * dbread if dbread else 28 * Q if D > 24 * Q else 12 * D) + 16 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 16 * M + 24 * live + 8 * (n + 1),     # each read's segment matches read, live ones written
         "assign": 24 * live + 32 * n + 4 * n + 8 * n,       # live sorted matches read, results + lengths
@@ -143,7 +145,7 @@ def roofline_of(kern, names, alg, traffic):
 RANDOM_GATHER = os.path.join(ROOT, "profiles", "r01", "random_gather.json")
 
 
-def random_roofline(kern, names, Qall, Q, matched, M, D):
+def random_roofline(kern, names, Qall, Q, matched, M, D, sweep=False):
     """The random-access kernels against the chip's measured random-line ceiling
     (tools/rand_gather.hip -> profiles/r01/random_gather.json: independent 4-B loads at random
     64-B lines; the filter probes 5.4 GB of probe lines, the unstaged join 144 GB of records).
@@ -161,7 +163,7 @@ def random_roofline(kern, names, Qall, Q, matched, M, D):
 
     out = {}
     req = {"filter": (float(Qall), 5.4)}
-    if D > 24 * Q:
+    if D > 24 * Q and not sweep:
         req["match_join"] = (2.0 * Q + float(matched) + M, 144.0)
     for k, (r, gb) in req.items():
         if k not in names or r <= 0:
@@ -180,7 +182,7 @@ class Tally:
     def __init__(self):
         self.kern = np.zeros(7)
         self.stage = np.zeros(5)
-        self.w = {k: 0.0 for k in ("qall", "q", "m", "live", "matched", "gallop", "bases", "reads", "slots")}
+        self.w = {k: 0.0 for k in ("qall", "q", "m", "live", "matched", "gallop", "bases", "reads", "slots", "dbread")}
         self.launches = 0
 
     def add(self, clf, bases, reads):
@@ -190,7 +192,7 @@ class Tally:
         st = clf.stats()
         for k, v in (("qall", qall), ("q", st["query_kmers"]), ("m", m), ("live", st["live_matches"]),
                      ("matched", st["matched_queries"]), ("gallop", st["gallop_queries"]), ("bases", bases),
-                     ("reads", reads), ("slots", st["slots"])):
+                     ("reads", reads), ("slots", st["slots"]), ("dbread", st["db_records_read"])):
             self.w[k] += v
         self.launches += 1
 
@@ -206,9 +208,10 @@ class Tally:
     def rooflines(self, names, D, traffic, mates):
         kern = self.kern_avg()
         alg = alg_bytes(self.avg("bases"), self.avg("reads"), self.avg("qall"), self.avg("q"), self.avg("m"), D,
-                        live=self.avg("live"), probe=names is KERNELS_PROBE, mates=mates)
+                        live=self.avg("live"), probe=names is KERNELS_PROBE, mates=mates, dbread=self.avg("dbread"))
         return (roofline_of(kern, names, alg, traffic),
-                random_roofline(kern, names, self.avg("qall"), self.avg("q"), self.avg("matched"), self.avg("m"), D))
+                random_roofline(kern, names, self.avg("qall"), self.avg("q"), self.avg("matched"), self.avg("m"), D,
+                                sweep=self.avg("dbread") > 0))
 
 
 # ---------------------------------------------------------------------------------------------

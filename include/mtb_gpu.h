@@ -195,7 +195,8 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
  * join found by a gallop over the DB (the run index covers probe lines of < 64K DB k-mers; queries
  * on longer lines fall back), [13] matches the direct join spilled past their read's stretch,
  * [14] query k-mers whose DB run held more than 48 k-mers (scanned a wave each, k_match_long),
- * [15] fused-filter reruns (the batch's present windows outgrew the output sized from earlier batches).
+ * [15] fused-filter reruns (the batch's present windows outgrew the output sized from earlier batches),
+ * [16] DB records the DB-sweep join read (MTB_JOIN=sweep: the tiles that held queries; 0 otherwise).
  * Query k-mers = windows whose AA 8-mer the DB holds. Counts [5]..[9] are over the live matches. */
 int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):

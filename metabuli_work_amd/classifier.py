@@ -232,7 +232,7 @@ class Classifier:
 
     STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
              "species_runs", "wave_runs", "wave_runs_emulated", "join_path", "live_matches", "gallop_queries",
-             "spilled_matches", "long_run_queries", "filter_reruns"]
+             "spilled_matches", "long_run_queries", "filter_reruns", "db_records_read"]
 
     def stats(self) -> dict:
         """Work counts of the last batch (mtb_last_stats)."""

@@ -164,7 +164,7 @@ struct mtb_ctx {
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
     double openS[7] = {0, 0, 0, 0, 0, 0, 0};
-    static constexpr int kNumStats = 16;
+    static constexpr int kNumStats = 17;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -867,8 +867,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (radix_counts_elems(Rc) + 1)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(radix_counts_elems(Rc) + n + 1)));
     HIP_TRY(c->mTotal.ensure(sizeof(unsigned long long) * kStageRegions));
-    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * (kStatStripes + 1)));
-    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+    HIP_TRY(c->probeStats.ensure(sizeof(unsigned long long) * kProbeStatsLen));
+    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
     // K1 extract: every window's key (the sentinel where no k-mer is emitted); fused with K1F for
     // the sort-merge join (the keys never reach HBM: timed as the filter)
     HIP_TRY(hipEventRecord(c->kev[0], s));
@@ -1039,7 +1039,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         if (direct && longN > c->longCap) {  // the list outgrew its buffer: once more, larger
             c->longCap = longN + longN / 8;
             HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
-            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
             continue;
         }
         c->stats[14] = direct ? longN : 0;
@@ -1063,7 +1063,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                 if (c->mStage.ensure(sizeof(mtb_match) * want) == hipSuccess &&
                     c->mRank.ensure(sizeof(uint32_t) * want) == hipSuccess) {
                     c->spillCap = want;
-                    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+                    HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
                     continue;
                 }
                 (void)hipGetLastError();
@@ -1072,7 +1072,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             direct = false;  // rerun staged
             HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
             HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+            HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
             continue;
         }
         M = 0;
@@ -1085,7 +1085,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         c->stageRegion = most + most / 8;  // grow once to the largest region (+12%) and rerun
         HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
-        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * (kStatStripes + 1), s));
+        HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
     }
     HIP_TRY(hipEventRecord(c->kev[7], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
@@ -1274,11 +1274,13 @@ static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, cons
     HIP_TRY(hipStreamSynchronize(s));
     c->stats[9] = dstat[1];
     {
-        std::vector<unsigned long long> ps(kStatStripes + 1);
+        std::vector<unsigned long long> ps(kProbeStatsLen);
         HIP_TRY(hipMemcpy(ps.data(), c->probeStats.p, sizeof(unsigned long long) * ps.size(), hipMemcpyDeviceToHost));
         c->stats[2] = 0;
         for (uint32_t i = 0; i < kStatStripes; i++) c->stats[2] += ps[i];  // queries with >= 1 match
         c->stats[12] = ps[kStatStripes];  // run-index fallbacks (gallop searches) of the probe join
+        c->stats[16] = 0;
+        for (uint32_t i = 0; i < kStatStripes; i++) c->stats[16] += ps[kStatStripes + 1 + i];  // K4S: DB records read
     }
     for (int k = 0; k < 4; k++) HIP_TRY(hipEventElapsedTime(&c->stageMs[k], c->ev[k], c->ev[k + 1]));
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));

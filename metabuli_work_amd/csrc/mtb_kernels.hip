@@ -2123,6 +2123,7 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
     }
     const uint32_t w = wave_sum_u32(hits);
     if ((threadIdx.x & 63) == 0 && w) atomicAdd(&stats[t % kStatStripes], (unsigned long long)w);
+    if (threadIdx.x == 0) atomicAdd(&stats[kStatStripes + 1 + t % kStatStripes], (unsigned long long)n);
 }
 
 uint64_t sweep_tiles(uint64_t D, uint32_t nom) { return D ? (D + nom - 1) / nom : 0; }

@@ -143,6 +143,8 @@ struct alignas(64) ProbeLine {
 };
 static_assert(sizeof(ProbeLine) == 64, "one probe line per 64-B segment");
 constexpr uint32_t kStatStripes = 256;
+// join statistics: [0, 256) matched-query stripes, [256] gallop fallbacks, [257, 513) K4S DB-record stripes
+constexpr uint32_t kProbeStatsLen = 2 * kStatStripes + 1;
 constexpr uint64_t kDbPad = 8;  // ~0 values after the resident DB
 constexpr uint64_t kProbeLines = (kAARankEnd + kLineRanks - 1) / kLineRanks + 1;  // + an end line (base D)
 void build_probe_lines(const DbRec* db, uint64_t D, const AADir& dir, ProbeLine* lines,
