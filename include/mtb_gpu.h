@@ -398,6 +398,19 @@ int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opts, mtb_classify
 int mtb_start_classify_multi(mtb_ctx* const* ctxs, int n_ctx, const mtb_classify_opts* opts,
                              mtb_classify_stats* stats);
 
+/* The same run over a DB larger than one GPU's HBM, range-partitioned:
+ * ctxs[p] holds part db_part = p of db_parts = n_ctx (one context per GPU, opened with
+ * mtb_params.db_part / db_parts). Every context matches each batch against its part
+ * (MTB_MATCH_ONLY); the per-read match segments go to the owner of their reads (context p owns
+ * the p-th 1/n of each batch's reads) by device-to-device copies (hipMemcpyPeerAsync over xGMI
+ * between GPUs); each owner scores its reads (mtb_assign_chunks) and one writer emits the batch in
+ * input order: the TSV and report are byte-identical to a one-context run over the whole DB. A
+ * context out of HBM halves the batch for all of them (MTB_RETRY, as a whole batch does). This is
+ * the reference's per-thread split seek over AA-aligned split entries (KmerMatcher.cpp:180-192,
+ * 255-271; IndexCreator.cpp:843-851) spread over GPUs. --em is refused (db_parts > 1). */
+int mtb_start_classify_partitioned(mtb_ctx* const* ctxs, int n_ctx, const mtb_classify_opts* opts,
+                                   mtb_classify_stats* stats);
+
 /* ---- --em: EM re-estimation of species abundances and read reassignment ------------------------
  * Replaces Reporter::writeMappings / Classifier::getTopSpecies (per batch) and Classifier::em +
  * reclassify (Classifier.cpp:209-386) after the last batch. */

@@ -23,7 +23,7 @@ EXPORTED = [
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
     "mtb_ctx_device", "mtb_start_classify_multi", "mtb_mask_reads", "mtb_workspace_bytes", "mtb_set_workspace_cap",
-    "mtb_open_phases",
+    "mtb_open_phases", "mtb_start_classify_partitioned",
 ]
 
 
@@ -85,6 +85,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_taxon_lineage.restype = ctypes.c_char_p
     L.mtb_start_classify.argtypes = [vp, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_start_classify_multi.argtypes = [P(vp), i32, P(MtbClassifyOpts), P(MtbClassifyStats)]
+    L.mtb_start_classify_partitioned.argtypes = [P(vp), i32, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_ctx_device.argtypes = [vp]
     L.mtb_mask_reads.argtypes = [vp, vp, vp, u32, vp]
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]

@@ -376,7 +376,7 @@ class Classifier:
     def startClassify(self, out_tsv: str, reads_per_batch: int = 0, report_tsv: Optional[str] = None,
                       max_bases: int = 0, threads: int = 0, em_tsv: Optional[str] = None,
                       em_report_tsv: Optional[str] = None, em_reclassify_report_tsv: Optional[str] = None,
-                      peers: Optional[List["Classifier"]] = None) -> int:
+                      peers: Optional[List["Classifier"]] = None, partitioned: bool = False) -> int:
         """Classifier::startClassify (Classifier.cpp:44-164) through the native pipeline
         (mtb_start_classify): FASTA/FASTQ(.gz / BGZF) readers and parsers, pinned batches of at most
         reads_per_batch reads (0: 4M, in practice bounded by max_bases; the first five batches ramping up
@@ -388,7 +388,10 @@ class Classifier:
         the reads classified; the run's timings are left in self.last_run.
 
         peers: more classifiers over the same DB, one per further GPU (mtb_start_classify_multi):
-        batch k runs on [self] + peers at k mod (1 + len(peers)), the output is the same files."""
+        batch k runs on [self] + peers at k mod (1 + len(peers)), the output is the same files.
+        partitioned: [self] + peers hold the parts of a range-partitioned DB (db_part = (p, P) in
+        list order); every batch is matched by all of them and scored by the owners of its reads
+        (mtb_start_classify_partitioned), the output is still the same files."""
         par = self.par
         opts = _abi.MtbClassifyOpts(
             query1=par.filenames[0].encode(), query2=par.filenames[1].encode() if par.seqMode == 2 else None,
@@ -398,7 +401,11 @@ class Classifier:
             em_tsv=em_tsv.encode() if em_tsv else None, em_report_tsv=em_report_tsv.encode() if em_report_tsv else None,
             em_reclassify_report_tsv=em_reclassify_report_tsv.encode() if em_reclassify_report_tsv else None)
         st = _abi.MtbClassifyStats()
-        if peers:
+        if partitioned:
+            hs = (ctypes.c_void_p * (1 + len(peers or [])))(self.handle, *[c.handle for c in peers or []])
+            check(lib().mtb_start_classify_partitioned(hs, len(hs), ctypes.byref(opts), ctypes.byref(st)),
+                  "mtb_start_classify_partitioned")
+        elif peers:
             hs = (ctypes.c_void_p * (1 + len(peers)))(self.handle, *[c.handle for c in peers])
             check(lib().mtb_start_classify_multi(hs, len(hs), ctypes.byref(opts), ctypes.byref(st)),
                   "mtb_start_classify_multi")

@@ -1514,6 +1514,18 @@ std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache;
 
 const mtb_params& ctx_params(const mtb_ctx* c) { return c->par; }
 
+int ctx_match_view(mtb_ctx* c, std::vector<uint64_t>& mOff, const mtb_match** m, const uint32_t** counts,
+                   const uint32_t** qlen) {
+    if (!c->matchOnly) { set_error("batch was not run with MTB_MATCH_ONLY"); return MTB_ERR_ARG; }
+    mOff.resize((size_t)c->nReads + 1);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy(mOff.data(), c->mOff.p, sizeof(uint64_t) * mOff.size(), hipMemcpyDeviceToHost));
+    *m = c->matches.as<mtb_match>();
+    *counts = c->readCnt.as<uint32_t>();
+    *qlen = c->qlen.as<uint32_t>();
+    return MTB_OK;
+}
+
 uint64_t ctx_workspace_bytes(const mtb_ctx* c) {
     uint64_t b = 0;
     for (DevBuf* x : batch_bufs(const_cast<mtb_ctx*>(c))) b += x->bytes;

@@ -493,6 +493,17 @@ struct DevMem {
     }
 };
 
+// A range-partitioned run's copy of a batch on a further context's device.
+struct PeerIn {
+    DevMem dseq1, dseq2, doff1, doff2;
+    hipEvent_t uploaded = nullptr;
+    int device = 0;
+    ~PeerIn() {
+        hipSetDevice(device);
+        if (uploaded) hipEventDestroy(uploaded);
+    }
+};
+
 struct Slot {
     int ctx = 0;             // the context (GPU) the slot's batches run on
     uint64_t index = 0;      // batch number in input order
@@ -514,6 +525,56 @@ struct Slot {
     hipEvent_t uploaded = nullptr;
     Pinned<mtb_result> res;  // pinned: the device-to-host copies run at full PCIe rate
     Pinned<mtb_taxcnt> tc;
+    std::vector<std::unique_ptr<PeerIn>> peers;  // range-partitioned run: the batch on contexts 1..P-1
+};
+
+// Threads of a range-partitioned run meeting once per step of a batch (C++17: no std::barrier).
+struct Barrier {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n, waiting = 0;
+    uint64_t gen = 0;
+    explicit Barrier(int k) : n(k) {}
+    void wait() {
+        std::unique_lock<std::mutex> l(mu);
+        const uint64_t g = gen;
+        if (++waiting == n) {
+            waiting = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(l, [&] { return gen != g; });
+        }
+    }
+};
+
+// One batch of a range-partitioned run, shared by the P partition
+// workers: every context matches the whole piece against its DB part (MTB_MATCH_ONLY), the
+// per-read match segments go to the owner of their reads (owner p: reads [lo + k p / P, lo + k (p+1) / P)
+// of a k-read piece) by device-to-device / peer copies, and each owner scores its reads with
+// mtb_assign_chunks. Pieces halve when a context runs out of HBM, as whole batches do.
+struct PartBatch {
+    explicit PartBatch(int P) : bar(P), rc(P), err(P), mOff(P), m(P), cnt(P), ql(P), tc(P) {}
+    Barrier bar;
+    std::deque<std::pair<uint32_t, uint32_t>> pieces;
+    std::vector<int> rc;
+    std::vector<std::string> err;
+    std::vector<std::vector<uint64_t>> mOff;
+    std::vector<const mtb_match*> m;
+    std::vector<const uint32_t*> cnt, ql;
+    std::vector<std::vector<mtb_taxcnt>> tc;
+    std::vector<mtb_taxcnt> all;
+    uint32_t cap = 0;  // the piece size that fitted (bounds later batches)
+    bool split = false;
+    int fail = MTB_OK;
+    std::string failMsg;
+};
+
+// An owner's staging on its device: the chunks of its reads' matches from every part, their
+// per-read counts, its reads' query lengths.
+struct OwnerStage {
+    DevMem m, cnt, ql;
+    hipStream_t st = nullptr;
 };
 
 // A context's slots, kept between runs (mtb::ctx_pipeline_cache): their pinned host buffers and
@@ -634,12 +695,25 @@ static int classify_slot(mtb_ctx* c, Slot* s, bool paired, bool em, uint32_t& ca
 
 }  // namespace
 
+static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opts* opt, mtb_classify_stats* stats,
+                          bool partitioned);
+
 extern "C" int mtb_start_classify(mtb_ctx* ctx, const mtb_classify_opts* opt, mtb_classify_stats* stats) {
-    return mtb_start_classify_multi(&ctx, 1, opt, stats);
+    return start_classify(&ctx, 1, opt, stats, false);
 }
 
 extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opts* opt,
                                         mtb_classify_stats* stats) {
+    return start_classify(ctxs, nCtx, opt, stats, false);
+}
+
+extern "C" int mtb_start_classify_partitioned(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opts* opt,
+                                              mtb_classify_stats* stats) {
+    return start_classify(ctxs, nCtx, opt, stats, true);
+}
+
+static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opts* opt, mtb_classify_stats* stats,
+                          bool partitioned) {
     using mtb::set_error;
     if (!ctxs || nCtx < 1 || !opt || !opt->query1 || !opt->out_tsv) {
         set_error("null argument");
@@ -659,17 +733,30 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     mtb_ctx* const ctx0 = ctxs[0];  // the writers' taxonomy, the report and --em
     // every context must classify a batch as ctx0 would: the same parameters (host threads aside)
     // over the whole of the same DB
+    std::vector<bool> partSeen(nCtx, false);
     for (int d = 0; d < nCtx; d++) {
         mtb_params a = mtb::ctx_params(ctxs[d]), b = mtb::ctx_params(ctx0);
-        if (a.db_parts > 1) {
+        if (!partitioned && a.db_parts > 1) {
             set_error("a context holds one part of a range-partitioned DB: use mtb_start_classify_partitioned");
             return MTB_ERR_ARG;
         }
+        if (partitioned) {  // one context per part, each part once
+            if (a.db_parts != nCtx || a.db_part < 0 || a.db_part >= nCtx || partSeen[a.db_part]) {
+                set_error("mtb_start_classify_partitioned needs one context per DB part (db_parts = n_ctx)");
+                return MTB_ERR_ARG;
+            }
+            partSeen[a.db_part] = true;
+            a.db_part = b.db_part = 0;
+        }
         a.threads = b.threads = 0;
-        if (memcmp(&a, &b, sizeof a) != 0 || mtb_db_kmers(ctxs[d]) != mtb_db_kmers(ctx0)) {
+        if (memcmp(&a, &b, sizeof a) != 0 || (!partitioned && mtb_db_kmers(ctxs[d]) != mtb_db_kmers(ctx0))) {
             set_error("the contexts differ in their parameters or DB: batches would be classified differently");
             return MTB_ERR_ARG;
         }
+    }
+    if (partitioned && nCtx < 2) {
+        set_error("a range-partitioned run needs >= 2 contexts");
+        return MTB_ERR_ARG;
     }
     const auto t0 = Clock::now();
     const bool paired = opt->query2 != nullptr;
@@ -783,7 +870,7 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
         bool end = false;
         uint64_t index = 0, firstRead = 0;
         while (!end && !eb.failed) {
-            const int d = (int)(index % (uint64_t)nCtx);
+            const int d = partitioned ? 0 : (int)(index % (uint64_t)nCtx);  // partitioned: every context, via ctx0's slots
             Slot* s = nullptr;
             if (!freeQ[d]->pop(s)) break;
             s->n = 0;
@@ -918,6 +1005,35 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
                      hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
             ok = ok && hipEventRecord(s->uploaded, up[d]) == hipSuccess;
             if (gl.owns_lock()) gl.unlock();
+            if (ok && partitioned) {  // the same batch on every further part's device, from the pinned host copy
+                bool same = s->peers.size() == (size_t)nCtx - 1;
+                for (int p = 1; same && p < nCtx; p++) same = s->peers[p - 1]->device == mtb_ctx_device(ctxs[p]);
+                if (!same) {
+                    s->peers.clear();
+                    for (int p = 1; p < nCtx; p++) {
+                        auto pi = std::make_unique<PeerIn>();
+                        pi->device = mtb_ctx_device(ctxs[p]);
+                        hipSetDevice(pi->device);
+                        hipEventCreateWithFlags(&pi->uploaded, hipEventDisableTiming);
+                        s->peers.push_back(std::move(pi));
+                    }
+                }
+                for (int p = 1; p < nCtx && ok; p++) {
+                    PeerIn& pi = *s->peers[p - 1];
+                    std::unique_lock<std::mutex> pl(*growMu.at(pi.device), std::defer_lock);
+                    if (pi.dseq1.cap < b1 + 1 || pi.doff1.cap < on || (paired && (pi.dseq2.cap < b2 + 1 || pi.doff2.cap < on)))
+                        pl.lock();
+                    ok = hipSetDevice(pi.device) == hipSuccess && pi.dseq1.ensure(b1 + 1) == hipSuccess &&
+                         pi.doff1.ensure(on) == hipSuccess &&
+                         hipMemcpyAsync(pi.dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up[p]) == hipSuccess &&
+                         hipMemcpyAsync(pi.doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up[p]) == hipSuccess;
+                    if (ok && paired)
+                        ok = pi.dseq2.ensure(b2 + 1) == hipSuccess && pi.doff2.ensure(on) == hipSuccess &&
+                             hipMemcpyAsync(pi.dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up[p]) == hipSuccess &&
+                             hipMemcpyAsync(pi.doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[p]) == hipSuccess;
+                    ok = ok && hipEventRecord(pi.uploaded, up[p]) == hipSuccess;
+                }
+            }
             if (!ok) {
                 eb.set(MTB_ERR_HIP, "batch upload failed");
                 freeQ[d]->push(s);
@@ -942,9 +1058,196 @@ extern "C" int mtb_start_classify_multi(mtb_ctx* const* ctxs, int nCtx, const mt
     std::vector<uint32_t> pieceCap(nCtx, 0);
     std::atomic<uint64_t> splitBatches{0};
     if (const char* e = getenv("MTB_PIECE_READS")) pieceCap.assign(nCtx, (uint32_t)strtoul(e, nullptr, 10));  // tests
+    // range-partitioned run: worker 0 takes each batch and hands it to the other parts' workers
+    std::vector<std::unique_ptr<BoundedQueue<Slot*>>> partQ;
+    std::unique_ptr<PartBatch> pb;
+    if (partitioned) {
+        for (int p = 0; p < nCtx; p++) partQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
+        pb.reset(new PartBatch(nCtx));
+        for (int a = 0; a < nCtx; a++)  // peer copies over xGMI where the devices differ
+            for (int b = 0; b < nCtx; b++) {
+                const int da = mtb_ctx_device(ctxs[a]), db = mtb_ctx_device(ctxs[b]);
+                if (da == db) continue;
+                hipSetDevice(da);
+                if (hipDeviceEnablePeerAccess(db, 0) != hipSuccess) (void)hipGetLastError();
+            }
+    }
+    auto partition_worker = [&](int p) {
+        mtb_ctx* c = ctxs[p];
+        const int dev = mtb_ctx_device(c);
+        PartBatch& B = *pb;
+        const int P = nCtx;
+        OwnerStage os;
+        if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&os.st, hipStreamNonBlocking) != hipSuccess)
+            eb.set(MTB_ERR_HIP, "cannot create the owner's copy stream");
+        // after each step: p == 0 reads every worker's status; a context out of HBM halves the piece
+        auto decide = [&](bool merge, uint32_t lo, uint32_t k, Slot* s) {
+            bool retry = false;
+            for (int q = 0; q < P; q++) {
+                if (B.rc[q] == MTB_RETRY || B.rc[q] == MTB_ERR_OOM) retry = true;
+                else if (B.rc[q] != MTB_OK && B.fail == MTB_OK) {
+                    B.fail = B.rc[q];
+                    B.failMsg = B.err[q];
+                }
+            }
+            if (B.fail != MTB_OK) return;
+            if (retry) {
+                if (k < 2) {
+                    B.fail = MTB_ERR_OOM;
+                    B.failMsg = "out of HBM for a one-read piece of a range-partitioned batch";
+                    return;
+                }
+                B.pieces.pop_front();
+                B.pieces.push_front({lo + k / 2, lo + k});
+                B.pieces.push_front({lo, lo + k / 2});
+                if (!B.cap || k / 2 < B.cap) {
+                    B.cap = k / 2;
+                    fprintf(stderr, "[mtb] partitioned batch %llu: out of HBM; pieces of <= %u reads\n",
+                            (unsigned long long)s->index, B.cap);
+                }
+                B.split = true;
+                return;
+            }
+            if (!merge) return;
+            for (int q = 0; q < P; q++) {  // the owners' lists in read order, offsets rebased
+                const uint32_t a = (uint32_t)((uint64_t)k * q / P), b = (uint32_t)((uint64_t)k * (q + 1) / P);
+                const uint32_t base = (uint32_t)B.all.size();
+                for (uint32_t i = lo + a; i < lo + b; i++) s->res.p[i].taxcnt_offset += base;
+                B.all.insert(B.all.end(), B.tc[q].begin(), B.tc[q].end());
+            }
+            B.pieces.pop_front();
+        };
+        Slot* s = nullptr;
+        while (true) {
+            if (p == 0) {
+                const auto w0 = Clock::now();
+                const bool got = readyQ[0]->pop(s);
+                waitS[0] += secs(w0, Clock::now());
+                for (int q = 1; q < P; q++)
+                    if (got) partQ[q]->push(s);
+                    else partQ[q]->close();
+                if (!got) break;
+            } else if (!partQ[p]->pop(s)) {
+                break;
+            }
+            const auto g0 = Clock::now();
+            const bool paired2 = paired;
+            const char* q1 = p == 0 ? (const char*)s->dseq1.p : (const char*)s->peers[p - 1]->dseq1.p;
+            const uint64_t* o1 = p == 0 ? (const uint64_t*)s->doff1.p : (const uint64_t*)s->peers[p - 1]->doff1.p;
+            const char* q2 = !paired2 ? nullptr : p == 0 ? (const char*)s->dseq2.p : (const char*)s->peers[p - 1]->dseq2.p;
+            const uint64_t* o2 = !paired2 ? nullptr : p == 0 ? (const uint64_t*)s->doff2.p
+                                                             : (const uint64_t*)s->peers[p - 1]->doff2.p;
+            hipSetDevice(dev);
+            const bool upOk = hipEventSynchronize(p == 0 ? s->uploaded : s->peers[p - 1]->uploaded) == hipSuccess;
+            B.rc[p] = upOk ? MTB_OK : MTB_ERR_HIP;
+            B.err[p] = upOk ? "" : "batch upload failed";
+            if (p == 0) {
+                s->rc = MTB_OK;
+                s->gpuS = 0;
+                s->em.clear();
+                s->tGpu0 = secs(t0, g0);
+                B.pieces.clear();
+                B.all.clear();
+                B.split = false;
+                B.fail = eb.failed ? MTB_ERR_INTERNAL : MTB_OK;  // skipped: an earlier failure ends the run
+                if (s->res.ensure(std::max<uint32_t>(s->n, 1)) != hipSuccess) B.fail = MTB_ERR_OOM;
+                const uint32_t step = B.cap && s->n > B.cap ? B.cap : std::max<uint32_t>(s->n, 1);
+                for (uint32_t lo = 0; lo < s->n; lo += step) B.pieces.push_back({lo, std::min<uint32_t>(s->n, lo + step)});
+                if (B.pieces.size() > 1) B.split = true;
+            }
+            B.bar.wait();
+            if (p == 0) decide(false, 0, 0, s);  // an upload failure
+            B.bar.wait();
+            while (B.fail == MTB_OK && !B.pieces.empty()) {
+                const uint32_t lo = B.pieces.front().first, k = B.pieces.front().second - lo;
+                // 1. every part matches the whole piece
+                int rc = mtb_classify_batch(c, q1, o1 + lo, q2, o2 ? o2 + lo : nullptr, k,
+                                            MTB_INPUT_DEVICE | MTB_MATCH_ONLY, nullptr);
+                if (rc == MTB_OK) rc = mtb::ctx_match_view(c, B.mOff[p], &B.m[p], &B.cnt[p], &B.ql[p]);
+                B.rc[p] = rc;
+                if (rc != MTB_OK) B.err[p] = mtb_last_error();
+                B.bar.wait();
+                const size_t nPieces = B.pieces.size();
+                B.bar.wait();  // (every worker has read the piece count before p == 0 may change it)
+                if (p == 0) decide(false, lo, k, s);
+                B.bar.wait();
+                if (B.fail != MTB_OK || B.pieces.size() != nPieces) continue;  // failed, or halved: again
+                // 2. the owner's reads' segments from every part, its reads' query lengths
+                const uint32_t a = (uint32_t)((uint64_t)k * p / P), b = (uint32_t)((uint64_t)k * (p + 1) / P),
+                               no = b - a;
+                uint64_t tot = 0;
+                for (int q = 0; q < P; q++) tot += B.mOff[q][b] - B.mOff[q][a];
+                rc = MTB_OK;
+                if (os.m.ensure(sizeof(mtb_match) * std::max<uint64_t>(tot, 1)) != hipSuccess ||
+                    os.cnt.ensure(sizeof(uint32_t) * ((size_t)P * no + 1)) != hipSuccess ||
+                    os.ql.ensure(sizeof(uint32_t) * (no + 1)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    rc = MTB_ERR_OOM;
+                }
+                uint64_t at = 0;
+                for (int q = 0; q < P && rc == MTB_OK && no; q++) {
+                    const int dq = mtb_ctx_device(ctxs[q]);
+                    const uint64_t nm = B.mOff[q][b] - B.mOff[q][a];
+                    if (nm && hipMemcpyPeerAsync((mtb_match*)os.m.p + at, dev, B.m[q] + B.mOff[q][a], dq,
+                                                 sizeof(mtb_match) * nm, os.st) != hipSuccess)
+                        rc = MTB_ERR_HIP;
+                    if (hipMemcpyPeerAsync((uint32_t*)os.cnt.p + (size_t)q * no, dev, B.cnt[q] + a, dq,
+                                           sizeof(uint32_t) * no, os.st) != hipSuccess)
+                        rc = MTB_ERR_HIP;
+                    at += nm;
+                }
+                if (rc == MTB_OK && no &&
+                    (hipMemcpyPeerAsync(os.ql.p, dev, B.ql[p] + a, dev, sizeof(uint32_t) * no, os.st) != hipSuccess ||
+                     hipStreamSynchronize(os.st) != hipSuccess))
+                    rc = MTB_ERR_HIP;
+                B.rc[p] = rc;
+                if (rc != MTB_OK) B.err[p] = "range-partitioned match hand-over failed";
+                B.bar.wait();  // every part's segments are copied: the contexts' workspaces may be reused
+                if (p == 0) decide(false, lo, k, s);
+                B.bar.wait();
+                if (B.fail != MTB_OK || B.pieces.size() != nPieces) continue;
+                // 3. the owner scores its reads (K5 + K6 over the chunks of every part)
+                B.tc[p].clear();
+                rc = MTB_OK;
+                if (no) {
+                    rc = mtb_assign_chunks(c, (const mtb_match*)os.m.p, tot, (const uint32_t*)os.cnt.p, (uint32_t)P,
+                                           (const uint32_t*)os.ql.p, no, MTB_INPUT_DEVICE, s->res.p + lo + a);
+                    uint64_t nt = 0;
+                    if (rc == MTB_OK) {
+                        mtb_get_taxcnt(c, nullptr, 0, &nt);
+                        B.tc[p].resize(nt);
+                        rc = mtb_get_taxcnt(c, B.tc[p].data(), nt, &nt);
+                    }
+                }
+                B.rc[p] = rc;
+                if (rc != MTB_OK) B.err[p] = mtb_last_error();
+                B.bar.wait();
+                if (p == 0) decide(true, lo, k, s);
+                B.bar.wait();
+            }
+            if (p == 0) {
+                if (B.fail == MTB_OK && s->tc.ensure(std::max<size_t>(B.all.size(), 1)) != hipSuccess) B.fail = MTB_ERR_OOM;
+                if (B.fail == MTB_OK) std::copy(B.all.begin(), B.all.end(), s->tc.p);
+                if (B.split) splitBatches++;
+                s->gpuS = secs(g0, Clock::now());
+                s->tGpu1 = s->tGpu0 + s->gpuS;
+                s->rc = B.fail;
+                if (B.fail != MTB_OK) {
+                    s->err = B.failMsg;
+                    if (!eb.failed) eb.set(B.fail, B.failMsg);
+                }
+                writeQ.push(s);
+            }
+        }
+        if (os.st) hipStreamDestroy(os.st);
+    };
     std::vector<std::thread> workers;
     for (int d = 0; d < nCtx; d++)
         workers.emplace_back([&, d] {
+            if (partitioned) {
+                partition_worker(d);
+                return;
+            }
             mtb_ctx* c = ctxs[d];
             if (hipSetDevice(mtb_ctx_device(c)) != hipSuccess) eb.set(MTB_ERR_HIP, "cannot select the device");
             Slot* s = nullptr;

@@ -291,3 +291,51 @@ def test_classify_two_ranks(make_db, mode):
     assert len(res) == len(ores)
     assert int(res["taxcnt_len"].sum()) == len(tc)
     compare_results(res, tc, ores, otc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("db_name,parts,cap", [("fmt2", 2, False), ("fmt2", 3, False), ("fmt1", 2, False),
+                                               ("fmt2_syncmer", 3, False), ("fmt2", 2, True)])
+def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap):
+    """mtb_start_classify_partitioned (SURVEY §8(e), config 5 natively): one context per DB part (all
+    on cuda:0 here), every batch matched by each part, the segments handed to the owners of their
+    reads and scored there; the TSV and report are byte-identical to the one-context run over the
+    whole DB, and its classifications are the oracle's. cap: one part's workspace capped so its
+    pieces halve (the whole group splits the batch)."""
+    from metabuli_work_amd import synth
+    from metabuli_work_amd.classifier import Classifier, LocalParameters
+
+    db_dir, _, gen = make_db(db_name)
+    r = _reads(gen, 43, n=2300)
+    p1, p2 = str(tmp_path / "q1.fq"), str(tmp_path / "q2.fq")
+    with open(p1, "wb") as f:
+        f.write(synth.fastq_bytes(r.seq1, r.off1, prefix="p"))
+    with open(p2, "wb") as f:
+        f.write(synth.fastq_bytes(r.seq2, r.off2, prefix="p"))
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir]).load_db_parameters(db_dir)
+    one, part = str(tmp_path / "one.tsv"), str(tmp_path / "part.tsv")
+    rep1, repp = str(tmp_path / "one_rep.tsv"), str(tmp_path / "part_rep.tsv")
+    with Classifier(par, db_dir=db_dir) as whole:
+        assert whole.startClassify(one, reads_per_batch=700, report_tsv=rep1) == r.n
+    clfs = [Classifier(par, db_dir=db_dir, db_part=(p, parts)) for p in range(parts)]
+    try:
+        if cap:
+            clfs[1].classify_batch(r.seq1, r.off1[:701], r.seq2, r.off2[:701], match_only=True)
+            clfs[1].set_workspace_cap(int(clfs[1].workspace_bytes * 0.45))
+        with pytest.raises(MtbError, match="one context per DB part"):  # every part must be there
+            clfs[0].startClassify(part, peers=[], partitioned=True)
+        assert clfs[0].startClassify(part, reads_per_batch=700, report_tsv=repp, peers=clfs[1:],
+                                     partitioned=True) == r.n
+        assert (clfs[0].last_run["split_batches"] > 0) == cap
+        with pytest.raises(MtbError, match="range-partitioned"):  # parts are refused by the replicated entry
+            clfs[0].startClassify(part, peers=clfs[1:])
+    finally:
+        for c in clfs:
+            c.close()
+    assert open(part, "rb").read() == open(one, "rb").read()
+    assert open(repp, "rb").read() == open(rep1, "rb").read()
+    odb = oc.OracleDb(db_dir)
+    ores, _ = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    body = [l.split("\t") for l in open(part).read().split("\n")[1:] if l]
+    assert [int(f[2]) for f in body] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
