@@ -691,9 +691,11 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
     // K5 reads sparse segments up to kSegSortSparse, and thins bigger ones straight from their stretches
     if (c->sparse && (!prune || (maxSeg > kSegSortSparse && !compact) || c->segsortGlobal ||
                       (c->mergeSeg && maxSeg > c->mergeSeg))) {
+        // the reads that overflowed their stretch were compacted with their spills by join_stage:
+        // re-copying them would put stale stretch entries over the scattered spills
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), c->chunkC,
-                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->spillShift, s);
-        // (the spilled ranks of the reads that overflowed their stretch are in place already)
+                                c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->spillShift, s,
+                                c->stats[13] ? 2 : 0);
         c->sparse = false;
     }
     HIP_TRY(launch_segsort(c->matches.as<mtb_match>(), c->mOff.as<uint64_t>(), n, Mc, c->matchesSorted.as<mtb_match>(),
@@ -1106,7 +1108,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     c->sparse = direct && !c->keepStages && !c->forceGeneric && !c->matchOnly;
     if (c->sparse && nSpill) {  // only the reads that overflowed their stretch: compacted + their spills
         launch_compact_segments(c->mDirect.as<SegMatch>(), c->slotOff.as<uint64_t>(), C, c->mOff.as<uint64_t>(), n,
-                                c->matches.as<mtb_match>(), c->spillShift, s, true);
+                                c->matches.as<mtb_match>(), c->spillShift, s, 1);
         launch_spill_scatter(c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(), c->mTotal.as<unsigned long long>(),
                              nSpill, c->mOff.as<uint64_t>(), n, c->matches.as<mtb_match>(), c->errFlag.as<int>(), s);
     } else if (direct && !c->sparse) {

@@ -1911,12 +1911,15 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 __global__ void __launch_bounds__(256) k_compact_segments(const SegMatch* __restrict__ in,
                                                           const uint64_t* __restrict__ dirOff, uint32_t C,
                                                           const uint64_t* __restrict__ readOff, uint32_t nReads,
-                                                          mtb_match* __restrict__ out, uint32_t capShift, int onlyOver) {
+                                                          mtb_match* __restrict__ out, uint32_t capShift, int mode) {
     const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= nReads) return;
     const uint64_t src = dirOff[r] * C, dst = readOff[r];
     const uint64_t cap = ((dirOff[r + 1] - dirOff[r]) * C) >> capShift;
-    if (onlyOver && readOff[r + 1] - dst <= cap) return;  // K5 reads this one in place
+    // mode 1: only the reads that overflowed their stretch (K5 reads the others in place); mode 2:
+    // all but those (compacted with their spills already, by a mode-1 pass + k_spill_scatter)
+    const bool over = readOff[r + 1] - dst > cap;
+    if ((mode == 1 && !over) || (mode == 2 && over)) return;
     const uint64_t n = min(readOff[r + 1] - dst, cap);  // ranks past it: spilled
     for (uint64_t i = lane; i < n; i += 64) out[dst + i] = seg_expand(in[src + i], (uint64_t)(r + 1) << 32);
 }
@@ -1945,9 +1948,9 @@ void launch_spill_scatter(const mtb_match* spill, const uint32_t* spillRank, con
 }
 
 void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
-                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s, bool onlyOver) {
+                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s, int mode) {
     if (nReads)
-        k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out, capShift, onlyOver ? 1 : 0);
+        k_compact_segments<<<(nReads + 3) / 4, 256, 0, s>>>(in, dirOff, C, readOff, nReads, out, capShift, mode);
 }
 
 void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint64_t region,

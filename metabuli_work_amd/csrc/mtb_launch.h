@@ -257,7 +257,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 // `region`, else *overflow is set and the caller reruns with a larger spill buffer or staged).
 // capShift (tests): stretches are taken as their size >> capShift, so that queries spill.
 void launch_compact_segments(const SegMatch* in, const uint64_t* dirOff, uint32_t C, const uint64_t* readOff,
-                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s, bool onlyOver = false);
+                             uint32_t nReads, mtb_match* out, uint32_t capShift, hipStream_t s, int mode = 0);
+// (mode 0: every read; 1: only the reads whose matches passed their stretch; 2: all but those)
 // the spilled matches to readOff[r] + rank (after launch_compact_segments)
 void launch_spill_scatter(const mtb_match* spill, const uint32_t* spillRank, const unsigned long long* total,
                           uint64_t nSpill, const uint64_t* readOff, uint32_t nReads, mtb_match* out, int* err,

@@ -353,3 +353,26 @@ def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
             assert clf.stats()["spilled_matches"] > 0
         compare_results(br.results, br.taxcnt, ores, otc)
     odb.close()
+
+
+@pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt1", "long")])
+@pytest.mark.parametrize("late", ["glob", "merge512", "nocompact"])
+def test_spill_then_late_compaction(make_db, db_name, kind, late, monkeypatch):
+    """Spilled queries (MTB_DIRECT=3 quarters the read stretches) with a K5 that compacts every
+    segment itself (global-scratch sort, the merge path above 512 matches, or no thinning of big
+    segments): the reads that overflowed were compacted with their spills by the join, and the late
+    compaction leaves them alone — the results are the oracle's."""
+    monkeypatch.setenv("MTB_DIRECT", "3")
+    monkeypatch.setenv("MTB_SEGSORT_GLOBAL", "1" if late == "glob" else "0")
+    monkeypatch.setenv("MTB_MERGE_SEG", "512" if late == "merge512" else "0")
+    monkeypatch.setenv("MTB_PRUNE_COMPACT", "0" if late == "nocompact" else "1")
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    reads = _reads(gen, kind, 1500 if kind != "long" else 60, 83)
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    odb.close()
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        assert clf.stats()["spilled_matches"] > 0
+        compare_results(br.results, br.taxcnt, ores, otc)
