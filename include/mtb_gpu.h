@@ -65,7 +65,10 @@ typedef struct mtb_params {
                                  BFS, Taxonomer.cpp:193-201) and record EM mappings (mtb_em)    */
     int32_t threads;          /* host threads (oracle / host parsing only)                     */
     int32_t mask_mode;        /* --mask-residues 1: tantan low-complexity masking of the reads
-                                 before extraction (KmerExtractor.cpp:328-335)                  */
+                                 before extraction (KmerExtractor.cpp:328-335). PARITY UNPINNED:
+                                 tantan and its scoring matrices are MMseqs2's, absent from the
+                                 reference tree; restated from the published algorithm with
+                                 +2/-3/-1 scores at uniform background            */
     int32_t db_part;          /* range-partitioned DB: this context holds part db_part of      */
     int32_t db_parts;         /* db_parts AA-aligned k-mer ranges (0 or 1 = the whole DB)      */
     float mask_prob;          /* --mask-prob (0.9): tantan's minMaskProb                       */
