@@ -742,25 +742,27 @@ __device__ uint32_t block_scan_u32(uint32_t x, uint32_t* total, uint32_t* sWave)
 // takes a contiguous chunk: species-run ids by a block scan of run starts, a flag per run that has
 // a (species, frame) pair, then the live elements written in order. rid: n words, runLive: n bytes
 // of scratch. Returns the live count.
-template <int kThreads, typename Idx, typename In>
+// kSp / kSpf: the right shifts of a key that leave its species / (species, frame) — 32 / 29 for the
+// hi word of match_key, 40 / 37 for the compact keys of the large sort.
+template <int kThreads, typename Idx, typename In, int kSp = 32, int kSpf = 29>
 __device__ uint32_t prune_pack_block(const uint64_t* H, const Idx* I, uint32_t* rid, uint8_t* runLive, long n,
                                      const In& in, mtb_match* __restrict__ out, uint64_t base,
                                      uint32_t* sWave, uint32_t pm) {
     const long per = (n + kThreads - 1) / kThreads;
     const long b = (long)threadIdx.x * per, e = min(n, b + per);
     uint32_t starts = 0;
-    for (long i = b; i < e; i++) starts += (i == 0 || (H[i] >> 32) != (H[i - 1] >> 32)) ? 1u : 0u;
+    for (long i = b; i < e; i++) starts += (i == 0 || (H[i] >> kSp) != (H[i - 1] >> kSp)) ? 1u : 0u;
     uint32_t nRuns;
     uint32_t run = block_scan_u32<kThreads>(starts, &nRuns, sWave);
     for (long i = b; i < e; i++) {
-        if (i == 0 || (H[i] >> 32) != (H[i - 1] >> 32)) run++;
+        if (i == 0 || (H[i] >> kSp) != (H[i - 1] >> kSp)) run++;
         rid[i] = run - 1;
     }
     for (long i = threadIdx.x; i < (long)nRuns; i += kThreads) runLive[i] = 0;
     __threadfence_block();  // the scratch may be global memory (segments over kBlockSeg)
     __syncthreads();
     for (long i = b; i < e; i++)
-        if (i + (long)pm - 1 < n && (H[i] >> 29) == (H[i + pm - 1] >> 29)) runLive[rid[i]] = 1;  // a group of >= pm
+        if (i + (long)pm - 1 < n && (H[i] >> kSpf) == (H[i + pm - 1] >> kSpf)) runLive[rid[i]] = 1;  // a group of >= pm
     __threadfence_block();
     __syncthreads();
     uint32_t mine = 0;
@@ -897,12 +899,125 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
     else segsort_mid_run(MatchIn{in, base}, L, out, base, n, liveCnt, r, pm);
 }
 
+// The large pruned sort on compact keys (segments of 2049..8192 matches: long reads), as the register
+// sorts do (prune_rank_sort): species:24 | frame:3 | pos:24 | slot:13 in one 64-bit key, the slot
+// naming the element's record (its lo key and original index) in LDS, so the 1024-thread network
+// moves 8 B per element instead of a 128-bit key and an index. Elements tied on (species, frame, pos)
+// are placed inside their tie by the lo key (hamming, dna, target), the rest of compareMatches'
+// order. Segments with a species or a position of 2^24 or more take the full-key sort (returns false).
+constexpr int kCSp = 40, kCSpf = 37, kCPos = 13;
+
+__device__ __forceinline__ void block_bitonic_u64(uint64_t* K, long p2) {
+    for (long k = 2; k <= p2; k <<= 1)
+        for (long j = k >> 1; j > 0; j >>= 1) {
+            for (long t = threadIdx.x; t < (p2 >> 1); t += kLargeThreads) {
+                const long i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const long ixj = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t a = K[i], b = K[ixj];
+                if ((a > b) == up) {
+                    K[i] = b;
+                    K[ixj] = a;
+                }
+            }
+            __syncthreads();
+        }
+}
+
+template <typename In>
+__device__ bool segsort_large_compact(const In& in, long n, uint64_t* K, uint64_t* Lo, uint16_t* orig,
+                                      uint32_t* sWave, mtb_match* __restrict__ out, uint64_t base,
+                                      uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
+    constexpr int kPer = kBlockSeg / kLargeThreads;  // 8
+    constexpr uint32_t logT = 14, T = 1u << logT;    // pair / species hashes: 64 KB each, in K and Lo
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(K);
+    uint32_t* flag = reinterpret_cast<uint32_t*>(Lo);
+    const long b = (long)threadIdx.x * kPer;
+    uint64_t h[kPer], l[kPer];
+    uint32_t hp[kPer], hs[kPer];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        h[k] = l[k] = 0;
+        hp[k] = hs[k] = 0;
+        if (b + k < n) {
+            match_key(in.full((uint32_t)(b + k)), h[k], l[k]);
+            bad |= (h[k] >> 32) >= (1ull << 24) || (h[k] & 0x1FFFFFFFull) >= (1ull << 24);
+            hp[k] = (uint32_t)(((h[k] >> 29) * 0x9E3779B97F4A7C15ull) >> (64 - logT));
+            hs[k] = (uint32_t)(((h[k] >> 32) * 0xC2B2AE3D27D4EB4Full) >> (64 - logT));
+        }
+    }
+    if (__syncthreads_or(bad)) return false;
+    for (uint32_t i = threadIdx.x; i < T; i += kLargeThreads) {
+        cnt[i] = 0;
+        flag[i] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n) atomicAdd(&cnt[hp[k]], 1u);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n && cnt[hp[k]] >= pm) flag[hs[k]] = 1;
+    __syncthreads();
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (b + k < n && flag[hs[k]]) mask |= 1u << k;
+    uint32_t m;
+    uint32_t at = block_scan_u32<kLargeThreads>((uint32_t)__popc(mask), &m, sWave);  // syncs: the tables are free
+    if (m == 0) {
+        if (threadIdx.x == 0) liveCnt[r] = 0;
+        return true;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if ((mask >> k) & 1u) {
+            K[at] = (h[k] >> 32) << kCSp | ((h[k] >> 29) & 7ull) << kCSpf | (h[k] & 0xFFFFFFull) << kCPos | at;
+            Lo[at] = l[k];
+            orig[at] = (uint16_t)(b + k);
+            at++;
+        }
+    long p2 = 2;
+    while (p2 < (long)m) p2 <<= 1;
+    for (long i = (long)m + threadIdx.x; i < p2; i += kLargeThreads) K[i] = ~0ull;
+    __syncthreads();
+    block_bitonic_u64(K, p2);
+    // places inside (species, frame, pos) ties, then the original index at each place
+    uint16_t pos[kPer], idx[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const long e = threadIdx.x + (long)j * kLargeThreads;
+        pos[j] = idx[j] = 0;
+        if (e < (long)m) {
+            const uint64_t k = K[e], pre = k >> kCPos, lo = Lo[k & (kBlockSeg - 1)];
+            long a = e;
+            for (long q = e - 1; q >= 0 && (K[q] >> kCPos) == pre; q--) a -= Lo[K[q] & (kBlockSeg - 1)] > lo;
+            for (long q = e + 1; q < (long)m && (K[q] >> kCPos) == pre; q++) a += Lo[K[q] & (kBlockSeg - 1)] < lo;
+            pos[j] = (uint16_t)a;
+            idx[j] = orig[k & (kBlockSeg - 1)];
+        }
+    }
+    __syncthreads();  // the lo keys are dead: their LDS takes the placed indices, run ids and flags
+    uint16_t* placed = reinterpret_cast<uint16_t*>(Lo);
+#pragma unroll
+    for (int j = 0; j < kPer; j++)
+        if (threadIdx.x + (long)j * kLargeThreads < (long)m) placed[pos[j]] = idx[j];
+    __syncthreads();
+    uint32_t* rid = reinterpret_cast<uint32_t*>(placed + kBlockSeg);
+    const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t, In, kCSp, kCSpf>(
+        K, placed, rid, reinterpret_cast<uint8_t*>(rid + kBlockSeg), (long)m, in, out, base, sWave, pm);
+    if (threadIdx.x == 0) liveCnt[r] = kept;
+    return true;
+}
+
 __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match* __restrict__ in,
                                                                  const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                                  uint64_t M, mtb_match* __restrict__ out,
                                                                  uint64_t* __restrict__ gScratch, int global,
                                                                  uint32_t* __restrict__ liveCnt, long mergeSeg, uint32_t pm,
-                                                                 const uint32_t* __restrict__ segLen) {
+                                                                 const uint32_t* __restrict__ segLen, int compact) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
     const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
@@ -916,6 +1031,9 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     long p2 = 2;
     while (p2 < n) p2 <<= 1;
     if (!global && n > mergeSeg) return;  // chunked LDS sorts + merge path (launch_segsort)
+    if (!global && liveCnt && compact &&
+        segsort_large_compact(MatchIn{in, base}, n, sh, sl, si, sWave, out, base, liveCnt, r, pm))
+        return;
     if (!global) {
         long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
         if (liveCnt) {
@@ -1280,7 +1398,7 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
         k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
-                                                         segLen);
+                                                         segLen, mode == 2 ? 1 : 0);
     MTB_HIP_RET(hipGetLastError());
     if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, segLen, s);
     return hipSuccess;
@@ -1299,7 +1417,7 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm,
-                                                         nullptr);
+                                                         nullptr, 0);
         return hipGetLastError();
     }
     // segments over thinAbove matches are thinned first when pruning (most of a long read's matches
