@@ -121,6 +121,8 @@ struct mtb_ctx {
     int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune)
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
+    bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
+                                 // (with the sweep join the context then holds no probe lines either)
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
     bool sparse = false;         // the batch's matches are still in the direct join's layout (mDirect, slotOff * chunkC)
     uint32_t maxW = 0;           // the batch's most windows in one frame of one read
@@ -388,7 +390,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : !strcmp(e, "sweep") ? 3 : 0;
     if (const char* e = getenv("MTB_SWEEP_NOM")) c->sweepNom = std::max(64u, std::min(4096u, (uint32_t)atoi(e)));
     if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
-    if (!c->forceGeneric) {
+    if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
+    if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
         build_probe_lines(c->db, c->D, c->dir, c->lines, s);
@@ -564,6 +567,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->emulateAll = src->emulateAll;
     c->pruneCompact = src->pruneCompact;
     c->noAlias = src->noAlias;
+    c->noFilter = src->noFilter;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -854,7 +858,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                       const uint64_t* dOff2, uint32_t n, uint64_t U, uint32_t C, uint64_t R, uint64_t Rc) {
     hipStream_t s = c->stream;
     const bool probe = c->probed;
-    const bool fused = c->lines && !probe && c->fuseFilter;
+    const bool filt = c->lines && (!c->noFilter || probe);  // K1F: only the windows whose AA 8-mer the DB holds go on
+    const bool fused = filt && !probe && c->fuseFilter;
     // The fused K1 + K1F writes only the present windows (Q, about half the slots at GTDB scale):
     // its output is sized by the largest present share seen (+1/8) instead of every slot, and the
     // sort's other side by Q once it is known; a batch past that share reruns the filter into a
@@ -907,7 +912,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(c->valsA.ensure(4 * std::max<uint64_t>(Q, 1)));
         qk = c->keysB.as<uint64_t>();
         qi = c->valsB.as<uint32_t>();
-    } else if (c->lines) {
+    } else if (filt) {
         if (probe) HIP_TRY(c->qFrom.ensure(8 * Rc + 8 * kDbPad));
         Q = launch_filter(c->keysA.as<uint64_t>(), R, c->lines, c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(),
                           probe ? c->qFrom.as<uint64_t>() : nullptr, c->mTotal.as<unsigned long long>(), c->rankLo,
@@ -922,12 +927,12 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     // not need a total order (K5 puts each read's matches in compareMatches order); a sort prefix
     // of ~6 amino acids is all the locality its DB windows need: three passes instead of five.
     HIP_TRY(hipEventRecord(c->kev[4], s));
-    const bool sweepJoin = c->joinMode == 3 && c->lines && !probe && c->directJoin && !c->forceGeneric;
+    const bool sweepJoin = c->joinMode == 3 && !probe && c->directJoin && !c->forceGeneric;
     const int sortLo = !sweepJoin && unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072))
                            ? c->sortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
-        if (c->lines) {
+        if (filt) {
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
                                  c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);

@@ -143,7 +143,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused", "64",
-                                    "6144", "6144:staged", "6144:spill", "6144:unfused"])
+                                    "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
     run index, or galloped from the probe line's lower bound with MTB_RUN_INDEX=0) — give the
@@ -161,6 +161,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_RUN_INDEX", "0" if mode == "gallop" else "1")
     monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2", "spill": "3"}.get(mode, "1"))
     monkeypatch.setenv("MTB_FUSE_FILTER", "0" if mode == "unfused" else "1")
+    monkeypatch.setenv("MTB_FILTER", "0" if mode == "nofilter" else "1")  # every window joined, absent AA 8-mers too
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, 2)
     reads = _reads(gen, "paired", 2000, seed=9)
@@ -322,14 +323,16 @@ def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
 
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt2_syncmer", "paired"),
                                           ("fmt1", "paired"), ("fmt1", "single")])
-@pytest.mark.parametrize("mode", ["default", "nom64", "hbm", "mixed", "spill"])
+@pytest.mark.parametrize("mode", ["default", "nom64", "hbm", "mixed", "spill", "nofilter"])
 def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
     """K4S, the DB-sweep join (MTB_JOIN=sweep: DB tiles ending at sort-prefix bucket bounds staged in
     LDS, each tile's queries searched there): the oracle's matches and results with tiles of the
     default size, many small tiles (MTB_SWEEP_NOM=64), every tile searched in HBM (MTB_SWEEP_LDS=0:
     the path of a bucket longer than an LDS tile), a mix (MTB_SWEEP_LDS=80), and queries spilling
-    past their read's stretch (MTB_DIRECT=3)."""
+    past their read's stretch (MTB_DIRECT=3), and every non-blank window sorted and swept with no
+    membership filter (MTB_FILTER=0: no K1F, no probe lines)."""
     monkeypatch.setenv("MTB_JOIN", "sweep")
+    monkeypatch.setenv("MTB_FILTER", "0" if mode == "nofilter" else "1")
     monkeypatch.setenv("MTB_SWEEP_NOM", "64" if mode in ("nom64", "mixed") else "2048")
     monkeypatch.setenv("MTB_SWEEP_LDS", {"hbm": "0", "mixed": "80"}.get(mode, "4096"))
     monkeypatch.setenv("MTB_DIRECT", "3" if mode == "spill" else "1")
@@ -348,6 +351,8 @@ def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
         assert np.array_equal(gm, omatches)
         matched = clf.stats()["matched_queries"]
         assert 0 < matched <= clf.stats()["query_kmers"]
+        if mode == "nofilter":  # every non-blank window went to the join
+            assert clf.stats()["query_kmers"] == br.query_kmers == int((info_seq(okmers["info"]) != 0).sum())
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
         if mode == "spill":
             assert clf.stats()["spilled_matches"] > 0
