@@ -4,10 +4,11 @@
 # batches. One JSON line per run in gpurun_out/.
 set -o pipefail
 common="--skip-config2 --e2e-pairs 0 --e2e-gzip-pairs 0 --em-pairs 0 --c5-kmers 0 --long-reads 0 --cpu-sample 0 --cold-pairs 0 --steps 3 --warmup 1"
-for j in ${JOINS:-default sweep}; do
+for j in ${JOINS:-default sweep sweepnf}; do
   for b in ${BATCHES:-2000000 3000000}; do
     tag=${j}_${b}
-    MTB_JOIN=$([ $j = default ] && echo "" || echo $j) timeout -k 10 300 python -u bench.py $common --variants "" \
+    MTB_JOIN=$([ $j = default ] && echo "" || echo sweep) MTB_FILTER=$([ $j = sweepnf ] && echo 0 || echo 1) \
+      timeout -k 10 300 python -u bench.py $common --variants "" \
       --gtdb-batch $b --detail gpurun_out/sw_${tag}_detail.json > gpurun_out/sw_${tag}.json 2> gpurun_out/sw_${tag}.log || exit $?
   done
 done
