@@ -2101,8 +2101,10 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
         const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(db) + b0);
         uint4 v[kLoad];
 #pragma unroll
-        for (int j = 0; j < kLoad; j++)  // clamped (not predicated): every load is issued, all in flight
-            v[j] = src[min(threadIdx.x + (uint32_t)j * 256, nv - 1)];
+        for (int j = 0; j < kLoad; j++) {  // every load in flight before the first LDS write
+            const uint32_t i = threadIdx.x + (uint32_t)j * 256;
+            v[j] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + (uint32_t)j * 256;
