@@ -515,7 +515,6 @@ struct Slot {
     float devMs = 0;     // MTB_PIPE_TRACE: the batch's device time (HIP events)
     uint64_t ws = 0;     // MTB_PIPE_TRACE: the context's workspace bytes after the batch
     std::vector<mtb_em_map> em;
-    Pinned<char> seq1, seq2;
     Pinned<uint64_t> off1, off2;
     std::string names;
     std::vector<uint64_t> noff;
@@ -577,11 +576,46 @@ struct OwnerStage {
     hipStream_t st = nullptr;
 };
 
+// One assembler copy thread's staging towards a context's device: two pinned chunks (one filled
+// while the other uploads) on a stream of its own. A batch's bases go to HBM through these chunks
+// instead of a pinned copy of the whole batch, so a run pins kCopyThreads x 2 x kStageChunk bytes
+// once per context (a whole-batch pinned slot was ~1.2 GB per mate at 3.5M-pair batches, pinned
+// step by step through the batch-size ramp of a context's first run).
+constexpr size_t kStageChunk = 8u << 20;
+struct Stager {
+    int device = 0;
+    char* buf[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    hipStream_t st = nullptr;
+    int k = 0;  // the buffer filled next
+    bool init(int dev) {
+        if (st) return true;
+        device = dev;
+        if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+        for (int i = 0; i < 2; i++)
+            if (hipHostMalloc((void**)&buf[i], kStageChunk, hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess)
+                return false;
+        return true;
+    }
+    ~Stager() {
+        hipSetDevice(device);
+        if (st) hipStreamSynchronize(st);
+        for (int i = 0; i < 2; i++) {
+            if (buf[i]) hipHostFree(buf[i]);
+            if (done[i]) hipEventDestroy(done[i]);
+        }
+        if (st) hipStreamDestroy(st);
+    }
+};
+
 // A context's slots, kept between runs (mtb::ctx_pipeline_cache): their pinned host buffers and
 // device input buffers are grown once, not re-pinned (hipHostMalloc) batch by batch every run.
 struct SlotPool {
     int device = 0;
     std::vector<std::unique_ptr<Slot>> slots;
+    std::unique_ptr<Stager> stagers[kCopyThreads];  // the assembler's copy threads towards this device
     // the mates' raw buffers and parse jobs (warm host memory instead of freshly faulted pages)
     std::shared_ptr<Recycler<RawBuf>> raws[2] = {std::make_shared<Recycler<RawBuf>>(),
                                                  std::make_shared<Recycler<RawBuf>>()};
@@ -592,6 +626,7 @@ struct SlotPool {
         for (auto& s : slots)
             if (s->uploaded) hipEventDestroy(s->uploaded);
         slots.clear();  // the buffers are freed on the context's device
+        for (auto& g : stagers) g.reset();
     }
 };
 
@@ -947,8 +982,8 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                     if (!mate) nameBytes += b.noff[hi] - b.noff[lo];
                 }
             }
-            if (s->seq1.ensure(b1 + 1) != hipSuccess || s->off1.ensure((size_t)s->n + 1) != hipSuccess ||
-                (paired && (s->seq2.ensure(b2 + 1) != hipSuccess || s->off2.ensure((size_t)s->n + 1) != hipSuccess))) {
+            if (s->off1.ensure((size_t)s->n + 1) != hipSuccess ||
+                (paired && s->off2.ensure((size_t)s->n + 1) != hipSuccess)) {
                 eb.set(MTB_ERR_OOM, "cannot allocate pinned host batch buffers");
                 freeQ[d]->push(s);
                 break;
@@ -957,15 +992,36 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
             s->noff.resize((size_t)s->n + 1);
             s->off1.p[0] = 0;
             if (paired) s->off2.p[0] = 0;
+            // the slot's device buffers live on its context's device (a new thread starts on device 0);
+            // growing them frees the smaller ones, and hipFree waits for the whole device: not while
+            // another context's batch runs there (growMu)
+            const int dev = mtb_ctx_device(ctxs[d]);
+            const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
+            bool ok = true;
+            {
+                std::unique_lock<std::mutex> gl(*growMu.at(dev), std::defer_lock);
+                if (s->dseq1.cap < b1 + 1 || s->doff1.cap < on || (paired && (s->dseq2.cap < b2 + 1 || s->doff2.cap < on)))
+                    gl.lock();
+                ok = hipSetDevice(dev) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
+                     s->doff1.ensure(on) == hipSuccess &&
+                     (!paired || (s->dseq2.ensure(b2 + 1) == hipSuccess && s->doff2.ensure(on) == hipSuccess));
+            }
+            // offsets and names by piece; the bases by staging chunk: each copy thread fills one of
+            // its pinned chunks from the pieces overlapping the chunk's range of the batch and
+            // uploads it while filling the other
+            auto pool = std::static_pointer_cast<SlotPool>(mtb::ctx_pipeline_cache(ctxs[d]));
+            const uint64_t nCh1 = (b1 + kStageChunk - 1) / kStageChunk, nCh2 = paired ? (b2 + kStageChunk - 1) / kStageChunk : 0;
+            size_t firstOf2 = 0;  // pieces are in mate order, by seqAt within a mate
+            while (firstOf2 < pieces.size() && pieces[firstOf2].mate == 0) firstOf2++;
             std::atomic<size_t> nextPiece{0};
-            auto copy = [&] {
+            std::atomic<uint64_t> nextChunk{0};
+            std::atomic<bool> stageOk{true};
+            auto copy = [&](size_t t) {
                 for (size_t i; (i = nextPiece.fetch_add(1)) < pieces.size();) {
                     const Piece& pc = pieces[i];
                     const RecordBlock& b = *pc.b;
-                    char* seq = pc.mate ? s->seq2.p : s->seq1.p;
                     uint64_t* off = pc.mate ? s->off2.p : s->off1.p;
                     const uint64_t base = b.off[pc.lo];
-                    memcpy(seq + pc.seqAt, b.seq.data() + base, b.off[pc.hi] - base);
                     for (uint32_t k = pc.lo; k < pc.hi; k++) off[pc.r + 1 + (k - pc.lo)] = pc.seqAt + (b.off[k + 1] - base);
                     if (!pc.mate) {
                         const uint64_t nb = b.noff[pc.lo];
@@ -974,38 +1030,64 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                             s->noff[pc.r + 1 + (k - pc.lo)] = pc.nameAt + (b.noff[k + 1] - nb);
                     }
                 }
+                Stager& g = *pool->stagers[t];
+                for (uint64_t c; stageOk && (c = nextChunk.fetch_add(1)) < nCh1 + nCh2;) {
+                    const int mate = c >= nCh1;
+                    const uint64_t lo = (mate ? c - nCh1 : c) * kStageChunk;
+                    const uint64_t hi = std::min<uint64_t>(lo + kStageChunk, mate ? b2 : b1);
+                    if (g.used[g.k] && hipEventSynchronize(g.done[g.k]) != hipSuccess) stageOk = false;
+                    char* dst = g.buf[g.k];
+                    // the mate's pieces overlapping [lo, hi): the first one by binary search on seqAt
+                    size_t a = mate ? firstOf2 : 0, e = mate ? pieces.size() : firstOf2;
+                    size_t i0 = std::upper_bound(pieces.begin() + a, pieces.begin() + e, lo,
+                                                 [](uint64_t x, const Piece& p) { return x < p.seqAt; }) -
+                                pieces.begin();
+                    for (size_t i = i0 > a ? i0 - 1 : a; i < e && pieces[i].seqAt < hi; i++) {
+                        const Piece& pc = pieces[i];
+                        const RecordBlock& b = *pc.b;
+                        const uint64_t pLo = pc.seqAt, pHi = pc.seqAt + (b.off[pc.hi] - b.off[pc.lo]);
+                        const uint64_t x0 = std::max(lo, pLo), x1 = std::min(hi, pHi);
+                        if (x0 < x1) memcpy(dst + (x0 - lo), b.seq.data() + b.off[pc.lo] + (x0 - pLo), x1 - x0);
+                    }
+                    char* dseq = (char*)(mate ? s->dseq2.p : s->dseq1.p);
+                    if (hipMemcpyAsync(dseq + lo, dst, hi - lo, hipMemcpyHostToDevice, g.st) != hipSuccess ||
+                        hipEventRecord(g.done[g.k], g.st) != hipSuccess)
+                        stageOk = false;
+                    g.used[g.k] = true;
+                    g.k ^= 1;
+                }
             };
-            {
+            const size_t nCopy = std::max<size_t>(1, std::min<size_t>(std::max<size_t>(pieces.size(), nCh1 + nCh2),
+                                                                      kCopyThreads));
+            for (size_t t = 0; ok && t < nCopy; t++) {
+                if (!pool->stagers[t]) pool->stagers[t].reset(new Stager());
+                ok = pool->stagers[t]->init(dev);
+            }
+            if (ok) {
                 std::vector<std::thread> cp;
-                const size_t nCopy = std::min<size_t>(pieces.size(), kCopyThreads);
                 for (size_t t = 1; t < nCopy; t++)
-                    cp.emplace_back([&] {
+                    cp.emplace_back([&, t] {
                         mtb::background_thread();
-                        copy();
+                        copy(t);
                     });
-                copy();
+                copy(0);
                 for (auto& t : cp) t.join();
+                ok = stageOk;
             }
             take1.clear();
             take2.clear();
-            // the slot's device buffers live on its context's device (a new thread starts on device 0)
-            const size_t on = sizeof(uint64_t) * ((size_t)s->n + 1);
-            // growing them frees the smaller ones, and hipFree waits for the whole device: not while
-            // another context's batch runs there (growMu, below)
-            std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(ctxs[d])), std::defer_lock);
-            if (s->dseq1.cap < b1 + 1 || s->doff1.cap < on || (paired && (s->dseq2.cap < b2 + 1 || s->doff2.cap < on)))
-                gl.lock();
-            bool ok = hipSetDevice(mtb_ctx_device(ctxs[d])) == hipSuccess && s->dseq1.ensure(b1 + 1) == hipSuccess &&
-                      s->doff1.ensure(on) == hipSuccess &&
-                      hipMemcpyAsync(s->dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
-                      hipMemcpyAsync(s->doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
-            if (ok && paired)
-                ok = s->dseq2.ensure(b2 + 1) == hipSuccess && s->doff2.ensure(on) == hipSuccess &&
-                     hipMemcpyAsync(s->dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
-                     hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess;
-            ok = ok && hipEventRecord(s->uploaded, up[d]) == hipSuccess;
-            if (gl.owns_lock()) gl.unlock();
-            if (ok && partitioned) {  // the same batch on every further part's device, from the pinned host copy
+            // the offsets behind the bases (the copy stream waits for every stager's last chunks)
+            if (ok) {
+                ok = hipSetDevice(dev) == hipSuccess;
+                for (size_t t = 0; ok && t < nCopy; t++)
+                    for (int k = 0; k < 2; k++)
+                        if (pool->stagers[t]->used[k] && hipStreamWaitEvent(up[d], pool->stagers[t]->done[k], 0) != hipSuccess)
+                            ok = false;
+                ok = ok && hipMemcpyAsync(s->doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess &&
+                     (!paired || hipMemcpyAsync(s->doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[d]) == hipSuccess) &&
+                     hipEventRecord(s->uploaded, up[d]) == hipSuccess;
+            }
+            if (ok && partitioned) {  // the same batch on every further part's device: copied from the first
                 bool same = s->peers.size() == (size_t)nCtx - 1;
                 for (int p = 1; same && p < nCtx; p++) same = s->peers[p - 1]->device == mtb_ctx_device(ctxs[p]);
                 if (!same) {
@@ -1018,19 +1100,19 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                         s->peers.push_back(std::move(pi));
                     }
                 }
-                for (int p = 1; p < nCtx && ok; p++) {
+                for (int p = 1; p < nCtx && ok; p++) {  // device to device (xGMI between GPUs)
                     PeerIn& pi = *s->peers[p - 1];
                     std::unique_lock<std::mutex> pl(*growMu.at(pi.device), std::defer_lock);
                     if (pi.dseq1.cap < b1 + 1 || pi.doff1.cap < on || (paired && (pi.dseq2.cap < b2 + 1 || pi.doff2.cap < on)))
                         pl.lock();
                     ok = hipSetDevice(pi.device) == hipSuccess && pi.dseq1.ensure(b1 + 1) == hipSuccess &&
-                         pi.doff1.ensure(on) == hipSuccess &&
-                         hipMemcpyAsync(pi.dseq1.p, s->seq1.p, b1, hipMemcpyHostToDevice, up[p]) == hipSuccess &&
-                         hipMemcpyAsync(pi.doff1.p, s->off1.p, on, hipMemcpyHostToDevice, up[p]) == hipSuccess;
+                         pi.doff1.ensure(on) == hipSuccess && hipStreamWaitEvent(up[p], s->uploaded, 0) == hipSuccess &&
+                         hipMemcpyPeerAsync(pi.dseq1.p, pi.device, s->dseq1.p, dev, b1, up[p]) == hipSuccess &&
+                         hipMemcpyPeerAsync(pi.doff1.p, pi.device, s->doff1.p, dev, on, up[p]) == hipSuccess;
                     if (ok && paired)
                         ok = pi.dseq2.ensure(b2 + 1) == hipSuccess && pi.doff2.ensure(on) == hipSuccess &&
-                             hipMemcpyAsync(pi.dseq2.p, s->seq2.p, b2, hipMemcpyHostToDevice, up[p]) == hipSuccess &&
-                             hipMemcpyAsync(pi.doff2.p, s->off2.p, on, hipMemcpyHostToDevice, up[p]) == hipSuccess;
+                             hipMemcpyPeerAsync(pi.dseq2.p, pi.device, s->dseq2.p, dev, b2, up[p]) == hipSuccess &&
+                             hipMemcpyPeerAsync(pi.doff2.p, pi.device, s->doff2.p, dev, on, up[p]) == hipSuccess;
                     ok = ok && hipEventRecord(pi.uploaded, up[p]) == hipSuccess;
                 }
             }
