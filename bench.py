@@ -822,6 +822,8 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     kern, stage = tally.kern_avg(), tally.stage_avg()
     Qb, Mb = tally.avg("q"), tally.avg("m")  # per 1M-pair batch
     work = clf.stats()
+    work["workspace_bytes"] = clf.workspace_bytes  # the context's batch workspace after the timed batches
+    work["join_env"] = os.environ.get("MTB_JOIN", "") + ("/nofilter" if os.environ.get("MTB_FILTER") == "0" else "")
     # run-index fallback rate: query k-mers whose DB run the join found by a gallop (all timed batches)
     work["run_index_fallback_rate"] = round(tally.avg("gallop") / max(1, Qb), 6)
     names = kernel_names(work)
