@@ -38,6 +38,7 @@ namespace {
 struct WsBudget {
     size_t cap = 0;  // 0: the device's memory is the only limit
     size_t used = 0;
+    double grow = 1.0;  // a growth step allocates need x grow when that fits (mtb::ctx_set_grow)
 };
 
 struct DevBuf {  // grow-only device allocation
@@ -55,8 +56,19 @@ struct DevBuf {  // grow-only device allocation
         if (budget) budget->used -= bytes;
         bytes = 0;
         size_t b = need + need / 8 + 256;
-        if (budget && budget->cap && budget->used + b > budget->cap) return hipErrorOutOfMemory;
-        hipError_t e = hipMalloc(&p, b);
+        hipError_t e = hipErrorOutOfMemory;
+        if (budget && budget->grow > 1.125) {  // a small batch of a ramp: straight to the full batch's size
+            const size_t big = (size_t)((double)need * budget->grow) + 256;
+            if (!budget->cap || budget->used + big <= budget->cap) {
+                e = hipMalloc(&p, big);
+                if (e == hipSuccess) b = big;
+                else (void)hipGetLastError();
+            }
+        }
+        if (e != hipSuccess) {
+            if (budget && budget->cap && budget->used + b > budget->cap) return hipErrorOutOfMemory;
+            e = hipMalloc(&p, b);
+        }
         if (e == hipSuccess) bytes = b;
         if (e == hipSuccess && budget) budget->used += b;
         if (trace) {
@@ -1520,6 +1532,8 @@ void ctx_release_workspace(mtb_ctx* c) {
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache; }
 
 const mtb_params& ctx_params(const mtb_ctx* c) { return c->par; }
+
+void ctx_set_grow(mtb_ctx* c, double scale) { c->ws.grow = scale < 1.0 ? 1.0 : scale > 32.0 ? 32.0 : scale; }
 
 int ctx_match_view(mtb_ctx* c, std::vector<uint64_t>& mOff, const mtb_match** m, const uint32_t** counts,
                    const uint32_t** qlen) {

@@ -74,6 +74,9 @@ void ctx_release_workspace(mtb_ctx* c);
 // destroyed with the context on its device.
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c);
 const mtb_params& ctx_params(const mtb_ctx* c);
+// A batch this much smaller than the run's full batches (the ramp of mtb_start_classify): workspace
+// growth steps allocate the full batch's size at once (clamped to [1, 32]; 1 = as needed)
+void ctx_set_grow(mtb_ctx* c, double scale);
 // After an MTB_MATCH_ONLY batch: the per-read match offsets (host copy, n_reads + 1) and device
 // views of the matches (grouped by read), per-read counts and query lengths (range-partitioned run)
 int ctx_match_view(mtb_ctx* c, std::vector<uint64_t>& mOff, const mtb_match** m, const uint32_t** counts,

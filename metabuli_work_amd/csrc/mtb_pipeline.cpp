@@ -1359,7 +1359,12 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                     rc = MTB_ERR_ARG;
                     mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
                 }
+                // a ramp batch grows the workspace to a full batch's size at once (not in five steps,
+                // each a device-wide hipFree)
+                const double full = std::min<double>((double)maxBases, (double)maxReads * s->bases / std::max<uint32_t>(s->n, 1));
+                mtb::ctx_set_grow(c, s->index < kRamp && !opt->max_reads && s->bases ? full / (double)s->bases : 1.0);
                 if (rc == MTB_OK) rc = classify_slot(c, s, paired, em, pieceCap[d], splitBatches);
+                mtb::ctx_set_grow(c, 1.0);
                 if (gl.owns_lock()) gl.unlock();
                 s->gpuS = secs(g0, Clock::now());
                 s->tGpu1 = s->tGpu0 + s->gpuS;
