@@ -1005,14 +1005,14 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         if (!c->tileRec) {
             const uint64_t nT = sweep_tiles(c->D, c->sweepNom);
             DevBuf tmp;
-            HIP_TRY(tmp.ensure(sizeof(uint64_t) * kSweepStarts));
+            HIP_TRY(tmp.ensure(sizeof(uint64_t) * kSweepStartsTmp));
             HIP_TRY(hipMalloc(&c->tileRec, sizeof(uint64_t) * (nT + 1)));
             HIP_TRY(hipMalloc(&c->tilePre, sizeof(uint32_t) * (nT + 1)));
             build_sweep_tiles(c->db, c->D, c->sweepNom, tmp.as<uint64_t>(), c->tileRec, c->tilePre, s);
             HIP_TRY(hipStreamSynchronize(s));
             c->nTiles = nT;
         }
-        HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * kSweepStarts));
+        HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * kSweepStartsTmp));
         build_query_starts(qk, Q, c->qStart.as<uint32_t>(), s);
     }
     if (direct) {  // the long-run list: grown to the largest seen

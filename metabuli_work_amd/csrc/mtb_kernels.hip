@@ -1986,17 +1986,89 @@ constexpr uint64_t kSweepPrefixes = 1ull << (kQuerySortHi - kQuerySortLo);
 
 __device__ __forceinline__ uint32_t key_prefix(uint64_t v) { return (uint32_t)(v >> kQuerySortLo); }
 
-// starts[p] = first index i of the sorted array with prefix(a[i]) >= p, for p in [0, 2^24]
-template <typename A>
-__global__ void k_prefix_starts(A a, uint64_t n, uint64_t* __restrict__ starts64, uint32_t* __restrict__ starts32) {
+// starts[p] = first index i of the sorted array with prefix(a[i]) >= p, for p in [0, 2^24]: each
+// element that opens a prefix writes its index there (the rest hold ~0 from a memset), then a
+// suffix minimum fills the prefixes no element has (the gaps are unbounded for a small array)
+template <typename A, typename S>
+__global__ void k_prefix_firsts(A a, uint64_t n, S* __restrict__ starts) {
     MTB_GRID_STRIDE(i, n + 1) {
-        const uint64_t p = i < n ? key_prefix(a[i]) : kSweepPrefixes;
-        const uint64_t from = i ? (uint64_t)key_prefix(a[i - 1]) + 1 : 0;
-        for (uint64_t x = from; x <= p; x++) {
-            if (starts64) starts64[x] = i;
-            if (starts32) starts32[x] = (uint32_t)i;
+        if (i == n) {
+            starts[kSweepPrefixes] = (S)n;
+        } else {
+            const uint32_t p = key_prefix(a[i]);
+            if (i == 0 || key_prefix(a[i - 1]) != p) starts[p] = (S)i;
         }
     }
+}
+
+constexpr int kSufTile = 1024;  // entries per block of the suffix minimum (4 per thread)
+
+template <typename S>
+__global__ void __launch_bounds__(256) k_suffix_min_tiles(S* __restrict__ x, uint64_t n, S* __restrict__ tileMin) {
+    __shared__ S sm[256];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSufTile;
+    S v[4];
+    S m = (S)~(S)0;
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {  // each thread's 4 entries, suffix min within them
+        const uint64_t i = t0 + threadIdx.x * 4 + k;
+        v[k] = i < n ? x[i] : (S)~(S)0;
+        m = min(m, v[k]);
+        v[k] = m;
+    }
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {  // suffix min over the threads (Hillis-Steele)
+        const S o = threadIdx.x + d < 256 ? sm[threadIdx.x + d] : (S)~(S)0;
+        __syncthreads();
+        sm[threadIdx.x] = min(sm[threadIdx.x], o);
+        __syncthreads();
+    }
+    const S after = threadIdx.x + 1 < 256 ? sm[threadIdx.x + 1] : (S)~(S)0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t i = t0 + threadIdx.x * 4 + k;
+        if (i < n) x[i] = min(v[k], after);
+    }
+    if (threadIdx.x == 0) tileMin[blockIdx.x] = sm[0];
+}
+
+// tileMin[t] <- the minimum over the tiles after t (one 1024-thread block, a chunk of tiles per thread)
+template <typename S>
+__global__ void __launch_bounds__(1024) k_suffix_min_carry(S* __restrict__ tileMin, uint64_t nTiles) {
+    __shared__ S sm[1024];
+    const uint64_t per = (nTiles + 1023) / 1024, b = threadIdx.x * per, e = min(nTiles, b + per);
+    S m = (S)~(S)0;
+    for (uint64_t t = b; t < e; t++) m = min(m, tileMin[t]);
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const S o = threadIdx.x + d < 1024 ? sm[threadIdx.x + d] : (S)~(S)0;
+        __syncthreads();
+        sm[threadIdx.x] = min(sm[threadIdx.x], o);
+        __syncthreads();
+    }
+    S after = threadIdx.x + 1 < 1024 ? sm[threadIdx.x + 1] : (S)~(S)0;
+    for (uint64_t t = e; t-- > b;) {
+        const S v = tileMin[t];
+        tileMin[t] = after;
+        after = min(after, v);
+    }
+}
+
+template <typename S>
+__global__ void k_suffix_min_apply(S* __restrict__ x, uint64_t n, const S* __restrict__ carry) {
+    MTB_GRID_STRIDE(i, n) x[i] = min(x[i], carry[i / kSufTile]);
+}
+
+template <typename A, typename S>
+static void prefix_starts(A a, uint64_t n, S* starts, S* tmp, hipStream_t s) {
+    const uint64_t m = kSweepPrefixes + 1, nT = (m + kSufTile - 1) / kSufTile;
+    hipMemsetAsync(starts, 0xFF, sizeof(S) * m, s);
+    k_prefix_firsts<<<stride_grid(n + 1), 256, 0, s>>>(a, n, starts);
+    k_suffix_min_tiles<<<(unsigned)nT, 256, 0, s>>>(starts, m, tmp);
+    k_suffix_min_carry<<<1, 1024, 0, s>>>(tmp, nT);
+    k_suffix_min_apply<<<stride_grid(m), 256, 0, s>>>(starts, m, tmp);
 }
 
 struct KeyArr {
@@ -2044,6 +2116,8 @@ __device__ __forceinline__ bool sweep_query(uint64_t q, const uint64_t* __restri
         if (i2 <= n && vals[i2 - 1] < aa2) p2 = i2;
     }
     uint64_t lo = p1, hi = p2;
+    if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
+    if (lo > hi) hi = lo;
     if (hi - lo > kLongRun) {  // a long run: scanned by a wave of its own (k_match_long), from HBM
         const uint32_t at = atomicAdd(longCnt, 1u);
         if (at < longCap) longList[at] = LongRun{q, lo + vOff, hi + vOff};
@@ -2135,13 +2209,13 @@ uint64_t sweep_tiles(uint64_t D, uint32_t nom) { return D ? (D + nom - 1) / nom 
 
 void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
                        uint32_t* tilePre, hipStream_t s) {
-    k_prefix_starts<<<stride_grid(D + 1), 256, 0, s>>>(DbVal{db}, D, pstartTmp, nullptr);
+    prefix_starts(DbVal{db}, D, pstartTmp, pstartTmp + kSweepStarts, s);
     const uint64_t nT = sweep_tiles(D, nom);
     k_sweep_tiles<<<stride_grid(nT + 1), 256, 0, s>>>(db, D, pstartTmp, nT, nom, tileRec, tilePre);
 }
 
 void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s) {
-    k_prefix_starts<<<stride_grid(Q + 1), 256, 0, s>>>(KeyArr{qkey}, Q, nullptr, qStart);
+    prefix_starts(KeyArr{qkey}, Q, qStart, qStart + kSweepStarts, s);
 }
 
 void launch_sweep(const uint64_t* tileRec, const uint32_t* tilePre, uint64_t nTiles, const uint32_t* qStart,

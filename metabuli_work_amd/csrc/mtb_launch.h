@@ -230,11 +230,12 @@ void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, co
                        uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                        uint32_t capShift, unsigned long long* stats, hipStream_t s);
 // K4S DB-sweep join (MTB_JOIN=sweep; direct output only): tiles of ~nom DB records ending at
-// sort-prefix bucket bounds, built once per context (pstartTmp: 2^24 + 1 u64 scratch; tileRec
+// sort-prefix bucket bounds, built once per context (pstartTmp: kSweepStartsTmp u64 scratch; tileRec
 // sweep_tiles + 1 u64, tilePre sweep_tiles + 1 u32); per batch the sorted queries' bucket starts
-// (qStart: 2^24 + 1 u32), then one block per tile.
+// (qStart: kSweepStartsTmp u32: the starts and their suffix-minimum scratch), then one block per tile.
 uint64_t sweep_tiles(uint64_t D, uint32_t nom);
 constexpr uint64_t kSweepStarts = (1ull << 24) + 1;
+constexpr uint64_t kSweepStartsTmp = kSweepStarts + (kSweepStarts + 1023) / 1024;
 void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
                        uint32_t* tilePre, hipStream_t s);
 void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s);
