@@ -320,8 +320,8 @@ def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap):
     clfs = [Classifier(par, db_dir=db_dir, db_part=(p, parts)) for p in range(parts)]
     try:
         if cap:
-            clfs[1].classify_batch(r.seq1, r.off1[:701], r.seq2, r.off2[:701], match_only=True)
-            clfs[1].set_workspace_cap(int(clfs[1].workspace_bytes * 0.45))
+            clfs[1].classify_batch(r.seq1, r.off1[:701], r.seq2, r.off2[:701])  # a whole 700-read batch's workspace
+            clfs[1].set_workspace_cap(int(clfs[1].workspace_bytes * 0.6))
         with pytest.raises(MtbError, match="one context per DB part"):  # every part must be there
             clfs[0].startClassify(part, peers=[], partitioned=True)
         assert clfs[0].startClassify(part, reads_per_batch=700, report_tsv=repp, peers=clfs[1:],
