@@ -127,6 +127,7 @@ struct mtb_ctx {
     uint64_t nTiles = 0;
     uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
     uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
+    bool sweepSmall = false;     // MTB_SWEEP_SMALL=1 (A/B): 24-KB LDS tiles (2048 records), nominal 1024
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
@@ -402,6 +403,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : !strcmp(e, "sweep") ? 3 : 0;
     if (const char* e = getenv("MTB_SWEEP_NOM")) c->sweepNom = std::max(64u, std::min(4096u, (uint32_t)atoi(e)));
     if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("MTB_SWEEP_SMALL")) {
+        c->sweepSmall = atoi(e) != 0;
+        if (c->sweepSmall && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
+    }
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
@@ -563,6 +568,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->joinMode = src->joinMode;
     c->sweepNom = src->sweepNom;
     c->sweepLdsCap = src->sweepLdsCap;
+    c->sweepSmall = src->sweepSmall;
     c->matchWinCap = src->matchWinCap;
     c->directJoin = src->directJoin;
     c->directRetry = src->directRetry;
@@ -1012,8 +1018,9 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             HIP_TRY(hipStreamSynchronize(s));
             c->nTiles = nT;
         }
-        HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * kSweepStartsTmp));
-        build_query_starts(qk, Q, c->qStart.as<uint32_t>(), s);
+        HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * (kSweepStartsTmp + c->nTiles + 1)));
+        build_query_starts(qk, Q, c->qStart.as<uint32_t>(), c->tilePre, c->nTiles,
+                           c->qStart.as<uint32_t>() + kSweepStartsTmp, s);
     }
     if (direct) {  // the long-run list: grown to the largest seen
         c->longCap = std::max<uint32_t>(c->longCap, (uint32_t)std::min<uint64_t>(std::max<uint64_t>(Q / 256, 1u << 16), 1u << 30));
@@ -1034,12 +1041,13 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                          c->stageRegion, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(), s);
         else if (sweep && direct)
-            launch_sweep(c->tileRec, c->tilePre, c->nTiles, c->qStart.as<uint32_t>(), qk, qi, c->unitInfo.as<uint64_t>(),
-                         C, c->db, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
-                         c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
-                         c->spillCap, c->errFlag.as<int>(), c->probeStats.as<unsigned long long>(),
-                         c->mDirect.as<SegMatch>(), c->ovFlag.as<int>(), c->spillShift, c->longList.as<LongRun>(),
-                         c->longCap, c->longCnt.as<uint32_t>(), c->sweepLdsCap, s);
+            launch_sweep(c->tileRec, c->qStart.as<uint32_t>() + kSweepStartsTmp, c->nTiles, qk, qi,
+                         c->unitInfo.as<uint64_t>(), C, c->db, c->D, c->spOf, (uint32_t)c->maxTax, c->par.kmer_format,
+                         c->readCnt.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(),
+                         c->mRank.as<uint32_t>(), c->spillCap, c->errFlag.as<int>(),
+                         c->probeStats.as<unsigned long long>(), c->mDirect.as<SegMatch>(), c->ovFlag.as<int>(),
+                         c->spillShift, c->longList.as<LongRun>(), c->longCap, c->longCnt.as<uint32_t>(),
+                         c->sweepLdsCap, c->sweepSmall, s);
         else
             launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->db, c->D, c->dir, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),

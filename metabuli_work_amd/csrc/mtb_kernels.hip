@@ -2094,20 +2094,19 @@ __global__ void k_sweep_tiles(const DbRec* __restrict__ db, uint64_t D, const ui
     }
 }
 
-// One query of a tile against the tile's records (LDS or HBM view; vOff = DB index of view[0]).
+// One query of a tile against the tile's records (LDS or HBM view; vOff = DB index of view[0]); its
+// key, slot and unit record are loaded by the caller (the first query of a thread while its tile is
+// still in flight).
 template <typename V, typename T>
-__device__ __forceinline__ bool sweep_query(uint64_t q, const uint64_t* __restrict__ qkey,
-                                            const uint32_t* __restrict__ qslot, const V& vals, const T& taxs,
-                                            uint32_t n, uint32_t pow2, uint64_t vOff, const uint64_t* __restrict__ unitInfo,
-                                            uint32_t C, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
+__device__ __forceinline__ bool sweep_query(uint64_t q, uint64_t key, uint32_t slot, ulonglong2 ur, const V& vals,
+                                            const T& taxs, uint32_t n, uint32_t pow2, uint64_t vOff, uint32_t C,
+                                            uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
                                             int kmerFormat, uint32_t* __restrict__ readCnt,
                                             unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
                                             uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
                                             SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
                                             LongRun* __restrict__ longList, uint32_t longCap,
                                             uint32_t* __restrict__ longCnt) {
-    const uint64_t key = qkey[q];
-    const uint32_t slot = qslot[q];
     const uint64_t aa = key & kAAMask, aa2 = aa + (1ull << 24);
     uint32_t p1 = 0, p2 = 0;  // lower bounds of aa and aa2: two fixed-trip searches, interleaved
     for (uint32_t step = pow2; step > 0; step >>= 1) {
@@ -2128,7 +2127,7 @@ __device__ __forceinline__ bool sweep_query(uint64_t q, const uint64_t* __restri
     const uint32_t c = run_select(hr, vals, vOff, lo, hi, D, thr);
     if (!c) return false;
     uint32_t pu;
-    const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, pu)];
+    (void)slot_unit(slot, C, pu);
     const uint64_t info = unit_info_at(ur.x, pu, kmerFormat);
     const uint32_t rk = atomicAdd(&readCnt[info_seq(info) - 1], c);
     const uint64_t o = (ur.y & kStretchLoMask) * C, cap = ((ur.y >> 40) * C) >> capShift;
@@ -2146,8 +2145,16 @@ __device__ __forceinline__ bool sweep_query(uint64_t q, const uint64_t* __restri
     return true;
 }
 
-__global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tilePre,
-                                               const uint32_t* __restrict__ qStart, const uint64_t* __restrict__ qkey,
+// tileQ[t] = the first sorted query of tile t's buckets (per batch: one coalesced pass, so a sweep
+// block reads its query range and its records' range in one round trip)
+__global__ void k_tile_queries(const uint32_t* __restrict__ tilePre, uint64_t nTiles, const uint32_t* __restrict__ qStart,
+                               uint32_t* __restrict__ tileQ) {
+    MTB_GRID_STRIDE(t, nTiles + 1) tileQ[t] = qStart[tilePre[t]];
+}
+
+template <uint32_t kCap>
+__global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tileQ,
+                                               const uint64_t* __restrict__ qkey,
                                                const uint32_t* __restrict__ qslot, const uint64_t* __restrict__ unitInfo,
                                                uint32_t C, const DbRec* __restrict__ db, uint64_t D,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
@@ -2158,18 +2165,42 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
                                                int* __restrict__ overflow, uint32_t capShift,
                                                LongRun* __restrict__ longList, uint32_t longCap,
                                                uint32_t* __restrict__ longCnt, uint32_t ldsCap) {
-    constexpr uint32_t kVec = kSweepCap * 12 / 16 + 1;  // 16-B vectors of a full tile (+1: unaligned start)
+    constexpr uint32_t kVec = kCap * 12 / 16 + 1;  // 16-B vectors of a full tile (+1: unaligned start)
     constexpr int kLoad = (int)((kVec + 255) / 256);
     __shared__ uint4 sRaw[kVec];
     const uint64_t t = blockIdx.x;
-    const uint32_t q0 = qStart[tilePre[t]], q1 = qStart[tilePre[t + 1]];
-    if (q0 >= q1) return;  // no query in the tile's buckets: its records are not read
+    const uint32_t q0 = tileQ[t], q1 = tileQ[t + 1];
     const uint64_t r0 = tileRec[t], r1 = tileRec[t + 1];
+    if (q0 >= q1) return;  // no query in the tile's buckets: its records are not read
     const uint32_t n = (uint32_t)(r1 - r0);
     uint32_t pow2 = 1;
     while (pow2 * 2 <= n) pow2 *= 2;
+    // the thread's first query: key and slot, then its unit record, loaded while the tile streams in
+    const uint64_t qa = q0 + threadIdx.x;
+    const bool has0 = qa < q1;
+    uint64_t key0 = 0;
+    uint32_t slot0 = 0;
+    if (has0) {
+        key0 = qkey[qa];
+        slot0 = qslot[qa];
+    }
     uint32_t hits = 0;
-    if (n <= ldsCap) {
+    auto unit_of = [&](uint32_t slot) {
+        uint32_t p;
+        return reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, p)];
+    };
+    auto run = [&](const auto& vals, const auto& taxs, ulonglong2 ur0) {
+        if (has0)
+            hits += sweep_query(qa, key0, slot0, ur0, vals, taxs, n, pow2, r0, C, D, spOf, maxTax, kmerFormat, readCnt,
+                                total, buf, bufRank, region, err, direct, overflow, capShift, longList, longCap, longCnt);
+        for (uint64_t q = qa + 256; q < q1; q += 256) {
+            const uint32_t slot = qslot[q];
+            hits += sweep_query(q, qkey[q], slot, unit_of(slot), vals, taxs, n, pow2, r0, C, D, spOf, maxTax,
+                                kmerFormat, readCnt, total, buf, bufRank, region, err, direct, overflow, capShift,
+                                longList, longCap, longCnt);
+        }
+    };
+    if (n <= ldsCap && n <= kCap) {
         const uint64_t b0 = (r0 * 12) & ~15ull;
         const uint32_t nv = (uint32_t)((r1 * 12 - b0 + 15) >> 4);  // the pad records make the tail readable
         const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(db) + b0);
@@ -2179,6 +2210,8 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
             const uint32_t i = threadIdx.x + (uint32_t)j * 256;
             v[j] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
         }
+        ulonglong2 ur0 = make_ulonglong2(0, 0);
+        if (has0) ur0 = unit_of(slot0);
 #pragma unroll
         for (int j = 0; j < kLoad; j++) {
             const uint32_t i = threadIdx.x + (uint32_t)j * 256;
@@ -2186,19 +2219,9 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
         }
         __syncthreads();
         const DbRec* rec = reinterpret_cast<const DbRec*>(reinterpret_cast<const char*>(sRaw) + (r0 * 12 - b0));
-        const DbVal vals{rec};
-        const DbTax taxs{rec};
-        for (uint64_t q = q0 + threadIdx.x; q < q1; q += 256)
-            hits += sweep_query(q, qkey, qslot, vals, taxs, n, pow2, r0, unitInfo, C, D, spOf, maxTax, kmerFormat,
-                                readCnt, total, buf, bufRank, region, err, direct, overflow, capShift, longList, longCap,
-                                longCnt);
+        run(DbVal{rec}, DbTax{rec}, ur0);
     } else {  // one sort-prefix bucket longer than an LDS tile (heavily shared AA 8-mers): from HBM
-        const DbVal vals{db + r0};
-        const DbTax taxs{db + r0};
-        for (uint64_t q = q0 + threadIdx.x; q < q1; q += 256)
-            hits += sweep_query(q, qkey, qslot, vals, taxs, n, pow2, r0, unitInfo, C, D, spOf, maxTax, kmerFormat,
-                                readCnt, total, buf, bufRank, region, err, direct, overflow, capShift, longList, longCap,
-                                longCnt);
+        run(DbVal{db + r0}, DbTax{db + r0}, has0 ? unit_of(slot0) : make_ulonglong2(0, 0));
     }
     const uint32_t w = wave_sum_u32(hits);
     if ((threadIdx.x & 63) == 0 && w) atomicAdd(&stats[t % kStatStripes], (unsigned long long)w);
@@ -2214,21 +2237,28 @@ void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* psta
     k_sweep_tiles<<<stride_grid(nT + 1), 256, 0, s>>>(db, D, pstartTmp, nT, nom, tileRec, tilePre);
 }
 
-void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s) {
+void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, const uint32_t* tilePre, uint64_t nTiles,
+                        uint32_t* tileQ, hipStream_t s) {
     prefix_starts(KeyArr{qkey}, Q, qStart, qStart + kSweepStarts, s);
+    k_tile_queries<<<stride_grid(nTiles + 1), 256, 0, s>>>(tilePre, nTiles, qStart, tileQ);
 }
 
-void launch_sweep(const uint64_t* tileRec, const uint32_t* tilePre, uint64_t nTiles, const uint32_t* qStart,
-                  const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db,
-                  uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt,
-                  unsigned long long* total, mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err,
-                  unsigned long long* stats, SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList,
-                  uint32_t longCap, uint32_t* longCnt, uint32_t ldsCap, hipStream_t s) {
+void launch_sweep(const uint64_t* tileRec, const uint32_t* tileQ, uint64_t nTiles, const uint64_t* qkey,
+                  const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D,
+                  const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
+                  mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
+                  SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList, uint32_t longCap,
+                  uint32_t* longCnt, uint32_t ldsCap, bool small, hipStream_t s) {
     if (!nTiles || D < 2) return;
-    k_sweep<<<(unsigned)nTiles, 256, 0, s>>>(tileRec, tilePre, qStart, qkey, qslot, unitInfo, C, db, D, spOf, maxTax,
-                                             kmerFormat, readCnt, total, buf, bufRank, region, err, stats, direct,
-                                             overflow, capShift, longList, longCap, longCnt,
-                                             std::min<uint32_t>(ldsCap, kSweepCap));
+    if (small)  // 24-KB tiles: twice the blocks per CU (tiles of more than 2048 records search HBM)
+        k_sweep<2048><<<(unsigned)nTiles, 256, 0, s>>>(tileRec, tileQ, qkey, qslot, unitInfo, C, db, D, spOf, maxTax,
+                                                       kmerFormat, readCnt, total, buf, bufRank, region, err, stats,
+                                                       direct, overflow, capShift, longList, longCap, longCnt, ldsCap);
+    else
+        k_sweep<kSweepCap><<<(unsigned)nTiles, 256, 0, s>>>(tileRec, tileQ, qkey, qslot, unitInfo, C, db, D, spOf,
+                                                            maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
+                                                            err, stats, direct, overflow, capShift, longList, longCap,
+                                                            longCnt, ldsCap);
 }
 
 }  // namespace mtb

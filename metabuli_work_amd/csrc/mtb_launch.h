@@ -238,13 +238,14 @@ constexpr uint64_t kSweepStarts = (1ull << 24) + 1;
 constexpr uint64_t kSweepStartsTmp = kSweepStarts + (kSweepStarts + 1023) / 1024;
 void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
                        uint32_t* tilePre, hipStream_t s);
-void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, hipStream_t s);
-void launch_sweep(const uint64_t* tileRec, const uint32_t* tilePre, uint64_t nTiles, const uint32_t* qStart,
-                  const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db,
-                  uint64_t D, const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt,
-                  unsigned long long* total, mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err,
-                  unsigned long long* stats, SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList,
-                  uint32_t longCap, uint32_t* longCnt, uint32_t ldsCap, hipStream_t s);  // ldsCap: tests (HBM tiles)
+void build_query_starts(const uint64_t* qkey, uint64_t Q, uint32_t* qStart, const uint32_t* tilePre, uint64_t nTiles,
+                        uint32_t* tileQ, hipStream_t s);  // + tileQ (nTiles + 1): each tile's first query
+void launch_sweep(const uint64_t* tileRec, const uint32_t* tileQ, uint64_t nTiles, const uint64_t* qkey,
+                  const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D,
+                  const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
+                  mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
+                  SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList, uint32_t longCap,
+                  uint32_t* longCnt, uint32_t ldsCap, bool small, hipStream_t s);  // ldsCap: tests (HBM tiles)
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,

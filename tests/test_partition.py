@@ -320,8 +320,13 @@ def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap):
     clfs = [Classifier(par, db_dir=db_dir, db_part=(p, parts)) for p in range(parts)]
     try:
         if cap:
-            clfs[1].classify_batch(r.seq1, r.off1[:701], r.seq2, r.off2[:701])  # a whole 700-read batch's workspace
-            clfs[1].set_workspace_cap(int(clfs[1].workspace_bytes * 0.6))
+            # between a 100-read and a 700-read batch's workspace (a part of the DB, fresh context)
+            with Classifier(par, db_dir=db_dir, db_part=(1, parts)) as probe:
+                probe.classify_batch(r.seq1, r.off1[:101], r.seq2, r.off2[:101])
+                small = probe.workspace_bytes
+                probe.classify_batch(r.seq1, r.off1[:701], r.seq2, r.off2[:701])
+                big = probe.workspace_bytes
+            clfs[1].set_workspace_cap((small + big) // 2)
         with pytest.raises(MtbError, match="one context per DB part"):  # every part must be there
             clfs[0].startClassify(part, peers=[], partitioned=True)
         assert clfs[0].startClassify(part, reads_per_batch=700, report_tsv=repp, peers=clfs[1:],
