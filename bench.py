@@ -105,7 +105,7 @@ def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2, dbread=0
         # written into the reads' segments (direct join)
         # the DB-sweep join (MTB_JOIN=sweep) reads the records of every tile that holds queries once,
         # coalesced (dbread of them: all D at these batch sizes)
-        "match_join": 12 * Q + (12 * dbread if dbread else 28 * Q if D > 24 * Q else 12 * D) + 16 * M,
+        "match_join": 12 * Q + (12 * dbread if dbread else 28 * Q if D > 12 * Q else 12 * D) + 16 * M,
         "match_transpose": 2 * 24 * M + 4 * M + 8 * n,      # staged matches (+ rank) read, written to segments
         "match_sort": 16 * M + 24 * live + 8 * (n + 1),     # each read's segment matches read, live ones written
         "assign": 24 * live + 32 * n + 4 * n + 8 * n,       # live sorted matches read, results + lengths
@@ -163,7 +163,7 @@ def random_roofline(kern, names, Qall, Q, matched, M, D, sweep=False):
 
     out = {}
     req = {"filter": (float(Qall), 5.4)}
-    if D > 24 * Q and not sweep:
+    if D > 12 * Q and not sweep:
         req["match_join"] = (2.0 * Q + float(matched) + M, 144.0)
     for k, (r, gb) in req.items():
         if k not in names or r <= 0:

@@ -973,7 +973,10 @@ void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, cons
 // directory instead.
 constexpr int kMatchQ = 256;
 constexpr int kMatchWin = 3072;
-constexpr uint32_t kStageFreeRatio = 24;  // D / Q above which K4 runs without LDS windows
+// D / Q above which K4 runs without LDS windows: a 256-query block's window (256 D / Q values) would
+// pass the 3072-value LDS cap and search HBM through the directory anyway (round 4: 24 sent 3M-pair
+// GTDB batches, D / Q = 17, through that path: join 35 -> 61 ms)
+constexpr uint32_t kStageFreeRatio = 12;
 constexpr int kFreePer = 1;               // queries per thread in the unstaged K4 (2: no gain with the run index; +1.6 ms before)
 constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
