@@ -100,7 +100,7 @@ def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2, dbread=0
         "extract": read_bytes,                               # K0 read metadata (the keys stay in the fused K1F)
         "kmer_sort": 2 * 3 * 12 * Q,                        # three passes over the (key, slot) pairs
         # queries, the DB (12-B value + taxID records) read once through the block windows, or, when
-        # the DB is much larger than the query stream (D > 24 Q), each query's run: its two
+        # the DB is much larger than the query stream (D > 12 Q), each query's run: its two
         # run-index entries (4 B) and the run's first two records (24 B); the 16-B segment matches
         # written into the reads' segments (direct join)
         # the DB-sweep join (MTB_JOIN=sweep) reads the records of every tile that holds queries once,
