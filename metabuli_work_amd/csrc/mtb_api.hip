@@ -128,6 +128,7 @@ struct mtb_ctx {
     uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
     uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
     bool sweepSmall = false;     // MTB_SWEEP_SMALL=1 (A/B): 24-KB LDS tiles (2048 records), nominal 1024
+    int sweepPersist = 1;        // MTB_SWEEP_PERSIST: resident blocks per CU slot (0: one block per tile)
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
@@ -403,6 +404,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : !strcmp(e, "sweep") ? 3 : 0;
     if (const char* e = getenv("MTB_SWEEP_NOM")) c->sweepNom = std::max(64u, std::min(4096u, (uint32_t)atoi(e)));
     if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("MTB_SWEEP_PERSIST")) c->sweepPersist = std::max(0, atoi(e));
     if (const char* e = getenv("MTB_SWEEP_SMALL")) {
         c->sweepSmall = atoi(e) != 0;
         if (c->sweepSmall && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
@@ -569,6 +571,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->sweepNom = src->sweepNom;
     c->sweepLdsCap = src->sweepLdsCap;
     c->sweepSmall = src->sweepSmall;
+    c->sweepPersist = src->sweepPersist;
     c->matchWinCap = src->matchWinCap;
     c->directJoin = src->directJoin;
     c->directRetry = src->directRetry;
@@ -1047,7 +1050,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->mRank.as<uint32_t>(), c->spillCap, c->errFlag.as<int>(),
                          c->probeStats.as<unsigned long long>(), c->mDirect.as<SegMatch>(), c->ovFlag.as<int>(),
                          c->spillShift, c->longList.as<LongRun>(), c->longCap, c->longCnt.as<uint32_t>(),
-                         c->sweepLdsCap, c->sweepSmall, s);
+                         c->sweepLdsCap, c->sweepSmall, c->sweepPersist, s);
         else
             launch_match(qk, qi, c->unitInfo.as<uint64_t>(), C, Q, c->db, c->D, c->dir, c->spOf,
                          (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),

@@ -2231,6 +2231,103 @@ __global__ void __launch_bounds__(256) k_sweep(const uint64_t* __restrict__ tile
     if (threadIdx.x == 0) atomicAdd(&stats[kStatStripes + 1 + t % kStatStripes], (unsigned long long)n);
 }
 
+// Persistent form of the sweep: a block walks tiles blockIdx.x, + gridDim.x, ... and keeps the next
+// tile's records in flight (in registers) while it searches the current one's queries from LDS, so a
+// CU's HBM requests do not stop during the query phases (the rank atomics and unit-record loads are
+// round trips). Tile descriptors (query range, record range) are loaded one tile further ahead.
+struct SweepDesc {
+    uint32_t q0, q1;
+    uint64_t r0, r1;
+};
+__device__ __forceinline__ SweepDesc sweep_desc(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tileQ,
+                                                uint64_t t, uint64_t nTiles) {
+    if (t >= nTiles) return SweepDesc{0, 0, 0, 0};
+    return SweepDesc{tileQ[t], tileQ[t + 1], tileRec[t], tileRec[t + 1]};
+}
+
+template <uint32_t kCap>
+__global__ void __launch_bounds__(256) k_sweep_p(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tileQ,
+                                                 uint64_t nTiles, const uint64_t* __restrict__ qkey,
+                                                 const uint32_t* __restrict__ qslot, const uint64_t* __restrict__ unitInfo,
+                                                 uint32_t C, const DbRec* __restrict__ db, uint64_t D,
+                                                 const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                                 uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
+                                                 mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
+                                                 uint64_t region, int* __restrict__ err,
+                                                 unsigned long long* __restrict__ stats, SegMatch* __restrict__ direct,
+                                                 int* __restrict__ overflow, uint32_t capShift,
+                                                 LongRun* __restrict__ longList, uint32_t longCap,
+                                                 uint32_t* __restrict__ longCnt, uint32_t ldsCap) {
+    constexpr uint32_t kVec = kCap * 12 / 16 + 1;
+    constexpr int kLoad = (int)((kVec + 255) / 256);
+    __shared__ uint4 sRaw[kVec];
+    const uint64_t G = gridDim.x;
+    uint64_t t = blockIdx.x;
+    SweepDesc cur = sweep_desc(tileRec, tileQ, t, nTiles);
+    SweepDesc nxt = sweep_desc(tileRec, tileQ, t + G, nTiles);
+    auto staged = [&](const SweepDesc& d) { return d.q0 < d.q1 && d.r1 - d.r0 <= (uint64_t)min(ldsCap, kCap); };
+    uint4 v[kLoad];
+    auto issue = [&](const SweepDesc& d) {  // the tile's 16-B vectors into registers (all in flight)
+        const uint64_t b0 = (d.r0 * 12) & ~15ull;
+        const uint32_t nv = (uint32_t)((d.r1 * 12 - b0 + 15) >> 4);
+        const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(db) + b0);
+#pragma unroll
+        for (int j = 0; j < kLoad; j++) {
+            const uint32_t i = threadIdx.x + (uint32_t)j * 256;
+            v[j] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if (staged(cur)) issue(cur);
+    uint32_t hits = 0;
+    uint64_t recs = 0;
+    while (t < nTiles) {
+        const bool st = staged(cur);
+        if (st) {
+            const uint64_t b0 = (cur.r0 * 12) & ~15ull;
+            const uint32_t nv = (uint32_t)((cur.r1 * 12 - b0 + 15) >> 4);
+            __syncthreads();  // the previous tile's searches are done with the LDS
+#pragma unroll
+            for (int j = 0; j < kLoad; j++) {
+                const uint32_t i = threadIdx.x + (uint32_t)j * 256;
+                if (i < nv) sRaw[i] = v[j];
+            }
+            __syncthreads();
+        }
+        // the next tile streams in while this one's queries are searched
+        const SweepDesc after = sweep_desc(tileRec, tileQ, t + 2 * G, nTiles);
+        if (staged(nxt)) issue(nxt);
+        if (cur.q0 < cur.q1) {
+            const uint32_t n = (uint32_t)(cur.r1 - cur.r0);
+            uint32_t pow2 = 1;
+            while (pow2 * 2 <= n) pow2 *= 2;
+            recs += n;
+            auto run = [&](const auto& vals, const auto& taxs) {
+                for (uint64_t q = cur.q0 + threadIdx.x; q < cur.q1; q += 256) {
+                    const uint32_t slot = qslot[q];
+                    uint32_t p;
+                    const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, p)];
+                    hits += sweep_query(q, qkey[q], slot, ur, vals, taxs, n, pow2, cur.r0, C, D, spOf, maxTax,
+                                        kmerFormat, readCnt, total, buf, bufRank, region, err, direct, overflow,
+                                        capShift, longList, longCap, longCnt);
+                }
+            };
+            if (st) {
+                const uint64_t b0 = (cur.r0 * 12) & ~15ull;
+                const DbRec* rec = reinterpret_cast<const DbRec*>(reinterpret_cast<const char*>(sRaw) + (cur.r0 * 12 - b0));
+                run(DbVal{rec}, DbTax{rec});
+            } else {  // a bucket longer than an LDS tile: from HBM
+                run(DbVal{db + cur.r0}, DbTax{db + cur.r0});
+            }
+        }
+        t += G;
+        cur = nxt;
+        nxt = after;
+    }
+    const uint32_t w = wave_sum_u32(hits);
+    if ((threadIdx.x & 63) == 0 && w) atomicAdd(&stats[blockIdx.x % kStatStripes], (unsigned long long)w);
+    if (threadIdx.x == 0 && recs) atomicAdd(&stats[kStatStripes + 1 + blockIdx.x % kStatStripes], (unsigned long long)recs);
+}
+
 uint64_t sweep_tiles(uint64_t D, uint32_t nom) { return D ? (D + nom - 1) / nom : 0; }
 
 void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
@@ -2251,8 +2348,25 @@ void launch_sweep(const uint64_t* tileRec, const uint32_t* tileQ, uint64_t nTile
                   const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
                   mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
                   SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList, uint32_t longCap,
-                  uint32_t* longCnt, uint32_t ldsCap, bool small, hipStream_t s) {
+                  uint32_t* longCnt, uint32_t ldsCap, bool small, int persist, hipStream_t s) {
     if (!nTiles || D < 2) return;
+    if (persist) {  // blocks resident on every CU (3 per CU at 48-KB tiles), each walking its tiles
+        int cus = 256;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        // resident blocks per CU: 3 for 48-KB tiles (LDS, and 145 VGPRs), 4 for 24-KB tiles (109 VGPRs)
+        const uint64_t g = std::min<uint64_t>(nTiles, (uint64_t)cus * (small ? 4 : 3) * persist);
+        if (small)
+            k_sweep_p<2048><<<(unsigned)g, 256, 0, s>>>(tileRec, tileQ, nTiles, qkey, qslot, unitInfo, C, db, D, spOf,
+                                                        maxTax, kmerFormat, readCnt, total, buf, bufRank, region, err,
+                                                        stats, direct, overflow, capShift, longList, longCap, longCnt,
+                                                        ldsCap);
+        else
+            k_sweep_p<kSweepCap><<<(unsigned)g, 256, 0, s>>>(tileRec, tileQ, nTiles, qkey, qslot, unitInfo, C, db, D,
+                                                             spOf, maxTax, kmerFormat, readCnt, total, buf, bufRank,
+                                                             region, err, stats, direct, overflow, capShift, longList,
+                                                             longCap, longCnt, ldsCap);
+        return;
+    }
     if (small)  // 24-KB tiles: twice the blocks per CU (tiles of more than 2048 records search HBM)
         k_sweep<2048><<<(unsigned)nTiles, 256, 0, s>>>(tileRec, tileQ, qkey, qslot, unitInfo, C, db, D, spOf, maxTax,
                                                        kmerFormat, readCnt, total, buf, bufRank, region, err, stats,

@@ -245,7 +245,8 @@ void launch_sweep(const uint64_t* tileRec, const uint32_t* tileQ, uint64_t nTile
                   const int32_t* spOf, uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total,
                   mtb_match* buf, uint32_t* bufRank, uint64_t region, int* err, unsigned long long* stats,
                   SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList, uint32_t longCap,
-                  uint32_t* longCnt, uint32_t ldsCap, bool small, hipStream_t s);  // ldsCap: tests (HBM tiles)
+                  uint32_t* longCnt, uint32_t ldsCap, bool small, int persist, hipStream_t s);
+// ldsCap: tests (HBM tiles); small: 24-KB tiles; persist: resident blocks per CU slot (0: a block per tile)
 void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* unitInfo, uint32_t C, uint64_t Q,
                   const DbRec* db, uint64_t D, const AADir& dir, const int32_t* spOf,
                   uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
