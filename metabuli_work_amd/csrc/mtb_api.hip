@@ -128,7 +128,7 @@ struct mtb_ctx {
     uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
     uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
     bool sweepSmall = false;     // MTB_SWEEP_SMALL=1 (A/B): 24-KB LDS tiles (2048 records), nominal 1024
-    int sweepPersist = 1;        // MTB_SWEEP_PERSIST: resident blocks per CU slot (0: one block per tile)
+    int sweepPersist = 2;        // MTB_SWEEP_PERSIST: 2 warp-specialised (default), 1 persistent, 0 a block per tile
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
@@ -404,11 +404,10 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->joinMode = !strcmp(e, "sort") ? 1 : !strcmp(e, "probe") ? 2 : !strcmp(e, "sweep") ? 3 : 0;
     if (const char* e = getenv("MTB_SWEEP_NOM")) c->sweepNom = std::max(64u, std::min(4096u, (uint32_t)atoi(e)));
     if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
-    if (const char* e = getenv("MTB_SWEEP_PERSIST")) c->sweepPersist = std::max(0, atoi(e));
-    if (const char* e = getenv("MTB_SWEEP_SMALL")) {
-        c->sweepSmall = atoi(e) != 0;
-        if (c->sweepSmall && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
-    }
+    if (const char* e = getenv("MTB_SWEEP_PERSIST")) c->sweepPersist = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("MTB_SWEEP_SMALL")) c->sweepSmall = atoi(e) != 0;
+    // the warp-specialised sweep stages 24-KB tiles: nominal 1024 records (tiles ~ one bucket)
+    if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));

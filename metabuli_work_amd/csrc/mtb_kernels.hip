@@ -2328,6 +2328,109 @@ __global__ void __launch_bounds__(256) k_sweep_p(const uint64_t* __restrict__ ti
     if (threadIdx.x == 0 && recs) atomicAdd(&stats[kStatStripes + 1 + blockIdx.x % kStatStripes], (unsigned long long)recs);
 }
 
+// Warp-specialised sweep (the default): a 512-thread block whose first four waves only stream tiles
+// (global -> registers -> one of two LDS buffers) and whose other four only search queries. The
+// vector-memory counter is per wave and in order, so in one wave a tile prefetch would hold up every
+// later query load and rank atomic until the whole tile arrived (the persistent form measured ~10 us
+// per tile); split over waves the two streams overlap. Lock-step iterations: in iteration k the
+// loaders write tile k (loaded during iteration k-1) into buffer k & 1 and issue tile k+1's loads,
+// while the searchers work on tile k-1 in the other buffer; one barrier ends the iteration.
+template <uint32_t kCap>
+__global__ void __launch_bounds__(512) k_sweep_ws(const uint64_t* __restrict__ tileRec, const uint32_t* __restrict__ tileQ,
+                                                  uint64_t nTiles, const uint64_t* __restrict__ qkey,
+                                                  const uint32_t* __restrict__ qslot,
+                                                  const uint64_t* __restrict__ unitInfo, uint32_t C,
+                                                  const DbRec* __restrict__ db, uint64_t D,
+                                                  const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                                  uint32_t* __restrict__ readCnt, unsigned long long* __restrict__ total,
+                                                  mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
+                                                  uint64_t region, int* __restrict__ err,
+                                                  unsigned long long* __restrict__ stats, SegMatch* __restrict__ direct,
+                                                  int* __restrict__ overflow, uint32_t capShift,
+                                                  LongRun* __restrict__ longList, uint32_t longCap,
+                                                  uint32_t* __restrict__ longCnt, uint32_t ldsCap) {
+    constexpr uint32_t kVec = kCap * 12 / 16 + 1;
+    constexpr int kLoad = (int)((kVec + 255) / 256);
+    __shared__ uint4 sBuf[2][kVec];
+    __shared__ SweepDesc sDesc[2];
+    const bool loader = threadIdx.x < 256;
+    const uint32_t lt = threadIdx.x & 255;
+    const uint64_t G = gridDim.x, t0 = blockIdx.x;
+    const uint64_t m = t0 < nTiles ? (nTiles - t0 + G - 1) / G : 0;  // this block's tiles
+    const uint32_t cap = min(ldsCap, kCap);
+    auto staged = [&](const SweepDesc& d) { return d.q0 < d.q1 && d.r1 - d.r0 <= (uint64_t)cap; };
+    uint4 v[kLoad];
+    SweepDesc dCur{0, 0, 0, 0}, dAhead{0, 0, 0, 0};
+    auto issue = [&](const SweepDesc& d) {
+        const uint64_t b0 = (d.r0 * 12) & ~15ull;
+        const uint32_t nv = (uint32_t)((d.r1 * 12 - b0 + 15) >> 4);
+        const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(db) + b0);
+#pragma unroll
+        for (int j = 0; j < kLoad; j++) {
+            const uint32_t i = lt + (uint32_t)j * 256;
+            v[j] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if (loader && m) {
+        dCur = sweep_desc(tileRec, tileQ, t0, nTiles);
+        if (staged(dCur)) issue(dCur);
+        dAhead = sweep_desc(tileRec, tileQ, t0 + G, nTiles);
+    }
+    uint32_t hits = 0;
+    uint64_t recs = 0;
+    for (uint64_t k = 0; k <= m; k++) {
+        if (loader) {
+            if (k < m) {  // tile k into buffer k & 1, then tile k + 1's loads
+                if (staged(dCur)) {
+                    const uint64_t b0 = (dCur.r0 * 12) & ~15ull;
+                    const uint32_t nv = (uint32_t)((dCur.r1 * 12 - b0 + 15) >> 4);
+#pragma unroll
+                    for (int j = 0; j < kLoad; j++) {
+                        const uint32_t i = lt + (uint32_t)j * 256;
+                        if (i < nv) sBuf[k & 1][i] = v[j];
+                    }
+                }
+                if (lt == 0) sDesc[k & 1] = dCur;
+                dCur = dAhead;
+                if (k + 1 < m && staged(dCur)) issue(dCur);
+                dAhead = sweep_desc(tileRec, tileQ, t0 + (k + 2) * G, nTiles);
+            }
+        } else if (k >= 1) {  // tile k - 1 from buffer (k - 1) & 1
+            const SweepDesc d = sDesc[(k - 1) & 1];
+            if (d.q0 < d.q1) {
+                const uint32_t n = (uint32_t)(d.r1 - d.r0);
+                uint32_t pow2 = 1;
+                while (pow2 * 2 <= n) pow2 *= 2;
+                recs += n;
+                auto run = [&](const auto& vals, const auto& taxs) {
+                    for (uint64_t q = d.q0 + lt; q < d.q1; q += 256) {
+                        const uint32_t slot = qslot[q];
+                        uint32_t p;
+                        const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, p)];
+                        hits += sweep_query(q, qkey[q], slot, ur, vals, taxs, n, pow2, d.r0, C, D, spOf, maxTax,
+                                            kmerFormat, readCnt, total, buf, bufRank, region, err, direct, overflow,
+                                            capShift, longList, longCap, longCnt);
+                    }
+                };
+                if (staged(d)) {
+                    const uint64_t b0 = (d.r0 * 12) & ~15ull;
+                    const DbRec* rec = reinterpret_cast<const DbRec*>(
+                        reinterpret_cast<const char*>(sBuf[(k - 1) & 1]) + (d.r0 * 12 - b0));
+                    run(DbVal{rec}, DbTax{rec});
+                } else {  // a bucket longer than an LDS tile: from HBM
+                    run(DbVal{db + d.r0}, DbTax{db + d.r0});
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!loader) {
+        const uint32_t w = wave_sum_u32(hits);
+        if ((threadIdx.x & 63) == 0 && w) atomicAdd(&stats[blockIdx.x % kStatStripes], (unsigned long long)w);
+        if (lt == 0 && recs) atomicAdd(&stats[kStatStripes + 1 + blockIdx.x % kStatStripes], (unsigned long long)recs);
+    }
+}
+
 uint64_t sweep_tiles(uint64_t D, uint32_t nom) { return D ? (D + nom - 1) / nom : 0; }
 
 void build_sweep_tiles(const DbRec* db, uint64_t D, uint32_t nom, uint64_t* pstartTmp, uint64_t* tileRec,
@@ -2350,6 +2453,16 @@ void launch_sweep(const uint64_t* tileRec, const uint32_t* tileQ, uint64_t nTile
                   SegMatch* direct, int* overflow, uint32_t capShift, LongRun* longList, uint32_t longCap,
                   uint32_t* longCnt, uint32_t ldsCap, bool small, int persist, hipStream_t s) {
     if (!nTiles || D < 2) return;
+    if (persist == 2) {  // warp-specialised: 24-KB tiles, two LDS buffers, 2 blocks of 512 threads per CU (121 VGPRs)
+        int cus = 256;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        const uint64_t g = std::min<uint64_t>(nTiles, (uint64_t)cus * 2);
+        k_sweep_ws<2048><<<(unsigned)g, 512, 0, s>>>(tileRec, tileQ, nTiles, qkey, qslot, unitInfo, C, db, D, spOf,
+                                                     maxTax, kmerFormat, readCnt, total, buf, bufRank, region, err,
+                                                     stats, direct, overflow, capShift, longList, longCap, longCnt,
+                                                     ldsCap);
+        return;
+    }
     if (persist) {  // blocks resident on every CU (3 per CU at 48-KB tiles), each walking its tiles
         int cus = 256;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
