@@ -372,6 +372,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     }
     c->openS[1] = since(tp);
     if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e));  // A/B only: invalid results
+    if (const char* e = getenv("MTB_AB_SWEEP_COUNT")) set_ab_sweep_count(atoi(e));  // A/B only: invalid results
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix

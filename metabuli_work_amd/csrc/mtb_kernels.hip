@@ -2148,6 +2148,9 @@ __device__ __forceinline__ bool sweep_query(uint64_t q, uint64_t key, uint32_t s
     return true;
 }
 
+__device__ int g_abSweepCount = 0;  // MTB_AB_SWEEP_COUNT=1 (A/B only): k_sweep_ws without emission
+void set_ab_sweep_count(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abSweepCount), &on, sizeof(int)); }
+
 // tileQ[t] = the first sorted query of tile t's buckets (per batch: one coalesced pass, so a sweep
 // block reads its query range and its records' range in one round trip)
 __global__ void k_tile_queries(const uint32_t* __restrict__ tilePre, uint64_t nTiles, const uint32_t* __restrict__ qStart,
@@ -2404,6 +2407,19 @@ __global__ void __launch_bounds__(512) k_sweep_ws(const uint64_t* __restrict__ t
                 recs += n;
                 auto run = [&](const auto& vals, const auto& taxs) {
                     for (uint64_t q = d.q0 + lt; q < d.q1; q += 256) {
+                        if (g_abSweepCount) {  // A/B only: the sweep's LDS work alone (no emission: invalid results)
+                            const uint64_t key = qkey[q], aa = key & kAAMask, aa2 = aa + (1ull << 24);
+                            uint32_t p1 = 0, p2 = 0;
+                            for (uint32_t step = pow2; step > 0; step >>= 1) {
+                                const uint32_t i1 = p1 + step, i2 = p2 + step;
+                                if (i1 <= n && vals[i1 - 1] < aa) p1 = i1;
+                                if (i2 <= n && vals[i2 - 1] < aa2) p2 = i2;
+                            }
+                            uint64_t hi = p2;
+                            uint32_t thr = 0;
+                            hits += run_select(hamming_rows(key), vals, d.r0, (uint64_t)p1, hi, D, thr) != 0;
+                            continue;
+                        }
                         const uint32_t slot = qslot[q];
                         uint32_t p;
                         const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot, C, p)];
