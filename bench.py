@@ -237,14 +237,17 @@ def main():
     ap.add_argument("--gtdb-kmers", type=float, default=12e9,
                     help="config 3: k-mers of the GTDB-scale DB (0 = skip config 3; config 2 is then the headline)")
     ap.add_argument("--gtdb-pairs", type=int, default=10_000_000, help="config 3: read pairs per rank per step")
-    ap.add_argument("--gtdb-batch", type=int, default=2_000_000,
-                    help="config 3 (and config 5): read pairs per mtb_classify_batch (the QuerySplit; 2M fits "
-                         "beside the 170 GB of DB arrays, profiles/r03/batch_sweep.json)")
+    ap.add_argument("--gtdb-batch", type=int, default=3_333_334,
+                    help="config 3 (and config 5): read pairs per mtb_classify_batch (the QuerySplit: three per "
+                         "10M-pair step, 88 GB of workspace beside the 171 GB of DB arrays since K6's scratch lives "
+                         "in dead buffers; 2M: 22.99M, 3M: 23.16M, 3.33M: 24.06M, 4M: 23.72M reads/s, "
+                         "profiles/r04/batch_sweep.json)")
     ap.add_argument("--gtdb-contexts", type=int, default=1,
                     help="experiments: config-3 batches spread over this many contexts on the GPU (mtb_clone), "
                          "each driven by a thread of its own (two batches in flight)")
-    ap.add_argument("--variant-batch", type=int, default=1_000_000,
-                    help="config-3 DB variants and --em: read pairs per mtb_classify_batch")
+    ap.add_argument("--variant-batch", type=int, default=2_000_000,
+                    help="config-3 DB variants and --em: read pairs per mtb_classify_batch (related: 16.01M at 1M, "
+                         "16.63M at 2M reads/s; 2M ran out of HBM before round 4)")
     ap.add_argument("--gtdb-species", type=int, default=129_671)
     ap.add_argument("--gtdb-true-species", type=int, default=1000)
     ap.add_argument("--gtdb-genome", type=int, default=3_000_000)

@@ -801,7 +801,7 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
     // beside a GTDB-scale DB), reached through a ramp of kRamp batches from 1/32 of it
     const uint32_t maxReads = opt->max_reads ? opt->max_reads : 4000000u;
     uint64_t maxBases = opt->max_bases;
-    if (!maxBases) {  // ~140 device bytes of workspace per base at GTDB scale; slots < 2^31
+    if (!maxBases) {  // ~90 device bytes of workspace per base at GTDB scale; slots < 2^31
         // per device: its free HBM plus what its contexts' grow-only workspaces already hold (their
         // next batches reuse it), shared by those contexts; 3/4 of a share for a context's batch
         std::map<int, std::pair<uint64_t, int>> avail;  // device -> (bytes, contexts)
@@ -820,7 +820,7 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
         }
         maxBases = 1ull << 30;
         for (auto& kv : avail)
-            maxBases = std::min<uint64_t>(maxBases, (uint64_t)(0.75 * (double)kv.second.first / kv.second.second / 140.0));
+            maxBases = std::min<uint64_t>(maxBases, (uint64_t)(0.75 * (double)kv.second.first / kv.second.second / 95.0));
         maxBases = std::max<uint64_t>(maxBases, 1ull << 20);
         // a context holding more than its share (e.g. grown by larger batches before) gives it back
         for (int d = 0; d < nCtx; d++) {
