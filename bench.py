@@ -1122,7 +1122,8 @@ def run_config5(args, world, rank, local, dev):
         if b - a not in offs:
             offs[b - a] = o1[:b - a + 1].contiguous()
     # parity sample: the first S/P reads of every owner's range of batch 0
-    own0 = owner_bounds(spans[0][1] - spans[0][0], P)
+    obs = [owner_bounds(b - a, P) for a, b in spans]  # each batch's owner ranges (the last batch may be shorter)
+    own0 = obs[0]
     per_owner = max(1, min(args.c5_sample // P, min(hi - lo for lo, hi in own0)))
     samp = np.concatenate([np.arange(lo, lo + per_owner) for lo, _ in own0])
     sub = None
@@ -1147,17 +1148,16 @@ def run_config5(args, world, rank, local, dev):
         part = rc.build(c0, c1, guard=True)
         rc.free_true()
         clf = Classifier(lp, db_resident=part, device=local, db_part=(rank, P))
-        ob = owner_bounds(B, P)
-        n_own = ob[rank][1] - ob[rank][0]
-        res = torch.empty((n_own * len(spans), RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-        c1g = ResultGather(dev, n_own * len(spans))
+        own = np.cumsum([0] + [o[rank][1] - o[rank][0] for o in obs])  # the last span may be shorter
+        res = torch.empty((int(own[-1]), RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        c1g = ResultGather(dev, int(own[-1]))
 
         def step():
             c1g.reset()
             for k, (a, b) in enumerate(spans):
                 o = offs[b - a]
                 classify_partitioned(clf, s1[a * L:b * L], o, s2[a * L:b * L], o, device_input=True, on_device=True)
-                c1g.add(clf, res[k * n_own:(k + 1) * n_own])
+                c1g.add(clf, res[int(own[k]):int(own[k + 1])])
             c1g.gather(res)
 
         for _ in range(max(1, args.warmup)):
@@ -1234,7 +1234,6 @@ def run_config5(args, world, rank, local, dev):
         else:
             keep_clf, keep_part = clf, part  # the owners' K5 + K6 run in this context
     rc.free_true()
-    ob = owner_bounds(B, P)
     assign_ms = np.zeros((P, len(spans)))
     a2a_ms = np.zeros((P, len(spans)))
     a2a_bytes = np.zeros(P)
@@ -1244,10 +1243,10 @@ def run_config5(args, world, rank, local, dev):
             c = store[p][k][1].to(torch.int64)
             cs = torch.zeros(c.numel() + 1, dtype=torch.int64, device=dev)
             torch.cumsum(c, 0, out=cs[1:])
-            csum[p, k] = cs[[lo for lo, _ in ob] + [ob[-1][1]]].cpu().tolist()
+            csum[p, k] = cs[[lo for lo, _ in obs[k]] + [obs[k][-1][1]]].cpu().tolist()
 
     def recv(r, k):
-        lo, hi = ob[r]
+        lo, hi = obs[k][r]
         ms = [store[p][k][0][csum[p, k][r]:csum[p, k][r + 1]] for p in range(P)]
         m = torch.cat([x.to(dev, non_blocking=True) for x in ms])
         cnt = torch.cat([store[p][k][1][lo:hi] for p in range(P)])
@@ -1257,6 +1256,7 @@ def run_config5(args, world, rank, local, dev):
         for k in range(len(spans)):
             # the all-to-all (not measurable on one GPU): rank r sends each peer q the matches of q's
             # reads against part r and receives q's part's matches of its own reads; one link per peer
+            ob = obs[k]
             sends = [(csum[r, k][q + 1] - csum[r, k][q]) * 24 + 4 * (ob[q][1] - ob[q][0]) for q in range(P) if q != r]
             recvs = [(csum[q, k][r + 1] - csum[q, k][r]) * 24 + 4 * (ob[r][1] - ob[r][0]) for q in range(P) if q != r]
             a2a_bytes[r] += sum(sends)
@@ -1276,7 +1276,7 @@ def run_config5(args, world, rank, local, dev):
         rs, ts = [], []
         for r in range(P):
             m, cnt, ql = recv(r, 0)
-            br = keep_clf.assign_chunks(m, m.shape[0], cnt, P, ql, ob[r][1] - ob[r][0])
+            br = keep_clf.assign_chunks(m, m.shape[0], cnt, P, ql, obs[0][r][1] - obs[0][r][0])
             res_r = br.results[:per_owner].copy()
             tc_r = [br.taxcnt[int(x["taxcnt_offset"]):int(x["taxcnt_offset"]) + int(x["taxcnt_len"])] for x in res_r]
             rs.append(res_r)
