@@ -2,7 +2,7 @@
 # Round-4 measurement: per workload, a rocprofv3 kernel trace and separate FETCH_SIZE / WRITE_SIZE
 # passes (each its own run; no tracing domains with --pmc) of one timed batch after one warm-up
 # batch; summarised into profiles-ready JSON by tools/traffic_json.py.
-#   gtdb     config 3: one 2M-pair batch (the bench's QuerySplit) vs the 12G-k-mer GTDB-scale DB
+#   gtdb     config 3: one GTDB_BATCH-pair batch (the bench's QuerySplit, 3333334) vs the 12G-k-mer GTDB-scale DB
 #   long     config 4: one 62.5k-read batch of ONT-like reads vs the same DB
 #   related  config 3's "related" DB variant
 #   syncmer  config 3's syncmer DB variant
@@ -11,21 +11,22 @@
 # Usage: tools/measure_r04.sh [workload ...]   (default: all). Output: gpurun_out/r04/prof/<workload>/
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04/prof
+O=gpurun_out/r04/prof${TAG:+_$TAG}  # TAG: a variant run (e.g. TAG=sweep MTB_JOIN=sweep) in its own directory
 mkdir -p $O
 Q="--cpu-sample 0 --e2e-pairs 0 --e2e-gzip-pairs 0 --em-pairs 0 --c5-kmers 0"
 declare -A CMD STEP BATCH
-GB=${GTDB_BATCH:-2000000}  # the headline's QuerySplit (the join follows MTB_JOIN / MTB_FILTER of the environment)
+GB=${GTDB_BATCH:-3333334}  # the headline's QuerySplit (the join follows MTB_JOIN / MTB_FILTER of the environment)
+VB=2000000  # the variants' QuerySplit (bench.py --variant-batch)
 CMD[gtdb]="bench.py --skip-config2 --steps 1 --warmup 1 --long-reads 0 --variants= --gtdb-pairs $GB --gtdb-batch $GB --cold-pairs 0 $Q"
 STEP[gtdb]=1; BATCH[gtdb]=$GB
 CMD[long]="bench.py --skip-config2 --steps 1 --warmup 0 --gtdb-pairs 2000 --gtdb-batch 1000 --variants= --long-reads 62500 --long-batch 62500 --cold-pairs 0 $Q"
 STEP[long]=3; BATCH[long]=62500
-CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
-STEP[related]=1; BATCH[related]=1000000
-CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
-STEP[syncmer]=1; BATCH[syncmer]=1000000
-CMD[conserved]="bench.py --variant-only conserved --steps 1 --warmup 1 --gtdb-pairs 1000000 $Q"
-STEP[conserved]=1; BATCH[conserved]=1000000
+CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
+STEP[related]=1; BATCH[related]=$VB
+CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
+STEP[syncmer]=1; BATCH[syncmer]=$VB
+CMD[conserved]="bench.py --variant-only conserved --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
+STEP[conserved]=1; BATCH[conserved]=$VB
 CMD[config2]="bench.py --gtdb-kmers 0 --steps 1 --warmup 1 --long-reads 0 --cold-pairs 0 $Q"
 STEP[config2]=1; BATCH[config2]=1000000
 W="${@:-gtdb long related syncmer conserved config2}"
