@@ -128,7 +128,7 @@ struct mtb_ctx {
     uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
     uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
     bool sweepSmall = false;     // MTB_SWEEP_SMALL=1 (A/B): 24-KB LDS tiles (2048 records), nominal 1024
-    int sweepPersist = 2;        // MTB_SWEEP_PERSIST: 2 warp-specialised (default), 1 persistent, 0 a block per tile
+    int sweepPersist = 1;        // MTB_SWEEP_PERSIST: 1 persistent (default: profiles/r04/join_ab.json), 2 warp-specialised, 0 a block per tile
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)

@@ -44,7 +44,8 @@ def stage_of(seq):
             stage, after_extract = "extract", True
         elif k.startswith("k_filter"):
             stage = "filter"
-        elif k.startswith("k_match_windows") or k.startswith("k_match<") or k == "k_match":
+        elif (k.startswith(("k_match_windows", "k_prefix_firsts", "k_suffix_min", "k_tile_queries", "k_sweep"))
+              or k.startswith("k_match<") or k == "k_match"):  # K4 or K4S (the sweep's query starts + sweep)
             stage = "match_join"
         elif k == "k_probe" or k.startswith("k_probe<"):
             stage = "probe_join"
