@@ -132,7 +132,7 @@ struct mtb_ctx {
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
     bool directRetry = false;    // MTB_DIRECT=2: every direct join is treated as overflowed (tests)
-    int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune)
+    int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune, 4 as 2 with the bitonic large sort)
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
@@ -391,7 +391,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_BIG_GROUPS")) c->bigGroups = atoi(e) != 0;
     if (const char* e = getenv("MTB_FUSE_FILTER")) c->fuseFilter = atoi(e) != 0;
     if (const char* e = getenv("MTB_PRESENT_SHARE")) c->presentShare = std::max(1e-6, atof(e));  // tests: filter reruns
-    if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : atoi(e) == 0 ? 0 : 2;
+    if (const char* e = getenv("MTB_PRUNE_AFTER")) c->pruneAfter = atoi(e) == 1 ? 1 : atoi(e) == 0 ? 0 : atoi(e) == 4 ? 4 : 2;
     if (const char* e = getenv("MTB_EMULATE_SORT")) c->emulateAll = atoi(e) != 0;
     if (const char* e = getenv("MTB_K6_ALIAS")) c->noAlias = atoi(e) == 0;
     if (c->forceGeneric) c->matchWinCap = 0;

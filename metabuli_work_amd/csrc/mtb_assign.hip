@@ -880,37 +880,56 @@ __device__ __forceinline__ void segsort_mid_run(const In& in, MidLds& L, mtb_mat
     for (long i = threadIdx.x; i < n; i += kMidThreads) out[base + i] = in.full(si[i]);
 }
 
+template <int kThreads, int kSeg, typename In>
+__device__ bool segsort_compact(const In& in, long n, uint64_t* K, uint64_t* Lo, uint16_t* orig, uint32_t* sWave,
+                                mtb_match* __restrict__ out, uint64_t base, uint32_t* __restrict__ liveCnt, uint32_t r,
+                                uint32_t pm, bool bitonic);
+
 // seg (nullable): the direct join's sparse per-read stretches (seg + inOff[r] * inC), as
 // k_segsort_small reads them, so that batches of <= kMidSeg matches per read need no compaction.
+// compact (pruning only): 1 the compact-key sort (segsort_compact), 2 the same on the bitonic network.
 __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __restrict__ in,
                                                              const uint64_t* __restrict__ mOff, uint32_t nReads,
                                                              mtb_match* __restrict__ out, uint32_t* __restrict__ liveCnt,
                                                              long mergeSeg, uint32_t pm,
                                                              const uint32_t* __restrict__ segLen,
                                                              const SegMatch* __restrict__ seg,
-                                                             const uint64_t* __restrict__ inOff, uint32_t inC) {
+                                                             const uint64_t* __restrict__ inOff, uint32_t inC,
+                                                             int compact) {
     __shared__ MidLds L;
     const uint32_t r = blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const long n = seg_len(mOff, segLen, r);
     if (n <= kSmallSeg || n > kMidSeg || n > mergeSeg) return;  // larger: k_segsort_large / merge path
-    if (sparse_read(seg, inOff, inC, r, n)) segsort_mid_run(sparse_in(seg, inOff, inC, r), L, out, base, n, liveCnt, r, pm);
-    else segsort_mid_run(MatchIn{in, base}, L, out, base, n, liveCnt, r, pm);
+    if (sparse_read(seg, inOff, inC, r, n)) {
+        const auto sin = sparse_in(seg, inOff, inC, r);
+        if (liveCnt && compact &&
+            segsort_compact<kMidThreads, kMidSeg>(sin, n, L.sh, L.sl, L.si, L.sWave, out, base, liveCnt, r, pm, compact == 2))
+            return;
+        segsort_mid_run(sin, L, out, base, n, liveCnt, r, pm);
+    } else {
+        if (liveCnt && compact &&
+            segsort_compact<kMidThreads, kMidSeg>(MatchIn{in, base}, n, L.sh, L.sl, L.si, L.sWave, out, base, liveCnt, r,
+                                                  pm, compact == 2))
+            return;
+        segsort_mid_run(MatchIn{in, base}, L, out, base, n, liveCnt, r, pm);
+    }
 }
 
-// The large pruned sort on compact keys (segments of 2049..8192 matches: long reads), as the register
-// sorts do (prune_rank_sort): species:24 | frame:3 | pos:24 | slot:13 in one 64-bit key, the slot
-// naming the element's record (its lo key and original index) in LDS, so the 1024-thread network
-// moves 8 B per element instead of a 128-bit key and an index. Elements tied on (species, frame, pos)
+// The LDS pruned sorts on compact keys (segments of 513..2048 matches on 256 threads, 2049..8192 on
+// 1024: long reads), as the register sorts do (prune_rank_sort): species:24 | frame:3 | pos:24 | slot:13
+// in one 64-bit key, the slot naming the element's record (its lo key and original index) in LDS, so
+// the sort moves 8 B per element instead of a 128-bit key and an index. Elements tied on (species, frame, pos)
 // are placed inside their tie by the lo key (hamming, dna, target), the rest of compareMatches'
 // order. Segments with a species or a position of 2^24 or more take the full-key sort (returns false).
 constexpr int kCSp = 40, kCSpf = 37, kCPos = 13;
 
+template <int kThreads>
 __device__ __forceinline__ void block_bitonic_u64(uint64_t* K, long p2) {
     for (long k = 2; k <= p2; k <<= 1)
         for (long j = k >> 1; j > 0; j >>= 1) {
-            for (long t = threadIdx.x; t < (p2 >> 1); t += kLargeThreads) {
+            for (long t = threadIdx.x; t < (p2 >> 1); t += kThreads) {
                 const long i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
                 const long ixj = i + j;
                 const bool up = (i & k) == 0;
@@ -924,12 +943,99 @@ __device__ __forceinline__ void block_bitonic_u64(uint64_t* K, long p2) {
         }
 }
 
-template <typename In>
-__device__ bool segsort_large_compact(const In& in, long n, uint64_t* K, uint64_t* Lo, uint16_t* orig,
-                                      uint32_t* sWave, mtb_match* __restrict__ out, uint64_t base,
-                                      uint32_t* __restrict__ liveCnt, uint32_t r, uint32_t pm) {
-    constexpr int kPer = kBlockSeg / kLargeThreads;  // 8
-    constexpr uint32_t logT = 14, T = 1u << logT;    // pair / species hashes: 64 KB each, in K and Lo
+// One wave's register bitonic sort of 64E keys (element e = 64 * slot + lane), as wave_bitonic_sort
+// on a single 64-bit key.
+template <int E>
+__device__ __forceinline__ void wave_sort_u64(uint64_t (&k)[E], int lane) {
+    auto stage = [&](auto kc, auto jc) {
+        constexpr int kk = decltype(kc)::value, j = decltype(jc)::value;
+        if constexpr (j >= 64) {
+            constexpr int js = j >> 6;
+#pragma unroll
+            for (int sl = 0; sl < E; sl++) {
+                if (sl & js) continue;
+                const int s2 = sl | js;
+                const bool up = ((64 * sl + lane) & kk) == 0;
+                const uint64_t a = k[sl], b = k[s2];
+                if ((a > b) == up) {
+                    k[sl] = b;
+                    k[s2] = a;
+                }
+            }
+        } else {
+            const bool lower = (lane & j) == 0;
+#pragma unroll
+            for (int sl = 0; sl < E; sl++) {
+                const bool up = ((64 * sl + lane) & kk) == 0;
+                const uint64_t p = xor_lane64c<j>(k[sl], lane);
+                if ((k[sl] > p) == (lower == up)) k[sl] = p;
+            }
+        }
+    };
+    bitonic_stages<2, 1, E>(stage);
+}
+
+// Sorts K[0, p2) ascending (p2 a power of two <= kSeg; every thread of the kThreads-thread block).
+// From max(kThreads, 512) keys on: runs of 512 sort in registers, a wave each (DPP / permlane moves,
+// no barriers), then log2(p2 / 512) merge rounds in place — each thread finds the merge-path split of
+// its p2 / kThreads outputs, merges them into registers and writes them back after a barrier —
+// instead of the bitonic network's up to ~90 barrier-separated LDS stages. Keys are distinct but for
+// the ~0 padding.
+template <int kThreads, int kSeg>
+__device__ void block_sort_u64(uint64_t* K, long p2) {
+    constexpr int E = 8, kRun = 64 * E, kOut = kSeg / kThreads;
+    static_assert(kSeg <= kRun * (kThreads / 64) && kOut <= 8, "a run per wave, <= 8 outputs per thread");
+    if (p2 < kThreads || p2 < kRun) {
+        block_bitonic_u64<kThreads>(K, p2);
+        return;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if ((long)w * kRun < p2) {
+        uint64_t k[E];
+#pragma unroll
+        for (int sl = 0; sl < E; sl++) k[sl] = K[w * kRun + 64 * sl + lane];
+        wave_sort_u64<E>(k, lane);
+#pragma unroll
+        for (int sl = 0; sl < E; sl++) K[w * kRun + 64 * sl + lane] = k[sl];
+    }
+    __syncthreads();
+    const int per = (int)(p2 / kThreads);  // outputs per thread: 1..kOut
+    for (long run = kRun; run < p2; run <<= 1) {
+        const long d0 = (long)threadIdx.x * per, ps = d0 & ~(2 * run - 1), d = d0 - ps;
+        const uint64_t* A = K + ps;
+        const uint64_t* B = A + run;
+        long lo = max(0l, d - run), hi = min(d, run);
+        while (lo < hi) {  // the first d outputs take i keys of A and d - i of B
+            const long i = (lo + hi) >> 1;
+            if (B[d - i - 1] > A[i]) lo = i + 1;
+            else hi = i;
+        }
+        long i = lo, j = d - lo;
+        uint64_t o[kOut];
+#pragma unroll
+        for (int t = 0; t < kOut; t++) {
+            if (t >= per) break;
+            const uint64_t a = i < run ? A[i] : ~0ull, b = j < run ? B[j] : ~0ull;
+            const bool takeA = j >= run || (i < run && a <= b);
+            o[t] = takeA ? a : b;
+            i += takeA;
+            j += !takeA;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < kOut; t++)
+            if (t < per) K[d0 + t] = o[t];
+        __syncthreads();
+    }
+}
+
+template <int kThreads, int kSeg, typename In>
+__device__ bool segsort_compact(const In& in, long n, uint64_t* K, uint64_t* Lo, uint16_t* orig, uint32_t* sWave,
+                                mtb_match* __restrict__ out, uint64_t base, uint32_t* __restrict__ liveCnt, uint32_t r,
+                                uint32_t pm, bool bitonic) {
+    constexpr int kPer = kSeg / kThreads;  // 8
+    static_assert(kPer == 8 && (kSeg == 2048 || kSeg == 8192) && kSeg <= (1 << kCPos), "compact geometry");
+    constexpr uint32_t logT = kSeg == 8192 ? 14 : 12, T = 1u << logT;  // pair / species hashes in K and Lo (2 kSeg words)
     uint32_t* cnt = reinterpret_cast<uint32_t*>(K);
     uint32_t* flag = reinterpret_cast<uint32_t*>(Lo);
     const long b = (long)threadIdx.x * kPer;
@@ -948,7 +1054,7 @@ __device__ bool segsort_large_compact(const In& in, long n, uint64_t* K, uint64_
         }
     }
     if (__syncthreads_or(bad)) return false;
-    for (uint32_t i = threadIdx.x; i < T; i += kLargeThreads) {
+    for (uint32_t i = threadIdx.x; i < T; i += kThreads) {
         cnt[i] = 0;
         flag[i] = 0;
     }
@@ -966,7 +1072,7 @@ __device__ bool segsort_large_compact(const In& in, long n, uint64_t* K, uint64_
     for (int k = 0; k < kPer; k++)
         if (b + k < n && flag[hs[k]]) mask |= 1u << k;
     uint32_t m;
-    uint32_t at = block_scan_u32<kLargeThreads>((uint32_t)__popc(mask), &m, sWave);  // syncs: the tables are free
+    uint32_t at = block_scan_u32<kThreads>((uint32_t)__popc(mask), &m, sWave);  // syncs: the tables are free
     if (m == 0) {
         if (threadIdx.x == 0) liveCnt[r] = 0;
         return true;
@@ -981,33 +1087,34 @@ __device__ bool segsort_large_compact(const In& in, long n, uint64_t* K, uint64_
         }
     long p2 = 2;
     while (p2 < (long)m) p2 <<= 1;
-    for (long i = (long)m + threadIdx.x; i < p2; i += kLargeThreads) K[i] = ~0ull;
+    for (long i = (long)m + threadIdx.x; i < p2; i += kThreads) K[i] = ~0ull;
     __syncthreads();
-    block_bitonic_u64(K, p2);
+    if (bitonic) block_bitonic_u64<kThreads>(K, p2);  // A/B: the plain LDS network
+    else block_sort_u64<kThreads, kSeg>(K, p2);
     // places inside (species, frame, pos) ties, then the original index at each place
     uint16_t pos[kPer], idx[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
-        const long e = threadIdx.x + (long)j * kLargeThreads;
+        const long e = threadIdx.x + (long)j * kThreads;
         pos[j] = idx[j] = 0;
         if (e < (long)m) {
-            const uint64_t k = K[e], pre = k >> kCPos, lo = Lo[k & (kBlockSeg - 1)];
+            const uint64_t k = K[e], pre = k >> kCPos, lo = Lo[k & (kSeg - 1)];
             long a = e;
-            for (long q = e - 1; q >= 0 && (K[q] >> kCPos) == pre; q--) a -= Lo[K[q] & (kBlockSeg - 1)] > lo;
-            for (long q = e + 1; q < (long)m && (K[q] >> kCPos) == pre; q++) a += Lo[K[q] & (kBlockSeg - 1)] < lo;
+            for (long q = e - 1; q >= 0 && (K[q] >> kCPos) == pre; q--) a -= Lo[K[q] & (kSeg - 1)] > lo;
+            for (long q = e + 1; q < (long)m && (K[q] >> kCPos) == pre; q++) a += Lo[K[q] & (kSeg - 1)] < lo;
             pos[j] = (uint16_t)a;
-            idx[j] = orig[k & (kBlockSeg - 1)];
+            idx[j] = orig[k & (kSeg - 1)];
         }
     }
     __syncthreads();  // the lo keys are dead: their LDS takes the placed indices, run ids and flags
     uint16_t* placed = reinterpret_cast<uint16_t*>(Lo);
 #pragma unroll
     for (int j = 0; j < kPer; j++)
-        if (threadIdx.x + (long)j * kLargeThreads < (long)m) placed[pos[j]] = idx[j];
+        if (threadIdx.x + (long)j * kThreads < (long)m) placed[pos[j]] = idx[j];
     __syncthreads();
-    uint32_t* rid = reinterpret_cast<uint32_t*>(placed + kBlockSeg);
-    const uint32_t kept = prune_pack_block<kLargeThreads, uint16_t, In, kCSp, kCSpf>(
-        K, placed, rid, reinterpret_cast<uint8_t*>(rid + kBlockSeg), (long)m, in, out, base, sWave, pm);
+    uint32_t* rid = reinterpret_cast<uint32_t*>(placed + kSeg);
+    const uint32_t kept = prune_pack_block<kThreads, uint16_t, In, kCSp, kCSpf>(
+        K, placed, rid, reinterpret_cast<uint8_t*>(rid + kSeg), (long)m, in, out, base, sWave, pm);
     if (threadIdx.x == 0) liveCnt[r] = kept;
     return true;
 }
@@ -1032,7 +1139,8 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     while (p2 < n) p2 <<= 1;
     if (!global && n > mergeSeg) return;  // chunked LDS sorts + merge path (launch_segsort)
     if (!global && liveCnt && compact &&
-        segsort_large_compact(MatchIn{in, base}, n, sh, sl, si, sWave, out, base, liveCnt, r, pm))
+        segsort_compact<kLargeThreads, kBlockSeg>(MatchIn{in, base}, n, sh, sl, si, sWave, out, base, liveCnt, r, pm,
+                                                  compact == 2))
         return;
     if (!global) {
         long m = n;  // elements sorted: the pre-pruned live ones (prune), or all
@@ -1378,7 +1486,8 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
                                const uint32_t* segLen, hipStream_t s, const SegMatch* seg, const uint64_t* inOff,
                                uint32_t inC, int mode) {
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
-    // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts
+    // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts (4: as 2, with
+    // the compact large sort on the plain bitonic network)
 #define MTB_REGS(E, M) k_segsort_regs<E, M><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen)
     if (!liveCnt) mode = 3;  // no pruning: the full-key sort
     if (maxSeg > 128) {
@@ -1395,10 +1504,11 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
     }
 #undef MTB_REGS
     if (maxSeg > kSmallSeg)
-        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC);
+        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC,
+                                                     mode == 2 ? 1 : mode == 4 ? 2 : 0);
     if (maxSeg > kMidSeg)
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
-                                                         segLen, mode == 2 ? 1 : 0);
+                                                         segLen, mode == 2 ? 1 : mode == 4 ? 2 : 0);
     MTB_HIP_RET(hipGetLastError());
     if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, segLen, s);
     return hipSuccess;
@@ -1600,7 +1710,7 @@ struct LdsRecs {
 template <typename R>
 __device__ __forceinline__ bool match_paths_regs(const R& M, uint64_t start, uint64_t end,
                                                  const AssignCfg& cfg, int minDepth, bool fwd,
-                                                 Path* __restrict__ P, uint64_t& nPout) {
+                                                 Path* __restrict__ P, uint64_t& nPout, bool emitLone = false) {
     Path cp[kRegPos], np[kRegPos];
     uint32_t cd[kRegPos], nd[kRegPos], nr[kRegPos];
     bool cc[kRegPos];
@@ -1628,6 +1738,7 @@ __device__ __forceinline__ bool match_paths_regs(const R& M, uint64_t start, uin
         nc++;
         k++;
     }
+    const bool stepped = k < end;  // a next position group follows (emitLone: see match_paths_serial)
     while (k < end) {
         const uint32_t nextPos = M.pos(k);
         nn = 0;
@@ -1701,6 +1812,10 @@ __device__ __forceinline__ bool match_paths_regs(const R& M, uint64_t start, uin
         nc = nn;
         currPos = nextPos;
     }
+    if (!stepped && emitLone)
+#pragma unroll
+        for (int y = 0; y < kRegPos; y++)
+            if (y < nc && cp[y].depth >= minDepth) P[nP++] = cp[y];
     nPout = nP;
     return true;
 }
@@ -1890,7 +2005,11 @@ __global__ void __launch_bounds__(64) k_match_paths_wave(const mtb_match* __rest
     if (lane == 63) b = end;
     if (b < a) b = a;
     uint64_t cnt = 0;
-    if (a < b) cnt = match_paths_serial(GlobalRecs{M}, a, b, cfg, minDepth, fwd, L, P, conn, multi) - a;
+    if (a < b) {  // the register DP when no position of the stretch holds more than kRegPos matches
+        uint64_t nPr = a;
+        if (!cfg.generic && match_paths_regs(GlobalRecs{M}, a, b, cfg, minDepth, fwd, P, nPr, multi)) cnt = nPr - a;
+        else cnt = match_paths_serial(GlobalRecs{M}, a, b, cfg, minDepth, fwd, L, P, conn, multi) - a;
+    }
     // exclusive scan of the counts over the lanes
     uint64_t inc = cnt;
 #pragma unroll

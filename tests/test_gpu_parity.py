@@ -38,10 +38,12 @@ def _reads(gen, kind, n, seed):
                                 rate_lower=0.002)
     if kind == "single":
         return synth.make_reads(gen, n, paired=False, seed=seed, short_frac=0.03, rate_n=0.002)
+    if kind == "longbig":  # segments past 2048 matches: thinning + the compact 2049-8192-match sorts
+        return synth.make_long_reads(gen, n, n50=12000, min_len=4000, seed=seed)
     return synth.make_long_reads(gen, n, n50=3000, min_len=400, seed=seed)
 
 
-SEQ_MODE = {"paired": 2, "single": 1, "long": 3}
+SEQ_MODE = {"paired": 2, "single": 1, "long": 3, "longbig": 3}
 
 
 def compare_results(gres, gtc, ores, otc):
@@ -218,7 +220,9 @@ def test_filter_output_rerun(make_db, db_name, kind, monkeypatch):
     ("fmt2", "paired", "0", "after1"), ("fmt2", "long", "0", "after1"), ("fmt2_syncmer", "long", "0", "after1"),
     ("fmt2", "long", "0", "big0"), ("fmt1", "long", "0", "big0"),
     ("fmt2", "long", "0", "0"), ("fmt2_syncmer", "long", "0", "0"),
-    ("fmt2", "long", "0", "512"), ("fmt1", "long", "0", "600"), ("fmt2_syncmer", "long", "0", "512")])
+    ("fmt2", "long", "0", "512"), ("fmt1", "long", "0", "600"), ("fmt2_syncmer", "long", "0", "512"),
+    ("fmt2", "long", "0", "after2"), ("fmt1", "longbig", "0", "after2"), ("fmt2_syncmer", "longbig", "0", "after2"),
+    ("fmt2", "longbig", "0", "after2"), ("fmt2", "longbig", "0", "after4"), ("fmt2", "paired", "0", "after2")])
 def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monkeypatch):
     """Dead-match pruning in every K5 variant, results against the oracle: long reads put segments
     in the 1024-thread LDS sort; MTB_SEGSORT_GLOBAL=1 sends every segment through the global-scratch
@@ -227,7 +231,8 @@ def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monk
     their sort (k_thin_big: lossy LDS counts of the whole segment), or, with MTB_PRUNE_COMPACT=0,
     sorted whole and pruned after the merge. The 129-512-match register sorts prune, then sort the
     live matches (default), or with MTB_PRUNE_AFTER=1 sort whole segments and prune on the sorted
-    order."""
+    order; MTB_PRUNE_AFTER=2 (the default) sorts on rank keys and runs the 2049-8192-match sorts on
+    compact keys (register runs + merge path), =4 the same on the LDS bitonic network."""
     monkeypatch.setenv("MTB_SEGSORT_GLOBAL", glob)
     monkeypatch.setenv("MTB_PRUNE_AFTER", merge[5:] if merge.startswith("after") else "0")
     monkeypatch.setenv("MTB_MERGE_SEG", "0" if merge.startswith(("after", "big")) else merge)
@@ -237,7 +242,7 @@ def test_pruned_segment_sorts(make_db, db_name, kind, glob, merge, compact, monk
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])
     odb = oc.OracleDb(db_dir)
-    reads = _reads(gen, kind, 1500 if kind != "long" else 60, 35)
+    reads = _reads(gen, kind, {"long": 60, "longbig": 40}.get(kind, 1500), 35)
     ores, otc = oc.classify(odb, par.to_c(), reads)
     with Classifier(par, db_dir=db_dir) as clf:
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
