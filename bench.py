@@ -1056,9 +1056,10 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
             if cold is not None:
                 out[mode]["first_run_reads_per_s"] = cold
                 out[mode]["first_run_note"] = (
-                    "the process's first startClassify: the headline context gives back its 2M-pair workspace, both "
-                    "contexts grow 1M-pair workspaces (hipFree waits for the device: the other context's batch) and "
-                    "the pinned slots and parse buffers are allocated; later runs reuse all of it")
+                    "the process's first startClassify after the headline: the headline context gives back its "
+                    "3.33M-pair workspace (~88 GB; the next allocation waits for the runtime's release of it), both "
+                    "contexts grow their workspaces and the pinned slots and parse buffers are allocated; later runs "
+                    "reuse all of it. A fresh context's one-shot run: cold_run")
             if check is not None:  # the file's first reads are the oracle sample's
                 out[mode]["tsv_oracle_lines"] = len(check[0])
                 out[mode]["tsv_matches_oracle"] = tsv_matches_oracle(tsv, *check)
