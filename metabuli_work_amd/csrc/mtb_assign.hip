@@ -1358,10 +1358,13 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
         k_chunk_sort<<<(unsigned)chunks.size(), kLargeThreads, 0, s>>>(in, mOff, dChunks, M, scratch, chunk, segLen);
         e = hipGetLastError();
     }
+    // every round's tiles planned at once and uploaded in one copy: the rounds then follow each other
+    // in stream order with no host round trip between them
     int b = 0;
     std::vector<uint4> tiles;
-    for (long w = chunk; e == hipSuccess && w < maxN; w *= 2) {
-        tiles.clear();
+    std::vector<size_t> roundAt;
+    for (long w = chunk; w < maxN; w *= 2) {
+        roundAt.push_back(tiles.size());
         for (uint32_t r : big) {
             const long n = nOf(r);
             for (long ps = 0; ps < n; ps += 2 * w) {
@@ -1369,14 +1372,17 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
                 for (long t = 0; t < len2; t += kMergeTile) tiles.push_back(make_uint4(r, (uint32_t)ps, (uint32_t)t, 0));
             }
         }
-        if (dTiles) hipFreeAsync(dTiles, s);
-        dTiles = nullptr;
+    }
+    roundAt.push_back(tiles.size());
+    if (e == hipSuccess && !tiles.empty()) {
         e = hipMallocAsync((void**)&dTiles, sizeof(uint4) * tiles.size(), s);
         if (e == hipSuccess) e = hipMemcpyAsync(dTiles, tiles.data(), sizeof(uint4) * tiles.size(), hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) break;
-        k_merge_tiles<<<(unsigned)tiles.size(), 256, 0, s>>>(mOff, dTiles, M, scratch, b, w, segLen);
+    }
+    long w = chunk;
+    for (size_t rr = 0; e == hipSuccess && rr + 1 < roundAt.size(); rr++, w *= 2) {
+        k_merge_tiles<<<(unsigned)(roundAt[rr + 1] - roundAt[rr]), 256, 0, s>>>(mOff, dTiles + roundAt[rr], M, scratch, b, w,
+                                                                                segLen);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host tile vector is reused
         b ^= 1;
     }
     if (e == hipSuccess) {
@@ -1384,6 +1390,7 @@ static hipError_t launch_merge_path(const mtb_match* in, const uint64_t* mOff, u
                                                                        segLen);
         e = hipGetLastError();
     }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host vectors the copies read stay alive until here
     if (dTiles) hipFreeAsync(dTiles, s);
     if (dChunks) hipFreeAsync(dChunks, s);
     if (dBig) hipFreeAsync(dBig, s);
