@@ -1449,9 +1449,28 @@ __device__ void thin_run(const In& in, bool inPlace, mtb_match* __restrict__ io,
     auto spSlot = [](const mtb_match& m) {
         return (uint32_t)(((uint64_t)m.species_id * 0xC2B2AE3D27D4EB4Full) >> (64 - kThinLog));
     };
-    for (long i = threadIdx.x; i < n; i += kLargeThreads) atomicAdd(&cnt[pairSlot(in.full((uint32_t)i))], 1u);
+    // the first kThinReg elements of each thread keep their two hash slots in registers, so the flag
+    // pass and the survivors' test read no records again (a record is re-read only if it survives)
+    constexpr int kThinReg = 16;
+    static_assert(kThinLog <= 16, "two slots per register");
+    uint32_t hs2[kThinReg];
+#pragma unroll
+    for (int t = 0; t < kThinReg; t++) {
+        const long i = threadIdx.x + (long)t * kLargeThreads;
+        hs2[t] = 0;
+        if (i < n) {
+            const mtb_match m = in.full((uint32_t)i);
+            hs2[t] = pairSlot(m) | spSlot(m) << 16;
+            atomicAdd(&cnt[hs2[t] & 0xFFFFu], 1u);
+        }
+    }
+    for (long i = threadIdx.x + (long)kThinReg * kLargeThreads; i < n; i += kLargeThreads)
+        atomicAdd(&cnt[pairSlot(in.full((uint32_t)i))], 1u);
     __syncthreads();
-    for (long i = threadIdx.x; i < n; i += kLargeThreads) {
+#pragma unroll
+    for (int t = 0; t < kThinReg; t++)
+        if (threadIdx.x + (long)t * kLargeThreads < n && cnt[hs2[t] & 0xFFFFu] >= pm) flag[hs2[t] >> 16] = 1;
+    for (long i = threadIdx.x + (long)kThinReg * kLargeThreads; i < n; i += kLargeThreads) {
         const mtb_match m = in.full((uint32_t)i);
         if (cnt[pairSlot(m)] >= pm) flag[spSlot(m)] = 1;
     }
@@ -1462,11 +1481,21 @@ __device__ void thin_run(const In& in, bool inPlace, mtb_match* __restrict__ io,
     const int lane = threadIdx.x & 63;
     for (long i0 = 0; i0 < n; i0 += kLargeThreads) {
         const long i = i0 + threadIdx.x;
+        const int t = (int)(i0 / kLargeThreads);
         mtb_match m;
         bool keep = false;
         if (i < n) {
-            m = in.full((uint32_t)i);
-            keep = flag[spSlot(m)] != 0;
+            uint32_t h = 0;
+#pragma unroll
+            for (int x = 0; x < kThinReg; x++)
+                if (x == t) h = hs2[x];
+            if (t < kThinReg) {
+                keep = flag[h >> 16] != 0;
+                if (keep) m = in.full((uint32_t)i);
+            } else {
+                m = in.full((uint32_t)i);
+                keep = flag[spSlot(m)] != 0;
+            }
         }
         const unsigned long long mk = __ballot(keep);
         uint32_t at = 0;
