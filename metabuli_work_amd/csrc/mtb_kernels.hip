@@ -1,6 +1,8 @@
 // HIP kernels of the classify hot path for CDNA4 (gfx950): K1 extract, K2 radix sort,
 // K3 diffIdx decode, K4 merge-match. K5/K6 (per-read match sort + assignment) are in
 // mtb_assign.hip. All integer/byte work, HBM-bound: no MFMA.
+#include <cstring>
+
 #include "mtb_launch.h"
 
 namespace mtb {
@@ -1594,11 +1596,14 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 }
 
 // K1 + K1F fused (the sort-merge join's default): each thread scans its unit's windows as k_extract
-// does, 16 at a time, probes the 16 keys' lines together and packs the present ones (block scan,
-// one atomic per block and group) — the window keys never go through HBM. The block's threads
-// share C, so every thread takes part in every group's scan (a unit past its windows, or a padding
-// unit, contributes sentinels). Output: qkey / qslot as k_filter's (slot = the window's K1 slot).
-template <int kPer>
+// does, 16 at a time, probes the 16 keys' lines together and packs the present ones (block-wide,
+// one counter atomic per block and group; below) — the window keys never go through HBM. The block's
+// threads share the group loop up to the block's longest unit (a unit past its windows, or a padding
+// unit, contributes sentinels). The emitted-window count goes to the counter once per wave at the
+// end: same-address atomics are what the kernel waits on when it has no probes to make (round 4:
+// a per-wave-per-group counter atomic tripled the probe-free pass, `MTB_AB_FILTER=1`). Output: qkey /
+// qslot as k_filter's (slot = the window's K1 slot).
+template <int kPer, bool kJMajor>
 __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -1611,13 +1616,23 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     __shared__ unsigned long long sOut;
-    load_extract_tables(tabs, sBase, sAA, sNum);
+    __shared__ uint32_t sMaxWin, sCnt[kPer * kWaves], sEx[kWaves][64];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const unsigned long long ltMask = (1ull << lane) - 1;
+    if (threadIdx.x == 0) sMaxWin = 0;
+    load_extract_tables(tabs, sBase, sAA, sNum);  // syncs
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
     const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
-    if (w.nWin > 0) reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
+    if (w.nWin > 0) {
+        reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
+        atomicMax(&sMaxWin, (uint32_t)w.nWin);
+    }
     WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
-    for (uint32_t g = 0; g < C; g += kPer) {
+    __syncthreads();
+    const uint32_t gEnd = min(C, sMaxWin);
+    uint32_t emitted = 0;
+    for (uint32_t g = 0; g < gEnd; g += kPer) {
         // each window's probe is issued as soon as its key is known; the words are tested after the
         // group's last key, so the 16 line reads overlap the scanning
         uint64_t k[kPer];
@@ -1635,34 +1650,76 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                 sh[j] = o & 31u;
             }
         }
-        uint32_t mask = 0, emitted = 0;
+        uint32_t mask = 0;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             mask |= (sh[j] < 32u ? (word[j] >> sh[j]) & 1u : 0u) << j;
             emitted += k[j] != kSentinel;
         }
-        unsigned long long tot;
-        const unsigned long long off =
-            block_exclusive_scan((unsigned long long)__popc(mask) | ((unsigned long long)emitted << 32), &tot) &
-            0xFFFFFFFFull;
-        if (threadIdx.x == 0) {
-            const unsigned long long present = tot & 0xFFFFFFFFull;
-            sOut = present ? atomicAdd(counter, present) : 0;
-            if (tot >> 32) atomicAdd(counter + 1, tot >> 32);
+        if constexpr (!kJMajor) {  // A/B (MTB_FILTER_PACK=thread): thread-major order, round 3's packing
+            const uint32_t pc = (uint32_t)__popc(mask);
+            const uint32_t inc = (uint32_t)wave_inclusive_scan((unsigned long long)pc);
+            if (lane == 63) sCnt[wv] = inc;
+            __syncthreads();
+            uint32_t off = inc - pc, tot = 0;
+#pragma unroll
+            for (int i = 0; i < kWaves; i++) {
+                off += i < wv ? sCnt[i] : 0u;
+                tot += sCnt[i];
+            }
+            if (threadIdx.x == 0) sOut = tot ? atomicAdd(counter, (unsigned long long)tot) : 0;
+            __syncthreads();
+            uint64_t pos = sOut + off;
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                if (!((mask >> j) & 1u)) continue;
+                if (pos < cap) {
+                    qkey[pos] = k[j];
+                    qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+                }
+                pos++;
+            }
+            continue;
         }
-        __syncthreads();
-        uint64_t pos = sOut + off;
-        __syncthreads();  // sOut is rewritten by the next group
+        // the block's present windows packed in (window j, wave, lane) order — the output needs no
+        // order: K2 sorts it and K5 puts each read's matches in compareMatches order — so every store
+        // instruction writes one contiguous stretch. Per group: a ballot per window j, each wave's 16
+        // counts to LDS, an exclusive scan of the block's 16 x kWaves counts by every wave (one entry
+        // per lane), one counter atomic, two barriers (the counts of the next group are written after
+        // this group's second barrier, by which every thread has read them; sOut after the next
+        // group's first, by which every thread has read it)
+        static_assert(kPer * kWaves <= 64, "one count per lane");
+        uint32_t myCnt = 0;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
+            const unsigned long long b = __ballot((mask >> j) & 1u);
+            if (lane == j) myCnt = (uint32_t)__popcll(b);
+        }
+        if (lane < kPer) sCnt[lane * kWaves + wv] = myCnt;
+        __syncthreads();
+        const uint32_t c = lane < kPer * kWaves ? sCnt[lane] : 0u;
+        const uint32_t inc = (uint32_t)wave_inclusive_scan((unsigned long long)c);
+        const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+        sEx[wv][lane] = inc - c;  // the wave's own copy of the offsets: read back per window below
+        if (threadIdx.x == 0) sOut = tot ? atomicAdd(counter, (unsigned long long)tot) : 0;
+        __syncthreads();
+        const uint64_t base = sOut;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const unsigned long long b = __ballot((mask >> j) & 1u);  // recomputed: no 16 live ballots
             if (!((mask >> j) & 1u)) continue;
+            const uint64_t pos = base + sEx[wv][j * kWaves + wv] + (uint32_t)__popcll(b & ltMask);
             if (pos < cap) {  // past the output's capacity: counted only (the caller grows it and reruns)
                 qkey[pos] = k[j];
                 qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
             }
-            pos++;
         }
     }
+    // the reference's "Query k-mer number" (KmerMatcher.cpp:143-152) counts every non-blank query
+    // k-mer, before any AA test: one atomic per wave
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) emitted += (uint32_t)__shfl_xor((int)emitted, d, 64);
+    if ((threadIdx.x & 63) == 0 && emitted) atomicAdd(counter + 1, (unsigned long long)emitted);
 }
 
 uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
@@ -1676,19 +1733,56 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
         const uint64_t threads = (nUnits + 63) / 64 * 64;
         // MTB_FILTER_PER (A/B): windows per probe group (16: the default; 8: fewer registers, more waves)
         static const int per = getenv("MTB_FILTER_PER") && atoi(getenv("MTB_FILTER_PER")) == 8 ? 8 : 16;
-        if (per == 8)
-            k_extract_filter<8><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-                seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
-        else
-            k_extract_filter<kFilterPer><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-                seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap);
+        // MTB_FILTER_PACK=thread (A/B): the present windows in thread-major order (round 3's packing)
+        static const bool jMajor = !(getenv("MTB_FILTER_PACK") && !strcmp(getenv("MTB_FILTER_PACK"), "thread"));
+        const unsigned blocks = (unsigned)((threads + 255) / 256);
+#define MTB_EF(P, J)                                                                                                  \
+    k_extract_filter<P, J><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,           \
+                                                  extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
+                                                  qslot, counter, rankLo, rankHi, cap)
+        if (per == 8) {
+            if (jMajor) MTB_EF(8, true);
+            else MTB_EF(8, false);
+        } else {
+            if (jMajor) MTB_EF(kFilterPer, true);
+            else MTB_EF(kFilterPer, false);
+        }
+#undef MTB_EF
     }
     unsigned long long Q[2] = {0, 0};
     hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     *emitted = Q[1];
+    // MTB_AB_FILTER=1 (diagnostics; results unaffected): after the real pass, two timed passes that
+    // write no output (cap 0) and count into a scratch word — with the probes, and with none (an empty
+    // rank range) — to split the kernel's time between the probe-line reads, the scan and the packing
+    static const bool abDiag = getenv("MTB_AB_FILTER") && atoi(getenv("MTB_AB_FILTER")) == 1;
+    if (abDiag && nUnits) {
+        const unsigned blocks = (unsigned)(((nUnits + 63) / 64 * 64 + 255) / 256);
+        unsigned long long* sc = nullptr;
+        hipEvent_t ev[3];
+        if (hipMalloc((void**)&sc, 2 * sizeof(unsigned long long)) == hipSuccess) {
+            for (auto& e : ev) hipEventCreate(&e);
+            hipMemsetAsync(sc, 0, 2 * sizeof(unsigned long long), s);
+            hipEventRecord(ev[0], s);
+            k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
+                                                                extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
+                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0);
+            hipEventRecord(ev[1], s);
+            k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
+                                                                extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
+                                                                lines, qkey, qslot, sc, 0, 0, 0);
+            hipEventRecord(ev[2], s);
+            hipStreamSynchronize(s);
+            float a = 0, b = 0;
+            hipEventElapsedTime(&a, ev[0], ev[1]);
+            hipEventElapsedTime(&b, ev[1], ev[2]);
+            fprintf(stderr, "[mtb ab filter] windows %llu present %llu: probes, no output %.3f ms; no probes %.3f ms\n",
+                    (unsigned long long)Q[1], (unsigned long long)Q[0], a, b);
+            for (auto& e : ev) hipEventDestroy(e);
+            hipFree(sc);
+        }
+    }
     return Q[0];
 }
 
