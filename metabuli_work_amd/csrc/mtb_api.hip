@@ -128,6 +128,7 @@ struct mtb_ctx {
     uint32_t sweepNom = 2048;    // MTB_SWEEP_NOM
     uint32_t sweepLdsCap = ~0u;  // MTB_SWEEP_LDS (tests): tiles over this many records search HBM
     bool sweepSmall = false;     // MTB_SWEEP_SMALL=1 (A/B): 24-KB LDS tiles (2048 records), nominal 1024
+    bool filterThreadMajor = false;  // MTB_FILTER_PACK=thread (A/B): K1F's output in round 3's thread-major order
     int sweepPersist = 1;        // MTB_SWEEP_PERSIST: 1 persistent (default: profiles/r04/join_ab.json), 2 warp-specialised, 0 a block per tile
     uint32_t matchWinCap = ~0u;  // MTB_MATCH_WINDOW (tests force the HBM-search path with 0)
     bool directJoin = true;      // MTB_DIRECT=0: the sort-merge join stages its matches (+ transpose)
@@ -407,6 +408,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_SWEEP_LDS")) c->sweepLdsCap = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("MTB_SWEEP_PERSIST")) c->sweepPersist = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("MTB_SWEEP_SMALL")) c->sweepSmall = atoi(e) != 0;
+    if (const char* e = getenv("MTB_FILTER_PACK")) c->filterThreadMajor = std::string(e) == "thread";
     // the warp-specialised sweep stages 24-KB tiles: nominal 1024 records (tiles ~ one bucket)
     if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
@@ -571,6 +573,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->sweepNom = src->sweepNom;
     c->sweepLdsCap = src->sweepLdsCap;
     c->sweepSmall = src->sweepSmall;
+    c->filterThreadMajor = src->filterThreadMajor;
     c->sweepPersist = src->sweepPersist;
     c->matchWinCap = src->matchWinCap;
     c->directJoin = src->directJoin;
@@ -922,7 +925,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                       c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
                                       c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
                                       c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
-                                      c->rankHi, &c->Qall, cap, s);
+                                      c->rankHi, &c->Qall, cap, c->filterThreadMajor, s);
             HIP_TRY(hipGetLastError());
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             if (Q <= cap) break;

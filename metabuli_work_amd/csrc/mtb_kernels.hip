@@ -1,8 +1,6 @@
 // HIP kernels of the classify hot path for CDNA4 (gfx950): K1 extract, K2 radix sort,
 // K3 diffIdx decode, K4 merge-match. K5/K6 (per-read match sort + assignment) are in
 // mtb_assign.hip. All integer/byte work, HBM-bound: no MFMA.
-#include <cstring>
-
 #include "mtb_launch.h"
 
 namespace mtb {
@@ -1727,14 +1725,13 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               uint64_t cap, hipStream_t s) {
+                               uint64_t cap, bool threadMajor, hipStream_t s) {
     hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     if (nUnits) {
         const uint64_t threads = (nUnits + 63) / 64 * 64;
         // MTB_FILTER_PER (A/B): windows per probe group (16: the default; 8: fewer registers, more waves)
         static const int per = getenv("MTB_FILTER_PER") && atoi(getenv("MTB_FILTER_PER")) == 8 ? 8 : 16;
-        // MTB_FILTER_PACK=thread (A/B): the present windows in thread-major order (round 3's packing)
-        static const bool jMajor = !(getenv("MTB_FILTER_PACK") && !strcmp(getenv("MTB_FILTER_PACK"), "thread"));
+        const bool jMajor = !threadMajor;
         const unsigned blocks = (unsigned)((threads + 255) / 256);
 #define MTB_EF(P, J)                                                                                                  \
     k_extract_filter<P, J><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,           \

@@ -166,12 +166,13 @@ void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, cons
 // K1 + K1F in one pass (sort-merge join): the present windows' keys and slots straight from the
 // reads (returns Q; *emitted = non-blank windows); unitInfo as launch_extract's. Only the first
 // `cap` present windows are written: Q > cap means the output must grow and the pass rerun.
+// threadMajor (A/B): round 3's output order (each thread's present windows together).
 uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                                const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               uint64_t cap, hipStream_t s);
+                               uint64_t cap, bool threadMajor, hipStream_t s);
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                        uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
                        uint64_t* emitted, hipStream_t s);

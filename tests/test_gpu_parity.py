@@ -189,13 +189,16 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     odb.close()
 
 
+@pytest.mark.parametrize("pack", ["", "thread"])
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2_syncmer", "long"), ("fmt1", "paired")])
-def test_filter_output_rerun(make_db, db_name, kind, monkeypatch):
+def test_filter_output_rerun(make_db, db_name, kind, pack, monkeypatch):
     """The fused K1 + K1F writes into a buffer sized from the present share of earlier batches; a
     batch whose present windows outgrow it reruns the filter into a larger one (MTB_PRESENT_SHARE
     starts the share far too small): the k-mers, matches and results stay the oracle's, and the
-    next batch fits without a rerun."""
+    next batch fits without a rerun. Both output orders: block-wide (window, wave, lane) (default)
+    and thread-major (MTB_FILTER_PACK=thread)."""
     monkeypatch.setenv("MTB_PRESENT_SHARE", "0.001")
+    monkeypatch.setenv("MTB_FILTER_PACK", pack)
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])
     opar = par.to_c()
