@@ -175,6 +175,7 @@ struct mtb_ctx {
     DevBuf chunkIn, chunkCnt, chunkSrcOff;  // mtb_assign_chunks staging
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
+    DevBuf sizeLists;                       // K5: reads of each size class above 128 matches (k_size_lists)
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
@@ -432,6 +433,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
             hipFree(pop);
             hipFree(tmp);
             HIP_TRY(hipMalloc(&c->runOff, (P + 1) * sizeof(uint16_t)));
+            HIP_TRY(hipMemsetAsync(c->runOff + P, 0, sizeof(uint16_t), s));  // the end entry is never a run's
             build_run_offsets(c->db, c->D, c->lines, c->lineP, c->runOff, s);
         }
     }
@@ -602,7 +604,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
     return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
@@ -711,6 +713,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
         HIP_TRY(c->segScratch.ensure(6 * sizeof(uint64_t) * Mc));
     const bool compact = prune && maxSeg > kSegSortRegs && !c->segsortGlobal && c->pruneCompact;
     if (compact) HIP_TRY(c->segLen.ensure(sizeof(uint32_t) * (n + 1)));  // big segments thinned before sorting
+    if (maxSeg > 128) HIP_TRY(c->sizeLists.ensure(sizeof(uint32_t) * (4 * (size_t)n + 4)));
     c->keepStages = !prune;  // mtb_get_matches: matchesSorted is complete only without pruning
     HIP_TRY(c->liveCnt.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->liveOff.ensure(sizeof(uint64_t) * (n + 1)));
@@ -733,7 +736,7 @@ static int assign_stage(mtb_ctx* c, uint32_t n, bool keep) {
                            c->sparse ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
                            c->chunkC | c->spillShift << 16,
                            compact ? c->segLen.as<uint32_t>() : nullptr,
-                           c->maxSeg.as<uint32_t>(), c->pruneAfter));
+                           c->maxSeg.as<uint32_t>(), c->pruneAfter, maxSeg > 128 ? c->sizeLists.as<uint32_t>() : nullptr));
     c->sparse = false;
     const mtb_match* kIn = c->matchesSorted.as<mtb_match>();
     const uint64_t* kOff = c->mOff.as<uint64_t>();

@@ -670,8 +670,9 @@ __global__ void __launch_bounds__(64) k_segsort_regs(const mtb_match* __restrict
                                                      const uint64_t* __restrict__ inOff, uint32_t inC,
                                                      uint32_t nReads, mtb_match* __restrict__ out,
                                                      uint32_t* __restrict__ liveCnt, uint32_t pm,
-                                                     const uint32_t* __restrict__ segLen) {
-    const uint32_t r = blockIdx.x;
+                                                     const uint32_t* __restrict__ segLen,
+                                                     const uint32_t* __restrict__ list) {
+    const uint32_t r = list ? list[blockIdx.x] : blockIdx.x;  // list: the reads of this size class
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const long nl = seg_len(mOff, segLen, r);
@@ -895,9 +896,9 @@ __global__ void __launch_bounds__(kMidThreads) k_segsort_mid(const mtb_match* __
                                                              const uint32_t* __restrict__ segLen,
                                                              const SegMatch* __restrict__ seg,
                                                              const uint64_t* __restrict__ inOff, uint32_t inC,
-                                                             int compact) {
+                                                             int compact, const uint32_t* __restrict__ list) {
     __shared__ MidLds L;
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = list ? list[blockIdx.x] : blockIdx.x;
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     const long n = seg_len(mOff, segLen, r);
@@ -1124,10 +1125,11 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
                                                                  uint64_t M, mtb_match* __restrict__ out,
                                                                  uint64_t* __restrict__ gScratch, int global,
                                                                  uint32_t* __restrict__ liveCnt, long mergeSeg, uint32_t pm,
-                                                                 const uint32_t* __restrict__ segLen, int compact) {
+                                                                 const uint32_t* __restrict__ segLen, int compact,
+                                                                 const uint32_t* __restrict__ list) {
     __shared__ uint64_t sh[kBlockSeg], sl[kBlockSeg];
     __shared__ uint16_t si[kBlockSeg];
-    const uint32_t r = blockIdx.x;  // one block per read; reads that k_segsort_small took exit
+    const uint32_t r = list ? list[blockIdx.x] : blockIdx.x;  // one block per read (of its size class)
     if (r >= nReads) return;
     const uint64_t base = mOff[r];
     long n = seg_len(mOff, segLen, r);
@@ -1196,17 +1198,30 @@ __global__ void __launch_bounds__(kLargeThreads) k_segsort_large(const mtb_match
     for (long i = threadIdx.x; i < n; i += kLargeThreads) out[base + i] = in[base + I[i]];
 }
 
-// Batch maxima: a wave reduction, then one atomic per wave (a per-thread atomicMax on one address
-// serialised a million atomics: 0.18 ms per config-3 batch).
-__device__ __forceinline__ void wave_max_to(uint32_t v, uint32_t* __restrict__ out) {
+// Batch maxima: 8 elements per thread, a wave and a block reduction, then one atomic per 256-thread
+// block (one atomicMax per wave on one address had serialised ~100k atomics: 0.59 ms per 3.33M-pair
+// batch).
+constexpr int kMaxPer = 8;
+__device__ __forceinline__ void block_max_to(uint32_t v, uint32_t* __restrict__ out) {
+    __shared__ uint32_t sM[4];
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    if ((threadIdx.x & 63) == 0 && v) atomicMax(out, v);
+    if ((threadIdx.x & 63) == 0) sM[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m = max(max(sM[0], sM[1]), max(sM[2], sM[3]));
+        if (m) atomicMax(out, m);
+    }
 }
+__device__ __forceinline__ uint64_t max_elem(uint32_t k) { return (uint64_t)blockIdx.x * (256 * kMaxPer) + k * 256 + threadIdx.x; }
+__host__ __device__ constexpr uint32_t max_blocks(uint32_t n) { return (n + 256 * kMaxPer - 1) / (256 * kMaxPer); }
 
-__global__ void k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* __restrict__ out) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    wave_max_to(i < n ? x[i] : 0u, out);
+__global__ void __launch_bounds__(256) k_max_u32(const uint32_t* __restrict__ x, uint32_t n, uint32_t* __restrict__ out) {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxPer; k++)
+        if (max_elem(k) < n) v = max(v, x[max_elem(k)]);
+    block_max_to(v, out);
 }
 
 // ---- segments over kBlockSeg matches (long reads): each kBlockSeg chunk sorts in LDS, then the
@@ -1511,41 +1526,129 @@ __device__ void thin_run(const In& in, bool inPlace, mtb_match* __restrict__ io,
     if (threadIdx.x == 0) segLen[r] = surv;
 }
 
-__global__ void k_max_seg_len(const uint32_t* __restrict__ segLen, uint32_t n, uint32_t* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    wave_max_to(i < n && segLen[i] != kSegSkip ? segLen[i] : 0u, out);
+__global__ void __launch_bounds__(256) k_max_seg_len(const uint32_t* __restrict__ segLen, uint32_t n,
+                                                     uint32_t* __restrict__ out) {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxPer; k++)
+        if (max_elem(k) < n && segLen[max_elem(k)] != kSegSkip) v = max(v, segLen[max_elem(k)]);
+    block_max_to(v, out);
+}
+
+// The reads of each size class above the small kernel's bound — (128, 256], (256, 512],
+// (512, 2048], (2048, ...) matches — as lists, so each register / LDS sort kernel launches one block
+// per read of its class instead of one per read of the batch (a read of another class exited at once
+// but held the kernel's LDS while it read its bounds: ~0.7 ms per kernel over a 3.33M-pair batch).
+// A block takes 1024 reads; one global atomic per class and block.
+constexpr int kSizeClasses = 4;
+constexpr int kSizeListReads = 1024;
+
+__global__ void __launch_bounds__(256) k_size_lists(const uint64_t* __restrict__ mOff, const uint32_t* __restrict__ segLen,
+                                                    uint32_t nReads, uint32_t maxSeg, uint32_t* __restrict__ lists,
+                                                    uint32_t* __restrict__ counts) {
+    __shared__ uint32_t sCnt[kSizeClasses], sBase[kSizeClasses];
+    if (threadIdx.x < kSizeClasses) sCnt[threadIdx.x] = 0;
+    __syncthreads();
+    constexpr int kPer = kSizeListReads / 256;
+    int cls[kPer];
+    uint32_t at[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t r = blockIdx.x * kSizeListReads + k * 256 + threadIdx.x;
+        cls[k] = -1;
+        at[k] = 0;
+        if (r < nReads) {
+            const long n = seg_len(mOff, segLen, r);  // segments over maxSeg are another pass's (thinned first)
+            cls[k] = n > (long)maxSeg ? -1 : n > kMidSeg ? 3 : n > kSmallSeg ? 2 : n > 256 ? 1 : n > 128 ? 0 : -1;
+        }
+        if (cls[k] >= 0) at[k] = atomicAdd(&sCnt[cls[k]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kSizeClasses)
+        sBase[threadIdx.x] = sCnt[threadIdx.x] ? atomicAdd(&counts[threadIdx.x], sCnt[threadIdx.x]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        if (cls[k] >= 0)
+            lists[(uint64_t)cls[k] * nReads + sBase[cls[k]] + at[k]] = blockIdx.x * kSizeListReads + k * 256 + threadIdx.x;
 }
 
 // Sort (and, with liveCnt and no segLen, prune) the segments of the given lengths.
 static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                                uint64_t* gScratch, uint32_t maxSeg, uint32_t* liveCnt, long chunk, uint32_t pm,
                                const uint32_t* segLen, hipStream_t s, const SegMatch* seg, const uint64_t* inOff,
-                               uint32_t inC, int mode) {
+                               uint32_t inC, int mode, uint32_t* lists) {
     k_segsort_small<<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen);
+    if (maxSeg <= 128) return hipGetLastError();
+    // MTB_SIZE_LISTS=0 (A/B): every bigger sort kernel over the whole batch, as before round 4
+    static const bool useLists = !(getenv("MTB_SIZE_LISTS") && atoi(getenv("MTB_SIZE_LISTS")) == 0);
+    if (!useLists || !lists) {
+#define MTB_REGS(E, M) k_segsort_regs<E, M><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen, nullptr)
+        if (!liveCnt) mode = 3;
+        if (maxSeg > 128) {
+            if (mode == 1) MTB_REGS(4, 1);
+            else if (mode == 0) MTB_REGS(4, 0);
+            else if (mode == 3) MTB_REGS(4, 3);
+            else MTB_REGS(4, 2);
+        }
+        if (maxSeg > 256) {
+            if (mode == 1) MTB_REGS(8, 1);
+            else if (mode == 0) MTB_REGS(8, 0);
+            else if (mode == 3) MTB_REGS(8, 3);
+            else MTB_REGS(8, 2);
+        }
+#undef MTB_REGS
+        if (maxSeg > kSmallSeg)
+            k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff,
+                                                         inC, mode == 2 ? 1 : mode == 4 ? 2 : 0, nullptr);
+        if (maxSeg > kMidSeg)
+            k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
+                                                             segLen, mode == 2 ? 1 : mode == 4 ? 2 : 0, nullptr);
+        MTB_HIP_RET(hipGetLastError());
+        if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, segLen, s);
+        return hipSuccess;
+    }
+    // the bigger segments' reads by size class (one host round trip for the four counts)
+    // lists: kSizeClasses * nReads + kSizeClasses words of the caller's workspace
+    uint32_t* dCnt = lists + (size_t)kSizeClasses * nReads;
+    uint32_t cnt[kSizeClasses] = {0, 0, 0, 0};
+    hipError_t e = hipMemsetAsync(dCnt, 0, sizeof(cnt), s);
+    if (e == hipSuccess) {
+        k_size_lists<<<(nReads + kSizeListReads - 1) / kSizeListReads, 256, 0, s>>>(mOff, segLen, nReads, maxSeg, lists, dCnt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, dCnt, sizeof(cnt), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint32_t* list4 = lists;
+    const uint32_t* list8 = lists + (size_t)nReads;
+    const uint32_t* listMid = lists + 2 * (size_t)nReads;
+    const uint32_t* listLarge = lists + 3 * (size_t)nReads;
     // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts (4: as 2, with
     // the compact large sort on the plain bitonic network)
-#define MTB_REGS(E, M) k_segsort_regs<E, M><<<nReads, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen)
+#define MTB_REGS(E, M, N, L) \
+    k_segsort_regs<E, M><<<N, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen, L)
     if (!liveCnt) mode = 3;  // no pruning: the full-key sort
-    if (maxSeg > 128) {
-        if (mode == 1) MTB_REGS(4, 1);
-        else if (mode == 0) MTB_REGS(4, 0);
-        else if (mode == 3) MTB_REGS(4, 3);
-        else MTB_REGS(4, 2);
+    if (e == hipSuccess && cnt[0]) {
+        if (mode == 1) MTB_REGS(4, 1, cnt[0], list4);
+        else if (mode == 0) MTB_REGS(4, 0, cnt[0], list4);
+        else if (mode == 3) MTB_REGS(4, 3, cnt[0], list4);
+        else MTB_REGS(4, 2, cnt[0], list4);
     }
-    if (maxSeg > 256) {
-        if (mode == 1) MTB_REGS(8, 1);
-        else if (mode == 0) MTB_REGS(8, 0);
-        else if (mode == 3) MTB_REGS(8, 3);
-        else MTB_REGS(8, 2);
+    if (e == hipSuccess && cnt[1]) {
+        if (mode == 1) MTB_REGS(8, 1, cnt[1], list8);
+        else if (mode == 0) MTB_REGS(8, 0, cnt[1], list8);
+        else if (mode == 3) MTB_REGS(8, 3, cnt[1], list8);
+        else MTB_REGS(8, 2, cnt[1], list8);
     }
 #undef MTB_REGS
-    if (maxSeg > kSmallSeg)
-        k_segsort_mid<<<nReads, kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC,
-                                                     mode == 2 ? 1 : mode == 4 ? 2 : 0);
-    if (maxSeg > kMidSeg)
-        k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
-                                                         segLen, mode == 2 ? 1 : mode == 4 ? 2 : 0);
-    MTB_HIP_RET(hipGetLastError());
+    if (e == hipSuccess && cnt[2])
+        k_segsort_mid<<<cnt[2], kMidThreads, 0, s>>>(in, mOff, nReads, out, liveCnt, chunk, pm, segLen, seg, inOff, inC,
+                                                     mode == 2 ? 1 : mode == 4 ? 2 : 0, listMid);
+    if (e == hipSuccess && cnt[3])
+        k_segsort_large<<<cnt[3], kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 0, liveCnt, chunk, pm,
+                                                         segLen, mode == 2 ? 1 : mode == 4 ? 2 : 0, listLarge);
+    if (e == hipSuccess) e = hipGetLastError();
+    MTB_HIP_RET(e);
     if (maxSeg > chunk) return launch_merge_path(in, mOff, nReads, M, out, gScratch, liveCnt, chunk, pm, segLen, s);
     return hipSuccess;
 }
@@ -1553,7 +1656,7 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
                           uint32_t pm, hipStream_t s, const SegMatch* seg, const uint64_t* inOff, uint32_t inC,
-                          uint32_t* segLen, uint32_t* maxTmp, int after) {
+                          uint32_t* segLen, uint32_t* maxTmp, int after, uint32_t* lists) {
     pm = max(pm, 2u);
     if (nReads == 0) return hipSuccess;
     // sparse input: the register sorts and the mid sort (segments of <= kSegSortSparse), and the
@@ -1563,27 +1666,29 @@ hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nR
     const long chunk = std::max<long>(kSmallSeg, std::min<long>(mergeSeg ? mergeSeg : kBlockSeg, kBlockSeg));
     if (global) {
         k_segsort_large<<<nReads, kLargeThreads, 0, s>>>(in, mOff, nReads, M, out, gScratch, 1, liveCnt, chunk, pm,
-                                                         nullptr, 0);
+                                                         nullptr, 0, nullptr);
         return hipGetLastError();
     }
     // segments over thinAbove matches are thinned first when pruning (most of a long read's matches
     // are dead: sorting the survivors, mostly within one 2048-entry LDS tile, beats sorting all)
     const long thinAbove = std::min<long>(chunk, kMidSeg);
     if (!liveCnt || maxSeg <= (uint32_t)thinAbove || !segLen)
-        return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC, after);
+        return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSeg, liveCnt, chunk, pm, nullptr, s, seg, inOff, inC, after,
+                            lists);
     // the others are sorted and pruned as usual; the big ones are thinned in place first
     // (k_thin_big), then sorted and pruned on their survivors
     MTB_HIP_RET(launch_sorts(in, mOff, nReads, M, out, gScratch, (uint32_t)thinAbove, liveCnt, chunk, pm, nullptr, s,
-                             seg, inOff, inC, after));
+                             seg, inOff, inC, after, lists));
     mtb_match* io = const_cast<mtb_match*>(in);  // K5's input buffer: the caller's, free to overwrite
     k_thin_big<<<nReads, kLargeThreads, 0, s>>>(io, out, mOff, nReads, thinAbove, pm, segLen, seg, inOff, inC);
     MTB_HIP_RET(hipMemsetAsync(maxTmp, 0, sizeof(uint32_t), s));
-    k_max_seg_len<<<(nReads + 255) / 256, 256, 0, s>>>(segLen, nReads, maxTmp);
+    k_max_seg_len<<<max_blocks(nReads), 256, 0, s>>>(segLen, nReads, maxTmp);
     uint32_t maxSurv = 0;
     MTB_HIP_RET(hipMemcpyAsync(&maxSurv, maxTmp, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MTB_HIP_RET(hipStreamSynchronize(s));
     if (maxSurv == 0) return hipSuccess;
-    return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSurv, liveCnt, chunk, pm, segLen, s, nullptr, nullptr, 0, after);
+    return launch_sorts(in, mOff, nReads, M, out, gScratch, maxSurv, liveCnt, chunk, pm, segLen, s, nullptr, nullptr, 0, after,
+                        lists);
 }
 
 // Live matches (front-packed in each sorted segment) into one dense array: a wave per read.
@@ -1610,19 +1715,22 @@ void launch_pack_live(const mtb_match* in, const uint64_t* mOff, const uint64_t*
     if (nReads) k_pack_live<<<(nReads + 3) / 4, 256, 0, s>>>(in, mOff, liveOff, nReads, out, err);
 }
 
-__global__ void k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    wave_max_to(i < n ? (uint32_t)min<uint64_t>(off[i + 1] - off[i], 0xFFFFFFFFull) : 0u, out);
+__global__ void __launch_bounds__(256) k_max_seg(const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ out) {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxPer; k++)
+        if (max_elem(k) < n) v = max(v, (uint32_t)min<uint64_t>(off[max_elem(k) + 1] - off[max_elem(k)], 0xFFFFFFFFull));
+    block_max_to(v, out);
 }
 
 void launch_max_seg(const uint64_t* off, uint32_t n, uint32_t* out, hipStream_t s) {
     hipMemsetAsync(out, 0, sizeof(uint32_t), s);
-    if (n) k_max_seg<<<(n + 255) / 256, 256, 0, s>>>(off, n, out);
+    if (n) k_max_seg<<<max_blocks(n), 256, 0, s>>>(off, n, out);
 }
 
 void launch_max_u32(const uint32_t* x, uint32_t n, uint32_t* out, hipStream_t s) {
     hipMemsetAsync(out, 0, sizeof(uint32_t), s);
-    if (n) k_max_u32<<<(n + 255) / 256, 256, 0, s>>>(x, n, out);
+    if (n) k_max_u32<<<max_blocks(n), 256, 0, s>>>(x, n, out);
 }
 
 struct TaxView {

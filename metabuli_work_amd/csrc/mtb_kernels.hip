@@ -1295,11 +1295,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 const uint64_t head = line_scan(pl, o, before, pc, present);
                 const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
                 if (cnt <= kRunIdxMax) {
+                    if (!present) {  // an absent rank (not filtered: MTB_FILTER=0) has no run; runOff[p] may
+                        lo[j] = hi[j] = base;  // be the next line's entry or the unset end entry
+                        continue;
+                    }
                     const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
                     const uint32_t a = runOff[p];
                     const uint32_t b = before + 1 < pc ? runOff[p + 1] : (uint32_t)cnt;
                     lo[j] = base + a;
-                    hi[j] = present ? base + b : base + a;  // an absent rank (not filtered here) has no run
+                    hi[j] = base + b;
                     continue;
                 }
             }

@@ -299,12 +299,14 @@ uint64_t clade_bytes();
 // `in` is overwritten then.
 // pruneAfter (A/B): segments of 129-512 matches are pruned (LDS hash counts), then their live
 // matches sorted (0, the default), or sorted whole, then pruned on the sorted order (1).
+// lists (4 n + 4 u32 device scratch, nullable): the reads of each size class above 128 matches, so
+// the bigger sorts launch a block per read of their class (null: over the whole batch).
 hipError_t launch_segsort(const mtb_match* in, const uint64_t* mOff, uint32_t nReads, uint64_t M, mtb_match* out,
                           uint64_t* gScratch, uint32_t maxSeg, bool global, uint32_t* liveCnt, uint32_t mergeSeg,
                           uint32_t pruneMin, hipStream_t s, const SegMatch* seg = nullptr,
                           const uint64_t* inOff = nullptr, uint32_t inC = 0 /* C | capShift << 16 */,
                           uint32_t* segLen = nullptr,
-                          uint32_t* maxTmp = nullptr, int pruneAfter = 0);
+                          uint32_t* maxTmp = nullptr, int pruneAfter = 0, uint32_t* lists = nullptr);
 // The fewest matches a (species, frame) group needs for getMatchPaths to emit a path: a path of
 // depth d chains >= 1 + ceil((d - 1) / maxCodonShift) matches (each link adds a shift of at most
 // maxCodonShift codons, Taxonomer.cpp:487-648), paths are emitted at depth >= MIN_DEPTH
