@@ -379,7 +379,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     if (const char* e = getenv("MTB_FORCE_GENERIC")) c->forceGeneric = atoi(e) != 0;
     if (const char* e = getenv("MTB_SORT_LO_FINE")) {  // experiments: the unstaged join's sort prefix
         const int v = atoi(e);
-        if (v >= 24 && v <= kQuerySortLo && (kQuerySortHi - v) % 8 == 0) c->sortLoFine = v;
+        if (v >= 24 && v <= 52 && (kQuerySortHi - v) % 8 == 0) c->sortLoFine = v;  // 44 / 52: coarser (A/B)
     }
     if (const char* e = getenv("MTB_DIRECT")) {  // 0: staged join; 2: direct, then rerun staged (tests the fallback)
         c->directJoin = atoi(e) != 0;
