@@ -77,6 +77,15 @@ class ResultGather:
         return gather_results(rec, self.pool[:self.used])
 
 
+VARIANT_BATCH = {"syncmer": 3_333_334, "conserved": 3_333_334, "related": 2_000_000, "em": 2_000_000}
+
+
+def variant_batch(args, variant):
+    """Read pairs per mtb_classify_batch of a config-3 DB variant (or the --em line): --variant-batch,
+    else the variant's own QuerySplit (VARIANT_BATCH: the largest that fits HBM beside its DB)."""
+    return args.variant_batch or VARIANT_BATCH.get(variant, 2_000_000)
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -245,9 +254,11 @@ def main():
     ap.add_argument("--gtdb-contexts", type=int, default=1,
                     help="experiments: config-3 batches spread over this many contexts on the GPU (mtb_clone), "
                          "each driven by a thread of its own (two batches in flight)")
-    ap.add_argument("--variant-batch", type=int, default=2_000_000,
-                    help="config-3 DB variants and --em: read pairs per mtb_classify_batch (related: 16.01M at 1M, "
-                         "16.63M at 2M reads/s; 2M ran out of HBM before round 4)")
+    ap.add_argument("--variant-batch", type=int, default=0,
+                    help="config-3 DB variants and --em: read pairs per mtb_classify_batch (0: per variant, "
+                         "VARIANT_BATCH — the largest that fits HBM beside the DB: related 2M (100.7 GB of "
+                         "workspace; 16.01M at 1M, 16.63M at 2M reads/s), syncmer and conserved 3.33M "
+                         "(40.86 -> 42.02M and 22.20 -> 22.75M against 2M, same box); --em 2M)")
     ap.add_argument("--gtdb-species", type=int, default=129_671)
     ap.add_argument("--gtdb-true-species", type=int, default=1000)
     ap.add_argument("--gtdb-genome", type=int, default=3_000_000)
@@ -746,7 +757,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle, run_length_histogram
 
     t0 = time.time()
-    N, B = args.gtdb_pairs, min(args.variant_batch if variant else args.gtdb_batch, args.gtdb_pairs)
+    N, B = args.gtdb_pairs, min(variant_batch(args, variant) if variant else args.gtdb_batch, args.gtdb_pairs)
     got = {}
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
@@ -894,7 +905,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     clf.close()
     em_line = None
     if rank == 0 and not variant and args.em_pairs > 0:
-        em_line = run_em(args, rdb, lp, s1, s2, o1, L, min(N, args.em_pairs), min(B, args.variant_batch), local)
+        em_line = run_em(args, rdb, lp, s1, s2, o1, L, min(N, args.em_pairs), min(B, variant_batch(args, "em")), local)
     long_line = None
     if "long" in got and not variant:
         ls1, lo1, n50 = got.pop("long")

@@ -16,17 +16,17 @@ mkdir -p $O
 Q="--cpu-sample 0 --e2e-pairs 0 --e2e-gzip-pairs 0 --em-pairs 0 --c5-kmers 0"
 declare -A CMD STEP BATCH
 GB=${GTDB_BATCH:-3333334}  # the headline's QuerySplit (the join follows MTB_JOIN / MTB_FILTER of the environment)
-VB=2000000  # the variants' QuerySplit (bench.py --variant-batch)
+VB=2000000; VB3=3333334  # the variants' QuerySplits (bench.py VARIANT_BATCH: related 2M, syncmer / conserved 3.33M)
 CMD[gtdb]="bench.py --skip-config2 --steps 1 --warmup 1 --long-reads 0 --variants= --gtdb-pairs $GB --gtdb-batch $GB --cold-pairs 0 $Q"
 STEP[gtdb]=1; BATCH[gtdb]=$GB
 CMD[long]="bench.py --skip-config2 --steps 1 --warmup 0 --gtdb-pairs 2000 --gtdb-batch 1000 --variants= --long-reads 62500 --long-batch 62500 --cold-pairs 0 $Q"
 STEP[long]=3; BATCH[long]=62500
 CMD[related]="bench.py --variant-only related --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
 STEP[related]=1; BATCH[related]=$VB
-CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
-STEP[syncmer]=1; BATCH[syncmer]=$VB
-CMD[conserved]="bench.py --variant-only conserved --steps 1 --warmup 1 --gtdb-pairs $VB $Q"
-STEP[conserved]=1; BATCH[conserved]=$VB
+CMD[syncmer]="bench.py --variant-only syncmer --steps 1 --warmup 1 --gtdb-pairs $VB3 $Q"
+STEP[syncmer]=1; BATCH[syncmer]=$VB3
+CMD[conserved]="bench.py --variant-only conserved --steps 1 --warmup 1 --gtdb-pairs $VB3 $Q"
+STEP[conserved]=1; BATCH[conserved]=$VB3
 CMD[config2]="bench.py --gtdb-kmers 0 --steps 1 --warmup 1 --long-reads 0 --cold-pairs 0 $Q"
 STEP[config2]=1; BATCH[config2]=1000000
 W="${@:-gtdb long related syncmer conserved config2}"
