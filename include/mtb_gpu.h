@@ -171,6 +171,11 @@ uint64_t mtb_workspace_bytes(const mtb_ctx* ctx);
  * index, [5] taxonomy and species map upload, [6] the whole open. */
 int mtb_open_phases(const mtb_ctx* ctx, double* sec, int n);
 int mtb_set_workspace_cap(mtb_ctx* ctx, uint64_t bytes);
+/* Gives the context's batch workspace back to the device (the next batch regrows it), e.g. when a
+ * server switches a context to another workload or frees HBM for another context; returns once
+ * the memory can be allocated again (the runtime's release of tens of GB is paid here, not by the
+ * next allocation of whatever runs next). */
+int mtb_release_workspace(mtb_ctx* ctx);
 int mtb_ctx_device(const mtb_ctx* ctx);                /* the HIP device the context runs on  */
 
 /* ---- the hot path ------------------------------------------------------------------------- */

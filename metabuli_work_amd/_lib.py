@@ -23,7 +23,7 @@ EXPORTED = [
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
     "mtb_ctx_device", "mtb_start_classify_multi", "mtb_mask_reads", "mtb_workspace_bytes", "mtb_set_workspace_cap",
-    "mtb_open_phases", "mtb_start_classify_partitioned",
+    "mtb_open_phases", "mtb_start_classify_partitioned", "mtb_release_workspace",
 ]
 
 
@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_workspace_bytes.argtypes = [vp]
     L.mtb_workspace_bytes.restype = u64
     L.mtb_set_workspace_cap.argtypes = [vp, u64]
+    L.mtb_release_workspace.argtypes = [vp]
     L.mtb_open_phases.argtypes = [vp, P(ctypes.c_double), i32]
     L.mtb_classify_batch.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp]
     L.mtb_get_taxcnt.argtypes = [vp, vp, u64, P(u64)]

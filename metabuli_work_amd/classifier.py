@@ -168,6 +168,10 @@ class Classifier:
         """Cap the batch workspace (0 = none): a batch past it is classified in pieces."""
         check(lib().mtb_set_workspace_cap(self.handle, int(nbytes)), "mtb_set_workspace_cap")
 
+    def release_workspace(self) -> None:
+        """Give the batch workspace back to the device (mtb_release_workspace)."""
+        check(lib().mtb_release_workspace(self.handle), "mtb_release_workspace")
+
     def set_stream(self, stream_ptr: int) -> None:
         check(lib().mtb_set_stream(self.handle, ctypes.c_void_p(stream_ptr)), "mtb_set_stream")
 

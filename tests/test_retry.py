@@ -86,3 +86,21 @@ def test_start_classify_splits_on_retry(make_db, tmp_path):
         assert clf.last_run["split_batches"] >= 1
     assert open(cut, "rb").read() == open(one, "rb").read()
     assert open(repc, "rb").read() == open(rep1, "rb").read()
+
+
+@pytest.mark.gpu
+def test_release_workspace(make_db):
+    """mtb_release_workspace gives the batch workspace back (0 bytes held) and the next batch regrows it
+    with the same results."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 800, paired=True, seed=62, short_frac=0.03)
+    par = LocalParameters(seqMode=2)
+    par.load_db_parameters(db_dir)
+    with Classifier(par, db_dir=db_dir) as clf:
+        a = clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        assert clf.workspace_bytes > 0
+        clf.release_workspace()
+        assert clf.workspace_bytes == 0
+        b = clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
+        assert clf.workspace_bytes > 0
+        _same(a, b)
