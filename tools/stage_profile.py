@@ -52,7 +52,7 @@ def stage_of(seq):
         elif k.startswith(("k_match_transpose", "k_compact_segments", "k_spill_scatter")):
             stage = "match_transpose"
         elif k.startswith(("k_segsort", "k_max_seg", "k_pack_live", "k_chunk_sort", "k_merge_tiles", "k_merge_finish",
-                           "k_thin_big")):
+                           "k_thin_big", "k_size_lists")):
             stage = "match_sort"
         elif stage == "match_sort" and not k.startswith("k_scan"):  # K5's live-count scan stays in K5
             stage = "assign"
