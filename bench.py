@@ -295,8 +295,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 paths on a one-GPU box (never the measurement): MTB_BENCH_BACKEND=gloo and
+    # MTB_BENCH_ONE_DEVICE=1 put every rank on cuda:0
+    if os.environ.get("MTB_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(os.environ.get("MTB_BENCH_BACKEND", "nccl"), init_method="env://")
         if args.db_parts <= 1:
             # the scaling runs time the headline lines (config 3 short and long reads) only: the CPU
             # baseline, the config-2 line, the DB variants, the file -> TSV and --em lines are
