@@ -381,8 +381,8 @@ def _cpu(c):
     if not isinstance(c, dict):
         return c
     s = _pick(c, ("value", "unit", "cores", "kind", "sample"))
-    if isinstance(s.get("sample"), str) and len(s["sample"]) > 160:
-        s["sample"] = s["sample"][:157] + "..."
+    if isinstance(s.get("sample"), str) and len(s["sample"]) > 240:
+        s["sample"] = s["sample"][:237] + "..."
     return s
 
 
