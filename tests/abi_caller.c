@@ -9,7 +9,8 @@
  *   abi_caller <db_dir> <seq_mode> <q1> [<q2>] <out.tsv> [<workspace_cap_bytes>]
  *       Classifier.cpp:6-32,81-133 in plain C: mtb_default_params, mtb_load_db_parameters, mtb_open,
  *       then per QuerySplit mtb_reader_next -> mtb_classify_batch -> mtb_get_taxcnt (halving a
- *       batch on MTB_RETRY, as Classifier.cpp:127-130 searches a split again), and mtb_close. Writes
+ *       batch on MTB_RETRY, as Classifier.cpp:127-130 searches a split again; the workspace given
+ *       back with mtb_release_workspace after every other split), and mtb_close. Writes
  *       one line per read: index, internal taxID (0 = unclassified), score bits (hex), hamming,
  *       query length, "taxID:count" list.
  */
@@ -200,6 +201,11 @@ int main(int argc, char** argv) {
         if (b.n_reads == 0) break;
         if ((err = classify_range(ctx, &b, 0, b.n_reads, first, out)) != 0) break;
         first += b.n_reads;
+        /* every other split: the workspace goes back and the next split regrows it */
+        if ((first / 1000) % 2 == 0 && (rc = mtb_release_workspace(ctx)) != MTB_OK) {
+            err = fail("mtb_release_workspace", rc);
+            break;
+        }
     }
     uint64_t qk = 0, m = 0;
     mtb_last_counts(ctx, &qk, &m);
