@@ -164,7 +164,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_DIRECT", {"staged": "0", "retry": "2", "spill": "3"}.get(mode, "1"))
     monkeypatch.setenv("MTB_FUSE_FILTER", "0" if mode == "unfused" else "1")
     monkeypatch.setenv("MTB_FILTER", "0" if mode == "nofilter" else "1")
-    # warp-specialised resident blocks (default), resident blocks walking their tiles, one block per
+    # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
     monkeypatch.setenv("MTB_SWEEP_SMALL", "1" if mode == "small" else "0")  # every window joined, absent AA 8-mers too
@@ -346,7 +346,7 @@ def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
     membership filter (MTB_FILTER=0: no K1F, no probe lines)."""
     monkeypatch.setenv("MTB_JOIN", "sweep")
     monkeypatch.setenv("MTB_FILTER", "0" if mode == "nofilter" else "1")
-    # warp-specialised resident blocks (default), resident blocks walking their tiles, one block per
+    # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
     monkeypatch.setenv("MTB_SWEEP_SMALL", "1" if mode == "small" else "0")
