@@ -43,3 +43,28 @@ def test_compact_line_drops_summaries_before_headline(tmp_path):
     assert "variants" not in line
     assert line["roofline"]["frac"] == full["roofline"]["frac"]
     assert line["cpu_baseline"]["value"] == full["cpu_baseline"]["value"]
+
+
+def test_round4_detail_round_trips(tmp_path):
+    """This round's full detail (profiles/r04/bench_detail.json) compacts to the committed line's
+    fields, the CPU baseline's sample text whole."""
+    b = _bench()
+    full = json.loads((ROOT / "profiles" / "r04" / "bench_detail.json").read_text())
+    line = b.compact_line(full, str(tmp_path / "d.json"))
+    assert len(json.dumps(line)) <= b.LINE_CAP
+    assert line["cpu_baseline"]["sample"] == full["cpu_baseline"]["sample"]
+    assert line["end_to_end"]["bgzf"]["tsv_matches_oracle"] is True
+    assert line["cold_run"]["tsv_matches_oracle"] is True
+
+
+def test_variant_batches():
+    """Per-variant QuerySplits unless --variant-batch names one for all."""
+    b = _bench()
+
+    class A:
+        variant_batch = 0
+
+    assert b.variant_batch(A, "related") == 2_000_000
+    assert b.variant_batch(A, "syncmer") == b.variant_batch(A, "conserved") == 3_333_334
+    A.variant_batch = 1_000_000
+    assert b.variant_batch(A, "syncmer") == 1_000_000
