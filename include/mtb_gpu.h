@@ -241,6 +241,18 @@ int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matche
  * arrays; out receives off[n] bytes: 'N' where masked (or not A/C/G/T/U), else the input letter. */
 int mtb_mask_reads(mtb_ctx* ctx, const char* seq, const uint64_t* off, uint32_t n_reads, char* out);
 
+/* compareDna's codon arithmetic alone (KmerMatcher.cpp:1117-1146 over KmerMatcher.h:66-158, 348-416),
+ * on the device K4 runs on: for each (query, target) DNA part the Hamming sum (getHammingDistanceSum),
+ * and the forward and reverse per-codon 2-bit words (getHammings / getHammings_reverse), from the
+ * device functions the join emits matches with. Host arrays; MTB_ERR_INTERNAL if the join's
+ * row-cached forms disagree with the plain forms on any pair. */
+/* bytes from src to dst, host or device memory either (hipMemcpyDefault: the runtime tells them
+ * apart); for bindings that assemble device-resident results of split batches (classifier.py). */
+int mtb_memcpy(void* dst, const void* src, uint64_t bytes);
+
+int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint64_t n, uint8_t* sum, uint16_t* fwd,
+                uint16_t* rev);
+
 /* ---- range-partitioned DB across GPUs ---------------------------- */
 /* A DB larger than one GPU's HBM is cut at split entries (DiffIdxSplit, Kmer.h:111-119; written
  * AA-group aligned by IndexCreator.cpp:843-851, read by KmerMatcher.cpp:180-192,255-271) into

@@ -23,7 +23,7 @@ EXPORTED = [
     "mtb_assign_chunks", "mtb_open_resident", "mtb_write_report", "mtb_copy_taxcnt", "mtb_original_taxid",
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
     "mtb_ctx_device", "mtb_start_classify_multi", "mtb_mask_reads", "mtb_workspace_bytes", "mtb_set_workspace_cap",
-    "mtb_open_phases", "mtb_start_classify_partitioned", "mtb_release_workspace",
+    "mtb_open_phases", "mtb_start_classify_partitioned", "mtb_release_workspace", "mtb_hamming", "mtb_memcpy",
 ]
 
 
@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
     L.mtb_start_classify_partitioned.argtypes = [P(vp), i32, P(MtbClassifyOpts), P(MtbClassifyStats)]
     L.mtb_ctx_device.argtypes = [vp]
     L.mtb_mask_reads.argtypes = [vp, vp, vp, u32, vp]
+    L.mtb_hamming.argtypes = [i32, vp, vp, u64, vp, vp, vp]
+    L.mtb_memcpy.argtypes = [vp, vp, u64]
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
     L.mtb_get_em_mappings.argtypes = [vp, u32, vp, u64, P(u64)]
     L.mtb_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, P(u64), P(MtbEmStats)]

@@ -195,17 +195,48 @@ class Classifier:
                     for a in (seq1, off1, seq2, off2)]
             self._keep = (seq1, off1, seq2, off2)
         res = np.zeros(n, RESULT_DTYPE) if fetch else None
+        self._dev_batch = None  # a new batch: the context's own result buffers again
         rc = check(lib().mtb_classify_batch(self.handle, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, flags,
                                             ptr(res) if fetch else ctypes.c_void_p(0)), "mtb_classify_batch")
         if rc == _abi.MTB_RETRY:
             # out of HBM for the batch's workspace: Classifier.cpp:127-130 searches the split again
-            # with a larger match buffer; here the batch is classified in halves (results fetched)
-            if not fetch or keep_stages or n < 2:
+            # with a larger match buffer; here the batch is classified in halves
+            if keep_stages or match_only or n < 2:
                 raise MtbError(f"mtb_classify_batch: {lib().mtb_last_error().decode()}")
+            if not fetch:  # results stay on the device: the halves' records and lists assembled there
+                self._classify_halves_device(seq1, off1, seq2, off2, n, device_input)
+                return None
             return self._classify_halves(seq1, off1, seq2, off2, n, device_input)
         if not fetch:
             return None
         return BatchResult(res, self.taxcnt(), *self.last_counts(), self.stage_ms())
+
+    def _classify_halves_device(self, seq1, off1, seq2, off2, n, device_input) -> None:
+        """classify_batch(fetch=False) past the workspace: the two halves (each split again if it
+        still does not fit) are classified in turn and their result records and taxID:count lists
+        copied device to device into buffers of this batch (the second half's list offsets rebased
+        onto the pooled list), which copy_results / copy_taxcnt / n_taxcnt / last_counts then serve
+        — the batch reads as one to the caller, as after an uncapped call."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        mid = n // 2
+        recs, pools, qk, mm = [], [], 0, 0
+        for lo, hi in ((0, mid), (mid, n)):
+            o1 = off1[lo:hi + 1]
+            o2 = off2[lo:hi + 1] if off2 is not None else None
+            self.classify_batch(seq1, o1, seq2, o2, device_input=device_input, fetch=False)
+            rec = torch.empty((hi - lo, _abi.RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            self.copy_results(rec.data_ptr(), on_device=True)
+            pool = torch.empty((max(self.n_taxcnt(), 1), _abi.TAXCNT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            nt = self.copy_taxcnt(pool.data_ptr(), on_device=True)
+            q, m = self.last_counts()
+            recs.append(rec)
+            pools.append(pool[:nt])
+            qk, mm = qk + q, mm + m
+        recs[1].view(torch.int32).view(-1, _abi.RESULT_DTYPE.itemsize // 4)[:, 4] += pools[0].shape[0]
+        torch.cuda.synchronize(dev)
+        self._dev_batch = (torch.cat(recs), torch.cat(pools), qk, mm)
 
     def _classify_halves(self, seq1, off1, seq2, off2, n, device_input) -> BatchResult:
         """The batch as two read ranges (offsets stay absolute into the same bases), each split
@@ -230,6 +261,8 @@ class Classifier:
         return tc
 
     def last_counts(self) -> Tuple[int, int]:
+        if getattr(self, "_dev_batch", None) is not None:
+            return self._dev_batch[2], self._dev_batch[3]
         q, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
         lib().mtb_last_counts(self.handle, ctypes.byref(q), ctypes.byref(m))
         return int(q.value), int(m.value)
@@ -256,17 +289,33 @@ class Classifier:
         lib().mtb_last_kernel_ms(self.handle, ms, 7)
         return np.array(list(ms), np.float32)
 
+    def _copy_dev(self, t, dst_ptr: int, on_device: bool) -> None:
+        """A batch assembled from halves (_classify_halves_device): its device tensor to dst."""
+        import torch
+
+        del on_device  # the runtime tells host from device pointers (unified addressing)
+        if t.numel():
+            torch.cuda.synchronize(t.device)
+            check(lib().mtb_memcpy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(t.data_ptr()), t.numel()), "mtb_memcpy")
+
     def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:
+        if getattr(self, "_dev_batch", None) is not None:
+            return self._copy_dev(self._dev_batch[0], dst_ptr, on_device)
         check(lib().mtb_copy_results(self.handle, ctypes.c_void_p(dst_ptr), int(on_device)), "mtb_copy_results")
 
     def n_taxcnt(self) -> int:
         """Pooled taxID:count entries of the last batch."""
+        if getattr(self, "_dev_batch", None) is not None:
+            return int(self._dev_batch[1].shape[0])
         nt = ctypes.c_uint64(0)
         lib().mtb_get_taxcnt(self.handle, ctypes.c_void_p(0), 0, ctypes.byref(nt))
         return int(nt.value)
 
     def copy_taxcnt(self, dst_ptr: int, on_device: bool = True) -> int:
         """The last batch's pooled taxID:count entries to dst (8 B each); returns their number."""
+        if getattr(self, "_dev_batch", None) is not None:
+            self._copy_dev(self._dev_batch[1], dst_ptr, on_device)
+            return int(self._dev_batch[1].shape[0])
         nt = ctypes.c_uint64(0)
         check(lib().mtb_copy_taxcnt(self.handle, ctypes.c_void_p(dst_ptr), int(on_device), ctypes.byref(nt)),
               "mtb_copy_taxcnt")

@@ -79,11 +79,16 @@ struct DevBuf {  // grow-only device allocation
         return e;
     }
     void release() {
-        if (p) hipFree(p);
+        if (!p) return;
+        hipFree(p);
         p = nullptr;
         if (budget) budget->used -= bytes;
         bytes = 0;
     }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }  // scratch DevBufs of an entry point are freed on every return path
     template <typename T>
     T* as() const { return (T*)p; }
 };
@@ -279,22 +284,83 @@ static double since(std::chrono::steady_clock::time_point& t) {
     return d;
 }
 
-static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out,
-                       const mtb_db_resident* res = nullptr, double readS = 0) {
-    auto t0 = std::chrono::steady_clock::now(), tp = t0;
-    int rc = validate_params(par);
-    if (rc != MTB_OK) return rc;
-    if (res) {
-        // a resident part of a range-partitioned DB (db_parts > 1): the caller passes the part's own
-        // records, its last one the next part's first k-mer (as slice_db_part keeps it), or none
-        // after the last part
-        if (!res->records || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
-    } else {
-        if (!check_db(db)) return MTB_ERR_DB;
-        if (db.nInfo < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
-        if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
+// K3 at open: diffIdx decoded chunk by chunk straight into the 12-B records (values in rank form
+// next to info & mask), so HBM holds the records plus one chunk's temporaries (~34 B per chunk word)
+// instead of the whole decode's (2 + 4 + 8 + 8 B per word and 4 + 8 B per k-mer: > 400 GB at the
+// GTDB scale's 12G k-mers). Each chunk's words come from the file (parallel preads into pinned
+// buffers) or the caller's host arrays, uploaded while the threads fill the next buffers; its whole
+// k-mers decode (the cut one goes to the next chunk), continuing the previous chunk's last value.
+// validateDatabase.cpp:78-131's checks ride along: the terminators counted over every chunk must
+// equal info's entries (checked before a chunk writes past them) and the last word must end a k-mer.
+// openS[0] gets the reads and uploads, openS[1] the decode (set by the caller from its clock).
+static int decode_db_chunked(mtb_ctx* c, HostDb& db, uint32_t mask, hipStream_t s) {
+    const uint64_t nDiff = db.nDiff, D = c->D;
+    uint64_t W = 1ull << 30;  // words per chunk (2 GB of diffIdx)
+    if (const char* e = getenv("MTB_DECODE_CHUNK_WORDS")) W = std::max<uint64_t>(8, strtoull(e, nullptr, 10));
+    W = std::max<uint64_t>(std::min(W, nDiff), 1);
+    DevBuf dDiff, dFlag, dIdx, dTmp, dVal, dInfo;  // chunk temporaries, freed on every return
+    HIP_TRY(dDiff.ensure(W * sizeof(uint16_t)));
+    HIP_TRY(dFlag.ensure(W * sizeof(uint32_t)));
+    HIP_TRY(dIdx.ensure((W + 2) * sizeof(uint64_t)));
+    HIP_TRY(dTmp.ensure(scan_tmp_elems(W) * sizeof(uint64_t)));
+    HIP_TRY(dVal.ensure(W * sizeof(uint64_t)));
+    HIP_TRY(dInfo.ensure(W * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&c->db, (D + kDbPad) * sizeof(DbRec)));
+    const bool fromFile = !db.diffFile.empty();
+    double upS = 0;
+    uint64_t w0 = 0, k0 = 0, carry = 0, seen = 0;  // seen: terminators so far (k0 stops at D)
+    HIP_TRY(hipStreamSynchronize(s));
+    while (w0 < nDiff) {
+        const uint64_t n = std::min(W, nDiff - w0);
+        auto u0 = std::chrono::steady_clock::now();
+        const bool got = fromFile ? read_to_device(db.diffFile, dDiff.p, n * sizeof(uint16_t), w0 * sizeof(uint16_t))
+                                  : upload_to_device(db.diffP + w0, dDiff.p, n * sizeof(uint16_t));
+        if (!got) return MTB_ERR_IO;
+        upS += since(u0);
+        uint64_t lastTerm = 0, lastValue = 0;
+        const uint64_t terms = decode_diff_chunk(dDiff.as<uint16_t>(), n, carry, dVal.as<uint64_t>(),
+                                                 dFlag.as<uint32_t>(), dIdx.as<uint64_t>(), dTmp.p, &lastTerm,
+                                                 &lastValue, s);
+        HIP_TRY(hipGetLastError());
+        const bool lastChunk = w0 + n == nDiff;
+        if (terms == 0) {  // no terminator in a whole chunk: a k-mer of > W words, or the tail ends mid k-mer
+            set_error("diffIdx ends mid k-mer");
+            return MTB_ERR_DB;
+        }
+        if (lastChunk && lastTerm != n - 1) {
+            set_error("diffIdx ends mid k-mer");
+            return MTB_ERR_DB;
+        }
+        seen += terms;
+        if (seen <= D) {  // the records of these k-mers: info & mask next to the rank-form values
+            u0 = std::chrono::steady_clock::now();
+            const bool gotInfo = fromFile ? read_to_device(db.infoFile, dInfo.p, terms * sizeof(uint32_t),
+                                                           k0 * sizeof(uint32_t))
+                                          : upload_to_device(db.infoP + k0, dInfo.p, terms * sizeof(uint32_t));
+            if (!gotInfo) return MTB_ERR_IO;
+            upS += since(u0);
+            launch_mask_info(dInfo.as<uint32_t>(), terms, mask, s);
+            if (c->par.kmer_format == 2) launch_to_rank_form(dVal.as<uint64_t>(), terms, s);
+            launch_pack_db(dVal.as<uint64_t>(), dInfo.as<uint32_t>(), terms, c->db + k0, s);
+            HIP_TRY(hipStreamSynchronize(s));
+            k0 += terms;
+        }
+        carry = lastValue;
+        w0 += lastTerm + 1;
     }
-    mtb_ctx* c = new mtb_ctx();
+    if (seen != D) {  // counted to the end, written only up to D
+        set_error("diffIdx k-mer count " + std::to_string(seen) + " != info entries " + std::to_string(D));
+        return MTB_ERR_DB;
+    }
+    c->openS[0] += upS;
+    return MTB_OK;
+}
+
+// Everything of an opening after the argument checks, into a fresh context (the caller closes it
+// on failure, so no error path leaks the context, its stream or device arrays).
+static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, const mtb_db_resident* res,
+                     double readS, std::chrono::steady_clock::time_point t0) {
+    auto tp = t0;
     c->device = device;
     c->par = *par;
     c->tables = make_tables();
@@ -317,49 +383,8 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     } else {
         c->D = db.nInfo;
         // diffIdx -> values (K3), info & mask (KmerMatcher.cpp:204-205, :381), then one record per k-mer
-        uint16_t* dDiff = nullptr;
-        uint32_t* dFlag = nullptr;
-        uint64_t *dIdx = nullptr, *dVal = nullptr;
-        uint32_t* dInfo = nullptr;
-        void* dTmp = nullptr;
-        const uint64_t nDiff = db.nDiff;
-        HIP_TRY(hipMalloc(&dVal, c->D * sizeof(uint64_t)));
-        HIP_TRY(hipMalloc(&dDiff, nDiff * sizeof(uint16_t)));
-        HIP_TRY(hipMalloc(&dFlag, nDiff * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&dIdx, (std::max(nDiff, c->D) + 1) * sizeof(uint64_t)));
-        HIP_TRY(hipMalloc(&dTmp, scan_tmp_elems(std::max(nDiff, c->D)) * sizeof(uint64_t)));
-        if (!db.diffFile.empty()) {
-            HIP_TRY(hipStreamSynchronize(s));
-            if (!read_to_device(db.diffFile, dDiff, nDiff * sizeof(uint16_t))) return MTB_ERR_IO;
-        } else {
-            HIP_TRY(hipMemcpyAsync(dDiff, db.diffP, nDiff * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-        }
-        const uint64_t terms = decode_diff_idx(dDiff, nDiff, dVal, c->D, dFlag, dIdx, dTmp, s);
-        if (terms != c->D) {  // validateDatabase.cpp:78-131 (checked before the decode writes by k-mer index)
-            set_error(terms == ~0ull ? "diffIdx ends mid k-mer"
-                                     : "diffIdx k-mer count " + std::to_string(terms) + " != info entries " +
-                                           std::to_string(c->D));
-            hipFree(dDiff); hipFree(dFlag); hipFree(dIdx); hipFree(dTmp); hipFree(dVal);
-            return MTB_ERR_DB;
-        }
-        HIP_TRY(hipStreamSynchronize(s));
-        hipFree(dDiff);
-        hipFree(dFlag);
-        hipFree(dIdx);
-        hipFree(dTmp);
-        HIP_TRY(hipMalloc(&dInfo, c->D * sizeof(uint32_t)));
-        if (!db.infoFile.empty()) {
-            if (!read_to_device(db.infoFile, dInfo, c->D * sizeof(uint32_t))) return MTB_ERR_IO;
-        } else {
-            HIP_TRY(hipMemcpyAsync(dInfo, db.infoP, c->D * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        }
-        launch_mask_info(dInfo, c->D, mask, s);
-        if (par->kmer_format == 2) launch_to_rank_form(dVal, c->D, s);
-        HIP_TRY(hipMalloc(&c->db, (c->D + kDbPad) * sizeof(DbRec)));
-        launch_pack_db(dVal, dInfo, c->D, c->db, s);
-        HIP_TRY(hipStreamSynchronize(s));
-        hipFree(dVal);
-        hipFree(dInfo);
+        const int drc = decode_db_chunked(c, db, mask, s);
+        if (drc != MTB_OK) return drc;
     }
     // + kDbPad records of value ~0 / taxID 0: the probe's 8-wide reads from any DB index need no bound
     HIP_TRY(hipMemcpyAsync(c->db + c->D, padRec, sizeof(padRec), hipMemcpyHostToDevice, s));
@@ -372,7 +397,7 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
         c->rankLo = ((uint64_t)ends[0].hi << 32 | ends[0].lo) >> 24;
         c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
-    c->openS[1] = since(tp);
+    c->openS[1] = since(tp) - (c->openS[0] - readS);  // the decode's uploads are in openS[0]
     if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e));  // A/B only: invalid results
     if (const char* e = getenv("MTB_AB_SWEEP_COUNT")) set_ab_sweep_count(atoi(e));  // A/B only: invalid results
     if (const char* e = getenv("MTB_MATCH_WINDOW")) c->matchWinCap = (uint32_t)strtoul(e, nullptr, 10);
@@ -471,6 +496,33 @@ static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** 
     bind_workspace(c, 0);
     c->openS[5] = since(tp);
     c->openS[6] = readS + std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return MTB_OK;
+}
+
+
+static int open_common(HostDb& db, const mtb_params* par, int device, mtb_ctx** out,
+                       const mtb_db_resident* res = nullptr, double readS = 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = validate_params(par);
+    if (rc != MTB_OK) return rc;
+    if (res) {
+        // a resident part of a range-partitioned DB (db_parts > 1): the caller passes the part's own
+        // records, its last one the next part's first k-mer (as slice_db_part keeps it), or none
+        // after the last part
+        if (!res->records || res->n_kmers < 2) { set_error("resident DB needs >= 2 k-mers"); return MTB_ERR_DB; }
+    } else {
+        if (!check_db(db)) return MTB_ERR_DB;
+        if (db.nInfo < 2) { set_error("DB has fewer than 2 k-mers"); return MTB_ERR_DB; }
+        if (par->db_parts > 1 && !slice_db_part(db, par->db_part, par->db_parts)) return MTB_ERR_DB;
+    }
+    mtb_ctx* c = new mtb_ctx();
+    rc = open_into(c, db, par, device, res, readS, t0);
+    if (rc != MTB_OK) {
+        const std::string msg = mtb_last_error();  // mtb_close must not mask the opening's error
+        mtb_close(c);
+        set_error(msg);
+        return rc;
+    }
     *out = c;
     return MTB_OK;
 }
@@ -1029,12 +1081,15 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     if (sweep) {  // K4S: the DB's tiles (once per context) and this batch's query bucket starts
         if (!c->tileRec) {
             const uint64_t nT = sweep_tiles(c->D, c->sweepNom);
-            DevBuf tmp;
+            DevBuf tmp, rec, pre;  // freed on every return; the tiles are kept only once built
             HIP_TRY(tmp.ensure(sizeof(uint64_t) * kSweepStartsTmp));
-            HIP_TRY(hipMalloc(&c->tileRec, sizeof(uint64_t) * (nT + 1)));
-            HIP_TRY(hipMalloc(&c->tilePre, sizeof(uint32_t) * (nT + 1)));
-            build_sweep_tiles(c->db, c->D, c->sweepNom, tmp.as<uint64_t>(), c->tileRec, c->tilePre, s);
+            HIP_TRY(rec.ensure(sizeof(uint64_t) * (nT + 1)));
+            HIP_TRY(pre.ensure(sizeof(uint32_t) * (nT + 1)));
+            build_sweep_tiles(c->db, c->D, c->sweepNom, tmp.as<uint64_t>(), rec.as<uint64_t>(), pre.as<uint32_t>(), s);
             HIP_TRY(hipStreamSynchronize(s));
+            c->tileRec = rec.as<uint64_t>();
+            c->tilePre = pre.as<uint32_t>();
+            rec.p = pre.p = nullptr;  // owned by the context now (mtb_close frees them)
             c->nTiles = nT;
         }
         HIP_TRY(c->qStart.ensure(sizeof(uint32_t) * (kSweepStartsTmp + c->nTiles + 1)));
@@ -1090,7 +1145,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         }
         c->stats[14] = direct ? longN : 0;
         if (direct && longN) {  // the long runs, a wave each; then the spill count and flag again
-            launch_match_long(c->longList.as<LongRun>(), longN, qk, qi, c->unitInfo.as<uint64_t>(), C, c->db, c->spOf,
+            launch_match_long(c->longList.as<LongRun>(), longN, qk, qi, c->unitInfo.as<uint64_t>(), C, c->db, c->D, c->spOf,
                               (uint32_t)c->maxTax, c->par.kmer_format, c->readCnt.as<uint32_t>(),
                               c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                               c->spillCap, c->errFlag.as<int>(), c->mDirect.as<SegMatch>(),
@@ -1116,6 +1171,9 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             }
             nSpill = 0;
             direct = false;  // rerun staged
+            // the sweep built no windows (it needs none); the staged join does, unless it runs unstaged
+            if (sweep && !unstaged_join(c->lines != nullptr, c->D, Q, std::min<uint32_t>(c->matchWinCap, 3072)))
+                launch_match_windows(qk, Q, c->db, c->D, c->dir, c->par.kmer_format, c->matchWin.as<uint64_t>(), s);
             HIP_TRY(c->mStage.ensure(sizeof(mtb_match) * c->stageRegion * kStageRegions));
             HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
             HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
@@ -1169,12 +1227,39 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     return MTB_OK;
 }
 
-// After an mtb_assign_* call: a device-side consistency check (err 2) is reported.
+// A batch's device-side error flag (mtb_launch.h kErr*) as the entry point's status and message.
+static int batch_error(int err) {
+    switch (err) {
+        case kErrTaxid:
+            set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
+            return MTB_ERR_DB;
+        case kErrProbeStash:
+            set_error("a DB AA run holds >= 2^24 k-mers (probe join stash limit): use MTB_JOIN=sort");
+            return MTB_ERR_DB;
+        case kErrStagedRead:
+            set_error("internal error: a staged or spilled match names a read outside the batch or past its segment");
+            return MTB_ERR_INTERNAL;
+        case kErrProbeCount:
+            set_error("internal error: emitted matches disagree with the probe counts");
+            return MTB_ERR_INTERNAL;
+        case kErrRunOutsideDb:
+            set_error("internal error: K4 found an AA run starting past the DB's end (run index or probe lines "
+                      "inconsistent with the DB records)");
+            return MTB_ERR_INTERNAL;
+        case kErrLiveCount:
+            set_error("internal error: K5 kept more live matches than a read's segment holds");
+            return MTB_ERR_INTERNAL;
+        default:
+            set_error("internal error: device error flag " + std::to_string(err));
+            return MTB_ERR_INTERNAL;
+    }
+}
+
+// After an mtb_assign_* call: a device-side consistency check is reported.
 static int check_err_flag(mtb_ctx* c) {
     int err = 0;
     HIP_TRY(hipMemcpy(&err, c->errFlag.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (err == 2) { set_error("internal error: inconsistent per-read match counts in K5"); return MTB_ERR_INTERNAL; }
-    return MTB_OK;
+    return err ? batch_error(err) : MTB_OK;
 }
 
 // SeqIterator::maskLowComplexityRegions on the device for the batch's mates: masked copies in
@@ -1204,6 +1289,43 @@ static int mask_mates(mtb_ctx* c, const uint8_t* seq1, const uint64_t* off1, con
 }
 
 extern "C" {
+
+int mtb_memcpy(void* dst, const void* src, uint64_t bytes) {
+    if (bytes && (!dst || !src)) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return MTB_OK;
+}
+
+int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint64_t n, uint8_t* sum, uint16_t* fwd,
+                uint16_t* rev) {
+    if (n && (!query || !target || !sum || !fwd || !rev)) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (!n) return MTB_OK;
+    HIP_TRY(hipSetDevice(device));
+    DevBuf a, b, s8, f16, r16, bad;
+    HIP_TRY(a.ensure(8 * n));
+    HIP_TRY(b.ensure(8 * n));
+    HIP_TRY(s8.ensure(n));
+    HIP_TRY(f16.ensure(2 * n));
+    HIP_TRY(r16.ensure(2 * n));
+    HIP_TRY(bad.ensure(8));
+    HIP_TRY(hipMemcpy(a.p, query, 8 * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b.p, target, 8 * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(bad.p, 0, 8));
+    launch_hamming_check(a.as<uint64_t>(), b.as<uint64_t>(), n, s8.as<uint8_t>(), f16.as<uint16_t>(),
+                         r16.as<uint16_t>(), bad.as<unsigned long long>(), nullptr);
+    HIP_TRY(hipGetLastError());
+    unsigned long long nBad = 0;
+    HIP_TRY(hipMemcpy(&nBad, bad.p, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sum, s8.p, n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fwd, f16.p, 2 * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rev, r16.p, 2 * n, hipMemcpyDeviceToHost));
+    if (nBad) {
+        set_error("internal error: K4's row-cached Hamming forms disagree with the plain forms on " +
+                  std::to_string(nBad) + " pairs");
+        return MTB_ERR_INTERNAL;
+    }
+    return MTB_OK;
+}
 
 int mtb_mask_reads(mtb_ctx* c, const char* seq, const uint64_t* off, uint32_t n, char* out) {
     if (!c || (n && (!seq || !off || !out))) { set_error("null argument"); return MTB_ERR_ARG; }
@@ -1332,20 +1454,7 @@ static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, cons
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     for (int k = 0; k < mtb_ctx::kNumKern; k++)
         HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
-    if (err == 2 || err == 4) {
-        set_error(err == 2 ? "internal error: a staged match names a read outside the batch"
-                           : "internal error: emitted matches disagree with the probe counts");
-        return MTB_ERR_INTERNAL;
-    }
-    if (err == 3) {
-        set_error("a DB AA run holds >= 2^24 k-mers (probe join stash limit): use MTB_JOIN=sort");
-        return MTB_ERR_DB;
-    }
-    if (err) {
-        set_error("a selected reference k-mer has taxID 0 or no species in taxID_list (KmerMatcher.cpp:432-441)");
-        return MTB_ERR_DB;
-    }
-    return MTB_OK;
+    return err ? batch_error(err) : MTB_OK;
 }
 
 // The reference's match-buffer exhaustion is a retry (KmerMatcher.cpp:474-476 returns false,
@@ -1359,14 +1468,9 @@ int mtb_classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, const c
     const int rc = classify_batch(c, seq, off, seq2, off2, n, flags, results);
     if (rc != MTB_ERR_OOM) return rc;
     (void)hipGetLastError();
-    (void)hipStreamSynchronize(c->stream);
     // the buffers the failed attempt grew would otherwise stay at its size: the pieces start clean
     const double held = c->ws.used * 1e-9;
-    for (DevBuf* b : batch_bufs(c)) b->release();
-    c->nReads = 0;
-    c->M = c->Q = c->Qall = c->nTaxcnt = 0;
-    c->sparse = false;
-    c->emValid = c->emPackedValid = false;
+    mtb::ctx_release_workspace(c);
     char msg[200];
     snprintf(msg, sizeof msg, "out of HBM for the workspace of a %u-read batch (%.2f GB held%s): classify it in smaller "
              "pieces", n, held, c->ws.cap ? ", capped" : "");
@@ -1554,6 +1658,16 @@ void ctx_release_workspace(mtb_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : batch_bufs(c)) b->release();
+    // the last batch's results went with the buffers: the getters (mtb_get_taxcnt / _matches /
+    // _query_kmers / _em_mappings) see an empty batch instead of freed device pointers
+    c->nReads = 0;
+    c->M = c->Q = c->Qall = c->nTaxcnt = c->liveM = 0;
+    c->qKeys = nullptr;
+    c->qSlots = nullptr;
+    c->sparse = false;
+    c->keepStages = false;
+    c->emValid = c->emPackedValid = false;
+    c->emHost.clear();
 }
 
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache; }

@@ -1702,7 +1702,7 @@ __global__ void __launch_bounds__(256) k_pack_live(const mtb_match* __restrict__
     // a live count above the segment, or live offsets past the matches, would be a K5 bug: never
     // copy out of bounds
     if (live > mOff[r + 1] - mOff[r] || liveOff[r + 1] > mOff[nReads]) {
-        if (lane == 0) atomicExch(err, 2);
+        if (lane == 0) atomicExch(err, kErrLiveCount);
         return;
     }
     const uint64_t* src = reinterpret_cast<const uint64_t*>(in + mOff[r]);

@@ -96,7 +96,9 @@ bool build_species_map(HostDb& db);
 bool load_db_files(const std::string& dir, HostDb& db, bool stream = false);
 // `bytes` of a file into device memory: parallel reads into pinned staging buffers, each uploaded
 // as soon as it is full (the file read and the PCIe upload overlap); false + set_error on failure
-bool read_to_device(const std::string& path, void* dst, uint64_t bytes);
+bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t fileOff = 0);
+// the same from host memory (pageable: copied into the pinned buffers by the threads)
+bool upload_to_device(const void* src, void* dst, uint64_t bytes);
 bool check_db(const HostDb& db);
 bool partition_bounds(const uint64_t* split, uint64_t nSplit, uint64_t D, int parts, std::vector<uint64_t>& start,
                       std::vector<uint64_t>& entry);

@@ -757,22 +757,36 @@ __global__ void k_deltas(const uint16_t* __restrict__ diff, uint64_t n, const ui
     }
 }
 
-uint64_t decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
-                         uint64_t* idxTmp, void* scanTmp, hipStream_t s) {
-    if (nDiff == 0) return 0;
-    k_term_flags<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, flagTmp);
-    exclusive_scan_u32(flagTmp, nDiff, idxTmp, scanTmp, s);
+__global__ void k_last_term(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ idx, uint64_t n,
+                            uint64_t last, uint64_t* __restrict__ out) {
+    MTB_GRID_STRIDE(i, n) if (flag[i] && idx[i] == last) *out = i;
+}
+
+__global__ void k_add_carry(uint64_t* v, uint64_t carry) { v[0] += carry; }
+
+// One chunk of diffIdx words that starts at a k-mer's first word: the values of the chunk's whole
+// k-mers (their count is returned) continue from carry, the last value of the chunk before; a k-mer
+// cut by the chunk's end is left to the next chunk, which starts at the word after *lastTerm (the
+// chunk index of the last terminator). idxTmp: n + 2 u64; scanTmp: scan_tmp_elems(n) u64.
+uint64_t decode_diff_chunk(const uint16_t* diff, uint64_t n, uint64_t carry, uint64_t* values, uint32_t* flagTmp,
+                           uint64_t* idxTmp, void* scanTmp, uint64_t* lastTerm, uint64_t* lastValue, hipStream_t s) {
+    *lastTerm = 0;
+    if (n == 0) return 0;
+    k_term_flags<<<stride_grid(n), 256, 0, s>>>(diff, n, flagTmp);
+    exclusive_scan_u32(flagTmp, n, idxTmp, scanTmp, s);
     uint64_t terms = 0;
-    uint16_t lastWord = 0;
-    hipMemcpyAsync(&terms, idxTmp + nDiff, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(&lastWord, diff + nDiff - 1, sizeof(uint16_t), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&terms, idxTmp + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
-    if (!(lastWord & 0x8000u)) return ~0ull;
-    if (terms != nKmers) return terms;
-    k_deltas<<<stride_grid(nDiff), 256, 0, s>>>(diff, nDiff, idxTmp, values);
+    if (terms == 0) return 0;
+    k_last_term<<<stride_grid(n), 256, 0, s>>>(flagTmp, idxTmp, n, terms - 1, idxTmp + n + 1);
+    k_deltas<<<stride_grid(n), 256, 0, s>>>(diff, n, idxTmp, values);
+    if (carry) k_add_carry<<<1, 1, 0, s>>>(values, carry);
+    hipMemcpyAsync(lastTerm, idxTmp + n + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     // inclusive scan of deltas = exclusive scan shifted by one: scan into idxTmp then take [1..]
-    exclusive_scan_u64(values, nKmers, idxTmp, scanTmp, s);
-    hipMemcpyAsync(values, idxTmp + 1, nKmers * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+    exclusive_scan_u64(values, terms, idxTmp, scanTmp, s);
+    hipMemcpyAsync(values, idxTmp + 1, terms * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(lastValue, values + terms - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
     return terms;
 }
 
@@ -1027,7 +1041,7 @@ __device__ __forceinline__ void emit_match(uint64_t key, const HamRows& hr, uint
                                            O* __restrict__ out, uint32_t* __restrict__ outRank, uint64_t w,
                                            uint32_t rank, int* __restrict__ err) {
     const int32_t sp = tax <= maxTax ? spOf[tax] : 0;
-    if (tax == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
+    if (tax == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
     mtb_match m;
     m.qinfo = info;
     m.target_id = tax;
@@ -1055,7 +1069,7 @@ __device__ __forceinline__ uint64_t run_emit(uint64_t key, const HamRows& hr, ui
         const uint32_t hs = hamming_sum_rows(hr, tv);
         if (hs > thr) continue;
         if (w >= wEnd) {
-            atomicExch(err, 4);
+            atomicExch(err, kErrProbeCount);
             return w;
         }
         emit_match(key, hr, info, tv, infos[t], hs, rev, spOf, maxTax, out, outRank, w++, rank++, err);
@@ -1330,6 +1344,14 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     bool small[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
+        // a run start past the DB's end can only come from an inconsistent run index or probe line
+        // (a run's lower bound is at most D): flagged, and the run taken as empty at the DB's end, so
+        // the speculative two-record read below stays inside the 8 pad records (KmerMatcher.cpp:363,378:
+        // the reader never runs past the DB)
+        if (live[j] && lo[j] + vOff > D) {
+            atomicExch(err, kErrRunOutsideDb);
+            lo[j] = D - vOff;
+        }
         if (hi[j] + vOff > D - 1) hi[j] = D - 1 - vOff;  // the last DB k-mer is never a candidate
         if (lo[j] > hi[j]) hi[j] = lo[j];
         small[j] = !staged && live[j] && hi[j] - lo[j] <= 2;
@@ -1487,14 +1509,19 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
 __global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ list, const uint64_t* __restrict__ qkey,
                                                    const uint32_t* __restrict__ qslot,
                                                    const uint64_t* __restrict__ unitInfo, uint32_t C,
-                                                   const DbRec* __restrict__ db, const int32_t* __restrict__ spOf,
-                                                   uint32_t maxTax, int kmerFormat, uint32_t* __restrict__ readCnt,
+                                                   const DbRec* __restrict__ db, uint64_t D,
+                                                   const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
+                                                   uint32_t* __restrict__ readCnt,
                                                    unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
                                                    uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
                                                    SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
                                                    int* __restrict__ overflow, uint32_t capShift,
                                                    unsigned long long* __restrict__ stats) {
     const LongRun lr = list[blockIdx.x];
+    if (lr.lo > lr.hi || lr.hi > D - 1) {  // the producers clamp runs to [0, D - 1]: never read past the DB
+        if (threadIdx.x == 0) atomicExch(err, kErrRunOutsideDb);
+        return;
+    }
     const uint32_t got = wave_long_run(qkey[lr.q], qslot[lr.q], lr.lo, lr.hi, DbVal{db}, DbTax{db}, unitInfo, C, spOf,
                                        maxTax, kmerFormat, readCnt, total, buf, bufRank, region, err, direct, dirOff,
                                        overflow, capShift, (int)threadIdx.x);
@@ -1502,11 +1529,11 @@ __global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ l
 }
 
 void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, const uint32_t* qslot,
-                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, const int32_t* spOf, uint32_t maxTax,
-                       int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint32_t* bufRank,
-                       uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                       uint32_t capShift, unsigned long long* stats, hipStream_t s) {
-    if (n) k_match_long<<<n, 64, 0, s>>>(list, qkey, qslot, unitInfo, C, db, spOf, maxTax, kmerFormat, readCnt, total, buf,
+                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D, const int32_t* spOf,
+                       uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
+                       uint32_t* bufRank, uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff,
+                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s) {
+    if (n) k_match_long<<<n, 64, 0, s>>>(list, qkey, qslot, unitInfo, C, db, D, spOf, maxTax, kmerFormat, readCnt, total, buf,
                                          bufRank, region, err, direct, dirOff, overflow, capShift, stats);
 }
 
@@ -1521,12 +1548,12 @@ __global__ void k_match_transpose(const mtb_match* __restrict__ buf, const uint3
     const mtb_match m = buf[i];
     const uint32_t r = info_seq(m.qinfo) - 1;
     if (r >= nReads) {  // cannot happen for staged matches; never write out of bounds
-        atomicExch(err, 2);
+        atomicExch(err, kErrStagedRead);
         return;
     }
     const uint64_t o = readOff[r] + bufRank[i];
     if (o >= readOff[r + 1]) {
-        atomicExch(err, 2);
+        atomicExch(err, kErrStagedRead);
         return;
     }
     out[o] = m;
@@ -1934,7 +1961,7 @@ __global__ void __launch_bounds__(256) k_probe(const uint64_t* __restrict__ qkey
         if (sums[k] > thr) continue;
         const uint32_t t = tax[k];
         const int32_t sp = t <= maxTax ? spOf[t] : 0;
-        if (t == 0 || sp <= 0) atomicExch(err, 1);  // KmerMatcher.cpp:432-441 exits
+        if (t == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
         mtb_match m;
         m.qinfo = info;
         m.target_id = t;
@@ -1965,6 +1992,29 @@ bool unstaged_join(bool lines, uint64_t D, uint64_t Q, uint32_t winCap) {
         return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)kStageFreeRatio;
     }();
     return lines && (D > ratio * Q || winCap == 0);
+}
+
+// mtb_hamming: the device's Hamming functions on given pairs — the row-cached forms K4 emits with
+// (hamming_sum_rows, hammings_rows) next to the plain forms (hamming_sum, hammings); bad counts
+// the pairs where the two disagree.
+__global__ void k_hamming_check(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint64_t n,
+                                uint8_t* __restrict__ sum, uint16_t* __restrict__ fwd, uint16_t* __restrict__ rev,
+                                unsigned long long* __restrict__ bad) {
+    MTB_GRID_STRIDE(i, n) {
+        const HamRows hr = hamming_rows(a[i]);
+        const uint32_t s = hamming_sum_rows(hr, b[i]);
+        const uint32_t f = hammings_rows(hr, a[i], b[i], false), r = hammings_rows(hr, a[i], b[i], true);
+        if (s != hamming_sum(a[i], b[i]) || f != hammings(a[i], b[i], false) || r != hammings(a[i], b[i], true))
+            atomicAdd(bad, 1ull);
+        sum[i] = (uint8_t)s;
+        fwd[i] = (uint16_t)f;
+        rev[i] = (uint16_t)r;
+    }
+}
+
+void launch_hamming_check(const uint64_t* a, const uint64_t* b, uint64_t n, uint8_t* sum, uint16_t* fwd, uint16_t* rev,
+                          unsigned long long* bad, hipStream_t s) {
+    if (n) k_hamming_check<<<stride_grid(n), 256, 0, s>>>(a, b, n, sum, fwd, rev, bad);
 }
 
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
@@ -2032,7 +2082,7 @@ __global__ void k_spill_scatter(const mtb_match* __restrict__ spill, const uint3
     const mtb_match m = spill[i];
     const uint32_t r = info_seq(m.qinfo) - 1;
     if (r >= nReads || readOff[r] + spillRank[i] >= readOff[r + 1]) {  // never write out of bounds
-        atomicExch(err, 2);
+        atomicExch(err, kErrStagedRead);
         return;
     }
     out[readOff[r] + spillRank[i]] = m;
@@ -2213,6 +2263,10 @@ __device__ __forceinline__ bool sweep_query(uint64_t q, uint64_t key, uint32_t s
         if (i2 <= n && vals[i2 - 1] < aa2) p2 = i2;
     }
     uint64_t lo = p1, hi = p2;
+    if (lo + vOff > D) {  // a tile past the DB's end (inconsistent tiles): flagged, the run taken as empty
+        atomicExch(err, kErrRunOutsideDb);
+        lo = D - vOff;
+    }
     if (hi + vOff > D - 1) hi = D - 1 - vOff;  // the last DB k-mer is never a candidate
     if (lo > hi) hi = lo;
     if (hi - lo > kLongRun) {  // a long run: scanned by a wave of its own (k_match_long), from HBM

@@ -9,6 +9,15 @@
 
 namespace mtb {
 
+// The batch's device-side error flag (errFlag, last writer wins); mtb_api.hip turns each into
+// its own message, so a failure names the check that caught it.
+constexpr int kErrTaxid = 1;         // a selected DB k-mer with taxID 0 or no species (KmerMatcher.cpp:432-441)
+constexpr int kErrStagedRead = 2;    // a staged or spilled match names a read outside the batch / past its segment
+constexpr int kErrProbeStash = 3;    // a DB AA run of >= 2^24 k-mers (probe join)
+constexpr int kErrProbeCount = 4;    // the probe join emitted other counts than it reserved
+constexpr int kErrRunOutsideDb = 5;  // K4: an AA run starting past the DB's end (run index / probe line inconsistent)
+constexpr int kErrLiveCount = 6;     // K5: a read's live-match count above its segment
+
 struct ReadMeta {  // per read: raw lengths, covered lengths, windows per frame of each mate
     int32_t len1, len2, ql1, ql2, w1, w2;
 };
@@ -102,10 +111,12 @@ constexpr uint64_t kAARankEnd = 37822859361ull;
 constexpr int kQuerySortLo = 36, kQuerySortHi = 60;
 constexpr int kQuerySortLoFine = 36;  // unstaged K4 sort prefix: 3 passes (4 passes, 28, measured 1.5 ms slower with the run index)
 
-// returns the terminal words of diff (the k-mers it holds; ~0 if its last word is not one) and decodes
-// only when that equals nKmers
-uint64_t decode_diff_idx(const uint16_t* diff, uint64_t nDiff, uint64_t* values, uint64_t nKmers, uint32_t* flagTmp,
-                         uint64_t* idxTmp, void* scanTmp, hipStream_t s);
+// K3 over one chunk of diffIdx words starting at a k-mer's first word: returns the whole k-mers it
+// holds, their values (continuing from carry, the previous chunk's last value) in values, the chunk
+// index of its last terminator word in *lastTerm and the last value in *lastValue (idxTmp n + 2 u64,
+// flagTmp n u32, scanTmp scan_tmp_elems(n) u64)
+uint64_t decode_diff_chunk(const uint16_t* diff, uint64_t n, uint64_t carry, uint64_t* values, uint32_t* flagTmp,
+                           uint64_t* idxTmp, void* scanTmp, uint64_t* lastTerm, uint64_t* lastValue, hipStream_t s);
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s);
 
 // A resident DB k-mer: its value in rank form (low / high 32 bits) and its taxID (info & mask) in
@@ -227,10 +238,10 @@ struct LongRun {
     uint64_t lo, hi;  // its DB run
 };
 void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, const uint32_t* qslot,
-                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, const int32_t* spOf, uint32_t maxTax,
-                       int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf, uint32_t* bufRank,
-                       uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                       uint32_t capShift, unsigned long long* stats, hipStream_t s);
+                       const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D, const int32_t* spOf,
+                       uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
+                       uint32_t* bufRank, uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff,
+                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s);
 // K4S DB-sweep join (MTB_JOIN=sweep; direct output only): tiles of ~nom DB records ending at
 // sort-prefix bucket bounds, built once per context (pstartTmp: kSweepStartsTmp u64 scratch; tileRec
 // sweep_tiles + 1 u64, tilePre sweep_tiles + 1 u32); per batch the sorted queries' bucket starts
@@ -277,6 +288,9 @@ void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint6
                             const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
                             int* err, hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
+// mtb_hamming's kernel (bad: u64 count of pairs where the row-cached and plain forms disagree)
+void launch_hamming_check(const uint64_t* a, const uint64_t* b, uint64_t n, uint8_t* sum, uint16_t* fwd, uint16_t* rev,
+                          unsigned long long* bad, hipStream_t s);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const DbRec* db, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
 

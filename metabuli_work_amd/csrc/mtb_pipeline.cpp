@@ -1307,6 +1307,9 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                 if (p == 0) decide(true, lo, k, s);
                 B.bar.wait();
             }
+            // every worker has read the loop's exit condition (B.fail, B.pieces) before worker 0
+            // finishes this batch and refills B with the next one's pieces
+            B.bar.wait();
             if (p == 0) {
                 if (B.fail == MTB_OK && s->tc.ensure(std::max<size_t>(B.all.size(), 1)) != hipSuccess) B.fail = MTB_ERR_OOM;
                 if (B.fail == MTB_OK) std::copy(B.all.begin(), B.all.end(), s->tc.p);

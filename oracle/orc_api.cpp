@@ -322,4 +322,24 @@ void orc_genetic_tables(int32_t* nuc2aa512, int32_t* nuc2num512, uint8_t* atcg25
     memcpy(irct256, kChars.iRCT, 256);
 }
 
+// The restated Hamming tables (orc_core.h: kHammingLookup, codonField) as the reference lays its
+// own out (KmerMatcher.h:66-158): lookup64[q * 8 + t]; lut512[k * 64 + (q << 3 | t)] = field k's
+// 2-bit value shifted to its place, as HAMMING_LUTk holds it.
+void orc_hamming_tables(uint8_t* lookup64, uint16_t* lut512) {
+    for (int q = 0; q < 8; q++)
+        for (int t = 0; t < 8; t++) {
+            lookup64[q * 8 + t] = kHammingLookup[q][t];
+            for (int k = 0; k < 8; k++) lut512[k * 64 + (q << 3 | t)] = (uint16_t)(codonField(q, t, k) << (2 * k));
+        }
+}
+
+// getHammingDistanceSum / getHammings / getHammings_reverse (KmerMatcher.h:348-416) as restated.
+void orc_hamming(const uint64_t* a, const uint64_t* b, uint64_t n, uint8_t* sum, uint16_t* fwd, uint16_t* rev) {
+    for (uint64_t i = 0; i < n; i++) {
+        sum[i] = hammingSum(a[i], b[i]);
+        fwd[i] = hammings(a[i], b[i]);
+        rev[i] = hammingsReverse(a[i], b[i]);
+    }
+}
+
 }  // extern "C"

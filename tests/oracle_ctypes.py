@@ -46,6 +46,10 @@ def lib():
         L.orc_set_threads.argtypes = [i32]
         L.orc_threads.restype = i32
         L.orc_genetic_tables.argtypes = [vp, vp, vp, vp]
+        L.orc_hamming_tables.argtypes = [vp, vp]
+        L.orc_hamming_tables.restype = None
+        L.orc_hamming.argtypes = [vp, vp, u64, vp, vp, vp]
+        L.orc_hamming.restype = None
         L.orc_write_report.argtypes = [vp, ctypes.c_char_p, i32, vp, vp, u64]
         L.orc_write_report.restype = i32
         L.orc_last_em_maps.argtypes = [vp, u64, ctypes.POINTER(u64)]

@@ -6,6 +6,7 @@ import pathlib
 import re
 
 import numpy as np
+import pytest
 
 from metabuli_work_amd import _abi
 from metabuli_work_amd._lib import EXPORTED, lib
@@ -77,6 +78,25 @@ def test_product_genetic_code_matches_reference_tables():
         if 7 in (a, b, c):
             continue
         assert num[a << 4 | b << 2 | c] == v
+
+
+@pytest.mark.gpu
+def test_device_hamming_pinned_to_reference():
+    """K4's codon arithmetic on the device (mtb_hamming: hamming_sum_rows / hammings_rows, the forms
+    emit_match uses, checked against the plain hamming_sum / hammings in the kernel) equals the
+    reference's getHammingDistanceSum / getHammings / getHammings_reverse on the golden pairs
+    (tables parsed from KmerMatcher.h:66-158, tests/golden/make_ref_tables.py): every codon pair at
+    every field, LUT7's rows 4-5 included, plus 2,048 random pairs."""
+    from tests.test_oracle import hamming_golden
+
+    _, a, b, esum, efwd, erev = hamming_golden()
+    n = len(a)
+    s, f, r = np.zeros(n, np.uint8), np.zeros(n, np.uint16), np.zeros(n, np.uint16)
+    rc = lib().mtb_hamming(0, a.ctypes.data, b.ctypes.data, n, s.ctypes.data, f.ctypes.data, r.ctypes.data)
+    assert rc == 0, lib().mtb_last_error().decode()
+    assert np.array_equal(s, esum)
+    assert np.array_equal(f, efwd)
+    assert np.array_equal(r, erev)
 
 
 def test_open_rejects_out_of_scope_params(tmp_path):

@@ -14,7 +14,12 @@ from tests import oracle_ctypes as oc
 
 
 @pytest.mark.gpu
-def test_open_from_files_phases_and_parity(make_db):
+@pytest.mark.parametrize("chunk", [None, "999", "65536"])
+def test_open_from_files_phases_and_parity(make_db, monkeypatch, chunk):
+    """chunk: diffIdx decoded in chunks of that many words (MTB_DECODE_CHUNK_WORDS; the default
+    is 2^30, one chunk here): k-mers cut by a chunk's end continue in the next, values carry over."""
+    if chunk:
+        monkeypatch.setenv("MTB_DECODE_CHUNK_WORDS", chunk)
     db_dir, taxo, gen = make_db("fmt2")
     r = synth.make_reads(gen, 700, paired=True, seed=81)
     par = LocalParameters(seqMode=2)
@@ -33,14 +38,21 @@ def test_open_from_files_phases_and_parity(make_db):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("damage", ["info_short", "diff_mid_kmer"])
-def test_open_rejects_inconsistent_files(make_db, tmp_path, damage):
+@pytest.mark.parametrize("chunk", [None, "1000"])
+@pytest.mark.parametrize("damage", ["info_short", "info_long", "diff_mid_kmer"])
+def test_open_rejects_inconsistent_files(make_db, tmp_path, monkeypatch, damage, chunk):
+    if chunk:
+        monkeypatch.setenv("MTB_DECODE_CHUNK_WORDS", chunk)
     db_dir, _, _ = make_db("fmt2")
     d = str(tmp_path / "db")
     shutil.copytree(db_dir, d)
     if damage == "info_short":
         info = np.fromfile(os.path.join(d, "info"), np.uint32)
         info[:-1].tofile(os.path.join(d, "info"))
+        msg = "k-mer count"
+    elif damage == "info_long":
+        info = np.fromfile(os.path.join(d, "info"), np.uint32)
+        np.concatenate([info, info[-1:]]).tofile(os.path.join(d, "info"))
         msg = "k-mer count"
     else:
         diff = np.fromfile(os.path.join(d, "diffIdx"), np.uint16)

@@ -31,6 +31,33 @@ def test_oracle_tables_pinned_to_reference_genetic_code():
     assert list(at) == g["atcg"] and list(rc) == g["iRCT"]
 
 
+def hamming_golden():
+    """tests/golden/hamming_tables.json: the reference's hammingLookup / HAMMING_LUT0..7 parsed out of
+    KmerMatcher.h:66-158 and its GET_3_BITS compiled in place (make_ref_tables.py), with the sums and
+    Hamming words its getHammingDistanceSum / getHammings / getHammings_reverse give on 2,560 pairs."""
+    g = json.loads((ROOT / "tests" / "golden" / "hamming_tables.json").read_text())
+    v = g["vectors"]
+    a = np.array([int(x) for x in v["a"]], np.uint64)
+    b = np.array([int(x) for x in v["b"]], np.uint64)
+    return g, a, b, np.array(v["sum"], np.uint8), np.array(v["fwd"], np.uint16), np.array(v["rev"], np.uint16)
+
+
+def test_oracle_hamming_tables_pinned_to_reference():
+    g, a, b, esum, efwd, erev = hamming_golden()
+    assert g["GET_3_BITS"] == [x & 7 for x in range(512)]  # the macro the functions index with
+    look = np.zeros(64, np.uint8)
+    lut = np.zeros(512, np.uint16)
+    oc.lib().orc_hamming_tables(look.ctypes.data, lut.ctypes.data)
+    assert look.reshape(8, 8).tolist() == g["hammingLookup"]
+    # every field k of every (query codon, target codon): the oracle's codonField, placed at its
+    # 2 bits, is the reference's HAMMING_LUTk entry (8 x 8 x 8 cases, LUT7 rows 4-5 included)
+    assert lut.reshape(8, 64).tolist() == g["HAMMING_LUT"]
+    n = len(a)
+    s, f, r = np.zeros(n, np.uint8), np.zeros(n, np.uint16), np.zeros(n, np.uint16)
+    oc.lib().orc_hamming(a.ctypes.data, b.ctypes.data, n, s.ctypes.data, f.ctypes.data, r.ctypes.data)
+    assert np.array_equal(s, esum) and np.array_equal(f, efwd) and np.array_equal(r, erev)
+
+
 @pytest.mark.parametrize("fmt,syncmer,smer", [(2, 0, 5), (2, 1, 5), (2, 1, 4), (1, 0, 5)])
 @pytest.mark.parametrize("paired", [True, False])
 def test_oracle_scanners_vs_closed_form(fmt, syncmer, smer, paired):

@@ -294,14 +294,17 @@ def test_classify_two_ranks(make_db, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("db_name,parts,cap", [("fmt2", 2, False), ("fmt2", 3, False), ("fmt1", 2, False),
-                                               ("fmt2_syncmer", 3, False), ("fmt2", 2, True)])
-def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap):
+@pytest.mark.parametrize("db_name,parts,cap,batch", [("fmt2", 2, False, 700), ("fmt2", 3, False, 700),
+                                                     ("fmt1", 2, False, 700), ("fmt2_syncmer", 3, False, 700),
+                                                     ("fmt2", 2, True, 700), ("fmt2", 3, False, 37)])
+def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap, batch):
     """mtb_start_classify_partitioned (SURVEY §8(e), config 5 natively): one context per DB part (all
     on cuda:0 here), every batch matched by each part, the segments handed to the owners of their
     reads and scored there; the TSV and report are byte-identical to the one-context run over the
     whole DB, and its classifications are the oracle's. cap: one part's workspace capped so its
-    pieces halve (the whole group splits the batch)."""
+    pieces halve (the whole group splits the batch). batch 37: ~60 small batches through the
+    workers' per-batch barriers (worker 0 must not refill the shared pieces before every part has
+    left the last batch's loop)."""
     from metabuli_work_amd import synth
     from metabuli_work_amd.classifier import Classifier, LocalParameters
 
@@ -329,7 +332,7 @@ def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap):
             clfs[1].set_workspace_cap((small + big) // 2)
         with pytest.raises(MtbError, match="one context per DB part"):  # every part must be there
             clfs[0].startClassify(part, peers=[], partitioned=True)
-        assert clfs[0].startClassify(part, reads_per_batch=700, report_tsv=repp, peers=clfs[1:],
+        assert clfs[0].startClassify(part, reads_per_batch=batch, report_tsv=repp, peers=clfs[1:],
                                      partitioned=True) == r.n
         assert (clfs[0].last_run["split_batches"] > 0) == cap
         with pytest.raises(MtbError, match="range-partitioned"):  # parts are refused by the replicated entry

@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 from metabuli_work_amd import synth
-from metabuli_work_amd.classifier import Classifier, LocalParameters
+from metabuli_work_amd._abi import RESULT_DTYPE, TAXCNT_DTYPE
+from metabuli_work_amd.classifier import BatchResult, Classifier, LocalParameters
 from tests import oracle_ctypes as oc
 
 
@@ -104,3 +105,54 @@ def test_release_workspace(make_db):
         b = clf.classify_batch(r.seq1, r.off1, r.seq2, r.off2)
         assert clf.workspace_bytes > 0
         _same(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frac", [0.6, 0.3])
+def test_device_resident_batch_split_on_retry(make_db, frac):
+    """classify_batch(fetch=False) — the bench's device-resident path, inputs and results in HBM — on
+    a capped context: the batch is classified in halves (split again where needed) and the halves'
+    result records and taxID:count lists assembled on the device, so copy_results / copy_taxcnt /
+    n_taxcnt / last_counts read one batch equal to the uncapped run and to the oracle; release of the
+    workspace afterwards leaves no stale batch behind (the getters see an empty one)."""
+    import torch
+
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 1500, paired=True, seed=64, short_frac=0.03)
+    par = LocalParameters(seqMode=2)
+    par.load_db_parameters(db_dir)
+    dev = torch.device("cuda", 0)
+    s1, o1 = torch.from_numpy(r.seq1).to(dev), torch.from_numpy(r.off1.astype(np.uint64).view(np.int64)).to(dev)
+    s2, o2 = torch.from_numpy(r.seq2).to(dev), torch.from_numpy(r.off2.astype(np.uint64).view(np.int64)).to(dev)
+
+    def run(clf):
+        clf.classify_batch(s1, o1, s2, o2, device_input=True, fetch=False)
+        rec = torch.zeros((r.n, 32), dtype=torch.uint8, device=dev)
+        clf.copy_results(rec.data_ptr(), on_device=True)
+        pool = torch.zeros((max(clf.n_taxcnt(), 1), 8), dtype=torch.uint8, device=dev)
+        nt = clf.copy_taxcnt(pool.data_ptr(), on_device=True)
+        torch.cuda.synchronize()
+        res = rec.cpu().numpy().view(RESULT_DTYPE).reshape(-1)
+        tc = pool[:nt].cpu().numpy().view(TAXCNT_DTYPE).reshape(-1)
+        return BatchResult(res, tc, *clf.last_counts(), None)
+
+    with Classifier(par, db_dir=db_dir) as full:
+        ref = run(full)
+        ws = full.workspace_bytes
+    with Classifier(par, db_dir=db_dir) as capped:
+        capped.set_workspace_cap(int(ws * frac))
+        got = run(capped)
+        assert capped.workspace_bytes <= int(ws * frac)
+        _same(got, ref)
+        assert got.query_kmers == ref.query_kmers and got.matches == ref.matches
+        # a later batch that fits serves the context's own buffers again
+        small = capped.classify_batch(r.seq1, r.off1[:101], r.seq2, r.off2[:101])
+        assert np.array_equal(small.results["classification"], ref.results["classification"][:100])
+        capped.release_workspace()
+        assert capped.n_taxcnt() == 0 and capped.last_counts() == (0, 0)
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    assert np.array_equal(got.results["classification"], ores["classification"])
+    assert np.array_equal(got.results["score"].view(np.uint32), ores["score"].view(np.uint32))
+    assert np.array_equal(got.taxcnt, otc)
