@@ -16,6 +16,7 @@ Prints one JSON line on rank 0.
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -285,6 +286,8 @@ def main():
                     help="config 5 on one GPU: DB parts, each timed in turn (with N >= 4 GPUs: one part per rank)")
     ap.add_argument("--c5-sample", type=int, default=24_000, help="config 5: read pairs of the oracle parity sample")
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
+    ap.add_argument("--cold-gtdb", type=int, default=1,
+                    help="config 3: open the GTDB-scale DB from host diffIdx/info/split (mtb_open_host) and time it")
     ap.add_argument("--cold-pairs", type=int, default=10_000_000,
                     help="cold one-shot line: read pairs of the file classified by a freshly opened context (0 = off)")
     ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r04", "bench_detail.json"),
@@ -368,6 +371,39 @@ def main():
 LINE_CAP = 8000  # the driver keeps only the tail of stdout (~15.5 KB): the one JSON line stays well under it
 
 
+def count_label(x) -> str:
+    """A count as the labels print it: 10000000 -> "10M", 3333334 -> "3.33M", 200000 -> "200k",
+    12.0e9 -> "12.0G" (k-mers keep one decimal in G)."""
+    x = float(x)
+    if x >= 1e9:
+        return f"{x / 1e9:.1f}G"
+    if x >= 1e6:
+        v = x / 1e6
+        return f"{v:.0f}M" if abs(v - round(v)) < 5e-3 else f"{v:.3g}M"
+    if x >= 1e3:
+        v = x / 1e3
+        return f"{v:.0f}k" if abs(v - round(v)) < 5e-3 else f"{v:.3g}k"
+    return f"{int(x)}"
+
+
+def hbm_note(nbytes) -> str:
+    """Whether a DB's resident bytes fit one MI355X (288 GB of HBM)."""
+    return "more than one GPU's 288 GB HBM" if nbytes > 288e9 else "fits one GPU's 288 GB HBM"
+
+
+def config3_label(pairs, read_len, db_kmers, species, batch, what="config 3") -> str:
+    """config.workload of a config-3 line, from the run's own parameters."""
+    return (f"{what}: {count_label(pairs)} x {read_len}bp paired reads per GPU vs a GTDB-scale DB "
+            f"({count_label(db_kmers)} k-mers, {species:,}-species skeleton taxonomy), format 2, DB + reads "
+            f"resident in HBM, {batch}-pair batches")
+
+
+def config5_label(pairs, read_len, db_kmers, parts) -> str:
+    return (f"config 5: {count_label(pairs)} x {read_len}bp read pairs per step vs a {count_label(db_kmers)}-k-mer "
+            f"GTDB-shaped DB ({db_kmers * 12 / 1e9:.0f} GB of records: {hbm_note(db_kmers * 12)}), range-partitioned "
+            f"into {parts} AA-aligned parts")
+
+
 def _pick(d, keys):
     return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
 
@@ -444,7 +480,10 @@ def compact_line(out, detail_path):
     c5 = out.get("config5")
     if isinstance(c5, dict):
         line["config5"] = _pick(c5, ("value", "unit", "ms_per_step", "parity_sample", "scaling"))
-        line["config5"]["workload"] = "10M pairs vs a 35G-k-mer DB in 8 AA-aligned parts (detail: config5)"
+        cfg = c5.get("config", {})
+        if "read_pairs" in cfg and "db_kmers" in cfg and "parts" in cfg:
+            line["config5"]["workload"] = (f"{count_label(cfg['read_pairs'])} pairs vs a {count_label(cfg['db_kmers'])}"
+                                           f"-k-mer DB in {cfg['parts']} AA-aligned parts (detail: config5)")
     line["detail"] = os.path.relpath(detail_path, ROOT) if detail_path else None
     # never overflow the driver's capture: drop the summaries, least important first
     for k in ("end_to_end", "em", "random_roofline", "pipeline_roofline", "kernel_ms", "variants", "config5",
@@ -571,8 +610,9 @@ def run_config2(args, world, rank, local, dev):
 
     out = {
         "value": round(value, 1), "ms_per_step": round(ms_per_step, 3),
-        "config": {"workload": "config 2: 1M x 150bp paired reads vs RefSeq-viral-sized DB (~10 GB), "
-                               "format 2, DB + reads resident in HBM",
+        "config": {"workload": f"config 2: {count_label(n)} x 150bp paired reads vs a RefSeq-viral-sized DB "
+                               f"({count_label(D)} k-mers, {db_bytes / 1e9:.1f} GB of diffIdx + info), format 2, "
+                               "DB + reads resident in HBM",
                    "read_pairs_per_gpu": n, "read_len": 150, "db_kmers": D,
                    "db_bytes": db_bytes, "query_kmers": Q, "matches": M,
                    "parallelism": f"reads sharded, DB replicated x{world}"},
@@ -646,6 +686,40 @@ def run_cold(args, hdb, par, lp, s1, s2, n, check=None):
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def run_cold_gtdb(args, host, odb, lp, local, reads, ores, otc):
+    """The GTDB-scale DB opened as the reference opens its DB on every run (KmerMatcher.cpp:127-138,
+    212-265; Classifier.cpp:6-32): from diffIdx / info / split — here the host copy the oracle holds
+    (encode_into_oracle: the resident DB re-encoded, 12G k-mers, ~108 GB) — through mtb_open_host
+    into a fresh context, after the resident DB was freed. open_phases_s has mtb_open_phases: the
+    uploads (read_s), the chunked K3 decode into records (decode_s), the AA directory, the probe
+    lines, the run index and the taxonomy. A parity check follows: the oracle sample's reads through
+    the new context against the oracle's results."""
+    diff, info, split = odb.arrays
+    h = host.c_struct()
+    h.diff_idx, h.n_diff_idx = diff.ctypes.data, len(diff)
+    h.info, h.n_info = info.ctypes.data, len(info)
+    h.split, h.n_split = split.ctypes.data, len(split) // 3
+    t0 = time.perf_counter()
+    clf = Classifier(lp, db_host=h, device=local)
+    open_s = time.perf_counter() - t0
+    try:
+        phases = clf.open_phases()
+        S = min(len(reads.off1) - 1, 200_000)
+        gb = clf.classify_batch(reads.seq1, reads.off1[:S + 1], reads.seq2, reads.off2[:S + 1])
+        ok = bool(np.array_equal(gb.results["classification"], ores["classification"][:S])
+                  and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32)[:S]))
+        n = clf.db_kmers
+    finally:
+        clf.close()
+    out = {"open_s": round(open_s, 3), "open_phases_s": phases, "db_kmers": n,
+           "db_bytes": int(diff.nbytes + info.nbytes), "diff_idx_words": len(diff),
+           "parity_sample_pairs": S, "parity_sample": ok,
+           "what": f"the config-3 DB ({n} k-mers) as diffIdx/info/split in host memory, mtb_open_host into a "
+                   "fresh context (the resident copy freed first): what a CLI run pays before its first batch"}
+    log(0, f"[bench] GTDB-scale cold open: {open_s:.2f}s {phases}, parity {ok}")
+    return out
 
 
 def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, db_name, db_kmers, workload):
@@ -779,6 +853,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     s1, o1, s2, o2 = got.pop("reads")
     lp = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1, syncmer=vr["syncmer"], smerLen=vr["smer_len"])
     clf = Classifier(lp, db_resident=rdb, device=local)
+    db_n, db_n_true = rdb.n, rdb.n_true  # (the resident DB may be freed before the line is built)
     log(rank, f"[bench] GTDB-scale context open ({time.time() - t0:.1f}s)")
     L = 150
     spans = [(a, min(N, a + B)) for a in range(0, N, B)]
@@ -920,15 +995,23 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         long_line = run_long_reads(args, lambda lpl: Classifier(lpl, db_resident=rdb, device=local), ls1, lo1, n50,
                                    world, rank, dev, odb, cores, "the GTDB-scale DB", rdb.n, "long")
         log(rank, f"[bench] config 3 long reads: {long_line['value']} reads/s")
+    cold_gtdb = None
+    if odb is not None and args.cold_gtdb:
+        # the resident DB goes first: the open builds its own records, probe lines and run index
+        host = rdb.host
+        clf = peers = None  # closed contexts still hold the resident records (Classifier._resident)
+        del rdb
+        gc.collect()
+        torch.cuda.empty_cache()
+        cold_gtdb = run_cold_gtdb(args, host, odb, lp, local, reads, ores, otc)
+        rdb = None
     if odb is not None:
         odb.close()
     out = {
         "value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "config": {"workload": "config 3: 10M x 150bp paired reads per GPU vs a GTDB-scale DB (~12G k-mers, "
-                               "129,671-species skeleton taxonomy), format 2, DB + reads resident in HBM, "
-                               f"{B}-pair batches",
-                   "read_pairs_per_gpu": N, "batch_pairs": B, "read_len": L, "db_kmers": rdb.n,
-                   "db_true_signal_kmers": rdb.n_true, "db_resident_bytes": rdb.n * 12,
+        "config": {"workload": config3_label(N, L, db_n, args.gtdb_species, B, tag),
+                   "read_pairs_per_gpu": N, "batch_pairs": B, "read_len": L, "db_kmers": db_n,
+                   "db_true_signal_kmers": db_n_true, "db_resident_bytes": db_n * 12,
                    "query_kmers_per_batch": int(Qb), "matches_per_batch": int(Mb),
                    "parallelism": f"reads sharded, DB replicated x{world}"},
         "roofline": roofline,
@@ -942,6 +1025,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         "end_to_end": e2e,
         "em": em_line,
         "pipeline_roofline": pipe,
+        "cold_run_gtdb": cold_gtdb,
     }
     if variant:
         out = {"variant": variant, "what": vr["what"], "value": out["value"], "unit": "reads/s",
@@ -1157,9 +1241,7 @@ def run_config5(args, world, rank, local, dev):
         ext, _, _ = oc.extract(lp.to_c(), sample)
         sub = SubDb.of_kmers(rc.host, ext, dev)
         del ext
-    common = {"workload": f"config 5: {N} x 150bp read pairs per step vs a {D / 1e9:.1f}G-k-mer GTDB-shaped DB "
-                          f"({D * 12 / 1e9:.0f} GB of records: more than one GPU's 288 GB HBM), range-partitioned "
-                          f"into {P} AA-aligned parts",
+    common = {"workload": config5_label(N, 150, D, P),
               "read_pairs": N, "batch_pairs": B, "db_kmers": D, "db_resident_bytes": D * 12, "parts": P,
               "part_kmers": part_kmers}
 

@@ -523,4 +523,5 @@ def encode_into_oracle(rdb: ResidentDb, oracle_cls, split_num: int = 4096, chunk
         split[3 * k] = np.uint64(int(to_native_fmt2(rdb.values(gv, gv + 1)).item()) & ((1 << 64) - 1))
         split[3 * k + 1] = gpos[gv + 1]
         split[3 * k + 2] = gv + 1
+    db.arrays = (diff, info, split)  # the host arrays, for mtb_open_host (bench: the GTDB-scale cold open)
     return db

@@ -68,3 +68,21 @@ def test_variant_batches():
     assert b.variant_batch(A, "syncmer") == b.variant_batch(A, "conserved") == 3_333_334
     A.variant_batch = 1_000_000
     assert b.variant_batch(A, "syncmer") == 1_000_000
+
+
+def test_workload_labels_follow_parameters():
+    """config.workload is built from the run's own numbers: a 1M-pair, 2G-k-mer
+    rehearsal can no longer call itself "config 3: 10M ... ~12G k-mers", nor a 48-GB DB larger than
+    one GPU's HBM."""
+    import re
+
+    b = _bench()
+    assert [b.count_label(x) for x in (10_000_000, 3_333_334, 200_000, 12.0e9, 1_000_000, 125_000)] == \
+        ["10M", "3.33M", "200k", "12.0G", "1M", "125k"]
+    for pairs, kmers in ((10_000_000, 12.02e9), (1_000_000, 2.0e9), (250_000, 9.8e8)):
+        lab = b.config3_label(pairs, 150, int(kmers), 129_671, 500_000)
+        m = re.match(r"config 3: (\S+) x 150bp .*\((\S+) k-mers, 129,671-species", lab)
+        assert m and m.group(1) == b.count_label(pairs) and m.group(2) == b.count_label(int(kmers)), lab
+    assert "more than one GPU" in b.config5_label(10_000_000, 150, int(35e9), 8)
+    small = b.config5_label(1_000_000, 150, int(4e9), 4)  # 48 GB of records
+    assert "fits one GPU" in small and "1M x 150bp" in small and "4.0G-k-mer" in small
