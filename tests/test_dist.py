@@ -1,4 +1,5 @@
-"""N>1 path on CPU: world_size-2 gloo processes shard the reads and all-gather the result records."""
+"""N>1 path on CPU: world_size-2 and -8 gloo processes shard the reads and all-gather the result records
+(world 8 as the 8-GPU node runs it, with ranks that hold no reads)."""
 import ctypes
 import os
 import socket
@@ -40,10 +41,11 @@ def _worker(rank, world, port, seq, off, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_shard_and_gather_gloo(world):
+@pytest.mark.parametrize("world,n_reads", [(2, 301), (8, 301), (8, 5)])
+def test_shard_and_gather_gloo(world, n_reads):
+    """(8, 5): three ranks shard no reads and still take part in the gather."""
     rng = np.random.default_rng(0)
-    lens = rng.integers(50, 5000, size=301)
+    lens = rng.integers(50, 5000, size=n_reads)
     off = np.zeros(len(lens) + 1, np.uint64)
     off[1:] = np.cumsum(lens)
     seq = rng.integers(65, 90, size=int(off[-1])).astype(np.uint8)
@@ -96,10 +98,11 @@ def _results_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rng = np.random.default_rng(100 + rank)
-    # two batches per rank, appended to one step pool as the bench's multi-GPU step does
+    # two batches per rank, appended to one step pool as the bench's multi-GPU step does; with 8
+    # ranks, ranks 5 and 6 classify no reads at all (an empty owner range)
     pool = torch.zeros((64, 8), dtype=torch.uint8)
     recs, used, want = [], 0, []
-    for n in (5 + rank, 0 if rank else 7):
+    for n in ((0, 0) if rank in (5, 6) else (5 + rank, 0 if rank else 7)):
         res, tc = _fake_batch(rng, n)
         want += _lists(res, tc)
         r = torch.from_numpy(res.view(np.uint8).reshape(-1, 32).copy())
@@ -112,10 +115,10 @@ def _results_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gather_results_rebases_taxcnt_gloo():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gather_results_rebases_taxcnt_gloo(world):
     """C1 with the taxID:count lists: rank 0 ends up with every rank's (classification, list) in
-    rank order, offsets pointing into one gathered pool."""
-    world = 2
+    rank order, offsets pointing into one gathered pool (world 8: two ranks with no reads)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -130,7 +133,7 @@ def test_gather_results_rebases_taxcnt_gloo():
     rec, tc = next(i for i in items if not isinstance(i[0], str))
     res = rec.reshape(-1).view(RESULT_DTYPE)
     tcs = tc.reshape(-1).view(TAXCNT_DTYPE)
-    assert _lists(res, tcs) == want[0] + want[1]
+    assert _lists(res, tcs) == sum((want[r] for r in range(world)), [])
     assert int(res["taxcnt_len"].sum()) == len(tcs)
 
 
@@ -157,7 +160,8 @@ def _bench_gather_worker(rank, world, port, q):
     import bench
 
     rng = np.random.default_rng(7 + rank)
-    sizes = [6, 3 + rank, 5]
+    # world 8: rank 3 holds no reads (three empty batches), the last batch is shorter than the rest
+    sizes = [0, 0, 0] if rank == 3 else [6, 3 + rank, 2]
     c1 = bench.ResultGather(torch.device("cpu"), 1)
     c1.pool = c1.pool[:2]  # a tiny pool: the adds must grow it
     rec = torch.empty((sum(sizes), 32), dtype=torch.uint8)
@@ -173,10 +177,10 @@ def _bench_gather_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_bench_result_gather_gloo():
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_result_gather_gloo(world):
     """bench.py's multi-GPU step (ResultGather: per-batch D2D copies + rebasing, one C1 gather)
     gives every rank all reads' (classification, taxID:count list) in rank order."""
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -187,7 +191,7 @@ def test_bench_result_gather_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = items[0][2] + items[1][2]
+    want = sum((items[r][2] for r in range(world)), [])
     for r in range(world):
         res = items[r][0].reshape(-1).view(RESULT_DTYPE)
         assert _lists(res, items[r][1].reshape(-1).view(TAXCNT_DTYPE)) == want
@@ -226,11 +230,12 @@ def _batch_shard_worker(rank, world, port, sizes, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_batches_sharded_gloo(world):
     """Batch-index sharding (dist.classify_batches_sharded): rank r materialises only batches
-    r, r + N, ...; the gathered records come back in batch order with their taxID:count lists."""
-    sizes = [4, 0, 7, 3, 5, 1, 6]
+    r, r + N, ...; the gathered records come back in batch order with their taxID:count lists.
+    World 8 over 7 batches: rank 7 takes none; the last batch is shorter than the rest."""
+    sizes = [4, 0, 7, 3, 5, 6, 1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -106,8 +106,10 @@ def _a2a_worker(rank, world, port, n, q):
     dist.destroy_process_group()
 
 
-def test_exchange_matches_gloo():
-    world, n = 2, 257
+@pytest.mark.parametrize("world,n", [(2, 257), (8, 257), (8, 5)])
+def test_exchange_matches_gloo(world, n):
+    """(8, 5): three owners hold no reads — their receive layout is empty, every rank still sends
+    them a zero-length chunk."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
