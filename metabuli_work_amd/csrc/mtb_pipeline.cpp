@@ -527,6 +527,67 @@ struct Slot {
     std::vector<std::unique_ptr<PeerIn>> peers;  // range-partitioned run: the batch on contexts 1..P-1
 };
 
+// Device-to-device copies of a range-partitioned run (the batch to the further parts' devices, the
+// owners' match segments): hipMemcpyPeerAsync over xGMI where the two devices have peer access, else
+// staged through a pinned host buffer, chunk by chunk and synchronously (a node without peer access
+// between some pair still runs; MTB_PEER_COPY=host forces the staging for every pair, same device
+// included: the GPU tests exercise it on cuda:0). Decided once per run, logged once per pair.
+struct PeerLinks {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<char> direct;  // [a * n + b]: a copy from context b's device to context a's is a peer copy
+    bool forced = false;
+    void init(mtb_ctx* const* ctxs, int nCtx) {
+        n = nCtx;
+        dev.resize(n);
+        for (int a = 0; a < n; a++) dev[a] = mtb_ctx_device(ctxs[a]);
+        const char* e = getenv("MTB_PEER_COPY");
+        forced = e && !strcmp(e, "host");
+        direct.assign((size_t)n * n, 1);
+        for (int a = 0; a < n; a++)
+            for (int b = 0; b < n; b++) {
+                if (forced) { direct[a * n + b] = 0; continue; }
+                if (dev[a] == dev[b]) continue;  // a device copy on one GPU
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, dev[a], dev[b]) != hipSuccess) can = 0;
+                if (can) {
+                    hipSetDevice(dev[a]);
+                    const hipError_t r = hipDeviceEnablePeerAccess(dev[b], 0);
+                    if (r != hipSuccess && r != hipErrorPeerAccessAlreadyEnabled) can = 0;
+                    (void)hipGetLastError();
+                }
+                direct[a * n + b] = (char)can;
+                if (!can)
+                    fprintf(stderr, "[mtb] no peer access from GPU %d to GPU %d: their copies are staged through host "
+                                    "memory\n", dev[a], dev[b]);
+            }
+        if (forced) fprintf(stderr, "[mtb] MTB_PEER_COPY=host: every device-to-device copy staged through host memory\n");
+    }
+    // bytes from context b's device memory to context a's; st: a stream of a's device (peer copies
+    // are queued on it; the staged path returns with the copy done)
+    bool copy(int a, void* dst, int b, const void* src, size_t bytes, hipStream_t st) const {
+        if (!bytes) return true;
+        if (direct[a * n + b]) return hipMemcpyPeerAsync(dst, dev[a], src, dev[b], bytes, st) == hipSuccess;
+        constexpr size_t kBounce = 64u << 20;
+        thread_local char* bounce = nullptr;  // one pinned buffer per copying thread, kept for the process
+        if (!bounce && hipHostMalloc((void**)&bounce, kBounce, hipHostMallocDefault) != hipSuccess) {
+            bounce = nullptr;
+            return false;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) return false;  // earlier work on st first
+        for (size_t off = 0; off < bytes; off += kBounce) {
+            const size_t len = std::min(kBounce, bytes - off);
+            if (hipSetDevice(dev[b]) != hipSuccess ||
+                hipMemcpy(bounce, (const char*)src + off, len, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipSetDevice(dev[a]) != hipSuccess ||
+                hipMemcpyAsync((char*)dst + off, bounce, len, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return false;
+        }
+        return true;
+    }
+};
+
 // Threads of a range-partitioned run meeting once per step of a batch (C++17: no std::barrier).
 struct Barrier {
     std::mutex mu;
@@ -849,6 +910,8 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
     // per context: kSlots slots (kept in the context between runs), a copy stream on its device,
     // free and ready queues
     std::vector<Slot*> slotMem;
+    PeerLinks links;  // range-partitioned run: peer copies or host-staged ones, per pair of contexts
+    if (partitioned) links.init(ctxs, nCtx);
     std::vector<hipStream_t> up(nCtx, nullptr);
     std::vector<std::unique_ptr<BoundedQueue<Slot*>>> freeQ, readyQ;
     for (int d = 0; d < nCtx; d++) {
@@ -1100,20 +1163,20 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                         s->peers.push_back(std::move(pi));
                     }
                 }
-                for (int p = 1; p < nCtx && ok; p++) {  // device to device (xGMI between GPUs)
+                for (int p = 1; p < nCtx && ok; p++) {  // device to device (xGMI between GPUs, or host-staged)
                     PeerIn& pi = *s->peers[p - 1];
                     std::unique_lock<std::mutex> pl(*growMu.at(pi.device), std::defer_lock);
                     if (pi.dseq1.cap < b1 + 1 || pi.doff1.cap < on || (paired && (pi.dseq2.cap < b2 + 1 || pi.doff2.cap < on)))
                         pl.lock();
-                    ok = hipSetDevice(pi.device) == hipSuccess && pi.dseq1.ensure(b1 + 1) == hipSuccess &&
+                    if (!links.direct[p * nCtx + 0]) ok = hipEventSynchronize(s->uploaded) == hipSuccess;  // staged: source ready
+                    ok = ok && hipSetDevice(pi.device) == hipSuccess && pi.dseq1.ensure(b1 + 1) == hipSuccess &&
                          pi.doff1.ensure(on) == hipSuccess && hipStreamWaitEvent(up[p], s->uploaded, 0) == hipSuccess &&
-                         hipMemcpyPeerAsync(pi.dseq1.p, pi.device, s->dseq1.p, dev, b1, up[p]) == hipSuccess &&
-                         hipMemcpyPeerAsync(pi.doff1.p, pi.device, s->doff1.p, dev, on, up[p]) == hipSuccess;
+                         links.copy(p, pi.dseq1.p, 0, s->dseq1.p, b1, up[p]) && links.copy(p, pi.doff1.p, 0, s->doff1.p, on, up[p]);
                     if (ok && paired)
-                        ok = pi.dseq2.ensure(b2 + 1) == hipSuccess && pi.doff2.ensure(on) == hipSuccess &&
-                             hipMemcpyPeerAsync(pi.dseq2.p, pi.device, s->dseq2.p, dev, b2, up[p]) == hipSuccess &&
-                             hipMemcpyPeerAsync(pi.doff2.p, pi.device, s->doff2.p, dev, on, up[p]) == hipSuccess;
-                    ok = ok && hipEventRecord(pi.uploaded, up[p]) == hipSuccess;
+                        ok = hipSetDevice(pi.device) == hipSuccess && pi.dseq2.ensure(b2 + 1) == hipSuccess &&
+                             pi.doff2.ensure(on) == hipSuccess && links.copy(p, pi.dseq2.p, 0, s->dseq2.p, b2, up[p]) &&
+                             links.copy(p, pi.doff2.p, 0, s->doff2.p, on, up[p]);
+                    ok = ok && hipSetDevice(pi.device) == hipSuccess && hipEventRecord(pi.uploaded, up[p]) == hipSuccess;
                 }
             }
             if (!ok) {
@@ -1146,13 +1209,6 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
     if (partitioned) {
         for (int p = 0; p < nCtx; p++) partQ.emplace_back(new BoundedQueue<Slot*>(kSlots));
         pb.reset(new PartBatch(nCtx));
-        for (int a = 0; a < nCtx; a++)  // peer copies over xGMI where the devices differ
-            for (int b = 0; b < nCtx; b++) {
-                const int da = mtb_ctx_device(ctxs[a]), db = mtb_ctx_device(ctxs[b]);
-                if (da == db) continue;
-                hipSetDevice(da);
-                if (hipDeviceEnablePeerAccess(db, 0) != hipSuccess) (void)hipGetLastError();
-            }
     }
     auto partition_worker = [&](int p) {
         mtb_ctx* c = ctxs[p];
@@ -1268,19 +1324,15 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                 }
                 uint64_t at = 0;
                 for (int q = 0; q < P && rc == MTB_OK && no; q++) {
-                    const int dq = mtb_ctx_device(ctxs[q]);
                     const uint64_t nm = B.mOff[q][b] - B.mOff[q][a];
-                    if (nm && hipMemcpyPeerAsync((mtb_match*)os.m.p + at, dev, B.m[q] + B.mOff[q][a], dq,
-                                                 sizeof(mtb_match) * nm, os.st) != hipSuccess)
-                        rc = MTB_ERR_HIP;
-                    if (hipMemcpyPeerAsync((uint32_t*)os.cnt.p + (size_t)q * no, dev, B.cnt[q] + a, dq,
-                                           sizeof(uint32_t) * no, os.st) != hipSuccess)
+                    if (!links.copy(p, (mtb_match*)os.m.p + at, q, B.m[q] + B.mOff[q][a], sizeof(mtb_match) * nm, os.st) ||
+                        !links.copy(p, (uint32_t*)os.cnt.p + (size_t)q * no, q, B.cnt[q] + a, sizeof(uint32_t) * no, os.st))
                         rc = MTB_ERR_HIP;
                     at += nm;
                 }
                 if (rc == MTB_OK && no &&
-                    (hipMemcpyPeerAsync(os.ql.p, dev, B.ql[p] + a, dev, sizeof(uint32_t) * no, os.st) != hipSuccess ||
-                     hipStreamSynchronize(os.st) != hipSuccess))
+                    (!links.copy(p, os.ql.p, p, B.ql[p] + a, sizeof(uint32_t) * no, os.st) ||
+                     hipSetDevice(dev) != hipSuccess || hipStreamSynchronize(os.st) != hipSuccess))
                     rc = MTB_ERR_HIP;
                 B.rc[p] = rc;
                 if (rc != MTB_OK) B.err[p] = "range-partitioned match hand-over failed";

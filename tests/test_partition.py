@@ -296,17 +296,22 @@ def test_classify_two_ranks(make_db, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("db_name,parts,cap,batch", [("fmt2", 2, False, 700), ("fmt2", 3, False, 700),
-                                                     ("fmt1", 2, False, 700), ("fmt2_syncmer", 3, False, 700),
-                                                     ("fmt2", 2, True, 700), ("fmt2", 3, False, 37)])
-def test_start_classify_partitioned(make_db, tmp_path, db_name, parts, cap, batch):
+@pytest.mark.parametrize("db_name,parts,cap,batch,peer", [("fmt2", 2, False, 700, ""), ("fmt2", 3, False, 700, ""),
+                                                          ("fmt1", 2, False, 700, ""), ("fmt2_syncmer", 3, False, 700, ""),
+                                                          ("fmt2", 2, True, 700, ""), ("fmt2", 3, False, 37, ""),
+                                                          ("fmt2", 3, False, 700, "host"), ("fmt2", 2, True, 300, "host")])
+def test_start_classify_partitioned(make_db, tmp_path, monkeypatch, db_name, parts, cap, batch, peer):
     """mtb_start_classify_partitioned (SURVEY §8(e), config 5 natively): one context per DB part (all
     on cuda:0 here), every batch matched by each part, the segments handed to the owners of their
     reads and scored there; the TSV and report are byte-identical to the one-context run over the
     whole DB, and its classifications are the oracle's. cap: one part's workspace capped so its
     pieces halve (the whole group splits the batch). batch 37: ~60 small batches through the
     workers' per-batch barriers (worker 0 must not refill the shared pieces before every part has
-    left the last batch's loop)."""
+    left the last batch's loop). peer "host": MTB_PEER_COPY=host, every device-to-device copy (the
+    batch to the further parts, the segments to their owners) staged through pinned host memory, as on
+    a node where hipDeviceCanAccessPeer is false for a pair."""
+    if peer:
+        monkeypatch.setenv("MTB_PEER_COPY", peer)
     from metabuli_work_amd import synth
     from metabuli_work_amd.classifier import Classifier, LocalParameters
 
