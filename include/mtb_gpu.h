@@ -204,7 +204,10 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
  * on longer lines fall back), [13] matches the direct join spilled past their read's stretch,
  * [14] query k-mers whose DB run held more than 48 k-mers (scanned a wave each, k_match_long),
  * [15] fused-filter reruns (the batch's present windows outgrew the output sized from earlier batches),
- * [16] DB records the DB-sweep join read (MTB_JOIN=sweep: the tiles that held queries; 0 otherwise).
+ * [16] DB records the DB-sweep join read (MTB_JOIN=sweep: the tiles that held queries; 0 otherwise),
+ * [17] / [18] with MTB_DUP_STATS=1 (diagnostic pass after the sort): query k-mers whose AA rank /
+ * whole value repeats an earlier query's in their 256-query K4 block (the reference's same-AA /
+ * identical-query reuse, KmerMatcher.cpp:277-353; 0 otherwise).
  * Query k-mers = windows whose AA 8-mer the DB holds. Counts [5]..[9] are over the live matches. */
 int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):

@@ -269,7 +269,8 @@ class Classifier:
 
     STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
              "species_runs", "wave_runs", "wave_runs_emulated", "join_path", "live_matches", "gallop_queries",
-             "spilled_matches", "long_run_queries", "filter_reruns", "db_records_read"]
+             "spilled_matches", "long_run_queries", "filter_reruns", "db_records_read", "dup_aa_queries",
+             "dup_key_queries"]
 
     def stats(self) -> dict:
         """Work counts of the last batch (mtb_last_stats)."""

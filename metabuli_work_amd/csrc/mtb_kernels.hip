@@ -2017,6 +2017,44 @@ void launch_hamming_check(const uint64_t* a, const uint64_t* b, uint64_t n, uint
     if (n) k_hamming_check<<<stride_grid(n), 256, 0, s>>>(a, b, n, sum, fwd, rev, bad);
 }
 
+// MTB_DUP_STATS=1 (diagnostic): how much of the reference's identical-query and same-AA reuse
+// (KmerMatcher.cpp:277-353: a query equal to the previous one replays its matches; one with the
+// same AA part re-runs compareDna on the cached candidates) the join's blocks could exploit. Per
+// block of 256 sorted queries (K4's unstaged block): the keys bitonic-sorted in LDS, then out[0] +=
+// queries whose AA rank equals an earlier one's in the block (a run lookup another query of the
+// block already made), out[1] += queries whose whole key (AA + DNA) does (identical queries).
+__global__ void __launch_bounds__(256) k_dup_stats(const uint64_t* __restrict__ qkey, uint64_t Q,
+                                                   unsigned long long* __restrict__ out) {
+    __shared__ uint64_t sk[256];
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    sk[threadIdx.x] = q < Q ? qkey[q] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= 256; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t i = threadIdx.x, l = i ^ j;
+            if (l > i) {
+                const uint64_t a = sk[i], b = sk[l];
+                if (((i & k) == 0) == (a > b)) {
+                    sk[i] = b;
+                    sk[l] = a;
+                }
+            }
+            __syncthreads();
+        }
+    const uint32_t i = threadIdx.x;
+    const bool valid = sk[i] != ~0ull && i > 0;
+    const uint32_t aa = valid && (sk[i] >> 24) == (sk[i - 1] >> 24), same = valid && sk[i] == sk[i - 1];
+    const int nAa = __syncthreads_count(aa), nSame = __syncthreads_count(same);
+    if (threadIdx.x == 0) {
+        if (nAa) atomicAdd(&out[0], (unsigned long long)nAa);
+        if (nSame) atomicAdd(&out[1], (unsigned long long)nSame);
+    }
+}
+
+void launch_dup_stats(const uint64_t* qkey, uint64_t Q, unsigned long long* out, hipStream_t s) {
+    if (Q) k_dup_stats<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, Q, out);
+}
+
 uint64_t match_window_elems(uint64_t Q) { return 2 * ((Q + kMatchQ - 1) / kMatchQ); }
 
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const DbRec* db, uint64_t D, const AADir& dir,

@@ -288,6 +288,9 @@ void launch_match_transpose(const mtb_match* buf, const uint32_t* bufRank, uint6
                             const unsigned long long* total, const uint64_t* readOff, uint32_t nReads, mtb_match* out,
                             int* err, hipStream_t s);
 uint64_t match_window_elems(uint64_t Q);
+// MTB_DUP_STATS (diagnostic): out[0] += queries repeating an earlier query's AA rank in their 256-query K4
+// block, out[1] += queries repeating its whole key (u64 x 2, accumulated)
+void launch_dup_stats(const uint64_t* qkey, uint64_t Q, unsigned long long* out, hipStream_t s);
 // mtb_hamming's kernel (bad: u64 count of pairs where the row-cached and plain forms disagree)
 void launch_hamming_check(const uint64_t* a, const uint64_t* b, uint64_t n, uint8_t* sum, uint16_t* fwd, uint16_t* rev,
                           unsigned long long* bad, hipStream_t s);

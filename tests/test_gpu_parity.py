@@ -399,3 +399,36 @@ def test_spill_then_late_compaction(make_db, db_name, kind, late, monkeypatch):
         if kind == "paired":  # (long reads keep their matches within a quarter of their stretch)
             assert clf.stats()["spilled_matches"] > 0
         compare_results(br.results, br.taxcnt, ores, otc)
+
+
+@pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt1", "long")])
+def test_dup_stats_counter(make_db, db_name, kind, monkeypatch):
+    """MTB_DUP_STATS=1: the repeated AA ranks / whole values per 256-query K4 block (mtb_last_stats
+    [17] / [18]: the reference's same-AA and identical-query reuse, KmerMatcher.cpp:277-353, that a
+    block could share) equal a host count over the query k-mers in the order K4 consumed them; the
+    results are unchanged."""
+    monkeypatch.setenv("MTB_DUP_STATS", "1")
+    db_dir, taxo, gen = make_db(db_name)
+    par = _params(db_dir, SEQ_MODE[kind])
+    reads = _reads(gen, kind, 1500 if kind == "paired" else 120, seed=91)
+    # the same reads twice: identical queries in plenty
+    reads = synth.Reads(np.concatenate([reads.seq1, reads.seq1]),
+                        np.concatenate([reads.off1[:-1], reads.off1 + reads.off1[-1]]),
+                        None if reads.seq2 is None else np.concatenate([reads.seq2, reads.seq2]),
+                        None if reads.off2 is None else np.concatenate([reads.off2[:-1], reads.off2 + reads.off2[-1]]),
+                        np.concatenate([reads.origin, reads.origin]))
+    with Classifier(par, db_dir=db_dir) as clf:
+        br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2, keep_stages=True)
+        st = clf.stats()
+        q = clf.query_kmers()["value"]
+    aa, same = 0, 0
+    for b in range(0, len(q), 256):
+        blk = np.sort(q[b:b + 256])
+        aa += int(np.count_nonzero((blk[1:] >> np.uint64(24)) == (blk[:-1] >> np.uint64(24))))
+        same += int(np.count_nonzero(blk[1:] == blk[:-1]))
+    assert st["dup_aa_queries"] == aa and st["dup_key_queries"] == same
+    assert same > 0 and aa >= same
+    odb = oc.OracleDb(db_dir)
+    ores, otc = oc.classify(odb, par.to_c(), reads)
+    odb.close()
+    compare_results(br.results, br.taxcnt, ores, otc)
