@@ -286,6 +286,10 @@ def main():
                     help="config 5 on one GPU: DB parts, each timed in turn (with N >= 4 GPUs: one part per rank)")
     ap.add_argument("--c5-sample", type=int, default=24_000, help="config 5: read pairs of the oracle parity sample")
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
+    ap.add_argument("--skewed-pairs", type=int, default=10_000_000,
+                    help="config 3: read pairs of the skewed-abundance line (log-normal genome abundance; 0 = off)")
+    ap.add_argument("--skew-sigma", type=float, default=2.0,
+                    help="skewed line: sigma of the log-normal per-genome abundance")
     ap.add_argument("--cold-gtdb", type=int, default=1,
                     help="config 3: open the GTDB-scale DB from host diffIdx/info/split (mtb_open_host) and time it")
     ap.add_argument("--cold-pairs", type=int, default=10_000_000,
@@ -688,6 +692,79 @@ def run_cold(args, hdb, par, lp, s1, s2, n, check=None):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def run_skewed(args, clf, reads, s1, s2, o1, B, L, world, rank, lp, odb):
+    """Config 3 with a skewed-abundance sample: the same GTDB-scale DB and
+    context, reads drawn with a log-normal per-genome abundance (sigma --skew-sigma) so a few species
+    get tens of x coverage per batch, as real samples do. Timed as the headline (its QuerySplits); then
+    one untimed batch of each sample with MTB_DUP_STATS=1 counts the query k-mers whose AA rank /
+    whole value repeats another's in its K4 block — the work the reference's identical-query and
+    same-AA reuse saves (KmerMatcher.cpp:277-353) — and a 200k-pair oracle parity sample."""
+    k1, ko1, k2, ko2 = reads
+    N = ko1.numel() - 1
+    spans = [(a, min(N, a + B)) for a in range(0, N, B)]
+    offs = {b - a: ko1[:b - a + 1].contiguous() for a, b in spans}
+    tally = Tally()
+
+    def step(timed):
+        for a, b in spans:
+            ob = offs[b - a]
+            clf.classify_batch(k1[a * L:b * L], ob, k2[a * L:b * L], ob, device_input=True, fetch=False)
+            if timed:
+                tally.add(clf, 2 * L * (b - a), b - a)
+
+    step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=k1.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = world * N * args.steps / el
+    dup = {}
+    os.environ["MTB_DUP_STATS"] = "1"
+    try:
+        for name, (q1, q2, qo) in (("skewed", (k1, k2, ko1)), ("uniform", (s1, s2, o1))):
+            b = min(B, qo.numel() - 1)
+            ob = qo[:b + 1].contiguous()
+            clf.classify_batch(q1[:b * L], ob, q2[:b * L], ob, device_input=True, fetch=False)
+            st = clf.stats()
+            dup[name] = {"query_kmers": st["query_kmers"], "dup_aa_queries": st["dup_aa_queries"],
+                         "dup_key_queries": st["dup_key_queries"],
+                         "dup_aa_rate": round(st["dup_aa_queries"] / max(1, st["query_kmers"]), 5),
+                         "dup_key_rate": round(st["dup_key_queries"] / max(1, st["query_kmers"]), 5)}
+    finally:
+        os.environ.pop("MTB_DUP_STATS", None)
+    parity = None
+    if odb is not None and args.variant_cpu_sample > 0:
+        from tests import oracle_ctypes as oc  # checker only
+        S = min(args.variant_cpu_sample, N)
+        h1, h2 = k1[:S * L].cpu().numpy(), k2[:S * L].cpu().numpy()
+        ho = ko1[:S + 1].cpu().numpy().astype(np.uint64)
+        sample = synth.Reads(h1, ho, h2, ho.copy(), np.zeros(S, np.int32))
+        ores, otc = oc.classify(odb, lp.to_c(), sample)
+        gb = clf.classify_batch(h1, ho, h2, ho.copy())
+        parity = bool(np.array_equal(gb.results["classification"], ores["classification"])
+                      and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
+                      and np.array_equal(gb.taxcnt, otc))
+    kern = tally.kern_avg()
+    names = kernel_names(clf.stats())
+    out = {"value": round(value, 1), "unit": "reads/s", "ms_per_step": round(el / args.steps * 1e3, 3),
+           "read_pairs_per_gpu": N, "batch_pairs": B, "abundance_sigma": args.skew_sigma,
+           "kernel_ms": {k: round(float(v), 3) for k, v in zip(names, kern)},
+           "query_kmers_per_batch": int(tally.avg("q")), "matches_per_batch": int(tally.avg("m")),
+           "duplicates": dup, "parity_sample": parity,
+           "what": "the headline DB and context, reads drawn with log-normal per-genome abundance "
+                   f"(sigma {args.skew_sigma}): a few species at tens of x coverage per batch"}
+    log(rank, f"[bench] config 3 skewed: {value / 1e6:.2f}M reads/s, duplicates {dup}, parity {parity}")
+    return out
+
+
 def run_cold_gtdb(args, host, odb, lp, local, reads, ores, otc):
     """The GTDB-scale DB opened as the reference opens its DB on every run (KmerMatcher.cpp:127-138,
     212-265; Classifier.cpp:6-32): from diffIdx / info / split — here the host copy the oracle holds
@@ -840,6 +917,9 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
         got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev)
+        if args.skewed_pairs > 0 and not variant:  # a skewed-abundance sample of the same genomes
+            got["skewed"] = make_reads_gpu(seq, off, min(N, args.skewed_pairs), args.seed * 1000 + 41 + 17 * rank, dev,
+                                           abundance_sigma=args.skew_sigma)
         if args.long_reads > 0 and not variant:
             got["long"] = make_long_reads_gpu(seq, off, args.long_reads, args.seed * 1000 + 37 + 17 * rank, dev)
 
@@ -976,6 +1056,10 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
                       and np.array_equal(gb.results["score"].view(np.uint32), ores["score"].view(np.uint32))
                       and np.array_equal(gb.taxcnt, otc))
         log(rank, f"[bench] {tag} CPU oracle: {cpu['value'] if cpu else '-'} reads/s, parity {parity}")
+    skewed = None
+    if "skewed" in got:
+        skewed = run_skewed(args, clf, got.pop("skewed"), s1, s2, o1, B, L, world, rank, lp,
+                            odb if rank == 0 else None)
     e2e = None
     for c in peers:
         c.close()
@@ -1026,6 +1110,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         "em": em_line,
         "pipeline_roofline": pipe,
         "cold_run_gtdb": cold_gtdb,
+        "skewed": skewed,
     }
     if variant:
         out = {"variant": variant, "what": vr["what"], "value": out["value"], "unit": "reads/s",

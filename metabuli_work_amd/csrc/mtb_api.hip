@@ -141,7 +141,6 @@ struct mtb_ctx {
     int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune, 4 as 2 with the bitonic large sort)
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
-    bool dupStats = false;       // MTB_DUP_STATS=1: count the repeated AA ranks / keys per K4 block (stats[17], [18])
     bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
                                  // (with the sweep join the context then holds no probe lines either)
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
@@ -439,7 +438,6 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     // the warp-specialised sweep stages 24-KB tiles: nominal 1024 records (tiles ~ one bucket)
     if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
-    if (const char* e = getenv("MTB_DUP_STATS")) c->dupStats = atoi(e) != 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
@@ -648,7 +646,6 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->pruneCompact = src->pruneCompact;
     c->noAlias = src->noAlias;
     c->noFilter = src->noFilter;
-    c->dupStats = src->dupStats;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -1043,7 +1040,8 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(hipEventRecord(c->ev[2], s));
     c->Q = Q;
     c->stats[1] = Q;
-    if (c->dupStats && !probe) {  // after the sort, before the join: what K4's blocks could share
+    const char* dupEnv = getenv("MTB_DUP_STATS");  // read per batch (a diagnostic the bench turns on for one batch)
+    if (dupEnv && atoi(dupEnv) != 0 && !probe) {  // after the sort, before the join: what K4's blocks could share
         unsigned long long dup[2] = {0, 0};
         HIP_TRY(c->devStats.ensure(sizeof(unsigned long long) * 4));
         HIP_TRY(hipMemsetAsync(c->devStats.as<unsigned long long>() + 2, 0, 2 * sizeof(unsigned long long), s));

@@ -88,13 +88,24 @@ def make_genomes_gpu(n_species, mean_len, strains, seed, dev, taxo=None, per_gen
     return taxo, gen, seq, off_t, lens
 
 
-def make_reads_gpu(seq, off_t, n_pairs, seed, dev, read_len=150, sub_rate=0.005, random_frac=0.1):
+def make_reads_gpu(seq, off_t, n_pairs, seed, dev, read_len=150, sub_rate=0.005, random_frac=0.1,
+                   abundance_sigma=0.0):
+    """abundance_sigma > 0: a skewed sample — genome g drawn with weight length_g * A_g, A_g log-normal
+    (mu 0, sigma abundance_sigma, seeded), so a few genomes take tens of x the coverage of the rest
+    (real samples); 0: proportional to length."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    # genome chosen proportionally to its length (searchsorted on the offsets: torch.multinomial is
-    # not run-to-run deterministic on this device)
-    u = (torch.rand(n_pairs, device=dev, generator=g, dtype=torch.float64) * float(off_t[-1].item())).long()
-    gsel = torch.searchsorted(off_t[1:], u, right=True).clamp(max=off_t.numel() - 2)
+    # genome chosen proportionally to its (weighted) length (searchsorted on the cumulative weights:
+    # torch.multinomial is not run-to-run deterministic on this device)
+    glen_all = (off_t[1:] - off_t[:-1]).double()
+    if abundance_sigma > 0:
+        ab = np.random.default_rng(seed).lognormal(0.0, abundance_sigma, off_t.numel() - 1)
+        w = glen_all * torch.from_numpy(ab).to(dev)
+    else:
+        w = glen_all
+    cw = torch.cumsum(w, 0)
+    u = torch.rand(n_pairs, device=dev, generator=g, dtype=torch.float64) * float(cw[-1].item())
+    gsel = torch.searchsorted(cw, u, right=True).clamp(max=off_t.numel() - 2)
     gl = (off_t[1:] - off_t[:-1])[gsel]
     ins = (torch.randn(n_pairs, device=dev, generator=g) * 30 + 300).round().long().clamp(min=read_len)
     ins = torch.minimum(ins, gl)
