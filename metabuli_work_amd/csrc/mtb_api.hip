@@ -141,6 +141,7 @@ struct mtb_ctx {
     int pruneAfter = 2;          // MTB_PRUNE_AFTER (A/B): launch_segsort's register-sort mode (2 rank keys, 0 full keys, 1 sort then prune, 4 as 2 with the bitonic large sort)
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
+    bool radixDigits = true;     // MTB_RADIX_DIGITS=0: K2's histograms read the keys, not 1-B digit side arrays
     bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
                                  // (with the sweep join the context then holds no probe lines either)
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
@@ -181,6 +182,7 @@ struct mtb_ctx {
     DevBuf liveCnt, liveOff;                // K5 pruning: live matches per read, their offsets
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     DevBuf sizeLists;                       // K5: reads of each size class above 128 matches (k_size_lists)
+    DevBuf digA, digB;                      // K2 digit side arrays (1 B per kept query k-mer, ping-pong)
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
@@ -438,6 +440,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     // the warp-specialised sweep stages 24-KB tiles: nominal 1024 records (tiles ~ one bucket)
     if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
+    if (const char* e = getenv("MTB_RADIX_DIGITS")) c->radixDigits = atoi(e) != 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
@@ -646,6 +649,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->pruneCompact = src->pruneCompact;
     c->noAlias = src->noAlias;
     c->noFilter = src->noFilter;
+    c->radixDigits = src->radixDigits;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -656,7 +660,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
     return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->digA, &c->digB, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
@@ -980,17 +984,22 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     const uint32_t* qi = nullptr;
     const uint64_t* qf = nullptr;
     HIP_TRY(hipEventRecord(c->kev[2], s));
+    // K2's digit side arrays: the fused K1F writes each kept key's first-pass digit (bits kQuerySortLo..)
+    const bool digits = fused && c->radixDigits && c->sortLoFine == kQuerySortLo;
     if (fused) {
         uint64_t cap = std::min<uint64_t>(R, (uint64_t)((double)R * c->presentShare) + 4096);
         for (int pass = 0; pass < 2; pass++) {
             HIP_TRY(c->keysB.ensure(8 * cap));
             HIP_TRY(c->valsB.ensure(4 * cap));
+            if (digits) HIP_TRY(c->digA.ensure(cap));
             cap = std::min<uint64_t>(c->keysB.bytes / 8, c->valsB.bytes / 4);  // all the buffers hold
+            if (digits) cap = std::min<uint64_t>(cap, c->digA.bytes);
             Q = launch_extract_filter(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
                                       c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
                                       c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
                                       c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
-                                      c->rankHi, &c->Qall, cap, c->filterThreadMajor, s);
+                                      c->rankHi, &c->Qall, cap, c->filterThreadMajor, s,
+                                      digits ? c->digA.as<uint8_t>() : nullptr);
             HIP_TRY(hipGetLastError());
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             if (Q <= cap) break;
@@ -999,6 +1008,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         }
         HIP_TRY(c->keysA.ensure(8 * std::max<uint64_t>(Q, 1)));
         HIP_TRY(c->valsA.ensure(4 * std::max<uint64_t>(Q, 1)));
+        if (digits) HIP_TRY(c->digB.ensure(std::max<uint64_t>(Q, 16)));
         qk = c->keysB.as<uint64_t>();
         qi = c->valsB.as<uint32_t>();
     } else if (filt) {
@@ -1022,9 +1032,11 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     if (!probe) {
         bool inB = false;
         if (filt) {
+            const bool dg = digits && sortLo == kQuerySortLo;
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
                                  c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,
-                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s,
+                                 dg ? c->digA.as<uint8_t>() : nullptr, dg ? c->digB.as<uint8_t>() : nullptr);
             qk = inB ? c->keysA.as<uint64_t>() : c->keysB.as<uint64_t>();
             qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
         } else {

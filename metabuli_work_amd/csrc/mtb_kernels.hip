@@ -595,13 +595,49 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
     counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
 }
 
+// The same histogram from a byte array of the pass's digits (written by the previous pass's scatter,
+// or by the fused K1F for the first): 1 B read per key instead of 8.
+__global__ void __launch_bounds__(256) k_radix_hist_dig(const uint8_t* __restrict__ dig, uint64_t n,
+                                                        uint32_t* __restrict__ counts, uint32_t nTiles) {
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+    constexpr int kVec = kRadixTile / kBlock / 16;  // uint4 loads per thread
+    uint4 d[kVec];
+    const bool full = base + kRadixTile <= n;
+#pragma unroll
+    for (int k = 0; k < kVec; k++) {
+        const uint64_t i = base + ((uint64_t)k * kBlock + threadIdx.x) * 16;
+        d[k] = full ? reinterpret_cast<const uint4*>(dig + base)[k * kBlock + threadIdx.x] : make_uint4(0, 0, 0, 0);
+        if (!full) {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; b++)
+                if (i + b < n) w[b >> 2] |= (uint32_t)dig[i + b] << (8 * (b & 3));
+            d[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kVec; k++) {
+        const uint64_t i = base + ((uint64_t)k * kBlock + threadIdx.x) * 16;
+        const uint32_t w[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+#pragma unroll
+        for (int b = 0; b < 16; b++)
+            if (full || i + b < n) atomicAdd(&hist[(w[b >> 2] >> (8 * (b & 3))) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    counts[(uint64_t)threadIdx.x * nTiles + blockIdx.x] = hist[threadIdx.x];
+}
+
 // V: value type (64-bit payloads, or 32-bit slot indices). GEN: the values are the input positions
-// (the first pass of a sort of slots), so none are read.
+// (the first pass of a sort of slots), so none are read. digOut (nullable): the next pass's digit
+// (bits [nextShift, nextShift + 8) of the key) of every written key, at its output position.
 template <typename V, bool FILTER, bool GEN>
 __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn, const V* __restrict__ valsIn,
                                                        uint64_t n, int shift, const uint64_t* __restrict__ offs,
                                                        uint32_t nTiles, uint64_t* __restrict__ keysOut,
-                                                       V* __restrict__ valsOut) {
+                                                       V* __restrict__ valsOut, uint8_t* __restrict__ digOut,
+                                                       int nextShift) {
     __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
@@ -678,7 +714,15 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         sDig[rk[r]] = (uint8_t)d;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < sKept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
+    if (digOut) {
+        for (uint32_t i = tid; i < sKept; i += kBlock) {
+            const uint64_t o = sDst[sDig[i]] + i;
+            keysOut[o] = sKV[i];
+            digOut[o] = (uint8_t)(sKV[i] >> nextShift);
+        }
+    } else {
+        for (uint32_t i = tid; i < sKept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
+    }
     __syncthreads();
     V* sV = reinterpret_cast<V*>(sKV);
 #pragma unroll
@@ -697,23 +741,29 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s) {
+                          hipStream_t s, uint8_t* digA, uint8_t* digB) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *ko = keysB;
     V *vi = valsA, *vo = valsB;
+    uint8_t *di = digA, *dg = digB;  // digit side arrays: digA holds the first pass's digits (no filter)
+    const bool digits = digA && digB && !filter;
     bool first = true;
     *inB = false;
     for (int shift = bitLo; shift < bitHi; shift += 8) {
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
         const bool f = first && filter, g = first && genVals;
-        if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        if (digits) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles);
+        else if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
-        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
-        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
-        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
-        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo);
+        uint8_t* dOut = digits && shift + 8 < bitHi ? dg : nullptr;
+        const int ns = shift + 8;
+        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
+        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
+        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
+        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
+        std::swap(di, dg);
         if (f) {
             uint64_t kept = 0;
             hipMemcpyAsync(&kept, offs + 256ull * nTiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
@@ -729,9 +779,9 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
 }
 
 template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*);
 template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*);
 
 // ------------------------------------------------------------------------------------------------
 // K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->
@@ -1641,7 +1691,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                                                         uint64_t* __restrict__ unitInfo, const ProbeLine* __restrict__ lines,
                                                         uint64_t* __restrict__ qkey, uint32_t* __restrict__ qslot,
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
-                                                        uint64_t rankHi, uint64_t cap) {
+                                                        uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     __shared__ unsigned long long sOut;
@@ -1705,6 +1755,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                 if (pos < cap) {
                     qkey[pos] = k[j];
                     qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+                    if (qdig) qdig[pos] = (uint8_t)(k[j] >> kQuerySortLo);
                 }
                 pos++;
             }
@@ -1741,6 +1792,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
             if (pos < cap) {  // past the output's capacity: counted only (the caller grows it and reruns)
                 qkey[pos] = k[j];
                 qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+                if (qdig) qdig[pos] = (uint8_t)(k[j] >> kQuerySortLo);  // the sort's first digit (K2's side array)
             }
         }
     }
@@ -1756,7 +1808,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               uint64_t cap, bool threadMajor, hipStream_t s) {
+                               uint64_t cap, bool threadMajor, hipStream_t s, uint8_t* qdig) {
     hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     if (nUnits) {
         const uint64_t threads = (nUnits + 63) / 64 * 64;
@@ -1767,7 +1819,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
 #define MTB_EF(P, J)                                                                                                  \
     k_extract_filter<P, J><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,           \
                                                   extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
-                                                  qslot, counter, rankLo, rankHi, cap)
+                                                  qslot, counter, rankLo, rankHi, cap, qdig)
         if (per == 8) {
             if (jMajor) MTB_EF(8, true);
             else MTB_EF(8, false);
@@ -1795,11 +1847,11 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
             hipEventRecord(ev[0], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0);
+                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr);
             hipEventRecord(ev[1], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, 0, 0, 0);
+                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr);
             hipEventRecord(ev[2], s);
             hipStreamSynchronize(s);
             float a = 0, b = 0;

@@ -97,11 +97,14 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
                     uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
 
 uint64_t radix_counts_elems(uint64_t n);
-// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read)
+// V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read).
+// digA / digB (nullable, n bytes each; not with filter): digit side arrays — digA holds every key's
+// first-pass digit (bits [bitLo, bitLo + 8)), each scatter writes the next pass's digits, and the
+// histograms read 1 B per key instead of the 8-B key.
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s);
+                          hipStream_t s, uint8_t* digA = nullptr, uint8_t* digB = nullptr);
 // format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
 uint64_t host_from_rank_form(uint64_t v);
@@ -183,7 +186,8 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               uint64_t cap, bool threadMajor, hipStream_t s);
+                               uint64_t cap, bool threadMajor, hipStream_t s,
+                               uint8_t* qdig = nullptr);
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                        uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
                        uint64_t* emitted, hipStream_t s);
