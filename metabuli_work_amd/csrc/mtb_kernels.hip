@@ -637,17 +637,27 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
                                                        uint64_t n, int shift, const uint64_t* __restrict__ offs,
                                                        uint32_t nTiles, uint64_t* __restrict__ keysOut,
                                                        V* __restrict__ valsOut, uint8_t* __restrict__ digOut,
-                                                       int nextShift) {
+                                                       int nextShift, int xcdMap) {
     __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
     __shared__ uint64_t sDst[256];  // global slot of this tile's first key of digit d, minus its tile offset
     __shared__ uint32_t sKept;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile + (uint64_t)w * kRadixSlice;
+    // XCD-aware tiles: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so block b
+    // takes tile (b mod 8)'s share start + b / 8: each XCD walks one contiguous eighth of the tiles in
+    // order, and the digit-d runs of consecutive tiles — adjacent in the output — are written through
+    // the same L2, which completes the lines a run leaves partial instead of two XCDs each writing
+    // part of a line (speed only: any mapping is correct)
+    uint32_t tile = blockIdx.x;
+    if (xcdMap) {
+        const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3, q = nTiles >> 3, r = nTiles & 7u;
+        tile = x * q + min(x, r) + i;
+    }
+    const uint64_t base = (uint64_t)tile * kRadixTile + (uint64_t)w * kRadixSlice;
     // the digit bases: one strided load per lane, issued first so its latency hides behind the
     // key loads (a dependent load per key in the write-out loop was the old bottleneck)
-    const uint64_t digitBase = offs[(uint64_t)tid * nTiles + blockIdx.x];
+    const uint64_t digitBase = offs[(uint64_t)tid * nTiles + tile];
     for (int x = tid; x < kWaves * 256; x += kBlock) (&waveHist[0][0])[x] = 0;
     __syncthreads();
 
@@ -657,7 +667,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
     // all loads first (unguarded for the full tiles) so the 32 loads of a lane are in flight
     // together; interleaving them with the ranking serialised 16 memory round trips per tile
-    if ((uint64_t)(blockIdx.x + 1) * kRadixTile <= n) {
+    if ((uint64_t)(tile + 1) * kRadixTile <= n) {
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
 #pragma unroll
@@ -758,11 +768,13 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
         uint8_t* dOut = digits && shift + 8 < bitHi ? dg : nullptr;
+        // MTB_RADIX_XCD=0 (A/B): tiles in block order instead of one contiguous eighth per XCD
+        static const int xcd = getenv("MTB_RADIX_XCD") ? atoi(getenv("MTB_RADIX_XCD")) : 1;
         const int ns = shift + 8;
-        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
-        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
-        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
-        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns);
+        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
+        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
+        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
+        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
         std::swap(di, dg);
         if (f) {
             uint64_t kept = 0;
