@@ -286,6 +286,8 @@ def main():
                     help="config 5 on one GPU: DB parts, each timed in turn (with N >= 4 GPUs: one part per rank)")
     ap.add_argument("--c5-sample", type=int, default=24_000, help="config 5: read pairs of the oracle parity sample")
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
+    ap.add_argument("--ab", default="", help="experiments: 'name=K=V,K=V;name2=...' same-box A/B of the headline")
+    ap.add_argument("--ab-repeat", type=int, default=2, help="--ab: rounds over the specs")
     ap.add_argument("--skewed-pairs", type=int, default=10_000_000,
                     help="config 3: read pairs of the skewed-abundance line (log-normal genome abundance; 0 = off)")
     ap.add_argument("--skew-sigma", type=float, default=2.0,
@@ -323,6 +325,11 @@ def main():
         c5 = run_config5(args, world, rank, local, dev)
         if rank == 0:
             print(json.dumps(c5))
+        return
+    if args.ab:  # experiments: the headline DB built once, environments A/B'd on it; one JSON line
+        v = run_gtdb(args, world, rank, local, dev)
+        if rank == 0:
+            print(json.dumps(v))
         return
     if args.variant_only:
         v = run_gtdb(args, world, rank, local, dev, variant=args.variant_only)
@@ -692,6 +699,55 @@ def run_cold(args, hdb, par, lp, s1, s2, n, check=None):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def run_ab(args, rdb, lp, s1, s2, o1, spans, L, local, rank):
+    """--ab 'name=K=V,K=V;name2=...': a same-box A/B on the headline workload with the GTDB-scale DB
+    built once — per spec a fresh context opened under its environment (knobs read at open, or per
+    batch), one warm-up step and --steps timed steps, specs interleaved --ab-repeat times. Returns
+    {name: [ {value, kernel_ms}, ... ]}."""
+    specs = []
+    for part in args.ab.split(";"):
+        name, _, envs = part.partition("=")
+        kv = dict(e.split("=", 1) for e in envs.split(",") if e)
+        specs.append((name, kv))
+    N = spans[-1][1]
+    offs = {b - a: o1[:b - a + 1].contiguous() for a, b in spans}
+    out = {name: [] for name, _ in specs}
+    for rep in range(args.ab_repeat):
+        for name, kv in specs:
+            old = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
+            try:
+                clf = Classifier(lp, db_resident=rdb, device=local)
+                tally = Tally()
+
+                def step(timed):
+                    for a, b in spans:
+                        ob = offs[b - a]
+                        clf.classify_batch(s1[a * L:b * L], ob, s2[a * L:b * L], ob, device_input=True, fetch=False)
+                        if timed:
+                            tally.add(clf, 2 * L * (b - a), b - a)
+                step(False)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    step(True)
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                names = kernel_names(clf.stats())
+                r = {"value": round(N * args.steps / el, 1),
+                     "kernel_ms": {k: round(float(v), 3) for k, v in zip(names, tally.kern_avg())}}
+                clf.close()
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            out[name].append(r)
+            log(rank, f"[bench ab] {name} #{rep}: {r['value'] / 1e6:.3f}M reads/s {r['kernel_ms']}")
+    return {"ab": out, "value": max(max(x["value"] for x in v) for v in out.values())}
+
+
 def run_skewed(args, clf, reads, s1, s2, o1, B, L, world, rank, lp, odb):
     """Config 3 with a skewed-abundance sample: the same GTDB-scale DB and
     context, reads drawn with a log-normal per-genome abundance (sigma --skew-sigma) so a few species
@@ -945,6 +1001,9 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     c1 = ResultGather(dev, N) if world > 1 else None
     tally = Tally()
 
+    if args.ab and not variant:  # experiments: same-box A/B of environments on this DB, then stop
+        clf.close()
+        return run_ab(args, rdb, lp, s1, s2, o1, spans, L, local, rank)
     peers = [clf.clone() for _ in range(args.gtdb_contexts - 1)] if not variant and world == 1 else []
 
     def step(timed):

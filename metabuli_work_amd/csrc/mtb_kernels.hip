@@ -768,8 +768,9 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
         uint8_t* dOut = digits && shift + 8 < bitHi ? dg : nullptr;
-        // MTB_RADIX_XCD=0 (A/B): tiles in block order instead of one contiguous eighth per XCD
-        static const int xcd = getenv("MTB_RADIX_XCD") ? atoi(getenv("MTB_RADIX_XCD")) : 1;
+        // MTB_RADIX_XCD=0 (A/B, read per sort): tiles in block order instead of one contiguous eighth per XCD
+        const char* xe = getenv("MTB_RADIX_XCD");
+        const int xcd = xe ? atoi(xe) : 1;
         const int ns = shift + 8;
         if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
