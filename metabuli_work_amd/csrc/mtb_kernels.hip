@@ -3,6 +3,8 @@
 // mtb_assign.hip. All integer/byte work, HBM-bound: no MFMA.
 #include "mtb_launch.h"
 
+#include <cstring>
+
 namespace mtb {
 
 // ------------------------------------------------------------------------------------------------
@@ -996,10 +998,98 @@ __global__ void k_line_bits(const DbRec* __restrict__ db, uint64_t D, ProbeLine*
     }
 }
 
+// The same bits a wave per line, with no global atomics: the line's DB records [base, next base)
+// are read coalesced (consecutive lines are consecutive record ranges), each run start ORs its bit
+// into the wave's 14 LDS words, and the wave stores the line's words once. k_line_bits above made
+// one random global atomicOr per present AA rank (10.2G at GTDB scale: 361 ms).
+constexpr int kLineWords = (int)(kLineRanks / 32);
+__global__ void __launch_bounds__(256) k_line_bits_wave(const DbRec* __restrict__ db, uint64_t D,
+                                                        ProbeLine* __restrict__ lines) {
+    __shared__ uint32_t sW[4][kLineWords];
+    const DbVal dbv{db};
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    for (uint64_t L = (uint64_t)blockIdx.x * 4 + wv; L < kProbeLines; L += (uint64_t)gridDim.x * 4) {
+        if (lane < kLineWords) sW[wv][lane] = 0;
+        const uint64_t b = lines[L].base & ((1ull << 40) - 1);
+        const uint64_t e = L + 1 < kProbeLines ? lines[L + 1].base & ((1ull << 40) - 1) : D;
+        const uint64_t r0 = L * kLineRanks;
+        for (uint64_t i0 = b; i0 < e; i0 += 64) {
+            const uint64_t i = i0 + lane;
+            const uint64_t r = i < e ? dbv[i] >> 24 : ~0ull;
+            // the previous record's rank: the lane below's, or (lane 0) the record before the chunk
+            uint64_t prev = __shfl_up(r, 1, 64);
+            if (lane == 0) prev = i > 0 ? dbv[i - 1] >> 24 : ~0ull;
+            if (i < e && (i == 0 || prev != r)) {
+                const uint32_t o = (uint32_t)(r - r0);
+                atomicOr(&sW[wv][o >> 5], 1u << (o & 31u));
+            }
+        }
+        // the wave's LDS writes are complete in program order; every lane reads its word after them
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < kLineWords) lines[L].bits[lane] = sW[wv][lane];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Run index a wave per line too: the line's words in registers, each run start's present-rank
+// index inside the line from the words' popcounts, its run start written at lineP[L] + that index.
+__global__ void __launch_bounds__(256) k_run_offsets_wave(const DbRec* __restrict__ db, uint64_t D,
+                                                          const ProbeLine* __restrict__ lines,
+                                                          const uint64_t* __restrict__ lineP,
+                                                          uint16_t* __restrict__ runOff) {
+    __shared__ uint32_t sPre[4][kLineWords];  // present ranks in the line's words before word k
+    __shared__ uint32_t sW[4][kLineWords];
+    const DbVal dbv{db};
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    for (uint64_t L = (uint64_t)blockIdx.x * 4 + wv; L < kProbeLines; L += (uint64_t)gridDim.x * 4) {
+        const uint64_t head = lines[L].base;
+        const uint64_t b = head & ((1ull << 40) - 1);
+        const uint64_t e = L + 1 < kProbeLines ? lines[L + 1].base & ((1ull << 40) - 1) : D;
+        if ((head >> 40) > kRunIdxMax || e <= b) continue;  // not indexed (its queries gallop), or empty
+        const uint32_t w = lane < kLineWords ? lines[L].bits[lane] : 0u;
+        const uint32_t pc = (uint32_t)__popc(w);
+        uint32_t inc = pc;  // inclusive scan of the word popcounts over lanes 0..13
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        if (lane < kLineWords) {
+            sPre[wv][lane] = inc - pc;
+            sW[wv][lane] = w;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t r0 = L * kLineRanks, p0 = lineP[L];
+        for (uint64_t i0 = b; i0 < e; i0 += 64) {
+            const uint64_t i = i0 + lane;
+            const uint64_t r = i < e ? dbv[i] >> 24 : ~0ull;
+            uint64_t prev = __shfl_up(r, 1, 64);
+            if (lane == 0) prev = i > 0 ? dbv[i - 1] >> 24 : ~0ull;
+            if (i < e && (i == 0 || prev != r)) {
+                const uint32_t o = (uint32_t)(r - r0), k = o >> 5;
+                const uint32_t before = sPre[wv][k] + (uint32_t)__popc(sW[wv][k] & ((1u << (o & 31u)) - 1u));
+                runOff[p0 + before] = (uint16_t)(i - b);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+static unsigned line_wave_grid() { return (unsigned)std::min<uint64_t>((kProbeLines + 3) / 4, 1u << 20); }
+
+static bool line_atomic_build() {  // MTB_LINE_BUILD=atomic (A/B): the per-k-mer atomic kernels
+    const char* e = getenv("MTB_LINE_BUILD");
+    return e && !strcmp(e, "atomic");
+}
+
 void build_probe_lines(const DbRec* db, uint64_t D, const AADir& dir, ProbeLine* lines, hipStream_t s) {
     k_line_base<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(db, D, dir, lines);
     k_line_count<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines);
-    if (D) k_line_bits<<<stride_grid(D), 256, 0, s>>>(db, D, lines);
+    if (!D) return;
+    if (line_atomic_build()) k_line_bits<<<stride_grid(D), 256, 0, s>>>(db, D, lines);
+    else k_line_bits_wave<<<line_wave_grid(), 256, 0, s>>>(db, D, lines);
 }
 
 // Run index: the exact DB run of every present AA rank, for the unstaged K4 (a DB much larger than
@@ -1040,7 +1130,9 @@ void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp
 
 void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s) {
-    if (D) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(db, D, lines, lineP, runOff);
+    if (!D) return;
+    if (line_atomic_build()) k_run_offsets<<<stride_grid(D), 256, 0, s>>>(db, D, lines, lineP, runOff);
+    else k_run_offsets_wave<<<line_wave_grid(), 256, 0, s>>>(db, D, lines, lineP, runOff);
 }
 
 // Query blocks: kMatchQ consecutive sorted queries span a narrow AA-rank range, so the DB values
