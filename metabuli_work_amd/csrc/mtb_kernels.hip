@@ -929,7 +929,8 @@ void launch_rec_rank_form(DbRec* db, uint64_t n, hipStream_t s) {
     if (n) k_rec_rank_form<<<stride_grid(n), 256, 0, s>>>(db, n);
 }
 void launch_rec_mask_info(DbRec* db, uint64_t n, uint32_t mask, hipStream_t s) {
-    if (n) k_rec_mask_info<<<stride_grid(n), 256, 0, s>>>(db, n, mask);
+    // Skip_redundancy 1 (modern DBs) keeps every bit: nothing to do (a 12G-record pass was 50 ms)
+    if (n && mask != ~0u) k_rec_mask_info<<<stride_grid(n), 256, 0, s>>>(db, n, mask);
 }
 
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s) {
@@ -2310,7 +2311,7 @@ __global__ void k_mask_info(uint32_t* info, uint64_t n, uint32_t mask) {
 }
 
 void launch_mask_info(uint32_t* info, uint64_t n, uint32_t mask, hipStream_t s) {
-    if (n) k_mask_info<<<stride_grid(n), 256, 0, s>>>(info, n, mask);
+    if (n && mask != ~0u) k_mask_info<<<stride_grid(n), 256, 0, s>>>(info, n, mask);
 }
 
 // ------------------------------------------------------------------------------------------------
