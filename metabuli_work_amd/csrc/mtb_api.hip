@@ -1083,7 +1083,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     }
     if (direct) {  // + the spill buffer (queries past their read's stretch), in mStage / mRank
         HIP_TRY(c->ovFlag.ensure(sizeof(int)));
-        c->spillCap = std::max<uint64_t>(c->spillCap, std::max<uint64_t>(Q / 64, 1u << 16));
+        c->spillCap = std::max<uint64_t>(c->spillCap, std::max<uint64_t>(Q / 64, 1u << 12));
         if (c->mStage.ensure(sizeof(mtb_match) * c->spillCap) != hipSuccess ||
             c->mRank.ensure(sizeof(uint32_t) * c->spillCap) != hipSuccess) {
             (void)hipGetLastError();
@@ -1120,7 +1120,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                            c->qStart.as<uint32_t>() + kSweepStartsTmp, s);
     }
     if (direct) {  // the long-run list: grown to the largest seen
-        c->longCap = std::max<uint32_t>(c->longCap, (uint32_t)std::min<uint64_t>(std::max<uint64_t>(Q / 256, 1u << 16), 1u << 30));
+        c->longCap = std::max<uint32_t>(c->longCap, (uint32_t)std::min<uint64_t>(std::max<uint64_t>(Q / 256, 1u << 12), 1u << 30));
         HIP_TRY(c->longList.ensure(sizeof(LongRun) * c->longCap));
         HIP_TRY(c->longCnt.ensure(sizeof(uint32_t)));
     }

@@ -26,7 +26,7 @@ def _lines(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cap", [0, 4_000_000, 6_000_000, 9_000_000, 16_000_000, 40_000_000])
+@pytest.mark.parametrize("cap", [0, 1_500_000, 3_000_000, 6_000_000, 12_000_000, 40_000_000])
 def test_c_caller_matches_oracle(make_db, tmp_path, cap):
     db_dir, taxo, gen = make_db("fmt2")
     r = synth.make_reads(gen, 2100, paired=True, seed=71, short_frac=0.03)
