@@ -1359,6 +1359,9 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // without the readCnt atomic (a wrong rank: the results are invalid), bounding what any scheme
 // that removes the atomic could save in the join; 2: nor the read's stretch bounds (dirOff).
 __device__ int g_abRankFree = 0;
+__device__ int g_matchXcd = 0;
+
+void set_match_xcd(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on, sizeof(int)); }
 
 void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int)); }
 
@@ -1387,7 +1390,14 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
     const DbVal dbv{db};
     const DbTax dbtax{db};
-    const uint64_t q0 = (uint64_t)blockIdx.x * (256 * kPer);
+    // g_matchXcd (MTB_MATCH_XCD=1, A/B): the unstaged join's blocks remapped so each XCD takes one
+    // contiguous eighth of the sorted queries (neighbouring blocks' probe lines and records through one L2)
+    uint32_t blk = blockIdx.x;
+    if (!kStage && g_matchXcd) {
+        const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3, q = gridDim.x >> 3, r = gridDim.x & 7u;
+        blk = x * q + min(x, r) + i;
+    }
+    const uint64_t q0 = (uint64_t)blk * (256 * kPer);
     const uint64_t q1 = min(q0 + (uint64_t)(256 * kPer), Q);
     // every independent load of the block is issued up front (query keys and infos, the window
     // bounds, then the window) so their latencies overlap instead of adding up
