@@ -299,7 +299,7 @@ def test_classify_two_ranks(make_db, mode):
 @pytest.mark.parametrize("db_name,parts,cap,batch,peer", [("fmt2", 2, False, 700, ""), ("fmt2", 3, False, 700, ""),
                                                           ("fmt1", 2, False, 700, ""), ("fmt2_syncmer", 3, False, 700, ""),
                                                           ("fmt2", 2, True, 700, ""), ("fmt2", 3, False, 37, ""),
-                                                          ("fmt2", 3, False, 700, "host"), ("fmt2", 2, True, 300, "host")])
+                                                          ("fmt2", 3, False, 700, "host"), ("fmt2", 2, True, 700, "host")])
 def test_start_classify_partitioned(make_db, tmp_path, monkeypatch, db_name, parts, cap, batch, peer):
     """mtb_start_classify_partitioned (SURVEY §8(e), config 5 natively): one context per DB part (all
     on cuda:0 here), every batch matched by each part, the segments handed to the owners of their
