@@ -1146,6 +1146,11 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         del rdb
         gc.collect()
         torch.cuda.empty_cache()
+        # settle the runtime's deferred release of the ~170 GB just freed (untimed): a fresh process
+        # opening its DB has nothing to release, and the first allocation after a large free waits
+        # for all of it
+        torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
         cold_gtdb = run_cold_gtdb(args, host, odb, lp, local, reads, ores, otc)
         rdb = None
     if odb is not None:

@@ -166,9 +166,10 @@ uint64_t mtb_db_kmers(const mtb_ctx* ctx);             /* number of reference k-
  * as the reference re-searches a split after its match buffer ran out (Classifier.cpp:127-130,
  * KmerMatcher.cpp:474-476); mtb_start_classify* halve such a batch down to one read. */
 uint64_t mtb_workspace_bytes(const mtb_ctx* ctx);
-/* Seconds the context's open took, by phase: [0] reading the DB files (mtb_open), [1] upload and
- * K3 decode of diffIdx into the resident records, [2] AA-prefix directory, [3] probe lines, [4] run
- * index, [5] taxonomy and species map upload, [6] the whole open. */
+/* Seconds the context's open took, by phase: [0] reading and uploading diffIdx / info (files or
+ * mtb_open_host's arrays, through pinned staging, chunk by chunk), [1] K3 decode of diffIdx into the
+ * resident records, [2] AA-prefix directory, [3] probe lines, [4] run index, [5] taxonomy and species
+ * map upload, [6] the whole open, [7] the records' allocation (part of [1]). */
 int mtb_open_phases(const mtb_ctx* ctx, double* sec, int n);
 int mtb_set_workspace_cap(mtb_ctx* ctx, uint64_t bytes);
 /* Gives the context's batch workspace back to the device (the next batch regrows it), e.g. when a

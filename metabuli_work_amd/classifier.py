@@ -156,7 +156,8 @@ class Classifier:
         """Device bytes of the batch workspace the context holds (mtb_workspace_bytes)."""
         return int(lib().mtb_workspace_bytes(self.handle))
 
-    OPEN_PHASES = ["read_s", "decode_s", "directory_s", "probe_lines_s", "run_index_s", "taxonomy_s", "total_s"]
+    OPEN_PHASES = ["read_s", "decode_s", "directory_s", "probe_lines_s", "run_index_s", "taxonomy_s", "total_s",
+                   "records_alloc_s"]
 
     def open_phases(self) -> dict:
         """Seconds of the context's open by phase (mtb_open_phases)."""

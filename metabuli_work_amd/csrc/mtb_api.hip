@@ -188,7 +188,7 @@ struct mtb_ctx {
     WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
-    double openS[7] = {0, 0, 0, 0, 0, 0, 0};
+    double openS[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [7]: the records' allocation (inside [1])
     static constexpr int kNumStats = 19;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
@@ -307,16 +307,21 @@ static int decode_db_chunked(mtb_ctx* c, HostDb& db, uint32_t mask, hipStream_t 
     HIP_TRY(dTmp.ensure(scan_tmp_elems(W) * sizeof(uint64_t)));
     HIP_TRY(dVal.ensure(W * sizeof(uint64_t)));
     HIP_TRY(dInfo.ensure(W * sizeof(uint32_t)));
+    auto a0 = std::chrono::steady_clock::now();
     HIP_TRY(hipMalloc(&c->db, (D + kDbPad) * sizeof(DbRec)));
+    c->openS[7] = since(a0);  // the records' allocation (waits for any memory the runtime still releases)
     const bool fromFile = !db.diffFile.empty();
     double upS = 0;
+    auto l0 = std::chrono::steady_clock::now();
+    StageLanes lanes(c->device);  // pinned staging reused by every chunk's uploads
+    upS += since(l0);
     uint64_t w0 = 0, k0 = 0, carry = 0, seen = 0;  // seen: terminators so far (k0 stops at D)
     HIP_TRY(hipStreamSynchronize(s));
     while (w0 < nDiff) {
         const uint64_t n = std::min(W, nDiff - w0);
         auto u0 = std::chrono::steady_clock::now();
-        const bool got = fromFile ? read_to_device(db.diffFile, dDiff.p, n * sizeof(uint16_t), w0 * sizeof(uint16_t))
-                                  : upload_to_device(db.diffP + w0, dDiff.p, n * sizeof(uint16_t));
+        const bool got = fromFile ? read_to_device(db.diffFile, dDiff.p, n * sizeof(uint16_t), w0 * sizeof(uint16_t), &lanes)
+                                  : upload_to_device(db.diffP + w0, dDiff.p, n * sizeof(uint16_t), &lanes);
         if (!got) return MTB_ERR_IO;
         upS += since(u0);
         uint64_t lastTerm = 0, lastValue = 0;
@@ -337,8 +342,8 @@ static int decode_db_chunked(mtb_ctx* c, HostDb& db, uint32_t mask, hipStream_t 
         if (seen <= D) {  // the records of these k-mers: info & mask next to the rank-form values
             u0 = std::chrono::steady_clock::now();
             const bool gotInfo = fromFile ? read_to_device(db.infoFile, dInfo.p, terms * sizeof(uint32_t),
-                                                           k0 * sizeof(uint32_t))
-                                          : upload_to_device(db.infoP + k0, dInfo.p, terms * sizeof(uint32_t));
+                                                           k0 * sizeof(uint32_t), &lanes)
+                                          : upload_to_device(db.infoP + k0, dInfo.p, terms * sizeof(uint32_t), &lanes);
             if (!gotInfo) return MTB_ERR_IO;
             upS += since(u0);
             launch_mask_info(dInfo.as<uint32_t>(), terms, mask, s);
@@ -704,7 +709,7 @@ uint64_t mtb_workspace_bytes(const mtb_ctx* c) { return c ? c->ws.used : 0; }
 
 int mtb_open_phases(const mtb_ctx* c, double* sec, int n) {
     if (!c || !sec) return MTB_ERR_ARG;
-    for (int i = 0; i < n && i < 7; i++) sec[i] = c->openS[i];
+    for (int i = 0; i < n && i < 8; i++) sec[i] = c->openS[i];
     return MTB_OK;
 }
 

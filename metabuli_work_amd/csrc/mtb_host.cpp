@@ -17,6 +17,7 @@
 #include <atomic>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <functional>
@@ -365,56 +366,74 @@ bool check_db(const HostDb& db) {
 // `bytes` into device memory through pinned staging buffers: up to 8 threads, each filling one of
 // its two 32-MB buffers (fill(buf, at, len): bytes [at, at + len) of the source) while the other
 // uploads. what names the source in the error message.
+StageLanes::StageLanes(int device) : dev(device) {
+    hipSetDevice(dev);
+    for (Lane& l : lane) {
+        bool good = hipStreamCreateWithFlags(&l.st, hipStreamNonBlocking) == hipSuccess;
+        for (int k = 0; k < 2 && good; k++)
+            good = hipHostMalloc((void**)&l.buf[k], kChunk, hipHostMallocDefault) == hipSuccess &&
+                   hipEventCreateWithFlags(&l.done[k], hipEventDisableTiming) == hipSuccess;
+        ok = ok && good;
+    }
+}
+
+StageLanes::~StageLanes() {
+    hipSetDevice(dev);
+    for (Lane& l : lane) {
+        if (l.st) hipStreamSynchronize(l.st);
+        for (int k = 0; k < 2; k++) {
+            if (l.buf[k]) hipHostFree(l.buf[k]);
+            if (l.done[k]) hipEventDestroy(l.done[k]);
+        }
+        if (l.st) hipStreamDestroy(l.st);
+    }
+}
+
+// `bytes` into device memory through pinned staging buffers: up to kLanes threads, each filling one
+// of its two 32-MB buffers (fill(buf, at, len): bytes [at, at + len) of the source) while the other
+// uploads. what names the source in the error message. lanes: buffers and streams reused across
+// calls (an open's chunked decode makes ~50 of them; each call pinning its own 16 buffers was most
+// of the GTDB-scale open's upload time), or none (made for this call).
 static bool stage_to_device(const std::function<bool(char*, uint64_t, uint64_t)>& fill, void* dst, uint64_t bytes,
-                            const std::string& what) {
-    constexpr uint64_t kChunk = 32ull << 20;
-    const unsigned nThreads = (unsigned)std::min<uint64_t>(8, (bytes + kChunk - 1) / kChunk);
-    std::atomic<uint64_t> next{0};
-    std::atomic<bool> ok{true};
-    std::string err;
-    std::mutex errMu;
+                            const std::string& what, StageLanes* lanes) {
     int dev = 0;
     hipGetDevice(&dev);
-    auto work = [&] {
+    std::unique_ptr<StageLanes> own;
+    if (!lanes || lanes->dev != dev) {
+        own.reset(new StageLanes(dev));
+        lanes = own.get();
+    }
+    if (!lanes->ok) { set_error("cannot pin staging buffers for " + what); return false; }
+    constexpr uint64_t kChunk = StageLanes::kChunk;
+    const unsigned nThreads = (unsigned)std::min<uint64_t>(StageLanes::kLanes, (bytes + kChunk - 1) / kChunk);
+    std::atomic<uint64_t> next{0};
+    std::atomic<bool> ok{true};
+    auto work = [&](unsigned t) {
         hipSetDevice(dev);
-        hipStream_t st = nullptr;
-        char* buf[2] = {nullptr, nullptr};
-        hipEvent_t done[2] = {nullptr, nullptr};
-        bool good = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-        for (int k = 0; k < 2 && good; k++)
-            good = hipHostMalloc((void**)&buf[k], kChunk, hipHostMallocDefault) == hipSuccess &&
-                   hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+        StageLanes::Lane& l = lanes->lane[t];
+        bool good = true;
         for (int k = 0; good && ok;) {  // alternate two buffers: read one while the other uploads
             const uint64_t at = next.fetch_add(kChunk);
             if (at >= bytes) break;
             const uint64_t len = std::min(kChunk, bytes - at);
-            if (hipEventSynchronize(done[k]) != hipSuccess) { good = false; break; }
-            good = fill(buf[k], at, len);
-            good = good && hipMemcpyAsync((char*)dst + at, buf[k], len, hipMemcpyHostToDevice, st) == hipSuccess &&
-                   hipEventRecord(done[k], st) == hipSuccess;
+            if (hipEventSynchronize(l.done[k]) != hipSuccess) { good = false; break; }
+            good = fill(l.buf[k], at, len);
+            good = good && hipMemcpyAsync((char*)dst + at, l.buf[k], len, hipMemcpyHostToDevice, l.st) == hipSuccess &&
+                   hipEventRecord(l.done[k], l.st) == hipSuccess;
             k ^= 1;
         }
-        if (st) good = hipStreamSynchronize(st) == hipSuccess && good;
-        for (int k = 0; k < 2; k++) {
-            if (buf[k]) hipHostFree(buf[k]);
-            if (done[k]) hipEventDestroy(done[k]);
-        }
-        if (st) hipStreamDestroy(st);
-        if (!good) {
-            ok = false;
-            std::lock_guard<std::mutex> l(errMu);
-            err = "cannot read or upload " + what;
-        }
+        good = hipStreamSynchronize(l.st) == hipSuccess && good;
+        if (!good) ok = false;
     };
     std::vector<std::thread> th;
-    for (unsigned t = 1; t < nThreads; t++) th.emplace_back(work);
-    work();
+    for (unsigned t = 1; t < nThreads; t++) th.emplace_back(work, t);
+    if (nThreads) work(0);
     for (auto& t : th) t.join();
-    if (!ok) set_error(err);
+    if (!ok) set_error("cannot read or upload " + what);
     return ok;
 }
 
-bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t fileOff) {
+bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t fileOff, StageLanes* lanes) {
     const int fd = open(path.c_str(), O_RDONLY);
     if (fd < 0) { set_error("cannot read " + path); return false; }
     const bool ok = stage_to_device(
@@ -426,18 +445,18 @@ bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t
             }
             return true;
         },
-        dst, bytes, path);
+        dst, bytes, path, lanes);
     close(fd);
     return ok;
 }
 
-bool upload_to_device(const void* src, void* dst, uint64_t bytes) {
+bool upload_to_device(const void* src, void* dst, uint64_t bytes, StageLanes* lanes) {
     return stage_to_device(
         [&](char* buf, uint64_t at, uint64_t len) {
             std::memcpy(buf, (const char*)src + at, len);
             return true;
         },
-        dst, bytes, "host arrays");
+        dst, bytes, "host arrays", lanes);
 }
 
 // ---- range partition of the DB at split entries -------------------------

@@ -96,9 +96,27 @@ bool build_species_map(HostDb& db);
 bool load_db_files(const std::string& dir, HostDb& db, bool stream = false);
 // `bytes` of a file into device memory: parallel reads into pinned staging buffers, each uploaded
 // as soon as it is full (the file read and the PCIe upload overlap); false + set_error on failure
-bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t fileOff = 0);
+// Pinned staging buffers and streams of the uploads below, reused across calls (the current device's)
+struct StageLanes {
+    static constexpr unsigned kLanes = 8;
+    static constexpr uint64_t kChunk = 32ull << 20;
+    struct Lane {
+        hipStream_t st = nullptr;
+        char* buf[2] = {nullptr, nullptr};
+        hipEvent_t done[2] = {nullptr, nullptr};
+    };
+    int dev = 0;
+    bool ok = true;
+    Lane lane[kLanes];
+    explicit StageLanes(int device);
+    ~StageLanes();
+    StageLanes(const StageLanes&) = delete;
+    StageLanes& operator=(const StageLanes&) = delete;
+};
+bool read_to_device(const std::string& path, void* dst, uint64_t bytes, uint64_t fileOff = 0,
+                    StageLanes* lanes = nullptr);
 // the same from host memory (pageable: copied into the pinned buffers by the threads)
-bool upload_to_device(const void* src, void* dst, uint64_t bytes);
+bool upload_to_device(const void* src, void* dst, uint64_t bytes, StageLanes* lanes = nullptr);
 bool check_db(const HostDb& db);
 bool partition_bounds(const uint64_t* split, uint64_t nSplit, uint64_t D, int parts, std::vector<uint64_t>& start,
                       std::vector<uint64_t>& entry);
