@@ -1360,6 +1360,9 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // that removes the atomic could save in the join; 2: nor the read's stretch bounds (dirOff).
 __device__ int g_abRankFree = 0;
 __device__ int g_matchXcd = 0;
+__device__ int g_shareRuns = 1;
+
+void set_share_runs(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_shareRuns), &on, sizeof(int)); }
 
 void set_match_xcd(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on, sizeof(int)); }
 
@@ -1386,6 +1389,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
     __shared__ ProbeLine sLines[kStage ? 1 : kMatchLines];  // the block's probe lines (sorted queries)
     __shared__ uint64_t sLineP[kStage ? 1 : kMatchLines];   // and their run-index bases
+    __shared__ unsigned long long sTbl[kStage ? 1 : 512];     // run sharing: (AA rank + 1) << 8 | leader
     __shared__ unsigned long long sBase;
     static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
     const DbVal dbv{db};
@@ -1415,6 +1419,34 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
     uint32_t nGallop = 0;  // probe-line queries whose run the run index does not hold (gallop fallback)
+    // Run sharing (the reference's same-AA reuse, KmerMatcher.cpp:315-353: a query whose AA part
+    // equals the previous one's reuses its candidates): the block's queries with the same AA rank —
+    // 13% of the queries of a uniform config-3 batch, 42% of a skewed-abundance one (MTB_DUP_STATS) —
+    // elect one leader through an LDS hash table; only the leader reads the run index and the run's
+    // first records, the followers take them from LDS. Each query still selects its own candidates.
+    constexpr bool kShare = !kStage && kPer == 1;
+    const bool share = kShare && g_shareRuns && lines != nullptr;
+    bool follower = false;
+    uint32_t leadT = threadIdx.x;
+    if (share) {
+        for (uint32_t i = threadIdx.x; i < 512; i += 256) sTbl[i] = 0ull;
+        __syncthreads();
+        if (live[0]) {
+            const uint64_t rk = (key[0] & kAAMask) >> 24;
+            const unsigned long long want = ((rk + 1) << 8) | threadIdx.x;
+            uint32_t h = (uint32_t)((rk * 0x9E3779B97F4A7C15ull) >> 55);  // 9 bits
+            while (true) {
+                const unsigned long long old = atomicCAS(&sTbl[h], 0ull, want);
+                if (old == 0ull) break;  // the rank's leader
+                if ((old >> 8) == rk + 1) {
+                    follower = true;
+                    leadT = (uint32_t)(old & 255u);
+                    break;
+                }
+                h = (h + 1) & 511u;
+            }
+        }
+    }
     if (kStage && staged) {
         constexpr int kLoad = kMatchWin / 256;
         uint64_t v[kLoad];
@@ -1464,7 +1496,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         for (int j = 0; j < kPer; j++) {
             const uint64_t aa = key[j] & kAAMask, x = aa >> 24, L = x / kLineRanks;
             const uint32_t o = (uint32_t)(x - L * kLineRanks);
-            if (!live[j]) {
+            if (!live[j] || follower) {  // a follower takes its leader's run below
                 lo[j] = hi[j] = 0;
                 continue;
             }
@@ -1521,12 +1553,43 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         if (hi[j] + vOff > D - 1) hi[j] = D - 1 - vOff;  // the last DB k-mer is never a candidate
         if (lo[j] > hi[j]) hi[j] = lo[j];
         small[j] = !staged && live[j] && hi[j] - lo[j] <= 2;
-        if (small[j]) {
+        if (small[j] && !follower) {
             const DbRec r0 = db[lo[j]], r1 = db[lo[j] + 1];
             rv[j][0] = (uint64_t)r0.hi << 32 | r0.lo;
             rv[j][1] = (uint64_t)r1.hi << 32 | r1.lo;
             rt[j][0] = r0.tax;
             rt[j][1] = r1.tax;
+        }
+    }
+    if (kShare && share) {  // the leaders' runs to their followers, through the (now free) line stage
+        __syncthreads();    // every line scan of the block is done
+        uint64_t* sLo = reinterpret_cast<uint64_t*>(sLines);
+        uint64_t* sHi = sLo + 256;
+        uint64_t* sRv = sHi + 256;
+        uint32_t* sRt = reinterpret_cast<uint32_t*>(sRv + 512);
+        static_assert(kStage || (256 * 8 * 4 + 512 * 4) <= sizeof(ProbeLine) * kMatchLines, "results fit the line stage");
+        const uint32_t t = threadIdx.x;
+        if (!follower) {
+            sLo[t] = lo[0];
+            sHi[t] = hi[0];
+            if (small[0]) {
+                sRv[2 * t] = rv[0][0];
+                sRv[2 * t + 1] = rv[0][1];
+                sRt[2 * t] = rt[0][0];
+                sRt[2 * t + 1] = rt[0][1];
+            }
+        }
+        __syncthreads();
+        if (follower) {
+            lo[0] = sLo[leadT];
+            hi[0] = sHi[leadT];
+            small[0] = live[0] && hi[0] - lo[0] <= 2;
+            if (small[0]) {
+                rv[0][0] = sRv[2 * leadT];
+                rv[0][1] = sRv[2 * leadT + 1];
+                rt[0][0] = sRt[2 * leadT];
+                rt[0][1] = sRt[2 * leadT + 1];
+            }
         }
     }
     // long runs (direct join): scanned by the whole wave below, not by the lane
