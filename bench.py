@@ -288,6 +288,7 @@ def main():
     ap.add_argument("--c5-only", action="store_true", help="experiments: run the config-5 line alone")
     ap.add_argument("--ab", default="", help="experiments: 'name=K=V,K=V;name2=...' same-box A/B of the headline")
     ap.add_argument("--ab-repeat", type=int, default=2, help="--ab: rounds over the specs")
+    ap.add_argument("--ab-skewed", action="store_true", help="--ab on the skewed-abundance reads (--skew-sigma)")
     ap.add_argument("--skewed-pairs", type=int, default=10_000_000,
                     help="config 3: read pairs of the skewed-abundance line (log-normal genome abundance; 0 = off)")
     ap.add_argument("--skew-sigma", type=float, default=2.0,
@@ -972,7 +973,8 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
     got = {}
 
     def grab(seq, off):  # reads sampled from the true-signal genomes before they are freed
-        got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev)
+        got["reads"] = make_reads_gpu(seq, off, N, args.seed * 1000 + 31 + 17 * rank, dev,
+                                      abundance_sigma=args.skew_sigma if args.ab and args.ab_skewed else 0.0)
         if args.skewed_pairs > 0 and not variant:  # a skewed-abundance sample of the same genomes
             got["skewed"] = make_reads_gpu(seq, off, min(N, args.skewed_pairs), args.seed * 1000 + 41 + 17 * rank, dev,
                                            abundance_sigma=args.skew_sigma)
