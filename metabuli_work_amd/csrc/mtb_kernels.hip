@@ -1360,7 +1360,7 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // that removes the atomic could save in the join; 2: nor the read's stretch bounds (dirOff).
 __device__ int g_abRankFree = 0;
 __device__ int g_matchXcd = 0;
-__device__ int g_shareRuns = 1;
+__device__ int g_shareRuns = 0;
 
 void set_share_runs(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_shareRuns), &on, sizeof(int)); }
 
@@ -1424,6 +1424,9 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     // 13% of the queries of a uniform config-3 batch, 42% of a skewed-abundance one (MTB_DUP_STATS) —
     // elect one leader through an LDS hash table; only the leader reads the run index and the run's
     // first records, the followers take them from LDS. Each query still selects its own candidates.
+    // Measured (round 5, same box): no gain — uniform 55.7 -> 57.3 ms, skewed 54.4 -> 55.7 ms per batch:
+    // the repeated lookups hit the L2 already, and the barriers hold each block on its slowest leader.
+    // Off by default (MTB_SHARE_RUNS=1: on).
     constexpr bool kShare = !kStage && kPer == 1;
     const bool share = kShare && g_shareRuns && lines != nullptr;
     bool follower = false;

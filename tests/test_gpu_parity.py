@@ -145,7 +145,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:noshare", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -169,7 +169,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     # probe lines and run index built by per-k-mer global atomics (round 4's) instead of a wave per line
     monkeypatch.setenv("MTB_LINE_BUILD", "atomic" if mode == "atomiclines" else "wave")
     monkeypatch.setenv("MTB_MATCH_XCD", "1" if mode == "matchxcd" else "0")  # K4 blocks per XCD eighth
-    monkeypatch.setenv("MTB_SHARE_RUNS", "0" if mode == "noshare" else "1")  # same-AA queries share one lookup
+    monkeypatch.setenv("MTB_SHARE_RUNS", "1" if mode == "share" else "0")  # same-AA queries share one lookup
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
