@@ -39,7 +39,8 @@ from metabuli_work_amd.gpu_synth import make_genomes_gpu, make_long_reads_gpu, m
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-stage HBM bytes of one batch from this round's rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/measure_r04.sh + tools/stage_profile.py), one file per workload
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r04")
+# this round's PMC passes first; a workload not re-measured this round falls back to the previous one
+TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", "r05"), os.path.join(ROOT, "profiles", "r04")]
 # the six timed kernels of mtb_last_kernel_ms, by join path (mtb_last_stats[10])
 KERNELS_SORT = ["extract", "filter", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpose", "match_sort", "assign"]
@@ -123,19 +124,21 @@ def alg_bytes(bases, n, Qall, Q, M, D, live=None, probe=False, mates=2, dbread=0
 
 
 def load_traffic(workload, kmers, batch):
-    """Per-stage HBM bytes of one batch of this workload (profiles/r04/stage_traffic_<workload>.json,
-    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes over the same workload: tools/measure_r04.sh),
+    """Per-stage HBM bytes of one batch of this workload (profiles/r05/ or r04/stage_traffic_<workload>.json,
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes over the same workload: tools/measure_r05.sh),
     when the profiled DB and batch shape match this run's (the synthetic DB's size varies by a few
     k-mers per build)."""
-    path = os.path.join(TRAFFIC_DIR, f"stage_traffic_{workload}.json")
-    try:
-        with open(path) as f:
-            tf = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    if tf.get("batch") != batch or abs(tf.get("kmers", 0) - kmers) > 1e-3 * max(kmers, 1):
-        return None, None
-    return tf, os.path.relpath(path, ROOT)
+    for d in TRAFFIC_DIRS:
+        path = os.path.join(d, f"stage_traffic_{workload}.json")
+        try:
+            with open(path) as f:
+                tf = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tf.get("batch") != batch or abs(tf.get("kmers", 0) - kmers) > 1e-3 * max(kmers, 1):
+            continue
+        return tf, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def roofline_of(kern, names, alg, traffic):

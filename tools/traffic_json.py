@@ -17,7 +17,7 @@ if stages["filter"]["hbm_bytes"] == 0 and stages["extract"]["hbm_bytes"] > 0:
     stage_ms["stage_ms"]["filter"], stage_ms["stage_ms"]["extract"] = stage_ms["stage_ms"]["extract"], 0.0
 out = {"workload": w, "kmers": b["config"]["db_kmers"], "batch": batch,
        "source": f"rocprofv3 --kernel-trace (stage_time) and separate --pmc FETCH_SIZE / WRITE_SIZE passes of one "
-                 f"{w} batch after a warm-up batch (tools/measure_r04.sh, tools/stage_profile.py); FETCH_SIZE doubled "
+                 f"{w} batch after a warm-up batch (tools/measure_r05.sh, tools/stage_profile.py); FETCH_SIZE doubled "
                  f"per MI355X_MICROARCH.md; the fused K1 + K1F kernel (k_extract_filter) is the filter stage",
        "stages": stages, "stage_ms": stage_ms}
 print(json.dumps(out, indent=1))
