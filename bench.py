@@ -298,6 +298,8 @@ def main():
                     help="skewed line: sigma of the log-normal per-genome abundance")
     ap.add_argument("--cold-gtdb", type=int, default=1,
                     help="config 3: open the GTDB-scale DB from host diffIdx/info/split (mtb_open_host) and time it")
+    ap.add_argument("--cold-settle-s", type=float, default=8.0,
+                    help="GTDB cold open: idle seconds after freeing the resident DB (the driver's wipe of freed HBM)")
     ap.add_argument("--cold-pairs", type=int, default=10_000_000,
                     help="cold one-shot line: read pairs of the file classified by a freshly opened context (0 = off)")
     ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r04", "bench_detail.json"),
@@ -1151,11 +1153,12 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
         del rdb
         gc.collect()
         torch.cuda.empty_cache()
-        # settle the runtime's deferred release of the ~170 GB just freed (untimed): a fresh process
-        # opening its DB has nothing to release, and the first allocation after a large free waits
-        # for all of it
-        torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        # let the driver finish wiping the ~170 GB just freed (untimed): freed HBM is cleared in the
+        # background at ~33 GB/s and an allocation that needs it waits for that (tools/alloc_probe.hip:
+        # 144 GB allocated 4.3 s after a free, 0.000 s fresh or after 6 s idle); a fresh process
+        # opening its DB has nothing being wiped
         torch.cuda.synchronize()
+        time.sleep(args.cold_settle_s)
         cold_gtdb = run_cold_gtdb(args, host, odb, lp, local, reads, ores, otc)
         rdb = None
     if odb is not None:
