@@ -302,7 +302,7 @@ def main():
                     help="GTDB cold open: idle seconds after freeing the resident DB (the driver's wipe of freed HBM)")
     ap.add_argument("--cold-pairs", type=int, default=10_000_000,
                     help="cold one-shot line: read pairs of the file classified by a freshly opened context (0 = off)")
-    ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r04", "bench_detail.json"),
+    ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r05", "bench_detail.json"),
                     help="side file for the full result tree (per-kernel splits, work counters, config-5 parts, "
                          "e2e host stages); the stdout line keeps the headline and one-line summaries")
     args = ap.parse_args()
