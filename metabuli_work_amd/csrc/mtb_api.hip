@@ -142,6 +142,13 @@ struct mtb_ctx {
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     bool radixDigits = true;     // MTB_RADIX_DIGITS=0: K2's histograms read the keys, not 1-B digit side arrays
+    // MTB_K1F_BINS: the fused K1F writes straight into K2's first-pass buckets (1: batches of >= 2^22
+    // present-window slots, 2: every batch, 0: off, the default — measured even);
+    // MTB_K1F_BINS_RC forces the bucket size (tests)
+    int binnedSort = 0;
+    uint64_t binRcForce = 0;
+    bool binDigits = true;  // MTB_K1F_BINS_DIG=0: the binned K1F writes no second-pass digits (K2 reads the keys)
+    uint64_t binHost[kSortBins] = {};  // the last binned K1F's bucket counts
     bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
                                  // (with the sweep join the context then holds no probe lines either)
     uint32_t spillShift = 0;     // MTB_DIRECT=3: read stretches taken as a quarter (queries spill; tests)
@@ -183,6 +190,7 @@ struct mtb_ctx {
     DevBuf segLen;                          // K5: survivors of the thinned big segments (k_thin_big)
     DevBuf sizeLists;                       // K5: reads of each size class above 128 matches (k_size_lists)
     DevBuf digA, digB;                      // K2 digit side arrays (1 B per kept query k-mer, ping-pong)
+    DevBuf binCnt, binTab;                  // binned K1F: bucket counts (kSortBins u64), K2's tile table
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
@@ -449,6 +457,9 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
     if (const char* e = getenv("MTB_RADIX_DIGITS")) c->radixDigits = atoi(e) != 0;
+    if (const char* e = getenv("MTB_K1F_BINS")) c->binnedSort = atoi(e);
+    if (const char* e = getenv("MTB_K1F_BINS_RC")) c->binRcForce = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("MTB_K1F_BINS_DIG")) c->binDigits = atoi(e) != 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
@@ -658,6 +669,9 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->noAlias = src->noAlias;
     c->noFilter = src->noFilter;
     c->radixDigits = src->radixDigits;
+    c->binnedSort = src->binnedSort;
+    c->binRcForce = src->binRcForce;
+    c->binDigits = src->binDigits;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -668,7 +682,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
     return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
                       &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->digA, &c->digB, &c->local, &c->paths,
+                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->digA, &c->digB, &c->binCnt, &c->binTab, &c->local, &c->paths,
                       &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
                       &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
                       &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
@@ -994,9 +1008,41 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     HIP_TRY(hipEventRecord(c->kev[2], s));
     // K2's digit side arrays: the fused K1F writes each kept key's first-pass digit (bits kQuerySortLo..)
     const bool digits = fused && c->radixDigits && c->sortLoFine == kQuerySortLo;
+    uint64_t binRc = 0;  // > 0: the batch's K1F wrote K2's first-pass buckets of binRc slots
     if (fused) {
         uint64_t cap = std::min<uint64_t>(R, (uint64_t)((double)R * c->presentShare) + 4096);
-        for (int pass = 0; pass < 2; pass++) {
+        // binned K1F: 2048 buckets (first digit x XCD) of rc slots, 1/16 over the expected present
+        // share plus 256 (the digits are near-uniform: the bits are the middle of a base-21 rank); a
+        // bucket past rc sends the batch through the packed K1F once more (counted as a rerun)
+        bool binned = digits && c->binnedSort && (c->binnedSort == 2 || cap >= (1ull << 22));
+        for (int pass = 0; pass < 2 && binned; pass++) {
+            uint64_t rc = c->binRcForce ? c->binRcForce : (cap + cap / 16) / kSortBins + 256;
+            rc = (rc + 63) / 64 * 64;  // tile starts 16-B aligned for the digit loads
+            const uint64_t slots = rc * kSortBins;
+            HIP_TRY(c->keysB.ensure(8 * slots));
+            HIP_TRY(c->valsB.ensure(4 * slots));
+            HIP_TRY(c->digA.ensure(slots));
+            HIP_TRY(c->binCnt.ensure(sizeof(unsigned long long) * kSortBins));
+            Q = launch_extract_filter(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
+                                      c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
+                                      c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
+                                      c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
+                                      c->rankHi, &c->Qall, slots, false, s,
+                                      c->binDigits ? c->digA.as<uint8_t>() : nullptr,
+                                      c->binCnt.as<unsigned long long>(), rc, c->binHost);
+            HIP_TRY(hipGetLastError());
+            if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
+            bool over = false;
+            for (int r = 0; r < kSortBins; r++) over |= c->binHost[r] > rc;
+            if (!over) {
+                binRc = rc;
+                break;
+            }
+            c->stats[15]++;  // a bucket overflowed: rerun packed, sized by the count just taken
+            cap = std::min<uint64_t>(R, Q + Q / 8);
+            binned = false;
+        }
+        for (int pass = 0; pass < 2 && !binRc; pass++) {
             HIP_TRY(c->keysB.ensure(8 * cap));
             HIP_TRY(c->valsB.ensure(4 * cap));
             if (digits) HIP_TRY(c->digA.ensure(cap));
@@ -1039,7 +1085,20 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                            ? c->sortLoFine : kQuerySortLo;
     if (!probe) {
         bool inB = false;
-        if (filt) {
+        if (binRc) {  // the first pass was K1F's: the tile table over its buckets, then the rest
+            HIP_TRY(c->binTab.ensure(sizeof(uint64_t) * std::max<uint64_t>(radix_binned_tiles(c->binHost, binRc), 1)));
+            const uint64_t rcn = radix_counts_elems(Q) + 256ull * kSortBins;
+            HIP_TRY(c->radixCounts.ensure(sizeof(uint32_t) * rcn));
+            HIP_TRY(c->radixOffs.ensure(sizeof(uint64_t) * (rcn + 1)));
+            HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(rcn + n + 1)));
+            Q = radix_sort_binned(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
+                                  c->valsA.as<uint32_t>(), c->binHost, c->binCnt.as<unsigned long long>(), binRc,
+                                  kQuerySortLo, kQuerySortHi, c->radixCounts.as<uint32_t>(),
+                                  c->radixOffs.as<uint64_t>(), c->scanTmp.p, c->binTab.as<uint64_t>(), &inB, s,
+                                  c->binDigits ? c->digA.as<uint8_t>() : nullptr, c->digB.as<uint8_t>());
+            qk = inB ? c->keysA.as<uint64_t>() : c->keysB.as<uint64_t>();
+            qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
+        } else if (filt) {
             const bool dg = digits && sortLo == kQuerySortLo;
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
                                  c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,

@@ -575,13 +575,18 @@ constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
 __device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) { return (uint32_t)((k >> shift) & 0xFF); }
 
+__device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab, uint32_t tile, uint64_t n,
+                                                uint64_t& base, uint64_t& end);
+
 template <bool FILTER>
 __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
-                                                    uint32_t* __restrict__ counts, uint32_t nTiles) {
+                                                    uint32_t* __restrict__ counts, uint32_t nTiles,
+                                                    const uint64_t* __restrict__ tab = nullptr) {
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+    uint64_t base;
+    radix_tile_span(tab, blockIdx.x, n, base, n);
     uint64_t key[kRadixItems];
 #pragma unroll
     for (int k = 0; k < kRadixItems; k++) {
@@ -599,12 +604,29 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
 
 // The same histogram from a byte array of the pass's digits (written by the previous pass's scatter,
 // or by the fused K1F for the first): 1 B read per key instead of 8.
+// tab (nullable): tile t is [tab[t] >> 14, + (tab[t] & 0x3FFF)) instead of [t * kRadixTile, ...) up to n
+// (the buckets of a binned K1F; starts are multiples of 16).
+__device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab, uint32_t tile, uint64_t n,
+                                                uint64_t& base, uint64_t& end) {
+    if (tab) {
+        const uint64_t e = tab[tile];
+        base = e >> 14;
+        end = base + (e & 0x3FFFu);
+    } else {
+        base = (uint64_t)tile * kRadixTile;
+        end = n;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_radix_hist_dig(const uint8_t* __restrict__ dig, uint64_t n,
-                                                        uint32_t* __restrict__ counts, uint32_t nTiles) {
+                                                        uint32_t* __restrict__ counts, uint32_t nTiles,
+                                                        const uint64_t* __restrict__ tab) {
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+    uint64_t base, end;
+    radix_tile_span(tab, blockIdx.x, n, base, end);
+    n = end;
     constexpr int kVec = kRadixTile / kBlock / 16;  // uint4 loads per thread
     uint4 d[kVec];
     const bool full = base + kRadixTile <= n;
@@ -639,7 +661,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
                                                        uint64_t n, int shift, const uint64_t* __restrict__ offs,
                                                        uint32_t nTiles, uint64_t* __restrict__ keysOut,
                                                        V* __restrict__ valsOut, uint8_t* __restrict__ digOut,
-                                                       int nextShift, int xcdMap) {
+                                                       int nextShift, int xcdMap, const uint64_t* __restrict__ tab) {
     __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
@@ -656,7 +678,10 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3, q = nTiles >> 3, r = nTiles & 7u;
         tile = x * q + min(x, r) + i;
     }
-    const uint64_t base = (uint64_t)tile * kRadixTile + (uint64_t)w * kRadixSlice;
+    uint64_t tBase, tEnd;
+    radix_tile_span(tab, tile, n, tBase, tEnd);
+    n = tEnd;
+    const uint64_t base = tBase + (uint64_t)w * kRadixSlice;
     // the digit bases: one strided load per lane, issued first so its latency hides behind the
     // key loads (a dependent load per key in the write-out loop was the old bottleneck)
     const uint64_t digitBase = offs[(uint64_t)tid * nTiles + tile];
@@ -669,7 +694,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
     // all loads first (unguarded for the full tiles) so the 32 loads of a lane are in flight
     // together; interleaving them with the ranking serialised 16 memory round trips per tile
-    if ((uint64_t)(tile + 1) * kRadixTile <= n) {
+    if (tBase + kRadixTile <= n) {
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
 #pragma unroll
@@ -765,7 +790,7 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
         if (nTiles == 0) break;
         const bool f = first && filter, g = first && genVals;
-        if (digits) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles);
+        if (digits) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles, nullptr);
         else if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
@@ -774,10 +799,10 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         const char* xe = getenv("MTB_RADIX_XCD");
         const int xcd = xe ? atoi(xe) : 1;
         const int ns = shift + 8;
-        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
-        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
-        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
-        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd);
+        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
+        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
+        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
+        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
         std::swap(di, dg);
         if (f) {
             uint64_t kept = 0;
@@ -792,6 +817,68 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
     }
     return cur;
 }
+
+// The tile table of a binned K1F's buckets (radix_sort_binned): one block, thread t walks digit t's 8
+// regions (t * 8 .. t * 8 + 7: the regions in digit order), its tile count scanned over the block.
+__global__ void __launch_bounds__(256) k_bin_tiles(const unsigned long long* __restrict__ binCnt, uint64_t rc,
+                                                   uint64_t* __restrict__ tab) {
+    uint64_t cnt[8], nt = 0;
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        cnt[x] = min((uint64_t)binCnt[threadIdx.x * 8 + x], rc);
+        nt += (cnt[x] + kRadixTile - 1) / kRadixTile;
+    }
+    unsigned long long tot;
+    uint64_t o = block_exclusive_scan(nt, &tot);
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        const uint64_t r0 = (uint64_t)(threadIdx.x * 8 + x) * rc;
+        for (uint64_t i = 0; i < cnt[x]; i += kRadixTile) tab[o++] = (r0 + i) << 14 | min<uint64_t>(kRadixTile, cnt[x] - i);
+    }
+}
+
+uint64_t radix_binned_tiles(const uint64_t* binHost, uint64_t rc) {
+    uint64_t nt = 0;
+    for (int r = 0; r < kSortBins; r++) nt += (std::min<uint64_t>(binHost[r], rc) + kRadixTile - 1) / kRadixTile;
+    return nt;
+}
+
+template <typename V>
+uint64_t radix_sort_binned(uint64_t* keysR, V* valsR, uint64_t* keysT, V* valsT, const uint64_t* binHost,
+                           const unsigned long long* binDev, uint64_t rc, int bitLo, int bitHi, uint32_t* counts,
+                           uint64_t* offs, void* scanTmp, uint64_t* tileTab, bool* inT, hipStream_t s, uint8_t* digR,
+                           uint8_t* digT) {
+    static_assert(kRadixTile < (1 << 14), "tile length in 14 bits");
+    uint64_t Q = 0;
+    for (int r = 0; r < kSortBins; r++) Q += binHost[r];
+    const uint32_t nTiles = (uint32_t)radix_binned_tiles(binHost, rc);
+    *inT = false;
+    if (!nTiles || bitLo + 8 >= bitHi) return Q;
+    // the second pass (bits bitLo + 8 ..) over the buckets in order -> (keysT, valsT) from slot 0
+    k_bin_tiles<<<1, kBlock, 0, s>>>(binDev, rc, tileTab);
+    const int shift = bitLo + 8, ns = shift + 8;
+    if (digR) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(digR, 0, counts, nTiles, tileTab);
+    else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(keysR, 0, shift, counts, nTiles, tileTab);  // no K1F digits
+    exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
+    const char* xe = getenv("MTB_RADIX_XCD");
+    const int xcd = xe ? atoi(xe) : 1;
+    k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(keysR, valsR, 0, shift, offs, nTiles, keysT, valsT,
+                                                              ns < bitHi ? digT : nullptr, ns, xcd, tileTab);
+    *inT = true;
+    if (ns < bitHi) {  // the rest: plain passes over the Q contiguous pairs
+        bool inB = false;
+        // (without K1F digits, digR is null: one remaining pass never writes the second digit array)
+        uint8_t* dOther = digR ? digR : (ns + 8 >= bitHi ? digT : nullptr);
+        radix_sort_pairs(keysT, valsT, keysR, valsR, Q, ns, bitHi, false, false, counts, offs, scanTmp, &inB, s, digT,
+                         dOther);
+        *inT = !inB;
+    }
+    return Q;
+}
+
+template uint64_t radix_sort_binned<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, const uint64_t*,
+                                              const unsigned long long*, uint64_t, int, int, uint32_t*, uint64_t*,
+                                              void*, uint64_t*, bool*, hipStream_t, uint8_t*, uint8_t*);
 
 template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
                                              uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*);
@@ -1864,7 +1951,8 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 // end: same-address atomics are what the kernel waits on when it has no probes to make (round 4:
 // a per-wave-per-group counter atomic tripled the probe-free pass, `MTB_AB_FILTER=1`). Output: qkey /
 // qslot as k_filter's (slot = the window's K1 slot).
-template <int kPer, bool kJMajor>
+constexpr uint32_t kBinStage = 2560;  // binned K1F: windows per group staged in LDS (a group keeps ~1.9k at GTDB scale)
+template <int kPer, bool kJMajor, bool kBinned = false>
 __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -1873,8 +1961,14 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                                                         uint64_t* __restrict__ unitInfo, const ProbeLine* __restrict__ lines,
                                                         uint64_t* __restrict__ qkey, uint32_t* __restrict__ qslot,
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
-                                                        uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig) {
+                                                        uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig,
+                                                        unsigned long long* __restrict__ binCnt, uint64_t binRc) {
     __shared__ uint8_t sBase[256];
+    __shared__ uint32_t sBin[256];
+    __shared__ uint32_t sBinBase[256];
+    // binned output's LDS stage (below): dynamic, launched only with binRc, so the packed form keeps
+    // its occupancy
+    extern __shared__ uint64_t sStageKey[];  // kBinStage keys, then kBinStage slots (as u32 at 2 kBinStage + i)
     __shared__ int8_t sAA[64], sNum[64];
     __shared__ unsigned long long sOut;
     __shared__ uint32_t sMaxWin, sCnt[kPer * kWaves], sEx[kWaves][64];
@@ -1951,6 +2045,77 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
         // this group's second barrier, by which every thread has read them; sOut after the next
         // group's first, by which every thread has read it)
         static_assert(kPer * kWaves <= 64, "one count per lane");
+        if constexpr (kBinned) {
+            // binned output (K2's first pass folded in): each present window goes straight into the
+            // bucket of its first sort digit d (key bits kQuerySortLo..+8) — region d * 8 + XCD of
+            // binRc slots, digit-major, so the regions in order are the first pass's output; the
+            // order inside a region is free (the first LSD pass need not be stable). Per group: a
+            // block histogram of the digits, one space reservation per non-empty bucket, three
+            // barriers. Blocks are dealt
+            // round-robin over the 8 XCDs, so a region's consecutive reservations come from one L2,
+            // which completes the lines the short runs leave partial. A bucket past binRc is counted
+            // only (the caller reruns the batch unbinned). The side digit written is the second
+            // pass's (bits kQuerySortLo + 8..).
+            const uint32_t xcd = blockIdx.x & 7u;
+            sBin[threadIdx.x] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPer; j++)
+                if ((mask >> j) & 1u) atomicAdd(&sBin[(uint32_t)(k[j] >> kQuerySortLo) & 0xFFu], 1u);
+            __syncthreads();
+            // the reservation, then the block scan of the bucket counts while it is in flight; then
+            // each window takes a slot of its digit's run in an LDS stage, and the stage leaves in
+            // digit order — consecutive threads write consecutive slots of one bucket, so a store
+            // instruction covers a few short runs instead of 64 lines (the unstaged form cost the
+            // fused kernel 10 ms per 3.33M-pair batch). Windows past the stage are written directly.
+            const uint32_t nb = sBin[threadIdx.x];
+            const uint32_t gb = nb ? (uint32_t)atomicAdd(binCnt + threadIdx.x * 8u + xcd, (unsigned long long)nb) : 0u;
+            unsigned long long tot;
+            const uint32_t st = (uint32_t)block_exclusive_scan(nb, &tot);
+            sBin[threadIdx.x] = st;  // the digit's stage cursor
+            // bucket slot of stage entry i of digit d: sBinBase[d] + i (mod 2^32). When the whole group
+            // fits the stage (block-uniform), it is stored after the staging, so the reservation's
+            // round trip overlaps it; else before, for the windows written directly
+            const bool fits = tot <= kBinStage;
+            if (!fits) sBinBase[threadIdx.x] = gb - st;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                if (!((mask >> j) & 1u)) continue;
+                const uint32_t d = (uint32_t)(k[j] >> kQuerySortLo) & 0xFFu;
+                const uint32_t p = atomicAdd(&sBin[d], 1u);
+                const uint32_t slot = (uint32_t)(slotBase + 64ull * (g + j));
+                if (p < kBinStage) {
+                    sStageKey[p] = k[j];
+                    reinterpret_cast<uint32_t*>(sStageKey)[2 * kBinStage + p] = slot;
+                } else {
+                    const uint32_t at = sBinBase[d] + p;
+                    if (at < binRc) {
+                        const uint64_t pos = (uint64_t)(d * 8u + xcd) * binRc + at;
+                        qkey[pos] = k[j];
+                        qslot[pos] = slot;
+                        if (qdig) qdig[pos] = (uint8_t)(k[j] >> (kQuerySortLo + 8));
+                    }
+                }
+            }
+            if (fits) sBinBase[threadIdx.x] = gb - st;
+            __syncthreads();
+            const uint32_t nst = min((uint32_t)tot, (uint32_t)kBinStage);
+            for (uint32_t i = threadIdx.x; i < nst; i += blockDim.x) {
+                const uint64_t key = sStageKey[i];
+                const uint32_t d = (uint32_t)(key >> kQuerySortLo) & 0xFFu;
+                const uint32_t at = sBinBase[d] + i;
+                if (at < binRc) {
+                    const uint64_t pos = (uint64_t)(d * 8u + xcd) * binRc + at;
+                    qkey[pos] = key;
+                    qslot[pos] = reinterpret_cast<const uint32_t*>(sStageKey)[2 * kBinStage + i];
+                    if (qdig) qdig[pos] = (uint8_t)(key >> (kQuerySortLo + 8));
+                }
+            }
+            // sBin / sBinBase / the stage are rewritten after the next group's first barrier, by which
+            // every thread has read them
+            continue;
+        }
         uint32_t myCnt = 0;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
@@ -1990,7 +2155,13 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen,
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
-                               uint64_t cap, bool threadMajor, hipStream_t s, uint8_t* qdig) {
+                               uint64_t cap, bool threadMajor, hipStream_t s, uint8_t* qdig,
+                               unsigned long long* binCnt, uint64_t binRc, uint64_t* binHost) {
+    if (binRc) {
+        // binned output: the writes go to 2048 regions of binRc slots; the bucket counts come back
+        threadMajor = false;
+        hipMemsetAsync(binCnt, 0, kSortBins * sizeof(unsigned long long), s);
+    }
     hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s);
     if (nUnits) {
         const uint64_t threads = (nUnits + 63) / 64 * 64;
@@ -1998,11 +2169,16 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
         static const int per = getenv("MTB_FILTER_PER") && atoi(getenv("MTB_FILTER_PER")) == 8 ? 8 : 16;
         const bool jMajor = !threadMajor;
         const unsigned blocks = (unsigned)((threads + 255) / 256);
+        const size_t lds = binRc ? kBinStage * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
 #define MTB_EF(P, J)                                                                                                  \
-    k_extract_filter<P, J><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,           \
+    k_extract_filter<P, J, false><<<blocks, 256, lds, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,         \
                                                   extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
-                                                  qslot, counter, rankLo, rankHi, cap, qdig)
-        if (per == 8) {
+                                                  qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc)
+        if (binRc) {
+            k_extract_filter<kFilterPer, true, true><<<blocks, 256, lds, s>>>(
+                seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
+                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc);
+        } else if (per == 8) {
             if (jMajor) MTB_EF(8, true);
             else MTB_EF(8, false);
         } else {
@@ -2013,8 +2189,13 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     }
     unsigned long long Q[2] = {0, 0};
     hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
+    if (binRc) hipMemcpyAsync(binHost, binCnt, kSortBins * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     *emitted = Q[1];
+    if (binRc) {
+        Q[0] = 0;
+        for (int r = 0; r < kSortBins; r++) Q[0] += binHost[r];
+    }
     // MTB_AB_FILTER=1 (diagnostics; results unaffected): after the real pass, two timed passes that
     // write no output (cap 0) and count into a scratch word — with the probes, and with none (an empty
     // rank range) — to split the kernel's time between the probe-line reads, the scan and the packing
@@ -2029,11 +2210,11 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
             hipEventRecord(ev[0], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr);
+                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0);
             hipEventRecord(ev[1], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr);
+                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0);
             hipEventRecord(ev[2], s);
             hipStreamSynchronize(s);
             float a = 0, b = 0;

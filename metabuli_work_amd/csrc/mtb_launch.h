@@ -105,6 +105,19 @@ template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
                           hipStream_t s, uint8_t* digA = nullptr, uint8_t* digB = nullptr);
+// K2 after a binned K1F (binRc > 0 above): the pairs already sit in the first pass's buckets —
+// kSortBins regions of rc slots, region d * 8 + XCD for first digit d (bits [bitLo, bitLo + 8)), the
+// region counts in binDev (device) and binHost (host copy) — with each key's second-pass digit in
+// digR. Sorts the remaining passes through a tile table over the regions (tileTab: at least
+// radix_binned_tiles(binHost, rc) entries); counts / offs sized radix_counts_elems(Q) + 256 * kSortBins.
+// Returns Q; *inT: the result is in (keysT, valsT), else in (keysR, valsR) from slot 0.
+constexpr int kSortBins = 2048;
+uint64_t radix_binned_tiles(const uint64_t* binHost, uint64_t rc);
+template <typename V>
+uint64_t radix_sort_binned(uint64_t* keysR, V* valsR, uint64_t* keysT, V* valsT, const uint64_t* binHost,
+                           const unsigned long long* binDev, uint64_t rc, int bitLo, int bitHi, uint32_t* counts,
+                           uint64_t* offs, void* scanTmp, uint64_t* tileTab, bool* inT, hipStream_t s, uint8_t* digR,
+                           uint8_t* digT);
 // format-2 DB values -> resident rank form (mtb_kernels.hip, to_rank_form); host inverse for getters
 void launch_to_rank_form(uint64_t* v, uint64_t n, hipStream_t s);
 uint64_t host_from_rank_form(uint64_t v);
@@ -187,7 +200,8 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
                                uint64_t cap, bool threadMajor, hipStream_t s,
-                               uint8_t* qdig = nullptr);
+                               uint8_t* qdig = nullptr, unsigned long long* binCnt = nullptr, uint64_t binRc = 0,
+                               uint64_t* binHost = nullptr);
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                        uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
                        uint64_t* emitted, hipStream_t s);

@@ -102,8 +102,7 @@ def test_stage_parity(make_db, db_name, kind):
         # K1 + K2: the multiset of query k-mers (blank reserved slots dropped, and those whose AA
         # 8-mer is absent from the DB: they cannot match, KmerMatcher.cpp compares AA parts first)
         gk = clf.query_kmers()
-        ok = okmers[info_seq(okmers["info"]) != 0]
-        ok = ok[np.isin(_aa_rank(ok["value"], par.kmerFormat), _db_aa_ranks(db_dir, par.kmerFormat))]
+        ok = okmers_present(okmers, db_dir, par)
         assert len(gk) == len(ok) == clf.stats()["query_kmers"]
         # mtb_last_counts: the reference's "Query k-mer number" (KmerMatcher.cpp:143-152), every
         # non-blank query k-mer before any DB test
@@ -127,6 +126,12 @@ def test_stage_parity(make_db, db_name, kind):
     odb.close()
 
 
+def okmers_present(okmers, db_dir, par):
+    """The oracle's query k-mers K1F keeps: non-blank, AA 8-mer present in the DB."""
+    ok = okmers[info_seq(okmers["info"]) != 0]
+    return ok[np.isin(_aa_rank(ok["value"], par.kmerFormat), _db_aa_ranks(db_dir, par.kmerFormat))]
+
+
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
 def test_end_to_end_batches(make_db, db_name):
     """Whole path, several batches, against oracle classify."""
@@ -145,7 +150,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -170,6 +175,11 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_LINE_BUILD", "atomic" if mode == "atomiclines" else "wave")
     monkeypatch.setenv("MTB_MATCH_XCD", "1" if mode == "matchxcd" else "0")  # K4 blocks per XCD eighth
     monkeypatch.setenv("MTB_SHARE_RUNS", "1" if mode == "share" else "0")  # same-AA queries share one lookup
+    # K1F writing straight into K2's first-pass buckets at any batch size; with 64-slot buckets, which
+    # overflow, so the batch reruns through the packed K1F
+    monkeypatch.setenv("MTB_K1F_BINS", "2" if mode.startswith("bins") else "0")
+    monkeypatch.setenv("MTB_K1F_BINS_RC", "64" if mode == "binsover" else "0")
+    monkeypatch.setenv("MTB_K1F_BINS_DIG", "0" if mode == "binsnodig" else "1")  # K2's second pass reads the keys
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
@@ -186,6 +196,12 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
         gm = clf.matches()
         assert len(gm) == len(omatches) == br.matches
         assert np.array_equal(gm, omatches)
+        if mode.startswith("bins"):  # K2's order after the binned first pass (or its packed rerun)
+            gk = clf.query_kmers()
+            pre = _aa_rank(gk["value"], par.kmerFormat) >> np.uint64(12)
+            assert len(gk) == clf.stats()["query_kmers"] and np.all(pre[1:] >= pre[:-1])
+            assert np.array_equal(_kmer_sorted(gk), _kmer_sorted(okmers_present(okmers, db_dir, par)))
+            assert clf.stats()["filter_reruns"] == (1 if mode == "binsover" else 0)
         if mode == "spill":
             assert clf.stats()["spilled_matches"] > 0
             ores, otc = oc.classify(odb, opar, reads)
