@@ -679,13 +679,27 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
 
 // Every grow-only batch buffer of a context (freed by mtb_close; their sum is the context's
 // workspace, mtb::ctx_workspace_bytes).
+#define MTB_BATCH_BUFS(X) \
+    X(seq1) X(off1) X(seq2) X(off2) X(meta) X(reserve) X(slotOff) X(qlen) X(scanTmp) X(keysA) X(valsA) X(keysB) \
+    X(valsB) X(radixCounts) X(radixOffs) X(readCnt) X(mOff) X(matches) X(matchesSorted) X(segScratch) X(maxSeg) \
+    X(errFlag) X(ordKA) X(ordVA) X(ordKB) X(ordVB) X(matchWin) X(unitRead) X(unitInfo) X(waveList) X(waveCount) \
+    X(devStats) X(mStage) X(mRank) X(mDirect) X(ovFlag) X(mTotal) X(qFrom) X(probeStats) X(longList) X(longCnt) \
+    X(qStart) X(chunkIn) X(chunkCnt) X(chunkSrcOff) X(liveCnt) X(liveOff) X(segLen) X(sizeLists) X(digA) \
+    X(digB) X(binCnt) X(binTab) X(local) X(paths) X(comb) X(conn) X(spScore) X(spKeep) X(gFlag) X(sFlag) \
+    X(pathCnt) X(gScan) X(sScan) X(gStart) X(sStart) X(clade) X(tcPool) X(tcLen) X(tcOff) X(tcOut) X(results) \
+    X(emMap) X(emCnt) X(emScratch) X(emPacked) X(emCnt32) X(emOff) X(maskOut1) X(maskOut2) X(maskProb) \
+    X(maskScale)
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
-    return {&c->seq1, &c->off1, &c->seq2, &c->off2, &c->meta, &c->reserve, &c->slotOff, &c->qlen,
-                      &c->scanTmp, &c->keysA, &c->valsA, &c->keysB, &c->valsB, &c->radixCounts,
-                      &c->radixOffs, &c->readCnt, &c->mOff, &c->matches, &c->matchesSorted, &c->segScratch, &c->maxSeg, &c->errFlag, &c->ordKA, &c->ordVA, &c->ordKB, &c->ordVB, &c->matchWin, &c->unitRead, &c->unitInfo, &c->waveList, &c->waveCount, &c->devStats, &c->mStage, &c->mRank, &c->mDirect, &c->ovFlag, &c->mTotal, &c->qFrom, &c->probeStats, &c->longList, &c->longCnt, &c->qStart, &c->chunkIn, &c->chunkCnt, &c->chunkSrcOff, &c->liveCnt, &c->liveOff, &c->segLen, &c->sizeLists, &c->digA, &c->digB, &c->binCnt, &c->binTab, &c->local, &c->paths,
-                      &c->comb, &c->conn, &c->spScore, &c->spKeep, &c->gFlag, &c->sFlag, &c->pathCnt, &c->gScan, &c->sScan, &c->gStart, &c->sStart, &c->clade, &c->tcPool, &c->tcLen,
-                      &c->tcOff, &c->tcOut, &c->results, &c->emMap, &c->emCnt, &c->emScratch, &c->emPacked,
-                      &c->emCnt32, &c->emOff, &c->maskOut1, &c->maskOut2, &c->maskProb, &c->maskScale};
+#define MTB_BUF_PTR(n) &c->n,
+    return {MTB_BATCH_BUFS(MTB_BUF_PTR)};
+#undef MTB_BUF_PTR
+}
+
+static const char* const* batch_buf_names() {
+#define MTB_BUF_NAME(n) #n,
+    static const char* const names[] = {MTB_BATCH_BUFS(MTB_BUF_NAME)};
+#undef MTB_BUF_NAME
+    return names;
 }
 
 void mtb_close(mtb_ctx* c) {
@@ -1544,6 +1558,19 @@ static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, cons
     HIP_TRY(hipEventElapsedTime(&c->stageMs[4], c->ev[0], c->ev[4]));
     for (int k = 0; k < mtb_ctx::kNumKern; k++)
         HIP_TRY(hipEventElapsedTime(&c->kernMs[k], c->kev[2 * k], c->kev[2 * k + 1]));
+    if (const char* e = getenv("MTB_WS_REPORT"); e && atoi(e)) {  // diagnostics: the batch buffers >= 256 MB
+        const std::vector<DevBuf*> bufs = batch_bufs(c);
+        const char* const* names = batch_buf_names();
+        std::vector<std::pair<uint64_t, const char*>> big;
+        for (size_t i = 0; i < bufs.size(); i++)
+            if (bufs[i]->bytes >= (256ull << 20)) big.push_back({bufs[i]->bytes, names[i]});
+        std::sort(big.begin(), big.end(), [](auto& a, auto& b) { return a.first > b.first; });
+        fprintf(stderr, "[mtb ws] %u reads, Q %llu, M %llu, live %llu: workspace %.2f GB (K6 scratch aliased %.2f GB):",
+                n, (unsigned long long)c->Q, (unsigned long long)c->M, (unsigned long long)c->liveM,
+                ctx_workspace_bytes(c) / 1e9, c->aliasBytes / 1e9);
+        for (auto& b : big) fprintf(stderr, " %s %.2f", b.second, b.first / 1e9);
+        fprintf(stderr, "\n");
+    }
     return err ? batch_error(err) : MTB_OK;
 }
 

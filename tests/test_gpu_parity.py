@@ -358,23 +358,25 @@ def test_choose_taxon_kernels(make_db, db_name, kind, wave, monkeypatch):
 @pytest.mark.parametrize("db_name,kind", [("fmt2", "paired"), ("fmt2", "long"), ("fmt2_syncmer", "paired"),
                                           ("fmt1", "paired"), ("fmt1", "single")])
 @pytest.mark.parametrize("mode", ["default", "nom64", "hbm", "mixed", "spill", "nofilter", "perblock", "persist",
-                                  "small"])
+                                  "small", "retry", "retrynofilter"])
 def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
     """K4S, the DB-sweep join (MTB_JOIN=sweep: DB tiles ending at sort-prefix bucket bounds staged in
     LDS, each tile's queries searched there): the oracle's matches and results with tiles of the
     default size, many small tiles (MTB_SWEEP_NOM=64), every tile searched in HBM (MTB_SWEEP_LDS=0:
     the path of a bucket longer than an LDS tile), a mix (MTB_SWEEP_LDS=80), and queries spilling
     past their read's stretch (MTB_DIRECT=3), and every non-blank window sorted and swept with no
-    membership filter (MTB_FILTER=0: no K1F, no probe lines)."""
+    membership filter (MTB_FILTER=0: no K1F, no probe lines); and the direct join's staged rerun
+    (MTB_DIRECT=2), which needs the match windows the sweep does not build, with and
+    without the filter."""
     monkeypatch.setenv("MTB_JOIN", "sweep")
-    monkeypatch.setenv("MTB_FILTER", "0" if mode == "nofilter" else "1")
+    monkeypatch.setenv("MTB_FILTER", "0" if mode.endswith("nofilter") else "1")
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
     monkeypatch.setenv("MTB_SWEEP_SMALL", "1" if mode == "small" else "0")
     monkeypatch.setenv("MTB_SWEEP_NOM", "64" if mode in ("nom64", "mixed") else "2048")
     monkeypatch.setenv("MTB_SWEEP_LDS", {"hbm": "0", "mixed": "80"}.get(mode, "4096"))
-    monkeypatch.setenv("MTB_DIRECT", "3" if mode == "spill" else "1")
+    monkeypatch.setenv("MTB_DIRECT", {"spill": "3", "retry": "2", "retrynofilter": "2"}.get(mode, "1"))
     db_dir, taxo, gen = make_db(db_name)
     par = _params(db_dir, SEQ_MODE[kind])
     reads = _reads(gen, kind, 1500 if kind != "long" else 60, seed=79)
@@ -390,7 +392,7 @@ def test_sweep_join(make_db, db_name, kind, mode, monkeypatch):
         assert np.array_equal(gm, omatches)
         matched = clf.stats()["matched_queries"]
         assert 0 < matched <= clf.stats()["query_kmers"]
-        if mode == "nofilter":  # every non-blank window went to the join
+        if mode.endswith("nofilter"):  # every non-blank window went to the join
             assert clf.stats()["query_kmers"] == br.query_kmers == int((info_seq(okmers["info"]) != 0).sum())
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
         if mode == "spill" and kind != "long" and db_name != "fmt2_syncmer":  # (long reads, syncmers: few matches per stretch)
