@@ -569,11 +569,20 @@ struct PeerLinks {
         if (!bytes) return true;
         if (direct[a * n + b]) return hipMemcpyPeerAsync(dst, dev[a], src, dev[b], bytes, st) == hipSuccess;
         constexpr size_t kBounce = 64u << 20;
-        thread_local char* bounce = nullptr;  // one pinned buffer per copying thread, kept for the process
-        if (!bounce && hipHostMalloc((void**)&bounce, kBounce, hipHostMallocDefault) != hipSuccess) {
-            bounce = nullptr;
+        // one pinned buffer per copying thread, freed when the thread ends (a run's workers end with it;
+        // thread-storage objects of the main thread go before the runtime's static teardown)
+        struct Bounce {
+            char* p = nullptr;
+            ~Bounce() {
+                if (p) (void)hipHostFree(p);
+            }
+        };
+        thread_local Bounce tb;
+        if (!tb.p && hipHostMalloc((void**)&tb.p, kBounce, hipHostMallocDefault) != hipSuccess) {
+            tb.p = nullptr;
             return false;
         }
+        char* const bounce = tb.p;
         if (hipStreamSynchronize(st) != hipSuccess) return false;  // earlier work on st first
         for (size_t off = 0; off < bytes; off += kBounce) {
             const size_t len = std::min(kBounce, bytes - off);
