@@ -149,13 +149,20 @@ def roofline_of(kern, names, alg, traffic):
     achieved = alg[dname] / (kern[dom] * 1e-3) / 1e9
     tf, src = traffic
     hbm = tf["stages"][dname]["hbm_bytes"] if tf and dname in tf.get("stages", {}) else None
-    return {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": hbm,
-            "traffic_source": src if hbm is not None else None, "alg_bytes_per_launch": int(alg[dname]),
-            "avg_launch_ms": round(float(kern[dom]), 3)}
+    out = {"bound": "hbm", "kernel": dname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": hbm,
+           "traffic_source": src if hbm is not None else None, "alg_bytes_per_launch": int(alg[dname]),
+           "avg_launch_ms": round(float(kern[dom]), 3)}
+    if hbm is not None:  # the HBM bytes it moves (random reads move 128-B lines) over its time
+        out["traffic_gb_per_s"] = round(hbm / (kern[dom] * 1e-3) / 1e9, 1)
+    return out
 
 
 RANDOM_GATHER = os.path.join(ROOT, "profiles", "r01", "random_gather.json")
+# round 5 (tools/calib_random_fetch.sh): each of those random loads is one 128-B memory-side request
+# (TCC_EA0_RDREQ_128B = loads), so the ceiling above is the HBM's bandwidth at 128-B lines
+RANDOM_LINE_BYTES = 128
+RANDOM_CALIBRATION = os.path.join(ROOT, "profiles", "r05", "random_fetch_calibration.json")
 
 
 def random_roofline(kern, names, Qall, Q, matched, M, D, sweep=False):
@@ -185,7 +192,9 @@ def random_roofline(kern, names, Qall, Q, matched, M, D, sweep=False):
         got = r / (ms * 1e-3) / 1e9
         out[k] = {"requests_per_launch": int(r), "achieved_greq_per_s": round(got, 2),
                   "ceiling_greq_per_s": ceiling(gb), "frac": round(got / ceiling(gb), 3),
-                  "source": os.path.relpath(RANDOM_GATHER, ROOT)}
+                  "ceiling_tb_per_s_at_128B": round(ceiling(gb) * RANDOM_LINE_BYTES / 1e3, 2),
+                  "source": os.path.relpath(RANDOM_GATHER, ROOT),
+                  "line_bytes_source": os.path.relpath(RANDOM_CALIBRATION, ROOT)}
     return out
 
 
@@ -427,7 +436,7 @@ def _pick(d, keys):
 
 def _roof(r):
     return _pick(r, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
-                     "alg_bytes_per_launch", "avg_launch_ms"))
+                     "alg_bytes_per_launch", "avg_launch_ms", "traffic_gb_per_s"))
 
 
 def _cpu(c):
@@ -468,7 +477,8 @@ def compact_line(out, detail_path):
     line["roofline"] = _roof(out.get("roofline"))
     line["cpu_baseline"] = _cpu(out.get("cpu_baseline"))
     if isinstance(out.get("random_roofline"), dict):
-        line["random_roofline"] = {k: _pick(v, ("frac", "achieved_greq_per_s", "ceiling_greq_per_s"))
+        line["random_roofline"] = {k: _pick(v, ("frac", "achieved_greq_per_s", "ceiling_greq_per_s",
+                                                "ceiling_tb_per_s_at_128B"))
                                    for k, v in out["random_roofline"].items()}
     if isinstance(out.get("pipeline_roofline"), dict):
         line["pipeline_roofline"] = _pick(out["pipeline_roofline"], ("achieved", "frac", "alg_bytes"))
