@@ -91,9 +91,16 @@ struct ErrorBox {
 };
 
 constexpr uint32_t kBlockReads = 8192;
-// parsed jobs a mate may hold ahead of the assembler: more than a 1M-read batch (~122 jobs), so the
-// splitter and the parsers keep going while the assembler fills and uploads a batch
-constexpr size_t kJobsAhead = 160;
+// parsed jobs a mate may hold ahead of the assembler: two full batches (a batch of up to 2.6M
+// 150-bp pairs is ~320 jobs of kBlockReads), so the splitter and the parsers run a batch ahead while
+// the assembler fills and uploads one (160 — less than one 1.55M-pair batch — held the splitter in
+// lockstep with the assembler: DESIGN §5 round 5). MTB_JOBS_AHEAD overrides it (A/B).
+constexpr size_t kJobsAhead = 640;
+static size_t jobs_ahead() {
+    const char* e = getenv("MTB_JOBS_AHEAD");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (size_t)v : kJobsAhead;
+}
 // and at most this many raw bytes per job (long reads: 8192 records would be ~80 MB a job)
 constexpr size_t kJobBytes = 4u << 20;
 constexpr int kSlots = 3;
@@ -188,6 +195,13 @@ struct Mapping {
     void release_part(size_t c) {  // the splitter is past part c
         if (--refs[c] == 0) drop(c);
     }
+    // a hold on part c only while it is still mapped (refs > 0), for the prefaulter
+    bool try_hold(size_t c) {
+        int r = refs[c].load();
+        while (r > 0 && !refs[c].compare_exchange_weak(r, r + 1)) {
+        }
+        return r > 0;
+    }
     ~Mapping() {
         for (size_t c = 0; c < parts; c++)
             if (!gone[c]) munmap((void*)(p + c * kPart), std::min(kPart, n - c * kPart));
@@ -272,7 +286,7 @@ struct MateReader {
     size_t head = 1u << 20;       // headroom for the unfinished record of the previous buffer
     size_t rawBytes = 32u << 20;  // raw buffer (MTB_PARSE_BUFFER: tests cut records at buffer ends)
     std::unique_ptr<mtb::ByteSource> src;
-    BoundedQueue<std::shared_ptr<ParseJob>> out{kJobsAhead}, work{kJobsAhead};
+    BoundedQueue<std::shared_ptr<ParseJob>> out{jobs_ahead()}, work{jobs_ahead()};
     struct Chunk {
         std::shared_ptr<RawBuf> buf;
         size_t got = 0;  // bytes at buf->p + head
@@ -314,12 +328,50 @@ struct MateReader {
 
     std::shared_ptr<Mapping> mapped;  // a plain file: split in place
 
+    // The mapped file's page tables filled ahead of the splitter by a helper thread: on a fresh
+    // mapping half of the splitter's scan time was page faults (a 1.25-GB tmpfs FASTQ: scan 0.151 s
+    // cold, 0.079 s prefaulted). Parts of kPart bytes, at most kAhead parts ahead of the splitter,
+    // each under a hold so it cannot be unmapped while touched. MTB_PREFAULT=0 turns it off (A/B).
+    static constexpr size_t kAhead = 4;
+    std::atomic<size_t> splitPos{0};
+    std::atomic<bool> splitDone{false};
+    void prefault_loop() {
+        const char* p = mapped->p;
+        const size_t n = mapped->n;
+        for (size_t c = 1; c < mapped->parts && !splitDone; c++) {  // part 0: the splitter's own first faults
+            while (!splitDone && c > splitPos.load() / Mapping::kPart + kAhead) std::this_thread::sleep_for(std::chrono::microseconds(200));
+            if (splitDone || (c + 1) * Mapping::kPart <= splitPos.load() || !mapped->try_hold(c)) continue;
+            // page by page: MADV_POPULATE_READ over a part held the mapping's lock long enough to slow the
+            // parsers, the batch assembly and the first batch (e2e plain 16.8-19.2 -> 14.4-15.8M pairs/s)
+            const size_t b = c * Mapping::kPart, e = std::min(n, b + Mapping::kPart);
+            volatile char sink = 0;
+            for (size_t i = b; i < e; i += 4096) sink = sink + p[i];
+            mapped->release(b, b + 1);
+        }
+    }
+
     // The mapped file's records cut into jobs (the whole file is in view: no carries).
     void split_mapped(ErrorBox* eb, std::string& err) {
         const char* p = mapped->p;
         const size_t n = mapped->n;
         size_t pos = 0, passed = 0;  // parts the splitter is past
+        const char* pf = getenv("MTB_PREFAULT");
+        std::thread prefaulter;
+        if (!(pf && atoi(pf) == 0) && mapped->parts > 1)
+            prefaulter = std::thread([this] {
+                mtb::background_thread();
+                prefault_loop();
+            });
+        struct Join {  // the prefaulter ends with the split, on every path out
+            MateReader* r;
+            std::thread& t;
+            ~Join() {
+                r->splitDone = true;
+                if (t.joinable()) t.join();
+            }
+        } join{this, prefaulter};
         while (!eb->failed && pos < n) {
+            splitPos = pos;
             uint32_t recs = 0;
             const auto s0 = Clock::now();
             const bool capped = n - pos > kJobBytes;
