@@ -1439,6 +1439,10 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
         }
         if (os.st) hipStreamDestroy(os.st);
     };
+    // MTB_GPU_SERIAL=1: the contexts sharing a device take turns for whole batches (their uploads,
+    // syncs and result copies still overlap the other's kernels) instead of running kernels
+    // concurrently, which slows each batch's memory-bound kernels
+    const bool gpuSerial = getenv("MTB_GPU_SERIAL") && atoi(getenv("MTB_GPU_SERIAL")) != 0;
     std::vector<std::thread> workers;
     for (int d = 0; d < nCtx; d++)
         workers.emplace_back([&, d] {
@@ -1470,7 +1474,7 @@ static int start_classify(mtb_ctx* const* ctxs, int nCtx, const mtb_classify_opt
                 // device — with two contexts on one GPU, for the other's batch; later batches reuse
                 // the workspace and overlap
                 std::unique_lock<std::mutex> gl(*growMu.at(mtb_ctx_device(c)), std::defer_lock);
-                if (s->index < kRamp + (uint64_t)nCtx) gl.lock();
+                if (s->index < kRamp + (uint64_t)nCtx || gpuSerial) gl.lock();
                 if (rc == MTB_OK && em && s->firstRead + s->n > 0xFFFFFFFFull) {
                     rc = MTB_ERR_ARG;
                     mtb::set_error("--em: more than 2^32 reads (MappingRes query IDs are 32-bit)");
