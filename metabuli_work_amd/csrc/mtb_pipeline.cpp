@@ -163,18 +163,23 @@ struct ParseJob {
 };
 
 // A plain (uncompressed) query file mapped whole: the splitter cuts records in the page cache's
-// own pages, with no read copy and no carried records. The mapping is given back in parts of kPart
+// own pages, with no read copy and no carried records. The mapping is given back in parts of partBytes
 // bytes as soon as the splitter is past a part and the parse jobs reading it are done (their
 // records are copied into blocks): the page-table teardown of a multi-GB mapping then runs on the
 // parse workers during the run, not as one munmap after the last batch.
 struct Mapping {
-    static constexpr size_t kPart = 64u << 20;
+    // parts of 64 MB (MTB_MAP_PART=<bytes>, whole pages: tests cut small files into many parts)
+    size_t partBytes = 64u << 20;
     const char* p = nullptr;
     size_t n = 0, parts = 0;
     std::unique_ptr<std::atomic<int>[]> refs;   // per part: its jobs + 1 while the splitter is not past it
     std::unique_ptr<std::atomic<bool>[]> gone;  // per part: unmapped
     void init() {
-        parts = (n + kPart - 1) / kPart;
+        if (const char* e = getenv("MTB_MAP_PART")) {
+            const size_t page = (size_t)sysconf(_SC_PAGESIZE), v = strtoull(e, nullptr, 10);
+            if (v) partBytes = (v + page - 1) / page * page;
+        }
+        parts = (n + partBytes - 1) / partBytes;
         refs.reset(new std::atomic<int>[parts]);
         gone.reset(new std::atomic<bool>[parts]);
         for (size_t c = 0; c < parts; c++) {
@@ -183,13 +188,13 @@ struct Mapping {
         }
     }
     void drop(size_t c) {
-        if (!gone[c].exchange(true)) munmap((void*)(p + c * kPart), std::min(kPart, n - c * kPart));
+        if (!gone[c].exchange(true)) munmap((void*)(p + c * partBytes), std::min(partBytes, n - c * partBytes));
     }
     void hold(size_t b, size_t e) {  // a job's bytes [b, e)
-        for (size_t c = b / kPart; c < parts && c * kPart < e; c++) refs[c]++;
+        for (size_t c = b / partBytes; c < parts && c * partBytes < e; c++) refs[c]++;
     }
     void release(size_t b, size_t e) {
-        for (size_t c = b / kPart; c < parts && c * kPart < e; c++)
+        for (size_t c = b / partBytes; c < parts && c * partBytes < e; c++)
             if (--refs[c] == 0) drop(c);
     }
     void release_part(size_t c) {  // the splitter is past part c
@@ -204,7 +209,7 @@ struct Mapping {
     }
     ~Mapping() {
         for (size_t c = 0; c < parts; c++)
-            if (!gone[c]) munmap((void*)(p + c * kPart), std::min(kPart, n - c * kPart));
+            if (!gone[c]) munmap((void*)(p + c * partBytes), std::min(partBytes, n - c * partBytes));
     }
 };
 
@@ -330,7 +335,7 @@ struct MateReader {
 
     // The mapped file's page tables filled ahead of the splitter by a helper thread: on a fresh
     // mapping half of the splitter's scan time was page faults (a 1.25-GB tmpfs FASTQ: scan 0.151 s
-    // cold, 0.079 s prefaulted). Parts of kPart bytes, at most kAhead parts ahead of the splitter,
+    // cold, 0.079 s prefaulted). Parts of partBytes bytes, at most kAhead parts ahead of the splitter,
     // each under a hold so it cannot be unmapped while touched. MTB_PREFAULT=0 turns it off (A/B).
     static constexpr size_t kAhead = 4;
     std::atomic<size_t> splitPos{0};
@@ -339,11 +344,11 @@ struct MateReader {
         const char* p = mapped->p;
         const size_t n = mapped->n;
         for (size_t c = 1; c < mapped->parts && !splitDone; c++) {  // part 0: the splitter's own first faults
-            while (!splitDone && c > splitPos.load() / Mapping::kPart + kAhead) std::this_thread::sleep_for(std::chrono::microseconds(200));
-            if (splitDone || (c + 1) * Mapping::kPart <= splitPos.load() || !mapped->try_hold(c)) continue;
+            while (!splitDone && c > splitPos.load() / mapped->partBytes + kAhead) std::this_thread::sleep_for(std::chrono::microseconds(200));
+            if (splitDone || (c + 1) * mapped->partBytes <= splitPos.load() || !mapped->try_hold(c)) continue;
             // page by page: MADV_POPULATE_READ over a part held the mapping's lock long enough to slow the
             // parsers, the batch assembly and the first batch (e2e plain 16.8-19.2 -> 14.4-15.8M pairs/s)
-            const size_t b = c * Mapping::kPart, e = std::min(n, b + Mapping::kPart);
+            const size_t b = c * mapped->partBytes, e = std::min(n, b + mapped->partBytes);
             volatile char sink = 0;
             for (size_t i = b; i < e; i += 4096) sink = sink + p[i];
             mapped->release(b, b + 1);
@@ -390,7 +395,7 @@ struct MateReader {
             j->recs = recs;
             mapped->hold(j->b, j->e);
             pos += used;
-            for (; passed < mapped->parts && (passed + 1) * Mapping::kPart <= pos; passed++) mapped->release_part(passed);
+            for (; passed < mapped->parts && (passed + 1) * mapped->partBytes <= pos; passed++) mapped->release_part(passed);
             if (!out.push(j)) break;
             if (!work.push(j)) {
                 j->err = "input stopped";

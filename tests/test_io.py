@@ -328,6 +328,43 @@ def test_start_classify_parse_buffer_edges(make_db, tmp_path, monkeypatch, raw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("part", [4096, 65536])
+def test_start_classify_mapped_parts_prefault(make_db, tmp_path, monkeypatch, part):
+    """Plain query files are mapped and given back in parts as the parse jobs finish with them, and a
+    helper thread touches the parts up to four ahead of each mate's splitter (round 5). With parts of
+    one page or 64 KB (MTB_MAP_PART) the prefaulter, the splitter and the parts' release interleave
+    over hundreds of parts: the TSV equals the run read through buffers (MTB_NO_MMAP) and the one
+    without prefaulting, byte for byte, and the oracle's taxIDs."""
+    db_dir, taxo, gen = make_db("fmt2")
+    r = synth.make_reads(gen, 1200, paired=True, seed=67, short_frac=0.02)
+    names = [f"m{i}" for i in range(r.n)]
+    p1, p2 = str(tmp_path / "q1.fq"), str(tmp_path / "q2.fq")
+    _write_fastq(p1, names, _mates(r, 1))
+    _write_fastq(p2, names, _mates(r, 2))
+    par = LocalParameters(seqMode=2, filenames=[p1, p2, db_dir])
+    par.load_db_parameters(db_dir)
+    out = {}
+    with Classifier(par, db_dir=db_dir) as clf:
+        for name, env in (("buffers", {"MTB_NO_MMAP": "1"}), ("noprefault", {"MTB_PREFAULT": "0"}),
+                          ("prefault", {"MTB_PREFAULT": "1"})):
+            for k in ("MTB_NO_MMAP", "MTB_PREFAULT"):
+                monkeypatch.delenv(k, raising=False)
+            monkeypatch.setenv("MTB_MAP_PART", str(part))
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            out[name] = str(tmp_path / f"{name}.tsv")
+            assert clf.startClassify(out[name], reads_per_batch=257) == r.n
+    ref = open(out["buffers"], "rb").read()
+    assert open(out["noprefault"], "rb").read() == ref
+    assert open(out["prefault"], "rb").read() == ref
+    odb = oc.OracleDb(db_dir)
+    ores, _ = oc.classify(odb, par.to_c(), r)
+    odb.close()
+    body = [l.split("\t") for l in ref.decode().split("\n")[1:] if l]
+    assert [int(f[2]) for f in body] == [int(o["classification"]) if o["is_classified"] else 0 for o in ores]
+
+
+@pytest.mark.gpu
 def test_clone_shares_db(make_db, tmp_path):
     """mtb_clone: a second context over the same DB arrays, with its own stream and workspace. Two
     batches in flight on one GPU through mtb_start_classify_multi write the one-context TSV and
