@@ -245,17 +245,23 @@ int mtb_assign_matches(mtb_ctx* ctx, const mtb_match* matches, uint64_t n_matche
  * arrays; out receives off[n] bytes: 'N' where masked (or not A/C/G/T/U), else the input letter. */
 int mtb_mask_reads(mtb_ctx* ctx, const char* seq, const uint64_t* off, uint32_t n_reads, char* out);
 
+/* bytes from src to dst, host or device memory either (hipMemcpyDefault: the runtime tells them
+ * apart); for bindings that assemble device-resident results of split batches (classifier.py). */
+int mtb_memcpy(void* dst, const void* src, uint64_t bytes);
+
 /* compareDna's codon arithmetic alone (KmerMatcher.cpp:1117-1146 over KmerMatcher.h:66-158, 348-416),
  * on the device K4 runs on: for each (query, target) DNA part the Hamming sum (getHammingDistanceSum),
  * and the forward and reverse per-codon 2-bit words (getHammings / getHammings_reverse), from the
  * device functions the join emits matches with. Host arrays; MTB_ERR_INTERNAL if the join's
  * row-cached forms disagree with the plain forms on any pair. */
-/* bytes from src to dst, host or device memory either (hipMemcpyDefault: the runtime tells them
- * apart); for bindings that assemble device-resident results of split batches (classifier.py). */
-int mtb_memcpy(void* dst, const void* src, uint64_t bytes);
-
 int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint64_t n, uint8_t* sum, uint16_t* fwd,
                 uint16_t* rev);
+
+/* Diagnostics (round 5): the opened DB's run-length lines (the unstaged join's runs without a
+ * run-index read) checked against its run index for every present AA rank within their reach:
+ * out[0] ranks checked, out[1] those the codes resolve, out[2] mismatches (MTB_ERR_INTERNAL when
+ * any). MTB_ERR_ARG when the context has no run-length lines (MTB_LINE_EXT=0) or no run index. */
+int mtb_line_ext_check(mtb_ctx* ctx, uint64_t out[3]);
 
 /* ---- range-partitioned DB across GPUs ---------------------------- */
 /* A DB larger than one GPU's HBM is cut at split entries (DiffIdxSplit, Kmer.h:111-119; written

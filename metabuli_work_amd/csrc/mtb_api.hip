@@ -123,6 +123,7 @@ struct mtb_ctx {
     ProbeLine* lines = nullptr;  // probe lines: AA 8-mer membership + DB run heads (5.4 GB)
     uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
     uint16_t* runOff = nullptr;  // ... and each present rank's run start in its line (2 B per present rank)
+    ProbeExt* lineExt = nullptr;  // run-length lines (64 B per probe line; MTB_LINE_EXT=1, A/B)
     AADir dir{};
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe, 3 sweep
@@ -255,10 +256,11 @@ static void free_db(mtb_ctx* c) {
         c->lines = nullptr;
         c->lineP = nullptr;
         c->runOff = nullptr;
+        c->lineExt = nullptr;
         return;
     }
     if (c->borrowedDb) c->db = nullptr;  // caller-owned (mtb_open_resident)
-    void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->db = nullptr;
@@ -266,6 +268,7 @@ static void free_db(mtb_ctx* c) {
     c->lines = nullptr;
     c->lineP = nullptr;
     c->runOff = nullptr;
+    c->lineExt = nullptr;
 }
 
 template <typename T>
@@ -483,6 +486,13 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
             HIP_TRY(hipMalloc(&c->runOff, (P + 1) * sizeof(uint16_t)));
             HIP_TRY(hipMemsetAsync(c->runOff + P, 0, sizeof(uint16_t), s));  // the end entry is never a run's
             build_run_offsets(c->db, c->D, c->lines, c->lineP, c->runOff, s);
+            // MTB_LINE_EXT=1 (A/B, off: the join went 55.9 -> 57.2-60.2 ms, profiles/r05/ab_lineext.json):
+            // run-length lines, so K4 finds most runs without the run-index read
+            const char* le = getenv("MTB_LINE_EXT");
+            if (le && atoi(le) != 0) {
+                HIP_TRY(hipMalloc(&c->lineExt, kProbeLines * sizeof(ProbeExt)));
+                build_line_ext(c->lines, c->lineP, c->runOff, c->lineExt, s);
+            }
         }
     }
     HIP_TRY(hipGetLastError());  // a failed launch (e.g. a bad grid) must not pass silently
@@ -514,7 +524,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     HIP_TRY(hipStreamSynchronize(s));
     c->dbArrays = std::make_shared<DbArrays>();
     c->dbArrays->device = device;
-    c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->spOf,
+    c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->spOf,
                         c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     bind_workspace(c, 0);
     c->openS[5] = since(tp);
@@ -628,6 +638,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->lines = src->lines;
     c->lineP = src->lineP;
     c->runOff = src->runOff;
+    c->lineExt = src->lineExt;
     c->dir = src->dir;
     c->rankLo = src->rankLo;
     c->rankHi = src->rankHi;
@@ -1236,7 +1247,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
                          direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
                          c->ovFlag.as<int>(), c->spillShift, direct ? c->longList.as<LongRun>() : nullptr,
-                         c->longCap, c->longCnt.as<uint32_t>(), s);
+                         c->longCap, c->longCnt.as<uint32_t>(), s, c->lineExt);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1398,6 +1409,25 @@ extern "C" {
 int mtb_memcpy(void* dst, const void* src, uint64_t bytes) {
     if (bytes && (!dst || !src)) { set_error("null argument"); return MTB_ERR_ARG; }
     if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return MTB_OK;
+}
+
+int mtb_line_ext_check(mtb_ctx* c, uint64_t* out) {
+    if (!c || !out) return MTB_ERR_ARG;
+    out[0] = out[1] = out[2] = 0;
+    if (!c->lineExt || !c->runOff) { set_error("no run-length lines (MTB_LINE_EXT=0, or no run index)"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf cnt;
+    HIP_TRY(cnt.ensure(3 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 3 * sizeof(unsigned long long), c->stream));
+    launch_line_ext_check(c->lines, c->lineP, c->runOff, c->lineExt, cnt.as<unsigned long long>(), c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, cnt.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out[2]) {
+        set_error("internal error: " + std::to_string(out[2]) + " runs from the run-length lines disagree with the run index");
+        return MTB_ERR_INTERNAL;
+    }
     return MTB_OK;
 }
 

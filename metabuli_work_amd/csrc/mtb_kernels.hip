@@ -1167,6 +1167,94 @@ __global__ void __launch_bounds__(256) k_run_offsets_wave(const DbRec* __restric
 
 static unsigned line_wave_grid() { return (unsigned)std::min<uint64_t>((kProbeLines + 3) / 4, 1u << 20); }
 
+// A present rank's run from its line's run-length codes xw (kExtRanks / 16 words): the codes' sum over
+// the ranks before it (sum: its run start minus the line's base, minus before) and its own code (run
+// length - 1); false when an escape (3) lies at or before it (the caller reads runOff instead).
+__device__ __forceinline__ bool ext_run(const uint32_t* xw, uint32_t before, uint32_t& sum, uint32_t& code) {
+    const uint32_t wq = before >> 4, f = before & 15u;
+    uint32_t esc = 0;
+    sum = 0;
+    code = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kExtRanks / 16; i++) {
+        const uint32_t w = xw[i];
+        const uint32_t mLt = i < wq ? ~0u : (i == wq ? (1u << (2 * f)) - 1u : 0u);
+        const uint32_t mLe = i < wq ? ~0u : (i == wq ? (f == 15u ? ~0u : (1u << (2 * f + 2)) - 1u) : 0u);
+        const uint32_t wl = w & mLt, we = w & mLe;
+        sum += (uint32_t)__popc(wl & 0x55555555u) + 2u * (uint32_t)__popc(wl & 0xAAAAAAAAu);
+        esc |= we & (we >> 1) & 0x55555555u;
+        if (i == wq) code = (w >> (2 * f)) & 3u;
+    }
+    return esc == 0;
+}
+
+// Every present rank of every indexed line against the run index (mtb_line_ext_check): out[0] the
+// ranks within the run-length lines' reach, out[1] those they resolve, out[2] mismatches.
+__global__ void __launch_bounds__(256) k_line_ext_check(const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ lineP,
+                                                        const uint16_t* __restrict__ runOff, const ProbeExt* __restrict__ ext,
+                                                        unsigned long long* __restrict__ out) {
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    unsigned long long n = 0, ok = 0, bad = 0;
+    for (uint64_t L = (uint64_t)blockIdx.x * 4 + wv; L + 1 < kProbeLines; L += (uint64_t)gridDim.x * 4) {
+        const uint64_t cnt = lines[L].base >> 40, p0 = lineP[L];
+        const uint32_t pc = (uint32_t)(lineP[L + 1] - p0);
+        if (cnt > kRunIdxMax) continue;
+        for (uint32_t k = (uint32_t)lane; k < min(pc, kExtRanks); k += 64) {
+            n++;
+            uint32_t sum, code;
+            if (!ext_run(ext[L].w, k, sum, code)) continue;
+            ok++;
+            const uint32_t a = runOff[p0 + k], b = k + 1 < pc ? runOff[p0 + k + 1] : (uint32_t)cnt;
+            bad += (k + sum != a || code + 1 != b - a) ? 1ull : 0ull;
+        }
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        n += __shfl_xor(n, d, 64);
+        ok += __shfl_xor(ok, d, 64);
+        bad += __shfl_xor(bad, d, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(out, n);
+        atomicAdd(out + 1, ok);
+        atomicAdd(out + 2, bad);
+    }
+}
+
+void launch_line_ext_check(const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, const ProbeExt* ext,
+                           unsigned long long* out, hipStream_t s) {
+    k_line_ext_check<<<line_wave_grid(), 256, 0, s>>>(lines, lineP, runOff, ext, out);
+}
+
+// Run-length lines, a wave per line: lane l codes present ranks 4l .. 4l + 3 of the line from their
+// run-index entries (the next rank's start, or the line's k-mer count for its last) into one byte.
+__global__ void __launch_bounds__(256) k_line_ext(const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ lineP,
+                                                  const uint16_t* __restrict__ runOff, ProbeExt* __restrict__ ext) {
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    for (uint64_t L = (uint64_t)blockIdx.x * 4 + wv; L < kProbeLines; L += (uint64_t)gridDim.x * 4) {
+        const uint64_t cnt = lines[L].base >> 40;
+        const uint64_t p0 = lineP[L];
+        const uint32_t pc = (uint32_t)(L + 1 < kProbeLines ? lineP[L + 1] - p0 : 0);
+        uint32_t byte = 0xFFu;  // escapes: a line the run index does not cover
+        if (cnt <= kRunIdxMax) {
+            byte = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t k = 4u * (uint32_t)lane + (uint32_t)j;
+                if (k >= pc) break;
+                const uint32_t a = runOff[p0 + k], b = k + 1 < pc ? runOff[p0 + k + 1] : (uint32_t)cnt;
+                byte |= min(b - a - 1u, 3u) << (2 * j);
+            }
+        }
+        reinterpret_cast<uint8_t*>(ext + L)[lane] = (uint8_t)byte;
+    }
+}
+
+void build_line_ext(const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, ProbeExt* ext,
+                    hipStream_t s) {
+    static_assert(kExtRanks == 4 * 64, "a byte of four codes per lane");
+    k_line_ext<<<line_wave_grid(), 256, 0, s>>>(lines, lineP, runOff, ext);
+}
+
 static bool line_atomic_build() {  // MTB_LINE_BUILD=atomic (A/B): the per-k-mer atomic kernels
     const char* e = getenv("MTB_LINE_BUILD");
     return e && !strcmp(e, "atomic");
@@ -1236,6 +1324,7 @@ constexpr int kMatchWin = 3072;
 constexpr uint32_t kStageFreeRatio = 12;
 constexpr int kFreePer = 1;               // queries per thread in the unstaged K4 (2: no gain with the run index; +1.6 ms before)
 constexpr int kMatchLines = 256;          // probe lines a block of the unstaged K4 stages in LDS (16 KB)
+constexpr int kExtLines = 128;            // run-length lines it stages beside them (MTB_LINE_EXT=1, A/B: 8 KB)
 constexpr uint64_t kRankEnd = 37822859361ull;  // 21^8 AA k-mers
 
 __device__ __forceinline__ uint64_t db_lower_bound(const DbVal& dbv, const AADir& d, uint64_t v) {
@@ -1472,12 +1561,15 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
                                                int* __restrict__ overflow, uint32_t capShift,
                                                LongRun* __restrict__ longList, uint32_t longCap,
-                                               uint32_t* __restrict__ longCnt) {
+                                               uint32_t* __restrict__ longCnt, const ProbeExt* __restrict__ lineExt) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
     __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
-    __shared__ ProbeLine sLines[kStage ? 1 : kMatchLines];  // the block's probe lines (sorted queries)
+    // the block's probe lines (sorted queries) and, behind them, their run-length lines
+    __shared__ uint4 sLineMem[kStage ? 1 : (kMatchLines + kExtLines) * 4];
+    ProbeLine* const sLines = reinterpret_cast<ProbeLine*>(sLineMem);
+    const uint32_t* const sExt = reinterpret_cast<const uint32_t*>(sLineMem + (kStage ? 0 : kMatchLines * 4));
     __shared__ uint64_t sLineP[kStage ? 1 : kMatchLines];   // and their run-index bases
     __shared__ unsigned long long sTbl[kStage ? 1 : 512];     // run sharing: (AA rank + 1) << 8 | leader
     __shared__ unsigned long long sBase;
@@ -1576,6 +1668,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         const uint64_t L0 = ((qkey[q0] >> sortLo) << sh) / kLineRanks;
         const uint64_t L1 = ((((qkey[q1 - 1] >> sortLo) + 1) << sh) - 1) / kLineRanks;
         const bool inLds = !kStage && L1 - L0 < (uint64_t)kMatchLines;
+        const bool extLds = lineExt && inLds && L1 - L0 < (uint64_t)kExtLines;
         if (!kStage && inLds) {
             const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;  // 4 x 16 B per line
             const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
@@ -1583,6 +1676,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
             for (uint32_t i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
             if (runOff)
                 for (uint32_t i = threadIdx.x; i <= (uint32_t)(L1 - L0); i += 256) sLineP[i] = lineP[L0 + i];
+            if (extLds) {
+                const uint4* esrc = reinterpret_cast<const uint4*>(lineExt + L0);
+                uint4* edst = sLineMem + kMatchLines * 4;
+                for (uint32_t i = threadIdx.x; i < nv; i += 256) edst[i] = esrc[i];
+            }
             __syncthreads();
         }
 #pragma unroll
@@ -1602,6 +1700,12 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                 if (cnt <= kRunIdxMax) {
                     if (!present) {  // an absent rank (not filtered: MTB_FILTER=0) has no run; runOff[p] may
                         lo[j] = hi[j] = base;  // be the next line's entry or the unset end entry
+                        continue;
+                    }
+                    uint32_t sum, code;
+                    if (extLds && before < kExtRanks && ext_run(sExt + (L - L0) * (kExtRanks / 16), before, sum, code)) {
+                        lo[j] = base + before + sum;  // no run-index read
+                        hi[j] = lo[j] + code + 1;
                         continue;
                     }
                     const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
@@ -1664,7 +1768,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         uint64_t* sHi = sLo + 256;
         uint64_t* sRv = sHi + 256;
         uint32_t* sRt = reinterpret_cast<uint32_t*>(sRv + 512);
-        static_assert(kStage || (256 * 8 * 4 + 512 * 4) <= sizeof(ProbeLine) * kMatchLines, "results fit the line stage");
+        static_assert(kStage || (256 * 8 * 4 + 512 * 4) <= sizeof(uint4) * (kMatchLines + kExtLines) * 4, "results fit the line stage");
         const uint32_t t = threadIdx.x;
         if (!follower) {
             sLo[t] = lo[0];
@@ -2492,7 +2596,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s) {
+                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
+                  const ProbeExt* lineExt) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -2502,14 +2607,15 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
-                                                        overflow, capShift, longList, longCap, longCnt);
+                                                        overflow, capShift, longList, longCap, longCnt,
+                                                        runOff ? lineExt : nullptr);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
                                                             stats, direct, dirOff, overflow, capShift, nullptr, 0,
-                                                            longCnt);
+                                                            longCnt, nullptr);
     }
 }
 

@@ -185,6 +185,21 @@ constexpr uint64_t kRunIdxMax = 0xFFFF;
 void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s);
 void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s);
+// Run-length lines (round 5): per probe line 64 B of 2-bit codes, one per present rank of the line
+// (its first kExtRanks), code = min(run length - 1, 3), 3 an escape (a run of >= 4, or a line the run
+// index does not cover: all codes 3). The unstaged K4 stages them beside the probe lines and finds a
+// query's run as base + before + the codes' sum over the ranks before it, code + 1 long — no random
+// run-index read — unless an escape lies at or before its rank (then runOff as before).
+constexpr uint32_t kExtRanks = 256;
+struct alignas(64) ProbeExt {
+    uint32_t w[kExtRanks / 16];
+};
+static_assert(sizeof(ProbeExt) == 64, "one run-length line per probe line");
+void build_line_ext(const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, ProbeExt* ext,
+                    hipStream_t s);
+// out (3 device words, zeroed): present ranks within reach, resolved by the codes, mismatches vs runOff
+void launch_line_ext_check(const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, const ProbeExt* ext,
+                           unsigned long long* out, hipStream_t s);
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count and sets
@@ -287,7 +302,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   uint32_t* bufRank, uint64_t region, int* err, uint32_t winCap, const uint64_t* win,
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
-                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s);
+                  uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
+                  const ProbeExt* lineExt = nullptr);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
 // slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A query whose ranks pass
 // its read's stretch spills its matches and their ranks to buf / bufRank (total[0] of them; at most

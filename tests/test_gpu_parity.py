@@ -132,6 +132,35 @@ def okmers_present(okmers, db_dir, par):
     return ok[np.isin(_aa_rank(ok["value"], par.kmerFormat), _db_aa_ranks(db_dir, par.kmerFormat))]
 
 
+def line_ext_check(clf):
+    """mtb_line_ext_check: (ranks within reach, resolved by the run-length codes, mismatches)."""
+    import ctypes
+    from metabuli_work_amd._lib import lib
+    out = (ctypes.c_uint64 * 3)()
+    rc = lib().mtb_line_ext_check(clf.handle, out)
+    assert rc == 0, lib().mtb_last_error().decode()
+    return tuple(int(x) for x in out)
+
+
+@pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1", "fmt2_acc"])
+def test_line_ext_matches_run_index(make_db, db_name, monkeypatch):
+    """The run-length lines built at open (2-bit run lengths per present AA rank beside each probe
+    line) give every present rank within their reach the run the run index holds: the same start
+    and length wherever no escape precedes it, and no DB leaves them empty of resolvable ranks. With
+    MTB_LINE_EXT=0 (the default) there are none and the entry point says so."""
+    db_dir, taxo, gen = make_db(db_name)
+    monkeypatch.setenv("MTB_LINE_EXT", "1")
+    with Classifier(_params(db_dir, 2), db_dir=db_dir) as clf:
+        n, ok, bad = line_ext_check(clf)
+        assert bad == 0 and n > 0 and ok > 0
+    monkeypatch.setenv("MTB_LINE_EXT", "0")
+    with Classifier(_params(db_dir, 2), db_dir=db_dir) as clf:
+        import ctypes
+        from metabuli_work_amd._lib import lib
+        out = (ctypes.c_uint64 * 3)()
+        assert lib().mtb_line_ext_check(clf.handle, out) != 0
+
+
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
 def test_end_to_end_batches(make_db, db_name):
     """Whole path, several batches, against oracle classify."""
@@ -150,7 +179,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -180,6 +209,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_K1F_BINS", "2" if mode.startswith("bins") else "0")
     monkeypatch.setenv("MTB_K1F_BINS_RC", "64" if mode == "binsover" else "0")
     monkeypatch.setenv("MTB_K1F_BINS_DIG", "0" if mode == "binsnodig" else "1")  # K2's second pass reads the keys
+    monkeypatch.setenv("MTB_LINE_EXT", "1" if mode == "ext" else "0")  # K4's runs from run-length lines (A/B)
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))

@@ -49,7 +49,7 @@ class _Capture(oc.OracleDb):
         return db, d, i, s
 
 
-def test_gtdb_shaped_resident_db_parity():
+def test_gtdb_shaped_resident_db_parity(monkeypatch):
     from metabuli_work_amd.classifier import Classifier, LocalParameters
     from metabuli_work_amd.gpu_synth import make_reads_gpu
     from metabuli_work_amd.gtdb_synth import build_gtdb_scale, encode_into_oracle
@@ -68,8 +68,12 @@ def test_gtdb_shaped_resident_db_parity():
     assert bool((v[1:] >= v[:-1]).all())
     reads = _host_reads(*got["reads"])
     par = LocalParameters(seqMode=2, kmerFormat=2, skipRedundancy=1)
+    from tests.test_gpu_parity import line_ext_check
+    monkeypatch.setenv("MTB_LINE_EXT", "1")  # the A/B's run-length lines, checked on a GTDB-shaped DB
     with Classifier(par, db_resident=rdb) as clf:
         br = clf.classify_batch(reads.seq1, reads.off1, reads.seq2, reads.off2)
+        n, ok, bad = line_ext_check(clf)  # the GTDB-shaped DB's run-length lines against its run index
+        assert bad == 0 and ok > 0.5 * n
     odb = encode_into_oracle(rdb, oc.OracleDb, chunk=1 << 20)
     ores, otc = oc.classify(odb, par.to_c(), reads)
     odb.close()
