@@ -42,6 +42,42 @@ def test_default_params_are_classify_defaults():
             assert getattr(p, f) == getattr(q, f), f
 
 
+# setClassifyDefaults fields -> mtb_params fields; the rest have no place in the hot path's parameters:
+# validateInput / validateDb (the CLI's file checks), verbosity / printLog / ramUsage (the CLI's logging
+# and its RAM-bounded query splits: here the batch comes from the caller or free HBM), hammingMargin and
+# maxGap (stored by KmerMatcher.cpp:29 / Taxonomer.cpp:27 and read nowhere on the path), matchPerKmer (the
+# reference's initial match-buffer factor: here the workspace grows to the batch, MTB_RETRY),
+# printLineage (the TSV writer's flag, MTB_WRITE_LINEAGE)
+_DEFAULT_FIELDS = {"syncmer": "syncmer", "smerLen": "smer_len", "kmerFormat": "kmer_format", "em": "em",
+                   "skipRedundancy": "skip_redundancy", "reducedAA": "reduced_aa", "seqMode": "seq_mode",
+                   "minScore": "min_score", "minSpScore": "min_sp_score", "minConsCnt": "min_cons_cnt",
+                   "minConsCntEuk": "min_cons_cnt_euk", "maskMode": "mask_mode", "maskProb": "mask_prob",
+                   "accessionLevel": "accession_level", "tieRatio": "tie_ratio"}
+_DEFAULT_OUTSIDE = {"validateInput", "validateDb", "verbosity", "printLog", "ramUsage", "hammingMargin", "maxGap",
+                    "matchPerKmer", "printLineage"}
+
+
+def test_default_params_pinned_to_reference_text():
+    """mtb_default_params against setClassifyDefaults as the reference writes it
+    (tests/golden/classify_defaults.json, parsed from src/workflow/classify.cpp:10-37 by
+    tests/golden/make_classify_defaults.py): every default the parameters carry is the reference's,
+    and every default there is either carried or listed above with the reason it is not."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "classify_defaults.json")))["defaults"]
+    assert set(g) == set(_DEFAULT_FIELDS) | _DEFAULT_OUTSIDE
+    p = _abi.MtbParams()
+    lib().mtb_default_params(ctypes.byref(p))
+    for ref, ours in _DEFAULT_FIELDS.items():
+        want = g[ref]["value"]
+        got = getattr(p, ours)
+        if isinstance(want, float):
+            assert abs(got - want) < 1e-6, (ref, got, want)
+        else:
+            assert got == int(want), (ref, got, want)
+    assert g["hammingMargin"]["value"] == 0 and g["maxGap"]["value"] == 0
+
+
 def test_load_db_parameters_quirks(tmp_path):
     d = tmp_path / "db"
     d.mkdir()
