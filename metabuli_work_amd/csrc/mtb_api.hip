@@ -143,6 +143,7 @@ struct mtb_ctx {
     int bigGroups = 1;           // MTB_BIG_GROUPS=0: no k_match_paths_wave (every group on a thread)
     bool fuseFilter = true;      // MTB_FUSE_FILTER=0: K1 writes every window's key, K1F reads them back
     bool radixDigits = true;     // MTB_RADIX_DIGITS=0: K2's histograms read the keys, not 1-B digit side arrays
+    bool radixAtomicFirst = false;  // MTB_RADIX_ATOMIC_FIRST=1 (A/B): K2's first pass ranks by LDS atomics
     // MTB_K1F_BINS: the fused K1F writes straight into K2's first-pass buckets (1: batches of >= 2^22
     // present-window slots, 2: every batch, 0: off, the default — measured even);
     // MTB_K1F_BINS_RC forces the bucket size (tests)
@@ -461,6 +462,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     if ((c->sweepSmall || c->sweepPersist == 2) && !getenv("MTB_SWEEP_NOM")) c->sweepNom = 1024;
     if (const char* e = getenv("MTB_FILTER")) c->noFilter = atoi(e) == 0;
     if (const char* e = getenv("MTB_RADIX_DIGITS")) c->radixDigits = atoi(e) != 0;
+    if (const char* e = getenv("MTB_RADIX_ATOMIC_FIRST")) c->radixAtomicFirst = atoi(e) != 0;
     if (const char* e = getenv("MTB_K1F_BINS")) c->binnedSort = atoi(e);
     if (const char* e = getenv("MTB_K1F_BINS_RC")) c->binRcForce = strtoull(e, nullptr, 10);
     if (const char* e = getenv("MTB_K1F_BINS_DIG")) c->binDigits = atoi(e) != 0;
@@ -681,6 +683,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->noAlias = src->noAlias;
     c->noFilter = src->noFilter;
     c->radixDigits = src->radixDigits;
+    c->radixAtomicFirst = src->radixAtomicFirst;
     c->binnedSort = src->binnedSort;
     c->binRcForce = src->binRcForce;
     c->binDigits = src->binDigits;
@@ -1129,13 +1132,15 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
             Q = radix_sort_pairs(c->keysB.as<uint64_t>(), c->valsB.as<uint32_t>(), c->keysA.as<uint64_t>(),
                                  c->valsA.as<uint32_t>(), Q, sortLo, kQuerySortHi, false, false,
                                  c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s,
-                                 dg ? c->digA.as<uint8_t>() : nullptr, dg ? c->digB.as<uint8_t>() : nullptr);
+                                 dg ? c->digA.as<uint8_t>() : nullptr, dg ? c->digB.as<uint8_t>() : nullptr,
+                                 c->radixAtomicFirst);
             qk = inB ? c->keysA.as<uint64_t>() : c->keysB.as<uint64_t>();
             qi = inB ? c->valsA.as<uint32_t>() : c->valsB.as<uint32_t>();
         } else {
             Q = radix_sort_pairs(c->keysA.as<uint64_t>(), c->valsA.as<uint32_t>(), c->keysB.as<uint64_t>(),
                                  c->valsB.as<uint32_t>(), R, kQuerySortLo, kQuerySortHi, true, true,
-                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s);
+                                 c->radixCounts.as<uint32_t>(), c->radixOffs.as<uint64_t>(), c->scanTmp.p, &inB, s,
+                                 nullptr, nullptr, c->radixAtomicFirst);
             qk = inB ? c->keysB.as<uint64_t>() : c->keysA.as<uint64_t>();
             qi = inB ? c->valsB.as<uint32_t>() : c->valsA.as<uint32_t>();
             c->Qall = Q;  // no membership filter: every non-blank window was sorted

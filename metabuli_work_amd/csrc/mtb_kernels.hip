@@ -661,7 +661,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
                                                        uint64_t n, int shift, const uint64_t* __restrict__ offs,
                                                        uint32_t nTiles, uint64_t* __restrict__ keysOut,
                                                        V* __restrict__ valsOut, uint8_t* __restrict__ digOut,
-                                                       int nextShift, int xcdMap, const uint64_t* __restrict__ tab) {
+                                                       int nextShift, int xcdMap, const uint64_t* __restrict__ tab,
+                                                       int atomicRank) {
     __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
     __shared__ uint8_t sDig[kRadixTile];
     __shared__ uint32_t waveHist[kWaves][256];
@@ -708,6 +709,21 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
             v[r] = GEN ? (V)i : (i < n ? valsIn[i] : (V)0);
         }
     }
+    // atomicRank (an LSD sort's first pass, when its input order need not be kept): each key's rank
+    // in its wave's slice from one LDS atomic on the wave's histogram — the order among a wave
+    // instruction's lanes of one digit is the hardware's, so later passes, which must be stable,
+    // keep the 8-ballot ranking (all three passes atomic: sort 15.8 -> 13.1-14.1 ms, but stability
+    // would then rest on an undocumented lane order; profiles/r05/ab_radixatomic_allpasses.json). The
+    // first pass alone measured even (ab_radixatomic_first.json): off by default (MTB_RADIX_ATOMIC_FIRST)
+    if (atomicRank) {
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) {
+            const uint64_t i = base + (uint64_t)r * 64 + lane;
+            const bool valid = i < n && (!FILTER || k[r] != kSentinel);
+            const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
+            rk[r] = valid ? (d << 16 | atomicAdd(&waveHist[w][d], 1u)) : ~0u;
+        }
+    } else
 #pragma unroll
     for (int r = 0; r < kRadixItems; r++) {
         const uint64_t i = base + (uint64_t)r * 64 + lane;
@@ -778,7 +794,7 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s, uint8_t* digA, uint8_t* digB) {
+                          hipStream_t s, uint8_t* digA, uint8_t* digB, bool unstableFirst) {
     uint64_t cur = n;
     uint64_t *ki = keysA, *ko = keysB;
     V *vi = valsA, *vo = valsB;
@@ -799,10 +815,11 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         const char* xe = getenv("MTB_RADIX_XCD");
         const int xcd = xe ? atoi(xe) : 1;
         const int ns = shift + 8;
-        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
-        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
-        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
-        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr);
+        const int ar = first && unstableFirst ? 1 : 0;
+        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+        else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+        else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+        else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         std::swap(di, dg);
         if (f) {
             uint64_t kept = 0;
@@ -863,7 +880,7 @@ uint64_t radix_sort_binned(uint64_t* keysR, V* valsR, uint64_t* keysT, V* valsT,
     const char* xe = getenv("MTB_RADIX_XCD");
     const int xcd = xe ? atoi(xe) : 1;
     k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(keysR, valsR, 0, shift, offs, nTiles, keysT, valsT,
-                                                              ns < bitHi ? digT : nullptr, ns, xcd, tileTab);
+                                                              ns < bitHi ? digT : nullptr, ns, xcd, tileTab, 0);
     *inT = true;
     if (ns < bitHi) {  // the rest: plain passes over the Q contiguous pairs
         bool inB = false;
@@ -881,9 +898,9 @@ template uint64_t radix_sort_binned<uint32_t>(uint64_t*, uint32_t*, uint64_t*, u
                                               void*, uint64_t*, bool*, hipStream_t, uint8_t*, uint8_t*);
 
 template uint64_t radix_sort_pairs<uint64_t>(uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*, bool);
 template uint64_t radix_sort_pairs<uint32_t>(uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int, int, bool, bool,
-                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*);
+                                             uint32_t*, uint64_t*, void*, bool*, hipStream_t, uint8_t*, uint8_t*, bool);
 
 // ------------------------------------------------------------------------------------------------
 // K3 diffIdx decode (getNextTargetKmer, KmerMatcher.h:282-297) at DB open: terminator flags ->

@@ -104,7 +104,9 @@ uint64_t radix_counts_elems(uint64_t n);
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
-                          hipStream_t s, uint8_t* digA = nullptr, uint8_t* digB = nullptr);
+                          hipStream_t s, uint8_t* digA = nullptr, uint8_t* digB = nullptr, bool unstableFirst = false);
+// unstableFirst: the first pass may permute keys of one digit (its input order carries nothing: the
+// query sort); it then ranks by LDS atomics instead of the stable 8-ballot ranking
 // K2 after a binned K1F (binRc > 0 above): the pairs already sit in the first pass's buckets —
 // kSortBins regions of rc slots, region d * 8 + XCD for first digit d (bits [bitLo, bitLo + 8)), the
 // region counts in binDev (device) and binHost (host copy) — with each key's second-pass digit in

@@ -179,7 +179,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -210,6 +210,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_K1F_BINS_RC", "64" if mode == "binsover" else "0")
     monkeypatch.setenv("MTB_K1F_BINS_DIG", "0" if mode == "binsnodig" else "1")  # K2's second pass reads the keys
     monkeypatch.setenv("MTB_LINE_EXT", "1" if mode == "ext" else "0")  # K4's runs from run-length lines (A/B)
+    monkeypatch.setenv("MTB_RADIX_ATOMIC_FIRST", "1" if mode == "atomicfirst" else "0")  # K2's first pass ranked by LDS atomics
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
