@@ -715,13 +715,30 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     // keep the 8-ballot ranking (all three passes atomic: sort 15.8 -> 13.1-14.1 ms, but stability
     // would then rest on an undocumented lane order; profiles/r05/ab_radixatomic_allpasses.json). The
     // first pass alone measured even (ab_radixatomic_first.json): off by default (MTB_RADIX_ATOMIC_FIRST)
-    if (atomicRank) {
+    if (atomicRank & 1) {
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
             const bool valid = i < n && (!FILTER || k[r] != kSentinel);
             const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
             rk[r] = valid ? (d << 16 | atomicAdd(&waveHist[w][d], 1u)) : ~0u;
+        }
+    } else if (!FILTER && !(atomicRank & 2) && tBase + kRadixTile <= n) {
+        // a full tile without sentinels (every tile of a sort but its last): every key is valid, so
+        // the ranking drops the per-key bound checks and the validity terms of its nine ballots
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) {
+            const uint32_t d = radix_digit(k[r], shift);
+            unsigned long long peers = ~0ull;
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const unsigned long long m = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? m : ~m;
+            }
+            const uint32_t before = waveHist[w][d];
+            const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
+            if (rankInWave == 0) waveHist[w][d] = before + (uint32_t)__popcll(peers);
+            rk[r] = d << 16 | (before + rankInWave);
         }
     } else
 #pragma unroll
@@ -815,7 +832,9 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         const char* xe = getenv("MTB_RADIX_XCD");
         const int xcd = xe ? atoi(xe) : 1;
         const int ns = shift + 8;
-        const int ar = first && unstableFirst ? 1 : 0;
+        // MTB_RADIX_FULLTILE=0 (A/B, read per sort): full tiles ranked by the general path too
+        const char* fe = getenv("MTB_RADIX_FULLTILE");
+        const int ar = (first && unstableFirst ? 1 : 0) | (fe && atoi(fe) == 0 ? 2 : 0);
         if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
