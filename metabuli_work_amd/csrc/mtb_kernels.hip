@@ -573,7 +573,12 @@ constexpr int kRadixItems = 32;
 constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
 constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
-__device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) { return (uint32_t)((k >> shift) & 0xFF); }
+// one 32-bit bit-field extract from the word holding the digit (shift is wave-uniform), not a 64-bit shift
+__device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) {
+    if (shift >= 32) return __builtin_amdgcn_ubfe((uint32_t)(k >> 32), (uint32_t)(shift - 32), 8u);
+    if (shift <= 24) return __builtin_amdgcn_ubfe((uint32_t)k, (uint32_t)shift, 8u);
+    return (uint32_t)((k >> shift) & 0xFF);
+}
 
 __device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab, uint32_t tile, uint64_t n,
                                                 uint64_t& base, uint64_t& end);
@@ -788,7 +793,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         for (uint32_t i = tid; i < sKept; i += kBlock) {
             const uint64_t o = sDst[sDig[i]] + i;
             keysOut[o] = sKV[i];
-            digOut[o] = (uint8_t)(sKV[i] >> nextShift);
+            digOut[o] = (uint8_t)radix_digit(sKV[i], nextShift);
         }
     } else {
         for (uint32_t i = tid; i < sKept; i += kBlock) keysOut[sDst[sDig[i]] + i] = sKV[i];
