@@ -565,12 +565,12 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
 // K2 LSD radix sort of (key, val) pairs on 8-bit digits of the key. Per pass: tile histograms
 // (digit-major so one device scan yields stable global offsets), scan, stable scatter through an
 // LDS-staged tile so each digit run leaves the block as one contiguous write. Each wave ranks its
-// own 1024-key slice with match-any ballots against a wave-private histogram, so the tile needs
-// two block barriers per pass rather than several per 256 keys. The first pass (FILTER) drops
+// own 2048-key slice against a wave-private histogram (from per-digit lane masks, or match-any
+// ballots), so the tile needs two block barriers per pass rather than several per 256 keys. The first pass (FILTER) drops
 // sentinel keys: the compaction of blank reserved slots costs nothing extra.
 // ------------------------------------------------------------------------------------------------
 constexpr int kRadixItems = 32;
-constexpr int kRadixTile = kBlock * kRadixItems;  // 4096 keys
+constexpr int kRadixTile = kBlock * kRadixItems;  // 8192 keys
 constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
 // one 32-bit bit-field extract from the word holding the digit (shift is wave-uniform), not a 64-bit shift
@@ -692,6 +692,8 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     // key loads (a dependent load per key in the write-out loop was the old bottleneck)
     const uint64_t digitBase = offs[(uint64_t)tid * nTiles + tile];
     for (int x = tid; x < kWaves * 256; x += kBlock) (&waveHist[0][0])[x] = 0;
+    if (atomicRank & 4)
+        for (int x = tid; x < kWaves * 256; x += kBlock) sKV[x] = 0;  // the digits' lane masks (below)
     __syncthreads();
 
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -719,7 +721,9 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     // instruction's lanes of one digit is the hardware's, so later passes, which must be stable,
     // keep the 8-ballot ranking (all three passes atomic: sort 15.8 -> 13.1-14.1 ms, but stability
     // would then rest on an undocumented lane order; profiles/r05/ab_radixatomic_allpasses.json). The
-    // first pass alone measured even (ab_radixatomic_first.json): off by default (MTB_RADIX_ATOMIC_FIRST)
+    // first pass alone measured even (ab_radixatomic_first.json): off by default (MTB_RADIX_ATOMIC_FIRST).
+    // atomicRank & 4 (the default): the lane-mask ranking below, stable by construction, in place of the
+    // nine ballots (sort 14.8 -> 14.2-14.3 ms same box, profiles/r05/ab_radix_orrank.json)
     if (atomicRank & 1) {
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) {
@@ -727,6 +731,28 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
             const bool valid = i < n && (!FILTER || k[r] != kSentinel);
             const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
             rk[r] = valid ? (d << 16 | atomicAdd(&waveHist[w][d], 1u)) : ~0u;
+        }
+    } else if (atomicRank & 4) {
+        // stable ranking from each digit's lane mask (sKV holds the masks until the keys are staged):
+        // every lane ORs its bit into its digit's word — the result does not depend on the order the
+        // lanes' ORs land in — and reads the word back (LDS operations of one wave complete in program
+        // order); the digit's lowest lane advances the count and clears the word for the next key
+        unsigned long long* sMask = reinterpret_cast<unsigned long long*>(sKV) + w * 256;
+#pragma unroll
+        for (int r = 0; r < kRadixItems; r++) {
+            const uint64_t i = base + (uint64_t)r * 64 + lane;
+            const bool valid = i < n && (!FILTER || k[r] != kSentinel);
+            const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
+            if (valid) __hip_atomic_fetch_or(&sMask[d], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const unsigned long long peers =
+                valid ? __hip_atomic_load(&sMask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
+            const uint32_t before = valid ? waveHist[w][d] : 0u;
+            const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
+            if (valid && rankInWave == 0) {
+                waveHist[w][d] = before + (uint32_t)__popcll(peers);
+                __hip_atomic_store(&sMask[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            rk[r] = valid ? (d << 16 | (before + rankInWave)) : ~0u;
         }
     } else if (!FILTER && !(atomicRank & 2) && tBase + kRadixTile <= n) {
         // a full tile without sentinels (every tile of a sort but its last): every key is valid, so
@@ -813,6 +839,13 @@ uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) 
 // Sorts n pairs by key bits [bitLo, bitHi). Returns the kept count (sentinels dropped when
 // filter). Result ends in (keysA, valsA) if the number of passes is even, else in (keysB, valsB);
 // *inB tells which. genVals: valsA is not read; the values are the input positions.
+// every pass ranked from the digits' lane masks (default: profiles/r05/ab_radix_orrank.json);
+// MTB_RADIX_ORRANK=0 (A/B, read per sort) ranks by the nine ballots
+static int radix_or_rank() {
+    const char* e = getenv("MTB_RADIX_ORRANK");
+    return !e || atoi(e) ? 4 : 0;
+}
+
 template <typename V>
 uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, uint64_t n, int bitLo, int bitHi,
                           bool filter, bool genVals, uint32_t* counts, uint64_t* offs, void* scanTmp, bool* inB,
@@ -839,7 +872,7 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         const int ns = shift + 8;
         // MTB_RADIX_FULLTILE=0 (A/B, read per sort): full tiles ranked by the general path too
         const char* fe = getenv("MTB_RADIX_FULLTILE");
-        const int ar = (first && unstableFirst ? 1 : 0) | (fe && atoi(fe) == 0 ? 2 : 0);
+        const int ar = (first && unstableFirst ? 1 : 0) | (fe && atoi(fe) == 0 ? 2 : 0) | radix_or_rank();
         if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
@@ -904,7 +937,8 @@ uint64_t radix_sort_binned(uint64_t* keysR, V* valsR, uint64_t* keysT, V* valsT,
     const char* xe = getenv("MTB_RADIX_XCD");
     const int xcd = xe ? atoi(xe) : 1;
     k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(keysR, valsR, 0, shift, offs, nTiles, keysT, valsT,
-                                                              ns < bitHi ? digT : nullptr, ns, xcd, tileTab, 0);
+                                                              ns < bitHi ? digT : nullptr, ns, xcd, tileTab,
+                                                              radix_or_rank());
     *inT = true;
     if (ns < bitHi) {  // the rest: plain passes over the Q contiguous pairs
         bool inB = false;

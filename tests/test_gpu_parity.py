@@ -179,7 +179,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "0:ballot", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -211,6 +211,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_K1F_BINS_DIG", "0" if mode == "binsnodig" else "1")  # K2's second pass reads the keys
     monkeypatch.setenv("MTB_LINE_EXT", "1" if mode == "ext" else "0")  # K4's runs from run-length lines (A/B)
     monkeypatch.setenv("MTB_RADIX_ATOMIC_FIRST", "1" if mode == "atomicfirst" else "0")  # K2's first pass ranked by LDS atomics
+    monkeypatch.setenv("MTB_RADIX_ORRANK", "0" if mode == "ballot" else "1")  # K2 ranked by ballots, or lane masks
     # warp-specialised resident blocks, resident blocks walking their tiles (the default form), one block per
     # tile; 24-KB tiles for the last two
     monkeypatch.setenv("MTB_SWEEP_PERSIST", {"perblock": "0", "persist": "1"}.get(mode, "2"))
@@ -233,6 +234,13 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
             assert len(gk) == clf.stats()["query_kmers"] and np.all(pre[1:] >= pre[:-1])
             assert np.array_equal(_kmer_sorted(gk), _kmer_sorted(okmers_present(okmers, db_dir, par)))
             assert clf.stats()["filter_reruns"] == (1 if mode == "binsover" else 0)
+        if mode in ("", "ballot"):
+            # K2's pair multiset, and its 24-bit prefix order, which the LSD passes after the first give only
+            # if they are stable (K1F's packing order, and so the order within a prefix, varies run to run)
+            gk = clf.query_kmers()
+            pre = _aa_rank(gk["value"], par.kmerFormat) >> np.uint64(12)
+            assert np.all(pre[1:] >= pre[:-1])
+            assert np.array_equal(_kmer_sorted(gk), _kmer_sorted(okmers_present(okmers, db_dir, par)))
         if mode == "spill":
             assert clf.stats()["spilled_matches"] > 0
             ores, otc = oc.classify(odb, opar, reads)
