@@ -738,6 +738,23 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         // lanes' ORs land in — and reads the word back (LDS operations of one wave complete in program
         // order); the digit's lowest lane advances the count and clears the word for the next key
         unsigned long long* sMask = reinterpret_cast<unsigned long long*>(sKV) + w * 256;
+        // a full tile without sentinels (every tile of a sort but its last): no per-key validity
+        // (MTB_RADIX_FULLTILE=0 for the A/B)
+        if (!FILTER && !(atomicRank & 2) && tBase + kRadixTile <= n) {
+#pragma unroll
+            for (int r = 0; r < kRadixItems; r++) {
+                const uint32_t d = radix_digit(k[r], shift);
+                __hip_atomic_fetch_or(&sMask[d], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned long long peers = __hip_atomic_load(&sMask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t before = waveHist[w][d];
+                const uint32_t rankInWave = (uint32_t)__popcll(peers & ltMask);
+                if (rankInWave == 0) {
+                    waveHist[w][d] = before + (uint32_t)__popcll(peers);
+                    __hip_atomic_store(&sMask[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                rk[r] = d << 16 | (before + rankInWave);
+            }
+        } else
 #pragma unroll
         for (int r = 0; r < kRadixItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
