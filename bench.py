@@ -88,6 +88,21 @@ def variant_batch(args, variant):
     return args.variant_batch or VARIANT_BATCH.get(variant, 2_000_000)
 
 
+def cpu_model() -> str:
+    """The host CPU's model name and the machine's logical CPUs (state nproc and the CPU
+    model beside the cores the baseline used)."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    name = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{name} (nproc {os.cpu_count()})"
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -158,44 +173,56 @@ def roofline_of(kern, names, alg, traffic):
     return out
 
 
-RANDOM_GATHER = os.path.join(ROOT, "profiles", "r01", "random_gather.json")
-# round 5 (tools/calib_random_fetch.sh): each of those random loads is one 128-B memory-side request
-# (TCC_EA0_RDREQ_128B = loads), so the ceiling above is the HBM's bandwidth at 128-B lines
-RANDOM_LINE_BYTES = 128
+# the random-line ceiling (tools/rand_gather.hip, tools/calib_random_fetch.sh): independent 4-B loads at
+# pseudo-random 64-B-aligned offsets of a buffer the size of the structure a kernel probes; every such
+# load is one 128-B memory-side read request (TCC_EA0_RDREQ_128B = loads), so the ceiling is the HBM's
+# bandwidth at 128-B lines (6.1-6.3 TB/s; a coalesced stream on the same box: 5.82 TB/s)
 RANDOM_CALIBRATION = os.path.join(ROOT, "profiles", "r05", "random_fetch_calibration.json")
+RANDOM_LINE_BYTES = 128
+# the random kernels and the buffer their random reads land in (GB): K1F the 5.4-GB probe lines,
+# the unstaged K4 the 144-GB DB records (and the run index)
+RANDOM_KERNELS = {"filter": 5.4, "match_join": 144.0}
 
 
-def random_roofline(kern, names, Qall, Q, matched, M, D, sweep=False):
-    """The random-access kernels against the chip's measured random-line ceiling
-    (tools/rand_gather.hip -> profiles/r01/random_gather.json: independent 4-B loads at random
-    64-B lines; the filter probes 5.4 GB of probe lines, the unstaged join 144 GB of records).
-    Requests per launch: K1F one probe line per emitted window (Qall; a syncmer scan emits about
-    half of its window slots); the unstaged K4 one run-index line and one record line per query,
-    one rank atomic per matched query, one scattered 16-B write per match."""
+def random_ceilings():
+    """{buffer_gb: ceiling TB/s at 128-B lines} of the calibration's plain random loads."""
     try:
-        with open(RANDOM_GATHER) as f:
+        with open(RANDOM_CALIBRATION) as f:
             runs = json.load(f)["runs"]
     except (OSError, ValueError, KeyError):
+        return {}
+    return {r["buffer_gb"]: r["tb_per_s_at_128B"] for r in runs if r.get("kind") == "load4"}
+
+
+def random_roofline(kern, names, traffic, Q=0, sweep=False):
+    """The random-access kernels against the chip's measured random-line ceiling, in bytes: the
+    kernel's HBM bytes per launch from the PMC passes (FETCH_SIZE doubled: a random read moves a
+    128-B line; WRITE_SIZE: a scattered 16-B store or atomic is one 32-B write request) over its
+    event-timed duration, against the random 128-B-line bandwidth over a buffer of the size it
+    probes. Reads, writes and atomics are each counted at the bytes they move, so frac <= 1 unless
+    the kernel beats the calibration itself. No PMC pass for the workload: no entry."""
+    ceil = random_ceilings()
+    tf, src = traffic
+    if not ceil or not tf:
         return None
-
-    def ceiling(gb):
-        return min(runs, key=lambda r: abs(r["buffer_gb"] - gb))["glines_per_s"]
-
     out = {}
-    req = {"filter": (float(Qall), 5.4)}
-    if D > 12 * Q and not sweep:
-        req["match_join"] = (2.0 * Q + float(matched) + M, 144.0)
-    for k, (r, gb) in req.items():
-        if k not in names or r <= 0:
+    for k, gb in RANDOM_KERNELS.items():
+        if k not in names or k not in tf.get("stages", {}) or (k == "match_join" and sweep):
             continue
+        st = tf["stages"][k]
         ms = float(kern[names.index(k)])
-        got = r / (ms * 1e-3) / 1e9
-        out[k] = {"requests_per_launch": int(r), "achieved_greq_per_s": round(got, 2),
-                  "ceiling_greq_per_s": ceiling(gb), "frac": round(got / ceiling(gb), 3),
-                  "ceiling_tb_per_s_at_128B": round(ceiling(gb) * RANDOM_LINE_BYTES / 1e3, 2),
-                  "source": os.path.relpath(RANDOM_GATHER, ROOT),
-                  "line_bytes_source": os.path.relpath(RANDOM_CALIBRATION, ROOT)}
-    return out
+        if ms <= 0 or not st.get("hbm_bytes"):
+            continue
+        c_gb = min(ceil, key=lambda g: abs(g - gb))
+        got = st["hbm_bytes"] / (ms * 1e-3) / 1e12
+        e = {"traffic_tb_per_s": round(got, 3), "ceiling_tb_per_s_at_128B": ceil[c_gb], "ceiling_buffer_gb": c_gb,
+             "frac": round(got / ceil[c_gb], 3), "hbm_bytes_per_launch": int(st["hbm_bytes"]),
+             "avg_launch_ms": round(ms, 3), "traffic_source": src,
+             "ceiling_source": os.path.relpath(RANDOM_CALIBRATION, ROOT)}
+        if Q > 0 and st.get("fetch_bytes"):
+            e["lines_fetched_per_query"] = round(st["fetch_bytes"] / RANDOM_LINE_BYTES / Q, 3)
+        out[k] = e
+    return out or None
 
 
 class Tally:
@@ -232,14 +259,59 @@ class Tally:
         alg = alg_bytes(self.avg("bases"), self.avg("reads"), self.avg("qall"), self.avg("q"), self.avg("m"), D,
                         live=self.avg("live"), probe=names is KERNELS_PROBE, mates=mates, dbread=self.avg("dbread"))
         return (roofline_of(kern, names, alg, traffic),
-                random_roofline(kern, names, self.avg("qall"), self.avg("q"), self.avg("matched"), self.avg("m"), D,
-                                sweep=self.avg("dbread") > 0))
+                random_roofline(kern, names, traffic, Q=self.avg("q"), sweep=self.avg("dbread") > 0))
 
 
 # ---------------------------------------------------------------------------------------------
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(gpus: int, argv, port: int):
+    """The command that runs this bench as `gpus` ranks on one node, one process per GPU (the
+    driver's own form: torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def resolve_world(gpus, env):
+    """How this process runs, from --gpus and the launcher's environment: ("launch", N) when it must
+    start N ranks itself (--gpus N > 1 and no WORLD_SIZE: the parent never touches the GPU), else
+    ("run", world). A WORLD_SIZE that disagrees with an explicit --gpus is an error: the line's n_gpus
+    would not be the GPU count asked for."""
+    ws = env.get("WORLD_SIZE")
+    if gpus is not None and gpus < 1:
+        raise ValueError(f"--gpus must be >= 1 (got {gpus})")
+    if ws is None:
+        return ("launch", gpus) if gpus is not None and gpus > 1 else ("run", 1)
+    ws = int(ws)
+    if gpus is not None and gpus != ws:
+        raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws}: launch with --nproc-per-node {gpus}, or drop --gpus")
+    return "run", ws
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Start `gpus` ranks as a child torch.distributed.run (before any GPU call in this process) and
+    return its exit code."""
+    import subprocess
+    if os.environ.get("MTB_BENCH_ONE_DEVICE") != "1":
+        have = torch.cuda.device_count()  # counts devices without initialising the GPU (this image)
+        if have < gpus:
+            raise SystemExit(f"[bench] --gpus {gpus} but {have} GPU(s) visible")
+    cmd = launcher_cmd(gpus, argv, free_port())
+    print(f"[bench] launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks, one process each). N > 1 without WORLD_SIZE: the bench starts the N ranks "
+                         "itself through torch.distributed.run; under a launcher it must equal WORLD_SIZE "
+                         "(default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=1_000_000, help="config 2: read pairs per rank per step")
@@ -311,12 +383,21 @@ def main():
                     help="GTDB cold open: idle seconds after freeing the resident DB (the driver's wipe of freed HBM)")
     ap.add_argument("--cold-pairs", type=int, default=10_000_000,
                     help="cold one-shot line: read pairs of the file classified by a freshly opened context (0 = off)")
-    ap.add_argument("--detail", default=os.path.join(ROOT, "profiles", "r05", "bench_detail.json"),
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--detail", default=DEFAULT_DETAIL,
                     help="side file for the full result tree (per-kernel splits, work counters, config-5 parts, "
                          "e2e host stages); the stdout line keeps the headline and one-line summaries")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    how, world = resolve_world(args.gpus, os.environ)
+    if how == "launch":
+        sys.exit(launch_ranks(world, sys.argv[1:]))
+    if args.launch_probe:  # tests: each rank reports what the launcher gave it, before any GPU call
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+        return
+    if world > 1 and args.detail == DEFAULT_DETAIL:
+        args.detail = DEFAULT_DETAIL.replace(".json", f"_n{world}.json")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N > 1 paths on a one-GPU box (never the measurement): MTB_BENCH_BACKEND=gloo and
@@ -333,7 +414,7 @@ def main():
             args.cpu_sample = 0
             args.skip_config2 = True
             args.variants = ""
-            args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = args.cold_pairs = 0
+            args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = args.cold_pairs = args.skewed_pairs = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.c5_only:
@@ -394,6 +475,7 @@ def main():
         dist.destroy_process_group()
 
 
+DEFAULT_DETAIL = os.path.join(ROOT, "profiles", "r06", "bench_detail.json")
 LINE_CAP = 8000  # the driver keeps only the tail of stdout (~15.5 KB): the one JSON line stays well under it
 
 
@@ -442,7 +524,7 @@ def _roof(r):
 def _cpu(c):
     if not isinstance(c, dict):
         return c
-    s = _pick(c, ("value", "unit", "cores", "kind", "sample"))
+    s = _pick(c, ("value", "unit", "cores", "cpu_model", "kind", "sample"))
     if isinstance(s.get("sample"), str) and len(s["sample"]) > 240:
         s["sample"] = s["sample"][:237] + "..."
     return s
@@ -477,8 +559,8 @@ def compact_line(out, detail_path):
     line["roofline"] = _roof(out.get("roofline"))
     line["cpu_baseline"] = _cpu(out.get("cpu_baseline"))
     if isinstance(out.get("random_roofline"), dict):
-        line["random_roofline"] = {k: _pick(v, ("frac", "achieved_greq_per_s", "ceiling_greq_per_s",
-                                                "ceiling_tb_per_s_at_128B"))
+        line["random_roofline"] = {k: _pick(v, ("frac", "traffic_tb_per_s", "ceiling_tb_per_s_at_128B",
+                                                "lines_fetched_per_query"))
                                    for k, v in out["random_roofline"].items()}
     if isinstance(out.get("pipeline_roofline"), dict):
         line["pipeline_roofline"] = _pick(out["pipeline_roofline"], ("achieved", "frac", "alg_bytes"))
@@ -613,7 +695,7 @@ def run_config2(args, world, rank, local, dev):
         tc0 = time.perf_counter()
         ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
         cpu_t = time.perf_counter() - tc0
-        cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+        cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "cpu_model": cpu_model(), "kind": "port",
                "sample": f"first {S} read pairs of the rank-0 batch, same DB; oracle/ (OpenMP C++ restatement "
                          f"of the reference path), {cpu_t:.1f}s wall",
                "stage_s": [round(x, 3) for x in stage_s]}
@@ -939,7 +1021,7 @@ def run_long_reads(args, open_clf, ls1, lo1, n50, world, rank, dev, odb, cores, 
         lres, ltc = oc.classify(odb, lopar, lreads)
         lcpu_t = time.perf_counter() - tc0
         gl = clfl.classify_batch(ls_h, lo_h)
-        long_cpu = {"value": round(LS / lcpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+        long_cpu = {"value": round(LS / lcpu_t, 1), "unit": "reads/s", "cores": cores, "cpu_model": cpu_model(), "kind": "port",
                     "sample": f"first {LS} long reads of the rank-0 shard, same DB, {lcpu_t:.1f}s wall",
                     "parity_sample": bool(np.array_equal(gl.results["classification"], lres["classification"])
                                           and np.array_equal(gl.results["score"].view(np.uint32),
@@ -1123,7 +1205,7 @@ def run_gtdb(args, world, rank, local, dev, variant=None):
             tc0 = time.perf_counter()
             ores, otc = oc.classify(odb, opar, reads, stage_s=stage_s)
             cpu_t = time.perf_counter() - tc0
-            cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+            cpu = {"value": round(S / cpu_t, 1), "unit": "reads/s", "cores": cores, "cpu_model": cpu_model(), "kind": "port",
                    "sample": f"first {S} read pairs of the rank-0 batch, same GTDB-scale DB re-encoded as diffIdx/"
                              f"info/split; oracle/ (OpenMP C++ restatement of the reference path), {cpu_t:.1f}s wall",
                    "stage_s": [round(x, 3) for x in stage_s]}

@@ -92,6 +92,19 @@ class BatchResult:
         return [(int(t), int(c)) for t, c in self.taxcnt[s:s + int(r["taxcnt_len"])]]
 
 
+@dataclasses.dataclass
+class _DevBatch:
+    """A batch classified in halves with its results left in HBM (Classifier._classify_halves_device):
+    the assembled device arrays and the halves' work counts and device times."""
+    results: object       # (n, 32) uint8 device tensor
+    taxcnt: object        # (T, 8) uint8 device tensor
+    query_kmers: int
+    matches: int
+    stats: dict
+    stage_ms: np.ndarray
+    kernel_ms: np.ndarray
+
+
 class Classifier:
     """GPU-resident classifier; one instance per device (mirrors Classifier.cpp:6-32)."""
 
@@ -125,6 +138,7 @@ class Classifier:
             check(lib().mtb_open(db_dir.encode(), ctypes.byref(cp), device, ctypes.byref(self.handle)), "mtb_open")
 
     def close(self) -> None:
+        self._dev_batch = None
         if self.handle:
             lib().mtb_close(self.handle)
             self.handle = ctypes.c_void_p()
@@ -170,7 +184,9 @@ class Classifier:
         check(lib().mtb_set_workspace_cap(self.handle, int(nbytes)), "mtb_set_workspace_cap")
 
     def release_workspace(self) -> None:
-        """Give the batch workspace back to the device (mtb_release_workspace)."""
+        """Give the batch workspace back to the device (mtb_release_workspace); an assembled batch
+        (_classify_halves_device) goes with it, so every getter sees the empty batch the C getters do."""
+        self._dev_batch = None
         check(lib().mtb_release_workspace(self.handle), "mtb_release_workspace")
 
     def set_stream(self, stream_ptr: int) -> None:
@@ -223,6 +239,7 @@ class Classifier:
         dev = torch.device("cuda", self.device)
         mid = n // 2
         recs, pools, qk, mm = [], [], 0, 0
+        stats, stage, kern = None, np.zeros(5, np.float32), np.zeros(7, np.float32)
         for lo, hi in ((0, mid), (mid, n)):
             o1 = off1[lo:hi + 1]
             o2 = off2[lo:hi + 1] if off2 is not None else None
@@ -235,9 +252,16 @@ class Classifier:
             recs.append(rec)
             pools.append(pool[:nt])
             qk, mm = qk + q, mm + m
+            # the batch's work counts and device times: the halves' summed (a batch maximum stays a
+            # maximum, the join path is the last half's)
+            st = self.stats()
+            stats = st if stats is None else {k: (max(stats[k], v) if k == "max_read_matches" else
+                                                  v if k == "join_path" else stats[k] + v) for k, v in st.items()}
+            stage += self.stage_ms()
+            kern += self.kernel_ms()
         recs[1].view(torch.int32).view(-1, _abi.RESULT_DTYPE.itemsize // 4)[:, 4] += pools[0].shape[0]
         torch.cuda.synchronize(dev)
-        self._dev_batch = (torch.cat(recs), torch.cat(pools), qk, mm)
+        self._dev_batch = _DevBatch(torch.cat(recs), torch.cat(pools), qk, mm, stats, stage, kern)
 
     def _classify_halves(self, seq1, off1, seq2, off2, n, device_input) -> BatchResult:
         """The batch as two read ranges (offsets stay absolute into the same bases), each split
@@ -255,6 +279,8 @@ class Classifier:
                            a.query_kmers + b.query_kmers, a.matches + b.matches, a.stage_ms + b.stage_ms)
 
     def taxcnt(self) -> np.ndarray:
+        if getattr(self, "_dev_batch", None) is not None:
+            return self._dev_batch.taxcnt.cpu().numpy().reshape(-1).view(TAXCNT_DTYPE).copy()
         nt = ctypes.c_uint64(0)
         lib().mtb_get_taxcnt(self.handle, ctypes.c_void_p(0), 0, ctypes.byref(nt))
         tc = np.zeros(int(nt.value), TAXCNT_DTYPE)
@@ -263,7 +289,7 @@ class Classifier:
 
     def last_counts(self) -> Tuple[int, int]:
         if getattr(self, "_dev_batch", None) is not None:
-            return self._dev_batch[2], self._dev_batch[3]
+            return self._dev_batch.query_kmers, self._dev_batch.matches
         q, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
         lib().mtb_last_counts(self.handle, ctypes.byref(q), ctypes.byref(m))
         return int(q.value), int(m.value)
@@ -274,19 +300,25 @@ class Classifier:
              "dup_key_queries"]
 
     def stats(self) -> dict:
-        """Work counts of the last batch (mtb_last_stats)."""
+        """Work counts of the last batch (mtb_last_stats; a batch assembled from halves: their sums)."""
+        if getattr(self, "_dev_batch", None) is not None:
+            return dict(self._dev_batch.stats)
         out = (ctypes.c_uint64 * len(self.STATS))()
         lib().mtb_last_stats(self.handle, out, len(self.STATS))
         return {k: int(v) for k, v in zip(self.STATS, out)}
 
     def stage_ms(self) -> np.ndarray:
+        if getattr(self, "_dev_batch", None) is not None:
+            return self._dev_batch.stage_ms.copy()
         ms = (ctypes.c_float * 5)()
         lib().mtb_last_stage_ms(self.handle, ms, 5)
         return np.array(list(ms), np.float32)
 
     def kernel_ms(self) -> np.ndarray:
         """[extract, filter, k-mer sort, join, match transpose, match sort, assign] of the last batch
-        (HIP events; the sort is 0 on the probe join)."""
+        (HIP events; the sort is 0 on the probe join; a batch assembled from halves: their sums)."""
+        if getattr(self, "_dev_batch", None) is not None:
+            return self._dev_batch.kernel_ms.copy()
         ms = (ctypes.c_float * 7)()
         lib().mtb_last_kernel_ms(self.handle, ms, 7)
         return np.array(list(ms), np.float32)
@@ -302,13 +334,13 @@ class Classifier:
 
     def copy_results(self, dst_ptr: int, on_device: bool = True) -> None:
         if getattr(self, "_dev_batch", None) is not None:
-            return self._copy_dev(self._dev_batch[0], dst_ptr, on_device)
+            return self._copy_dev(self._dev_batch.results, dst_ptr, on_device)
         check(lib().mtb_copy_results(self.handle, ctypes.c_void_p(dst_ptr), int(on_device)), "mtb_copy_results")
 
     def n_taxcnt(self) -> int:
         """Pooled taxID:count entries of the last batch."""
         if getattr(self, "_dev_batch", None) is not None:
-            return int(self._dev_batch[1].shape[0])
+            return int(self._dev_batch.taxcnt.shape[0])
         nt = ctypes.c_uint64(0)
         lib().mtb_get_taxcnt(self.handle, ctypes.c_void_p(0), 0, ctypes.byref(nt))
         return int(nt.value)
@@ -316,8 +348,8 @@ class Classifier:
     def copy_taxcnt(self, dst_ptr: int, on_device: bool = True) -> int:
         """The last batch's pooled taxID:count entries to dst (8 B each); returns their number."""
         if getattr(self, "_dev_batch", None) is not None:
-            self._copy_dev(self._dev_batch[1], dst_ptr, on_device)
-            return int(self._dev_batch[1].shape[0])
+            self._copy_dev(self._dev_batch.taxcnt, dst_ptr, on_device)
+            return int(self._dev_batch.taxcnt.shape[0])
         nt = ctypes.c_uint64(0)
         check(lib().mtb_copy_taxcnt(self.handle, ctypes.c_void_p(dst_ptr), int(on_device), ctypes.byref(nt)),
               "mtb_copy_taxcnt")

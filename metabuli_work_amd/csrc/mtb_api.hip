@@ -178,7 +178,9 @@ struct mtb_ctx {
     std::shared_ptr<void> pipelineCache;  // mtb_pipeline.cpp's slots, kept between runs
     mutable mtb::TaxText taxText;  // per taxID: original ID digits + rank, built on first use
     mutable std::once_flag taxTextOnce;
-    // batch workspace
+    // batch workspace. ws comes before every DevBuf: members are destroyed in reverse order, and a
+    // DevBuf still holding memory at mtb_close gives its bytes back to ws in its destructor
+    WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
     DevBuf seq1, off1, seq2, off2, meta, reserve, slotOff, qlen, scanTmp;
     DevBuf keysA, valsA, keysB, valsB, radixCounts, radixOffs;
     DevBuf readCnt, mOff, matches, matchesSorted, segScratch, maxSeg, errFlag;
@@ -195,7 +197,6 @@ struct mtb_ctx {
     DevBuf binCnt, binTab;                  // binned K1F: bucket counts (kSortBins u64), K2's tile table
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     uint64_t liveM = 0;                     // matches K6 read in the last batch
-    WsBudget ws;                            // the batch buffers' bytes (+ MTB_WORKSPACE_CAP)
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
     double openS[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [7]: the records' allocation (inside [1])
@@ -1821,6 +1822,9 @@ void ctx_release_workspace(mtb_ctx* c) {
     c->keepStages = false;
     c->emValid = c->emPackedValid = false;
     c->emHost.clear();
+    for (auto& v : c->stats) v = 0;  // mtb_last_stats / _stage_ms / _kernel_ms: the empty batch too
+    for (auto& v : c->stageMs) v = 0.f;
+    for (auto& v : c->kernMs) v = 0.f;
 }
 
 std::shared_ptr<void>& ctx_pipeline_cache(mtb_ctx* c) { return c->pipelineCache; }

@@ -944,7 +944,22 @@ uint64_t radix_sort_binned(uint64_t* keysR, V* valsR, uint64_t* keysT, V* valsT,
     for (int r = 0; r < kSortBins; r++) Q += binHost[r];
     const uint32_t nTiles = (uint32_t)radix_binned_tiles(binHost, rc);
     *inT = false;
-    if (!nTiles || bitLo + 8 >= bitHi) return Q;
+    if (!nTiles) return Q;
+    if (bitLo + 8 >= bitHi) {
+        // one pass in all: K1F's buckets are already the sorted order, but gapped (bucket r at r * rc);
+        // pack them into (keysT, valsT) slots [0, Q) as the caller reads them (never taken with
+        // kQuerySortLo/Hi, which need three passes)
+        uint64_t o = 0;
+        for (int r = 0; r < kSortBins; r++) {
+            const uint64_t n = std::min<uint64_t>(binHost[r], rc);
+            if (!n) continue;
+            hipMemcpyAsync(keysT + o, keysR + (uint64_t)r * rc, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+            hipMemcpyAsync(valsT + o, valsR + (uint64_t)r * rc, n * sizeof(V), hipMemcpyDeviceToDevice, s);
+            o += n;
+        }
+        *inT = true;
+        return o;
+    }
     // the second pass (bits bitLo + 8 ..) over the buckets in order -> (keysT, valsT) from slot 0
     k_bin_tiles<<<1, kBlock, 0, s>>>(binDev, rc, tileTab);
     const int shift = bitLo + 8, ns = shift + 8;

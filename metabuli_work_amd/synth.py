@@ -184,6 +184,13 @@ def make_genomes(taxo: Taxonomy, genome_len: int = 20000, strain_div: float = 0.
             emit(base, sp, sp)
         for k in kids:
             emit(_mutate(rng, base, strain_div), k, sp)
+    return _with_blocks(rng, seqs, taxids, species, min_block, max_block)
+
+
+def _with_blocks(rng, seqs, taxids, species, min_block: int = 300, max_block: int = 3000) -> Genomes:
+    """Genomes with gene blocks (the stand-in for Prodigal's gene calls that the DB writer extracts
+    k-mers from): consecutive blocks of min_block..max_block bases on a random strand, short gaps
+    between them."""
     off = np.zeros(len(seqs) + 1, np.uint64)
     off[1:] = np.cumsum([len(s) for s in seqs])
     bg, bs, be, bst = [], [], [], []
@@ -197,6 +204,28 @@ def make_genomes(taxo: Taxonomy, genome_len: int = 20000, strain_div: float = 0.
             pos = end + 1 + int(rng.integers(0, 60))
     return Genomes(np.concatenate(seqs), off, np.array(taxids, np.int32), np.array(species, np.int32),
                    np.array(bg, np.int32), np.array(bs, np.int32), np.array(be, np.int32), np.array(bst, np.int32))
+
+
+CONFIG1_GENOME_LENS = (2_000_000, 1_500_000, 1_000_000)
+
+
+def make_config1(seed: int = 1):
+    """SURVEY §8(d) config 1 (BASELINE.json configs[0], the reference's CPU-runnable case): three
+    random genomes (GC 0.5; 2.0 / 1.5 / 1.0 Mbp; seed 1), each its own species in one genus —
+    root 1 -> genus 2 -> species 3, 4, 5 -> strains 6, 7, 8 (a genome per strain). Returns
+    (Taxonomy, Genomes)."""
+    rng = np.random.default_rng(seed)
+    taxo = Taxonomy(np.array([1, 2, 3, 4, 5, 6, 7, 8], np.int32), np.array([1, 1, 2, 2, 2, 3, 4, 5], np.int32),
+                    ["no rank", "genus", "species", "species", "species", "no rank", "no rank", "no rank"],
+                    ["root", "genus_2", "species_3", "species_4", "species_5", "strain_6", "strain_7", "strain_8"])
+    seqs = [_random_dna(rng, L, gc=0.5) for L in CONFIG1_GENOME_LENS]
+    return taxo, _with_blocks(rng, seqs, [6, 7, 8], [3, 4, 5])
+
+
+def make_config1_reads(gen: Genomes, n_reads: int = 10_000, seed: int = 2) -> Reads:
+    """Config 1's reads: single-end 150 bp, 90% sampled from the genomes with 0.5% substitutions,
+    10% random; seed 2."""
+    return make_reads(gen, n_reads, paired=False, read_len=150, sub_rate=0.005, random_frac=0.1, seed=seed)
 
 
 def concat_reads(parts: List["Reads"]) -> "Reads":

@@ -138,6 +138,7 @@ def test_device_resident_batch_split_on_retry(make_db, frac):
 
     with Classifier(par, db_dir=db_dir) as full:
         ref = run(full)
+        ref_stats = full.stats()
         ws = full.workspace_bytes
     with Classifier(par, db_dir=db_dir) as capped:
         capped.set_workspace_cap(int(ws * frac))
@@ -145,11 +146,21 @@ def test_device_resident_batch_split_on_retry(make_db, frac):
         assert capped.workspace_bytes <= int(ws * frac)
         _same(got, ref)
         assert got.query_kmers == ref.query_kmers and got.matches == ref.matches
+        # every getter serves the assembled batch: the host taxID:count list, the work
+        # counts summed over the pieces, the pieces' device times
+        assert np.array_equal(capped.taxcnt(), ref.taxcnt)
+        st = capped.stats()
+        assert st["query_kmers"] == ref.query_kmers and st["matches"] == ref.matches
+        assert st["slots"] == ref_stats["slots"] and st["max_read_matches"] == ref_stats["max_read_matches"]
+        assert capped.stage_ms()[4] > 0 and capped.kernel_ms().sum() > 0
         # a later batch that fits serves the context's own buffers again
         small = capped.classify_batch(r.seq1, r.off1[:101], r.seq2, r.off2[:101])
         assert np.array_equal(small.results["classification"], ref.results["classification"][:100])
+        # a second assembled batch, then a release: nothing of it is served afterwards
+        run(capped)
         capped.release_workspace()
         assert capped.n_taxcnt() == 0 and capped.last_counts() == (0, 0)
+        assert len(capped.taxcnt()) == 0 and capped.stats()["matches"] == 0
     odb = oc.OracleDb(db_dir)
     ores, otc = oc.classify(odb, par.to_c(), r)
     odb.close()
