@@ -257,6 +257,29 @@ int mtb_memcpy(void* dst, const void* src, uint64_t bytes);
 int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint64_t n, uint8_t* sum, uint16_t* fwd,
                 uint16_t* rev);
 
+/* The path's dependency-free helper functions on the device, as the kernels call them (round 6;
+ * pinned by tests/golden/ref_functions.json, which the reference's own function bodies computed):
+ * fn selects one, every case i reads param[i], a[i], b[i] and writes out[i] (floats as their IEEE
+ * bit pattern; MTB_PIN_TAXONOMER_SHAPE writes 6 values per case). n_out = cases written (values for
+ * the decode). Host arrays. */
+#define MTB_PIN_SCORE_INCREMENT 0     /* Taxonomer::calScoreIncrement(a, shift = param), Taxonomer.cpp:650-661 */
+#define MTB_PIN_HAMMING_INCREMENT 1   /* calHammingDistIncrement(a, param), :663-669                            */
+#define MTB_PIN_IS_CONSECUTIVE 2      /* isConsecutive(dna a, dna b, shift = param; 0 = no shift), :671-683     */
+#define MTB_PIN_IS_CONSECUTIVE2 3     /* isConsecutive2(a, b, param), :686-699                                 */
+#define MTB_PIN_MATCH_SCORE 4         /* Match::getScore of rightEndHamming a, Match.h:32-44                   */
+#define MTB_PIN_RIGHT_PART_SCORE 5    /* Match::getRightPartScore(range = param), Match.h:46-57               */
+#define MTB_PIN_LEFT_PART_SCORE 6     /* Match::getLeftPartScore(param), Match.h:59-70                        */
+#define MTB_PIN_RIGHT_PART_HAMMING 7  /* Match::getRightPartHammingDist(param), Match.h:72-78                 */
+#define MTB_PIN_LEFT_PART_HAMMING 8   /* Match::getLeftPartHammingDist(param), Match.h:80-86                  */
+#define MTB_PIN_MAX_COVERED_LENGTH 9  /* LocalUtil::getMaxCoveredLength<int>(a), LocalUtil.h:50-59            */
+#define MTB_PIN_QUERY_KMER_NUMBER 10  /* LocalUtil::getQueryKmerNumber<int>(a, spaceNum = param), :45-48       */
+#define MTB_PIN_TAXONOMER_SHAPE 11    /* a = syncmer << 16 | smer_len, b = seq_mode: dnaShift, maxCodonShift,
+                                       * denominator, bitsPerCodon, totalDnaBits, lastCodonMask (Taxonomer.cpp:34-58) */
+#define MTB_PIN_DECODE_DIFF_IDX 12    /* a = n diffIdx words: every k-mer value (getNextTargetKmer,
+                                       * KmerMatcher.h:282-297) through K3's decode (decode_diff_chunk)   */
+int mtb_pin_eval(int device, int fn, const int64_t* param, const uint64_t* a, const uint64_t* b, uint64_t n,
+                 int64_t* out, uint64_t* n_out);
+
 /* Diagnostics (round 5): the opened DB's run-length lines (the unstaged join's runs without a
  * run-index read) checked against its run index for every present AA rank within their reach:
  * out[0] ranks checked, out[1] those the codes resolve, out[2] mismatches (MTB_ERR_INTERNAL when

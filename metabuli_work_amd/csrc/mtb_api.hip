@@ -2237,3 +2237,63 @@ int mtb_assign_matches(mtb_ctx* c, const mtb_match* m, uint64_t nm, const uint32
 }
 
 }  // extern "C"
+
+extern "C" int mtb_pin_eval(int device, int fn, const int64_t* param, const uint64_t* a, const uint64_t* b,
+                            uint64_t n, int64_t* out, uint64_t* n_out) {
+    if (!n_out || (n && (!a || !out || (fn != MTB_PIN_DECODE_DIFF_IDX && !param)))) {
+        set_error("null argument");
+        return MTB_ERR_ARG;
+    }
+    *n_out = 0;
+    if (fn < MTB_PIN_SCORE_INCREMENT || fn > MTB_PIN_DECODE_DIFF_IDX) { set_error("unknown pin function"); return MTB_ERR_ARG; }
+    if (fn == MTB_PIN_TAXONOMER_SHAPE) {  // the host-side parameters the assign kernels get (assign_args)
+        for (uint64_t i = 0; i < n; i++) {
+            mtb_params par;
+            mtb_default_params(&par);
+            par.syncmer = (int)(a[i] >> 16);
+            par.smer_len = (int)(a[i] & 0xFF);
+            par.seq_mode = (int)b[i];
+            const AssignArgs g = assign_args(par);
+            const int64_t v[6] = {g.dnaShift, g.maxCodonShift, g.denominator, kBitsPerCodon, kTotalDnaBits,
+                                  (int64_t)((1u << (kTotalDnaBits - kBitsPerCodon)) - 1u)};
+            for (int k = 0; k < 6; k++) out[6 * i + k] = v[k];
+        }
+        *n_out = n;
+        return MTB_OK;
+    }
+    if (!n) return MTB_OK;
+    HIP_TRY(hipSetDevice(device));
+    if (fn == MTB_PIN_DECODE_DIFF_IDX) {  // K3 as mtb_open runs it: one chunk from the stream's start
+        std::vector<uint16_t> w(n);
+        for (uint64_t i = 0; i < n; i++) w[i] = (uint16_t)a[i];
+        DevBuf diff, flag, idx, tmp, val;
+        HIP_TRY(diff.ensure(2 * n));
+        HIP_TRY(flag.ensure(4 * n));
+        HIP_TRY(idx.ensure(8 * (n + 2)));
+        HIP_TRY(tmp.ensure(scan_tmp_elems(n) * sizeof(uint64_t)));
+        HIP_TRY(val.ensure(8 * n));
+        HIP_TRY(hipMemcpy(diff.p, w.data(), 2 * n, hipMemcpyHostToDevice));
+        uint64_t lastTerm = 0, lastValue = 0;
+        const uint64_t terms = decode_diff_chunk(diff.as<uint16_t>(), n, 0, val.as<uint64_t>(), flag.as<uint32_t>(),
+                                                 idx.as<uint64_t>(), tmp.p, &lastTerm, &lastValue, nullptr);
+        HIP_TRY(hipGetLastError());
+        if (terms && lastTerm != n - 1) { set_error("diffIdx ends mid k-mer"); return MTB_ERR_DB; }
+        HIP_TRY(hipMemcpy(out, val.p, 8 * terms, hipMemcpyDeviceToHost));
+        *n_out = terms;
+        return MTB_OK;
+    }
+    DevBuf dp, da, db, dout;
+    HIP_TRY(dp.ensure(8 * n));
+    HIP_TRY(da.ensure(8 * n));
+    HIP_TRY(db.ensure(8 * n));
+    HIP_TRY(dout.ensure(8 * n));
+    HIP_TRY(hipMemcpy(dp.p, param, 8 * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(da.p, a, 8 * n, hipMemcpyHostToDevice));
+    if (b) HIP_TRY(hipMemcpy(db.p, b, 8 * n, hipMemcpyHostToDevice));
+    else HIP_TRY(hipMemset(db.p, 0, 8 * n));
+    launch_pin_eval(fn, dp.as<int64_t>(), da.as<uint64_t>(), db.as<uint64_t>(), n, dout.as<int64_t>(), nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout.p, 8 * n, hipMemcpyDeviceToHost));
+    *n_out = n;
+    return MTB_OK;
+}

@@ -1773,19 +1773,6 @@ struct Clade {
     int32_t removed;
 };
 
-__device__ __forceinline__ float score_fields(uint32_t reh, int range, bool left) {
-    float s = 0.0f;
-    for (int c = 0; c < range; c++) {
-        uint32_t h = left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u;
-        s += codon_score(h);
-    }
-    return s;
-}
-__device__ __forceinline__ int ham_fields(uint32_t reh, int range, bool left) {
-    int s = 0;
-    for (int c = 0; c < range; c++) s += (int)(left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u);
-    return s;
-}
 
 // ------------------------------------------------------------------------------------------------
 // K6 as three kernels over the sorted match array. Work items are the runs the reference loops
@@ -1817,12 +1804,6 @@ __global__ void k_group_keys(const uint64_t* __restrict__ gStart, uint64_t nG, u
     vals[g] = 0;
 }
 
-// isConsecutive / isConsecutive2 (Taxonomer.cpp:677-699) of a current match (dc) and the next (dn)
-__device__ __forceinline__ bool consecutive(uint32_t dc, uint32_t dn, uint32_t sh, uint32_t lowMask, bool fwd,
-                                            int kmerFormat) {
-    if (kmerFormat == 2) return fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
-    return fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
-}
 
 // getMatchPaths with the DP state in registers: only the current and the next position group are
 // live, and both are almost always small (one DB k-mer per strain at a position). Returns false,
@@ -1907,18 +1888,13 @@ __device__ __forceinline__ bool match_paths_regs(const R& M, uint64_t start, uin
         }
         const int shift = (int)((nextPos - currPos) / 3);
         if (shift > 0 && shift <= cfg.maxCodonShift) {
-            const uint32_t sh = 3u * (uint32_t)shift;
-            const uint32_t lowMask = (1u << (24u - sh)) - 1u;
+            const uint32_t sh = kBitsPerCodon * (uint32_t)shift;
+            const uint32_t lowMask = (1u << (kTotalDnaBits - sh)) - 1u;
 #pragma unroll
             for (int x = 0; x < kRegPos; x++) {
                 if (x >= nn) continue;
-                float inc = 0.0f;
-                int hinc = 0;
-                for (int c = 0; c < shift; c++) {
-                    uint32_t h = (nr[x] >> (2 * c)) & 3u;
-                    inc += codon_score(h);
-                    hinc += (int)h;
-                }
+                const float inc = score_fields(nr[x], shift, false);  // calScoreIncrement
+                const int hinc = ham_fields(nr[x], shift, false);     // calHammingDistIncrement
                 bool found = false;
                 float bestScore = 0.0f;
                 Path bp{};
@@ -1999,29 +1975,18 @@ __device__ uint64_t match_paths_serial(const R& M, uint64_t start, uint64_t end,
         stepped = true;
         const int shift = (int)(((uint64_t)nextPos - currPos) / 3);
         if (shift > 0 && shift <= cfg.maxCodonShift) {
-            const uint32_t sh = 3u * (uint32_t)shift;
-            const uint32_t lowMask = (1u << (24u - sh)) - 1u;
+            const uint32_t sh = kBitsPerCodon * (uint32_t)shift;
+            const uint32_t lowMask = (1u << (kTotalDnaBits - sh)) - 1u;
             for (uint64_t nx = nxS; nx < nxE; nx++) {
                 const uint32_t nreh = M.reh(nx);
-                float inc = 0.0f;
-                int hinc = 0;
-                for (int c = 0; c < shift; c++) {
-                    uint32_t h = (nreh >> (2 * c)) & 3u;
-                    inc += codon_score(h);
-                    hinc += (int)h;
-                }
+                const float inc = score_fields(nreh, shift, false);  // calScoreIncrement
+                const int hinc = ham_fields(nreh, shift, false);     // calHammingDistIncrement
                 int64_t best = -1;
                 float bestScore = 0.0f;
                 const uint32_t dn = M.dna(nx);
                 for (uint64_t cu = curS; cu < curE; cu++) {
                     const uint32_t dc = M.dna(cu);
-                    bool cons;
-                    if (cfg.kmerFormat == 2) {  // isConsecutive2 (Taxonomer.cpp:692-699)
-                        cons = fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
-                    } else {                    // isConsecutive (Taxonomer.cpp:677-683)
-                        cons = fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
-                    }
-                    if (cons) {
+                    if (consecutive(dc, dn, sh, lowMask, fwd, cfg.kmerFormat)) {
                         conn[cu] = 1;
                         if (L[cu].score > bestScore) { best = (int64_t)cu; bestScore = L[cu].score; }
                     }
@@ -3477,6 +3442,42 @@ void launch_em_reclassify(const float* score, const uint32_t* spIdx, const int32
                           mtb_em_read* out, hipStream_t s) {
     TaxView tv{t.nodeOf, t.nodeTax, t.parent, t.depth, t.flags, t.spParent, t.maxTax};
     if (nQ) k_em_reclassify<<<(unsigned)((nQ + 255) / 256), 256, 0, s>>>(score, spIdx, spTax, qOff, qId, nQ, p, lf, tv, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// mtb_pin_eval: the helpers getMatchPaths, the path trims and K0 compute with, evaluated one case per
+// thread exactly as those kernels call them (tests: tests/golden/ref_functions.json, computed by the
+// reference's own function bodies).
+// ------------------------------------------------------------------------------------------------
+__global__ void k_pin_eval(int fn, const int64_t* __restrict__ param, const uint64_t* __restrict__ a,
+                           const uint64_t* __restrict__ b, uint64_t n, int64_t* __restrict__ out) {
+    MTB_GRID_STRIDE(i, n) {
+        const int p = (int)param[i];
+        const uint32_t x = (uint32_t)a[i];
+        const uint32_t sh = kBitsPerCodon * (uint32_t)(p ? p : 1);  // shift 0: the shift-less form, one codon
+        const uint32_t lowMask = (1u << (kTotalDnaBits - sh)) - 1u;
+        int64_t r = 0;
+        switch (fn) {
+            case MTB_PIN_SCORE_INCREMENT: r = __float_as_uint(score_fields(x, p, false)); break;
+            case MTB_PIN_HAMMING_INCREMENT: r = ham_fields(x, p, false); break;
+            case MTB_PIN_IS_CONSECUTIVE: r = consecutive(x, (uint32_t)b[i], sh, lowMask, true, 1); break;
+            case MTB_PIN_IS_CONSECUTIVE2: r = consecutive(x, (uint32_t)b[i], sh, lowMask, true, 2); break;
+            case MTB_PIN_MATCH_SCORE: r = __float_as_uint(score_fields(x, 8, false)); break;
+            case MTB_PIN_RIGHT_PART_SCORE: r = __float_as_uint(score_fields(x, p, false)); break;
+            case MTB_PIN_LEFT_PART_SCORE: r = __float_as_uint(score_fields(x, p, true)); break;
+            case MTB_PIN_RIGHT_PART_HAMMING: r = ham_fields(x, p, false); break;
+            case MTB_PIN_LEFT_PART_HAMMING: r = ham_fields(x, p, true); break;
+            case MTB_PIN_MAX_COVERED_LENGTH: r = max_covered_length((int)a[i]); break;
+            case MTB_PIN_QUERY_KMER_NUMBER: r = query_kmer_number((int)a[i], p); break;
+            default: r = -1;
+        }
+        out[i] = r;
+    }
+}
+
+void launch_pin_eval(int fn, const int64_t* param, const uint64_t* a, const uint64_t* b, uint64_t n, int64_t* out,
+                     hipStream_t s) {
+    if (n) k_pin_eval<<<stride_grid(n), 256, 0, s>>>(fn, param, a, b, n, out);
 }
 
 }  // namespace mtb

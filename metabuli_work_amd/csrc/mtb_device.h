@@ -51,6 +51,14 @@ __host__ __device__ inline int max_covered_length(int len) {
     int r = len % 3;
     return r == 2 ? len - 2 : (r == 1 ? len - 4 : len - 3);
 }
+__host__ __device__ inline int query_kmer_number(int len, int spaceNum = 0, int kLength = 8) {
+    return (max_covered_length(len) / 3 - kLength - spaceNum + 1) * 6;
+}
+
+// The Taxonomer's codon geometry (Taxonomer.cpp:50-58): 3-bit codons, 24 DNA bits (reduced-AA's
+// 4-bit codons are refused).
+constexpr uint32_t kBitsPerCodon = 3;
+constexpr uint32_t kTotalDnaBits = 24;
 
 // Base byte -> 2-bit code {A:0, C:1, T:2, G:3} or 7 (N / anything else). This is
 // nuc2int(atcg[c]) (GeneticCode.h:6, common.cpp:13-17) folded into one 256-entry table; the
@@ -151,6 +159,33 @@ __device__ __forceinline__ uint32_t hammings(uint64_t a, uint64_t b, bool revers
 
 // Match::getScore and partial scores (Match.h:32-70): 3 for an exact codon, else 2 - 0.5h.
 __host__ __device__ inline float codon_score(uint32_t h) { return h == 0 ? 3.0f : 2.0f - 0.5f * (float)h; }
+
+// The score of the first / last `range` codon fields of a rightEndHamming word, summed in the
+// reference's order: Match::getScore (range 8), getRightPartScore / getLeftPartScore (Match.h:32-70),
+// and Taxonomer::calScoreIncrement (the first `shift` fields, Taxonomer.cpp:650-661).
+__host__ __device__ inline float score_fields(uint32_t reh, int range, bool left) {
+    float s = 0.0f;
+    for (int c = 0; c < range; c++) {
+        uint32_t h = left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u;
+        s += codon_score(h);
+    }
+    return s;
+}
+// getRightPartHammingDist / getLeftPartHammingDist (Match.h:72-86), calHammingDistIncrement (Taxonomer.cpp:663-669)
+__host__ __device__ inline int ham_fields(uint32_t reh, int range, bool left) {
+    int s = 0;
+    for (int c = 0; c < range; c++) s += (int)(left ? (reh >> (14 - 2 * c)) & 3u : (reh >> (2 * c)) & 3u);
+    return s;
+}
+
+// isConsecutive / isConsecutive2 (Taxonomer.cpp:677-699) of a current match's DNA encoding (dc) and the
+// next's (dn), shifted by sh = 3 * shift bits (lowMask = 2^(24 - sh) - 1); fwd false: the two swapped,
+// as getMatchPaths' reverse frames call them (Taxonomer.cpp:600-620). Format 2 -> isConsecutive2.
+__host__ __device__ inline bool consecutive(uint32_t dc, uint32_t dn, uint32_t sh, uint32_t lowMask, bool fwd,
+                                            int kmerFormat) {
+    if (kmerFormat == 2) return fwd ? ((dc & lowMask) == (dn >> sh)) : ((dn & lowMask) == (dc >> sh));
+    return fwd ? ((dc >> sh) == (dn & lowMask)) : ((dn >> sh) == (dc & lowMask));
+}
 
 // The value of lane ^ J (J = 1..32) without the LDS crossbar (__shfl_xor is a ds_bpermute): DPP
 // quad_perm for 1 and 2, row_shl / row_shr for 4, row_ror:8 for 8 (a rotation by half a 16-lane row

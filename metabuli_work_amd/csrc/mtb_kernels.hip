@@ -238,13 +238,13 @@ __global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* _
     if (i >= n) return;
     int len1 = (int)(off1[i + 1] - off1[i]);
     int ql1 = max_covered_length(len1);
-    int w1 = ql1 / 3 - 7;  // getQueryKmerNumber / 6
+    int w1 = query_kmer_number(len1) / 6;  // windows per frame (KmerExtractor.cpp:462,481)
     int len2 = 0, ql2 = 0, w2 = 0;
     bool empty = w1 < 1;
     if (paired) {
         len2 = (int)(off2[i + 1] - off2[i]);
         ql2 = max_covered_length(len2);
-        w2 = ql2 / 3 - 7;
+        w2 = query_kmer_number(len2) / 6;
         if (w2 < 1) empty = true;
     }
     ReadMeta m;

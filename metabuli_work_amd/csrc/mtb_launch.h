@@ -333,6 +333,10 @@ void launch_dup_stats(const uint64_t* qkey, uint64_t Q, unsigned long long* out,
 // mtb_hamming's kernel (bad: u64 count of pairs where the row-cached and plain forms disagree)
 void launch_hamming_check(const uint64_t* a, const uint64_t* b, uint64_t n, uint8_t* sum, uint16_t* fwd, uint16_t* rev,
                           unsigned long long* bad, hipStream_t s);
+// mtb_pin_eval: the dependency-free helpers (score_fields, ham_fields, consecutive, max_covered_length,
+// query_kmer_number: mtb_device.h) on case vectors, fn = MTB_PIN_* (include/mtb_gpu.h), one thread per case
+void launch_pin_eval(int fn, const int64_t* param, const uint64_t* a, const uint64_t* b, uint64_t n, int64_t* out,
+                     hipStream_t s);
 void launch_match_windows(const uint64_t* qkey, uint64_t Q, const DbRec* db, uint64_t D, const AADir& dir,
                           int kmerFormat, uint64_t* win, hipStream_t s);
 

@@ -256,7 +256,7 @@ inline int maxCoveredLength(int len) {
     if (len % 3 == 1) return len - 4;
     return len - 3;
 }
-inline int queryKmerNumber(int len, int k = 8) { return (maxCoveredLength(len) / 3 - k + 1) * 6; }
+inline int queryKmerNumber(int len, int k = 8, int spaceNum = 0) { return (maxCoveredLength(len) / 3 - k - spaceNum + 1) * 6; }
 
 // QueryKmerInfo bitfield (Kmer.h:11-16): pos [0,32), seqID [32,61), frame [61,64).
 inline uint64_t packInfo(uint32_t seqId, uint32_t pos, uint32_t frame) {

@@ -48,6 +48,10 @@ struct Reads {
     uint32_t n;
 };
 
+// getNextTargetKmer (KmerMatcher.h:282-297) over a whole diffIdx word stream from 0: the values of its
+// whole k-mers in order; returns their number (orc_match.cpp; the pin hook, orc_pin_eval).
+uint64_t decodeDiffIdx(const uint16_t* diff, uint64_t nWords, uint64_t* values);
+
 // KmerExtractor::extractQueryKmers (KmerExtractor.cpp:52-81): fills the reserved buffer exactly as
 // the reference does (unused reserved slots stay {0,0}) and sorts it by compareQueryKmer.
 void extractQueryKmers(const mtb_params& par, const Reads& reads, std::vector<mtb_kmer>& buf,

@@ -48,6 +48,16 @@ static inline uint64_t nextTargetKmer(uint64_t looking, const uint16_t* diff, si
     return d + looking;
 }
 
+uint64_t decodeDiffIdx(const uint16_t* diff, uint64_t nWords, uint64_t* values) {
+    size_t idx = 0, totalPos = 0;
+    uint64_t v = 0, k = 0;
+    while (idx < nWords) {
+        v = nextTargetKmer(v, diff, idx, totalPos);
+        values[k++] = v;
+    }
+    return k;
+}
+
 struct QueryKmerSplit {
     size_t start, end;
     DiffIdxSplit split;

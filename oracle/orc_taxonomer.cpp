@@ -51,6 +51,43 @@ static int leftPartHamming(const mtb_match& m, int range) {
     return s;
 }
 
+// The Taxonomer constructor's shape parameters (Taxonomer.cpp:34-58; reducedAA is refused by the path,
+// so 3-bit codons): dnaShift, maxCodonShift, denominator, bitsPerCodon, totalDnaBits, lastCodonMask.
+struct TaxShape {
+    int dnaShift, maxCodonShift, denominator, bitsPerCodon, totalDnaBits;
+    uint32_t lastCodonMask;
+};
+static TaxShape taxShape(const mtb_params& par) {
+    TaxShape t;
+    if (par.syncmer) { t.dnaShift = (8 - par.smer_len) * 3; t.maxCodonShift = 8 - par.smer_len; }
+    else { t.dnaShift = 3; t.maxCodonShift = 1; }
+    t.denominator = (par.seq_mode == 1 || par.seq_mode == 2) ? 100 : 1000;
+    t.bitsPerCodon = 3; t.totalDnaBits = 24; t.lastCodonMask = 0x1FFFFF;
+    return t;
+}
+
+// calScoreIncrement / calHammingDistIncrement (Taxonomer.cpp:650-669)
+static float scoreIncrement(uint16_t h, int shift) {
+    float inc = 0;
+    for (int i = 0; i < shift; i++) {
+        uint8_t x = (h >> (i * 2)) & 3;
+        inc += (x == 0) ? 3.0f : 2.0f - 0.5f * x;
+    }
+    return inc;
+}
+static int hammingIncrement(uint16_t h, int shift) {
+    int inc = 0;
+    for (int i = 0; i < shift; i++) inc += (h >> (i * 2)) & 3;
+    return inc;
+}
+// isConsecutive / isConsecutive2 of two DNA encodings (Taxonomer.cpp:677-699)
+static bool consecutive1(uint32_t a, uint32_t b, int shift, int bitsPerCodon, int totalDnaBits) {
+    return (a >> (bitsPerCodon * shift)) == (b & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1));
+}
+static bool consecutive2(uint32_t a, uint32_t b, int shift, int bitsPerCodon, int totalDnaBits) {
+    return (a & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1)) == (b >> (bitsPerCodon * shift));
+}
+
 struct TaxonScore {
     TaxID taxId = 0;
     float score = 0.0f;
@@ -79,10 +116,12 @@ public:
         tieRatio = par.tie_ratio;
         accessionLevel = par.accession_level;
         kmerFormat = par.kmer_format;
-        if (par.syncmer) { dnaShift = (8 - par.smer_len) * 3; maxCodonShift = 8 - par.smer_len; }
-        else { dnaShift = 3; maxCodonShift = 1; }
-        denominator = (par.seq_mode == 1 || par.seq_mode == 2) ? 100 : 1000;
-        bitsPerCodon = 3; totalDnaBits = 24;
+        const TaxShape t = taxShape(par);
+        dnaShift = t.dnaShift;
+        maxCodonShift = t.maxCodonShift;
+        denominator = t.denominator;
+        bitsPerCodon = t.bitsPerCodon;
+        totalDnaBits = t.totalDnaBits;
     }
 
     void chooseBestTaxon(uint32_t currentQuery, size_t offset, size_t end, const mtb_match* matchList,
@@ -114,26 +153,13 @@ private:
     void getSpeciesCladeCounts(TaxID speciesTaxID);
     TaxID BFS(TaxID root, unsigned int maxCnt);
 
-    float calScoreIncrement(uint16_t h, int shift) const {
-        float inc = 0;
-        for (int i = 0; i < shift; i++) {
-            uint8_t x = (h >> (i * 2)) & 3;
-            inc += (x == 0) ? 3.0f : 2.0f - 0.5f * x;
-        }
-        return inc;
-    }
-    int calHammingDistIncrement(uint16_t h, int shift) const {
-        int inc = 0;
-        for (int i = 0; i < shift; i++) inc += (h >> (i * 2)) & 3;
-        return inc;
-    }
+    float calScoreIncrement(uint16_t h, int shift) const { return scoreIncrement(h, shift); }
+    int calHammingDistIncrement(uint16_t h, int shift) const { return hammingIncrement(h, shift); }
     bool isConsecutive(const mtb_match* a, const mtb_match* b, int shift) const {  // Taxonomer.cpp:677-683
-        return (a->dna_encoding >> (bitsPerCodon * shift)) ==
-               (b->dna_encoding & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1));
+        return consecutive1(a->dna_encoding, b->dna_encoding, shift, bitsPerCodon, totalDnaBits);
     }
     bool isConsecutive2(const mtb_match* a, const mtb_match* b, int shift) const {  // :692-699
-        return (a->dna_encoding & ((1U << (totalDnaBits - bitsPerCodon * shift)) - 1)) ==
-               (b->dna_encoding >> (bitsPerCodon * shift));
+        return consecutive2(a->dna_encoding, b->dna_encoding, shift, bitsPerCodon, totalDnaBits);
     }
 };
 
@@ -503,3 +529,55 @@ void emReassign(const Db& db, const mtb_em_map* maps, size_t n, size_t totalQuer
 }
 
 }  // namespace orc
+
+// Pin hook (test infrastructure: tests/test_oracle.py checks these restatements against
+// tests/golden/ref_functions.json, which the reference's own function bodies computed): the
+// dependency-free helpers above on caller vectors, fn = MTB_PIN_* (include/mtb_gpu.h).
+extern "C" int orc_pin_eval(int fn, const int64_t* param, const uint64_t* a, const uint64_t* b, uint64_t n,
+                            int64_t* out, uint64_t* n_out) {
+    using namespace orc;
+    auto fbits = [](float f) { uint32_t u; memcpy(&u, &f, 4); return (int64_t)u; };
+    *n_out = n;
+    if (fn == MTB_PIN_DECODE_DIFF_IDX) {
+        std::vector<uint16_t> w(n);
+        for (uint64_t i = 0; i < n; i++) w[i] = (uint16_t)a[i];
+        std::vector<uint64_t> v(n);
+        *n_out = decodeDiffIdx(w.data(), n, v.data());
+        for (uint64_t i = 0; i < *n_out; i++) out[i] = (int64_t)v[i];
+        return MTB_OK;
+    }
+    const TaxShape t = taxShape(mtb_params{});
+    for (uint64_t i = 0; i < n; i++) {
+        const int p = (int)param[i];
+        mtb_match m{};
+        m.right_end_hamming = (uint16_t)a[i];
+        switch (fn) {
+            case MTB_PIN_SCORE_INCREMENT: out[i] = fbits(scoreIncrement((uint16_t)a[i], p)); break;
+            case MTB_PIN_HAMMING_INCREMENT: out[i] = hammingIncrement((uint16_t)a[i], p); break;
+            case MTB_PIN_IS_CONSECUTIVE:  // shift 0: the shift-less form (one codon, lastCodonMask)
+                out[i] = consecutive1((uint32_t)a[i], (uint32_t)b[i], p ? p : 1, t.bitsPerCodon, t.totalDnaBits); break;
+            case MTB_PIN_IS_CONSECUTIVE2:
+                out[i] = consecutive2((uint32_t)a[i], (uint32_t)b[i], p ? p : 1, t.bitsPerCodon, t.totalDnaBits); break;
+            case MTB_PIN_MATCH_SCORE: out[i] = fbits(matchScore(m)); break;
+            case MTB_PIN_RIGHT_PART_SCORE: out[i] = fbits(rightPartScore(m, p)); break;
+            case MTB_PIN_LEFT_PART_SCORE: out[i] = fbits(leftPartScore(m, p)); break;
+            case MTB_PIN_RIGHT_PART_HAMMING: out[i] = rightPartHamming(m, p); break;
+            case MTB_PIN_LEFT_PART_HAMMING: out[i] = leftPartHamming(m, p); break;
+            case MTB_PIN_MAX_COVERED_LENGTH: out[i] = maxCoveredLength((int)a[i]); break;
+            case MTB_PIN_QUERY_KMER_NUMBER: out[i] = queryKmerNumber((int)a[i], 8, p); break;
+            case MTB_PIN_TAXONOMER_SHAPE: {
+                mtb_params par{};
+                par.syncmer = (int)(a[i] >> 16);
+                par.smer_len = (int)(a[i] & 0xFF);
+                par.seq_mode = (int)b[i];
+                const TaxShape q = taxShape(par);
+                const int64_t v[6] = {q.dnaShift, q.maxCodonShift, q.denominator, q.bitsPerCodon, q.totalDnaBits,
+                                      (int64_t)q.lastCodonMask};
+                for (int k = 0; k < 6; k++) out[6 * i + k] = v[k];
+                break;
+            }
+            default: return MTB_ERR_ARG;
+        }
+    }
+    return MTB_OK;
+}
