@@ -150,6 +150,11 @@ struct mtb_ctx {
     int binnedSort = 0;
     uint64_t binRcForce = 0;
     bool binDigits = true;  // MTB_K1F_BINS_DIG=0: the binned K1F writes no second-pass digits (K2 reads the keys)
+    // MTB_UNIFORM_UNITS: uniform K1 units (every read 6 per mate, k_read_units) when every frame of the
+    // batch is one chunk, so K4 rebuilds a matched query's info from its slot and a 4-B read length
+    // instead of a 16-B unit record (round 6)
+    bool uniformUnits = true;
+    uint32_t upr = 0;  // the last batch's units per read when uniform, else 0
     uint64_t binHost[kSortBins] = {};  // the last binned K1F's bucket counts
     bool noFilter = false;       // MTB_FILTER=0: no K1F; every non-blank window is sorted and joined
                                  // (with the sweep join the context then holds no probe lines either)
@@ -196,6 +201,7 @@ struct mtb_ctx {
     DevBuf digA, digB;                      // K2 digit side arrays (1 B per kept query k-mer, ping-pong)
     DevBuf binCnt, binTab;                  // binned K1F: bucket counts (kSortBins u64), K2's tile table
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
+    DevBuf readLens;                        // K0: the mates' lengths, 16 bits each (uniform units' K4)
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
@@ -467,6 +473,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     if (const char* e = getenv("MTB_K1F_BINS")) c->binnedSort = atoi(e);
     if (const char* e = getenv("MTB_K1F_BINS_RC")) c->binRcForce = strtoull(e, nullptr, 10);
     if (const char* e = getenv("MTB_K1F_BINS_DIG")) c->binDigits = atoi(e) != 0;
+    if (const char* e = getenv("MTB_UNIFORM_UNITS")) c->uniformUnits = atoi(e) != 0;
     if (!c->forceGeneric && !(c->joinMode == 3 && c->noFilter)) {
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
@@ -688,6 +695,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->binnedSort = src->binnedSort;
     c->binRcForce = src->binRcForce;
     c->binDigits = src->binDigits;
+    c->uniformUnits = src->uniformUnits;
     bind_workspace(c, src->ws.cap);
     *out = c;
     return MTB_OK;
@@ -704,7 +712,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     X(digB) X(binCnt) X(binTab) X(local) X(paths) X(comb) X(conn) X(spScore) X(spKeep) X(gFlag) X(sFlag) \
     X(pathCnt) X(gScan) X(sScan) X(gStart) X(sStart) X(clade) X(tcPool) X(tcLen) X(tcOff) X(tcOut) X(results) \
     X(emMap) X(emCnt) X(emScratch) X(emPacked) X(emCnt32) X(emOff) X(maskOut1) X(maskOut2) X(maskProb) \
-    X(maskScale)
+    X(maskScale) X(readLens)
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
 #define MTB_BUF_PTR(n) &c->n,
     return {MTB_BATCH_BUFS(MTB_BUF_PTR)};
@@ -1027,7 +1035,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
     if (!fused)
         launch_extract(dSeq1, dOff1, dSeq2, dOff2, c->meta.as<ReadMeta>(), c->slotOff.as<uint64_t>(),
                        c->unitRead.as<uint32_t>(), U, C, c->tables, c->par.kmer_format, c->par.syncmer,
-                       c->par.smer_len, c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s);
+                       c->par.smer_len, c->keysA.as<uint64_t>(), c->unitInfo.as<uint64_t>(), s, c->upr);
     HIP_TRY(hipEventRecord(c->kev[1], s));
     // K1F: the windows whose AA 8-mer the DB holds (MTB_FORCE_GENERIC: no filter, the sort's first
     // pass drops the sentinels)
@@ -1059,7 +1067,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                       c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
                                       c->rankHi, &c->Qall, slots, false, s,
                                       c->binDigits ? c->digA.as<uint8_t>() : nullptr,
-                                      c->binCnt.as<unsigned long long>(), rc, c->binHost);
+                                      c->binCnt.as<unsigned long long>(), rc, c->binHost, c->upr);
             HIP_TRY(hipGetLastError());
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             bool over = false;
@@ -1083,7 +1091,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                       c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
                                       c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
                                       c->rankHi, &c->Qall, cap, c->filterThreadMajor, s,
-                                      digits ? c->digA.as<uint8_t>() : nullptr);
+                                      digits ? c->digA.as<uint8_t>() : nullptr, nullptr, 0, nullptr, c->upr);
             HIP_TRY(hipGetLastError());
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             if (Q <= cap) break;
@@ -1253,7 +1261,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
                          direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
                          c->ovFlag.as<int>(), c->spillShift, direct ? c->longList.as<LongRun>() : nullptr,
-                         c->longCap, c->longCnt.as<uint32_t>(), s, c->lineExt);
+                         c->longCap, c->longCnt.as<uint32_t>(), s, c->lineExt, c->upr, c->readLens.as<uint32_t>());
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1535,15 +1543,18 @@ static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, cons
     HIP_TRY(c->qlen.ensure(sizeof(uint32_t) * (n + 1)));
     HIP_TRY(c->maxSeg.ensure(sizeof(uint32_t)));
     HIP_TRY(c->scanTmp.ensure(sizeof(uint64_t) * scan_tmp_elems(n + 1)));
+    HIP_TRY(c->readLens.ensure(sizeof(uint32_t) * (n + 1)));
     launch_read_meta(dOff1, dOff2, n, paired, c->meta.as<ReadMeta>(), c->qlen.as<uint32_t>(), c->maxSeg.as<uint32_t>(),
-                     s);
+                     c->readLens.as<uint32_t>(), s);
     uint32_t maxW = 0;
     HIP_TRY(hipMemcpyAsync(&maxW, c->maxSeg.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // chunk = the longest frame when it is short (no padding for uniform short reads), else 64
     const uint32_t C = std::min<uint32_t>(std::max<uint32_t>(maxW, 1), 64);
     c->maxW = maxW;
-    launch_read_units(c->meta.as<ReadMeta>(), n, C, c->reserve.as<uint32_t>(), s);
+    // uniform units: every frame one chunk (maxW <= 64), 6 units per mate for every read
+    c->upr = c->uniformUnits && maxW <= 64 ? (paired ? 12u : 6u) : 0u;
+    launch_read_units(c->meta.as<ReadMeta>(), n, C, c->upr, c->reserve.as<uint32_t>(), s);
     exclusive_scan_u32(c->reserve.as<uint32_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t U = 0;
     HIP_TRY(hipMemcpyAsync(&U, c->slotOff.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));

@@ -233,7 +233,7 @@ void exclusive_scan_u64(const uint64_t* in, uint64_t n, uint64_t* out, void* tmp
 // ------------------------------------------------------------------------------------------------
 __global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* __restrict__ off2, uint32_t n,
                             int paired, ReadMeta* __restrict__ meta, uint32_t* __restrict__ qlen,
-                            uint32_t* __restrict__ maxW) {
+                            uint32_t* __restrict__ maxW, uint32_t* __restrict__ readLens) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int len1 = (int)(off1[i + 1] - off1[i]);
@@ -253,16 +253,23 @@ __global__ void k_read_meta(const uint64_t* __restrict__ off1, const uint64_t* _
     m.w2 = (empty || !paired) ? 0 : w2;
     meta[i] = m;
     qlen[i] = (uint32_t)(ql1 + ql2);
+    // the mates' lengths in 16 bits each (K4 rebuilds a uniform unit's info from them; read only when
+    // every frame is one chunk, i.e. reads of a few hundred bases)
+    readLens[i] = (uint32_t)min(len1, 0xFFFF) | (uint32_t)min(len2, 0xFFFF) << 16;
     const uint32_t w = (uint32_t)max(m.w1, m.w2);
     if (w) atomicMax(maxW, w);
 }
 
-// K1 work units per read: each (mate, frame) is cut into chunks of C windows.
-__global__ void k_read_units(const ReadMeta* __restrict__ meta, uint32_t n, uint32_t C, uint32_t* __restrict__ units) {
+// K1 work units per read: each (mate, frame) is cut into chunks of C windows. Uniform units (upr > 0:
+// every frame of the batch fits one chunk): every read gets upr = 6 per mate units, a read whose mate
+// is too short included (its units hold no window), so unit u is read u / upr's (mate, frame)
+// u % upr and K4 needs no unit record (unit_windows, k_match).
+__global__ void k_read_units(const ReadMeta* __restrict__ meta, uint32_t n, uint32_t C, uint32_t upr,
+                             uint32_t* __restrict__ units) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const ReadMeta m = meta[i];
-    units[i] = 6u * ((uint32_t)(m.w1 + C - 1) / C + (uint32_t)(m.w2 + C - 1) / C);
+    units[i] = upr ? upr : 6u * ((uint32_t)(m.w1 + C - 1) / C + (uint32_t)(m.w2 + C - 1) / C);
 }
 
 __global__ void k_unit_read(const uint64_t* __restrict__ uOff, uint32_t n, uint32_t* __restrict__ unitRead) {
@@ -272,14 +279,14 @@ __global__ void k_unit_read(const uint64_t* __restrict__ uOff, uint32_t n, uint3
 }
 
 void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
-                      uint32_t* qlen, uint32_t* maxW, hipStream_t s) {
+                      uint32_t* qlen, uint32_t* maxW, uint32_t* readLens, hipStream_t s) {
     hipMemsetAsync(maxW, 0, sizeof(uint32_t), s);
     if (n == 0) return;
-    k_read_meta<<<(n + 255) / 256, 256, 0, s>>>(off1, off2, n, paired, meta, qlen, maxW);
+    k_read_meta<<<(n + 255) / 256, 256, 0, s>>>(off1, off2, n, paired, meta, qlen, maxW, readLens);
 }
 
-void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t* units, hipStream_t s) {
-    if (n) k_read_units<<<(n + 255) / 256, 256, 0, s>>>(meta, n, C, units);
+void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t upr, uint32_t* units, hipStream_t s) {
+    if (n) k_read_units<<<(n + 255) / 256, 256, 0, s>>>(meta, n, C, upr, units);
 }
 
 void launch_unit_read(const uint64_t* uOff, uint32_t n, uint32_t* unitRead, hipStream_t s) {
@@ -324,15 +331,17 @@ __device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits,
                                                     const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                     const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                     const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
-                                                    const uint32_t* __restrict__ unitRead, int kmerFormat) {
+                                                    const uint32_t* __restrict__ unitRead, int kmerFormat,
+                                                    uint32_t upr) {
     UnitWindows w{};
     if (u >= nUnits) return w;
-    const uint32_t r = unitRead[u];
+    const uint32_t r = upr ? (uint32_t)(u / upr) : unitRead[u];
     const ReadMeta m = meta[r];
-    const uint64_t first = uOff[r];
-    w.stretch = first | (uOff[r + 1] - first) << 40;
+    const uint64_t first = upr ? (uint64_t)r * upr : uOff[r];
+    w.stretch = first | (upr ? (uint64_t)upr : uOff[r + 1] - first) << 40;
     uint32_t local = (uint32_t)(u - first);
-    const uint32_t c1 = (uint32_t)(m.w1 + C - 1) / C, c2 = (uint32_t)(m.w2 + C - 1) / C;
+    // uniform units: one chunk per (mate, frame), windows or not (k_read_units)
+    const uint32_t c1 = upr ? 1u : (uint32_t)(m.w1 + C - 1) / C, c2 = upr ? 1u : (uint32_t)(m.w2 + C - 1) / C;
     uint32_t cpf = c1;
     int mate = 0;
     if (local >= 6 * c1) { local -= 6 * c1; mate = 1; cpf = c2; }
@@ -526,13 +535,14 @@ __global__ void __launch_bounds__(256) k_extract(const uint8_t* __restrict__ seq
                                                  const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
                                                  const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
                                                  ExtractTables tabs, int kmerFormat, int syncmer, int smerLen,
-                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ unitInfo) {
+                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ unitInfo,
+                                                 uint32_t upr) {
     __shared__ uint8_t sBase[256];
     __shared__ int8_t sAA[64], sNum[64];
     load_extract_tables(tabs, sBase, sAA, sNum);
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
-    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
+    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat, upr);
     // slots of this unit past its windows (and of padding units) hold the sentinel
     for (int p = max(w.nWin, 0); p < (int)C; p++) keys[slotBase + 64ull * p] = kSentinel;
     if (w.nWin <= 0) return;
@@ -553,12 +563,12 @@ static ExtractTables extract_tables(const HostTables& t) {
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
                     uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* unitInfo, hipStream_t s) {
+                    uint64_t* unitInfo, hipStream_t s, uint32_t upr) {
     if (nUnits == 0) return;
     const uint64_t threads = (nUnits + 63) / 64 * 64;  // whole waves: padding units write sentinels
     k_extract<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits,
                                                                 C, extract_tables(t), kmerFormat, syncmer, smerLen,
-                                                                keys, unitInfo);
+                                                                keys, unitInfo, upr);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1654,6 +1664,30 @@ void set_match_xcd(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on
 
 void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int)); }
 
+// The info of window p of uniform unit u (k_read_units: upr units per read, one per (mate, frame)), as
+// unit_windows + unit_info_at compute it: read u / upr, mate and frame from u % upr, the frame's first
+// window at its begin (KmerExtractor.cpp:374-378) plus the mate-2 offset (:341-345). Only the reverse
+// frames, the load orders from the right and mate 2 need the read's lengths (one 4-B load from a
+// 4-B-per-read array instead of the 16-B unit record of a unit array 12x its size).
+__device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, uint32_t upr,
+                                                      const uint32_t* __restrict__ readLens, int kmerFormat) {
+    const uint32_t r = u / upr, local = u - r * upr;
+    const uint32_t mate = local >= 6u ? 1u : 0u, frame = local - 6u * mate;
+    const bool fwd = frame < 3u;
+    const bool fromLeft = (kmerFormat == 2) ? fwd : !fwd;
+    uint32_t pos0 = frame, posOffset = 0;
+    if (mate || !fromLeft || !fwd) {
+        const uint32_t L = readLens[r];
+        const int len1 = (int)(L & 0xFFFFu), len = mate ? (int)(L >> 16) : len1;
+        const int used = max_covered_length(len);
+        int begin = (int)frame;
+        if (!fwd) { begin = (len % 3) - ((int)frame % 3); if (begin < 0) begin += 3; }
+        pos0 = fromLeft ? (uint32_t)begin : (uint32_t)(begin + used - 1 - 3 * 8 + 1);
+        if (mate) posOffset = (uint32_t)max_covered_length(len1) + 3u;
+    }
+    return unit_info_at(pack_info(r + 1, pos0 + posOffset, frame), p, kmerFormat);
+}
+
 template <bool kStage, int kPer>
 __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
@@ -1668,7 +1702,8 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
                                                int* __restrict__ overflow, uint32_t capShift,
                                                LongRun* __restrict__ longList, uint32_t longCap,
-                                               uint32_t* __restrict__ longCnt, const ProbeExt* __restrict__ lineExt) {
+                                               uint32_t* __restrict__ longCnt, const ProbeExt* __restrict__ lineExt,
+                                               uint32_t upr, const uint32_t* __restrict__ readLens) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -1924,7 +1959,13 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                    : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
                             : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
-        if (c[j]) {  // only matched queries need their info and their read's segment bounds (one 16-B load)
+        if (c[j] && upr) {  // uniform units: the info and the segment bounds from the slot and the read's lengths
+            uint32_t p;
+            const uint32_t u = slot_unit(slot[j], C, p);
+            info[j] = uniform_unit_info(u, p, upr, readLens, kmerFormat);
+            const uint64_t r = info_seq(info[j]) - 1;
+            stretch[j] = r * upr | (uint64_t)upr << 40;
+        } else if (c[j]) {  // only matched queries need their info and their read's segment bounds (one 16-B load)
             uint32_t p;
             const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot[j], C, p)];
             info[j] = unit_info_at(ur.x, p, kmerFormat);
@@ -2180,7 +2221,8 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                                                         uint64_t* __restrict__ qkey, uint32_t* __restrict__ qslot,
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
                                                         uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig,
-                                                        unsigned long long* __restrict__ binCnt, uint64_t binRc) {
+                                                        unsigned long long* __restrict__ binCnt, uint64_t binRc,
+                                                        uint32_t upr) {
     __shared__ uint8_t sBase[256];
     __shared__ uint32_t sBin[256];
     __shared__ uint32_t sBinBase[256];
@@ -2196,7 +2238,7 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
     load_extract_tables(tabs, sBase, sAA, sNum);  // syncs
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t slotBase = (u >> 6) * 64ull * C + (u & 63u);
-    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat);
+    const UnitWindows w = unit_windows(u, nUnits, C, seq1, off1, seq2, off2, meta, uOff, unitRead, kmerFormat, upr);
     if (w.nWin > 0) {
         reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
         atomicMax(&sMaxWin, (uint32_t)w.nWin);
@@ -2374,7 +2416,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
                                uint64_t cap, bool threadMajor, hipStream_t s, uint8_t* qdig,
-                               unsigned long long* binCnt, uint64_t binRc, uint64_t* binHost) {
+                               unsigned long long* binCnt, uint64_t binRc, uint64_t* binHost, uint32_t upr) {
     if (binRc) {
         // binned output: the writes go to 2048 regions of binRc slots; the bucket counts come back
         threadMajor = false;
@@ -2391,11 +2433,11 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
 #define MTB_EF(P, J)                                                                                                  \
     k_extract_filter<P, J, false><<<blocks, 256, lds, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,         \
                                                   extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
-                                                  qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc)
+                                                  qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr)
         if (binRc) {
             k_extract_filter<kFilterPer, true, true><<<blocks, 256, lds, s>>>(
                 seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc);
+                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr);
         } else if (per == 8) {
             if (jMajor) MTB_EF(8, true);
             else MTB_EF(8, false);
@@ -2428,11 +2470,11 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
             hipEventRecord(ev[0], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0);
+                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0, upr);
             hipEventRecord(ev[1], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0);
+                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0, upr);
             hipEventRecord(ev[2], s);
             hipStreamSynchronize(s);
             float a = 0, b = 0;
@@ -2704,7 +2746,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
-                  const ProbeExt* lineExt) {
+                  const ProbeExt* lineExt, uint32_t upr, const uint32_t* readLens) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -2715,14 +2757,14 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
                                                         overflow, capShift, longList, longCap, longCnt,
-                                                        runOff ? lineExt : nullptr);
+                                                        runOff ? lineExt : nullptr, upr, readLens);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
                                                             stats, direct, dirOff, overflow, capShift, nullptr, 0,
-                                                            longCnt, nullptr);
+                                                            longCnt, nullptr, upr, readLens);
     }
 }
 

@@ -86,15 +86,16 @@ void launch_run_index(const mtb_match* M, uint64_t nM, uint8_t* flags, unsigned 
                       uint64_t* sScan, uint64_t* gStart, uint64_t* sStart, hipStream_t s);
 
 void launch_read_meta(const uint64_t* off1, const uint64_t* off2, uint32_t n, int paired, ReadMeta* meta,
-                      uint32_t* qlen, uint32_t* maxW, hipStream_t s);
-void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t* units, hipStream_t s);
+                      uint32_t* qlen, uint32_t* maxW, uint32_t* readLens, hipStream_t s);
+// upr > 0: uniform units (every read upr units, one per (mate, frame); k_read_units)
+void launch_read_units(const ReadMeta* meta, uint32_t n, uint32_t C, uint32_t upr, uint32_t* units, hipStream_t s);
 void launch_unit_read(const uint64_t* uOff, uint32_t n, uint32_t* unitRead, hipStream_t s);
 uint64_t extract_slots(uint64_t nUnits, uint32_t C);
 // K1 over nUnits chunks of <= C windows; writes extract_slots(nUnits, C) slots
 void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2,
                     const ReadMeta* meta, const uint64_t* uOff, const uint32_t* unitRead, uint64_t nUnits,
                     uint32_t C, const HostTables& t, int kmerFormat, int syncmer, int smerLen, uint64_t* keys,
-                    uint64_t* unitInfo, hipStream_t s);  // keys per slot, info per unit (slot_info)
+                    uint64_t* unitInfo, hipStream_t s, uint32_t upr = 0);  // keys per slot, info per unit (slot_info)
 
 uint64_t radix_counts_elems(uint64_t n);
 // V = uint64_t or uint32_t; genVals: the values are the input positions (valsA not read).
@@ -218,7 +219,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
                                uint64_t cap, bool threadMajor, hipStream_t s,
                                uint8_t* qdig = nullptr, unsigned long long* binCnt = nullptr, uint64_t binRc = 0,
-                               uint64_t* binHost = nullptr);
+                               uint64_t* binHost = nullptr, uint32_t upr = 0);
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                        uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
                        uint64_t* emitted, hipStream_t s);
@@ -305,7 +306,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
-                  const ProbeExt* lineExt = nullptr);
+                  const ProbeExt* lineExt = nullptr, uint32_t upr = 0, const uint32_t* readLens = nullptr);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
 // slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A query whose ranks pass
 // its read's stretch spills its matches and their ranks to buf / bufRank (total[0] of them; at most
