@@ -404,8 +404,11 @@ def main():
     # MTB_BENCH_ONE_DEVICE=1 put every rank on cuda:0
     if os.environ.get("MTB_BENCH_ONE_DEVICE") == "1":
         local = 0
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)  # before the process group: RCCL's communicator binds this rank's GPU
     if world > 1:
-        dist.init_process_group(os.environ.get("MTB_BENCH_BACKEND", "nccl"), init_method="env://")
+        backend = os.environ.get("MTB_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, init_method="env://", device_id=dev if backend == "nccl" else None)
         if args.db_parts <= 1:
             # the scaling runs time the headline lines (config 3 short and long reads) only: the CPU
             # baseline, the config-2 line, the DB variants, the file -> TSV and --em lines are
@@ -415,8 +418,6 @@ def main():
             args.skip_config2 = True
             args.variants = ""
             args.e2e_pairs = args.e2e_gzip_pairs = args.em_pairs = args.cold_pairs = args.skewed_pairs = 0
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
     if args.c5_only:
         c5 = run_config5(args, world, rank, local, dev)
         if rank == 0:

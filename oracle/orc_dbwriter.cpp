@@ -6,6 +6,7 @@
 // (:1245-1265). Used to make the synthetic fixture DBs of the parity tests.
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <memory>
 #include <parallel/algorithm>
 
@@ -32,6 +33,37 @@ static void getDiffIdx(uint64_t& lastKmer, uint64_t entry, std::vector<uint16_t>
     }
     for (int i = idx + 1; i <= 4; i++) out.push_back(buffer[i]);
     lastKmer = entry;
+}
+
+// writeTargetFilesAndSplits (IndexCreator.cpp:811-865) over the unique (value, taxID) list: diffIdx,
+// info and the AA-aligned split entries (MARKER = ~16777215, IndexCreator.cpp:31-37, AminoAcidPart
+// IndexCreator.h:209-214)
+static void writeTargetSplits(const uint64_t* values, const uint32_t* ids, size_t uniqKmerCnt, int splitNum, Db& db) {
+    size_t sizeOfSplit = uniqKmerCnt / (size_t)(splitNum - 1);
+    std::vector<size_t> offsetList(splitNum + 1);
+    for (int os = 0; os < splitNum; os++) offsetList[os] = os * sizeOfSplit;
+    offsetList[splitNum] = UINT64_MAX;
+    db.split.assign(splitNum, DiffIdxSplit{0, 0, 0});
+    int offsetListIdx = 1, splitListIdx = 1, splitCheck = 0;
+    uint64_t AAofTempSplitOffset = UINT64_MAX, lastKmer = 0;
+    const uint64_t AAMASK = ~(uint64_t)16777215;
+    db.diffIdx.clear();
+    db.info.clear();
+    db.diffIdx.reserve(uniqKmerCnt * 3);
+    db.info.reserve(uniqKmerCnt);
+    for (size_t u = 0; u < uniqKmerCnt; u++) {
+        db.info.push_back(ids[u]);
+        getDiffIdx(lastKmer, values[u], db.diffIdx);
+        if ((lastKmer & AAMASK) != AAofTempSplitOffset && splitCheck == 1) {
+            db.split[splitListIdx++] = {lastKmer, (uint64_t)db.diffIdx.size(), (uint64_t)db.info.size()};
+            splitCheck = 0;
+        }
+        if (db.info.size() == offsetList[offsetListIdx]) {
+            AAofTempSplitOffset = lastKmer & AAMASK;
+            splitCheck = 1;
+            offsetListIdx++;
+        }
+    }
 }
 
 bool buildDb(const mtb_params& par, const Taxonomy& tax, const BuildInput& in, Db& db, std::string* err) {
@@ -71,34 +103,13 @@ bool buildDb(const mtb_params& par, const Taxonomy& tax, const BuildInput& in, D
         i = j;
     }
     // writeTargetFilesAndSplits
-    const int splitNum = in.splitNum;
-    size_t uniqKmerCnt = uniq.size();
-    size_t sizeOfSplit = uniqKmerCnt / (size_t)(splitNum - 1);
-    std::vector<size_t> offsetList(splitNum + 1);
-    for (int os = 0; os < splitNum; os++) offsetList[os] = os * sizeOfSplit;
-    offsetList[splitNum] = UINT64_MAX;
-    db.split.assign(splitNum, DiffIdxSplit{0, 0, 0});
-    int offsetListIdx = 1, splitListIdx = 1, splitCheck = 0;
-    uint64_t AAofTempSplitOffset = UINT64_MAX, lastKmer = 0;
-    const uint64_t AAMASK = ~(uint64_t)16777215;
-    db.diffIdx.clear();
-    db.info.clear();
-    db.diffIdx.reserve(uniqKmerCnt * 3);
-    db.info.reserve(uniqKmerCnt);
-    for (size_t u = 0; u < uniqKmerCnt; u++) {
-        const TargetKmer& k = kmers[uniq[u]];
-        db.info.push_back((uint32_t)k.taxId);
-        getDiffIdx(lastKmer, k.value, db.diffIdx);
-        if ((lastKmer & AAMASK) != AAofTempSplitOffset && splitCheck == 1) {
-            db.split[splitListIdx++] = {lastKmer, (uint64_t)db.diffIdx.size(), (uint64_t)db.info.size()};
-            splitCheck = 0;
-        }
-        if (db.info.size() == offsetList[offsetListIdx]) {
-            AAofTempSplitOffset = lastKmer & AAMASK;
-            splitCheck = 1;
-            offsetListIdx++;
-        }
+    std::vector<uint64_t> uv(uniq.size());
+    std::vector<uint32_t> ui(uniq.size());
+    for (size_t u = 0; u < uniq.size(); u++) {
+        uv[u] = kmers[uniq[u]].value;
+        ui[u] = (uint32_t)kmers[uniq[u]].taxId;
     }
+    writeTargetSplits(uv.data(), ui.data(), uniq.size(), in.splitNum, db);
     // taxID_list: the set of genome taxIDs (IndexCreator.cpp:329-333)
     std::vector<TaxID> ids(in.genomeTaxId, in.genomeTaxId + in.nGenomes);
     std::sort(ids.begin(), ids.end());
@@ -143,3 +154,22 @@ bool writeDbFiles(const Db& db, const mtb_params& par, const std::string& dir, s
 }
 
 }  // namespace orc
+
+// Pin hook (test infrastructure: tests/test_ref_writer.py checks it against tests/golden/ref_writer.npz,
+// which the reference's own writeTargetFilesAndSplits / getDiffIdx produced): the writer alone over a
+// caller's sorted unique (value, taxID) list. diff_out holds at least 5 n words; *n_diff = words written.
+extern "C" int orc_pin_write_db(const uint64_t* values, const uint32_t* ids, uint64_t n, int split_num,
+                                uint16_t* diff_out, uint64_t* n_diff, uint32_t* info_out, uint64_t* split_out) {
+    if (split_num < 2) return MTB_ERR_ARG;
+    orc::Db db;
+    orc::writeTargetSplits(values, ids, n, split_num, db);
+    memcpy(diff_out, db.diffIdx.data(), db.diffIdx.size() * 2);
+    *n_diff = db.diffIdx.size();
+    memcpy(info_out, db.info.data(), db.info.size() * 4);
+    for (int i = 0; i < split_num; i++) {
+        split_out[3 * i] = db.split[i].ADkmer;
+        split_out[3 * i + 1] = db.split[i].diffIdxOffset;
+        split_out[3 * i + 2] = db.split[i].infoIdxOffset;
+    }
+    return MTB_OK;
+}

@@ -50,6 +50,7 @@ def lib():
         L.orc_hamming_tables.restype = None
         L.orc_hamming.argtypes = [vp, vp, u64, vp, vp, vp]
         L.orc_pin_eval.argtypes = [ctypes.c_int, vp, vp, vp, u64, vp, vp]
+        L.orc_pin_write_db.argtypes = [vp, vp, u64, ctypes.c_int, vp, vp, vp, vp]
         L.orc_hamming.restype = None
         L.orc_write_report.argtypes = [vp, ctypes.c_char_p, i32, vp, vp, u64]
         L.orc_write_report.restype = i32
