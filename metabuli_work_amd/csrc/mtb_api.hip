@@ -202,6 +202,7 @@ struct mtb_ctx {
     DevBuf binCnt, binTab;                  // binned K1F: bucket counts (kSortBins u64), K2's tile table
     DevBuf maskOut1, maskOut2, maskProb, maskScale;  // K0M tantan masking: masked mates + scratch
     DevBuf readLens;                        // K0: the mates' lengths, 16 bits each (uniform units' K4)
+    DevBuf readCnt64;                       // uniform units' K4: per-read count | mate lengths << 32
     uint64_t liveM = 0;                     // matches K6 read in the last batch
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
@@ -712,7 +713,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     X(digB) X(binCnt) X(binTab) X(local) X(paths) X(comb) X(conn) X(spScore) X(spKeep) X(gFlag) X(sFlag) \
     X(pathCnt) X(gScan) X(sScan) X(gStart) X(sStart) X(clade) X(tcPool) X(tcLen) X(tcOff) X(tcOut) X(results) \
     X(emMap) X(emCnt) X(emScratch) X(emPacked) X(emCnt32) X(emOff) X(maskOut1) X(maskOut2) X(maskProb) \
-    X(maskScale) X(readLens)
+    X(maskScale) X(readLens) X(readCnt64)
 static std::vector<DevBuf*> batch_bufs(mtb_ctx* c) {
 #define MTB_BUF_PTR(n) &c->n,
     return {MTB_BATCH_BUFS(MTB_BUF_PTR)};
@@ -1232,8 +1233,16 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(c->longCnt.ensure(sizeof(uint32_t)));
     }
     bool spillGrown = false;  // the spill buffer grows once per batch (then the staged join)
+    // uniform units on the sort-merge join: its rank atomics go to 64-bit counters that also hand back
+    // the read's lengths (k_match), copied to readCnt after the join
+    unsigned long long* cnt64 = nullptr;
+    if (c->upr && !probe && !(sweep && direct)) {
+        HIP_TRY(c->readCnt64.ensure(sizeof(unsigned long long) * (n + 1)));
+        cnt64 = c->readCnt64.as<unsigned long long>();
+    }
     for (int attempt = 0; attempt < 5; attempt++) {
         HIP_TRY(hipMemsetAsync(c->readCnt.p, 0, sizeof(uint32_t) * (n + 1), s));
+        if (cnt64) launch_cnt64_init(c->readLens.as<uint32_t>(), n, cnt64, s);
         HIP_TRY(hipMemsetAsync(c->mTotal.p, 0, sizeof(unsigned long long) * kStageRegions, s));
         int overflow = 0;
         uint32_t longN = 0;
@@ -1261,7 +1270,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                          c->lines, c->lineP, c->runOff, sortLo, c->probeStats.as<unsigned long long>(),
                          direct ? c->mDirect.as<SegMatch>() : nullptr, c->slotOff.as<uint64_t>(),
                          c->ovFlag.as<int>(), c->spillShift, direct ? c->longList.as<LongRun>() : nullptr,
-                         c->longCap, c->longCnt.as<uint32_t>(), s, c->lineExt, c->upr, c->readLens.as<uint32_t>());
+                         c->longCap, c->longCnt.as<uint32_t>(), s, c->lineExt, cnt64 ? c->upr : 0u, cnt64);
         HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long) * kStageRegions,
                                hipMemcpyDeviceToHost, s));
         if (direct) HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1280,7 +1289,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                               c->mTotal.as<unsigned long long>(), c->mStage.as<mtb_match>(), c->mRank.as<uint32_t>(),
                               c->spillCap, c->errFlag.as<int>(), c->mDirect.as<SegMatch>(),
                               c->slotOff.as<uint64_t>(), c->ovFlag.as<int>(), c->spillShift,
-                              c->probeStats.as<unsigned long long>(), s);
+                              c->probeStats.as<unsigned long long>(), s, cnt64);
             HIP_TRY(hipMemcpyAsync(regTot.data(), c->mTotal.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipMemcpyAsync(&overflow, c->ovFlag.p, sizeof(int), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
@@ -1321,6 +1330,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
         HIP_TRY(c->mRank.ensure(sizeof(uint32_t) * c->stageRegion * kStageRegions));
         HIP_TRY(hipMemsetAsync(c->probeStats.p, 0, sizeof(unsigned long long) * kProbeStatsLen, s));
     }
+    if (cnt64) launch_cnt64_counts(cnt64, n, c->readCnt.as<uint32_t>(), s);
     HIP_TRY(hipEventRecord(c->kev[7], s));
     exclusive_scan_u32(c->readCnt.as<uint32_t>(), n, c->mOff.as<uint64_t>(), c->scanTmp.p, s);
     if (direct) {  // M = the per-read counts' total (the direct join claims no staging stretches)

@@ -1585,7 +1585,7 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
                                                   mtb_match* __restrict__ buf, uint32_t* __restrict__ bufRank,
                                                   uint64_t region, int* __restrict__ err, SegMatch* __restrict__ direct,
                                                   const uint64_t* __restrict__ dirOff, int* __restrict__ overflow,
-                                                  uint32_t capShift, int lane) {
+                                                  uint32_t capShift, int lane, unsigned long long* __restrict__ cnt64) {
     const HamRows hr = hamming_rows(key);
     uint32_t mn = 255;
     for (uint64_t t = lo + lane; t < hi; t += 64) mn = min(mn, hamming_sum_rows(hr, vals[t]));
@@ -1597,7 +1597,8 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
     const uint64_t info = slot_info(slot, C, unitInfo, kmerFormat);
     const uint32_t r = info_seq(info) - 1;
     uint32_t rk = 0;
-    if (lane == 0) rk = atomicAdd(&readCnt[r], c);
+    // uniform units: the read's 64-bit counter (k_match's, count in the low word)
+    if (lane == 0) rk = cnt64 ? (uint32_t)atomicAdd(&cnt64[r], (unsigned long long)c) : atomicAdd(&readCnt[r], c);
     rk = (uint32_t)__shfl((int)rk, 0, 64);
     // staged join (direct == nullptr): the block's staging stretch is claimed by the caller's count;
     // here only the direct join's long runs come (the staged path keeps them on the lane)
@@ -1666,18 +1667,17 @@ void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree)
 
 // The info of window p of uniform unit u (k_read_units: upr units per read, one per (mate, frame)), as
 // unit_windows + unit_info_at compute it: read u / upr, mate and frame from u % upr, the frame's first
-// window at its begin (KmerExtractor.cpp:374-378) plus the mate-2 offset (:341-345). Only the reverse
-// frames, the load orders from the right and mate 2 need the read's lengths (one 4-B load from a
-// 4-B-per-read array instead of the 16-B unit record of a unit array 12x its size).
-__device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, uint32_t upr,
-                                                      const uint32_t* __restrict__ readLens, int kmerFormat) {
+// window at its begin (KmerExtractor.cpp:374-378) plus the mate-2 offset (:341-345). L: the read's
+// mate lengths (16 bits each), which k_match gets back from its rank atomic (the read's 64-bit counter
+// carries them above the count), so a matched query reads no unit record and no length.
+__device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, uint32_t upr, uint32_t L,
+                                                      int kmerFormat) {
     const uint32_t r = u / upr, local = u - r * upr;
     const uint32_t mate = local >= 6u ? 1u : 0u, frame = local - 6u * mate;
     const bool fwd = frame < 3u;
     const bool fromLeft = (kmerFormat == 2) ? fwd : !fwd;
     uint32_t pos0 = frame, posOffset = 0;
     if (mate || !fromLeft || !fwd) {
-        const uint32_t L = readLens[r];
         const int len1 = (int)(L & 0xFFFFu), len = mate ? (int)(L >> 16) : len1;
         const int used = max_covered_length(len);
         int begin = (int)frame;
@@ -1703,7 +1703,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                                                int* __restrict__ overflow, uint32_t capShift,
                                                LongRun* __restrict__ longList, uint32_t longCap,
                                                uint32_t* __restrict__ longCnt, const ProbeExt* __restrict__ lineExt,
-                                               uint32_t upr, const uint32_t* __restrict__ readLens) {
+                                               uint32_t upr, unsigned long long* __restrict__ cnt64) {
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -1959,23 +1959,28 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                    : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
                             : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
-        if (c[j] && upr) {  // uniform units: the info and the segment bounds from the slot and the read's lengths
+        if (c[j] && upr && !abFree) {
+            // uniform units: the read and the segment bounds from the slot; one 64-bit atomic on the
+            // read's counter reserves the ranks (low word) and returns its mate lengths (high word)
             uint32_t p;
             const uint32_t u = slot_unit(slot[j], C, p);
-            info[j] = uniform_unit_info(u, p, upr, readLens, kmerFormat);
-            const uint64_t r = info_seq(info[j]) - 1;
-            stretch[j] = r * upr | (uint64_t)upr << 40;
+            const uint32_t r = u / upr;
+            const unsigned long long old = atomicAdd(&cnt64[r], (unsigned long long)c[j]);
+            rk[j] = (uint32_t)old;
+            info[j] = uniform_unit_info(u, p, upr, (uint32_t)(old >> 32), kmerFormat);
+            stretch[j] = (uint64_t)r * upr | (uint64_t)upr << 40;
         } else if (c[j]) {  // only matched queries need their info and their read's segment bounds (one 16-B load)
             uint32_t p;
             const ulonglong2 ur = reinterpret_cast<const ulonglong2*>(unitInfo)[slot_unit(slot[j], C, p)];
             info[j] = unit_info_at(ur.x, p, kmerFormat);
             stretch[j] = ur.y;
+            // the returned count is the query's first rank inside its read's segment
+            rk[j] = abFree ? (slot[j] & 7u) : atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         } else {
             info[j] = 0;
             stretch[j] = 0;
+            rk[j] = 0;
         }
-        // the returned count is the query's first rank inside its read's segment
-        rk[j] = !c[j] ? 0 : abFree ? (slot[j] & 7u) : atomicAdd(&readCnt[info_seq(info[j]) - 1], c[j]);
         mine += c[j];
     }
     int hit = 0;
@@ -2094,7 +2099,8 @@ __global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ l
                                                    uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
                                                    SegMatch* __restrict__ direct, const uint64_t* __restrict__ dirOff,
                                                    int* __restrict__ overflow, uint32_t capShift,
-                                                   unsigned long long* __restrict__ stats) {
+                                                   unsigned long long* __restrict__ stats,
+                                                   unsigned long long* __restrict__ cnt64) {
     const LongRun lr = list[blockIdx.x];
     if (lr.lo > lr.hi || lr.hi > D - 1) {  // the producers clamp runs to [0, D - 1]: never read past the DB
         if (threadIdx.x == 0) atomicExch(err, kErrRunOutsideDb);
@@ -2102,7 +2108,7 @@ __global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ l
     }
     const uint32_t got = wave_long_run(qkey[lr.q], qslot[lr.q], lr.lo, lr.hi, DbVal{db}, DbTax{db}, unitInfo, C, spOf,
                                        maxTax, kmerFormat, readCnt, total, buf, bufRank, region, err, direct, dirOff,
-                                       overflow, capShift, (int)threadIdx.x);
+                                       overflow, capShift, (int)threadIdx.x, cnt64);
     if (threadIdx.x == 0 && got) atomicAdd(&stats[blockIdx.x % kStatStripes], 1ull);  // a matched query
 }
 
@@ -2110,9 +2116,27 @@ void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, co
                        const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D, const int32_t* spOf,
                        uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                        uint32_t* bufRank, uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff,
-                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s) {
+                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s,
+                       unsigned long long* cnt64) {
     if (n) k_match_long<<<n, 64, 0, s>>>(list, qkey, qslot, unitInfo, C, db, D, spOf, maxTax, kmerFormat, readCnt, total, buf,
-                                         bufRank, region, err, direct, dirOff, overflow, capShift, stats);
+                                         bufRank, region, err, direct, dirOff, overflow, capShift, stats, cnt64);
+}
+
+// Uniform units' read counters (k_match): count 0 in the low word, the mate lengths above it.
+__global__ void k_cnt64_init(const uint32_t* __restrict__ readLens, uint32_t n, unsigned long long* __restrict__ cnt64) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cnt64[i] = (unsigned long long)readLens[i] << 32;
+}
+// ... and the counts back into the per-read u32 counts every later stage reads.
+__global__ void k_cnt64_counts(const unsigned long long* __restrict__ cnt64, uint32_t n, uint32_t* __restrict__ readCnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) readCnt[i] = (uint32_t)cnt64[i];
+}
+void launch_cnt64_init(const uint32_t* readLens, uint32_t n, unsigned long long* cnt64, hipStream_t s) {
+    if (n) k_cnt64_init<<<(n + 255) / 256, 256, 0, s>>>(readLens, n, cnt64);
+}
+void launch_cnt64_counts(const unsigned long long* cnt64, uint32_t n, uint32_t* readCnt, hipStream_t s) {
+    if (n) k_cnt64_counts<<<(n + 255) / 256, 256, 0, s>>>(cnt64, n, readCnt);
 }
 
 // Each staged match into its read's segment at the rank the join reserved for it (no atomics);
@@ -2746,7 +2770,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
-                  const ProbeExt* lineExt, uint32_t upr, const uint32_t* readLens) {
+                  const ProbeExt* lineExt, uint32_t upr, unsigned long long* cnt64) {
     if (Q == 0 || D < 2) return;
     winCap = std::min<uint32_t>(winCap, kMatchWin);
     // a block's window holds ~256 * D / Q values: far past the LDS cap, every block would take the
@@ -2757,14 +2781,14 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                                                         kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                         win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
                                                         overflow, capShift, longList, longCap, longCnt,
-                                                        runOff ? lineExt : nullptr, upr, readLens);
+                                                        runOff ? lineExt : nullptr, upr, cnt64);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
                                                             maxTax, kmerFormat, readCnt, total, buf, bufRank, region,
                                                             err, winCap, win, lines, nullptr, nullptr, kQuerySortLo,
                                                             stats, direct, dirOff, overflow, capShift, nullptr, 0,
-                                                            longCnt, nullptr, upr, readLens);
+                                                            longCnt, nullptr, upr, cnt64);
     }
 }
 

@@ -280,7 +280,7 @@ void launch_match_long(const LongRun* list, uint32_t n, const uint64_t* qkey, co
                        const uint64_t* unitInfo, uint32_t C, const DbRec* db, uint64_t D, const int32_t* spOf,
                        uint32_t maxTax, int kmerFormat, uint32_t* readCnt, unsigned long long* total, mtb_match* buf,
                        uint32_t* bufRank, uint64_t region, int* err, SegMatch* direct, const uint64_t* dirOff,
-                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s);
+                       int* overflow, uint32_t capShift, unsigned long long* stats, hipStream_t s, unsigned long long* cnt64 = nullptr);
 // K4S DB-sweep join (MTB_JOIN=sweep; direct output only): tiles of ~nom DB records ending at
 // sort-prefix bucket bounds, built once per context (pstartTmp: kSweepStartsTmp u64 scratch; tileRec
 // sweep_tiles + 1 u64, tilePre sweep_tiles + 1 u32); per batch the sorted queries' bucket starts
@@ -306,7 +306,11 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                   const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, int sortLo,
                   unsigned long long* stats, SegMatch* direct, const uint64_t* dirOff, int* overflow,
                   uint32_t capShift, LongRun* longList, uint32_t longCap, uint32_t* longCnt, hipStream_t s,
-                  const ProbeExt* lineExt = nullptr, uint32_t upr = 0, const uint32_t* readLens = nullptr);
+                  const ProbeExt* lineExt = nullptr, uint32_t upr = 0, unsigned long long* cnt64 = nullptr);
+// uniform units (upr): k_match and k_match_long reserve ranks on 64-bit per-read counters whose high
+// word holds the mate lengths (launch_cnt64_init from the K0 lengths, launch_cnt64_counts back to readCnt)
+void launch_cnt64_init(const uint32_t* readLens, uint32_t n, unsigned long long* cnt64, hipStream_t s);
+void launch_cnt64_counts(const unsigned long long* cnt64, uint32_t n, uint32_t* readCnt, hipStream_t s);
 // direct (nullable): no staging; each read's matches go straight to direct + dirOff[r] * C (its K1
 // slot stretch, dirOff = the per-read unit offsets) at its reserved ranks. A query whose ranks pass
 // its read's stretch spills its matches and their ranks to buf / bufRank (total[0] of them; at most

@@ -151,7 +151,7 @@ def test_device_resident_batch_split_on_retry(make_db, frac):
         assert np.array_equal(capped.taxcnt(), ref.taxcnt)
         st = capped.stats()
         assert st["query_kmers"] == ref_stats["query_kmers"] and st["matches"] == ref_stats["matches"] == ref.matches
-        assert st["slots"] == ref_stats["slots"] and st["max_read_matches"] == ref_stats["max_read_matches"]
+        assert st["max_read_matches"] == ref_stats["max_read_matches"]  # (slots: each piece pads its own units)
         assert capped.stage_ms()[4] > 0 and capped.kernel_ms().sum() > 0
         # a later batch that fits serves the context's own buffers again
         small = capped.classify_batch(r.seq1, r.off1[:101], r.seq2, r.off2[:101])
