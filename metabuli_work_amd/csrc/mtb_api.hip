@@ -2119,7 +2119,8 @@ int mtb_get_query_kmers(mtb_ctx* c, mtb_kmer* out, uint64_t cap, uint64_t* n_out
     if (c->probed) { set_error("the probe join keeps no sorted query k-mers (MTB_JOIN=probe)"); return MTB_ERR_ARG; }
     if (!c->qSlots) { set_error("no query k-mers kept"); return MTB_ERR_ARG; }
     if (cap < c->Q) return MTB_RETRY;
-    std::vector<uint64_t> k(c->Q), ui(c->unitInfo.bytes / 8);
+    // the unit records' buffer is sized need + need / 8 + 256 bytes (DevBuf::ensure): not a multiple of 8
+    std::vector<uint64_t> k(c->Q), ui((c->unitInfo.bytes + 7) / 8);
     std::vector<uint32_t> v(c->Q);
     const void* kp = c->qKeys;
     const void* vp = c->qSlots;

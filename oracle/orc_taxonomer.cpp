@@ -127,6 +127,16 @@ public:
     void chooseBestTaxon(uint32_t currentQuery, size_t offset, size_t end, const mtb_match* matchList,
                          std::vector<Query>& queryList);
 
+    // pin hook (orc_pin_combine): combineMatchPaths over the caller's paths alone
+    float combineForPin(std::vector<MatchPath>& paths, std::vector<MatchPath>& out, int readLength) {
+        matchPaths.swap(paths);
+        combinedMatchPaths.clear();
+        const float s = combineMatchPaths(0, 0, readLength);
+        out = combinedMatchPaths;
+        matchPaths.swap(paths);
+        return s;
+    }
+
 private:
     const Db& db;
     const mtb_params& par;
@@ -578,6 +588,45 @@ extern "C" int orc_pin_eval(int fn, const int64_t* param, const uint64_t* a, con
             }
             default: return MTB_ERR_ARG;
         }
+    }
+    return MTB_OK;
+}
+
+// Pin hook (tests/test_ref_paths.py against tests/golden/ref_paths.npz, which the reference's own
+// combineMatchPaths / trimMatchPath / isMatchPathOverlapped / MatchPath produced): one species run's
+// paths — start, end, score, hammingDist, and the rightEndHamming of their start and end matches —
+// combined. Returns the score (score / readLength); comb_out gets (start, end, hammingDist, score bits)
+// per kept path.
+extern "C" int orc_pin_combine(const int32_t* start, const int32_t* end, const float* score, const int32_t* hd,
+                               const uint16_t* reh_start, const uint16_t* reh_end, uint64_t n, int read_length,
+                               float* score_out, int32_t* comb_out, uint64_t* n_comb) {
+    using namespace orc;
+    static const Db db;
+    static const mtb_params par{};
+    Taxonomer t(db, par);
+    std::vector<mtb_match> ms(2 * n);
+    std::vector<MatchPath> paths(n), out;
+    for (uint64_t i = 0; i < n; i++) {
+        ms[2 * i] = mtb_match{};
+        ms[2 * i + 1] = mtb_match{};
+        ms[2 * i].right_end_hamming = reh_start[i];
+        ms[2 * i + 1].right_end_hamming = reh_end[i];
+        MatchPath& p = paths[i];
+        p.start = start[i];
+        p.end = end[i];
+        p.score = score[i];
+        p.hammingDist = hd[i];
+        p.depth = 1;
+        p.startMatch = &ms[2 * i];
+        p.endMatch = &ms[2 * i + 1];
+    }
+    *score_out = t.combineForPin(paths, out, read_length);
+    *n_comb = out.size();
+    for (size_t i = 0; i < out.size(); i++) {
+        comb_out[4 * i] = out[i].start;
+        comb_out[4 * i + 1] = out[i].end;
+        comb_out[4 * i + 2] = out[i].hammingDist;
+        memcpy(&comb_out[4 * i + 3], &out[i].score, 4);
     }
     return MTB_OK;
 }
