@@ -581,7 +581,6 @@ void launch_extract(const uint8_t* seq1, const uint64_t* off1, const uint8_t* se
 // ------------------------------------------------------------------------------------------------
 constexpr int kRadixItems = 32;
 constexpr int kRadixTile = kBlock * kRadixItems;  // 8192 keys
-constexpr int kRadixSlice = 64 * kRadixItems;      // keys per wave
 
 // one 32-bit bit-field extract from the word holding the digit (shift is wave-uniform), not a 64-bit shift
 __device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) {
@@ -590,26 +589,28 @@ __device__ __forceinline__ uint32_t radix_digit(uint64_t k, int shift) {
     return (uint32_t)((k >> shift) & 0xFF);
 }
 
+template <int TILE>
 __device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab, uint32_t tile, uint64_t n,
                                                 uint64_t& base, uint64_t& end);
 
-template <bool FILTER>
+template <bool FILTER, int TILE = kRadixTile>
 __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__ keys, uint64_t n, int shift,
                                                     uint32_t* __restrict__ counts, uint32_t nTiles,
                                                     const uint64_t* __restrict__ tab = nullptr) {
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
+    constexpr int kItems = TILE / kBlock;
     uint64_t base;
-    radix_tile_span(tab, blockIdx.x, n, base, n);
-    uint64_t key[kRadixItems];
+    radix_tile_span<TILE>(tab, blockIdx.x, n, base, n);
+    uint64_t key[kItems];
 #pragma unroll
-    for (int k = 0; k < kRadixItems; k++) {
+    for (int k = 0; k < kItems; k++) {
         const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
         key[k] = i < n ? keys[i] : kSentinel;
     }
 #pragma unroll
-    for (int k = 0; k < kRadixItems; k++) {
+    for (int k = 0; k < kItems; k++) {
         const uint64_t i = base + (uint64_t)k * kBlock + threadIdx.x;
         if (i < n && (!FILTER || key[k] != kSentinel)) atomicAdd(&hist[radix_digit(key[k], shift)], 1u);
     }
@@ -621,6 +622,7 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint64_t* __restrict__
 // or by the fused K1F for the first): 1 B read per key instead of 8.
 // tab (nullable): tile t is [tab[t] >> 14, + (tab[t] & 0x3FFF)) instead of [t * kRadixTile, ...) up to n
 // (the buckets of a binned K1F; starts are multiples of 16).
+template <int TILE>
 __device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab, uint32_t tile, uint64_t n,
                                                 uint64_t& base, uint64_t& end) {
     if (tab) {
@@ -628,11 +630,12 @@ __device__ __forceinline__ void radix_tile_span(const uint64_t* __restrict__ tab
         base = e >> 14;
         end = base + (e & 0x3FFFu);
     } else {
-        base = (uint64_t)tile * kRadixTile;
+        base = (uint64_t)tile * TILE;
         end = n;
     }
 }
 
+template <int TILE = kRadixTile>
 __global__ void __launch_bounds__(256) k_radix_hist_dig(const uint8_t* __restrict__ dig, uint64_t n,
                                                         uint32_t* __restrict__ counts, uint32_t nTiles,
                                                         const uint64_t* __restrict__ tab) {
@@ -640,11 +643,11 @@ __global__ void __launch_bounds__(256) k_radix_hist_dig(const uint8_t* __restric
     hist[threadIdx.x] = 0;
     __syncthreads();
     uint64_t base, end;
-    radix_tile_span(tab, blockIdx.x, n, base, end);
+    radix_tile_span<TILE>(tab, blockIdx.x, n, base, end);
     n = end;
-    constexpr int kVec = kRadixTile / kBlock / 16;  // uint4 loads per thread
+    constexpr int kVec = TILE / kBlock / 16;  // uint4 loads per thread
     uint4 d[kVec];
-    const bool full = base + kRadixTile <= n;
+    const bool full = base + TILE <= n;
 #pragma unroll
     for (int k = 0; k < kVec; k++) {
         const uint64_t i = base + ((uint64_t)k * kBlock + threadIdx.x) * 16;
@@ -671,15 +674,16 @@ __global__ void __launch_bounds__(256) k_radix_hist_dig(const uint8_t* __restric
 // V: value type (64-bit payloads, or 32-bit slot indices). GEN: the values are the input positions
 // (the first pass of a sort of slots), so none are read. digOut (nullable): the next pass's digit
 // (bits [nextShift, nextShift + 8) of the key) of every written key, at its output position.
-template <typename V, bool FILTER, bool GEN>
+template <typename V, bool FILTER, bool GEN, int TILE = kRadixTile>
 __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restrict__ keysIn, const V* __restrict__ valsIn,
                                                        uint64_t n, int shift, const uint64_t* __restrict__ offs,
                                                        uint32_t nTiles, uint64_t* __restrict__ keysOut,
                                                        V* __restrict__ valsOut, uint8_t* __restrict__ digOut,
                                                        int nextShift, int xcdMap, const uint64_t* __restrict__ tab,
                                                        int atomicRank) {
-    __shared__ uint64_t sKV[kRadixTile];  // keys, then (after they are written out) values
-    __shared__ uint8_t sDig[kRadixTile];
+    constexpr int kItems = TILE / kBlock, kSlice = 64 * kItems;
+    __shared__ uint64_t sKV[TILE];  // keys, then (after they are written out) values
+    __shared__ uint8_t sDig[TILE];
     __shared__ uint32_t waveHist[kWaves][256];
     __shared__ uint64_t sDst[256];  // global slot of this tile's first key of digit d, minus its tile offset
     __shared__ uint32_t sKept;
@@ -695,9 +699,9 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         tile = x * q + min(x, r) + i;
     }
     uint64_t tBase, tEnd;
-    radix_tile_span(tab, tile, n, tBase, tEnd);
+    radix_tile_span<TILE>(tab, tile, n, tBase, tEnd);
     n = tEnd;
-    const uint64_t base = tBase + (uint64_t)w * kRadixSlice;
+    const uint64_t base = tBase + (uint64_t)w * kSlice;
     // the digit bases: one strided load per lane, issued first so its latency hides behind the
     // key loads (a dependent load per key in the write-out loop was the old bottleneck)
     const uint64_t digitBase = offs[(uint64_t)tid * nTiles + tile];
@@ -707,20 +711,20 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __syncthreads();
 
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t k[kRadixItems];
-    V v[kRadixItems];
-    uint32_t rk[kRadixItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
+    uint64_t k[kItems];
+    V v[kItems];
+    uint32_t rk[kItems];  // digit << 16 | rank within this wave's slice; ~0 = not kept
     // all loads first (unguarded for the full tiles) so the 32 loads of a lane are in flight
     // together; interleaving them with the ranking serialised 16 memory round trips per tile
-    if (tBase + kRadixTile <= n) {
+    if (tBase + TILE <= n) {
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
+        for (int r = 0; r < kItems; r++) k[r] = keysIn[base + (uint64_t)r * 64 + lane];
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++)
+        for (int r = 0; r < kItems; r++)
             v[r] = GEN ? (V)(base + (uint64_t)r * 64 + lane) : valsIn[base + (uint64_t)r * 64 + lane];
     } else {
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) {
+        for (int r = 0; r < kItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
             k[r] = i < n ? keysIn[i] : kSentinel;
             v[r] = GEN ? (V)i : (i < n ? valsIn[i] : (V)0);
@@ -736,7 +740,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     // nine ballots (sort 14.8 -> 14.2-14.3 ms same box, profiles/r05/ab_radix_orrank.json)
     if (atomicRank & 1) {
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) {
+        for (int r = 0; r < kItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
             const bool valid = i < n && (!FILTER || k[r] != kSentinel);
             const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
@@ -750,9 +754,9 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         unsigned long long* sMask = reinterpret_cast<unsigned long long*>(sKV) + w * 256;
         // a full tile without sentinels (every tile of a sort but its last): no per-key validity
         // (MTB_RADIX_FULLTILE=0 for the A/B)
-        if (!FILTER && !(atomicRank & 2) && tBase + kRadixTile <= n) {
+        if (!FILTER && !(atomicRank & 2) && tBase + TILE <= n) {
 #pragma unroll
-            for (int r = 0; r < kRadixItems; r++) {
+            for (int r = 0; r < kItems; r++) {
                 const uint32_t d = radix_digit(k[r], shift);
                 __hip_atomic_fetch_or(&sMask[d], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned long long peers = __hip_atomic_load(&sMask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -766,7 +770,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
             }
         } else
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) {
+        for (int r = 0; r < kItems; r++) {
             const uint64_t i = base + (uint64_t)r * 64 + lane;
             const bool valid = i < n && (!FILTER || k[r] != kSentinel);
             const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
@@ -781,11 +785,11 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
             }
             rk[r] = valid ? (d << 16 | (before + rankInWave)) : ~0u;
         }
-    } else if (!FILTER && !(atomicRank & 2) && tBase + kRadixTile <= n) {
+    } else if (!FILTER && !(atomicRank & 2) && tBase + TILE <= n) {
         // a full tile without sentinels (every tile of a sort but its last): every key is valid, so
         // the ranking drops the per-key bound checks and the validity terms of its nine ballots
 #pragma unroll
-        for (int r = 0; r < kRadixItems; r++) {
+        for (int r = 0; r < kItems; r++) {
             const uint32_t d = radix_digit(k[r], shift);
             unsigned long long peers = ~0ull;
 #pragma unroll
@@ -800,7 +804,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
         }
     } else
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
+    for (int r = 0; r < kItems; r++) {
         const uint64_t i = base + (uint64_t)r * 64 + lane;
         const bool valid = i < n && (!FILTER || k[r] != kSentinel);
         const uint32_t d = valid ? radix_digit(k[r], shift) : 0u;
@@ -834,7 +838,7 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     // keys and values go through one LDS tile in two rounds (half the LDS of staging both, so
     // twice the resident blocks per CU to hide the ranking's dependency chains)
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
+    for (int r = 0; r < kItems; r++) {
         if (rk[r] == ~0u) continue;
         const uint32_t d = rk[r] >> 16;
         rk[r] = waveHist[w][d] + (rk[r] & 0xFFFFu);  // now the tile position
@@ -854,13 +858,21 @@ __global__ void __launch_bounds__(256) k_radix_scatter(const uint64_t* __restric
     __syncthreads();
     V* sV = reinterpret_cast<V*>(sKV);
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++)
+    for (int r = 0; r < kItems; r++)
         if (rk[r] != ~0u) sV[rk[r]] = v[r];
     __syncthreads();
     for (uint32_t i = tid; i < sKept; i += kBlock) valsOut[sDst[sDig[i]] + i] = sV[i];
 }
 
-uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + kRadixTile - 1) / kRadixTile) + 1; }
+// sized for the smallest tile radix_sort_pairs may take (MTB_RADIX_TILE=4096)
+uint64_t radix_counts_elems(uint64_t n) { return 256ull * ((n + 4095) / 4096) + 1; }
+
+// MTB_RADIX_TILE=4096 (A/B, read per sort): 4096-key tiles, 16 keys per lane (42 KB of LDS per block
+// instead of 78: three resident blocks per CU instead of two), twice the tiles and histogram counts
+static uint32_t radix_tile() {
+    const char* e = getenv("MTB_RADIX_TILE");
+    return e && atoi(e) == 4096 ? 4096u : (uint32_t)kRadixTile;
+}
 
 
 // Sorts n pairs by key bits [bitLo, bitHi). Returns the kept count (sentinels dropped when
@@ -884,11 +896,16 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
     const bool digits = digA && digB && !filter;
     bool first = true;
     *inB = false;
+    const uint32_t T = radix_tile();
     for (int shift = bitLo; shift < bitHi; shift += 8) {
-        uint32_t nTiles = (uint32_t)((cur + kRadixTile - 1) / kRadixTile);
+        uint32_t nTiles = (uint32_t)((cur + T - 1) / T);
         if (nTiles == 0) break;
         const bool f = first && filter, g = first && genVals;
-        if (digits) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles, nullptr);
+        if (T == 4096) {
+            if (digits) k_radix_hist_dig<4096><<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles, nullptr);
+            else if (f) k_radix_hist<true, 4096><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+            else k_radix_hist<false, 4096><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
+        } else if (digits) k_radix_hist_dig<<<nTiles, kBlock, 0, s>>>(di, cur, counts, nTiles, nullptr);
         else if (f) k_radix_hist<true><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         else k_radix_hist<false><<<nTiles, kBlock, 0, s>>>(ki, cur, shift, counts, nTiles);
         exclusive_scan_u32(counts, 256ull * nTiles, offs, scanTmp, s);
@@ -900,7 +917,12 @@ uint64_t radix_sort_pairs(uint64_t* keysA, V* valsA, uint64_t* keysB, V* valsB, 
         // MTB_RADIX_FULLTILE=0 (A/B, read per sort): full tiles ranked by the general path too
         const char* fe = getenv("MTB_RADIX_FULLTILE");
         const int ar = (first && unstableFirst ? 1 : 0) | (fe && atoi(fe) == 0 ? 2 : 0) | radix_or_rank();
-        if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+        if (T == 4096) {
+            if (f && g) k_radix_scatter<V, true, true, 4096><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+            else if (f) k_radix_scatter<V, true, false, 4096><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+            else if (g) k_radix_scatter<V, false, true, 4096><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+            else k_radix_scatter<V, false, false, 4096><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
+        } else if (f && g) k_radix_scatter<V, true, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (f) k_radix_scatter<V, true, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else if (g) k_radix_scatter<V, false, true><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
         else k_radix_scatter<V, false, false><<<nTiles, kBlock, 0, s>>>(ki, vi, cur, shift, offs, nTiles, ko, vo, dOut, ns, xcd, nullptr, ar);
