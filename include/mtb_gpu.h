@@ -280,6 +280,12 @@ int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint6
 int mtb_pin_eval(int device, int fn, const int64_t* param, const uint64_t* a, const uint64_t* b, uint64_t n,
                  int64_t* out, uint64_t* n_out);
 
+/* K2 alone (round 6; SURVEY §8(b)'s staged mtb_sort): n (key, value) pairs sorted on key bits
+ * [bit_lo, bit_hi) by the query sort's LSD radix passes, stable (equal keys keep their input order).
+ * Host arrays; the tests check the stability directly (tests/test_radix.py). */
+int mtb_sort_pairs(int device, const uint64_t* keys, const uint32_t* vals, uint64_t n, int bit_lo, int bit_hi,
+                   uint64_t* keys_out, uint32_t* vals_out);
+
 /* Diagnostics (round 5): the opened DB's run-length lines (the unstaged join's runs without a
  * run-index read) checked against its run index for every present AA rank within their reach:
  * out[0] ranks checked, out[1] those the codes resolve, out[2] mismatches (MTB_ERR_INTERNAL when

@@ -2319,3 +2319,32 @@ extern "C" int mtb_pin_eval(int device, int fn, const int64_t* param, const uint
     *n_out = n;
     return MTB_OK;
 }
+
+// K2 alone (staged entry): the (key, 32-bit value) pairs sorted on key bits [bit_lo, bit_hi) by the
+// LSD radix sort the query sort runs (radix_sort_pairs: every pass stable, with the knobs it reads —
+// MTB_RADIX_ORRANK, MTB_RADIX_TILE, MTB_RADIX_FULLTILE, MTB_RADIX_XCD), 8-bit digits. Host arrays.
+extern "C" int mtb_sort_pairs(int device, const uint64_t* keys, const uint32_t* vals, uint64_t n, int bit_lo,
+                              int bit_hi, uint64_t* keys_out, uint32_t* vals_out) {
+    if (n && (!keys || !vals || !keys_out || !vals_out)) { set_error("null argument"); return MTB_ERR_ARG; }
+    if (bit_lo < 0 || bit_hi > 64 || bit_lo >= bit_hi || n >= (1ull << 32)) { set_error("bad sort range"); return MTB_ERR_ARG; }
+    if (!n) return MTB_OK;
+    HIP_TRY(hipSetDevice(device));
+    DevBuf ka, va, kb, vb, cnt, offs, tmp;
+    const uint64_t rc = radix_counts_elems(n);
+    HIP_TRY(ka.ensure(8 * n));
+    HIP_TRY(va.ensure(4 * n));
+    HIP_TRY(kb.ensure(8 * n));
+    HIP_TRY(vb.ensure(4 * n));
+    HIP_TRY(cnt.ensure(4 * rc));
+    HIP_TRY(offs.ensure(8 * (rc + 1)));
+    HIP_TRY(tmp.ensure(8 * scan_tmp_elems(rc)));
+    HIP_TRY(hipMemcpy(ka.p, keys, 8 * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(va.p, vals, 4 * n, hipMemcpyHostToDevice));
+    bool inB = false;
+    radix_sort_pairs(ka.as<uint64_t>(), va.as<uint32_t>(), kb.as<uint64_t>(), vb.as<uint32_t>(), n, bit_lo, bit_hi,
+                     false, false, cnt.as<uint32_t>(), offs.as<uint64_t>(), tmp.p, &inB, nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(keys_out, inB ? kb.p : ka.p, 8 * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(vals_out, inB ? vb.p : va.p, 4 * n, hipMemcpyDeviceToHost));
+    return MTB_OK;
+}
