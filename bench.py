@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-stage HBM bytes of one batch from this round's rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/measure_r04.sh + tools/stage_profile.py), one file per workload
 # this round's PMC passes first; a workload not re-measured this round falls back to the previous one
-TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", "r05"), os.path.join(ROOT, "profiles", "r04")]
+TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", d) for d in ("r06", "r05", "r04")]
 # the six timed kernels of mtb_last_kernel_ms, by join path (mtb_last_stats[10])
 KERNELS_SORT = ["extract", "filter", "kmer_sort", "match_join", "match_transpose", "match_sort", "assign"]
 KERNELS_PROBE = ["extract", "filter", "kmer_sort", "probe_join", "match_transpose", "match_sort", "assign"]
