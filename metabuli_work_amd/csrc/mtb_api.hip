@@ -425,7 +425,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
         c->rankHi = par->db_part == par->db_parts - 1 ? ~0ull : ((uint64_t)ends[1].hi << 32 | ends[1].lo) >> 24;
     }
     c->openS[1] = since(tp) - (c->openS[0] - readS);  // the decode's uploads are in openS[0]
-    if (const char* e = getenv("MTB_AB_RANK_FREE")) set_ab_rank_free(atoi(e));  // A/B only: invalid results
+    set_ab_rank_free(getenv("MTB_AB_RANK_FREE") ? atoi(getenv("MTB_AB_RANK_FREE")) : 0);  // A/B only: invalid results
     set_pair_read(getenv("MTB_PAIR_READ") ? atoi(getenv("MTB_PAIR_READ")) : 0);
     set_match_xcd(getenv("MTB_MATCH_XCD") ? atoi(getenv("MTB_MATCH_XCD")) : 0);  // (device-wide: set at each open)
     // run sharing measured no gain (the repeated lookups already hit the L2: profiles/r05/ab_share*.json): off

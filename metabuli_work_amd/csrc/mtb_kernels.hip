@@ -1674,6 +1674,7 @@ __device__ __forceinline__ uint32_t wave_long_run(uint64_t key, uint32_t slot, u
 // A/B only (MTB_AB_RANK_FREE): k_match takes a query's rank in its read's segment
 // without the readCnt atomic (a wrong rank: the results are invalid), bounding what any scheme
 // that removes the atomic could save in the join; 2: nor the read's stretch bounds (dirOff).
+// Uniform units (round 6): 3 = no rank atomic (fixed lengths), 4 = nor the match writes.
 __device__ int g_abRankFree = 0;
 __device__ int g_matchXcd = 0;
 __device__ int g_shareRuns = 0;
@@ -1981,7 +1982,14 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
                    : staged ? run_select(hr[j], sDb, vOff, lo[j], hi[j], D, thr[j])
                             : run_select(hr[j], dbv, vOff, lo[j], hi[j], D, thr[j]);
         }
-        if (c[j] && upr && !abFree) {
+        if (c[j] && upr && abFree >= 3) {  // A/B: the uniform path without its atomic (invalid results)
+            uint32_t p;
+            const uint32_t u = slot_unit(slot[j], C, p);
+            const uint32_t r = u / upr;
+            rk[j] = slot[j] & 7u;
+            info[j] = uniform_unit_info(u, p, upr, 150u | 150u << 16, kmerFormat);
+            stretch[j] = (uint64_t)r * upr | (uint64_t)upr << 40;
+        } else if (c[j] && upr && !abFree) {
             // uniform units: the read and the segment bounds from the slot; one 64-bit atomic on the
             // read's counter reserves the ranks (low word) and returns its mate lengths (high word)
             uint32_t p;
@@ -2034,7 +2042,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         // bound sets the overflow flag and the caller reruns the batch with a larger one
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
-            if (!c[j]) continue;
+            if (!c[j] || abFree == 4) continue;
             const uint64_t o = abFree == 2 ? 0 : (stretch[j] & kStretchLoMask) * C;
             const uint64_t cap = abFree == 2 ? (1u << 20) : ((stretch[j] >> 40) * C) >> capShift;
             if (rk[j] + c[j] > cap) {
