@@ -1682,7 +1682,11 @@ __device__ int g_pairRead = 0;
 
 void set_pair_read(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pairRead), &on, sizeof(int)); }
 
-void set_share_runs(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_shareRuns), &on, sizeof(int)); }
+static int h_shareRuns = 0;  // host copy: the lean join (no sharing table) when off
+void set_share_runs(int on) {
+    h_shareRuns = on;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_shareRuns), &on, sizeof(int));
+}
 
 void set_match_xcd(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on, sizeof(int)); }
 
@@ -1711,8 +1715,10 @@ __device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, ui
     return unit_info_at(pack_info(r + 1, pos0 + posOffset, frame), p, kmerFormat);
 }
 
-template <bool kStage, int kPer>
-__global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
+// kLean: the unstaged join without the A/B options' LDS (run-length lines, run sharing): 18 KB of LDS
+// per block instead of 31, so LDS no longer caps the resident waves below what the VGPRs allow
+template <bool kStage, int kPer, bool kLean = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const DbRec* __restrict__ db, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
@@ -1732,11 +1738,11 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
     __shared__ uint32_t sInfo[kStage ? kMatchWin : 1];
     // the block's probe lines (sorted queries) and, behind them, their run-length lines
-    __shared__ uint4 sLineMem[kStage ? 1 : (kMatchLines + kExtLines) * 4];
+    __shared__ uint4 sLineMem[kStage ? 1 : (kMatchLines + (kLean ? 0 : kExtLines)) * 4];
     ProbeLine* const sLines = reinterpret_cast<ProbeLine*>(sLineMem);
     const uint32_t* const sExt = reinterpret_cast<const uint32_t*>(sLineMem + (kStage ? 0 : kMatchLines * 4));
     __shared__ uint64_t sLineP[kStage ? 1 : kMatchLines];   // and their run-index bases
-    __shared__ unsigned long long sTbl[kStage ? 1 : 512];     // run sharing: (AA rank + 1) << 8 | leader
+    __shared__ unsigned long long sTbl[kStage || kLean ? 1 : 512];  // run sharing: (AA rank + 1) << 8 | leader
     __shared__ unsigned long long sBase;
     static_assert(!kStage || kPer * 256 == kMatchQ, "staged blocks are the window blocks");
     const DbVal dbv{db};
@@ -1774,7 +1780,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
     // Measured (round 5, same box): no gain — uniform 55.7 -> 57.3 ms, skewed 54.4 -> 55.7 ms per batch:
     // the repeated lookups hit the L2 already, and the barriers hold each block on its slowest leader.
     // Off by default (MTB_SHARE_RUNS=1: on).
-    constexpr bool kShare = !kStage && kPer == 1;
+    constexpr bool kShare = !kStage && kPer == 1 && !kLean;
     const bool share = kShare && g_shareRuns && lines != nullptr;
     bool follower = false;
     uint32_t leadT = threadIdx.x;
@@ -1833,7 +1839,7 @@ __global__ void __launch_bounds__(256) k_match(const uint64_t* __restrict__ qkey
         const uint64_t L0 = ((qkey[q0] >> sortLo) << sh) / kLineRanks;
         const uint64_t L1 = ((((qkey[q1 - 1] >> sortLo) + 1) << sh) - 1) / kLineRanks;
         const bool inLds = !kStage && L1 - L0 < (uint64_t)kMatchLines;
-        const bool extLds = lineExt && inLds && L1 - L0 < (uint64_t)kExtLines;
+        const bool extLds = !kLean && lineExt && inLds && L1 - L0 < (uint64_t)kExtLines;
         if (!kStage && inLds) {
             const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;  // 4 x 16 B per line
             const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
@@ -2807,11 +2813,20 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
     // HBM path anyway
     if (unstaged_join(lines != nullptr, D, Q, winCap)) {
         const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
-        k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
-                                                        kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
-                                                        win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
-                                                        overflow, capShift, longList, longCap, longCnt,
-                                                        runOff ? lineExt : nullptr, upr, cnt64);
+        // MTB_MATCH_LEAN=0 (A/B): the full-LDS form even without run-length lines or sharing
+        static const bool leanOk = !getenv("MTB_MATCH_LEAN") || atoi(getenv("MTB_MATCH_LEAN")) != 0;
+        if (leanOk && !(runOff && lineExt) && !h_shareRuns)
+            k_match<false, kFreePer, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
+                                                                  kmerFormat, readCnt, total, buf, bufRank, region, err,
+                                                                  winCap, win, lines, lineP, runOff, sortLo, stats,
+                                                                  direct, dirOff, overflow, capShift, longList, longCap,
+                                                                  longCnt, nullptr, upr, cnt64);
+        else
+            k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
+                                                            kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
+                                                            win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
+                                                            overflow, capShift, longList, longCap, longCnt,
+                                                            runOff ? lineExt : nullptr, upr, cnt64);
     } else {
         const unsigned blocks = (unsigned)((Q + kMatchQ - 1) / kMatchQ);
         k_match<true, kMatchQ / 256><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf,
