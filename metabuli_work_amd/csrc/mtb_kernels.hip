@@ -2813,8 +2813,9 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
     // HBM path anyway
     if (unstaged_join(lines != nullptr, D, Q, winCap)) {
         const unsigned blocks = (unsigned)((Q + 256 * kFreePer - 1) / (256 * kFreePer));
-        // MTB_MATCH_LEAN=0 (A/B): the full-LDS form even without run-length lines or sharing
-        static const bool leanOk = !getenv("MTB_MATCH_LEAN") || atoi(getenv("MTB_MATCH_LEAN")) != 0;
+        // MTB_MATCH_LEAN=0 (A/B, read per batch): the full-LDS form even without run-length lines or sharing
+        const char* le = getenv("MTB_MATCH_LEAN");
+        const bool leanOk = !le || atoi(le) != 0;
         if (leanOk && !(runOff && lineExt) && !h_shareRuns)
             k_match<false, kFreePer, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                                   kmerFormat, readCnt, total, buf, bufRank, region, err,
