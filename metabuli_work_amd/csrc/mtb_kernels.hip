@@ -1717,8 +1717,8 @@ __device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, ui
 
 // kLean: the unstaged join without the A/B options' LDS (run-length lines, run sharing): 18 KB of LDS
 // per block instead of 31, so LDS no longer caps the resident waves below what the VGPRs allow
-template <bool kStage, int kPer, bool kLean = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
+template <bool kStage, int kPer, int kLeanWaves = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanWaves ? kLeanWaves : 1))) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const DbRec* __restrict__ db, uint64_t D, AADir d,
                                                const int32_t* __restrict__ spOf, uint32_t maxTax, int kmerFormat,
@@ -1733,6 +1733,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLean 
                                                LongRun* __restrict__ longList, uint32_t longCap,
                                                uint32_t* __restrict__ longCnt, const ProbeExt* __restrict__ lineExt,
                                                uint32_t upr, unsigned long long* __restrict__ cnt64) {
+    constexpr bool kLean = kLeanWaves != 0;
     // without staging (a DB much larger than the query stream: windows over the LDS cap) the
     // kernel holds no LDS window, so twice as many blocks fit on a CU to overlap the random reads
     __shared__ uint64_t sDb[kStage ? kMatchWin : 1];
@@ -2816,13 +2817,21 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         // MTB_MATCH_LEAN=0 (A/B, read per batch): the full-LDS form even without run-length lines or sharing
         const char* le = getenv("MTB_MATCH_LEAN");
         const bool leanOk = !le || atoi(le) != 0;
-        if (leanOk && !(runOff && lineExt) && !h_shareRuns)
-            k_match<false, kFreePer, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
-                                                                  kmerFormat, readCnt, total, buf, bufRank, region, err,
-                                                                  winCap, win, lines, lineP, runOff, sortLo, stats,
-                                                                  direct, dirOff, overflow, capShift, longList, longCap,
-                                                                  longCnt, nullptr, upr, cnt64);
-        else
+        // MTB_MATCH_WAVES (A/B, read per batch): the lean form's waves per SIMD — 6 (80 VGPRs, no
+        // spills; the default), 7 or 8 (72 / 64 VGPRs with scratch spills)
+        const char* we = getenv("MTB_MATCH_WAVES");
+        const int waves = we ? atoi(we) : 6;
+#define MTB_K4_LEAN(W)                                                                                             \
+    k_match<false, kFreePer, W><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax, kmerFormat, \
+                                                       readCnt, total, buf, bufRank, region, err, winCap, win, lines,   \
+                                                       lineP, runOff, sortLo, stats, direct, dirOff, overflow, capShift, \
+                                                       longList, longCap, longCnt, nullptr, upr, cnt64)
+        if (leanOk && !(runOff && lineExt) && !h_shareRuns) {
+            if (waves == 8) MTB_K4_LEAN(8);
+            else if (waves == 7) MTB_K4_LEAN(7);
+            else MTB_K4_LEAN(6);
+        } else
+#undef MTB_K4_LEAN
             k_match<false, kFreePer><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                             kmerFormat, readCnt, total, buf, bufRank, region, err, winCap,
                                                             win, lines, lineP, runOff, sortLo, stats, direct, dirOff,
