@@ -208,7 +208,8 @@ int mtb_last_counts(const mtb_ctx* ctx, uint64_t* query_kmers, uint64_t* matches
  * [16] DB records the DB-sweep join read (MTB_JOIN=sweep: the tiles that held queries; 0 otherwise),
  * [17] / [18] with MTB_DUP_STATS=1 (diagnostic pass after the sort): query k-mers whose AA rank /
  * whole value repeats an earlier query's in their 256-query K4 block (the reference's same-AA /
- * identical-query reuse, KmerMatcher.cpp:277-353; 0 otherwise).
+ * identical-query reuse, KmerMatcher.cpp:277-353; 0 otherwise), [19] K1 units per read when the
+ * batch took uniform units (12 paired, 6 single-end: every frame one chunk, MTB_UNIFORM_UNITS; 0 otherwise).
  * Query k-mers = windows whose AA 8-mer the DB holds. Counts [5]..[9] are over the live matches. */
 int mtb_last_stats(const mtb_ctx* ctx, uint64_t* out, int n);
 /* Per-stage device time of the last batch in ms (HIP events on the launch stream):

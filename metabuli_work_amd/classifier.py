@@ -253,10 +253,11 @@ class Classifier:
             pools.append(pool[:nt])
             qk, mm = qk + q, mm + m
             # the batch's work counts and device times: the halves' summed (a batch maximum stays a
-            # maximum, the join path is the last half's)
+            # maximum, the join path and the unit layout are the last half's)
             st = self.stats()
             stats = st if stats is None else {k: (max(stats[k], v) if k == "max_read_matches" else
-                                                  v if k == "join_path" else stats[k] + v) for k, v in st.items()}
+                                                  v if k in ("join_path", "uniform_units") else stats[k] + v)
+                                              for k, v in st.items()}
             stage += self.stage_ms()
             kern += self.kernel_ms()
         recs[1].view(torch.int32).view(-1, _abi.RESULT_DTYPE.itemsize // 4)[:, 4] += pools[0].shape[0]
@@ -297,7 +298,7 @@ class Classifier:
     STATS = ["slots", "query_kmers", "matched_queries", "matches", "max_read_matches", "groups", "groups_ge2",
              "species_runs", "wave_runs", "wave_runs_emulated", "join_path", "live_matches", "gallop_queries",
              "spilled_matches", "long_run_queries", "filter_reruns", "db_records_read", "dup_aa_queries",
-             "dup_key_queries"]
+             "dup_key_queries", "uniform_units"]
 
     def stats(self) -> dict:
         """Work counts of the last batch (mtb_last_stats; a batch assembled from halves: their sums)."""

@@ -207,7 +207,7 @@ struct mtb_ctx {
     // mtb_open_phases: seconds of the DB files' read, upload + K3 decode into records, AA directory,
     // probe lines, run index, taxonomy + species map, and the whole open
     double openS[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [7]: the records' allocation (inside [1])
-    static constexpr int kNumStats = 19;
+    static constexpr int kNumStats = 20;
     uint64_t stats[kNumStats] = {};  // mtb_last_stats
     uint32_t chunkC = 1;  // K1 windows per unit of the last batch
     uint64_t stageRegion = 0;  // slots per staging region of mStage (grows to the largest seen)
@@ -1564,6 +1564,7 @@ static int classify_batch(mtb_ctx* c, const char* seq, const uint64_t* off, cons
     c->maxW = maxW;
     // uniform units: every frame one chunk (maxW <= 64), 6 units per mate for every read
     c->upr = c->uniformUnits && maxW <= 64 ? (paired ? 12u : 6u) : 0u;
+    c->stats[19] = c->upr;
     launch_read_units(c->meta.as<ReadMeta>(), n, C, c->upr, c->reserve.as<uint32_t>(), s);
     exclusive_scan_u32(c->reserve.as<uint32_t>(), n, c->slotOff.as<uint64_t>(), c->scanTmp.p, s);
     uint64_t U = 0;
