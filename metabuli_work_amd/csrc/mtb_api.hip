@@ -426,6 +426,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     }
     c->openS[1] = since(tp) - (c->openS[0] - readS);  // the decode's uploads are in openS[0]
     set_ab_rank_free(getenv("MTB_AB_RANK_FREE") ? atoi(getenv("MTB_AB_RANK_FREE")) : 0);  // A/B only: invalid results
+    set_match_prefetch(getenv("MTB_MATCH_PREFETCH") ? atoi(getenv("MTB_MATCH_PREFETCH")) : 0);
     set_pair_read(getenv("MTB_PAIR_READ") ? atoi(getenv("MTB_PAIR_READ")) : 0);
     set_match_xcd(getenv("MTB_MATCH_XCD") ? atoi(getenv("MTB_MATCH_XCD")) : 0);  // (device-wide: set at each open)
     // run sharing measured no gain (the repeated lookups already hit the L2: profiles/r05/ab_share*.json): off

@@ -1679,6 +1679,16 @@ __device__ int g_abRankFree = 0;
 __device__ int g_matchXcd = 0;
 __device__ int g_shareRuns = 0;
 __device__ int g_pairRead = 0;
+// MTB_MATCH_PREFETCH=<m> (A/B, lean join): while a query's run-index entry is in flight, read the record
+// line its run most likely starts in — base + before + before * m / 256 (m ~ 256 * (records per
+// present rank - 1): 45 at GTDB scale) — so the dependent record read that follows hits the L2 when
+// the guess lands in the right line; 0: off
+__device__ int g_prefetch = 0;
+static int h_prefetch = 0;
+void set_match_prefetch(int m) {
+    h_prefetch = m;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prefetch), &m, sizeof(int));
+}
 
 void set_pair_read(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pairRead), &on, sizeof(int)); }
 
@@ -1717,7 +1727,7 @@ __device__ __forceinline__ uint64_t uniform_unit_info(uint32_t u, uint32_t p, ui
 
 // kLean: the unstaged join without the A/B options' LDS (run-length lines, run sharing): 18 KB of LDS
 // per block instead of 31, so LDS no longer caps the resident waves below what the VGPRs allow
-template <bool kStage, int kPer, int kLeanWaves = 0>
+template <bool kStage, int kPer, int kLeanWaves = 0, bool kPrefetch = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanWaves ? kLeanWaves : 1))) k_match(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot,
                                                const uint64_t* __restrict__ unitInfo, uint32_t C,
                                                uint64_t Q, const DbRec* __restrict__ db, uint64_t D, AADir d,
@@ -1772,6 +1782,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
     const uint64_t winLo = kStage ? win[2 * blockIdx.x] : 0, winN = kStage ? win[2 * blockIdx.x + 1] - winLo : 0;
     const bool staged = kStage && winN <= (uint64_t)winCap;
     uint64_t lo[kPer], hi[kPer];
+    uint32_t pfw = 0;      // MTB_MATCH_PREFETCH's speculative reads (kept live below, never used)
     uint32_t nGallop = 0;  // probe-line queries whose run the run index does not hold (gallop fallback)
     // Run sharing (the reference's same-AA reuse, KmerMatcher.cpp:315-353: a query whose AA part
     // equals the previous one's reuses its candidates): the block's queries with the same AA rank —
@@ -1881,8 +1892,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
                         continue;
                     }
                     const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
-                    const uint32_t a = runOff[p];
-                    const uint32_t b = before + 1 < pc ? runOff[p + 1] : (uint32_t)cnt;
+                    // both entries read unconditionally (p + 1 <= the index's end entry, allocated): no
+                    // branch between the loads and the prefetch's issue
+                    const uint32_t a = runOff[p], b1 = runOff[p + 1];
+                    const uint32_t b = before + 1 < pc ? b1 : (uint32_t)cnt;
+                    if (kPrefetch) {  // after the run-index reads, unconditionally: waiting for them leaves it in flight
+                        const uint64_t gi = base + before + (((uint64_t)before * (uint32_t)g_prefetch) >> 8);
+                        pfw |= reinterpret_cast<const uint32_t*>(db)[3 * min(gi, D) + 2];
+                    }
                     lo[j] = base + a;
                     hi[j] = base + b;
                     continue;
@@ -2033,6 +2050,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
             if (longq[j] && at < longCap) longList[at] = LongRun{q0 + threadIdx.x + (uint64_t)j * 256, lo[j], hi[j]};
         }
     }
+    if (kPrefetch && pfw == 0xFFFFFFFFu && key[0] == ~0ull) atomicAdd(&stats[kStatStripes], 0ull);  // keeps the prefetches
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
     if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
     if (!kStage && lines) {  // the fallback counter sits past the stripes (rare: a lane-0 atomic per wave)
@@ -2822,11 +2840,17 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         const char* we = getenv("MTB_MATCH_WAVES");
         const int waves = we ? atoi(we) : 6;
 #define MTB_K4_LEAN(W)                                                                                             \
-    k_match<false, kFreePer, W><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax, kmerFormat, \
+    k_match<false, kFreePer, W, false><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax, kmerFormat, \
                                                        readCnt, total, buf, bufRank, region, err, winCap, win, lines,   \
                                                        lineP, runOff, sortLo, stats, direct, dirOff, overflow, capShift, \
                                                        longList, longCap, longCnt, nullptr, upr, cnt64)
-        if (leanOk && !(runOff && lineExt) && !h_shareRuns) {
+        if (leanOk && !(runOff && lineExt) && !h_shareRuns && h_prefetch && runOff) {
+            k_match<false, kFreePer, 6, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
+                                                                     kmerFormat, readCnt, total, buf, bufRank, region,
+                                                                     err, winCap, win, lines, lineP, runOff, sortLo,
+                                                                     stats, direct, dirOff, overflow, capShift, longList,
+                                                                     longCap, longCnt, nullptr, upr, cnt64);
+        } else if (leanOk && !(runOff && lineExt) && !h_shareRuns) {
             if (waves == 8) MTB_K4_LEAN(8);
             else if (waves == 7) MTB_K4_LEAN(7);
             else MTB_K4_LEAN(6);

@@ -269,6 +269,7 @@ constexpr uint32_t kStageRegions = 256;
 void set_ab_rank_free(int on);  // A/B only: k_match without the per-read rank atomic (invalid results)
 void set_match_xcd(int on);     // MTB_MATCH_XCD (A/B): the unstaged join's blocks in one contiguous eighth per XCD
 void set_share_runs(int on);    // MTB_SHARE_RUNS=1 (A/B, off by default): same-AA queries of a block share one run lookup
+void set_match_prefetch(int m);
 void set_pair_read(int on);  // MTB_PAIR_READ=1 (A/B): K4 reads a run's second record for one-record runs too
 void set_ab_sweep_count(int on);  // A/B only: k_sweep_ws searches and selects but emits nothing (invalid results)
 
