@@ -1690,7 +1690,11 @@ void set_match_prefetch(int m) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prefetch), &m, sizeof(int));
 }
 
-void set_pair_read(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pairRead), &on, sizeof(int)); }
+static int h_pairRead = 0, h_matchXcd = 0, h_abRankFree = 0;  // host copies: k_join_uniform runs only without them
+void set_pair_read(int on) {
+    h_pairRead = on;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pairRead), &on, sizeof(int));
+}
 
 static int h_shareRuns = 0;  // host copy: the lean join (no sharing table) when off
 void set_share_runs(int on) {
@@ -1698,9 +1702,15 @@ void set_share_runs(int on) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_shareRuns), &on, sizeof(int));
 }
 
-void set_match_xcd(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on, sizeof(int)); }
+void set_match_xcd(int on) {
+    h_matchXcd = on;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_matchXcd), &on, sizeof(int));
+}
 
-void set_ab_rank_free(int on) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int)); }
+void set_ab_rank_free(int on) {
+    h_abRankFree = on;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_abRankFree), &on, sizeof(int));
+}
 
 // The info of window p of uniform unit u (k_read_units: upr units per read, one per (mate, frame)), as
 // unit_windows + unit_info_at compute it: read u / upr, mate and frame from u % upr, the frame's first
@@ -2140,6 +2150,168 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
                      w, w + c[j], rk[j], err);
         }
         w += c[j];
+    }
+}
+
+// The production join alone (round 6): k_match's unstaged path for the one configuration the bench's
+// batches take — run index, uniform units (the read's 64-bit counter), direct output, long-run list,
+// none of the A/B options — with nothing else in the kernel, so its register peak is that path's:
+// the run's two records, their taxa's species (read beside the rank atomic instead of after it)
+// and the query's Hamming rows: 50 VGPRs and 18.7 KB of LDS, so 8 waves per SIMD (the hardware's most;
+// k_match's lean form: 6). Same matches at the same ranks as k_match (KmerMatcher.cpp:360-448).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot, uint32_t C, uint64_t Q,
+               const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
+               int kmerFormat, unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
+               uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
+               const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ lineP,
+               const uint16_t* __restrict__ runOff, int sortLo, unsigned long long* __restrict__ stats,
+               SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
+               LongRun* __restrict__ longList, uint32_t longCap, uint32_t* __restrict__ longCnt, uint32_t upr,
+               unsigned long long* __restrict__ cnt64) {
+    __shared__ uint4 sLineMem[kMatchLines * 4];
+    __shared__ uint64_t sLineP[kMatchLines];
+    const ProbeLine* const sLines = reinterpret_cast<const ProbeLine*>(sLineMem);
+    const DbVal dbv{db};
+    const DbTax dbtax{db};
+    const uint64_t q0 = (uint64_t)blockIdx.x * 256, q1 = min(q0 + 256, Q);
+    const uint64_t q = q0 + threadIdx.x;
+    const bool live = q < q1;
+    const uint64_t key = live ? qkey[q] : 0;
+    const uint32_t slot = live ? qslot[q] : 0;
+    // the block's probe lines (one contiguous stretch: sorted queries) and their run-index bases in LDS
+    const int sh = sortLo - 24;
+    const uint64_t L0 = ((qkey[q0] >> sortLo) << sh) / kLineRanks;
+    const uint64_t L1 = ((((qkey[q1 - 1] >> sortLo) + 1) << sh) - 1) / kLineRanks;
+    const bool inLds = L1 - L0 < (uint64_t)kMatchLines;
+    if (inLds) {
+        const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;
+        const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
+        for (uint32_t i = threadIdx.x; i < nv; i += 256) sLineMem[i] = src[i];
+        for (uint32_t i = threadIdx.x; i <= (uint32_t)(L1 - L0); i += 256) sLineP[i] = lineP[L0 + i];
+        __syncthreads();
+    }
+    uint64_t lo = 0, hi = 0;
+    bool gallop = false;
+    if (live) {
+        const uint64_t aa = key & kAAMask, x = aa >> 24, L = x / kLineRanks;
+        const uint32_t o = (uint32_t)(x - L * kLineRanks);
+        const ProbeLine* pl = inLds ? sLines + (L - L0) : lines + L;
+        uint32_t before, pc;
+        bool present;
+        const uint64_t head = line_scan(pl, o, before, pc, present);
+        const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
+        if (cnt > kRunIdxMax) {  // a line the run index does not hold: gallop from its lower bound
+            gallop = true;
+            lo = gallop_lower1(dbv, base + before, aa);
+            hi = gallop_lower1(dbv, lo, aa + (1ull << 24));
+        } else if (present) {
+            const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
+            const uint32_t a = runOff[p], b1 = runOff[p + 1];
+            lo = base + a;
+            hi = base + (before + 1 < pc ? b1 : (uint32_t)cnt);
+        } else {
+            lo = hi = base;
+        }
+        if (lo > D) {  // an inconsistent run index or probe line (k_match's check)
+            atomicExch(err, kErrRunOutsideDb);
+            lo = D;
+        }
+        if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
+        if (lo > hi) hi = lo;
+    }
+    const uint64_t n = hi - lo;
+    const bool longq = n > kLongRun;
+    const bool small = live && n <= 2;
+    uint64_t v0 = 0, v1 = 0;
+    uint32_t t0 = 0, t1 = 0;
+    if (small && n) {  // the run's records (a random read moves a 128-B line: the second only if present)
+        const DbRec r0 = db[lo], r1 = n == 2 ? db[lo + 1] : DbRec{0, 0, 0};
+        v0 = (uint64_t)r0.hi << 32 | r0.lo;
+        v1 = (uint64_t)r1.hi << 32 | r1.lo;
+        t0 = r0.tax;
+        t1 = r1.tax;
+    }
+    const HamRows hr = hamming_rows(key);
+    uint32_t c = 0, thr = 0, s0 = 255, s1 = 255;
+    if (small) {
+        s0 = n > 0 ? hamming_sum_rows(hr, v0) : 255u;
+        s1 = n > 1 ? hamming_sum_rows(hr, v1) : 255u;
+        thr = min(min(s0, s1) * 2u, 7u);
+        c = (uint32_t)(s0 <= thr) + (uint32_t)(s1 <= thr);
+    } else if (live && !longq) {
+        c = run_select(hr, dbv, 0, lo, hi, D, thr);
+    }
+    // the selected records' species (L2-resident spOf) in flight with the rank atomic below
+    const bool e0 = small && s0 <= thr, e1 = small && s1 <= thr;
+    const int32_t sp0 = e0 ? (t0 <= maxTax ? spOf[t0] : 0) : 0;
+    const int32_t sp1 = e1 ? (t1 <= maxTax ? spOf[t1] : 0) : 0;
+    uint32_t rk = 0, r = 0;
+    uint64_t info = 0;
+    if (c) {
+        uint32_t p;
+        const uint32_t u = slot_unit(slot, C, p);
+        r = u / upr;
+        const unsigned long long old = atomicAdd(&cnt64[r], (unsigned long long)c);
+        rk = (uint32_t)old;
+        info = uniform_unit_info(u, p, upr, (uint32_t)(old >> 32), kmerFormat);
+    }
+    const uint64_t lm = __ballot(longq && live);
+    if (lm) {  // the wave's long queries to the long-run list (one atomic per wave), for k_match_long
+        const int lane = (int)(threadIdx.x & 63);
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(longCnt, (uint32_t)__popcll(lm));
+        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(lm & ((1ull << lane) - 1));
+        if (longq && live && at < longCap) longList[at] = LongRun{q, lo, hi};
+    }
+    const int blockHits = __syncthreads_count(c != 0);
+    if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);
+    const uint64_t gw = __ballot(gallop);
+    if (gw && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)__popcll(gw));
+    if (!c) return;
+    const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
+    // the read's stretch of upr units (C slots each) bounds its segment; ranks past it spill to buf
+    const uint64_t cap = ((uint64_t)upr * C) >> capShift;
+    const bool spill = rk + c > cap;
+    uint64_t w = rk;
+    if (spill) {
+        const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c);
+        if (sp + c > region) {
+            atomicExch(overflow, 1);
+            return;
+        }
+        w = sp;
+    }
+    SegMatch* const out = direct + (uint64_t)r * upr * C;
+    if (small) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (!(k ? e1 : e0)) continue;
+            const uint64_t tv = k ? v1 : v0;
+            const uint32_t tax = k ? t1 : t0, hs = k ? s1 : s0;
+            const int32_t sp = k ? sp1 : sp0;
+            if (tax == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
+            mtb_match m;
+            m.qinfo = info;
+            m.target_id = tax;
+            m.species_id = (uint32_t)sp;
+            m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
+            m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
+            m.hamming = (uint8_t)hs;
+            m.pad = 0;
+            if (spill) {
+                bufRank[w] = rk++;
+                buf[w] = m;
+            } else {
+                out[w] = seg_pack(m);
+            }
+            w++;
+        }
+    } else if (spill) {
+        run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
+    } else {
+        run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, out, (uint32_t*)nullptr, w, w + c, 0,
+                 err);
     }
 }
 
@@ -2844,6 +3016,17 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                                                        readCnt, total, buf, bufRank, region, err, winCap, win, lines,   \
                                                        lineP, runOff, sortLo, stats, direct, dirOff, overflow, capShift, \
                                                        longList, longCap, longCnt, nullptr, upr, cnt64)
+        // MTB_JOIN_FAST=0 (A/B, read per batch): the production configuration through k_match's lean form
+        // instead of k_join_uniform
+        const char* fe = getenv("MTB_JOIN_FAST");
+        const bool fastOk = (!fe || atoi(fe) != 0) && leanOk && lines && runOff && !lineExt && direct && longList &&
+                            upr && cnt64 && !h_shareRuns && !h_prefetch && !h_pairRead && !h_matchXcd &&
+                            !h_abRankFree;
+        if (fastOk) {
+            k_join_uniform<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank,
+                                                  region, err, lines, lineP, runOff, sortLo, stats, direct, overflow,
+                                                  capShift, longList, longCap, longCnt, upr, cnt64);
+        } else
         if (leanOk && !(runOff && lineExt) && !h_shareRuns && h_prefetch && runOff) {
             k_match<false, kFreePer, 6, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
                                                                      kmerFormat, readCnt, total, buf, bufRank, region,

@@ -33,10 +33,14 @@ def _reads(gen, n, lens, paired, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("window", ["", "0"])
 @pytest.mark.parametrize("paired", [True, False])
 @pytest.mark.parametrize("lens,uniform", [((150,), True), ((215, 216, 217), True), ((216, 217, 218), False),
                                           ((60, 100, 213), True)])
-def test_uniform_units_parity(make_db, monkeypatch, paired, lens, uniform):
+def test_uniform_units_parity(make_db, monkeypatch, paired, lens, uniform, window):
+    """window "0": the unstaged join (k_join_uniform when the layout is on, k_match otherwise)."""
+    if window:
+        monkeypatch.setenv("MTB_MATCH_WINDOW", window)
     from metabuli_work_amd.classifier import Classifier, LocalParameters
     from tests.test_gpu_parity import compare_results
 
