@@ -124,6 +124,7 @@ struct mtb_ctx {
     uint64_t* lineP = nullptr;   // run index: present ranks before each line (0.7 GB) ...
     uint16_t* runOff = nullptr;  // ... and each present rank's run start in its line (2 B per present rank)
     ProbeExt* lineExt = nullptr;  // run-length lines (64 B per probe line; MTB_LINE_EXT=1, A/B)
+    uint64_t* link = nullptr;     // link lines: K1F's window pairs (14.4 GB; MTB_LINK_LINES=0: none)
     AADir dir{};
     uint64_t rankLo = 0, rankHi = ~0ull;  // AA-rank range of the held DB part (K1F drops the rest)
     int joinMode = 0;            // MTB_JOIN: 0 default (sort-merge), 1 sort, 2 probe, 3 sweep
@@ -266,10 +267,11 @@ static void free_db(mtb_ctx* c) {
         c->lineP = nullptr;
         c->runOff = nullptr;
         c->lineExt = nullptr;
+        c->link = nullptr;
         return;
     }
     if (c->borrowedDb) c->db = nullptr;  // caller-owned (mtb_open_resident)
-    void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
+    void* ptrs[] = {c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->link, c->spOf, c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->db = nullptr;
@@ -278,6 +280,7 @@ static void free_db(mtb_ctx* c) {
     c->lineP = nullptr;
     c->runOff = nullptr;
     c->lineExt = nullptr;
+    c->link = nullptr;
 }
 
 template <typename T>
@@ -480,6 +483,17 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
         HIP_TRY(hipMalloc(&c->lines, kProbeLines * sizeof(ProbeLine)));
         HIP_TRY(hipMemsetAsync(c->lines, 0, kProbeLines * sizeof(ProbeLine), s));
         build_probe_lines(c->db, c->D, c->dir, c->lines, s);
+        // link lines for the fused K1F (the sort-merge join's; MTB_LINK_LINES=0, A/B: probe lines only).
+        // A device without the 14.4 GB left for them runs without (same results, one probe per window)
+        const char* ll = getenv("MTB_LINK_LINES");
+        if ((!ll || atoi(ll) != 0) && c->joinMode != 2 && c->joinMode != 3) {
+            if (hipMalloc(&c->link, kLinkSlots * sizeof(uint64_t)) == hipSuccess) {
+                build_link_lines(c->lines, c->link, s);
+            } else {
+                (void)hipGetLastError();  // the failed allocation's error is not the open's
+                c->link = nullptr;
+            }
+        }
         HIP_TRY(hipStreamSynchronize(s));
         c->openS[3] = since(tp);
         const char* ri = getenv("MTB_RUN_INDEX");  // 0: no run index (the unstaged join gallops)
@@ -536,7 +550,7 @@ static int open_into(mtb_ctx* c, HostDb& db, const mtb_params* par, int device, 
     HIP_TRY(hipStreamSynchronize(s));
     c->dbArrays = std::make_shared<DbArrays>();
     c->dbArrays->device = device;
-    c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->spOf,
+    c->dbArrays->own = {c->borrowedDb ? nullptr : c->db, c->dirMem, c->lines, c->lineP, c->runOff, c->lineExt, c->link, c->spOf,
                         c->tNodeOf, c->tNodeTax, c->tParent, c->tDepth, c->tSpParent, c->tFlags};
     bind_workspace(c, 0);
     c->openS[5] = since(tp);
@@ -651,6 +665,7 @@ int mtb_clone(const mtb_ctx* src, mtb_ctx** out) {
     c->lineP = src->lineP;
     c->runOff = src->runOff;
     c->lineExt = src->lineExt;
+    c->link = src->link;
     c->dir = src->dir;
     c->rankLo = src->rankLo;
     c->rankHi = src->rankHi;
@@ -1093,7 +1108,7 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                       c->par.smer_len, c->unitInfo.as<uint64_t>(), c->lines, c->keysB.as<uint64_t>(),
                                       c->valsB.as<uint32_t>(), c->mTotal.as<unsigned long long>(), c->rankLo,
                                       c->rankHi, &c->Qall, cap, c->filterThreadMajor, s,
-                                      digits ? c->digA.as<uint8_t>() : nullptr, nullptr, 0, nullptr, c->upr);
+                                      digits ? c->digA.as<uint8_t>() : nullptr, nullptr, 0, nullptr, c->upr, c->link);
             HIP_TRY(hipGetLastError());
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             if (Q <= cap) break;

@@ -382,6 +382,8 @@ struct WinScanner {
     uint64_t aaAcc = 0, dnaAcc = 0, smAcc = 0;
     uint64_t sm0 = 0, sm1 = 0, sm2 = 0, sm3 = 0, sm4 = 0, sm5 = 0, sm6 = 0, sm7 = 0;
     int run = 0, j;
+    // the last window's rank split for the link lines: its first seven AAs' rank, first and last AA
+    uint32_t first7 = 0, firstAA = 0, lastAA = 0;
 
     __device__ __forceinline__ WinScanner(const UnitWindows& w_, const uint8_t* b, const int8_t* a, const int8_t* n,
                                           int sync, int smerLen)
@@ -440,7 +442,11 @@ struct WinScanner {
         // both formats' resident key: base-21 rank of the 8 AA codes (to_rank_form)
         uint64_t aaPart = 0;
 #pragma unroll
-        for (int k = 7; k >= 0; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
+        for (int k = 7; k >= 1; k--) aaPart = aaPart * 21 + ((aaAcc >> (5 * k)) & 31u);
+        first7 = (uint32_t)aaPart;
+        lastAA = (uint32_t)(aaAcc & 31u);
+        firstAA = (uint32_t)((aaAcc >> 35) & 31u);
+        aaPart = aaPart * 21 + lastAA;
         return (aaPart << 24) | (dnaAcc & 0xFFFFFFull);
     }
 };
@@ -1441,6 +1447,29 @@ __global__ void k_run_offsets(const DbRec* __restrict__ db, uint64_t D, const Pr
 void build_line_prefix(const ProbeLine* lines, uint64_t* lineP, uint32_t* popTmp, void* scanTmp, hipStream_t s) {
     k_line_pop<<<(unsigned)((kProbeLines + 255) / 256), 256, 0, s>>>(lines, popTmp);
     exclusive_scan_u32(popTmp, kProbeLines, lineP, scanTmp, s);
+}
+
+// Bit r of the probe lines' membership bitmap.
+__device__ __forceinline__ uint32_t probe_bit(const ProbeLine* __restrict__ lines, uint64_t r) {
+    const uint64_t L = r / kLineRanks;
+    const uint32_t o = (uint32_t)(r - L * kLineRanks);
+    return (lines[L].bits[o >> 5] >> (o & 31u)) & 1u;
+}
+
+// One thread per AA 7-mer S: its 21 right extensions (ranks 21 S .. 21 S + 20, consecutive) and its 21
+// left extensions (ranks x 21^7 + S: for each x the wave's lanes read consecutive ranks) from the
+// probe lines, through the caches.
+__global__ void __launch_bounds__(256) k_link_lines(const ProbeLine* __restrict__ lines, uint64_t* __restrict__ link) {
+    MTB_GRID_STRIDE(S, kLinkSlots) {
+        uint32_t right = 0, left = 0;
+        for (uint32_t y = 0; y < 21; y++) right |= probe_bit(lines, 21 * S + y) << y;
+        for (uint32_t x = 0; x < 21; x++) left |= probe_bit(lines, (uint64_t)x * kLinkSlots + S) << x;
+        link[S] = (uint64_t)left << 32 | right;
+    }
+}
+
+void build_link_lines(const ProbeLine* lines, uint64_t* link, hipStream_t s) {
+    k_link_lines<<<stride_grid(kLinkSlots), 256, 0, s>>>(lines, link);
 }
 
 void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
@@ -2462,8 +2491,10 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 // a per-wave-per-group counter atomic tripled the probe-free pass, `MTB_AB_FILTER=1`). Output: qkey /
 // qslot as k_filter's (slot = the window's K1 slot).
 constexpr uint32_t kBinStage = 2560;  // binned K1F: windows per group staged in LDS (a group keeps ~1.9k at GTDB scale)
-template <int kPer, bool kJMajor, bool kBinned = false>
-__global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
+// kLink: window pairs through the link lines — 3: at the registers the code takes (132 VGPRs, 3 waves per
+// SIMD), 4: held to 128 (4 waves, a few spills); 0: one probe-line read per window
+template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink == 4 ? 4 : 1))) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
                                                         const uint32_t* __restrict__ unitRead, uint64_t nUnits, uint32_t C,
@@ -2473,7 +2504,8 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
                                                         uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig,
                                                         unsigned long long* __restrict__ binCnt, uint64_t binRc,
-                                                        uint32_t upr) {
+                                                        uint32_t upr, const uint64_t* __restrict__ link) {
+    static_assert(kLink == 0 || kPer % 2 == 0, "windows probed in pairs");
     __shared__ uint8_t sBase[256];
     __shared__ uint32_t sBin[256];
     __shared__ uint32_t sBinBase[256];
@@ -2503,17 +2535,42 @@ __global__ void __launch_bounds__(256) k_extract_filter(const uint8_t* __restric
         // group's last key, so the 16 line reads overlap the scanning
         uint64_t k[kPer];
         uint32_t word[kPer], sh[kPer];
+        uint32_t f0 = 0, t0 = 0, h0 = 0, y0 = 0;
+        bool ok0 = false;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             k[j] = (int)(g + j) < w.nWin ? sc.next() : kSentinel;
-            word[j] = 0;
-            sh[j] = 32;
-            const uint64_t xr = k[j] >> 24;
-            if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {
-                const uint64_t L = xr / kLineRanks;
-                const uint32_t o = (uint32_t)(xr - L * kLineRanks);
-                word[j] = lines[L].bits[o >> 5];
-                sh[j] = o & 31u;
+            if constexpr (kLink) {
+                // the scanner's split of the window's rank r = 21 h + y = f 21^7 + t (no division)
+                const uint64_t r = k[j] >> 24;
+                const bool ok = k[j] != kSentinel && r >= rankLo && r < rankHi;
+                const uint32_t h = sc.first7, y = sc.lastAA, f = sc.firstAA;
+                if (!(j & 1)) {
+                    f0 = f, h0 = h, y0 = y, ok0 = ok;
+                    t0 = (uint32_t)(r - (uint64_t)f * kLinkSlots);
+                    continue;
+                }
+                // windows j - 1 and j: consecutive windows of the frame (the last seven AAs of the first
+                // are the first seven of the second) read the two halves of their shared 7-mer's word —
+                // one 8-B stretch, one memory request; else each window the right half of its own first
+                // seven's. Unconditional loads (a window without a probe reads word 0, which every such
+                // window shares): no branch between the group's loads
+                const bool shared = ok0 && ok && t0 == h;
+                const uint32_t* l32 = reinterpret_cast<const uint32_t*>(link);
+                word[j - 1] = l32[!ok0 ? 0u : (shared ? 2 * (uint64_t)t0 + 1 : 2 * (uint64_t)h0)];
+                word[j] = l32[!ok ? 0u : 2 * (uint64_t)h];
+                sh[j - 1] = !ok0 ? 32u : (shared ? f0 : y0);
+                sh[j] = !ok ? 32u : y;
+            } else {
+                word[j] = 0;
+                sh[j] = 32;
+                const uint64_t xr = k[j] >> 24;
+                if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {
+                    const uint64_t L = xr / kLineRanks;
+                    const uint32_t o = (uint32_t)(xr - L * kLineRanks);
+                    word[j] = lines[L].bits[o >> 5];
+                    sh[j] = o & 31u;
+                }
             }
         }
         uint32_t mask = 0;
@@ -2667,7 +2724,8 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                uint64_t* unitInfo, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
                                uint64_t cap, bool threadMajor, hipStream_t s, uint8_t* qdig,
-                               unsigned long long* binCnt, uint64_t binRc, uint64_t* binHost, uint32_t upr) {
+                               unsigned long long* binCnt, uint64_t binRc, uint64_t* binHost, uint32_t upr,
+                               const uint64_t* link) {
     if (binRc) {
         // binned output: the writes go to 2048 regions of binRc slots; the bucket counts come back
         threadMajor = false;
@@ -2684,11 +2742,22 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
 #define MTB_EF(P, J)                                                                                                  \
     k_extract_filter<P, J, false><<<blocks, 256, lds, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,         \
                                                   extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
-                                                  qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr)
+                                                  qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, nullptr)
         if (binRc) {
             k_extract_filter<kFilterPer, true, true><<<blocks, 256, lds, s>>>(
                 seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
-                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr);
+                unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, nullptr);
+        } else if (link && jMajor) {  // window pairs through the link lines (the default when the context has them)
+            // MTB_LINK_WAVES (A/B, read per batch): 4 (spills) or 3 (none)
+            const char* lw = getenv("MTB_LINK_WAVES");
+            if (lw && atoi(lw) == 3)
+                k_extract_filter<kFilterPer, true, false, 3><<<blocks, 256, lds, s>>>(
+                    seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
+                    smerLen, unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link);
+            else
+                k_extract_filter<kFilterPer, true, false, 4><<<blocks, 256, lds, s>>>(
+                    seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
+                    smerLen, unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link);
         } else if (per == 8) {
             if (jMajor) MTB_EF(8, true);
             else MTB_EF(8, false);
@@ -2721,11 +2790,11 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
             hipEventRecord(ev[0], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0, upr);
+                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0, upr, nullptr);
             hipEventRecord(ev[1], s);
             k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
                                                                 extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0, upr);
+                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0, upr, nullptr);
             hipEventRecord(ev[2], s);
             hipStreamSynchronize(s);
             float a = 0, b = 0;

@@ -204,6 +204,15 @@ void build_line_ext(const ProbeLine* lines, const uint64_t* lineP, const uint16_
 void launch_line_ext_check(const ProbeLine* lines, const uint64_t* lineP, const uint16_t* runOff, const ProbeExt* ext,
                            unsigned long long* out, hipStream_t s);
 
+// Link lines (round 6): per AA 7-mer S (kLinkSlots = 21^7 of them) one u64 — bit y (0..20) set iff the
+// DB holds the 8-mer of rank 21 S + y (S then y), bit 32 + x iff it holds rank x 21^7 + S (x then S) —
+// built from the probe lines (same membership). Consecutive windows of a frame share 7 AAs, so the
+// fused K1F tests both with one random 8-B read of their shared 7-mer's word (14.4 GB) instead of two
+// probe-line reads; a window without a partner reads its own word (as S then y).
+constexpr uint64_t kLinkSlots = 1801088541ull;  // 21^7
+static_assert(kLinkSlots * 21 == kAARankEnd, "21^8 AA ranks");
+void build_link_lines(const ProbeLine* lines, uint64_t* link, hipStream_t s);
+
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count and sets
 // *emitted to the non-blank windows (the reference's query k-mer count). counter: 2 device words.
@@ -219,7 +228,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                                unsigned long long* counter, uint64_t rankLo, uint64_t rankHi, uint64_t* emitted,
                                uint64_t cap, bool threadMajor, hipStream_t s,
                                uint8_t* qdig = nullptr, unsigned long long* binCnt = nullptr, uint64_t binRc = 0,
-                               uint64_t* binHost = nullptr, uint32_t upr = 0);
+                               uint64_t* binHost = nullptr, uint32_t upr = 0, const uint64_t* link = nullptr);
 uint64_t launch_filter(const uint64_t* keys, uint64_t R, const ProbeLine* lines, uint64_t* qkey, uint32_t* qslot,
                        uint64_t* qfrom, unsigned long long* counter, uint64_t rankLo, uint64_t rankHi,
                        uint64_t* emitted, hipStream_t s);
