@@ -179,9 +179,9 @@ def roofline_of(kern, names, alg, traffic):
 # bandwidth at 128-B lines (6.1-6.3 TB/s; a coalesced stream on the same box: 5.82 TB/s)
 RANDOM_CALIBRATION = os.path.join(ROOT, "profiles", "r05", "random_fetch_calibration.json")
 RANDOM_LINE_BYTES = 128
-# the random kernels and the buffer their random reads land in (GB): K1F the 5.4-GB probe lines,
-# the unstaged K4 the 144-GB DB records (and the run index)
-RANDOM_KERNELS = {"filter": 5.4, "match_join": 144.0}
+# the random kernels and the buffer their random reads land in (GB): K1F the 14.4-GB link lines (round 6;
+# the nearest calibrated buffer prices it), the unstaged K4 the 144-GB DB records (and the run index)
+RANDOM_KERNELS = {"filter": 14.4, "match_join": 144.0}
 
 
 def random_ceilings():

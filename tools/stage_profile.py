@@ -2,7 +2,7 @@
 
 Dispatches are attributed to the pipeline stages bench.py reports (kernel_ms) by their order
 within a step: a step starts at k_read_meta; extract = up to and including k_extract; filter =
-k_filter; kmer_sort = everything from there to the join; match_join = k_match_windows + k_match
+k_filter; kmer_sort = everything from there to the join; match_join = k_match_windows + k_match (or k_join_uniform)
 (probe_join = k_probe on MTB_JOIN=probe), with the per-read count scan and a rerun if the staging
 buffer grew; match_transpose = k_match_transpose or k_compact_segments (direct join); match_sort = k_segsort_* (+ the live-match scan
 and k_pack_live); assign = the rest of
@@ -45,7 +45,7 @@ def stage_of(seq):
         elif k.startswith("k_filter"):
             stage = "filter"
         elif (k.startswith(("k_match_windows", "k_prefix_firsts", "k_suffix_min", "k_tile_queries", "k_sweep"))
-              or k.startswith("k_match<") or k == "k_match"):  # K4 or K4S (the sweep's query starts + sweep)
+              or k.startswith("k_match<") or k == "k_match" or k == "k_join_uniform"):  # K4 or K4S (the sweep's query starts + sweep)
             stage = "match_join"
         elif k == "k_probe" or k.startswith("k_probe<"):
             stage = "probe_join"
