@@ -293,6 +293,13 @@ int mtb_sort_pairs(int device, const uint64_t* keys, const uint32_t* vals, uint6
  * any). MTB_ERR_ARG when the context has no run-length lines (MTB_LINE_EXT=0) or no run index. */
 int mtb_line_ext_check(mtb_ctx* ctx, uint64_t out[3]);
 
+/* Diagnostics (round 6): the opened DB's link lines (K1F's one read per window pair: per AA 7-mer S
+ * the 21 8-mers S·y and the 21 x·S) checked against its probe lines for every AA rank r — bit r % 21
+ * of word r / 21 and bit 32 + r / 21^7 of word r % 21^7 must equal membership bit r: out[0] ranks
+ * checked (21^8), out[1] present ranks, out[2] disagreeing bits (MTB_ERR_INTERNAL when any).
+ * MTB_ERR_ARG when the context has no link lines (MTB_LINK_LINES=0, the probe or sweep join). */
+int mtb_link_check(mtb_ctx* ctx, uint64_t out[3]);
+
 /* ---- range-partitioned DB across GPUs ---------------------------- */
 /* A DB larger than one GPU's HBM is cut at split entries (DiffIdxSplit, Kmer.h:111-119; written
  * AA-group aligned by IndexCreator.cpp:843-851, read by KmerMatcher.cpp:180-192,255-271) into

@@ -24,7 +24,7 @@ EXPORTED = [
     "mtb_taxon_lineage", "mtb_start_classify", "mtb_get_em_mappings", "mtb_em", "mtb_write_em_results",
     "mtb_ctx_device", "mtb_start_classify_multi", "mtb_mask_reads", "mtb_workspace_bytes", "mtb_set_workspace_cap",
     "mtb_open_phases", "mtb_start_classify_partitioned", "mtb_release_workspace", "mtb_hamming", "mtb_memcpy",
-    "mtb_line_ext_check", "mtb_pin_eval", "mtb_sort_pairs",
+    "mtb_line_ext_check", "mtb_link_check", "mtb_pin_eval", "mtb_sort_pairs",
 ]
 
 
@@ -95,6 +95,7 @@ def lib() -> ctypes.CDLL:
     L.mtb_sort_pairs.argtypes = [i32, vp, vp, u64, i32, i32, vp, vp]
     L.mtb_memcpy.argtypes = [vp, vp, u64]
     L.mtb_line_ext_check.argtypes = [vp, vp]
+    L.mtb_link_check.argtypes = [vp, vp]
     L.mtb_write_report.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint64, vp, vp, ctypes.c_uint64]
     L.mtb_get_em_mappings.argtypes = [vp, u32, vp, u64, P(u64)]
     L.mtb_em.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, u64, P(u64), P(MtbEmStats)]

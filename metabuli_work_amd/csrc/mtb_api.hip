@@ -1471,6 +1471,25 @@ int mtb_line_ext_check(mtb_ctx* c, uint64_t* out) {
     return MTB_OK;
 }
 
+int mtb_link_check(mtb_ctx* c, uint64_t* out) {
+    if (!c || !out) return MTB_ERR_ARG;
+    out[0] = out[1] = out[2] = 0;
+    if (!c->link || !c->lines) { set_error("no link lines (MTB_LINK_LINES=0, the probe or sweep join, or no memory for them)"); return MTB_ERR_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf cnt;
+    HIP_TRY(cnt.ensure(3 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 3 * sizeof(unsigned long long), c->stream));
+    launch_link_check(c->lines, c->link, cnt.as<unsigned long long>(), c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, cnt.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out[2]) {
+        set_error("internal error: " + std::to_string(out[2]) + " link-line bits disagree with the probe lines");
+        return MTB_ERR_INTERNAL;
+    }
+    return MTB_OK;
+}
+
 int mtb_hamming(int device, const uint64_t* query, const uint64_t* target, uint64_t n, uint8_t* sum, uint16_t* fwd,
                 uint16_t* rev) {
     if (n && (!query || !target || !sum || !fwd || !rev)) { set_error("null argument"); return MTB_ERR_ARG; }

@@ -1472,6 +1472,44 @@ void build_link_lines(const ProbeLine* lines, uint64_t* link, hipStream_t s) {
     k_link_lines<<<stride_grid(kLinkSlots), 256, 0, s>>>(lines, link);
 }
 
+// mtb_link_check: every AA rank's membership bit against both link bits that stand for it — bit
+// r % 21 of word r / 21 and bit 32 + r / 21^7 of word r % 21^7, by plain division (the definition,
+// not the builder's loops). A thread per 32-rank bitmap word; out: ranks, present ranks, mismatches.
+__global__ void __launch_bounds__(256) k_link_check(const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ link,
+                                                    unsigned long long* __restrict__ out) {
+    constexpr uint32_t kWords = kLineRanks / 32;
+    unsigned long long n = 0, present = 0, bad = 0;
+    MTB_GRID_STRIDE(wi, (kProbeLines - 1) * kWords) {
+        const uint64_t L = wi / kWords;
+        const uint32_t k = (uint32_t)(wi - L * kWords);
+        const uint32_t word = lines[L].bits[k];
+        const uint64_t r0 = L * kLineRanks + 32ull * k;
+        for (uint32_t b = 0; b < 32 && r0 + b < kAARankEnd; b++) {
+            const uint64_t r = r0 + b;
+            const uint32_t bit = (word >> b) & 1u;
+            const uint32_t right = (uint32_t)(link[r / 21] >> (r % 21)) & 1u;
+            const uint32_t left = (uint32_t)(link[r % kLinkSlots] >> (32 + r / kLinkSlots)) & 1u;
+            n++;
+            present += bit;
+            bad += (right != bit) + (left != bit);
+        }
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        n += __shfl_xor(n, d, 64);
+        present += __shfl_xor(present, d, 64);
+        bad += __shfl_xor(bad, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], n);
+        atomicAdd(&out[1], present);
+        atomicAdd(&out[2], bad);
+    }
+}
+
+void launch_link_check(const ProbeLine* lines, const uint64_t* link, unsigned long long* out, hipStream_t s) {
+    k_link_check<<<stride_grid((kProbeLines - 1) * (kLineRanks / 32)), 256, 0, s>>>(lines, link, out);
+}
+
 void build_run_offsets(const DbRec* db, uint64_t D, const ProbeLine* lines, const uint64_t* lineP,
                        uint16_t* runOff, hipStream_t s) {
     if (!D) return;
@@ -2491,9 +2529,10 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 // a per-wave-per-group counter atomic tripled the probe-free pass, `MTB_AB_FILTER=1`). Output: qkey /
 // qslot as k_filter's (slot = the window's K1 slot).
 constexpr uint32_t kBinStage = 2560;  // binned K1F: windows per group staged in LDS (a group keeps ~1.9k at GTDB scale)
-// kLink: window pairs through the link lines — 3: at the registers the code takes (132 VGPRs, 3 waves per
-// SIMD), 4: held to 128 (4 waves, a few spills); 0: one probe-line read per window
-template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0>
+// kLink: window pairs through the link lines — 3: at the registers the code takes (3 waves per SIMD),
+// 4: held to 128 VGPRs (4 waves, a few spills); 0: one probe-line read per window. kSplit: the group's
+// probes issued after its scan instead of as each window's (pair's) key is known
+template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0, bool kSplit = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink == 4 ? 4 : 1))) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -2533,6 +2572,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
     for (uint32_t g = 0; g < gEnd; g += kPer) {
         // each window's probe is issued as soon as its key is known; the words are tested after the
         // group's last key, so the 16 line reads overlap the scanning
+        // each probe's word index (u32 offsets into the link lines, < 2 * 21^7, or the probe lines,
+        // < 16 * kProbeLines; 0 for a window without a probe: a shared, cached word), its read issued at
+        // once, or (kSplit) with the group's others after the scan: a load's wait counter drains in issue
+        // order, so a probe issued between two windows makes the next window's base loads wait for it
+        const uint32_t* const src = kLink ? reinterpret_cast<const uint32_t*>(link) : reinterpret_cast<const uint32_t*>(lines);
         uint64_t k[kPer];
         uint32_t word[kPer], sh[kPer];
         uint32_t f0 = 0, t0 = 0, h0 = 0, y0 = 0;
@@ -2553,14 +2597,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
                 // windows j - 1 and j: consecutive windows of the frame (the last seven AAs of the first
                 // are the first seven of the second) read the two halves of their shared 7-mer's word —
                 // one 8-B stretch, one memory request; else each window the right half of its own first
-                // seven's. Unconditional loads (a window without a probe reads word 0, which every such
-                // window shares): no branch between the group's loads
+                // seven's
                 const bool shared = ok0 && ok && t0 == h;
-                const uint32_t* l32 = reinterpret_cast<const uint32_t*>(link);
-                word[j - 1] = l32[!ok0 ? 0u : (shared ? 2 * (uint64_t)t0 + 1 : 2 * (uint64_t)h0)];
-                word[j] = l32[!ok ? 0u : 2 * (uint64_t)h];
+                word[j - 1] = !ok0 ? 0u : (shared ? 2u * t0 + 1u : 2u * h0);
+                word[j] = !ok ? 0u : 2u * h;
                 sh[j - 1] = !ok0 ? 32u : (shared ? f0 : y0);
                 sh[j] = !ok ? 32u : y;
+                if constexpr (!kSplit) {
+                    word[j - 1] = src[word[j - 1]];
+                    word[j] = src[word[j]];
+                }
             } else {
                 word[j] = 0;
                 sh[j] = 32;
@@ -2568,10 +2614,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
                 if (k[j] != kSentinel && xr >= rankLo && xr < rankHi) {
                     const uint64_t L = xr / kLineRanks;
                     const uint32_t o = (uint32_t)(xr - L * kLineRanks);
-                    word[j] = lines[L].bits[o >> 5];
+                    word[j] = (uint32_t)(L * (sizeof(ProbeLine) / 4) + 2 + (o >> 5));  // bits[o / 32] of line L
                     sh[j] = o & 31u;
                 }
+                if constexpr (!kSplit) word[j] = src[word[j]];
             }
+        }
+        if constexpr (kSplit) {
+            asm volatile("" ::: "memory");  // the probes stay behind the scan's base loads
+#pragma unroll
+            for (int j = 0; j < kPer; j++) word[j] = src[word[j]];
         }
         uint32_t mask = 0;
 #pragma unroll
@@ -2740,7 +2792,7 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
         const unsigned blocks = (unsigned)((threads + 255) / 256);
         const size_t lds = binRc ? kBinStage * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
 #define MTB_EF(P, J)                                                                                                  \
-    k_extract_filter<P, J, false><<<blocks, 256, lds, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,         \
+    k_extract_filter<P, J, false, 0, true><<<blocks, 256, lds, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, \
                                                   extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo, lines, qkey, \
                                                   qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, nullptr)
         if (binRc) {
@@ -2748,16 +2800,21 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
                 seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,
                 unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, nullptr);
         } else if (link && jMajor) {  // window pairs through the link lines (the default when the context has them)
-            // MTB_LINK_WAVES (A/B, read per batch): 4 (spills) or 3 (none)
-            const char* lw = getenv("MTB_LINK_WAVES");
-            if (lw && atoi(lw) == 3)
-                k_extract_filter<kFilterPer, true, false, 3><<<blocks, 256, lds, s>>>(
-                    seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
-                    smerLen, unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link);
-            else
-                k_extract_filter<kFilterPer, true, false, 4><<<blocks, 256, lds, s>>>(
-                    seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
-                    smerLen, unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link);
+            // MTB_LINK_FORM (A/B, read per batch): w<waves><s|i>[8] — 4 or 3 waves per SIMD, probes issued
+            // after the group's scan (s) or interleaved (i), groups of 8 windows instead of 16
+            const char* lf = getenv("MTB_LINK_FORM");
+            const std::string f = lf ? lf : "w4i";
+#define MTB_EFL(P, W, S)                                                                                            \
+    k_extract_filter<P, true, false, W, S><<<blocks, 256, lds, s>>>(                                                \
+        seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
+        unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
+            if (f == "w3i") MTB_EFL(16, 3, false);
+            else if (f == "w3s") MTB_EFL(16, 3, true);
+            else if (f == "w4s") MTB_EFL(16, 4, true);
+            else if (f == "w3i8") MTB_EFL(8, 3, false);
+            else if (f == "w3s8") MTB_EFL(8, 3, true);
+            else MTB_EFL(16, 4, false);
+#undef MTB_EFL
         } else if (per == 8) {
             if (jMajor) MTB_EF(8, true);
             else MTB_EF(8, false);
@@ -2787,15 +2844,20 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
         if (hipMalloc((void**)&sc, 2 * sizeof(unsigned long long)) == hipSuccess) {
             for (auto& e : ev) hipEventCreate(&e);
             hipMemsetAsync(sc, 0, 2 * sizeof(unsigned long long), s);
+            // the form the batch ran (link lines: without probes every window reads word 0, from the cache)
             hipEventRecord(ev[0], s);
-            k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
-                                                                extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, rankLo, rankHi, 0, nullptr, nullptr, 0, upr, nullptr);
-            hipEventRecord(ev[1], s);
-            k_extract_filter<kFilterPer, true><<<blocks, 256, 0, s>>>(seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C,
-                                                                extract_tables(t), kmerFormat, syncmer, smerLen, unitInfo,
-                                                                lines, qkey, qslot, sc, 0, 0, 0, nullptr, nullptr, 0, upr, nullptr);
-            hipEventRecord(ev[2], s);
+            for (int pass = 0; pass < 2; pass++) {
+                const uint64_t lo = pass ? 0 : rankLo, hi = pass ? 0 : rankHi;
+                if (link)
+                    k_extract_filter<kFilterPer, true, false, 4><<<blocks, 256, 0, s>>>(
+                        seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
+                        smerLen, unitInfo, lines, qkey, qslot, sc, lo, hi, 0, nullptr, nullptr, 0, upr, link);
+                else
+                    k_extract_filter<kFilterPer, true, false, 0, true><<<blocks, 256, 0, s>>>(
+                        seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
+                        smerLen, unitInfo, lines, qkey, qslot, sc, lo, hi, 0, nullptr, nullptr, 0, upr, nullptr);
+                hipEventRecord(ev[pass + 1], s);
+            }
             hipStreamSynchronize(s);
             float a = 0, b = 0;
             hipEventElapsedTime(&a, ev[0], ev[1]);

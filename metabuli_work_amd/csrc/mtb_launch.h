@@ -212,6 +212,8 @@ void launch_line_ext_check(const ProbeLine* lines, const uint64_t* lineP, const 
 constexpr uint64_t kLinkSlots = 1801088541ull;  // 21^7
 static_assert(kLinkSlots * 21 == kAARankEnd, "21^8 AA ranks");
 void build_link_lines(const ProbeLine* lines, uint64_t* link, hipStream_t s);
+// out (3 device words, zeroed): AA ranks checked, present ranks, link bits that disagree with the probe lines
+void launch_link_check(const ProbeLine* lines, const uint64_t* link, unsigned long long* out, hipStream_t s);
 
 // K1F: the present windows of keys[0..R) (AA 8-mer in the DB) packed, in no particular order, into
 // qkey/qslot (and, when qfrom is given, their DB lower bounds); returns their count and sets

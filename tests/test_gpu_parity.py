@@ -161,6 +161,28 @@ def test_line_ext_matches_run_index(make_db, db_name, monkeypatch):
         assert lib().mtb_line_ext_check(clf.handle, out) != 0
 
 
+@pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1", "fmt2_acc"])
+def test_link_lines_match_probe_lines(make_db, db_name, monkeypatch):
+    """The link lines built at open (round 6: per AA 7-mer the 21 AAs that may follow it and the 21
+    that may precede it) hold, for every one of the 21^8 AA ranks, the membership bit of the probe
+    lines in both places that stand for it (mtb_link_check, by plain division). Without them
+    (MTB_LINK_LINES=0) the entry point says so, and K1F reads the probe lines."""
+    import ctypes
+    from metabuli_work_amd._lib import lib
+    db_dir, taxo, gen = make_db(db_name)
+    with Classifier(_params(db_dir, 2), db_dir=db_dir) as clf:
+        out = (ctypes.c_uint64 * 3)()
+        rc = lib().mtb_link_check(clf.handle, out)
+        assert rc == 0, lib().mtb_last_error().decode()
+        # (the DB's last k-mer, never a candidate, may or may not leave its rank's bit)
+        assert out[0] == 21 ** 8 and out[2] == 0
+        assert abs(int(out[1]) - len(_db_aa_ranks(db_dir, clf.par.kmerFormat))) <= 1
+    monkeypatch.setenv("MTB_LINK_LINES", "0")
+    with Classifier(_params(db_dir, 2), db_dir=db_dir) as clf:
+        out = (ctypes.c_uint64 * 3)()
+        assert lib().mtb_link_check(clf.handle, out) != 0
+
+
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt2_syncmer", "fmt1"])
 def test_end_to_end_batches(make_db, db_name):
     """Whole path, several batches, against oracle classify."""
