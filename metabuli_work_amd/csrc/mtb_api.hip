@@ -1110,6 +1110,10 @@ static int join_stage(mtb_ctx* c, const uint8_t* dSeq1, const uint64_t* dOff1, c
                                       c->rankHi, &c->Qall, cap, c->filterThreadMajor, s,
                                       digits ? c->digA.as<uint8_t>() : nullptr, nullptr, 0, nullptr, c->upr, c->link);
             HIP_TRY(hipGetLastError());
+            if (Q == ~0ull) {  // launch_extract_filter's flag: a block's bases past K1F's LDS stage
+                set_error("internal error: K1F sequence stage overflow");
+                return MTB_ERR_INTERNAL;
+            }
             if (R) c->presentShare = std::max(c->presentShare, std::min(1.0, 1.125 * (double)Q / (double)R));
             if (Q <= cap) break;
             cap = std::min<uint64_t>(R, Q + Q / 8);  // Q <= R: the second pass fits

@@ -375,6 +375,7 @@ __device__ __forceinline__ UnitWindows unit_windows(uint64_t u, uint64_t nUnits,
 // its resident rank-form key (AA rank << 24 | DNA part; kSentinel when not emitted).
 struct WinScanner {
     const UnitWindows& w;
+    const uint8_t* seq;  // the unit's mate: w.seq in HBM, or its copy in the block's LDS stage (K1F)
     const uint8_t* sBase;
     const int8_t *sAA, *sNum;
     int syncmer, nSm;
@@ -386,38 +387,32 @@ struct WinScanner {
     uint32_t first7 = 0, firstAA = 0, lastAA = 0;
 
     __device__ __forceinline__ WinScanner(const UnitWindows& w_, const uint8_t* b, const int8_t* a, const int8_t* n,
-                                          int sync, int smerLen)
-        : w(w_), sBase(b), sAA(a), sNum(n), syncmer(sync), nSm(8 - smerLen + 1),
+                                          int sync, int smerLen, const uint8_t* seqAt)
+        : w(w_), seq(seqAt), sBase(b), sAA(a), sNum(n), syncmer(sync), nSm(8 - smerLen + 1),
           smMask((smerLen >= 13) ? ~0ull : ((1ull << (5 * smerLen)) - 1)), j(w_.pFirst) {
         if (w.nWin > 0)
             for (int k = 0; k < 7; k++) codon();
     }
     __device__ __forceinline__ void codon() {
+        // branch-free (selects only): the loads of a codon sit in one basic block, so the wait before them
+        // is for them alone, not a conservative drain of every load in flight (the K1F probes)
+        const int d = w.fromLeft ? 1 : -1;
         const int c0 = w.fromLeft ? w.s0 + 3 * j : w.e0 - 3 * j;  // first base of the triplet in load order
-        const uint8_t* seq = w.seq;
-        uint32_t b1, b2, b3;
-        if (w.fromLeft) {
-            const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + 1]], z = sBase[seq[c0 + 2]];
-            if (w.comp) { b1 = z; b2 = y; b3 = x; } else { b1 = x; b2 = y; b3 = z; }
-        } else {
-            const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 - 1]], z = sBase[seq[c0 - 2]];
-            if (w.comp) { b1 = x; b2 = y; b3 = z; } else { b1 = z; b2 = y; b3 = x; }
-        }
-        int aa = -1, num = 0;
-        if ((b1 | b2 | b3) < 4u) {
-            if (w.comp) { b1 ^= 2u; b2 ^= 2u; b3 ^= 2u; }
-            const int idx = (int)(b1 << 4 | b2 << 2 | b3);
-            aa = sAA[idx];
-            num = sNum[idx];
-        }
-        if (aa < 0) {
-            run = 0;
-        } else {
-            run++;
-            aaAcc = (aaAcc << 5) | (uint64_t)aa;
-            dnaAcc = (dnaAcc << 3) | (uint64_t)num;
-            smAcc = ((smAcc << 5) | (uint64_t)aa) & smMask;
-        }
+        const uint32_t x = sBase[seq[c0]], y = sBase[seq[c0 + d]], z = sBase[seq[c0 + 2 * d]];
+        // load order x, y, z is the codon's for a forward read from the left or a reverse one from the
+        // right; the other two cases read it backwards
+        const bool back = w.fromLeft == w.comp;
+        const uint32_t cm = w.comp ? 2u : 0u;  // complement of a valid code (iRCT)
+        const uint32_t b1 = (back ? z : x) ^ cm, b2 = y ^ cm, b3 = (back ? x : z) ^ cm;
+        const bool valid = ((x | y | z) < 4u);
+        const int idx = (int)(((b1 << 4) | (b2 << 2) | b3) & 63u);
+        const int aaT = sAA[idx], numT = sNum[idx];
+        const int aa = valid ? aaT : -1, num = valid ? numT : 0;
+        const bool ok = aa >= 0;
+        run = ok ? run + 1 : 0;
+        aaAcc = ok ? (aaAcc << 5) | (uint64_t)aa : aaAcc;
+        dnaAcc = ok ? (dnaAcc << 3) | (uint64_t)num : dnaAcc;
+        smAcc = ok ? ((smAcc << 5) | (uint64_t)aa) & smMask : smAcc;
         if (syncmer) {
             sm7 = sm6; sm6 = sm5; sm5 = sm4; sm4 = sm3; sm3 = sm2; sm2 = sm1; sm1 = sm0; sm0 = smAcc;
         }
@@ -455,7 +450,7 @@ struct WinScanner {
 template <typename F>
 __device__ __forceinline__ void unit_scan(const UnitWindows& w, const uint8_t* sBase, const int8_t* sAA,
                                           const int8_t* sNum, int syncmer, int smerLen, F&& f) {
-    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);
+    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen, w.seq);
     for (int p = 0; p < w.nWin; p++) {
         const uint64_t key = sc.next();
         f(p, key != kSentinel, key);
@@ -2531,8 +2526,11 @@ __global__ void __launch_bounds__(256) k_filter(const uint64_t* __restrict__ key
 constexpr uint32_t kBinStage = 2560;  // binned K1F: windows per group staged in LDS (a group keeps ~1.9k at GTDB scale)
 // kLink: window pairs through the link lines — 3: at the registers the code takes (3 waves per SIMD),
 // 4: held to 128 VGPRs (4 waves, a few spills); 0: one probe-line read per window. kSplit: the group's
-// probes issued after its scan instead of as each window's (pair's) key is known
-template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0, bool kSplit = false>
+// probes issued after its scan instead of as each window's (pair's) key is known. kSeqLds (uniform units
+// only): the block's reads' bases staged in LDS first, so the scan loads nothing from HBM — a load's
+// wait counter drains in issue order, and a base load issued behind a probe waits for that probe
+constexpr uint32_t kSeqStage = 10240;  // >= 23 read pairs (or 44 single reads) of <= 219 bp: a uniform batch's block
+template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0, bool kSplit = false, bool kSeqLds = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink == 4 ? 4 : 1))) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -2565,13 +2563,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
         reinterpret_cast<ulonglong2*>(unitInfo)[u] = make_ulonglong2(w.info0, w.stretch);
         atomicMax(&sMaxWin, (uint32_t)w.nWin);
     }
-    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen);  // loads nothing for a unit without windows
+    __shared__ uint8_t sSeq[kSeqLds ? kSeqStage : 1];
+    // the scanner's bases: in HBM, or (kSeqLds) always an LDS address, so its loads are LDS reads (a
+    // pointer that may be either is a flat load, which waits on the probes' counter too)
+    const uint8_t* seqAt = kSeqLds ? sSeq : w.seq;
+    if constexpr (kSeqLds) {
+        // the block's reads r0..r1 (upr units each): mate 1's bases, then mate 2's, copied with
+        // coalesced byte loads
+        const uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x, uL = min(u0 + blockDim.x, nUnits) - 1;
+        const uint64_t r0 = u0 / upr, r1 = uL / upr;
+        const uint64_t a1 = off1[r0], n1 = off1[r1 + 1] - a1;
+        const uint64_t a2 = seq2 ? off2[r0] : 0, n2 = seq2 ? off2[r1 + 1] - a2 : 0;
+        if (n1 + n2 <= kSeqStage) {
+            for (uint32_t i = threadIdx.x; i < n1; i += blockDim.x) sSeq[i] = seq1[a1 + i];
+            for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) sSeq[n1 + i] = seq2[a2 + i];
+            if (w.nWin > 0) {
+                const uint64_t r = u / upr;
+                seqAt = (u - r * upr) >= 6u ? sSeq + n1 + (off2[r] - a2) : sSeq + (off1[r] - a1);
+            }
+        } else if (threadIdx.x == 0) {
+            // cannot happen in a uniform batch (mates <= 219 bp); flagged in the emitted count, never silent
+            atomicOr(counter + 1, 1ull << 63);
+        }
+    }
+    __syncthreads();
+    WinScanner sc(w, sBase, sAA, sNum, syncmer, smerLen, seqAt);  // loads nothing for a unit without windows
     __syncthreads();
     const uint32_t gEnd = min(C, sMaxWin);
     uint32_t emitted = 0;
     for (uint32_t g = 0; g < gEnd; g += kPer) {
-        // each window's probe is issued as soon as its key is known; the words are tested after the
-        // group's last key, so the 16 line reads overlap the scanning
         // each probe's word index (u32 offsets into the link lines, < 2 * 21^7, or the probe lines,
         // < 16 * kProbeLines; 0 for a window without a probe: a shared, cached word), its read issued at
         // once, or (kSplit) with the group's others after the scan: a load's wait counter drains in issue
@@ -2808,12 +2828,23 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     k_extract_filter<P, true, false, W, S><<<blocks, 256, lds, s>>>(                                                \
         seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
         unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
-            if (f == "w3i") MTB_EFL(16, 3, false);
+#define MTB_EFLS(P, W, S)                                                                                           \
+    k_extract_filter<P, true, false, W, S, true><<<blocks, 256, lds, s>>>(                                          \
+        seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
+        unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
+            // the bases staged in LDS (uniform batches; MTB_K1F_SEQ_LDS=0, A/B: read from HBM)
+            const char* sl = getenv("MTB_K1F_SEQ_LDS");
+            const bool seqLds = upr && (!sl || atoi(sl) != 0);
+            if (seqLds && f == "w3i") MTB_EFLS(16, 3, false);
+            else if (seqLds && f == "w3i8") MTB_EFLS(8, 3, false);
+            else if (seqLds) MTB_EFLS(16, 4, false);
+            else if (f == "w3i") MTB_EFL(16, 3, false);
             else if (f == "w3s") MTB_EFL(16, 3, true);
             else if (f == "w4s") MTB_EFL(16, 4, true);
             else if (f == "w3i8") MTB_EFL(8, 3, false);
             else if (f == "w3s8") MTB_EFL(8, 3, true);
             else MTB_EFL(16, 4, false);
+#undef MTB_EFLS
 #undef MTB_EFL
         } else if (per == 8) {
             if (jMajor) MTB_EF(8, true);
@@ -2828,6 +2859,12 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     hipMemcpyAsync(Q, counter, sizeof(Q), hipMemcpyDeviceToHost, s);
     if (binRc) hipMemcpyAsync(binHost, binCnt, kSortBins * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
+    if (Q[1] >> 63) {  // a block's bases past the LDS stage (kSeqLds): never expected in a uniform batch
+        fprintf(stderr, "[mtb] internal error: K1F sequence stage overflow\n");
+        Q[1] &= ~(1ull << 63);
+        *emitted = ~0ull;
+        return ~0ull;
+    }
     *emitted = Q[1];
     if (binRc) {
         Q[0] = 0;
