@@ -2221,7 +2221,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
 // the run's two records, their taxa's species (read beside the rank atomic instead of after it)
 // and the query's Hamming rows: 50 VGPRs and 18.7 KB of LDS, so 8 waves per SIMD (the hardware's most;
 // k_match's lean form: 6). Same matches at the same ranks as k_match (KmerMatcher.cpp:360-448).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+// kMode 1 (round 6, default; MTB_JOIN_WAVE=0: kMode 0, the block form): each wave stages its own 64
+// queries' probe lines (≤ 16, one 16-B load per lane) and their run-index bases in a wave-private LDS
+// stretch, and tallies its matched queries with a lane-0 atomic on a stats stripe: no block barrier,
+// so the block's four waves run their dependent read chains (run index, records, rank atomic) out of
+// step with each other (join 47.4 -> 42.9 ms per 3.33M-pair batch, profiles/r06/ab_k4_wave.json).
+// kMode 2 / 3 (MTB_JOIN_WAVE=2 / 3, A/B: 7 / 6 waves per SIMD): resident waves walk their 64-query tiles with the next tile's probe
+// lines and the tile after's keys loaded while the current tile joins, so a tile's chain starts at
+// its run-index read.
+constexpr int kWaveLines = 16;
+template <int kMode>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? 7 : (kMode == 3 ? 6 : 8))))
 k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot, uint32_t C, uint64_t Q,
                const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
                int kmerFormat, unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
@@ -2231,149 +2241,250 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
                SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
                LongRun* __restrict__ longList, uint32_t longCap, uint32_t* __restrict__ longCnt, uint32_t upr,
                unsigned long long* __restrict__ cnt64) {
-    __shared__ uint4 sLineMem[kMatchLines * 4];
-    __shared__ uint64_t sLineP[kMatchLines];
-    const ProbeLine* const sLines = reinterpret_cast<const ProbeLine*>(sLineMem);
+    constexpr bool kWave = kMode != 0;
+    constexpr int kStageLines = kWave ? kWaveLines : kMatchLines;
+    __shared__ uint4 sLineMem[(kWave ? 4 : 1) * kStageLines * 4];
+    __shared__ uint64_t sLineP[(kWave ? 4 : 1) * kStageLines];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    uint4* const myLines = sLineMem + (kWave ? wv * kStageLines * 4 : 0);
+    uint64_t* const myLineP = sLineP + (kWave ? wv * kStageLines : 0);
+    const ProbeLine* const sLines = reinterpret_cast<const ProbeLine*>(myLines);
     const DbVal dbv{db};
     const DbTax dbtax{db};
-    const uint64_t q0 = (uint64_t)blockIdx.x * 256, q1 = min(q0 + 256, Q);
-    const uint64_t q = q0 + threadIdx.x;
-    const bool live = q < q1;
-    const uint64_t key = live ? qkey[q] : 0;
-    const uint32_t slot = live ? qslot[q] : 0;
-    // the block's probe lines (one contiguous stretch: sorted queries) and their run-index bases in LDS
     const int sh = sortLo - 24;
-    const uint64_t L0 = ((qkey[q0] >> sortLo) << sh) / kLineRanks;
-    const uint64_t L1 = ((((qkey[q1 - 1] >> sortLo) + 1) << sh) - 1) / kLineRanks;
-    const bool inLds = L1 - L0 < (uint64_t)kMatchLines;
-    if (inLds) {
-        const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;
-        const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
-        for (uint32_t i = threadIdx.x; i < nv; i += 256) sLineMem[i] = src[i];
-        for (uint32_t i = threadIdx.x; i <= (uint32_t)(L1 - L0); i += 256) sLineP[i] = lineP[L0 + i];
-        __syncthreads();
-    }
-    uint64_t lo = 0, hi = 0;
-    bool gallop = false;
-    if (live) {
-        const uint64_t aa = key & kAAMask, x = aa >> 24, L = x / kLineRanks;
-        const uint32_t o = (uint32_t)(x - L * kLineRanks);
-        const ProbeLine* pl = inLds ? sLines + (L - L0) : lines + L;
-        uint32_t before, pc;
-        bool present;
-        const uint64_t head = line_scan(pl, o, before, pc, present);
-        const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
-        if (cnt > kRunIdxMax) {  // a line the run index does not hold: gallop from its lower bound
-            gallop = true;
-            lo = gallop_lower1(dbv, base + before, aa);
-            hi = gallop_lower1(dbv, lo, aa + (1ull << 24));
-        } else if (present) {
-            const uint64_t p = (inLds ? sLineP[L - L0] : lineP[L]) + before;
-            const uint32_t a = runOff[p], b1 = runOff[p + 1];
-            lo = base + a;
-            hi = base + (before + 1 < pc ? b1 : (uint32_t)cnt);
-        } else {
-            lo = hi = base;
-        }
-        if (lo > D) {  // an inconsistent run index or probe line (k_match's check)
-            atomicExch(err, kErrRunOutsideDb);
-            lo = D;
-        }
-        if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
-        if (lo > hi) hi = lo;
-    }
-    const uint64_t n = hi - lo;
-    const bool longq = n > kLongRun;
-    const bool small = live && n <= 2;
-    uint64_t v0 = 0, v1 = 0;
-    uint32_t t0 = 0, t1 = 0;
-    if (small && n) {  // the run's records (a random read moves a 128-B line: the second only if present)
-        const DbRec r0 = db[lo], r1 = n == 2 ? db[lo + 1] : DbRec{0, 0, 0};
-        v0 = (uint64_t)r0.hi << 32 | r0.lo;
-        v1 = (uint64_t)r1.hi << 32 | r1.lo;
-        t0 = r0.tax;
-        t1 = r1.tax;
-    }
-    const HamRows hr = hamming_rows(key);
-    uint32_t c = 0, thr = 0, s0 = 255, s1 = 255;
-    if (small) {
-        s0 = n > 0 ? hamming_sum_rows(hr, v0) : 255u;
-        s1 = n > 1 ? hamming_sum_rows(hr, v1) : 255u;
-        thr = min(min(s0, s1) * 2u, 7u);
-        c = (uint32_t)(s0 <= thr) + (uint32_t)(s1 <= thr);
-    } else if (live && !longq) {
-        c = run_select(hr, dbv, 0, lo, hi, D, thr);
-    }
-    // the selected records' species (L2-resident spOf) in flight with the rank atomic below
-    const bool e0 = small && s0 <= thr, e1 = small && s1 <= thr;
-    const int32_t sp0 = e0 ? (t0 <= maxTax ? spOf[t0] : 0) : 0;
-    const int32_t sp1 = e1 ? (t1 <= maxTax ? spOf[t1] : 0) : 0;
-    uint32_t rk = 0, r = 0;
-    uint64_t info = 0;
-    if (c) {
-        uint32_t p;
-        const uint32_t u = slot_unit(slot, C, p);
-        r = u / upr;
-        const unsigned long long old = atomicAdd(&cnt64[r], (unsigned long long)c);
-        rk = (uint32_t)old;
-        info = uniform_unit_info(u, p, upr, (uint32_t)(old >> 32), kmerFormat);
-    }
-    const uint64_t lm = __ballot(longq && live);
-    if (lm) {  // the wave's long queries to the long-run list (one atomic per wave), for k_match_long
-        const int lane = (int)(threadIdx.x & 63);
-        uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(longCnt, (uint32_t)__popcll(lm));
-        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(lm & ((1ull << lane) - 1));
-        if (longq && live && at < longCap) longList[at] = LongRun{q, lo, hi};
-    }
-    const int blockHits = __syncthreads_count(c != 0);
-    if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);
-    const uint64_t gw = __ballot(gallop);
-    if (gw && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)__popcll(gw));
-    if (!c) return;
-    const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
-    // the read's stretch of upr units (C slots each) bounds its segment; ranks past it spill to buf
-    const uint64_t cap = ((uint64_t)upr * C) >> capShift;
-    const bool spill = rk + c > cap;
-    uint64_t w = rk;
-    if (spill) {
-        const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c);
-        if (sp + c > region) {
-            atomicExch(overflow, 1);
-            return;
-        }
-        w = sp;
-    }
-    SegMatch* const out = direct + (uint64_t)r * upr * C;
-    if (small) {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (!(k ? e1 : e0)) continue;
-            const uint64_t tv = k ? v1 : v0;
-            const uint32_t tax = k ? t1 : t0, hs = k ? s1 : s0;
-            const int32_t sp = k ? sp1 : sp0;
-            if (tax == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
-            mtb_match m;
-            m.qinfo = info;
-            m.target_id = tax;
-            m.species_id = (uint32_t)sp;
-            m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
-            m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
-            m.hamming = (uint8_t)hs;
-            m.pad = 0;
-            if (spill) {
-                bufRank[w] = rk++;
-                buf[w] = m;
+    // the probe lines a stretch of sorted queries spans, from its first and last keys
+    auto lineSpan = [&](uint64_t kFirst, uint64_t kLast, uint64_t& L0, uint64_t& L1) {
+        L0 = ((kFirst >> sortLo) << sh) / kLineRanks;
+        L1 = ((((kLast >> sortLo) + 1) << sh) - 1) / kLineRanks;
+    };
+    // one query: its run from the (staged) probe line and the run index, its records, selection, the
+    // rank atomic, the matches into its read's segment (KmerMatcher.cpp:360-448)
+    auto join = [&](const uint64_t q, const bool live, const uint64_t key, const uint32_t slot, const uint64_t L0,
+                    const bool inLds, const uint32_t tile) {
+        uint64_t lo = 0, hi = 0;
+        bool gallop = false;
+        if (live) {
+            const uint64_t aa = key & kAAMask, x = aa >> 24, L = x / kLineRanks;
+            const uint32_t o = (uint32_t)(x - L * kLineRanks);
+            const ProbeLine* pl = inLds ? sLines + (L - L0) : lines + L;
+            uint32_t before, pc;
+            bool present;
+            const uint64_t head = line_scan(pl, o, before, pc, present);
+            const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
+            if (cnt > kRunIdxMax) {  // a line the run index does not hold: gallop from its lower bound
+                gallop = true;
+                lo = gallop_lower1(dbv, base + before, aa);
+                hi = gallop_lower1(dbv, lo, aa + (1ull << 24));
+            } else if (present) {
+                const uint64_t p = (inLds ? myLineP[L - L0] : lineP[L]) + before;
+                const uint32_t a = runOff[p], b1 = runOff[p + 1];
+                lo = base + a;
+                hi = base + (before + 1 < pc ? b1 : (uint32_t)cnt);
             } else {
-                out[w] = seg_pack(m);
+                lo = hi = base;
             }
-            w++;
+            if (lo > D) {  // an inconsistent run index or probe line (k_match's check)
+                atomicExch(err, kErrRunOutsideDb);
+                lo = D;
+            }
+            if (hi > D - 1) hi = D - 1;  // the last DB k-mer is never a candidate
+            if (lo > hi) hi = lo;
         }
-    } else if (spill) {
-        run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
+        const uint64_t n = hi - lo;
+        const bool longq = n > kLongRun;
+        const bool small = live && n <= 2;
+        uint64_t v0 = 0, v1 = 0;
+        uint32_t t0 = 0, t1 = 0;
+        if (small && n) {  // the run's records (a random read moves a 128-B line: the second only if present)
+            const DbRec r0 = db[lo], r1 = n == 2 ? db[lo + 1] : DbRec{0, 0, 0};
+            v0 = (uint64_t)r0.hi << 32 | r0.lo;
+            v1 = (uint64_t)r1.hi << 32 | r1.lo;
+            t0 = r0.tax;
+            t1 = r1.tax;
+        }
+        const HamRows hr = hamming_rows(key);
+        uint32_t c = 0, thr = 0, s0 = 255, s1 = 255;
+        if (small) {
+            s0 = n > 0 ? hamming_sum_rows(hr, v0) : 255u;
+            s1 = n > 1 ? hamming_sum_rows(hr, v1) : 255u;
+            thr = min(min(s0, s1) * 2u, 7u);
+            c = (uint32_t)(s0 <= thr) + (uint32_t)(s1 <= thr);
+        } else if (live && !longq) {
+            c = run_select(hr, dbv, 0, lo, hi, D, thr);
+        }
+        // the selected records' species (L2-resident spOf) in flight with the rank atomic below
+        const bool e0 = small && s0 <= thr, e1 = small && s1 <= thr;
+        const int32_t sp0 = e0 ? (t0 <= maxTax ? spOf[t0] : 0) : 0;
+        const int32_t sp1 = e1 ? (t1 <= maxTax ? spOf[t1] : 0) : 0;
+        uint32_t rk = 0, r = 0;
+        uint64_t info = 0;
+        if (c) {
+            uint32_t p;
+            const uint32_t u = slot_unit(slot, C, p);
+            r = u / upr;
+            const unsigned long long old = atomicAdd(&cnt64[r], (unsigned long long)c);
+            rk = (uint32_t)old;
+            info = uniform_unit_info(u, p, upr, (uint32_t)(old >> 32), kmerFormat);
+        }
+        const uint64_t lm = __ballot(longq && live);
+        if (lm) {  // the wave's long queries to the long-run list (one atomic per wave), for k_match_long
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(longCnt, (uint32_t)__popcll(lm));
+            at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(lm & ((1ull << lane) - 1));
+            if (longq && live && at < longCap) longList[at] = LongRun{q, lo, hi};
+        }
+        if (kMode != 0) {  // matched queries: a lane-0 atomic per wave on its stripe
+            const uint64_t hw = __ballot(c != 0);
+            if (lane == 0 && hw) atomicAdd(&stats[tile % kStatStripes], (unsigned long long)__popcll(hw));
+        } else {
+            const int blockHits = __syncthreads_count(c != 0);
+            if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);
+        }
+        const uint64_t gw = __ballot(gallop);
+        if (gw && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)__popcll(gw));
+        if (!c) return;
+        const bool rev = ((info_frame(info) < 3) != (kmerFormat == 2));
+        // the read's stretch of upr units (C slots each) bounds its segment; ranks past it spill to buf
+        const uint64_t cap = ((uint64_t)upr * C) >> capShift;
+        const bool spill = rk + c > cap;
+        uint64_t w = rk;
+        if (spill) {
+            const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c);
+            if (sp + c > region) {
+                atomicExch(overflow, 1);
+                return;
+            }
+            w = sp;
+        }
+        SegMatch* const out = direct + (uint64_t)r * upr * C;
+        if (small) {
+    #pragma unroll
+            for (int k = 0; k < 2; k++) {
+                if (!(k ? e1 : e0)) continue;
+                const uint64_t tv = k ? v1 : v0;
+                const uint32_t tax = k ? t1 : t0, hs = k ? s1 : s0;
+                const int32_t sp = k ? sp1 : sp0;
+                if (tax == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
+                mtb_match m;
+                m.qinfo = info;
+                m.target_id = tax;
+                m.species_id = (uint32_t)sp;
+                m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
+                m.right_end_hamming = (uint16_t)hammings_rows(hr, key, tv, rev);
+                m.hamming = (uint8_t)hs;
+                m.pad = 0;
+                if (spill) {
+                    bufRank[w] = rk++;
+                    buf[w] = m;
+                } else {
+                    out[w] = seg_pack(m);
+                }
+                w++;
+            }
+        } else if (spill) {
+            run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, buf, bufRank, w, w + c, rk, err);
+        } else {
+            run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, out, (uint32_t*)nullptr, w, w + c, 0,
+                     err);
+        }
+    };
+    if constexpr (kMode < 2) {
+        // the wave's first query (kMode 1 runs with 256- or 64-thread blocks: MTB_JOIN_WAVE=4, A/B)
+        const uint64_t waveId = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        const uint64_t q0 = kWave ? waveId * 64 : (uint64_t)blockIdx.x * 256;
+        if (kWave && q0 >= Q) return;  // a wave past the queries (no block barrier below in this form)
+        const uint64_t q1 = min(q0 + (kWave ? 64 : 256), Q);
+        const uint64_t q = q0 + (kWave ? (uint64_t)lane : threadIdx.x);
+        const bool live = q < q1;
+        const uint64_t key = live ? qkey[q] : 0;
+        const uint32_t slot = live ? qslot[q] : 0;
+        // the block's (wave's) probe lines (one contiguous stretch: sorted queries) and their run-index
+        // bases in LDS
+        uint64_t L0, L1;
+        lineSpan(kWave ? (uint64_t)__shfl((long long)key, 0, 64) : qkey[q0],
+                 kWave ? (uint64_t)__shfl((long long)key, (int)(q1 - q0 - 1), 64) : qkey[q1 - 1], L0, L1);
+        const bool inLds = L1 - L0 < (uint64_t)kStageLines;
+        if (inLds) {
+            const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;
+            const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
+            if (kWave) {  // one 16-B load per lane and a base per line, both in flight together
+                uint4 v{0, 0, 0, 0};
+                uint64_t lp = 0;
+                if ((uint32_t)lane < nv) v = src[lane];
+                if ((uint32_t)lane <= (uint32_t)(L1 - L0)) lp = lineP[L0 + lane];
+                if ((uint32_t)lane < nv) myLines[lane] = v;
+                if ((uint32_t)lane <= (uint32_t)(L1 - L0)) myLineP[lane] = lp;
+                // the wave's LDS writes complete in program order before any lane reads them back
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                for (uint32_t i = threadIdx.x; i < nv; i += 256) myLines[i] = src[i];
+                for (uint32_t i = threadIdx.x; i <= (uint32_t)(L1 - L0); i += 256) myLineP[i] = lineP[L0 + i];
+                __syncthreads();
+            }
+        }
+        join(q, live, key, slot, L0, inLds, (uint32_t)waveId);
     } else {
-        run_emit(key, hr, info, dbv, dbtax, lo, hi, thr, spOf, maxTax, kmerFormat, out, (uint32_t*)nullptr, w, w + c, 0,
-                 err);
+        // resident waves: tile t = 64 sorted queries; wave w takes tiles w, w + W, w + 2W, ...
+        const uint64_t nT = (Q + 63) / 64, W = (uint64_t)gridDim.x * 4;
+        uint64_t t = (uint64_t)blockIdx.x * 4 + (uint64_t)wv;
+        if (t >= nT) return;
+        auto tileKeys = [&](uint64_t tt, uint64_t& k) {
+            const uint64_t qq = tt * 64 + (uint64_t)lane;
+            k = (tt < nT && qq < Q) ? qkey[qq] : 0;
+        };
+        auto tileSpan = [&](uint64_t tt, uint64_t k, uint64_t& L0, uint64_t& L1) {
+            const uint64_t qa = tt * 64, qb = min(qa + 64, Q);
+            lineSpan((uint64_t)__shfl((long long)k, 0, 64), (uint64_t)__shfl((long long)k, (int)(qb - qa - 1), 64), L0,
+                     L1);
+        };
+        auto stageLoad = [&](uint64_t L0, uint64_t L1, uint4& v, uint64_t& lp) {
+            v = uint4{0, 0, 0, 0};
+            lp = 0;
+            if (L1 - L0 < (uint64_t)kWaveLines) {
+                if ((uint32_t)lane < (uint32_t)(L1 - L0 + 1) * 4) v = reinterpret_cast<const uint4*>(lines + L0)[lane];
+                if ((uint32_t)lane <= (uint32_t)(L1 - L0)) lp = lineP[L0 + lane];
+            }
+        };
+        auto stageStore = [&](uint64_t L0, uint64_t L1, const uint4& v, uint64_t lp) {
+            if (L1 - L0 < (uint64_t)kWaveLines) {
+                if ((uint32_t)lane < (uint32_t)(L1 - L0 + 1) * 4) myLines[lane] = v;
+                if ((uint32_t)lane <= (uint32_t)(L1 - L0)) myLineP[lane] = lp;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS writes done; loads stay in flight
+            __builtin_amdgcn_wave_barrier();
+        };
+        uint64_t kc, kn, L0c, L1c;
+        tileKeys(t, kc);
+        tileKeys(t + W, kn);
+        tileSpan(t, kc, L0c, L1c);
+        {
+            uint4 v;
+            uint64_t lp;
+            stageLoad(L0c, L1c, v, lp);
+            stageStore(L0c, L1c, v, lp);
+        }
+        for (;;) {
+            const bool more = t + W < nT;
+            uint64_t L0n = 0, L1n = 0, kk;
+            uint4 v{0, 0, 0, 0};
+            uint64_t lp = 0;
+            if (more) {  // the next tile's probe lines in flight (its keys arrived during the last tile)
+                tileSpan(t + W, kn, L0n, L1n);
+                stageLoad(L0n, L1n, v, lp);
+            }
+            tileKeys(t + 2 * W, kk);  // the keys of the tile after it
+            const uint64_t q = t * 64 + (uint64_t)lane;
+            const uint32_t sc = q < Q ? qslot[q] : 0;  // needed at the rank atomic: in flight with the run index
+            join(q, q < Q, kc, sc, L0c, L1c - L0c < (uint64_t)kWaveLines, (uint32_t)t);
+            if (!more) break;
+            stageStore(L0n, L1n, v, lp);
+            t += W;
+            kc = kn;
+            kn = kk;
+            L0c = L0n;
+            L1c = L1n;
+        }
     }
 }
 
@@ -3191,9 +3302,31 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                             upr && cnt64 && !h_shareRuns && !h_prefetch && !h_pairRead && !h_matchXcd &&
                             !h_abRankFree;
         if (fastOk) {
-            k_join_uniform<<<(unsigned)((Q + 255) / 256), 256, 0, s>>>(qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank,
-                                                  region, err, lines, lineP, runOff, sortLo, stats, direct, overflow,
-                                                  capShift, longList, longCap, longCnt, upr, cnt64);
+            // MTB_JOIN_WAVE=1 (A/B, read per batch): the per-wave staging form
+            const char* wf = getenv("MTB_JOIN_WAVE");
+            const int wmode = wf ? atoi(wf) : 1;
+            unsigned grid = (unsigned)((Q + 255) / 256);
+#define MTB_K4_JOIN(M)                                                                                              \
+    k_join_uniform<M><<<grid, 256, 0, s>>>(qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank,  \
+                                           region, err, lines, lineP, runOff, sortLo, stats, direct, overflow,      \
+                                           capShift, longList, longCap, longCnt, upr, cnt64)
+            if (wmode == 2 || wmode == 3) {  // resident waves: 7 (6) blocks of 4 waves per CU
+                int dev = 0, cus = 256;
+                if (hipGetDevice(&dev) == hipSuccess)
+                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                grid = std::min<unsigned>(grid, (unsigned)std::max(cus, 1) * (wmode == 2 ? 7u : 6u));
+                if (wmode == 2) MTB_K4_JOIN(2);
+                else MTB_K4_JOIN(3);
+            } else if (wmode == 4) {  // a wave per block: a finished wave frees its slot at once
+                k_join_uniform<1><<<(unsigned)((Q + 63) / 64), 64, 0, s>>>(
+                    qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank, region, err, lines, lineP,
+                    runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64);
+            } else if (wmode == 1) {
+                MTB_K4_JOIN(1);
+            } else {
+                MTB_K4_JOIN(0);
+            }
+#undef MTB_K4_JOIN
         } else
         if (leanOk && !(runOff && lineExt) && !h_shareRuns && h_prefetch && runOff) {
             k_match<false, kFreePer, 6, true><<<blocks, 256, 0, s>>>(qkey, qslot, unitInfo, C, Q, db, D, dir, spOf, maxTax,
