@@ -1328,6 +1328,25 @@ __device__ __forceinline__ bool ext_run(const uint32_t* xw, uint32_t before, uin
     return esc == 0;
 }
 
+// ext_run in a rolled loop over the words up to the rank's own (the wave join: fewer live registers)
+__device__ __forceinline__ bool ext_run_rolled(const uint32_t* xw, uint32_t before, uint32_t& sum, uint32_t& code) {
+    const uint32_t wq = before >> 4, f = before & 15u;
+    uint32_t esc = 0, acc = 0;
+#pragma nounroll
+    for (uint32_t i = 0; i < wq; i++) {
+        const uint32_t w = xw[i];
+        acc += (uint32_t)__popc(w & 0x55555555u) + 2u * (uint32_t)__popc(w & 0xAAAAAAAAu);
+        esc |= w & (w >> 1) & 0x55555555u;
+    }
+    const uint32_t w = xw[wq];
+    const uint32_t mLt = (1u << (2 * f)) - 1u, mLe = f == 15u ? ~0u : (1u << (2 * f + 2)) - 1u;
+    const uint32_t wl = w & mLt, we = w & mLe;
+    sum = acc + (uint32_t)__popc(wl & 0x55555555u) + 2u * (uint32_t)__popc(wl & 0xAAAAAAAAu);
+    esc |= we & (we >> 1) & 0x55555555u;
+    code = (w >> (2 * f)) & 3u;
+    return esc == 0;
+}
+
 // Every present rank of every indexed line against the run index (mtb_line_ext_check): out[0] the
 // ranks within the run-length lines' reach, out[1] those they resolve, out[2] mismatches.
 __global__ void __launch_bounds__(256) k_line_ext_check(const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ lineP,
@@ -2231,7 +2250,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
 // its run-index read.
 constexpr int kWaveLines = 16;
 template <int kMode>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? 7 : (kMode == 3 ? 6 : 8))))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 || kMode == 5 ? 7 : (kMode == 3 ? 6 : 8))))
 k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot, uint32_t C, uint64_t Q,
                const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
                int kmerFormat, unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
@@ -2240,10 +2259,14 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
                const uint16_t* __restrict__ runOff, int sortLo, unsigned long long* __restrict__ stats,
                SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
                LongRun* __restrict__ longList, uint32_t longCap, uint32_t* __restrict__ longCnt, uint32_t upr,
-               unsigned long long* __restrict__ cnt64) {
+               unsigned long long* __restrict__ cnt64, const ProbeExt* __restrict__ lineExt) {
     constexpr bool kWave = kMode != 0;
-    constexpr int kStageLines = kWave ? kWaveLines : kMatchLines;
+    constexpr bool kExt = kMode == 5;  // the wave form with run-length lines staged beside the probe lines
+    constexpr int kStageLines = kWave ? kWaveLines : kMatchLines;  // (per wave / per block)
     __shared__ uint4 sLineMem[(kWave ? 4 : 1) * kStageLines * 4];
+    __shared__ uint4 sExtMem[kExt ? 4 * kWaveLines * 4 : 1];
+    uint4* const myExt4 = sExtMem + (kExt ? (threadIdx.x >> 6) * kWaveLines * 4 : 0);
+    const uint32_t* const myExt = reinterpret_cast<const uint32_t*>(myExt4);
     __shared__ uint64_t sLineP[(kWave ? 4 : 1) * kStageLines];
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
     uint4* const myLines = sLineMem + (kWave ? wv * kStageLines * 4 : 0);
@@ -2276,10 +2299,16 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
                 lo = gallop_lower1(dbv, base + before, aa);
                 hi = gallop_lower1(dbv, lo, aa + (1ull << 24));
             } else if (present) {
-                const uint64_t p = (inLds ? myLineP[L - L0] : lineP[L]) + before;
-                const uint32_t a = runOff[p], b1 = runOff[p + 1];
-                lo = base + a;
-                hi = base + (before + 1 < pc ? b1 : (uint32_t)cnt);
+                uint32_t sum = 0, code = 0;
+                if (kExt && inLds && before < kExtRanks && ext_run_rolled(myExt + (L - L0) * (kExtRanks / 16), before, sum, code)) {
+                    lo = base + before + sum;  // no run-index read (the codes before it hold no escape)
+                    hi = lo + code + 1;
+                } else {
+                    const uint64_t p = (inLds ? myLineP[L - L0] : lineP[L]) + before;
+                    const uint32_t a = runOff[p], b1 = runOff[p + 1];
+                    lo = base + a;
+                    hi = base + (before + 1 < pc ? b1 : (uint32_t)cnt);
+                }
             } else {
                 lo = hi = base;
             }
@@ -2408,11 +2437,13 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
             const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;
             const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
             if (kWave) {  // one 16-B load per lane and a base per line, both in flight together
-                uint4 v{0, 0, 0, 0};
+                uint4 v{0, 0, 0, 0}, xv{0, 0, 0, 0};
                 uint64_t lp = 0;
                 if ((uint32_t)lane < nv) v = src[lane];
+                if (kExt && (uint32_t)lane < nv) xv = reinterpret_cast<const uint4*>(lineExt + L0)[lane];
                 if ((uint32_t)lane <= (uint32_t)(L1 - L0)) lp = lineP[L0 + lane];
                 if ((uint32_t)lane < nv) myLines[lane] = v;
+                if (kExt && (uint32_t)lane < nv) myExt4[lane] = xv;
                 if ((uint32_t)lane <= (uint32_t)(L1 - L0)) myLineP[lane] = lp;
                 // the wave's LDS writes complete in program order before any lane reads them back
                 __builtin_amdgcn_s_waitcnt(0);
@@ -3298,7 +3329,9 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
         // MTB_JOIN_FAST=0 (A/B, read per batch): the production configuration through k_match's lean form
         // instead of k_join_uniform
         const char* fe = getenv("MTB_JOIN_FAST");
-        const bool fastOk = (!fe || atoi(fe) != 0) && leanOk && lines && runOff && !lineExt && direct && longList &&
+        const char* wfe = getenv("MTB_JOIN_WAVE");  // run-length lines: only the wave form (mode 5) reads them
+        const bool fastOk = (!fe || atoi(fe) != 0) && leanOk && lines && runOff &&
+                            (!lineExt || !wfe || atoi(wfe) == 1) && direct && longList &&
                             upr && cnt64 && !h_shareRuns && !h_prefetch && !h_pairRead && !h_matchXcd &&
                             !h_abRankFree;
         if (fastOk) {
@@ -3309,7 +3342,7 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
 #define MTB_K4_JOIN(M)                                                                                              \
     k_join_uniform<M><<<grid, 256, 0, s>>>(qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank,  \
                                            region, err, lines, lineP, runOff, sortLo, stats, direct, overflow,      \
-                                           capShift, longList, longCap, longCnt, upr, cnt64)
+                                           capShift, longList, longCap, longCnt, upr, cnt64, lineExt)
             if (wmode == 2 || wmode == 3) {  // resident waves: 7 (6) blocks of 4 waves per CU
                 int dev = 0, cus = 256;
                 if (hipGetDevice(&dev) == hipSuccess)
@@ -3320,7 +3353,14 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
             } else if (wmode == 4) {  // a wave per block: a finished wave frees its slot at once
                 k_join_uniform<1><<<(unsigned)((Q + 63) / 64), 64, 0, s>>>(
                     qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank, region, err, lines, lineP,
-                    runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64);
+                    runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64, nullptr);
+            } else if (lineExt) {  // MTB_LINE_EXT=1 with the wave form: runs from the staged run-length lines
+                MTB_K4_JOIN(5);
+            } else if (wmode == 1 && getenv("MTB_JOIN_PAD")) {
+                // A/B diagnostic: dynamic LDS reserved per block (unused) to cap the waves per SIMD
+                k_join_uniform<1><<<grid, 256, (size_t)atoi(getenv("MTB_JOIN_PAD")), s>>>(
+                    qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank, region, err, lines, lineP,
+                    runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64, lineExt);
             } else if (wmode == 1) {
                 MTB_K4_JOIN(1);
             } else {
