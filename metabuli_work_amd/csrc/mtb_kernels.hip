@@ -2519,6 +2519,236 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
     }
 }
 
+// k_join_uniform's wave form with two queries per lane (MTB_JOIN_WAVE=6, A/B): a wave takes 128 sorted
+// queries (lane l: queries l and l + 64) and stages their ≤ 32 probe lines; each phase of the chain
+// (run index, records, rank atomic) issues both queries' requests before waiting, so a SIMD keeps two
+// chains in flight per lane. K4 is bound by the chains in flight (8 / 6 / 4 waves per SIMD: 41.6 /
+// 46-49.5 / 56 ms per batch, profiles/r06/ab_k4_occ.json). Same matches at the same ranks.
+constexpr int kPairLines = 32;
+template <int kW>  // waves per SIMD the registers are held to (MTB_JOIN_WAVE=6 / 7 / 8)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW)))
+k_join_pair(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot, uint32_t C, uint64_t Q,
+            const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
+            int kmerFormat, unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
+            uint32_t* __restrict__ bufRank, uint64_t region, int* __restrict__ err,
+            const ProbeLine* __restrict__ lines, const uint64_t* __restrict__ lineP,
+            const uint16_t* __restrict__ runOff, int sortLo, unsigned long long* __restrict__ stats,
+            SegMatch* __restrict__ direct, int* __restrict__ overflow, uint32_t capShift,
+            LongRun* __restrict__ longList, uint32_t longCap, uint32_t* __restrict__ longCnt, uint32_t upr,
+            unsigned long long* __restrict__ cnt64) {
+    __shared__ uint4 sLineMem[4 * kPairLines * 4];
+    __shared__ uint64_t sLineP[4 * kPairLines];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    uint4* const myLines = sLineMem + wv * kPairLines * 4;
+    uint64_t* const myLineP = sLineP + wv * kPairLines;
+    const ProbeLine* const sLines = reinterpret_cast<const ProbeLine*>(myLines);
+    const DbVal dbv{db};
+    const DbTax dbtax{db};
+    const uint64_t waveId = (uint64_t)blockIdx.x * 4 + (uint64_t)wv;
+    const uint64_t q0 = waveId * 128;
+    if (q0 >= Q) return;
+    const uint64_t q1 = min(q0 + 128, Q);
+    uint64_t q[2], key[2];
+    uint32_t slot[2];
+    bool live[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        q[j] = q0 + (uint64_t)(64 * j + lane);
+        live[j] = q[j] < q1;
+        key[j] = live[j] ? qkey[q[j]] : 0;
+        slot[j] = live[j] ? qslot[q[j]] : 0;
+    }
+    const int sh = sortLo - 24;
+    const int last = (int)(q1 - q0 - 1);
+    const uint64_t kFirst = (uint64_t)__shfl((long long)key[0], 0, 64);
+    const uint64_t kLast = (uint64_t)(last < 64 ? __shfl((long long)key[0], last, 64) : __shfl((long long)key[1], last - 64, 64));
+    const uint64_t L0 = ((kFirst >> sortLo) << sh) / kLineRanks;
+    const uint64_t L1 = ((((kLast >> sortLo) + 1) << sh) - 1) / kLineRanks;
+    const bool inLds = L1 - L0 < (uint64_t)kPairLines;
+    if (inLds) {  // two 16-B loads per lane and a base per line, all in flight together
+        const uint32_t nv = (uint32_t)(L1 - L0 + 1) * 4;
+        const uint4* src = reinterpret_cast<const uint4*>(lines + L0);
+        uint4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
+        uint64_t lp = 0;
+        if ((uint32_t)lane < nv) v0 = src[lane];
+        if ((uint32_t)lane + 64 < nv) v1 = src[lane + 64];
+        if ((uint32_t)lane <= (uint32_t)(L1 - L0)) lp = lineP[L0 + lane];
+        if ((uint32_t)lane < nv) myLines[lane] = v0;
+        if ((uint32_t)lane + 64 < nv) myLines[lane + 64] = v1;
+        if ((uint32_t)lane <= (uint32_t)(L1 - L0)) myLineP[lane] = lp;
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the runs: line scans from LDS, then both run-index reads
+    uint64_t lo[2] = {0, 0}, hi[2] = {0, 0};
+    bool gallop[2] = {false, false};
+    uint64_t rp[2] = {0, 0}, rbase[2] = {0, 0};
+    uint32_t rcnt[2] = {0, 0}, rlast[2] = {0, 0};
+    bool needIdx[2] = {false, false};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if (!live[j]) continue;
+        const uint64_t aa = key[j] & kAAMask, x = aa >> 24, L = x / kLineRanks;
+        const uint32_t o = (uint32_t)(x - L * kLineRanks);
+        const ProbeLine* pl = inLds ? sLines + (L - L0) : lines + L;
+        uint32_t before, pc;
+        bool present;
+        const uint64_t head = line_scan(pl, o, before, pc, present);
+        const uint64_t base = head & ((1ull << 40) - 1), cnt = head >> 40;
+        if (cnt > kRunIdxMax) {  // a line the run index does not hold: gallop from its lower bound
+            gallop[j] = true;
+            lo[j] = gallop_lower1(dbv, base + before, aa);
+            hi[j] = gallop_lower1(dbv, lo[j], aa + (1ull << 24));
+        } else if (present) {
+            needIdx[j] = true;
+            rp[j] = (inLds ? myLineP[L - L0] : lineP[L]) + before;
+            rbase[j] = base;
+            rcnt[j] = (uint32_t)cnt;
+            rlast[j] = before + 1 < pc ? 0u : 1u;
+        } else {
+            lo[j] = hi[j] = base;
+        }
+    }
+    uint32_t ra[2] = {0, 0}, rb[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+        if (needIdx[j]) {
+            ra[j] = runOff[rp[j]];
+            rb[j] = runOff[rp[j] + 1];
+        }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if (needIdx[j]) {
+            lo[j] = rbase[j] + ra[j];
+            hi[j] = rbase[j] + (rlast[j] ? rcnt[j] : rb[j]);
+        }
+        if (live[j]) {
+            if (lo[j] > D) {  // an inconsistent run index or probe line (k_match's check)
+                atomicExch(err, kErrRunOutsideDb);
+                lo[j] = D;
+            }
+            if (hi[j] > D - 1) hi[j] = D - 1;  // the last DB k-mer is never a candidate
+            if (lo[j] > hi[j]) hi[j] = lo[j];
+        }
+    }
+    // the runs' records, both queries' in flight together
+    bool small[2], longq[2];
+    uint64_t v0[2] = {0, 0}, v1[2] = {0, 0};
+    uint32_t t0[2] = {0, 0}, t1[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint64_t n = hi[j] - lo[j];
+        longq[j] = live[j] && n > kLongRun;
+        small[j] = live[j] && n <= 2;
+        if (small[j] && n) {
+            const DbRec r0 = db[lo[j]], r1 = n == 2 ? db[lo[j] + 1] : DbRec{0, 0, 0};
+            v0[j] = (uint64_t)r0.hi << 32 | r0.lo;
+            v1[j] = (uint64_t)r1.hi << 32 | r1.lo;
+            t0[j] = r0.tax;
+            t1[j] = r1.tax;
+        }
+    }
+    uint32_t c[2] = {0, 0}, thr[2] = {0, 0}, s0[2] = {255, 255}, s1[2] = {255, 255};
+    int32_t sp0[2] = {0, 0}, sp1[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const HamRows hr = hamming_rows(key[j]);
+        const uint64_t n = hi[j] - lo[j];
+        if (small[j]) {
+            s0[j] = n > 0 ? hamming_sum_rows(hr, v0[j]) : 255u;
+            s1[j] = n > 1 ? hamming_sum_rows(hr, v1[j]) : 255u;
+            thr[j] = min(min(s0[j], s1[j]) * 2u, 7u);
+            c[j] = (uint32_t)(s0[j] <= thr[j]) + (uint32_t)(s1[j] <= thr[j]);
+        } else if (live[j] && !longq[j]) {
+            c[j] = run_select(hr, dbv, 0, lo[j], hi[j], D, thr[j]);
+        }
+        const bool e0 = small[j] && s0[j] <= thr[j], e1 = small[j] && s1[j] <= thr[j];
+        sp0[j] = e0 ? (t0[j] <= maxTax ? spOf[t0[j]] : 0) : 0;
+        sp1[j] = e1 ? (t1[j] <= maxTax ? spOf[t1[j]] : 0) : 0;
+    }
+    // both rank atomics in flight together
+    uint32_t rk[2] = {0, 0}, rr[2] = {0, 0};
+    uint64_t info[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+        if (c[j]) {
+            uint32_t p;
+            const uint32_t u = slot_unit(slot[j], C, p);
+            rr[j] = u / upr;
+            const unsigned long long old = atomicAdd(&cnt64[rr[j]], (unsigned long long)c[j]);
+            rk[j] = (uint32_t)old;
+            info[j] = uniform_unit_info(u, p, upr, (uint32_t)(old >> 32), kmerFormat);
+        }
+    uint32_t hits = 0, gal = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint64_t lm = __ballot(longq[j]);
+        if (lm) {  // the wave's long queries to the long-run list (one atomic per wave), for k_match_long
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(longCnt, (uint32_t)__popcll(lm));
+            at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(lm & ((1ull << lane) - 1));
+            if (longq[j] && at < longCap) longList[at] = LongRun{q[j], lo[j], hi[j]};
+        }
+        hits += (uint32_t)__popcll(__ballot(c[j] != 0));
+        gal += (uint32_t)__popcll(__ballot(gallop[j]));
+    }
+    if (lane == 0 && hits) atomicAdd(&stats[waveId % kStatStripes], (unsigned long long)hits);
+    if (lane == 0 && gal) atomicAdd(&stats[kStatStripes], (unsigned long long)gal);
+    const uint64_t cap = ((uint64_t)upr * C) >> capShift;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if (!c[j]) continue;
+        const bool rev = ((info_frame(info[j]) < 3) != (kmerFormat == 2));
+        // the read's stretch of upr units (C slots each) bounds its segment; ranks past it spill to buf
+        const bool spill = rk[j] + c[j] > cap;
+        uint64_t w = rk[j];
+        if (spill) {
+            const uint64_t sp = atomicAdd(&total[0], (unsigned long long)c[j]);
+            if (sp + c[j] > region) {
+                atomicExch(overflow, 1);
+                continue;
+            }
+            w = sp;
+        }
+        SegMatch* const out = direct + (uint64_t)rr[j] * upr * C;
+        if (small[j]) {
+            const HamRows hr = hamming_rows(key[j]);
+            uint32_t rkj = rk[j];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                if (!(k ? s1[j] <= thr[j] : s0[j] <= thr[j])) continue;
+                const uint64_t tv = k ? v1[j] : v0[j];
+                const uint32_t tax = k ? t1[j] : t0[j], hs = k ? s1[j] : s0[j];
+                const int32_t sp = k ? sp1[j] : sp0[j];
+                if (tax == 0 || sp <= 0) atomicExch(err, kErrTaxid);  // KmerMatcher.cpp:432-441 exits
+                mtb_match m;
+                m.qinfo = info[j];
+                m.target_id = tax;
+                m.species_id = (uint32_t)sp;
+                m.dna_encoding = (uint32_t)(tv & 0xFFFFFFull);
+                m.right_end_hamming = (uint16_t)hammings_rows(hr, key[j], tv, rev);
+                m.hamming = (uint8_t)hs;
+                m.pad = 0;
+                if (spill) {
+                    bufRank[w] = rkj++;
+                    buf[w] = m;
+                } else {
+                    out[w] = seg_pack(m);
+                }
+                w++;
+            }
+        } else {
+            const HamRows hr = hamming_rows(key[j]);
+            if (spill)
+                run_emit(key[j], hr, info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, buf, bufRank, w,
+                         w + c[j], rk[j], err);
+            else
+                run_emit(key[j], hr, info[j], dbv, dbtax, lo[j], hi[j], thr[j], spOf, maxTax, kmerFormat, out,
+                         (uint32_t*)nullptr, w, w + c[j], 0, err);
+        }
+    }
+}
+
 // The long-run list of the direct join: one wave per long query (wave_long_run).
 __global__ void __launch_bounds__(64) k_match_long(const LongRun* __restrict__ list, const uint64_t* __restrict__ qkey,
                                                    const uint32_t* __restrict__ qslot,
@@ -3356,6 +3586,16 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                     runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64, nullptr);
             } else if (lineExt) {  // MTB_LINE_EXT=1 with the wave form: runs from the staged run-length lines
                 MTB_K4_JOIN(5);
+            } else if (wmode >= 6 && wmode <= 8) {  // two queries per lane
+#define MTB_K4_PAIR(W)                                                                                              \
+    k_join_pair<W><<<(unsigned)((Q + 511) / 512), 256, 0, s>>>(qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat,   \
+                                                              total, buf, bufRank, region, err, lines, lineP, runOff, \
+                                                              sortLo, stats, direct, overflow, capShift, longList,    \
+                                                              longCap, longCnt, upr, cnt64)
+                if (wmode == 6) MTB_K4_PAIR(6);
+                else if (wmode == 7) MTB_K4_PAIR(7);
+                else MTB_K4_PAIR(8);
+#undef MTB_K4_PAIR
             } else if (wmode == 1 && getenv("MTB_JOIN_PAD")) {
                 // A/B diagnostic: dynamic LDS reserved per block (unused) to cap the waves per SIMD
                 k_join_uniform<1><<<grid, 256, (size_t)atoi(getenv("MTB_JOIN_PAD")), s>>>(

@@ -201,7 +201,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:nofast", "0:blockjoin", "0:pipejoin", "0:wave64join", "0:nolink", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "0:ballot", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:nofast", "0:blockjoin", "0:pipejoin", "0:wave64join", "0:pairjoin", "6144:pairjoin", "0:nolink", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "0:ballot", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -232,7 +232,7 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_JOIN_FAST", "0" if mode == "nofast" else "1")
     # k_join_uniform's staging: per wave (the default), per block (round 6's first form), or resident waves
     # with the next tile's lines and keys in flight (A/B)
-    monkeypatch.setenv("MTB_JOIN_WAVE", {"blockjoin": "0", "pipejoin": "2", "wave64join": "4"}.get(mode, "1"))
+    monkeypatch.setenv("MTB_JOIN_WAVE", {"blockjoin": "0", "pipejoin": "2", "wave64join": "4", "pairjoin": "7"}.get(mode, "1"))
     # the fused K1F's one probe-line read per window instead of the link lines' one read per window pair
     monkeypatch.setenv("MTB_LINK_LINES", "0" if mode == "nolink" else "1")
     # K1F writing straight into K2's first-pass buckets at any batch size; with 64-slot buckets, which
