@@ -17,7 +17,7 @@ def stage(k):
         return "filter"
     if k.startswith("k_radix") or k.startswith("k_scan") and False:
         return "kmer_sort"
-    if k.startswith("k_match<") or k == "k_join_uniform":
+    if k.startswith(("k_match<", "k_join_uniform<", "k_join_pair<")) or k == "k_join_uniform":
         return "match_join"
     if k.startswith(("k_compact_segments", "k_spill_scatter")):
         return "match_transpose"

@@ -45,7 +45,7 @@ def stage_of(seq):
         elif k.startswith("k_filter"):
             stage = "filter"
         elif (k.startswith(("k_match_windows", "k_prefix_firsts", "k_suffix_min", "k_tile_queries", "k_sweep"))
-              or k.startswith("k_match<") or k == "k_match" or k == "k_join_uniform"):  # K4 or K4S (the sweep's query starts + sweep)
+              or k.startswith(("k_match<", "k_join_uniform<", "k_join_pair<")) or k in ("k_match", "k_join_uniform")):  # K4 or K4S (the sweep's query starts + sweep)
             stage = "match_join"
         elif k == "k_probe" or k.startswith("k_probe<"):
             stage = "probe_join"
