@@ -2902,7 +2902,11 @@ constexpr uint32_t kBinStage = 2560;  // binned K1F: windows per group staged in
 // only): the block's reads' bases staged in LDS first, so the scan loads nothing from HBM — a load's
 // wait counter drains in issue order, and a base load issued behind a probe waits for that probe
 constexpr uint32_t kSeqStage = 10240;  // >= 23 read pairs (or 44 single reads) of <= 219 bp: a uniform batch's block
-template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0, bool kSplit = false, bool kSeqLds = false>
+// kWavePack (MTB_K1F_WAVEPACK=1, A/B): each wave packs its own present windows with its own counter
+// atomic per group — no block barrier per group (the K4 finding: a block's waves held at a barrier
+// wait for its slowest lane's random reads)
+template <int kPer, bool kJMajor, bool kBinned = false, int kLink = 0, bool kSplit = false, bool kSeqLds = false,
+          bool kWavePack = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink == 4 ? 4 : 1))) k_extract_filter(const uint8_t* __restrict__ seq1, const uint64_t* __restrict__ off1,
                                                         const uint8_t* __restrict__ seq2, const uint64_t* __restrict__ off2,
                                                         const ReadMeta* __restrict__ meta, const uint64_t* __restrict__ uOff,
@@ -3134,6 +3138,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
             const unsigned long long b = __ballot((mask >> j) & 1u);
             if (lane == j) myCnt = (uint32_t)__popcll(b);
         }
+        if constexpr (kWavePack) {  // the wave's present windows in (window j, lane) order
+            const uint32_t inc = (uint32_t)wave_inclusive_scan((unsigned long long)myCnt);
+            const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+            unsigned long long wb = 0;
+            if (lane == 0 && tot) wb = atomicAdd(counter, (unsigned long long)tot);
+            const uint64_t base = (uint64_t)__shfl((long long)wb, 0, 64);
+            const uint32_t ex = inc - myCnt;  // lane j: window j's offset in the wave's stretch
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                const unsigned long long b = __ballot((mask >> j) & 1u);
+                const uint32_t exj = (uint32_t)__shfl((int)ex, j, 64);
+                if (!((mask >> j) & 1u)) continue;
+                const uint64_t pos = base + exj + (uint32_t)__popcll(b & ltMask);
+                if (pos < cap) {  // past the output's capacity: counted only (the caller grows it and reruns)
+                    qkey[pos] = k[j];
+                    qslot[pos] = (uint32_t)(slotBase + 64ull * (g + j));
+                    if (qdig) qdig[pos] = (uint8_t)(k[j] >> kQuerySortLo);
+                }
+            }
+            continue;
+        }
         if (lane < kPer) sCnt[lane * kWaves + wv] = myCnt;
         __syncthreads();
         const uint32_t c = lane < kPer * kWaves ? sCnt[lane] : 0u;
@@ -3204,10 +3229,16 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     k_extract_filter<P, true, false, W, S, true><<<blocks, 256, lds, s>>>(                                          \
         seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
         unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
+            const char* wp = getenv("MTB_K1F_WAVEPACK");  // A/B, read per batch
+            const bool wavePack = wp && atoi(wp) != 0;
             // the bases staged in LDS (uniform batches; MTB_K1F_SEQ_LDS=0, A/B: read from HBM)
             const char* sl = getenv("MTB_K1F_SEQ_LDS");
             const bool seqLds = upr && (!sl || atoi(sl) != 0);
-            if (seqLds && f == "w3i") MTB_EFLS(16, 3, false);
+            if (seqLds && wavePack && f == "w4i")
+                k_extract_filter<16, true, false, 4, false, true, true><<<blocks, 256, lds, s>>>(
+                    seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer,
+                    smerLen, unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link);
+            else if (seqLds && f == "w3i") MTB_EFLS(16, 3, false);
             else if (seqLds && f == "w3i8") MTB_EFLS(8, 3, false);
             else if (seqLds) MTB_EFLS(16, 4, false);
             else if (f == "w3i") MTB_EFL(16, 3, false);

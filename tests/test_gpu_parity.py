@@ -201,7 +201,7 @@ def test_end_to_end_batches(make_db, db_name):
 
 @pytest.mark.parametrize("db_name", ["fmt2", "fmt1"])
 @pytest.mark.parametrize("window", ["0", "0:gallop", "0:staged", "0:retry", "0:spill", "0:fine28", "0:unfused",
-                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:nofast", "0:blockjoin", "0:pipejoin", "0:wave64join", "0:pairjoin", "6144:pairjoin", "0:nolink", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "0:ballot", "64",
+                                    "0:nodigits", "0:atomiclines", "0:matchxcd", "0:nofast", "0:blockjoin", "0:pipejoin", "0:wave64join", "0:pairjoin", "0:wavepack", "0:nolink", "0:share", "0:bins", "0:binsover", "0:binsnodig", "0:ext", "0:atomicfirst", "0:ballot", "64",
                                     "6144", "6144:staged", "6144:spill", "6144:unfused", "0:nofilter", "6144:nofilter"])
 def test_match_window_paths(make_db, db_name, window, monkeypatch):
     """K4's search paths — DB window staged in LDS, or HBM search (the unstaged join: runs from the
@@ -235,6 +235,8 @@ def test_match_window_paths(make_db, db_name, window, monkeypatch):
     monkeypatch.setenv("MTB_JOIN_WAVE", {"blockjoin": "0", "pipejoin": "2", "wave64join": "4", "pairjoin": "7"}.get(mode, "1"))
     # the fused K1F's one probe-line read per window instead of the link lines' one read per window pair
     monkeypatch.setenv("MTB_LINK_LINES", "0" if mode == "nolink" else "1")
+    # the fused K1F packing its present windows per wave, no block barrier per group (A/B, round 6)
+    monkeypatch.setenv("MTB_K1F_WAVEPACK", "1" if mode == "wavepack" else "0")
     # K1F writing straight into K2's first-pass buckets at any batch size; with 64-slot buckets, which
     # overflow, so the batch reruns through the packed K1F
     monkeypatch.setenv("MTB_K1F_BINS", "2" if mode.startswith("bins") else "0")
