@@ -2917,7 +2917,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
                                                         unsigned long long* __restrict__ counter, uint64_t rankLo,
                                                         uint64_t rankHi, uint64_t cap, uint8_t* __restrict__ qdig,
                                                         unsigned long long* __restrict__ binCnt, uint64_t binRc,
-                                                        uint32_t upr, const uint64_t* __restrict__ link) {
+                                                        uint32_t upr, const uint64_t* __restrict__ link,
+                                                        int emitPerBlock = 0) {
     static_assert(kLink == 0 || kPer % 2 == 0, "windows probed in pairs");
     __shared__ uint8_t sBase[256];
     __shared__ uint32_t sBin[256];
@@ -3181,9 +3182,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLink 
         }
     }
     // the reference's "Query k-mer number" (KmerMatcher.cpp:143-152) counts every non-blank query
-    // k-mer, before any AA test: one atomic per wave
+    // k-mer, before any AA test: one atomic per wave, or (emitPerBlock, the default for the production
+    // form) per block — the count shares its line with the output counter the groups' atomics wait on,
+    // and same-line atomics are served one at a time
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) emitted += (uint32_t)__shfl_xor((int)emitted, d, 64);
+    if (emitPerBlock) {
+        __shared__ uint32_t sEmit[kWaves];
+        if ((threadIdx.x & 63) == 0) sEmit[wv] = emitted;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t e = 0;
+#pragma unroll
+            for (int i = 0; i < kWaves; i++) e += sEmit[i];
+            if (e) atomicAdd(counter + 1, (unsigned long long)e);
+        }
+        return;
+    }
     if ((threadIdx.x & 63) == 0 && emitted) atomicAdd(counter + 1, (unsigned long long)emitted);
 }
 
@@ -3225,10 +3240,13 @@ uint64_t launch_extract_filter(const uint8_t* seq1, const uint64_t* off1, const 
     k_extract_filter<P, true, false, W, S><<<blocks, 256, lds, s>>>(                                                \
         seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
         unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
+            // MTB_K1F_EMIT_BLOCK=0 (A/B, read per batch): the emitted count by one atomic per wave
+            const char* eb = getenv("MTB_K1F_EMIT_BLOCK");
+            const int emitBlock = !eb || atoi(eb) != 0;
 #define MTB_EFLS(P, W, S)                                                                                           \
     k_extract_filter<P, true, false, W, S, true><<<blocks, 256, lds, s>>>(                                          \
         seq1, off1, seq2, off2, meta, uOff, unitRead, nUnits, C, extract_tables(t), kmerFormat, syncmer, smerLen,   \
-        unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link)
+        unitInfo, lines, qkey, qslot, counter, rankLo, rankHi, cap, qdig, binCnt, binRc, upr, link, emitBlock)
             const char* wp = getenv("MTB_K1F_WAVEPACK");  // A/B, read per batch
             const bool wavePack = wp && atoi(wp) != 0;
             // the bases staged in LDS (uniform batches; MTB_K1F_SEQ_LDS=0, A/B: read from HBM)
