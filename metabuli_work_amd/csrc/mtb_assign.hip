@@ -2046,18 +2046,22 @@ __device__ __forceinline__ void match_paths_group(const R& recs, const mtb_match
 // kPathStage matches.
 constexpr int kPathStage = 1024;
 
-__global__ void __launch_bounds__(64) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
+// kLds = false (MTB_PATHS_NOLDS=1, A/B): no stage at all — at GTDB scale a wave's span of groups
+// rarely fits one (~2,200 matches) — so neither the 10-KB stage nor the register budget holds the
+// kernel at 4 waves per SIMD (kW: the waves the registers are held to)
+template <bool kLds, int kW>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kW))) k_match_paths(const mtb_match* __restrict__ M, const uint64_t* __restrict__ gStart,
                                                     const uint64_t* __restrict__ order, uint64_t nWork, AssignCfg cfg,
                                                     TaxView tax, Path* __restrict__ L, Path* __restrict__ P,
                                                     uint8_t* __restrict__ conn, uint32_t* __restrict__ pathCnt,
                                                     uint64_t* __restrict__ bigList, uint32_t* __restrict__ bigCount) {
-    __shared__ uint32_t sPos[kPathStage], sDh[kPathStage];
-    __shared__ uint16_t sReh[kPathStage];
+    __shared__ uint32_t sPos[kLds ? kPathStage : 1], sDh[kLds ? kPathStage : 1];
+    __shared__ uint16_t sReh[kLds ? kPathStage : 1];
     const uint64_t w0 = (uint64_t)blockIdx.x * 64;
     const uint64_t i = w0 + threadIdx.x;
     const uint64_t wLast = min(w0 + 63, nWork - 1);
-    const uint64_t spanLo = gStart[(uint32_t)order[w0]], spanHi = gStart[(uint32_t)order[wLast] + 1];
-    const bool staged = spanHi - spanLo <= (uint64_t)kPathStage;
+    const uint64_t spanLo = kLds ? gStart[(uint32_t)order[w0]] : 0, spanHi = kLds ? gStart[(uint32_t)order[wLast] + 1] : 0;
+    const bool staged = kLds && spanHi - spanLo <= (uint64_t)kPathStage;
     if (staged) {
         for (uint64_t k = spanLo + threadIdx.x; k < spanHi; k += 64) {
             const mtb_match m = M[k];
@@ -3106,9 +3110,18 @@ void launch_assign(const mtb_match* matches, const uint64_t* mOff, const uint32_
                 // groups of >= kBigGroup matches queue for a wave each (long reads' serial tail)
                 const bool waves = !a.generic && a.bigGroups && nM >= kBigGroup;
                 if (waves) hipMemsetAsync(s.waveCount, 0, sizeof(uint32_t), st);
-                k_match_paths<<<(unsigned)((heavy + 63) / 64), 64, 0, st>>>(
-                    matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths,
-                    s.conn, s.pathCnt, waves ? s.waveList : nullptr, s.waveCount);
+                // MTB_PATHS_NOLDS=<waves> (A/B, read per batch): the unstaged form held to 5 or 6 waves
+                const char* nl = getenv("MTB_PATHS_NOLDS");
+                const int nlw = nl ? atoi(nl) : 0;
+#define MTB_PATHS(L, W)                                                                                             \
+    k_match_paths<L, W><<<(unsigned)((heavy + 63) / 64), 64, 0, st>>>(                                              \
+        matches, s.gStart, inB ? s.ordKB : s.ordKA, heavy, cfg, tv, (Path*)s.local, (Path*)s.paths, s.conn,         \
+        s.pathCnt, waves ? s.waveList : nullptr, s.waveCount)
+                if (nlw == 6) MTB_PATHS(false, 6);
+                else if (nlw == 5) MTB_PATHS(false, 5);
+                else if (nlw == 4) MTB_PATHS(false, 4);
+                else MTB_PATHS(true, 1);
+#undef MTB_PATHS
                 if (waves) {
                     uint32_t nBig = 0;
                     hipMemcpyAsync(&nBig, s.waveCount, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
