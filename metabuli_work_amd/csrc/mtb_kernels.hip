@@ -2143,7 +2143,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
     }
     if (kPrefetch && pfw == 0xFFFFFFFFu && key[0] == ~0ull) atomicAdd(&stats[kStatStripes], 0ull);  // keeps the prefetches
     const int blockHits = __syncthreads_count(hit >= 1) + (kPer > 1 ? __syncthreads_count(hit >= 2) : 0);
-    if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);  // matched queries
+    // matched queries, on the block's stats stripe (one word for every block queued its atomics)
+    if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[blockIdx.x % kStatStripes], (unsigned long long)blockHits);
     if (!kStage && lines) {  // the fallback counter sits past the stripes (rare: a lane-0 atomic per wave)
         uint32_t w = 0;
 #pragma unroll
@@ -2367,7 +2368,7 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
             if (lane == 0 && hw) atomicAdd(&stats[tile % kStatStripes], (unsigned long long)__popcll(hw));
         } else {
             const int blockHits = __syncthreads_count(c != 0);
-            if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[0], (unsigned long long)blockHits);
+            if (threadIdx.x == 0 && blockHits) atomicAdd(&stats[blockIdx.x % kStatStripes], (unsigned long long)blockHits);
         }
         const uint64_t gw = __ballot(gallop);
         if (gw && (threadIdx.x & 63) == 0) atomicAdd(&stats[kStatStripes], (unsigned long long)__popcll(gw));
