@@ -1625,8 +1625,10 @@ static hipError_t launch_sorts(const mtb_match* in, const uint64_t* mOff, uint32
     const uint32_t* listLarge = lists + 3 * (size_t)nReads;
     // mode (MTB_PRUNE_AFTER, A/B): segsort_regs' kMode of the E 4 and E 8 register sorts (4: as 2, with
     // the compact large sort on the plain bitonic network)
+    // MTB_SEGSORT_PAD=<bytes> (A/B diagnostic): unused dynamic LDS per block, to cap the waves per SIMD
+    static const size_t segPad = getenv("MTB_SEGSORT_PAD") ? (size_t)atoi(getenv("MTB_SEGSORT_PAD")) : 0;
 #define MTB_REGS(E, M, N, L) \
-    k_segsort_regs<E, M><<<N, 64, 0, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen, L)
+    k_segsort_regs<E, M><<<N, 64, segPad, s>>>(in, mOff, seg, inOff, inC, nReads, out, liveCnt, pm, segLen, L)
     if (!liveCnt) mode = 3;  // no pruning: the full-key sort
     if (e == hipSuccess && cnt[0]) {
         if (mode == 1) MTB_REGS(4, 1, cnt[0], list4);
