@@ -2251,7 +2251,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kLeanW
 // its run-index read.
 constexpr int kWaveLines = 16;
 template <int kMode>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 || kMode == 5 ? 7 : (kMode == 3 ? 6 : 8))))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? 7 : (kMode == 3 ? 6 : 8))))
 k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qslot, uint32_t C, uint64_t Q,
                const DbRec* __restrict__ db, uint64_t D, const int32_t* __restrict__ spOf, uint32_t maxTax,
                int kmerFormat, unsigned long long* __restrict__ total, mtb_match* __restrict__ buf,
@@ -2418,9 +2418,16 @@ k_join_uniform(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ q
                      err);
         }
     };
-    if constexpr (kMode < 2) {
-        // the wave's first query (kMode 1 runs with 256- or 64-thread blocks: MTB_JOIN_WAVE=4, A/B)
-        const uint64_t waveId = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if constexpr (kMode < 2 || kMode >= 5) {
+        // the wave's first query (kMode 1 runs with 256- or 64-thread blocks: MTB_JOIN_WAVE=4, A/B).
+        // kMode 7 (MTB_JOIN_WAVE=7, A/B): blocks dealt round-robin over the 8 XCDs walk contiguous
+        // eighths of the sorted queries, so neighbouring tiles share one L2
+        uint64_t blk = blockIdx.x;
+        if (kMode == 7) {
+            const uint64_t x = blk & 7u, i = blk >> 3, qn = gridDim.x >> 3, rn = gridDim.x & 7u;
+            blk = x * qn + min(x, rn) + i;
+        }
+        const uint64_t waveId = (blk * blockDim.x + threadIdx.x) >> 6;
         const uint64_t q0 = kWave ? waveId * 64 : (uint64_t)blockIdx.x * 256;
         if (kWave && q0 >= Q) return;  // a wave past the queries (no block barrier below in this form)
         const uint64_t q1 = min(q0 + (kWave ? 64 : 256), Q);
@@ -3651,6 +3658,8 @@ void launch_match(const uint64_t* qkey, const uint32_t* qslot, const uint64_t* u
                 k_join_uniform<1><<<grid, 256, (size_t)atoi(getenv("MTB_JOIN_PAD")), s>>>(
                     qkey, qslot, C, Q, db, D, spOf, maxTax, kmerFormat, total, buf, bufRank, region, err, lines, lineP,
                     runOff, sortLo, stats, direct, overflow, capShift, longList, longCap, longCnt, upr, cnt64, lineExt);
+            } else if (wmode == 7) {
+                MTB_K4_JOIN(7);
             } else if (wmode == 1) {
                 MTB_K4_JOIN(1);
             } else {
